@@ -1,0 +1,386 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by RUNNING THE REFERENCE task code (stub-imported, see refload.py).
+
+Run in the build container only (needs /root/reference):  python tests/golden/make_goldens.py
+Writes small ``.npz`` fixtures next to this file; those fixtures (data only) are committed and are
+what ``tests/`` checks the oracle and the HIP path against.
+
+Reference code exercised (all unmodified, executed through a fake ``self`` that carries the
+attributes Isaac Gym would have created):
+  * ``Ur5SihMultiObjectManipulation.post_physics_step`` chain  (configurable_vec_task.py:359-414):
+    observable post_step callbacks (ur5sih.py:233-345, multi_object.py:121-417, 770-772),
+    ``compute_reward`` -> ``_update_reset_buf`` / ``_update_rew_buf`` / ``_update_success_rate``
+    (multi_object_manipulation.py:232-351), ``compute_observations`` (observable_vec_task.py:183-203),
+    plus VecTask.step's timeout rule (vec_task.py:424);
+  * ``pre_physics_step`` controllers (configurable_vec_task.py:347-357; ur5sih.py:397-405, 485-527);
+  * ``reset_idx`` steady state (multi_object_manipulation.py:33-71, 73-91, 175-230; ur5sih.py:616-632);
+  * quaternion utilities (utils/torch_jit_utils.py:41-123, 233-235) and ``randomize_rotation``
+    (multi_object_manipulation.py:12-15).
+Physics (``gym.simulate``) is a no-op in the fake gym: these goldens pin the task math only.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+import yaml
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import refload  # noqa: E402
+
+REF_CFG = "/root/reference/isaacgymenvs/cfg/task"
+SCENE = os.path.join(HERE, "..", "..", "isaacgym-hand-arm_amd", "handarm_hip", "assets", "ur5sih_scene.json")
+
+
+class AttrDict(dict):
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+def wrap(o):
+    if isinstance(o, dict):
+        return AttrDict({k: wrap(v) for k, v in o.items()})
+    if isinstance(o, list):
+        return [wrap(v) for v in o]
+    return o
+
+
+class Vec3:
+    def __init__(self, v):
+        self.x, self.y, self.z = [float(t) for t in v]
+
+
+class Mat33:
+    def __init__(self, m):
+        m = np.asarray(m).reshape(3, 3)
+        self.x, self.y, self.z = Vec3(m[0]), Vec3(m[1]), Vec3(m[2])
+
+
+class FakeObject:
+    def __init__(self, rec):
+        self.name = rec["name"]
+        self.mass = rec["mass"]
+        self.com = Vec3(rec["com"])
+        self.inertia = Mat33(rec["inertia"])
+        q = np.array(rec["bbox_from_origin_quat"])
+        from scipy.spatial.transform import Rotation as R
+        T = np.eye(4)
+        T[:3, :3] = R.from_quat(q).as_matrix()
+        T[:3, 3] = rec["bbox_from_origin_pos"]
+        self._to_origin = np.linalg.inv(T)
+        self._extents = np.array(rec["bbox_extents"])
+
+    def find_bounding_box_from_mesh(self):
+        return self._to_origin, self._extents
+
+
+class FakeGym:
+    """Records every tensor-API call; simulate/refresh are no-ops (physics is not pinned here)."""
+
+    def __init__(self, body_names):
+        self.body_names = body_names
+        self.calls = []
+        self.tensors = {}
+
+    def find_actor_rigid_body_index(self, env_ptr, handle, name, domain):
+        return 1 + self.body_names.index(name)   # env body order: goal(0), robot(1..29), ...
+
+    def acquire_actor_root_state_tensor(self, sim):
+        return self.tensors["root"]
+
+    def acquire_rigid_body_state_tensor(self, sim):
+        return self.tensors["body"]
+
+    def acquire_dof_state_tensor(self, sim):
+        return self.tensors["dof"]
+
+    def acquire_net_contact_force_tensor(self, sim):
+        return self.tensors["contact"]
+
+    def __getattr__(self, name):
+        def rec(*args, **kw):
+            self.calls.append(name)
+        return rec
+
+
+def make_task(num_envs, num_initial_poses=1, seed=0):
+    mom = refload.load("isaacgymenvs.tasks.hand_arm.task.multi_object_manipulation")
+    avt = refload.load("isaacgymenvs.tasks.hand_arm.base.actionable_vec_task")
+    obs_mod = refload.load("isaacgymenvs.tasks.hand_arm.utils.observables")
+    scene = json.load(open(SCENE))
+    cfg_base = wrap(yaml.safe_load(open(os.path.join(REF_CFG, "Ur5SihBase.yaml"))))
+    cfg_env = wrap(yaml.safe_load(open(os.path.join(REF_CFG, "Ur5SihMultiObject.yaml"))))
+    cfg_task_raw = yaml.safe_load(open(os.path.join(REF_CFG, "Ur5SihMultiObjectManipulation.yaml")))
+    cfg_task = wrap(cfg_task_raw)
+    cfg_env.objects.drop.num_initial_poses = num_initial_poses
+    e = cfg_task_raw["env"]
+    obs_list = e["proprioceptive_observations"] + e["object_observations"] + e["task_observations"]
+
+    T = mom.Ur5SihMultiObjectManipulation
+    t = object.__new__(T)
+    t.cfg = {"env": {"observations": list(obs_list), "teacher_observations": list(obs_list),
+                     "actions": list(e["actions"]), "numEnvs": num_envs}}
+    t.cfg_base, t.cfg_env, t.cfg_task = cfg_base, cfg_env, cfg_task
+    t.num_environments = num_envs
+    t.device = "cpu"
+    t.rl_device = "cpu"
+    t.dt = cfg_base.sim.dt
+    t.max_episode_length = cfg_task.rl.reset.max_episode_length
+    t.headless = True
+    t.objects_dropped = False
+    links = scene["robot"]["links"]
+    dofs = scene["robot"]["dofs"]
+    t.gym = FakeGym([l["name"] for l in links])
+    t.sim = None
+    t.viewer = None
+    t.env_ptrs = [0]
+    t.ur5sih_handles = [0]
+    # _acquire_robot_urdf / _acquire_robot_asset (ur5sih.py:58-121)
+    t.ur5sih_actuated_dof_names = ["shoulder_pan_joint", "shoulder_lift_joint", "elbow_joint", "wrist_1_joint",
+                                   "wrist_2_joint", "wrist_3_joint", "thumb_opposition", "thumb_flexion",
+                                   "index_finger", "middle_finger", "ring_finger"]
+    t.ur5sih_dof_names = [d["name"] for d in dofs]
+    t.ur5sih_dof_count = len(dofs)
+    t.ur5sih_actuated_dof_indices = [t.ur5sih_dof_names.index(n) for n in t.ur5sih_actuated_dof_names]
+    t.ur5sih_dof_lower_limits = torch.tensor([d["lower"] for d in dofs], dtype=torch.float32)
+    t.ur5sih_dof_upper_limits = torch.tensor([d["upper"] for d in dofs], dtype=torch.float32)
+    t.ur5sih_actuated_dof_lower_limits = t.ur5sih_dof_lower_limits[t.ur5sih_actuated_dof_indices]
+    t.ur5sih_actuated_dof_upper_limits = t.ur5sih_dof_upper_limits[t.ur5sih_actuated_dof_indices]
+    t.ur5sih_rigid_body_count = len(links)
+    t.ur5sih_num_body_surface_samples = [1]   # synthetic robot point cloud: registered, never active
+    # _create_envs (multi_object.py:477-677): actor order goal, robot, table, objects
+    g = torch.Generator().manual_seed(seed)
+    n_obj = cfg_env.objects.num_objects
+    t.objects = [FakeObject(o) for o in scene["objects"][:3]]
+    t.object_indices = torch.stack([torch.randperm(len(t.objects), generator=g)[:n_obj] for _ in range(num_envs)])
+    t.num_actors, t.num_bodies, t.num_dofs = 3 + n_obj, 1 + len(links) + 1 + n_obj, len(dofs)
+    A = t.num_actors
+    t.ur5sih_actor_indices = torch.arange(num_envs, dtype=torch.int32) * A + 1
+    t.object_actor_indices = (torch.arange(num_envs, dtype=torch.int32)[:, None] * A + 3
+                              + torch.arange(n_obj, dtype=torch.int32)[None]).to(torch.int32)
+    t.goal_actor_indices = torch.arange(num_envs, dtype=torch.int32) * A
+    t.object_actor_env_indices = [3 + i for i in range(n_obj)]
+    t.goal_actor_env_index = 0
+    t.ur5sih_rigid_body_env_indices = list(range(1, 1 + len(links)))
+    t.object_configuration_indices = torch.zeros(num_envs, dtype=torch.int64)
+    t.target_object_index = torch.zeros(num_envs, dtype=torch.int64)
+    t.target_object_actor_env_index = torch.zeros(num_envs, dtype=torch.int64)
+    # VecTask.allocate_buffers (vec_task.py:329-354)
+    avt.ActionableVecTask.__init__(t)
+    t._active_observations = obs_mod.ActiveObservables()
+    t.register_observables()
+    t._active_observations.add([t._registered_observables[n] for n in t.cfg["env"]["observations"]])
+    t._active_observations.add([t._registered_observables[n] for n in t.cfg["env"]["teacher_observations"]])
+    t.cfg["env"]["numObservations"], t.observations_start_end = t._compute_num_observations(obs_list)
+    t.cfg["env"]["numTeacherObservations"], t.teacher_observations_start_end = t._compute_num_observations(obs_list)
+    t._sorted_observations = t._active_observations.sort(t._registered_observables)
+    t.num_observations = t.cfg["env"]["numObservations"]
+    t.num_teacher_observations = t.cfg["env"]["numTeacherObservations"]
+    N = num_envs
+    t.obs_buf = torch.zeros((N, t.num_observations))
+    t.teacher_obs_buf = torch.zeros((N, t.num_teacher_observations))
+    t.rew_buf = torch.zeros(N)
+    t.reset_buf = torch.ones(N, dtype=torch.long)
+    t.timeout_buf = torch.zeros(N, dtype=torch.long)
+    t.progress_buf = torch.zeros(N, dtype=torch.long)
+    t.extras = {}
+    t.obs_dict = {}
+    t.gym.tensors = {"root": torch.zeros(N * A, 13), "body": torch.zeros(N * t.num_bodies, 13),
+                     "dof": torch.zeros(N * t.num_dofs, 2), "contact": torch.zeros(N * t.num_bodies, 3)}
+    t.acquire_simulation_tensors()
+    t.log_data = {}
+    for a in t._sorted_actions.values():
+        a.callback.post_init()
+    for o in t._sorted_observations.values():
+        o.callback.post_init()
+    for o in t._sorted_observations.values():
+        o.callback.post_step()
+    t._reset_buffers(torch.arange(N))
+    return t, mom
+
+
+def rand_quat(g, shape):
+    q = torch.randn(*shape, 4, generator=g)
+    return q / q.norm(dim=-1, keepdim=True)
+
+
+def fill_random_state(t, g):
+    N, A, B = t.num_envs, t.num_actors, t.num_bodies
+    rs = t.root_state.view(N, A, 13)
+    rs[..., 0:3] = torch.rand(N, A, 3, generator=g) * torch.tensor([0.6, 0.6, 0.5]) + torch.tensor([0.0, 0.3, 0.5])
+    rs[..., 3:7] = rand_quat(g, (N, A))
+    rs[..., 7:13] = torch.randn(N, A, 6, generator=g) * 0.3
+    bs = t.body_state.view(N, B, 13)
+    bs[..., 0:3] = torch.rand(N, B, 3, generator=g) * torch.tensor([0.6, 0.6, 0.5]) + torch.tensor([0.0, 0.3, 0.5])
+    bs[..., 3:7] = rand_quat(g, (N, B))
+    bs[..., 7:13] = torch.randn(N, B, 6, generator=g) * 0.3
+    lo, hi = t.ur5sih_dof_lower_limits, t.ur5sih_dof_upper_limits
+    lo = torch.maximum(lo, torch.tensor(-3.0))
+    hi = torch.minimum(hi, torch.tensor(3.0))
+    ds = t.dof_state.view(N, t.num_dofs, 2)
+    ds[..., 0] = lo + (hi - lo) * torch.rand(N, t.num_dofs, generator=g)
+    ds[..., 1] = torch.randn(N, t.num_dofs, generator=g)
+    t.contact_force[:] = torch.randn(N, B, 3, generator=g)
+
+
+def gen_obs_reward(path, N=16, steps=6, seed=1):
+    t, mom = make_task(N, num_initial_poses=2, seed=seed)
+    g = torch.Generator().manual_seed(seed + 100)
+    n_obj, P = t.cfg_env.objects.num_objects, 2
+    t.objects_dropped = True
+    t.object_pos_initial = torch.rand(N, P, n_obj, 3, generator=g) * 0.3 + torch.tensor([0.1, 0.4, 0.5])
+    t.object_quat_initial = rand_quat(g, (N, P, n_obj))
+    out = {k: [] for k in ["root", "body", "dof", "contact", "targets", "goal_pos", "target_idx", "cfg_idx",
+                           "progress_in", "reset_in", "reached_in", "obs", "teacher", "rew", "reset", "timeout",
+                           "progress", "reached", "log_overall", "log_obj", "log_terms", "bbox"]}
+    for s in range(steps):
+        fill_random_state(t, g)
+        t.dof_position_targets[:] = torch.randn(N, 17, generator=g)
+        t.goal_pos[:] = torch.rand(N, 3, generator=g) * 0.3 + torch.tensor([0.13, 0.43, 0.7])
+        t.target_object_index[:] = torch.randint(n_obj, (N,), generator=g)
+        t.target_object_actor_env_index[:] = torch.tensor(t.object_actor_env_indices)[t.target_object_index]
+        t.object_configuration_indices[:] = torch.randint(P, (N,), generator=g)
+        # place target objects near goal / lifted sometimes so every reward branch is exercised
+        near = torch.rand(N, generator=g) < 0.5
+        rs = t.root_state.view(N, t.num_actors, 13)
+        ar = torch.arange(N)
+        rs[ar[near], t.target_object_actor_env_index[near], 0:3] = (
+            t.goal_pos[near] + 0.06 * (torch.rand(int(near.sum()), 3, generator=g) - 0.5))
+        t.progress_buf[:] = torch.randint(196, 202, (N,), generator=g)
+        t.reset_buf[:] = (torch.rand(N, generator=g) < 0.2).long()
+        t.goal_reached_before[:] = torch.rand(N, generator=g) < 0.3
+        out["root"].append(t.root_state.clone()); out["body"].append(t.body_state.clone())
+        out["dof"].append(t.dof_state.clone()); out["contact"].append(t.contact_force.clone())
+        out["targets"].append(t.dof_position_targets.clone()); out["goal_pos"].append(t.goal_pos.clone())
+        out["target_idx"].append(t.target_object_index.clone()); out["cfg_idx"].append(t.object_configuration_indices.clone())
+        out["progress_in"].append(t.progress_buf.clone()); out["reset_in"].append(t.reset_buf.clone())
+        out["reached_in"].append(t.goal_reached_before.clone())
+        t.log_data = {}
+        t.post_physics_step()
+        timeout = (t.progress_buf >= t.max_episode_length - 1) & (t.reset_buf != 0)   # vec_task.py:424
+        out["obs"].append(t.obs_buf.clone()); out["teacher"].append(t.teacher_obs_buf.clone())
+        out["rew"].append(t.rew_buf.clone()); out["reset"].append(t.reset_buf.clone())
+        out["timeout"].append(timeout.clone()); out["progress"].append(t.progress_buf.clone())
+        out["reached"].append(t.goal_reached_before.clone())
+        out["bbox"].append(t.object_bounding_box.clone())
+        out["log_overall"].append(torch.tensor(float(t.log_data.get("success_rate_ewma/overall", float("nan")))))
+        out["log_obj"].append(torch.tensor([float(t.log_data.get("success_rate_ewma/" + o.name, float("nan")))
+                                            for o in t.objects]))
+        out["log_terms"].append(torch.tensor([float(t.log_data["reward_terms/" + k]) for k in t.cfg_task.rl.reward]))
+    arrays = {k: torch.stack(v).numpy() for k, v in out.items()}
+    arrays["object_indices"] = t.object_indices.numpy()
+    arrays["object_pos_initial"] = t.object_pos_initial.numpy()
+    arrays["object_quat_initial"] = t.object_quat_initial.numpy()
+    arrays["bbox_from_origin_pos"] = t.object_bounding_box_from_origin_pos.numpy()
+    arrays["bbox_from_origin_quat"] = t.object_bounding_box_from_origin_quat.numpy()
+    arrays["obs_names"] = np.array(t.cfg["env"]["observations"])
+    arrays["obs_start_end"] = np.array([t.observations_start_end[n] for n in t.cfg["env"]["observations"]])
+    arrays["reward_terms"] = np.array(list(t.cfg_task.rl.reward.keys()))
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, {k: v.shape for k, v in arrays.items()})
+
+
+def gen_controller(path, N=16, steps=12, seed=2):
+    t, mom = make_task(N, seed=seed)
+    g = torch.Generator().manual_seed(seed + 100)
+    t.reset_buf[:] = 0
+    # controller state as after a reset (ur5sih.py:388-389, 466-478)
+    fill_random_state(t, g)
+    t._reset_ur5_joint_pos_controller(torch.arange(N))
+    t._reset_sih_servo_pos_controller(torch.arange(N))
+    out = {k: [] for k in ["actions", "dof_pos", "targets", "ur5_target", "servo", "smoothed"]}
+    out["init_ur5_target"] = t.ur5_joint_pos_target.clone()
+    out["init_servo"] = t.sih_servo_commands.clone()
+    for s in range(steps):
+        ds = t.dof_state.view(N, 17, 2)
+        ds[..., 0] = t.ur5sih_dof_lower_limits.clamp(min=-3) + (t.ur5sih_dof_upper_limits.clamp(max=3)
+                     - t.ur5sih_dof_lower_limits.clamp(min=-3)) * torch.rand(N, 17, generator=g)
+        actions = torch.rand(N, 11, generator=g) * 2.4 - 1.2
+        if s % 4 == 3:
+            actions[:, 6:] = torch.sign(actions[:, 6:])  # drive servo commands into their limits
+        out["actions"].append(actions.clone()); out["dof_pos"].append(t.dof_state.view(N, 17, 2)[..., 0].clone())
+        t.pre_physics_step(actions)
+        out["targets"].append(t.dof_position_targets.clone()); out["ur5_target"].append(t.ur5_joint_pos_target.clone())
+        out["servo"].append(t.sih_servo_commands.clone()); out["smoothed"].append(t.sih_smoothed_actions.clone())
+    arrays = {k: (torch.stack(v) if isinstance(v, list) else v).numpy() for k, v in out.items()}
+    # spline coefficients as the reference built them (for the oracle's own table check)
+    for nm in ["thumb_proximal", "thumb_distal", "index_proximal", "index_distal", "middle_proximal",
+               "middle_distal", "ring_proximal", "ring_distal"]:
+        sp = getattr(t, nm + "_spline")
+        arrays["spline_" + nm] = torch.stack([torch.cat([sp._t[:-1]]), sp._a[:, 0], sp._b[:, 0],
+                                              sp._two_c[:, 0], sp._three_d[:, 0]]).numpy()
+        arrays["knots_" + nm] = sp._t.numpy()
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, {k: v.shape for k, v in arrays.items()})
+
+
+def gen_reset(path, N=16, seed=3, P=2):
+    t, mom = make_task(N, num_initial_poses=P, seed=seed)
+    g = torch.Generator().manual_seed(seed + 100)
+    n_obj = t.cfg_env.objects.num_objects
+    t.objects_dropped = True
+    fill_random_state(t, g)
+    t.object_pos_initial = torch.rand(N, P, n_obj, 3, generator=g) * 0.3 + torch.tensor([0.1, 0.4, 0.5])
+    t.object_quat_initial = rand_quat(g, (N, P, n_obj))
+    t.sih_servo_commands[:] = torch.rand(N, 5, generator=g) * 1000
+    t.sih_smoothed_actions[:] = torch.rand(N, 5, generator=g)
+    t.progress_buf[:] = 200
+    t.goal_reached_before[:] = True
+    root_before = t.root_state.clone()
+    dof_before = t.dof_state.clone()
+    torch.manual_seed(1234)
+    t.reset_idx(torch.arange(N))
+    torch.manual_seed(1234)    # the same draws, in reference order (a10)
+    d_cfg = torch.randint(P, (N,), dtype=torch.int64)
+    d_tgt = torch.randint(n_obj, (N,), dtype=torch.int64)
+    d_goal = torch.rand((N, 3), dtype=torch.float32)
+    arrays = dict(root_before=root_before.numpy(), dof_before=dof_before.numpy(),
+                  object_pos_initial=t.object_pos_initial.numpy(), object_quat_initial=t.object_quat_initial.numpy(),
+                  draw_cfg=d_cfg.numpy(), draw_target=d_tgt.numpy(), draw_goal=d_goal.numpy(),
+                  root_after=t.root_state.numpy(), dof_after=t.dof_state.numpy(),
+                  targets=t.dof_position_targets.numpy(), ur5_target=t.ur5_joint_pos_target.numpy(),
+                  servo=t.sih_servo_commands.numpy(), smoothed=t.sih_smoothed_actions.numpy(),
+                  target_idx=t.target_object_index.numpy(), cfg_idx=t.object_configuration_indices.numpy(),
+                  goal_pos=t.goal_pos.numpy(), progress=t.progress_buf.numpy(), reset=t.reset_buf.numpy(),
+                  reached=t.goal_reached_before.numpy(), gym_calls=np.array(t.gym.calls))
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, {k: v.shape for k, v in arrays.items()})
+
+
+def gen_quat(path, M=64, seed=4):
+    tu = refload.load("isaacgym.torch_utils")
+    mom = refload.load("isaacgymenvs.tasks.hand_arm.task.multi_object_manipulation")
+    g = torch.Generator().manual_seed(seed)
+    a, b = rand_quat(g, (M,)), rand_quat(g, (M,))
+    v = torch.randn(M, 3, generator=g)
+    ang = torch.rand(M, generator=g) * 6 - 3
+    axis = torch.randn(M, 3, generator=g)
+    r0, r1 = torch.rand(M, generator=g) * 2 - 1, torch.rand(M, generator=g) * 2 - 1
+    x = torch.rand(M, 4, generator=g) * 2 - 1
+    lo, hi = -torch.rand(M, 4, generator=g), torch.rand(M, 4, generator=g)
+    xu = torch.tensor([1.0, 0, 0]).repeat(M, 1)
+    yu = torch.tensor([0.0, 1, 0]).repeat(M, 1)
+    arrays = dict(a=a.numpy(), b=b.numpy(), v=v.numpy(), ang=ang.numpy(), axis=axis.numpy(), r0=r0.numpy(),
+                  r1=r1.numpy(), x=x.numpy(), lo=lo.numpy(), hi=hi.numpy(),
+                  quat_mul=tu.quat_mul(a, b).numpy(), quat_apply=tu.quat_apply(a, v).numpy(),
+                  quat_rotate=tu.quat_rotate(a, v).numpy(), quat_conjugate=tu.quat_conjugate(a).numpy(),
+                  quat_from_angle_axis=tu.quat_from_angle_axis(ang, axis).numpy(),
+                  randomize_rotation=mom.randomize_rotation(r0, r1, xu, yu).numpy(),
+                  scale=tu.scale(x, lo, hi).numpy(), unscale=tu.unscale(x, lo, hi).numpy())
+    np.savez_compressed(path, **arrays)
+    print("wrote", path)
+
+
+if __name__ == "__main__":
+    gen_quat(os.path.join(HERE, "quat_utils.npz"))
+    gen_controller(os.path.join(HERE, "ur5sih_controller.npz"))
+    gen_obs_reward(os.path.join(HERE, "ur5sih_obs_reward.npz"))
+    gen_reset(os.path.join(HERE, "ur5sih_reset.npz"))

@@ -1,0 +1,370 @@
+#!/usr/bin/env python3
+"""Offline asset pipeline: reference URDF + meshes -> committed scene model (JSON).
+
+Runs ONLY in the build container (it reads /root/reference/assets, which does not exist on the GPU
+box). Its output, ``isaacgym-hand-arm_amd/handarm_hip/assets/ur5sih_scene.json``, is committed and is
+the only thing the runtime reads.
+
+What it restates (and why), with reference citations:
+
+* Robot asset: ``assets/hand_arm/robot/hand_arm_collision_is_visual.urdf`` loaded with
+  ``fix_base_link``, ``override_com``, ``override_inertia``, ``disable_gravity``
+  (``tasks/hand_arm/base/ur5sih.py:169-180``) and actor pose ``(0, 0, table_height)``
+  (``ur5sih.py:125``).
+* Body / DOF order: Isaac Gym orders bodies depth-first; siblings are visited in link-name order
+  (inferred, SURVEY.md §8 a2: it puts ``thumb_opposition`` at DOF 14 exactly as
+  ``Ur5SihBase.yaml:8`` and the gain table ``Ur5SihBase.yaml:3-4`` require).
+* Collision geometry: PhysX cooks a convex hull (<= 64 vertices on the GPU pipeline) for every
+  dynamic mesh shape; we do the same offline (scipy Qhull) and reduce to <= ``MAX_LINK_VERTS`` /
+  ``MAX_OBJ_VERTS`` vertices by farthest-point sampling. YCB objects are V-HACD decomposed in the
+  reference (``multi_object.py:37-43``); the three default objects are close to convex, so one hull
+  each is used (documented deviation, parity vs PhysX unpinned).
+* The SIH palm visual mesh is missing from the reference checkout (``.MISSING_LARGE_BLOBS:58``); the
+  palm uses the five convex collision pieces that ``hand_arm.urdf:360-385`` assigns to it.
+* Mass properties: links/objects with an URDF ``<inertial>`` keep its mass; COM and inertia come from
+  the collision hulls (override_com / override_inertia). Links without ``<inertial>`` get
+  density 1000 kg/m^3 x hull volume (Isaac Gym's default asset density).
+* Object bounding boxes (``multi_object.py:84-88,743-768``): trimesh ``oriented_bounds`` is absent
+  here; we compute a minimum-volume box over hull-facet-normal candidate frames (2-D rotating
+  calipers in the orthogonal plane), which is the same search trimesh performs. Parity unpinned.
+"""
+import json
+import math
+import os
+import struct
+import sys
+import xml.etree.ElementTree as ET
+
+import numpy as np
+from scipy.spatial import ConvexHull
+
+REF = "/root/reference"
+ASSETS = os.path.join(REF, "assets", "hand_arm")
+ROBOT_URDF = os.path.join(ASSETS, "robot", "hand_arm_collision_is_visual.urdf")
+PALM_URDF = os.path.join(ASSETS, "robot", "hand_arm.urdf")
+OUT = os.path.join(os.path.dirname(__file__), "..", "isaacgym-hand-arm_amd", "handarm_hip",
+                   "assets", "ur5sih_scene.json")
+
+MAX_LINK_VERTS = 32
+MAX_OBJ_VERTS = 64
+DENSITY = 1000.0
+TABLE_HEIGHT = 0.5  # Ur5SihMultiObject.yaml:48
+YCB_POOL = ["015_peach", "005_tomato_soup_can", "006_mustard_bottle",   # default set (yaml:11)
+            "004_sugar_box", "007_tuna_fish_can", "008_pudding_box", "009_gelatin_box",
+            "010_potted_meat_can", "013_apple", "014_lemon", "016_pear", "017_orange",
+            "018_plum", "025_mug", "061_foam_brick", "077_rubiks_cube"]
+
+
+# ----------------------------------------------------------------------------- math helpers
+def rpy_to_matrix(r, p, y):
+    cr, sr, cp, sp, cy, sy = math.cos(r), math.sin(r), math.cos(p), math.sin(p), math.cos(y), math.sin(y)
+    return np.array([[cy * cp, cy * sp * sr - sy * cr, cy * sp * cr + sy * sr],
+                     [sy * cp, sy * sp * sr + cy * cr, sy * sp * cr - cy * sr],
+                     [-sp, cp * sr, cp * cr]])
+
+
+def matrix_to_quat(R):
+    """Rotation matrix -> quaternion (x, y, z, w), w >= 0."""
+    t = np.trace(R)
+    if t > 0:
+        s = math.sqrt(t + 1.0) * 2
+        w, x, y, z = 0.25 * s, (R[2, 1] - R[1, 2]) / s, (R[0, 2] - R[2, 0]) / s, (R[1, 0] - R[0, 1]) / s
+    elif R[0, 0] > R[1, 1] and R[0, 0] > R[2, 2]:
+        s = math.sqrt(1.0 + R[0, 0] - R[1, 1] - R[2, 2]) * 2
+        w, x, y, z = (R[2, 1] - R[1, 2]) / s, 0.25 * s, (R[0, 1] + R[1, 0]) / s, (R[0, 2] + R[2, 0]) / s
+    elif R[1, 1] > R[2, 2]:
+        s = math.sqrt(1.0 + R[1, 1] - R[0, 0] - R[2, 2]) * 2
+        w, x, y, z = (R[0, 2] - R[2, 0]) / s, (R[0, 1] + R[1, 0]) / s, 0.25 * s, (R[1, 2] + R[2, 1]) / s
+    else:
+        s = math.sqrt(1.0 + R[2, 2] - R[0, 0] - R[1, 1]) * 2
+        w, x, y, z = (R[1, 0] - R[0, 1]) / s, (R[0, 2] + R[2, 0]) / s, (R[1, 2] + R[2, 1]) / s, 0.25 * s
+    q = np.array([x, y, z, w])
+    if q[3] < 0:
+        q = -q
+    return q / np.linalg.norm(q)
+
+
+# ----------------------------------------------------------------------------- mesh IO
+def load_obj(path):
+    verts, faces = [], []
+    with open(path) as f:
+        for line in f:
+            if line.startswith("v "):
+                verts.append([float(t) for t in line.split()[1:4]])
+            elif line.startswith("f "):
+                idx = [int(t.split("/")[0]) - 1 for t in line.split()[1:]]
+                for k in range(1, len(idx) - 1):
+                    faces.append([idx[0], idx[k], idx[k + 1]])
+    return np.array(verts, dtype=np.float64), np.array(faces, dtype=np.int64)
+
+
+def load_stl(path):
+    with open(path, "rb") as f:
+        data = f.read()
+    n = struct.unpack("<I", data[80:84])[0]
+    if 84 + 50 * n == len(data):
+        rec = np.frombuffer(data[84:], dtype=np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)),
+                                                        ("a", "<u2")]), count=n)
+        tri = rec["v"].astype(np.float64).reshape(-1, 3)
+    else:  # ascii
+        tri = np.array([[float(t) for t in ln.split()[1:4]] for ln in data.decode().splitlines()
+                        if ln.strip().startswith("vertex")])
+    faces = np.arange(len(tri)).reshape(-1, 3)
+    return tri, faces
+
+
+def load_mesh(path, scale):
+    v, f = load_obj(path) if path.lower().endswith(".obj") else load_stl(path)
+    return v * np.asarray(scale, dtype=np.float64), f
+
+
+# ----------------------------------------------------------------------------- hulls
+def reduce_points(points, max_verts):
+    hull = ConvexHull(points)
+    pts = points[hull.vertices]
+    if len(pts) <= max_verts:
+        return pts
+    c = pts.mean(0)
+    chosen = [int(np.argmax(np.linalg.norm(pts - c, axis=1)))]
+    d = np.linalg.norm(pts - pts[chosen[0]], axis=1)
+    while len(chosen) < max_verts:
+        i = int(np.argmax(d))
+        chosen.append(i)
+        d = np.minimum(d, np.linalg.norm(pts - pts[i], axis=1))
+    return pts[chosen]
+
+
+def hull_planes(points):
+    hull = ConvexHull(points)
+    planes = []
+    for eq in hull.equations:  # n.x + d <= 0 inside
+        n, d = eq[:3], eq[3]
+        dup = False
+        for p in planes:
+            if np.dot(p[:3], n) > 1 - 1e-6 and abs(p[3] - d) < 1e-7:
+                dup = True
+                break
+        if not dup:
+            planes.append(np.concatenate([n, [d]]))
+    verts = points[hull.vertices]
+    return verts, np.array(planes), hull
+
+
+def polyhedron_mass_props(points):
+    """Volume, centroid and inertia (about centroid, unit density) of the convex hull of points."""
+    hull = ConvexHull(points)
+    P = hull.points
+    c0 = P[hull.vertices].mean(0)
+    tri = P[hull.simplices]                                   # (F, 3, 3)
+    flip = np.einsum("fi,fi->f", np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0]),
+                     hull.equations[:, :3]) < 0
+    tri[flip] = tri[flip][:, [0, 2, 1]]
+    A = np.transpose(tri - c0, (0, 2, 1))                     # columns = a-c0, b-c0, c-c0
+    det = np.linalg.det(A)
+    vol = det.sum() / 6.0
+    com = (det[:, None] / 6.0 * (tri.sum(1) + c0) / 4.0).sum(0) / vol
+    canon = np.array([[2, 1, 1], [1, 2, 1], [1, 1, 2]]) / 120.0
+    cov = np.einsum("f,fij,jk,flk->il", det, A, canon, A)
+    d = com - c0
+    cov_com = cov - vol * np.outer(d, d)
+    inertia = np.trace(cov_com) * np.eye(3) - cov_com
+    return vol, com, inertia
+
+
+def min_volume_obb(points):
+    """Minimum-volume oriented box over facet-normal candidate frames (trimesh-style search)."""
+    verts, _, hull = hull_planes(points)
+    best = None
+    for eq in hull.equations:
+        n = eq[:3] / np.linalg.norm(eq[:3])
+        a = np.array([1.0, 0, 0]) if abs(n[0]) < 0.9 else np.array([0, 1.0, 0])
+        u = np.cross(n, a)
+        u /= np.linalg.norm(u)
+        w = np.cross(n, u)
+        p2 = np.stack([verts @ u, verts @ w], 1)
+        h2 = ConvexHull(p2)
+        hp = p2[h2.vertices]
+        hn = verts @ n
+        for k in range(len(hp)):
+            e = hp[(k + 1) % len(hp)] - hp[k]
+            e /= np.linalg.norm(e)
+            ep = np.array([-e[1], e[0]])
+            s1, s2 = p2 @ e, p2 @ ep
+            ext = np.array([s1.max() - s1.min(), s2.max() - s2.min(), hn.max() - hn.min()])
+            vol = ext.prod()
+            if best is None or vol < best[0]:
+                ax = e[0] * u + e[1] * w
+                ay = ep[0] * u + ep[1] * w
+                az = np.cross(ax, ay)
+                R = np.stack([ax, ay, az], 1)
+                cz = verts @ az
+                ext[2] = cz.max() - cz.min()
+                ctr = ax * (s1.max() + s1.min()) / 2 + ay * (s2.max() + s2.min()) / 2 + az * (cz.max() + cz.min()) / 2
+                best = (ext.prod(), R, ctr, ext)
+    _, R, ctr, ext = best
+    # trimesh convention: extents sorted is not guaranteed; keep frame as found.
+    return R, ctr, ext
+
+
+def hull_record(points, max_verts):
+    pts = reduce_points(points, max_verts)
+    verts, planes, _ = hull_planes(pts)
+    center = 0.5 * (verts.min(0) + verts.max(0))
+    radius = float(np.linalg.norm(verts - center, axis=1).max())
+    return {"verts": verts.tolist(), "planes": planes.tolist(), "center": center.tolist(),
+            "radius": radius}
+
+
+# ----------------------------------------------------------------------------- URDF
+def parse_origin(el):
+    if el is None:
+        return np.zeros(3), np.eye(3)
+    xyz = [float(t) for t in el.get("xyz", "0 0 0").split()]
+    rpy = [float(t) for t in el.get("rpy", "0 0 0").split()]
+    return np.array(xyz), rpy_to_matrix(*rpy)
+
+
+def link_collision_points(link_el, base_dir, palm_override=None):
+    pts = []
+    pieces = []
+    colls = link_el.findall("collision")
+    if palm_override is not None:
+        colls = palm_override
+    for c in colls:
+        g = c.find("geometry/mesh")
+        if g is None:
+            continue
+        path = os.path.join(base_dir, g.get("filename"))
+        if not os.path.exists(path):
+            return None
+        scale = [float(t) for t in g.get("scale", "1 1 1").split()]
+        v, _ = load_mesh(path, scale)
+        o, R = parse_origin(c.find("origin"))
+        v = v @ R.T + o
+        pieces.append(v)
+        pts.append(v)
+    if not pts:
+        return []
+    return pieces
+
+
+def build_robot():
+    base_dir = os.path.dirname(ROBOT_URDF)
+    root = ET.parse(ROBOT_URDF).getroot()
+    links = {l.get("name"): l for l in root.findall("link")}
+    joints = root.findall("joint")
+    children = {}
+    parent_joint = {}
+    for j in joints:
+        p, c = j.find("parent").get("link"), j.find("child").get("link")
+        children.setdefault(p, []).append(c)
+        parent_joint[c] = j
+    roots = [n for n in links if n not in parent_joint]
+    assert roots == ["base_link"], roots
+    order = []
+
+    def dfs(n):
+        order.append(n)
+        for c in sorted(children.get(n, [])):
+            dfs(c)
+    dfs("base_link")
+    idx = {n: i for i, n in enumerate(order)}
+
+    palm_colls = [l for l in ET.parse(PALM_URDF).getroot().findall("link") if l.get("name") == "palm"][0]
+    palm_colls = palm_colls.findall("collision")
+
+    prop_gain = [120., 120., 120., 120., 120., 120., 20., 10., 20., 10., 20., 10., 20., 10., 20., 20., 10.]
+    deriv_gain = [20., 20., 20., 20., 20., 20., 6., 2., 6., 2., 6., 2., 6., 2., 6., 6., 2.]
+
+    out_links, dofs, hulls = [], [], []
+    for n in order:
+        el = links[n]
+        j = parent_joint.get(n)
+        rec = {"name": n, "parent": -1, "joint": None, "type": "fixed", "origin_pos": [0, 0, 0],
+               "origin_quat": [0, 0, 0, 1], "axis": [0, 0, 1], "dof": -1}
+        if j is not None:
+            o, R = parse_origin(j.find("origin"))
+            rec.update(parent=idx[j.find("parent").get("link")], joint=j.get("name"),
+                       type=j.get("type"), origin_pos=o.tolist(), origin_quat=matrix_to_quat(R).tolist())
+            ax = j.find("axis")
+            if ax is not None:
+                a = np.array([float(t) for t in ax.get("xyz").split()])
+                rec["axis"] = (a / np.linalg.norm(a)).tolist()
+            if j.get("type") == "revolute":
+                lim = j.find("limit")
+                rec["dof"] = len(dofs)
+                dofs.append({"name": j.get("name"), "link": idx[n], "lower": float(lim.get("lower")),
+                             "upper": float(lim.get("upper")), "effort": float(lim.get("effort")),
+                             "velocity": float(lim.get("velocity")),
+                             "kp": prop_gain[len(dofs)], "kd": deriv_gain[len(dofs)]})
+        pieces = link_collision_points(el, base_dir, palm_colls if n == "palm" else None)
+        inertial = el.find("inertial")
+        mass = float(inertial.find("mass").get("value")) if inertial is not None else None
+        if pieces:
+            allp = np.concatenate(pieces, 0)
+            vol, com, I_unit = polyhedron_mass_props(allp)
+            if mass is None:
+                mass = DENSITY * vol
+            inertia = I_unit * (mass / vol)
+            for pc in pieces:
+                h = hull_record(pc, MAX_LINK_VERTS)
+                h.update(owner="link", index=idx[n])
+                hulls.append(h)
+        elif inertial is not None:
+            o, R = parse_origin(inertial.find("origin"))
+            ie = inertial.find("inertia")
+            I = np.array([[float(ie.get("ixx")), float(ie.get("ixy")), float(ie.get("ixz"))],
+                          [float(ie.get("ixy")), float(ie.get("iyy")), float(ie.get("iyz"))],
+                          [float(ie.get("ixz")), float(ie.get("iyz")), float(ie.get("izz"))]])
+            com, inertia = o, R @ I @ R.T
+        else:
+            mass, com, inertia = 0.0, np.zeros(3), np.zeros((3, 3))
+        rec.update(mass=float(mass), com=np.asarray(com).tolist(), inertia=np.asarray(inertia).reshape(-1).tolist())
+        out_links.append(rec)
+    return {"links": out_links, "dofs": dofs, "base_pos": [0.0, 0.0, TABLE_HEIGHT],
+            "base_quat": [0.0, 0.0, 0.0, 1.0]}, hulls
+
+
+def build_object(name):
+    urdf = os.path.join(ASSETS, "object_sets", "urdf", "ycb", name + ".urdf")
+    root = ET.parse(urdf).getroot()
+    link = root.find("link")
+    mass = float(link.find("inertial/mass").get("value"))
+    mesh = link.find("collision/geometry/mesh").get("filename")
+    v, _ = load_mesh(os.path.normpath(os.path.join(os.path.dirname(urdf), mesh)), [1, 1, 1])
+    hull = hull_record(v, MAX_OBJ_VERTS)
+    vol, com, I_unit = polyhedron_mass_props(v)
+    R, ctr, ext = min_volume_obb(reduce_points(v, 256))
+    return {"name": name, "mass": mass, "com": com.tolist(),
+            "inertia": (I_unit * mass / vol).reshape(-1).tolist(), "hull": hull,
+            "bbox_from_origin_pos": ctr.tolist(), "bbox_from_origin_quat": matrix_to_quat(R).tolist(),
+            "bbox_extents": ext.tolist()}
+
+
+def box_hull(half):
+    hx, hy, hz = half
+    verts = [[sx * hx, sy * hy, sz * hz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)]
+    planes = [[1, 0, 0, -hx], [-1, 0, 0, -hx], [0, 1, 0, -hy], [0, -1, 0, -hy], [0, 0, 1, -hz], [0, 0, -1, -hz]]
+    return {"verts": verts, "planes": planes, "center": [0, 0, 0], "radius": float(np.linalg.norm(half))}
+
+
+def main():
+    robot, link_hulls = build_robot()
+    objects = [build_object(n) for n in YCB_POOL
+               if os.path.exists(os.path.join(ASSETS, "object_sets", "urdf", "ycb", n + ".urdf"))]
+    table = {"pos": [0.2925, 0.38, TABLE_HEIGHT / 2], "quat": [0, 0, 0, 1],    # multi_object.py:536,628
+             "half_extents": [0.375, 0.55, TABLE_HEIGHT / 2]}
+    table["hull"] = box_hull(table["half_extents"])
+    scene = {"robot": robot, "link_hulls": link_hulls, "objects": objects, "table": table,
+             "goal_radius": 0.02,
+             "generator": "tools/build_model.py (reference assets @ /root/reference/assets/hand_arm)"}
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    with open(OUT, "w") as f:
+        json.dump(scene, f, indent=None, separators=(",", ":"))
+    nm = sum(1 for l in robot["links"] if l["mass"] > 0)
+    print(f"links={len(robot['links'])} dofs={len(robot['dofs'])} massive={nm} link_hulls={len(link_hulls)} "
+          f"objects={[o['name'] for o in objects]} -> {OUT} ({os.path.getsize(OUT)} B)")
+
+
+if __name__ == "__main__":
+    sys.exit(main())
