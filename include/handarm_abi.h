@@ -1,0 +1,207 @@
+/*
+ * handarm_abi.h - C ABI of the MI355X hand-arm simulator (libhandarm_hip.so).
+ *
+ * This is the drop-in boundary for the reference's LOWER surface, the Isaac Gym tensor API that
+ * the hand_arm task code calls, plus one fused entry point that runs the task's
+ * whole VecTask.step() on the device.  Plain pointers and sizes only; all device pointers are HIP
+ * device memory (allocated by the caller, e.g. torch); every call is asynchronous on `stream`
+ * (a hipStream_t passed as void*; NULL = default stream) and single-threaded per handle.
+ * Every function returns 0 on success or a negative HA_E_* code.
+ *
+ * Reference call each entry point replaces (file:line under /root/reference/isaacgymenvs):
+ *   ha_create / ha_bind_state      gym.create_sim + prepare_sim + acquire_*_tensor + wrap_tensor
+ *                                  (tasks/base/vec_task.py:58-64,288; hand_arm/base/observable_vec_task.py:123-155)
+ *   ha_simulate                    gym.simulate (vec_task.py:412; multi_object_manipulation.py:67,124,139,172)
+ *   ha_refresh                     gym.refresh_{dof_state,actor_root_state,rigid_body_state,net_contact_force}_tensor
+ *                                  (observable_vec_task.py:173-177)
+ *   ha_set_dof_position_target     gym.set_dof_position_target_tensor (hand_arm/base/actionable_vec_task.py:39-40)
+ *   ha_set_actor_root_state_indexed   gym.set_actor_root_state_tensor_indexed (multi_object_manipulation.py:89,118,167,228)
+ *   ha_set_dof_state_indexed          gym.set_dof_state_tensor_indexed (hand_arm/base/ur5sih.py:630)
+ *   ha_set_dof_position_target_indexed gym.set_dof_position_target_tensor_indexed (ur5sih.py:626)
+ *   ha_set_object_collision_filter gym.set_actor_rigid_shape_properties(filter) loop (multi_object.py:693-703)
+ *   ha_task_step                   VecTask.step for Ur5SihMultiObjectManipulation, fused
+ *                                  (vec_task.py:390-441 -> configurable_vec_task.py:347-414)
+ *   ha_task_observe                post_step callbacks + compute_reward + compute_observations alone
+ *   ha_task_reset                  reset_idx steady state (multi_object_manipulation.py:33-71)
+ */
+#ifndef HANDARM_ABI_H
+#define HANDARM_ABI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HA_ABI_VERSION 1
+
+/* capacities of the static model */
+#define HA_MAX_LINKS 32
+#define HA_MAX_DOFS 24
+#define HA_MAX_HULLS 64
+#define HA_MAX_VERTS 4096
+#define HA_MAX_PLANES 8192
+#define HA_MAX_POOL 32
+#define HA_MAX_OBJ 3           /* objects per env (Ur5SihMultiObject.yaml:2) */
+#define HA_MAX_INIT_POSES 4    /* objects.drop.num_initial_poses */
+#define HA_MAX_SPLINE_PIECES 8
+#define HA_N_SPLINES 8
+#define HA_MAX_MPAIRS 192
+
+/* error codes */
+#define HA_OK 0
+#define HA_E_ARG -1
+#define HA_E_HIP -2
+#define HA_E_STATE -3
+#define HA_E_MODEL -4
+
+/* flags for ha_task_step / ha_simulate */
+#define HA_FLAG_NO_PHYSICS 1u      /* skip physics substeps (task-math parity tests) */
+#define HA_FLAG_REPLAY_DRAWS 2u    /* reset draws come from ha_state_t.reset_draws (host RNG replay) */
+#define HA_FLAG_OBS_ONLY 4u        /* ha_task_observe: compute_observations only (VecTask.reset) */
+
+/* Static scene model (built offline by tools/build_model.py, packed by handarm_hip/model.py). */
+typedef struct ha_model_t {
+    int32_t n_links, n_dofs, n_link_hulls, n_pool, n_hulls;
+    int32_t link_parent[HA_MAX_LINKS];
+    int32_t link_dof[HA_MAX_LINKS];             /* -1 = fixed joint */
+    int32_t link_table_collide[HA_MAX_LINKS];   /* 1 = link hulls collide with table/ground */
+    float link_origin_pos[HA_MAX_LINKS][3];     /* joint origin in parent frame */
+    float link_origin_quat[HA_MAX_LINKS][4];    /* xyzw */
+    float link_axis[HA_MAX_LINKS][3];           /* joint axis in joint frame */
+    float link_mass[HA_MAX_LINKS];
+    float link_com[HA_MAX_LINKS][3];            /* link frame */
+    float link_inertia[HA_MAX_LINKS][9];        /* about COM, link frame, row-major */
+    float dof_lower[HA_MAX_DOFS], dof_upper[HA_MAX_DOFS], dof_effort[HA_MAX_DOFS];
+    float dof_kp[HA_MAX_DOFS], dof_kd[HA_MAX_DOFS];
+    float base_pos[3], base_quat[4];
+    /* convex hulls: [0, n_link_hulls) robot, then object pool hulls, then the table */
+    int32_t hull_link[HA_MAX_HULLS];            /* owning robot link, or -1 */
+    int32_t hull_vert_start[HA_MAX_HULLS], hull_nverts[HA_MAX_HULLS];
+    int32_t hull_plane_start[HA_MAX_HULLS], hull_nplanes[HA_MAX_HULLS];
+    float hull_center[HA_MAX_HULLS][3], hull_radius[HA_MAX_HULLS];
+    float verts[HA_MAX_VERTS][4];               /* xyz, pad */
+    float planes[HA_MAX_PLANES][4];             /* n.x + d <= 0 inside */
+    /* object pool */
+    int32_t pool_hull[HA_MAX_POOL];
+    float pool_mass[HA_MAX_POOL], pool_com[HA_MAX_POOL][3], pool_inertia[HA_MAX_POOL][9];
+    float pool_bbox_pos[HA_MAX_POOL][3], pool_bbox_quat[HA_MAX_POOL][4], pool_bbox_ext[HA_MAX_POOL][3];
+    /* static geometry */
+    int32_t table_hull;
+    float table_pos[3], table_quat[4];
+    /* derived topology (filled by the host packer) */
+    int32_t link_level[HA_MAX_LINKS];           /* depth in the tree, root = 0 */
+    int32_t max_level;
+    int32_t dof_link[HA_MAX_DOFS];
+    int32_t n_mpairs;                           /* (d, e) with e an ancestor-or-self DOF of d */
+    int32_t mpair[HA_MAX_MPAIRS][2];
+} ha_model_t;
+
+/* Simulation + task parameters (Ur5SihBase.yaml, Ur5SihMultiObject*.yaml). */
+typedef struct ha_params_t {
+    float dt;                  /* sim dt, 1/60 */
+    int32_t substeps;          /* 2 */
+    int32_t control_freq_inv;  /* 3 */
+    int32_t solver_iters;      /* position iterations, 8 */
+    float gravity[3];
+    float friction;            /* 1.0 */
+    float contact_margin;      /* speculative contact distance */
+    float baumgarte;           /* penetration correction per substep */
+    float max_depen_vel;
+    float object_ang_damping;  /* Isaac Gym asset default 0.5 */
+    float joint_limit_margin;
+    /* task */
+    int32_t n_objects;         /* 3 */
+    int32_t num_initial_poses; /* P */
+    int32_t max_episode_length;/* 200 */
+    float action_dt;           /* dt used by the UR5 relative controller (VecTask.dt = sim dt) */
+    float sih_alpha;           /* 0.8 */
+    float reward_reaching, reward_lifting, reward_goal, reward_success;
+    float lifting_threshold, goal_threshold;
+    float goal_pos[3], goal_noise[3];
+    float reset_pose[HA_MAX_DOFS];
+    float servo_lower[5], servo_upper[5];
+    float proximal_coef[4];    /* thumb, index, middle, ring */
+    int32_t spline_pieces[HA_N_SPLINES];
+    /* [spline][field t0,a,b,two_c,three_d][piece] */
+    float spline[HA_N_SPLINES][5][HA_MAX_SPLINE_PIECES];
+    float thumb_opposition_gain;  /* -1.571 / 2675 */
+    uint64_t seed;
+} ha_params_t;
+
+/* Device buffers (caller-allocated). Layouts match the Isaac Gym tensors exactly. */
+typedef struct ha_state_t {
+    float* root_state;          /* [N][A=3+n_obj][13] pos, quat xyzw, linvel(COM), angvel */
+    float* rigid_body_state;    /* [N][B=1+n_links+1+n_obj][13] */
+    float* dof_state;           /* [N][D][2] pos, vel */
+    float* net_contact_force;   /* [N][B][3] */
+    float* sim_targets;         /* [N][D] position targets the physics sees */
+    float* dof_position_targets;/* [N][D] task-side tensor (observed) */
+    /* task */
+    const float* actions;       /* [N][11] */
+    float* obs;                 /* [N][147] */
+    float* teacher_obs;         /* [N][147] */
+    float* rew;                 /* [N] */
+    int64_t* reset_buf;         /* [N] */
+    int64_t* progress_buf;      /* [N] */
+    uint8_t* timeout_buf;       /* [N] bool */
+    uint8_t* goal_reached_before; /* [N] bool */
+    float* goal_pos;            /* [N][3] */
+    int64_t* target_object_index;      /* [N] */
+    int64_t* object_configuration_indices; /* [N] */
+    int64_t* object_indices;    /* [N][n_obj] pool ids */
+    float* object_pos_initial;  /* [N][P][n_obj][3] */
+    float* object_quat_initial; /* [N][P][n_obj][4] */
+    float* ur5_target;          /* [N][6] */
+    float* servo;               /* [N][5] */
+    float* smoothed;            /* [N][5] */
+    float* obs_cache;           /* [N][n_obj][7] object pose seen by the previous observable refresh */
+    float* reset_draws;         /* [N][5] cfg-draw, target-draw (as float ints), goal u[3] (replay mode) */
+    uint32_t* episode;          /* [N] episode counter (device RNG stream) */
+    int32_t* stats;             /* [S] per-step counters, see HA_STAT_* */
+    float* term_sums;           /* [4] reward term sums for the step */
+    int32_t* flags;             /* [4] device flags: [0] any env needs reset (written by the step kernel) */
+    uint8_t* collision_enabled; /* [N][n_obj] object collision filter (drop init) */
+} ha_state_t;
+
+/* stats layout (int32): [0] num_resets, [1] num_successes, then per pool object
+ * [2 + 2*i] resets with pool object i as target, [3 + 2*i] successes */
+#define HA_STAT_SIZE (2 + 2 * HA_MAX_POOL)
+
+typedef struct ha_handle_s* ha_handle;
+
+int ha_abi_version(void);
+/* sizeof the three structs as compiled into the library (host-side mirror check) */
+int ha_struct_sizes(int32_t* model_size, int32_t* params_size, int32_t* state_size);
+int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_envs, ha_handle* out);
+int ha_destroy(ha_handle h);
+int ha_bind_state(ha_handle h, const ha_state_t* state);
+/* gym-style tensor API */
+int ha_simulate(ha_handle h, int32_t n_calls, uint32_t flags, void* stream);
+int ha_refresh(ha_handle h, void* stream);
+int ha_set_dof_position_target(ha_handle h, const float* targets, void* stream);
+int ha_set_actor_root_state_indexed(ha_handle h, const float* root_state, const int32_t* actor_indices,
+                                    int32_t n, void* stream);
+int ha_set_dof_state_indexed(ha_handle h, const float* dof_state, const int32_t* actor_indices, int32_t n,
+                             void* stream);
+int ha_set_dof_position_target_indexed(ha_handle h, const float* targets, const int32_t* actor_indices,
+                                       int32_t n, void* stream);
+int ha_set_object_collision_filter(ha_handle h, const uint8_t* enabled, void* stream);
+/* fused task entry points */
+/* per-step log counters go to slot (step_counter % n_slots) of stats[n_slots][HA_STAT_SIZE] and
+ * term_sums[n_slots][4]; the slot is zeroed on the stream before the step kernel. Default 1 slot. */
+int ha_set_stats_ring(ha_handle h, int32_t n_slots);
+int ha_task_step(ha_handle h, uint32_t flags, void* stream);
+int ha_task_observe(ha_handle h, uint32_t flags, void* stream);
+int ha_task_reset(ha_handle h, uint32_t flags, void* stream);
+/* last kernel time in ms measured with HIP events around the most recent physics/step launch (-1 if none) */
+float ha_last_kernel_ms(ha_handle h);
+/* per-launch HIP-event timing of the env kernel (bench roofline): record up to max_launches launches
+ * (0 disables); ha_kernel_times synchronises and returns the recorded durations in ms */
+int ha_enable_kernel_timing(ha_handle h, int32_t max_launches);
+int ha_kernel_times(ha_handle h, float* out_ms, int32_t max, int32_t* n_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,115 @@
+// ha_device.h - gfx950 device helpers: small vector/quaternion math and wavefront (64-lane) primitives.
+// One environment is simulated by one 64-lane wavefront; `lane` = threadIdx.x.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define HD __device__ __forceinline__
+
+struct f3 { float x, y, z; };
+struct qf { float x, y, z, w; };
+
+HD f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
+HD f3 operator+(f3 a, f3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+HD f3 operator-(f3 a, f3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+HD f3 operator*(f3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
+HD float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+HD f3 cross3(f3 a, f3 b) { return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+HD f3 ld3(const float* p) { return mk3(p[0], p[1], p[2]); }
+HD void st3(float* p, f3 a) { p[0] = a.x; p[1] = a.y; p[2] = a.z; }
+HD qf ldq(const float* p) { return qf{p[0], p[1], p[2], p[3]}; }
+HD void stq(float* p, qf q) { p[0] = q.x; p[1] = q.y; p[2] = q.z; p[3] = q.w; }
+
+// Hamilton product (same expression as the C oracle)
+HD qf qmul(qf a, qf b) {
+    return qf{a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y, a.w * b.y - a.x * b.z + a.y * b.w + a.z * b.x,
+              a.w * b.z + a.x * b.y - a.y * b.x + a.z * b.w, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z};
+}
+HD f3 qrot(qf q, f3 v) {
+    f3 u = mk3(q.x, q.y, q.z);
+    f3 t = cross3(u, v) * 2.0f;
+    return (v + t * q.w) + cross3(u, t);
+}
+HD qf qnormalize(qf q) {
+    float n = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    return qf{q.x / n, q.y / n, q.z / n, q.w / n};
+}
+HD qf qaxis(f3 a, float ang) {
+    float s = sinf(0.5f * ang), c = cosf(0.5f * ang);
+    return qf{a.x * s, a.y * s, a.z * s, c};
+}
+HD void qmat(qf q, float R[9]) {
+    float x = q.x, y = q.y, z = q.z, w = q.w;
+    R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w); R[2] = 2 * (x * z + y * w);
+    R[3] = 2 * (x * y + z * w); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
+    R[6] = 2 * (x * z - y * w); R[7] = 2 * (y * z + x * w); R[8] = 1 - 2 * (x * x + y * y);
+}
+HD f3 mv3(const float M[9], f3 v) {
+    return mk3(M[0] * v.x + M[1] * v.y + M[2] * v.z, M[3] * v.x + M[4] * v.y + M[5] * v.z,
+               M[6] * v.x + M[7] * v.y + M[8] * v.z);
+}
+HD void rart3(const float R[9], const float* A, float out[9]) {
+    float T[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) T[i * 3 + j] = R[i * 3] * A[j] + R[i * 3 + 1] * A[3 + j] + R[i * 3 + 2] * A[6 + j];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+            out[i * 3 + j] = T[i * 3] * R[j * 3] + T[i * 3 + 1] * R[j * 3 + 1] + T[i * 3 + 2] * R[j * 3 + 2];
+}
+HD void inv3(const float A[9], float out[9]) {
+    float c0 = A[4] * A[8] - A[5] * A[7], c1 = A[5] * A[6] - A[3] * A[8], c2 = A[3] * A[7] - A[4] * A[6];
+    float det = A[0] * c0 + A[1] * c1 + A[2] * c2;
+    float id = 1.0f / det;
+    out[0] = c0 * id; out[1] = (A[2] * A[7] - A[1] * A[8]) * id; out[2] = (A[1] * A[5] - A[2] * A[4]) * id;
+    out[3] = c1 * id; out[4] = (A[0] * A[8] - A[2] * A[6]) * id; out[5] = (A[2] * A[3] - A[0] * A[5]) * id;
+    out[6] = c2 * id; out[7] = (A[1] * A[6] - A[0] * A[7]) * id; out[8] = (A[0] * A[4] - A[1] * A[3]) * id;
+}
+
+// ---------------------------------------------------------------- wavefront primitives (wave64)
+HD int lane_id() { return threadIdx.x & 63; }
+// Block == one wavefront: s_barrier is a no-op wait for lockstep lanes but orders the LDS traffic.
+HD void wsync() { __syncthreads(); }
+
+HD float wave_max(float x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x = fmaxf(x, __shfl_xor(x, off, 64));
+    return x;
+}
+HD float wave_min(float x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x = fminf(x, __shfl_xor(x, off, 64));
+    return x;
+}
+HD float wave_sum(float x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+}
+HD int wave_sum_i(int x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+}
+// arg-min / arg-max with ties broken toward the smaller index (matches a sequential strict-compare scan)
+HD void wave_argmin(float& v, int& i) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        float ov = __shfl_xor(v, off, 64);
+        int oi = __shfl_xor(i, off, 64);
+        if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; }
+    }
+}
+HD void wave_argmax(float& v, int& i) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        float ov = __shfl_xor(v, off, 64);
+        int oi = __shfl_xor(i, off, 64);
+        if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+    }
+}
+HD float bcast(float x, int src) { return __shfl(x, src, 64); }
+HD int bcast_i(int x, int src) { return __shfl(x, src, 64); }

@@ -1,0 +1,800 @@
+// ha_physics.h - one-wavefront-per-environment articulated + rigid-body physics for gfx950.
+//
+// Algorithm (identical to oracle/physics_oracle.c, which is its scalar restatement):
+//   FK (level-synchronous over the link tree) -> CRBA joint-space inertia + RNEA velocity-product
+//   forces in world-frame spatial algebra -> implicit PD drives (effort-saturating) folded into the
+//   inertia -> Cholesky (lane i owns row i) -> convex-hull contacts (SAT + incident vertices, <= 4 per
+//   pair) -> one constraint row per lane: lane r builds J_r, solves Y_r = M^-1 J_r^T in registers and
+//   the column A[:, r] of the Delassus matrix J M^-1 J^T -> projected Gauss-Seidel sweeps where the
+//   residual w = A lambda + b lives one element per lane (no cross-lane reductions in the sweep) ->
+//   velocity update through an LDS transpose -> symplectic Euler.
+#pragma once
+#include "ha_device.h"
+#include "../../include/handarm_abi.h"
+
+#define MAXC 21
+#define MAXR 64
+#define RS 40
+#define NOBJ HA_MAX_OBJ
+#define MAXD 24
+#define MAXB (1 + HA_MAX_LINKS + 1 + NOBJ)
+
+// What the task observables read after refresh_simulation_tensors(): flange pose, fingertip states,
+// dof positions, object root states (filled from FK in the fused step, or from the state tensors).
+struct ObsIn {
+    float flange[8];
+    float tip[5][10];      // pos, quat, linvel
+    float dofpos[MAXD];
+    float obj[NOBJ][13];
+    float pad[2];
+};
+
+struct EnvLDS {
+    ObsIn in;
+    float q[MAXD], qd[MAXD], tgt[MAXD];
+    float lp[HA_MAX_LINKS][4], lq[HA_MAX_LINKS][4];
+    float ax[MAXD][4], an[MAXD][4];
+    float Ic[HA_MAX_LINKS][13];                 // composite spatial inertia (m, h, J) at world origin
+    float Vl[HA_MAX_LINKS][6], Al[HA_MAX_LINKS][6], Fl[HA_MAX_LINKS][6];
+    float M[MAXD * MAXD];
+    float Cb[MAXD], rhs[MAXD];
+    float v[RS];
+    float oc[NOBJ][4], oq[NOBJ][4], ov[NOBJ][4], ow[NOBJ][4], oIinv[NOBJ][12], om[NOBJ];
+    int pool[NOBJ], coll[NOBJ];
+    float cx[MAXC][4], cn[MAXC][4], csep[MAXC];
+    int ca[MAXC], cb[MAXC];
+    int nc, nr, pad0, pad1;
+    float wvA[64][4], wvB[64][4], wpR[128][4];
+    float J[MAXR * RS];                         // rows; reused as the [NV][64] transpose after the solve
+    float vt[MAXR], lo[MAXR], hi[MAXR];
+    int fric_of[MAXR], rcontact[MAXR];
+    float cforce[MAXB][3];
+    float obs[160];
+    float scratch[64];
+};
+
+struct SimCtx {
+    const ha_model_t* __restrict__ m;
+    const ha_params_t* __restrict__ p;
+    EnvLDS* s;
+    int lane, D, NO, L;
+};
+
+// ----------------------------------------------------------------------------- kinematics
+HD void fk(SimCtx& c) {
+    EnvLDS& s = *c.s;
+    const ha_model_t& m = *c.m;
+    int lane = c.lane;
+    if (lane == 0) {
+        st3(s.lp[0], ld3(m.base_pos));
+        stq(s.lq[0], ldq(m.base_quat));
+    }
+    wsync();
+    for (int lev = 1; lev <= m.max_level; lev++) {
+        if (lane < c.L && m.link_level[lane] == lev) {
+            int i = lane, par = m.link_parent[i];
+            qf pq = ldq(s.lq[par]);
+            f3 p = ld3(s.lp[par]) + qrot(pq, ld3(m.link_origin_pos[i]));
+            qf r = qmul(pq, ldq(m.link_origin_quat[i]));
+            int d = m.link_dof[i];
+            if (d >= 0) {
+                r = qmul(r, qaxis(ld3(m.link_axis[i]), s.q[d]));
+                st3(s.ax[d], qrot(r, ld3(m.link_axis[i])));
+                st3(s.an[d], p);
+            }
+            st3(s.lp[i], p);
+            stq(s.lq[i], r);
+        }
+        wsync();
+    }
+}
+
+struct SInert { float m; f3 h; float J[9]; };
+
+HD void inert_apply(const SInert& I, f3 w, f3 v, f3& n, f3& f) {
+    n = mv3(I.J, w) + cross3(I.h, v);
+    f = v * I.m - cross3(I.h, w);
+}
+HD void inert_apply_lds(const float* Ic, f3 w, f3 v, f3& n, f3& f) {
+    f3 h = mk3(Ic[1], Ic[2], Ic[3]);
+    n = mv3(Ic + 4, w) + cross3(h, v);
+    f = v * Ic[0] - cross3(h, w);
+}
+
+// joint-space inertia s.M (D x D) and velocity-product forces s.Cb
+HD void dynamics(SimCtx& c) {
+    EnvLDS& s = *c.s;
+    const ha_model_t& m = *c.m;
+    int lane = c.lane, D = c.D, L = c.L;
+    SInert I;
+    bool own = lane < L;
+    if (own) {
+        int i = lane;
+        float R[9], Iw[9];
+        qf lq = ldq(s.lq[i]);
+        qmat(lq, R);
+        f3 cc = ld3(s.lp[i]) + qrot(lq, ld3(m.link_com[i]));
+        rart3(R, m.link_inertia[i], Iw);
+        float mm = m.link_mass[i];
+        I.m = mm;
+        I.h = cc * mm;
+        float ccd = dot3(cc, cc);
+        float cv[3] = {cc.x, cc.y, cc.z};
+#pragma unroll
+        for (int a = 0; a < 3; a++)
+#pragma unroll
+            for (int b = 0; b < 3; b++) I.J[a * 3 + b] = Iw[a * 3 + b] + mm * ((a == b ? ccd : 0.0f) - cv[a] * cv[b]);
+        float* ic = s.Ic[i];
+        ic[0] = I.m; ic[1] = I.h.x; ic[2] = I.h.y; ic[3] = I.h.z;
+#pragma unroll
+        for (int k = 0; k < 9; k++) ic[4 + k] = I.J[k];
+        if (i == 0) {
+#pragma unroll
+            for (int k = 0; k < 6; k++) { s.Vl[0][k] = 0.f; s.Al[0][k] = 0.f; }
+        }
+    }
+    // zero M
+    for (int k = lane; k < D * D; k += 64) s.M[k] = 0.0f;
+    wsync();
+    // twists / bias accelerations, level by level
+    for (int lev = 1; lev <= m.max_level; lev++) {
+        if (own && m.link_level[lane] == lev) {
+            int i = lane, par = m.link_parent[i], d = m.link_dof[i];
+            f3 vw = ld3(&s.Vl[par][0]), vv = ld3(&s.Vl[par][3]);
+            f3 aw = ld3(&s.Al[par][0]), av = ld3(&s.Al[par][3]);
+            if (d >= 0) {
+                f3 axd = ld3(s.ax[d]), and_ = ld3(s.an[d]);
+                float qd = s.qd[d];
+                f3 sw = axd * qd, sv = cross3(and_, axd) * qd;
+                vw = vw + sw;
+                vv = vv + sv;
+                aw = aw + cross3(vw, sw);
+                av = av + (cross3(vw, sv) + cross3(vv, sw));
+            }
+            st3(&s.Vl[i][0], vw); st3(&s.Vl[i][3], vv);
+            st3(&s.Al[i][0], aw); st3(&s.Al[i][3], av);
+        }
+        wsync();
+    }
+    if (own) {
+        int i = lane;
+        f3 vw = ld3(&s.Vl[i][0]), vv = ld3(&s.Vl[i][3]);
+        f3 aw = ld3(&s.Al[i][0]), av = ld3(&s.Al[i][3]);
+        f3 n1, f1, n2, f2;
+        inert_apply(I, aw, av, n1, f1);
+        inert_apply(I, vw, vv, n2, f2);
+        f3 fn = n1 + (cross3(vw, n2) + cross3(vv, f2));
+        f3 ff = f1 + cross3(vw, f2);
+        st3(&s.Fl[i][0], fn); st3(&s.Fl[i][3], ff);
+    }
+    wsync();
+    // backward accumulation of forces and composite inertia, deepest level first
+    for (int lev = m.max_level; lev >= 1; lev--) {
+        if (own && m.link_level[lane] == lev) {
+            int i = lane, par = m.link_parent[i];
+#pragma unroll
+            for (int k = 0; k < 6; k++) atomicAdd(&s.Fl[par][k], s.Fl[i][k]);
+#pragma unroll
+            for (int k = 0; k < 13; k++) atomicAdd(&s.Ic[par][k], s.Ic[i][k]);
+        }
+        wsync();
+    }
+    if (lane < D) {
+        int i = m.dof_link[lane];
+        f3 axd = ld3(s.ax[lane]), and_ = ld3(s.an[lane]);
+        s.Cb[lane] = dot3(axd, ld3(&s.Fl[i][0])) + dot3(cross3(and_, axd), ld3(&s.Fl[i][3]));
+    }
+    for (int k = lane; k < m.n_mpairs; k += 64) {
+        int d = m.mpair[k][0], e = m.mpair[k][1];
+        int i = m.dof_link[d];
+        f3 axd = ld3(s.ax[d]), and_ = ld3(s.an[d]);
+        f3 n, f;
+        inert_apply_lds(s.Ic[i], axd, cross3(and_, axd), n, f);
+        f3 axe = ld3(s.ax[e]), ane = ld3(s.an[e]);
+        float val = dot3(axe, n) + dot3(cross3(ane, axe), f);
+        s.M[d * D + e] = val;
+        s.M[e * D + d] = val;
+    }
+    wsync();
+}
+
+// in-place Cholesky of s.M (lower triangle), same operation order as the oracle (left-looking)
+HD void cholesky(SimCtx& c) {
+    EnvLDS& s = *c.s;
+    int lane = c.lane, D = c.D;
+    float* A = s.M;
+    for (int j = 0; j < D; j++) {
+        if (lane == j) {
+            float t = A[j * D + j];
+            for (int k = 0; k < j; k++) t -= A[j * D + k] * A[j * D + k];
+            A[j * D + j] = sqrtf(fmaxf(t, 1e-30f));
+        }
+        wsync();
+        if (lane > j && lane < D) {
+            float t = A[lane * D + j];
+            for (int k = 0; k < j; k++) t -= A[lane * D + k] * A[j * D + k];
+            A[lane * D + j] = t / A[j * D + j];
+        }
+        wsync();
+    }
+}
+
+// x (registers, MAXD) <- M^-1 x using the factor in s.M
+HD void chol_solve_regs(const SimCtx& c, float (&x)[MAXD]) {
+    const float* Lm = c.s->M;
+    int D = c.D;
+#pragma unroll
+    for (int i = 0; i < MAXD; i++) {
+        if (i < D) {
+            float t = x[i];
+#pragma unroll
+            for (int k = 0; k < i; k++) t -= Lm[i * D + k] * x[k];
+            x[i] = t / Lm[i * D + i];
+        }
+    }
+#pragma unroll
+    for (int i = MAXD - 1; i >= 0; i--) {
+        if (i < D) {
+            float t = x[i];
+#pragma unroll
+            for (int k = i + 1; k < MAXD; k++)
+                if (k < D) t -= Lm[k * D + i] * x[k];
+            x[i] = t / Lm[i * D + i];
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------- collision
+struct PoseF { f3 p; qf q; };
+
+HD PoseF object_pose(const SimCtx& c, int o) {
+    const EnvLDS& s = *c.s;
+    qf q = ldq(s.oq[o]);
+    return PoseF{ld3(s.oc[o]) - qrot(q, ld3(c.m->pool_com[s.pool[o]])), q};
+}
+
+HD void world_plane(const ha_model_t& m, int hull, int k, PoseF P, f3& n, float& d) {
+    const float* pl = m.planes[m.hull_plane_start[hull] + k];
+    n = qrot(P.q, mk3(pl[0], pl[1], pl[2]));
+    d = pl[3] - dot3(n, P.p);
+}
+
+// append up to 4 reduced contacts (lane 0 does the list bookkeeping, same policy as the oracle)
+HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int b) {
+    EnvLDS& s = *c.s;
+    int lane = c.lane;
+    int idx[4];
+    int k = 0;
+    float v0 = valid ? sep : 3.0e38f;
+    int i0 = valid ? lane : 1 << 20;
+    wave_argmin(v0, i0);
+    if (i0 >= (1 << 20)) return;
+    idx[k++] = i0;
+    f3 p0 = mk3(bcast(pt.x, i0), bcast(pt.y, i0), bcast(pt.z, i0));
+    f3 dd = pt - p0;
+    float v1 = valid ? dot3(dd, dd) : -1.0f;
+    int i1 = lane;
+    wave_argmax(v1, i1);
+    if (v1 > 1e-12f) {
+        idx[k++] = i1;
+        f3 p1 = mk3(bcast(pt.x, i1), bcast(pt.y, i1), bcast(pt.z, i1));
+        f3 e = p1 - p0;
+        float sv = dot3(cross3(e, pt - p0), n);
+        float v2 = valid ? sv : -3.0e38f;
+        int i2 = lane;
+        wave_argmax(v2, i2);
+        float v3 = valid ? sv : 3.0e38f;
+        int i3 = lane;
+        wave_argmin(v3, i3);
+        if (v2 > 1e-12f) idx[k++] = i2;
+        if (v3 < -1e-12f) idx[k++] = i3;
+    }
+    // gather the chosen points to every lane, lane 0 appends
+    f3 P[4];
+    float S[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        int src = t < k ? idx[t] : 0;
+        P[t] = mk3(bcast(pt.x, src), bcast(pt.y, src), bcast(pt.z, src));
+        S[t] = bcast(sep, src);
+    }
+    if (lane == 0) {
+        for (int t = 0; t < k; t++) {
+            int slot;
+            if (s.nc >= MAXC) {
+                int w = 0;
+                for (int j = 1; j < MAXC; j++)
+                    if (s.csep[j] > s.csep[w]) w = j;
+                if (s.csep[w] <= S[t]) continue;
+                slot = w;
+            } else {
+                slot = s.nc++;
+            }
+            st3(s.cx[slot], P[t]);
+            st3(s.cn[slot], n);
+            s.csep[slot] = S[t];
+            s.ca[slot] = a;
+            s.cb[slot] = b;
+        }
+    }
+    wsync();
+}
+
+HD void collide_ground(SimCtx& c, int hull, PoseF P, int a) {
+    const ha_model_t& m = *c.m;
+    float mg = c.p->contact_margin;
+    f3 ctr = P.p + qrot(P.q, ld3(m.hull_center[hull]));
+    if (ctr.z - m.hull_radius[hull] > mg) return;
+    int lane = c.lane;
+    bool valid = false;
+    f3 pt = mk3(0, 0, 0);
+    float sep = 0;
+    if (lane < m.hull_nverts[hull]) {
+        f3 v = P.p + qrot(P.q, ld3(m.verts[m.hull_vert_start[hull] + lane]));
+        if (v.z <= mg) {
+            valid = true;
+            pt = v - mk3(0, 0, 0.5f * v.z);
+            sep = v.z;
+        }
+    }
+    emit_contacts(c, valid, pt, sep, mk3(0, 0, 1), a, -1);
+}
+
+// hull A (body a) vs hull B (body b); normal from B to A
+HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int b) {
+    EnvLDS& s = *c.s;
+    const ha_model_t& m = *c.m;
+    float mg = c.p->contact_margin;
+    int lane = c.lane;
+    f3 ca = PA.p + qrot(PA.q, ld3(m.hull_center[ha]));
+    f3 cb = PB.p + qrot(PB.q, ld3(m.hull_center[hb]));
+    f3 dc = ca - cb;
+    float rr = m.hull_radius[ha] + m.hull_radius[hb] + mg;
+    if (dot3(dc, dc) > rr * rr) return;
+    int nva = m.hull_nverts[ha], nvb = m.hull_nverts[hb];
+    int npa = m.hull_nplanes[ha], npb = m.hull_nplanes[hb];
+    if (lane < nva) st3(s.wvA[lane], PA.p + qrot(PA.q, ld3(m.verts[m.hull_vert_start[ha] + lane])));
+    if (lane < nvb) st3(s.wvB[lane], PB.p + qrot(PB.q, ld3(m.verts[m.hull_vert_start[hb] + lane])));
+    wsync();
+    // SAT over the face normals of A (planes k = lane, lane + 64)
+    float best = -3.0e38f;
+    int bestk = 1 << 20;
+    for (int k = lane; k < npa; k += 64) {
+        f3 n; float d;
+        world_plane(m, ha, k, PA, n, d);
+        float mn = 3.0e38f;
+        for (int i = 0; i < nvb; i++) mn = fminf(mn, dot3(n, ld3(s.wvB[i])) + d);
+        if (mn > best) { best = mn; bestk = k; }
+    }
+    wave_argmax(best, bestk);
+    float sepA = best;
+    int kA = bestk;
+    if (sepA > mg) return;
+    best = -3.0e38f;
+    bestk = 1 << 20;
+    for (int k = lane; k < npb; k += 64) {
+        f3 n; float d;
+        world_plane(m, hb, k, PB, n, d);
+        float mn = 3.0e38f;
+        for (int i = 0; i < nva; i++) mn = fminf(mn, dot3(n, ld3(s.wvA[i])) + d);
+        if (mn > best) { best = mn; bestk = k; }
+    }
+    wave_argmax(best, bestk);
+    float sepB = best;
+    int kB = bestk;
+    if (sepB > mg) return;
+    for (int pass = 0; pass < 2; pass++) {
+        bool refB = (sepB >= sepA) ? (pass == 0) : (pass == 1);
+        int hr = refB ? hb : ha, kr = refB ? kB : kA;
+        PoseF Pr = refB ? PB : PA;
+        int nvi = refB ? nva : nvb, npr = m.hull_nplanes[hr];
+        wsync();
+        for (int k = lane; k < npr; k += 64) {
+            f3 n; float d;
+            world_plane(m, hr, k, Pr, n, d);
+            st3(s.wpR[k], n);
+            s.wpR[k][3] = d;
+        }
+        wsync();
+        f3 nref = ld3(s.wpR[kr]);
+        float dref = s.wpR[kr][3];
+        bool valid = false;
+        f3 pt = mk3(0, 0, 0);
+        float dist = 0;
+        if (lane < nvi) {
+            f3 vi = ld3(refB ? s.wvA[lane] : s.wvB[lane]);
+            dist = dot3(nref, vi) + dref;
+            if (dist <= mg) {
+                float mx = -3.0e38f;
+                for (int k = 0; k < npr; k++) {
+                    if (k == kr) continue;
+                    mx = fmaxf(mx, dot3(ld3(s.wpR[k]), vi) + s.wpR[k][3]);
+                }
+                if (mx <= mg) {
+                    valid = true;
+                    pt = vi - nref * (0.5f * dist);
+                }
+            }
+        }
+        if (__ballot(valid)) {
+            f3 n = refB ? nref : nref * -1.0f;
+            emit_contacts(c, valid, pt, dist, n, a, b);
+            return;
+        }
+    }
+}
+
+// pair enumeration in the oracle's order (see detect() in physics_oracle.c)
+HD bool pair_desc(const SimCtx& c, int p, int& kind, int& A, int& B) {
+    int NO = c.NO, NLH = c.m->n_link_hulls;
+    for (int o = 0; o < NO; o++) {
+        int n = 2 + (NO - 1 - o) + NLH;
+        if (p < n) {
+            A = o;
+            if (p == 0) { kind = 0; B = -1; }
+            else if (p == 1) { kind = 1; B = -1; }
+            else if (p < 2 + (NO - 1 - o)) { kind = 2; B = o + 1 + (p - 2); }
+            else { kind = 3; B = p - 2 - (NO - 1 - o); }
+            return true;
+        }
+        p -= n;
+    }
+    if (p < NLH) { kind = 4; A = p; B = -1; return true; }
+    return false;
+}
+
+HD void detect(SimCtx& c) {
+    EnvLDS& s = *c.s;
+    const ha_model_t& m = *c.m;
+    int lane = c.lane;
+    if (lane == 0) s.nc = 0;
+    int NO = c.NO, NLH = m.n_link_hulls;
+    int npairs = 0;
+    for (int o = 0; o < NO; o++) npairs += 2 + (NO - 1 - o) + NLH;
+    npairs += NLH;
+    PoseF Ptab{ld3(m.table_pos), ldq(m.table_quat)};
+    wsync();
+    for (int base = 0; base < npairs; base += 64) {
+        // parallel broad phase: one pair per lane
+        bool cand = false;
+        int p = base + lane;
+        int kind = -1, A = -1, B = -1;
+        if (p < npairs && pair_desc(c, p, kind, A, B)) {
+            float mg = c.p->contact_margin;
+            if (kind <= 3) {
+                cand = s.coll[A] != 0;
+                if (kind == 2) cand = cand && s.coll[B] != 0;
+                if (cand) {
+                    int ho = m.pool_hull[s.pool[A]];
+                    PoseF Po = object_pose(c, A);
+                    f3 co = Po.p + qrot(Po.q, ld3(m.hull_center[ho]));
+                    float ro = m.hull_radius[ho];
+                    if (kind == 0) {
+                        cand = co.z - ro <= mg;
+                    } else {
+                        int hb;
+                        PoseF Pb;
+                        if (kind == 1) { hb = m.table_hull; Pb = Ptab; }
+                        else if (kind == 2) { hb = m.pool_hull[s.pool[B]]; Pb = object_pose(c, B); }
+                        else { hb = B; int Lk = m.hull_link[B]; Pb = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; }
+                        f3 cbb = Pb.p + qrot(Pb.q, ld3(m.hull_center[hb]));
+                        f3 dc = co - cbb;
+                        float rr = ro + m.hull_radius[hb] + mg;
+                        cand = dot3(dc, dc) <= rr * rr;
+                    }
+                }
+            } else {
+                int Lk = m.hull_link[A];
+                cand = m.link_table_collide[Lk] != 0;
+                if (cand) {
+                    f3 ch = ld3(s.lp[Lk]) + qrot(ldq(s.lq[Lk]), ld3(m.hull_center[A]));
+                    f3 ct = Ptab.p + qrot(Ptab.q, ld3(m.hull_center[m.table_hull]));
+                    f3 dc = ch - ct;
+                    float rr = m.hull_radius[A] + m.hull_radius[m.table_hull] + mg;
+                    cand = dot3(dc, dc) <= rr * rr;
+                }
+            }
+        }
+        uint64_t mask = __ballot(cand);
+        while (mask) {
+            int bit = __ffsll((unsigned long long)mask) - 1;
+            mask &= mask - 1;
+            int q = base + bit;
+            pair_desc(c, q, kind, A, B);
+            if (kind <= 3) {
+                int ho = m.pool_hull[s.pool[A]];
+                PoseF Po = object_pose(c, A);
+                if (kind == 0) collide_ground(c, ho, Po, A);
+                else if (kind == 1) collide_hulls(c, ho, Po, m.table_hull, Ptab, A, -1);
+                else if (kind == 2) collide_hulls(c, ho, Po, m.pool_hull[s.pool[B]], object_pose(c, B), A, B);
+                else {
+                    int Lk = m.hull_link[B];
+                    collide_hulls(c, B, PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}, ho, Po, 100 + Lk, A);
+                }
+            } else {
+                int Lk = m.hull_link[A];
+                collide_hulls(c, A, PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}, m.table_hull, Ptab, 100 + Lk, -1);
+            }
+        }
+    }
+    wsync();
+}
+
+// ----------------------------------------------------------------------------- constraint rows
+HD void jac_body(const SimCtx& c, int body, f3 x, f3 dir, float sgn, float* J) {
+    const EnvLDS& s = *c.s;
+    int D = c.D;
+    if (body < 0) return;
+    if (body < 100) {
+        f3 r = x - ld3(s.oc[body]);
+        f3 ang = cross3(r, dir);
+        float* Jo = J + D + 6 * body;
+        Jo[0] += sgn * dir.x; Jo[1] += sgn * dir.y; Jo[2] += sgn * dir.z;
+        Jo[3] += sgn * ang.x; Jo[4] += sgn * ang.y; Jo[5] += sgn * ang.z;
+        return;
+    }
+    for (int j = body - 100; j >= 0; j = c.m->link_parent[j]) {
+        int d = c.m->link_dof[j];
+        if (d < 0) continue;
+        J[d] += sgn * dot3(ld3(s.ax[d]), cross3(x - ld3(s.an[d]), dir));
+    }
+}
+
+HD void tangents(f3 n, f3& t1, f3& t2) {
+    f3 a = fabsf(n.x) < 0.9f ? mk3(1, 0, 0) : mk3(0, 1, 0);
+    f3 t = cross3(n, a);
+    float l = sqrtf(dot3(t, t));
+    t1 = t * (1.0f / l);
+    t2 = cross3(n, t1);
+}
+
+HD void substep(SimCtx& c, float hdt) {
+    EnvLDS& s = *c.s;
+    const ha_model_t& m = *c.m;
+    const ha_params_t& p = *c.p;
+    int lane = c.lane, D = c.D, NO = c.NO;
+    int NV = D + 6 * NO;
+    fk(c);
+    dynamics(c);
+    // implicit PD drives with effort saturation
+    if (lane < D) {
+        int d = lane;
+        float kp = m.dof_kp[d], kd = m.dof_kd[d], eff = m.dof_effort[d];
+        float q = s.q[d], qd = s.qd[d];
+        float fpred = kp * (s.tgt[d] - q - hdt * qd) - kd * qd;
+        float tau;
+        if (fabsf(fpred) > eff) {
+            tau = fpred > 0 ? eff : -eff;
+        } else {
+            tau = kp * (s.tgt[d] - q) - kd * qd - hdt * kp * qd;
+            s.M[d * D + d] += hdt * kd + hdt * hdt * kp;
+        }
+        s.rhs[d] = hdt * (tau - s.Cb[d]);
+    }
+    wsync();
+    cholesky(c);
+    {
+        float x[MAXD];
+#pragma unroll
+        for (int i = 0; i < MAXD; i++) x[i] = i < D ? s.rhs[i] : 0.0f;
+        chol_solve_regs(c, x);
+        wsync();
+#pragma unroll
+        for (int i = 0; i < MAXD; i++)
+            if (i < D && lane == i) s.v[i] = s.qd[i] + x[i];
+    }
+    if (lane < NO) {
+        int o = lane;
+        float damp = 1.0f / (1.0f + hdt * p.object_ang_damping);
+        f3 lv = ld3(s.ov[o]) + ld3(p.gravity) * hdt;
+        f3 av = ld3(s.ow[o]) * damp;
+        float* vo = s.v + D + 6 * o;
+        vo[0] = lv.x; vo[1] = lv.y; vo[2] = lv.z; vo[3] = av.x; vo[4] = av.y; vo[5] = av.z;
+        float R[9], Iw[9], Ii[9];
+        qmat(ldq(s.oq[o]), R);
+        rart3(R, m.pool_inertia[s.pool[o]], Iw);
+        inv3(Iw, Ii);
+#pragma unroll
+        for (int k = 0; k < 9; k++) s.oIinv[o][k] = Ii[k];
+        s.om[o] = m.pool_mass[s.pool[o]];
+    }
+    wsync();
+    detect(c);
+    // ---- rows: lane r owns row r
+    int nc = s.nc;
+    int ncrow = 3 * nc;    // nc <= MAXC = 21 -> <= 63 rows
+    int r = lane;
+    float* Jr = s.J + r * RS;
+    for (int k = 0; k < RS; k++) Jr[k] = 0.0f;
+    float vt = 0.f, lo = 0.f, hi = 0.f;
+    int fric_of = -1, rcont = -1;
+    if (r < ncrow) {
+        int ci = r / 3, k = r % 3;
+        f3 n = ld3(s.cn[ci]), t1, t2;
+        tangents(n, t1, t2);
+        f3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
+        f3 x = ld3(s.cx[ci]);
+        jac_body(c, s.ca[ci], x, dir, 1.0f, Jr);
+        jac_body(c, s.cb[ci], x, dir, -1.0f, Jr);
+        rcont = ci;
+        if (k == 0) {
+            float sp = s.csep[ci];
+            vt = sp > 0 ? -sp / hdt : -p.baumgarte * sp / hdt;
+            if (vt > p.max_depen_vel) vt = p.max_depen_vel;
+            hi = 3.0e38f;
+        } else {
+            fric_of = r - k;
+        }
+    }
+    // joint-limit rows, compacted after the contact rows in (dof, lower/upper) order
+    bool lim_lo = false, lim_up = false;
+    float s_lo = 0, s_up = 0;
+    if (lane < D) {
+        s_lo = s.q[lane] - m.dof_lower[lane];
+        s_up = m.dof_upper[lane] - s.q[lane];
+        lim_lo = s_lo <= p.joint_limit_margin;
+        lim_up = s_up <= p.joint_limit_margin;
+    }
+    int cnt = (int)lim_lo + (int)lim_up;
+    // exclusive prefix sum over lanes
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        int t = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += t;
+    }
+    int excl = incl - cnt;
+    int nlim = bcast_i(incl, 63);
+    int nr = ncrow + nlim;
+    if (nr > MAXR) nr = MAXR;
+    wsync();
+    for (int side = 0; side < 2; side++) {
+        bool act = side == 0 ? lim_lo : lim_up;
+        int rr = ncrow + excl + (side == 1 && lim_lo ? 1 : 0);
+        if (act && rr < MAXR) {
+            float* Jl = s.J + rr * RS;
+            Jl[lane] = side == 0 ? 1.0f : -1.0f;
+            float sp = side == 0 ? s_lo : s_up;
+            s.vt[rr] = sp > 0 ? -sp / hdt : -p.baumgarte * sp / hdt;
+            s.lo[rr] = 0.f;
+            s.hi[rr] = 3.0e38f;
+            s.fric_of[rr] = -1;
+            s.rcontact[rr] = -1;
+        }
+    }
+    if (r < ncrow) {
+        s.vt[r] = vt; s.lo[r] = lo; s.hi[r] = hi; s.fric_of[r] = fric_of; s.rcontact[r] = rcont;
+    }
+    wsync();
+    // ---- Y_r = M^-1 J_r^T (registers) and the Delassus column A[:, r]
+    float y[RS];
+#pragma unroll
+    for (int k = 0; k < RS; k++) y[k] = 0.0f;
+    bool myrow = r < nr;
+    if (myrow) {
+        float x[MAXD];
+#pragma unroll
+        for (int i = 0; i < MAXD; i++) x[i] = i < D ? Jr[i] : 0.0f;
+        chol_solve_regs(c, x);
+#pragma unroll
+        for (int i = 0; i < MAXD; i++)
+            if (i < D) y[i] = x[i];
+        // object blocks: (J_lin / m, I_world^-1 J_ang)
+#pragma unroll
+        for (int t = 0; t < RS; t++) {
+            if (t >= D && t < NV) {
+                int o = (t - D) / 6, k = (t - D) - 6 * o;
+                const float* Jo = Jr + D + 6 * o;
+                if (k < 3) {
+                    y[t] = Jo[k] * (1.0f / s.om[o]);
+                } else {
+                    const float* Ir = s.oIinv[o] + 3 * (k - 3);
+                    y[t] = Ir[0] * Jo[3] + Ir[1] * Jo[4] + Ir[2] * Jo[5];
+                }
+            }
+        }
+    }
+    float A[MAXR];
+    float w = 0.f, lam = 0.f, rinv = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXR; k++) {
+        A[k] = 0.f;
+        if (k < nr && myrow) {
+            const float* Jk = s.J + k * RS;
+            float a = 0.f;
+#pragma unroll
+            for (int t = 0; t < RS; t++)
+                if (t < NV) a += Jk[t] * y[t];
+            A[k] = a;
+        }
+    }
+    if (myrow) {
+        float b = 0.f;
+        for (int t = 0; t < NV; t++) b += Jr[t] * s.v[t];
+        w = b - s.vt[r];
+#pragma unroll
+        for (int k = 0; k < MAXR; k++)
+            if (k == r) { A[k] += 1e-9f; rinv = A[k]; }
+        lo = s.lo[r]; hi = s.hi[r]; fric_of = s.fric_of[r];
+    }
+    // ---- projected Gauss-Seidel: row r's residual / impulse live in lane r
+    const float mu = p.friction;
+    for (int it = 0; it < p.solver_iters; it++) {
+#pragma unroll
+        for (int k = 0; k < MAXR; k++) {
+            if (k < nr) {
+                float wk = bcast(w, k), lk = bcast(lam, k), akk = bcast(rinv, k);
+                float lok = bcast(lo, k), hik = bcast(hi, k);
+                int fo = bcast_i(fric_of, k);
+                if (fo >= 0) {
+                    hik = mu * bcast(lam, fo);
+                    lok = -hik;
+                }
+                float nl = lk - wk / akk;
+                nl = nl < lok ? lok : (nl > hik ? hik : nl);
+                float dl = nl - lk;
+                if (dl != 0.0f) {
+                    if (lane == k) lam = nl;
+                    w += A[k] * dl;
+                }
+            }
+        }
+    }
+    wsync();
+    // ---- v += sum_r Y_r lam_r  (transpose through LDS, sequential sum in row order like the oracle)
+    float* T = s.J;    // [NV][64]
+    if (myrow) {
+#pragma unroll
+        for (int t = 0; t < RS; t++)
+            if (t < NV) T[t * 64 + r] = y[t] * lam;
+    }
+    s.scratch[lane] = lam;
+    wsync();
+    if (lane < NV) {
+        float acc = s.v[lane];
+        for (int k = 0; k < nr; k++) acc += T[lane * 64 + k];
+        s.v[lane] = acc;
+    }
+    // contact forces (last substep wins, like the oracle)
+    if (lane == 0) {
+        for (int b = 0; b < MAXB; b++) s.cforce[b][0] = s.cforce[b][1] = s.cforce[b][2] = 0.f;
+        for (int ci = 0; ci < nc; ci++) {
+            int r0 = 3 * ci;
+            if (r0 + 2 >= nr) break;
+            f3 n = ld3(s.cn[ci]), t1, t2;
+            tangents(n, t1, t2);
+            f3 f = (n * s.scratch[r0] + t1 * s.scratch[r0 + 1]) + t2 * s.scratch[r0 + 2];
+            f = f * (1.0f / hdt);
+            int bodies[2] = {s.ca[ci], s.cb[ci]};
+            for (int sd = 0; sd < 2; sd++) {
+                int bd = bodies[sd];
+                float sg = sd == 0 ? 1.0f : -1.0f;
+                int idx = -1;
+                if (bd >= 100) idx = 1 + (bd - 100);
+                else if (bd >= 0) idx = 1 + m.n_links + 1 + bd;
+                if (idx < 0) continue;
+                s.cforce[idx][0] += sg * f.x; s.cforce[idx][1] += sg * f.y; s.cforce[idx][2] += sg * f.z;
+            }
+        }
+    }
+    wsync();
+    // ---- integrate
+    if (lane < D) {
+        float vv = s.v[lane];
+        s.qd[lane] = vv;
+        s.q[lane] += hdt * vv;
+    }
+    if (lane < NO) {
+        int o = lane;
+        const float* vo = s.v + D + 6 * o;
+        f3 lv = mk3(vo[0], vo[1], vo[2]), av = mk3(vo[3], vo[4], vo[5]);
+        st3(s.ov[o], lv);
+        st3(s.ow[o], av);
+        st3(s.oc[o], ld3(s.oc[o]) + lv * hdt);
+        qf q = ldq(s.oq[o]);
+        qf dq = qmul(qf{av.x, av.y, av.z, 0.0f}, q);
+        stq(s.oq[o], qnormalize(qf{q.x + 0.5f * hdt * dq.x, q.y + 0.5f * hdt * dq.y, q.z + 0.5f * hdt * dq.z,
+                                   q.w + 0.5f * hdt * dq.w}));
+    }
+    wsync();
+}

@@ -1,0 +1,462 @@
+// handarm_hip.hip - kernels and C ABI of libhandarm_hip.so (MI355X / gfx950).
+//
+// One 64-lane wavefront simulates one environment; a launch has one 64-thread workgroup per env,
+// so a 8192-env shard is 8192 workgroups (32 per CU). Per-env state is staged in LDS (EnvLDS) for
+// the whole env-step (all substeps) and written back once; the gym tensors keep the Isaac Gym
+// env-major layouts so one env's slice is contiguous and its loads/stores are coalesced.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ha_task.h"
+
+enum { MODE_SIMULATE = 0, MODE_STEP = 1, MODE_OBSERVE = 2, MODE_RESET = 3 };
+
+// ----------------------------------------------------------------------------- state load/store
+__device__ void load_env(SimCtx& c, const ha_state_t& st, int env) {
+    EnvLDS& s = *c.s;
+    int lane = c.lane, D = c.D, NO = c.NO, A = 3 + NO;
+    if (lane < D) {
+        s.q[lane] = st.dof_state[((size_t)env * D + lane) * 2];
+        s.qd[lane] = st.dof_state[((size_t)env * D + lane) * 2 + 1];
+        s.tgt[lane] = st.sim_targets[(size_t)env * D + lane];
+    }
+    if (lane < NO) {
+        int o = lane;
+        const float* r = st.root_state + ((size_t)env * A + 3 + o) * 13;
+        int pid = (int)st.object_indices[(size_t)env * NO + o];
+        s.pool[o] = pid;
+        qf q = ldq(r + 3);
+        stq(s.oq[o], q);
+        st3(s.oc[o], ld3(r) + qrot(q, ld3(c.m->pool_com[pid])));
+        st3(s.ov[o], ld3(r + 7));
+        st3(s.ow[o], ld3(r + 10));
+        s.coll[o] = st.collision_enabled ? st.collision_enabled[(size_t)env * NO + o] : 1;
+    }
+    for (int b = lane; b < MAXB; b += 64) s.cforce[b][0] = s.cforce[b][1] = s.cforce[b][2] = 0.0f;
+    wsync();
+}
+
+// writes dof_state, object root states, rigid_body_state, net_contact_force; fills the observation
+// snapshot from the same (final) kinematics.
+__device__ void store_env(SimCtx& c, const ha_state_t& st, int env, ObsIn* in) {
+    EnvLDS& s = *c.s;
+    const ha_model_t& m = *c.m;
+    int lane = c.lane, D = c.D, NO = c.NO, A = 3 + NO, L = c.L, B = 1 + L + 1 + NO;
+    fk(c);
+    // link twists (level-synchronous)
+    if (lane == 0) for (int k = 0; k < 6; k++) s.Vl[0][k] = 0.f;
+    wsync();
+    for (int lev = 1; lev <= m.max_level; lev++) {
+        if (lane < L && m.link_level[lane] == lev) {
+            int i = lane, par = m.link_parent[i], d = m.link_dof[i];
+            f3 vw = ld3(&s.Vl[par][0]), vv = ld3(&s.Vl[par][3]);
+            if (d >= 0) {
+                f3 axd = ld3(s.ax[d]);
+                vw = vw + axd * s.qd[d];
+                vv = vv + cross3(ld3(s.an[d]), axd) * s.qd[d];
+            }
+            st3(&s.Vl[i][0], vw);
+            st3(&s.Vl[i][3], vv);
+        }
+        wsync();
+    }
+    if (lane < D) {
+        st.dof_state[((size_t)env * D + lane) * 2] = s.q[lane];
+        st.dof_state[((size_t)env * D + lane) * 2 + 1] = s.qd[lane];
+        st.sim_targets[(size_t)env * D + lane] = s.tgt[lane];
+    }
+    if (lane < NO) {
+        int o = lane;
+        float* r = st.root_state + ((size_t)env * A + 3 + o) * 13;
+        qf q = ldq(s.oq[o]);
+        f3 pos = ld3(s.oc[o]) - qrot(q, ld3(m.pool_com[s.pool[o]]));
+        st3(r, pos); stq(r + 3, q); st3(r + 7, ld3(s.ov[o])); st3(r + 10, ld3(s.ow[o]));
+    }
+    wsync();
+    float* bs = st.rigid_body_state + (size_t)env * B * 13;
+    const float* rs = st.root_state + (size_t)env * A * 13;
+    // rigid bodies: goal(0), robot links 1..L, table L+1, objects L+2.. ; 13 floats each
+    for (int e = lane; e < B * 13; e += 64) {
+        int b = e / 13, k = e % 13;
+        float v;
+        if (b == 0) v = rs[k];
+        else if (b <= L) {
+            int i = b - 1;
+            if (k < 3) v = s.lp[i][k];
+            else if (k < 7) v = s.lq[i][k - 3];
+            else if (k < 10) {
+                f3 cc = ld3(s.lp[i]) + qrot(ldq(s.lq[i]), ld3(m.link_com[i]));
+                f3 lin = ld3(&s.Vl[i][3]) + cross3(ld3(&s.Vl[i][0]), cc);
+                v = k == 7 ? lin.x : (k == 8 ? lin.y : lin.z);
+            } else v = s.Vl[i][k - 7];
+        } else if (b == L + 1) v = rs[2 * 13 + k];
+        else {
+            int o = b - L - 2;
+            if (k < 3) { f3 pos = ld3(s.oc[o]) - qrot(ldq(s.oq[o]), ld3(m.pool_com[s.pool[o]])); v = k == 0 ? pos.x : (k == 1 ? pos.y : pos.z); }
+            else if (k < 7) v = s.oq[o][k - 3];
+            else if (k < 10) v = s.ov[o][k - 7];
+            else v = s.ow[o][k - 10];
+        }
+        bs[e] = v;
+    }
+    for (int e = lane; e < B * 3; e += 64) st.net_contact_force[(size_t)env * B * 3 + e] = s.cforce[e / 3][e % 3];
+    if (in) {
+        if (lane < 7) in->flange[lane] = lane < 3 ? s.lp[LINK_FLANGE][lane] : s.lq[LINK_FLANGE][lane - 3];
+        if (lane < 50) {
+            int t = lane / 10, k = lane % 10, i = c_tip_links[t];
+            float v;
+            if (k < 3) v = s.lp[i][k];
+            else if (k < 7) v = s.lq[i][k - 3];
+            else {
+                f3 cc = ld3(s.lp[i]) + qrot(ldq(s.lq[i]), ld3(m.link_com[i]));
+                f3 lin = ld3(&s.Vl[i][3]) + cross3(ld3(&s.Vl[i][0]), cc);
+                v = k == 7 ? lin.x : (k == 8 ? lin.y : lin.z);
+            }
+            in->tip[t][k] = v;
+        }
+        if (lane < D) in->dofpos[lane] = s.q[lane];
+        for (int e = lane; e < NO * 13; e += 64) {
+            int o = e / 13, k = e % 13;
+            float v;
+            if (k < 3) { f3 pos = ld3(s.oc[o]) - qrot(ldq(s.oq[o]), ld3(m.pool_com[s.pool[o]])); v = k == 0 ? pos.x : (k == 1 ? pos.y : pos.z); }
+            else if (k < 7) v = s.oq[o][k - 3];
+            else if (k < 10) v = s.ov[o][k - 7];
+            else v = s.ow[o][k - 10];
+            in->obj[o][k] = v;
+        }
+    }
+    wsync();
+}
+
+// observation snapshot straight from the (refreshed) state tensors
+__device__ void snapshot_from_tensors(SimCtx& c, const ha_state_t& st, int env, ObsIn* in) {
+    int lane = c.lane, D = c.D, NO = c.NO, A = 3 + NO, L = c.L, B = 1 + L + 1 + NO;
+    const float* bs = st.rigid_body_state + (size_t)env * B * 13;
+    if (lane < 7) in->flange[lane] = bs[(1 + LINK_FLANGE) * 13 + lane];
+    if (lane < 50) {
+        int t = lane / 10, k = lane % 10;
+        in->tip[t][k] = bs[(1 + c_tip_links[t]) * 13 + k];
+    }
+    if (lane < D) in->dofpos[lane] = st.dof_state[((size_t)env * D + lane) * 2];
+    for (int e = lane; e < NO * 13; e += 64) in->obj[e / 13][e % 13] = st.root_state[((size_t)env * A + 3) * 13 + e];
+    if (lane < NO) c.s->pool[lane] = (int)st.object_indices[(size_t)env * NO + lane];
+    wsync();
+}
+
+__device__ void run_physics(SimCtx& c, int n_calls) {
+    float hdt = c.p->dt / (float)c.p->substeps;
+    for (int k = 0; k < n_calls; k++)
+        for (int sub = 0; sub < c.p->substeps; sub++) substep(c, hdt);
+}
+
+// ----------------------------------------------------------------------------- the kernel
+extern "C" __global__ void __launch_bounds__(64)
+ha_env_kernel(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params, ha_state_t st,
+              int num_envs, int mode, int n_calls, uint32_t flags, int stat_slot) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int env = blockIdx.x;
+    if (env >= num_envs) return;
+    SimCtx c;
+    c.m = model;
+    c.p = params;
+    c.s = reinterpret_cast<EnvLDS*>(smem);
+    c.lane = threadIdx.x;
+    c.D = model->n_dofs;
+    c.NO = params->n_objects;
+    c.L = model->n_links;
+    ObsIn& in = c.s->in;
+    ha_state_t S = st;
+    if (mode == MODE_STEP || mode == MODE_OBSERVE) {
+        S.stats = st.stats + stat_slot * HA_STAT_SIZE;
+        S.term_sums = st.term_sums + stat_slot * 4;
+    }
+    if (mode == MODE_OBSERVE) {
+        snapshot_from_tensors(c, S, env, &in);
+        post_step(c, S, env, in, (flags & HA_FLAG_OBS_ONLY) != 0);
+        return;
+    }
+    load_env(c, S, env);
+    if (mode == MODE_SIMULATE) {
+        run_physics(c, n_calls);
+        store_env(c, S, env, nullptr);
+        return;
+    }
+    if (mode == MODE_RESET) {
+        task_reset(c, S, env, flags);
+        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics(c, 1);
+        task_reset_finish(c, S, env);
+        store_env(c, S, env, nullptr);
+        return;
+    }
+    // MODE_STEP: VecTask.step (vec_task.py:390-441) for Ur5SihMultiObjectManipulation
+    bool do_reset = S.reset_buf[env] != 0;                   // configurable_vec_task.py:348
+    controller_step(c, S, env);                               // :350-354
+    if (do_reset) {                                           // :356-357 -> reset_idx
+        task_reset(c, S, env, flags);
+        // reset_idx's extra gym.simulate (multi_object_manipulation.py:67). The reference resets every
+        // env on the same step (ur5sih.py:617 asserts it), so a per-env extra call is equivalent.
+        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics(c, 1);
+        task_reset_finish(c, S, env);
+    }
+    if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics(c, c.p->control_freq_inv);   // vec_task.py:409-412
+    store_env(c, S, env, &in);
+    post_step(c, S, env, in, false);                           // configurable_vec_task.py:359-390
+}
+
+// ----------------------------------------------------------------------------- indexed setters
+extern "C" __global__ void ha_copy_indexed_kernel(float* dst, const float* src, const int32_t* idx, int n, int row,
+                                                  int rows_per_index) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    int per = row * rows_per_index;
+    if (t >= n * per) return;
+    int i = t / per, k = t % per;
+    size_t base = (size_t)idx[i] * per;
+    dst[base + k] = src[base + k];
+}
+
+// ----------------------------------------------------------------------------- C ABI
+struct ha_handle_s {
+    ha_model_t* d_model;
+    ha_params_t* d_params;
+    ha_params_t h_params;
+    int N, NO, D, L, A, B;
+    ha_state_t st;
+    int bound;
+    int stat_slots;
+    long long step_counter;
+    hipEvent_t ev0, ev1;
+    int timed;
+    int t_max, t_count;
+    hipEvent_t* t_ev;     // 2 * t_max events
+};
+
+#define HIPCHK(x)                                                                     \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            fprintf(stderr, "handarm_hip: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return HA_E_HIP;                                                          \
+        }                                                                             \
+    } while (0)
+
+static size_t lds_bytes() { return sizeof(EnvLDS); }
+
+extern "C" {
+
+int ha_abi_version(void) { return HA_ABI_VERSION; }
+
+int ha_struct_sizes(int32_t* model_size, int32_t* params_size, int32_t* state_size) {
+    if (!model_size || !params_size || !state_size) return HA_E_ARG;
+    *model_size = (int32_t)sizeof(ha_model_t);
+    *params_size = (int32_t)sizeof(ha_params_t);
+    *state_size = (int32_t)sizeof(ha_state_t);
+    return HA_OK;
+}
+
+int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_envs, ha_handle* out) {
+    if (!model || !params || !out || num_envs <= 0) return HA_E_ARG;
+    if (model->n_dofs > MAXD || model->n_links > HA_MAX_LINKS || params->n_objects > NOBJ ||
+        model->n_dofs + 6 * params->n_objects > RS || model->n_link_hulls + model->n_pool + 1 > HA_MAX_HULLS)
+        return HA_E_MODEL;
+    for (int k = 0; k < model->n_hulls; k++)
+        if (model->hull_nverts[k] > 64 || model->hull_nplanes[k] > 128) return HA_E_MODEL;
+    if (params->num_initial_poses < 1 || params->num_initial_poses > HA_MAX_INIT_POSES) return HA_E_ARG;
+    ha_handle h = (ha_handle)calloc(1, sizeof(ha_handle_s));
+    h->N = num_envs;
+    h->NO = params->n_objects;
+    h->D = model->n_dofs;
+    h->L = model->n_links;
+    h->A = 3 + h->NO;
+    h->B = 1 + h->L + 1 + h->NO;
+    h->h_params = *params;
+    h->stat_slots = 1;
+    HIPCHK(hipMalloc(&h->d_model, sizeof(ha_model_t)));
+    HIPCHK(hipMalloc(&h->d_params, sizeof(ha_params_t)));
+    HIPCHK(hipMemcpy(h->d_model, model, sizeof(ha_model_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->d_params, params, sizeof(ha_params_t), hipMemcpyHostToDevice));
+    HIPCHK(hipFuncSetAttribute((const void*)ha_env_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds_bytes()));
+    HIPCHK(hipEventCreate(&h->ev0));
+    HIPCHK(hipEventCreate(&h->ev1));
+    *out = h;
+    return HA_OK;
+}
+
+int ha_destroy(ha_handle h) {
+    if (!h) return HA_E_ARG;
+    (void)hipFree(h->d_model);
+    (void)hipFree(h->d_params);
+    (void)hipEventDestroy(h->ev0);
+    (void)hipEventDestroy(h->ev1);
+    free(h);
+    return HA_OK;
+}
+
+int ha_bind_state(ha_handle h, const ha_state_t* state) {
+    if (!h || !state) return HA_E_ARG;
+    const void* req[] = {state->root_state, state->rigid_body_state, state->dof_state, state->net_contact_force,
+                         state->sim_targets};
+    for (auto p : req)
+        if (!p) return HA_E_ARG;
+    h->st = *state;
+    h->bound = 1;
+    return HA_OK;
+}
+
+static int launch(ha_handle h, int mode, int n_calls, uint32_t flags, int slot, void* stream) {
+    if (!h || !h->bound) return HA_E_STATE;
+    hipStream_t s = (hipStream_t)stream;
+    bool rec = h->t_ev && h->t_count < h->t_max;
+    (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count] : h->ev0, s);
+    hipLaunchKernelGGL(ha_env_kernel, dim3(h->N), dim3(64), lds_bytes(), s, h->d_model, h->d_params, h->st, h->N,
+                       mode, n_calls, flags, slot);
+    HIPCHK(hipGetLastError());
+    (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count + 1] : h->ev1, s);
+    if (rec) {
+        (void)hipEventRecord(h->ev1, s);
+        h->t_count++;
+    }
+    h->timed = 1;
+    return HA_OK;
+}
+
+int ha_simulate(ha_handle h, int32_t n_calls, uint32_t flags, void* stream) {
+    if (n_calls < 0) return HA_E_ARG;
+    if (n_calls == 0 || (flags & HA_FLAG_NO_PHYSICS)) return HA_OK;
+    return launch(h, MODE_SIMULATE, n_calls, flags, 0, stream);
+}
+
+// The bound tensors ARE the simulation state (zero-copy), so refresh has nothing to copy.
+int ha_refresh(ha_handle h, void* stream) {
+    (void)stream;
+    return (h && h->bound) ? HA_OK : HA_E_STATE;
+}
+
+int ha_set_dof_position_target(ha_handle h, const float* targets, void* stream) {
+    if (!h || !h->bound || !targets) return HA_E_ARG;
+    if (targets != h->st.sim_targets)
+        HIPCHK(hipMemcpyAsync(h->st.sim_targets, targets, sizeof(float) * h->N * h->D, hipMemcpyDeviceToDevice,
+                              (hipStream_t)stream));
+    return HA_OK;
+}
+
+static int copy_indexed(ha_handle h, float* dst, const float* src, const int32_t* idx, int n, int row, int rpi,
+                        void* stream) {
+    if (!h || !h->bound || !src || !idx || n < 0) return HA_E_ARG;
+    if (n == 0 || src == dst) return HA_OK;
+    int total = n * row * rpi;
+    hipLaunchKernelGGL(ha_copy_indexed_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, dst, src,
+                       idx, n, row, rpi);
+    HIPCHK(hipGetLastError());
+    return HA_OK;
+}
+
+// actor indices are global (env * A + actor); the root-state tensor row of actor a is a
+int ha_set_actor_root_state_indexed(ha_handle h, const float* root_state, const int32_t* actor_indices, int32_t n,
+                                    void* stream) {
+    return copy_indexed(h, h ? h->st.root_state : nullptr, root_state, actor_indices, n, 13, 1, stream);
+}
+
+// only the robot actor owns DOFs; its DOF rows of env e are e*D .. e*D+D-1 (actor index -> env = a / A)
+__global__ void ha_copy_dof_kernel(float* dst, const float* src, const int32_t* idx, int n, int A, int D, int w) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * D * w) return;
+    int i = t / (D * w), k = t % (D * w);
+    size_t env = (size_t)(idx[i] / A);
+    dst[env * D * w + k] = src[env * D * w + k];
+}
+
+static int copy_dof_indexed(ha_handle h, float* dst, const float* src, const int32_t* idx, int n, int w,
+                            void* stream) {
+    if (!h || !h->bound || !src || !idx || n < 0) return HA_E_ARG;
+    if (n == 0 || src == dst) return HA_OK;
+    int total = n * h->D * w;
+    hipLaunchKernelGGL(ha_copy_dof_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, dst, src,
+                       idx, n, h->A, h->D, w);
+    HIPCHK(hipGetLastError());
+    return HA_OK;
+}
+
+int ha_set_dof_state_indexed(ha_handle h, const float* dof_state, const int32_t* actor_indices, int32_t n,
+                             void* stream) {
+    return copy_dof_indexed(h, h ? h->st.dof_state : nullptr, dof_state, actor_indices, n, 2, stream);
+}
+
+int ha_set_dof_position_target_indexed(ha_handle h, const float* targets, const int32_t* actor_indices, int32_t n,
+                                       void* stream) {
+    return copy_dof_indexed(h, h ? h->st.sim_targets : nullptr, targets, actor_indices, n, 1, stream);
+}
+
+int ha_set_object_collision_filter(ha_handle h, const uint8_t* enabled, void* stream) {
+    if (!h || !h->bound || !enabled || !h->st.collision_enabled) return HA_E_ARG;
+    if (enabled != h->st.collision_enabled)
+        HIPCHK(hipMemcpyAsync(h->st.collision_enabled, enabled, (size_t)h->N * h->NO, hipMemcpyDeviceToDevice,
+                              (hipStream_t)stream));
+    return HA_OK;
+}
+
+int ha_set_stats_ring(ha_handle h, int32_t n_slots) {
+    if (!h || n_slots < 1) return HA_E_ARG;
+    h->stat_slots = n_slots;
+    h->step_counter = 0;
+    return HA_OK;
+}
+
+int ha_task_step(ha_handle h, uint32_t flags, void* stream) {
+    if (!h || !h->bound || !h->st.actions || !h->st.obs || !h->st.stats || !h->st.term_sums) return HA_E_STATE;
+    int slot = (int)(h->step_counter % h->stat_slots);
+    h->step_counter++;
+    HIPCHK(hipMemsetAsync(h->st.stats + slot * HA_STAT_SIZE, 0, sizeof(int32_t) * HA_STAT_SIZE, (hipStream_t)stream));
+    HIPCHK(hipMemsetAsync(h->st.term_sums + slot * 4, 0, sizeof(float) * 4, (hipStream_t)stream));
+    return launch(h, MODE_STEP, 0, flags, slot, stream);
+}
+
+int ha_task_observe(ha_handle h, uint32_t flags, void* stream) {
+    if (!h || !h->bound || !h->st.obs) return HA_E_STATE;
+    HIPCHK(hipMemsetAsync(h->st.stats, 0, sizeof(int32_t) * HA_STAT_SIZE, (hipStream_t)stream));
+    HIPCHK(hipMemsetAsync(h->st.term_sums, 0, sizeof(float) * 4, (hipStream_t)stream));
+    return launch(h, MODE_OBSERVE, 0, flags, 0, stream);
+}
+
+int ha_task_reset(ha_handle h, uint32_t flags, void* stream) {
+    if (!h || !h->bound) return HA_E_STATE;
+    return launch(h, MODE_RESET, 0, flags, 0, stream);
+}
+
+int ha_enable_kernel_timing(ha_handle h, int32_t max_launches) {
+    if (!h || max_launches < 0) return HA_E_ARG;
+    if (h->t_ev) {
+        for (int i = 0; i < 2 * h->t_max; i++) (void)hipEventDestroy(h->t_ev[i]);
+        free(h->t_ev);
+        h->t_ev = nullptr;
+    }
+    h->t_max = max_launches;
+    h->t_count = 0;
+    if (max_launches == 0) return HA_OK;
+    h->t_ev = (hipEvent_t*)calloc(2 * max_launches, sizeof(hipEvent_t));
+    for (int i = 0; i < 2 * max_launches; i++) HIPCHK(hipEventCreate(&h->t_ev[i]));
+    return HA_OK;
+}
+
+int ha_kernel_times(ha_handle h, float* out_ms, int32_t max, int32_t* n_out) {
+    if (!h || !out_ms || !n_out) return HA_E_ARG;
+    int n = h->t_count < max ? h->t_count : max;
+    for (int i = 0; i < n; i++) {
+        HIPCHK(hipEventSynchronize(h->t_ev[2 * i + 1]));
+        HIPCHK(hipEventElapsedTime(&out_ms[i], h->t_ev[2 * i], h->t_ev[2 * i + 1]));
+    }
+    *n_out = n;
+    return HA_OK;
+}
+
+float ha_last_kernel_ms(ha_handle h) {
+    if (!h || !h->timed) return -1.0f;
+    float ms = -1.0f;
+    if (hipEventSynchronize(h->ev1) != hipSuccess) return -1.0f;
+    if (hipEventElapsedTime(&ms, h->ev0, h->ev1) != hipSuccess) return -1.0f;
+    return ms;
+}
+
+}  // extern "C"

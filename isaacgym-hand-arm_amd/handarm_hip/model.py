@@ -1,0 +1,295 @@
+"""Host-side model packing: scene JSON + task config -> the C-ABI structs of include/handarm_abi.h.
+
+The ctypes classes below mirror ``ha_model_t`` / ``ha_params_t`` / ``ha_state_t`` field for field;
+``tests/test_abi.py`` checks their sizes against the compiled libraries (``ha_struct_sizes``).
+Config values and their reference sources:
+  sim:    dt 1/60, substeps 2, position iterations 8      (cfg/task/Ur5SihBase.yaml:27-31)
+  task:   controlFrequencyInv 3, episode length 200, reward scales, thresholds
+          (cfg/task/Ur5SihMultiObjectManipulation.yaml:21,55-74)
+  env:    3 objects, drop/goal regions, table height 0.5   (cfg/task/Ur5SihMultiObject.yaml)
+  robot:  reset pose, kp/kd                                 (cfg/task/Ur5SihBase.yaml:3-9)
+  servo:  limits, spline knots, proximal coefficients       (tasks/hand_arm/base/ur5sih.py:437-456)
+"""
+import ctypes as C
+import json
+import os
+
+import numpy as np
+
+ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "ur5sih_scene.json")
+
+MAX_LINKS, MAX_DOFS, MAX_HULLS, MAX_VERTS, MAX_PLANES = 32, 24, 64, 4096, 8192
+MAX_POOL, MAX_OBJ, MAX_INIT_POSES, MAX_SPLINE_PIECES, N_SPLINES = 32, 3, 4, 8, 8
+MAX_MPAIRS = 192
+STAT_SIZE = 2 + 2 * MAX_POOL
+
+FLAG_NO_PHYSICS = 1
+FLAG_REPLAY_DRAWS = 2
+FLAG_OBS_ONLY = 4
+
+f32, i32 = C.c_float, C.c_int32
+
+
+def arr(t, *dims):
+    for d in reversed(dims):
+        t = t * d
+    return t
+
+
+class HaModel(C.Structure):
+    _fields_ = [
+        ("n_links", i32), ("n_dofs", i32), ("n_link_hulls", i32), ("n_pool", i32), ("n_hulls", i32),
+        ("link_parent", arr(i32, MAX_LINKS)), ("link_dof", arr(i32, MAX_LINKS)),
+        ("link_table_collide", arr(i32, MAX_LINKS)),
+        ("link_origin_pos", arr(f32, MAX_LINKS, 3)), ("link_origin_quat", arr(f32, MAX_LINKS, 4)),
+        ("link_axis", arr(f32, MAX_LINKS, 3)), ("link_mass", arr(f32, MAX_LINKS)),
+        ("link_com", arr(f32, MAX_LINKS, 3)), ("link_inertia", arr(f32, MAX_LINKS, 9)),
+        ("dof_lower", arr(f32, MAX_DOFS)), ("dof_upper", arr(f32, MAX_DOFS)), ("dof_effort", arr(f32, MAX_DOFS)),
+        ("dof_kp", arr(f32, MAX_DOFS)), ("dof_kd", arr(f32, MAX_DOFS)),
+        ("base_pos", arr(f32, 3)), ("base_quat", arr(f32, 4)),
+        ("hull_link", arr(i32, MAX_HULLS)), ("hull_vert_start", arr(i32, MAX_HULLS)),
+        ("hull_nverts", arr(i32, MAX_HULLS)), ("hull_plane_start", arr(i32, MAX_HULLS)),
+        ("hull_nplanes", arr(i32, MAX_HULLS)), ("hull_center", arr(f32, MAX_HULLS, 3)),
+        ("hull_radius", arr(f32, MAX_HULLS)),
+        ("verts", arr(f32, MAX_VERTS, 4)), ("planes", arr(f32, MAX_PLANES, 4)),
+        ("pool_hull", arr(i32, MAX_POOL)), ("pool_mass", arr(f32, MAX_POOL)), ("pool_com", arr(f32, MAX_POOL, 3)),
+        ("pool_inertia", arr(f32, MAX_POOL, 9)), ("pool_bbox_pos", arr(f32, MAX_POOL, 3)),
+        ("pool_bbox_quat", arr(f32, MAX_POOL, 4)), ("pool_bbox_ext", arr(f32, MAX_POOL, 3)),
+        ("table_hull", i32), ("table_pos", arr(f32, 3)), ("table_quat", arr(f32, 4)),
+        ("link_level", arr(i32, MAX_LINKS)), ("max_level", i32), ("dof_link", arr(i32, MAX_DOFS)),
+        ("n_mpairs", i32), ("mpair", arr(i32, MAX_MPAIRS, 2)),
+    ]
+
+
+class HaParams(C.Structure):
+    _fields_ = [
+        ("dt", f32), ("substeps", i32), ("control_freq_inv", i32), ("solver_iters", i32),
+        ("gravity", arr(f32, 3)), ("friction", f32), ("contact_margin", f32), ("baumgarte", f32),
+        ("max_depen_vel", f32), ("object_ang_damping", f32), ("joint_limit_margin", f32),
+        ("n_objects", i32), ("num_initial_poses", i32), ("max_episode_length", i32),
+        ("action_dt", f32), ("sih_alpha", f32),
+        ("reward_reaching", f32), ("reward_lifting", f32), ("reward_goal", f32), ("reward_success", f32),
+        ("lifting_threshold", f32), ("goal_threshold", f32),
+        ("goal_pos", arr(f32, 3)), ("goal_noise", arr(f32, 3)), ("reset_pose", arr(f32, MAX_DOFS)),
+        ("servo_lower", arr(f32, 5)), ("servo_upper", arr(f32, 5)), ("proximal_coef", arr(f32, 4)),
+        ("spline_pieces", arr(i32, N_SPLINES)), ("spline", arr(f32, N_SPLINES, 5, MAX_SPLINE_PIECES)),
+        ("thumb_opposition_gain", f32), ("seed", C.c_uint64),
+    ]
+
+
+P = C.c_void_p
+
+
+STATE_FIELDS = ["root_state", "rigid_body_state", "dof_state", "net_contact_force", "sim_targets",
+                "dof_position_targets", "actions", "obs", "teacher_obs", "rew", "reset_buf", "progress_buf",
+                "timeout_buf", "goal_reached_before", "goal_pos", "target_object_index",
+                "object_configuration_indices", "object_indices", "object_pos_initial", "object_quat_initial",
+                "ur5_target", "servo", "smoothed", "obs_cache", "reset_draws", "episode", "stats", "term_sums",
+                "flags", "collision_enabled"]
+
+
+def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, num_actions=11, num_obs=147):
+    """name -> (shape, numpy dtype) of every ha_state_t buffer (Isaac Gym tensor layouts)."""
+    N, D, A, B, P = num_envs, n_dofs, 3 + n_obj, 1 + n_links + 1 + n_obj, num_initial_poses
+    f, i64, u8, i32, u32 = np.float32, np.int64, np.uint8, np.int32, np.uint32
+    return {
+        "root_state": ((N * A, 13), f), "rigid_body_state": ((N * B, 13), f), "dof_state": ((N * D, 2), f),
+        "net_contact_force": ((N * B, 3), f), "sim_targets": ((N, D), f), "dof_position_targets": ((N, D), f),
+        "actions": ((N, num_actions), f), "obs": ((N, num_obs), f), "teacher_obs": ((N, num_obs), f),
+        "rew": ((N,), f), "reset_buf": ((N,), i64), "progress_buf": ((N,), i64), "timeout_buf": ((N,), u8),
+        "goal_reached_before": ((N,), u8), "goal_pos": ((N, 3), f), "target_object_index": ((N,), i64),
+        "object_configuration_indices": ((N,), i64), "object_indices": ((N, n_obj), i64),
+        "object_pos_initial": ((N, P, n_obj, 3), f), "object_quat_initial": ((N, P, n_obj, 4), f),
+        "ur5_target": ((N, 6), f), "servo": ((N, 5), f), "smoothed": ((N, 5), f), "obs_cache": ((N, n_obj, 7), f),
+        "reset_draws": ((N, 5), f), "episode": ((N,), u32), "stats": ((STAT_SIZE,), i32), "term_sums": ((4,), f),
+        "flags": ((4,), i32), "collision_enabled": ((N, n_obj), u8),
+    }
+
+
+class HaState(C.Structure):
+    _fields_ = [(n, P) for n in STATE_FIELDS]
+
+
+def load_scene(path=ASSET):
+    with open(path) as f:
+        return json.load(f)
+
+
+# links whose hulls may touch the table (the base-mounted shoulder/upper arm sit on it and would
+# only produce contacts against a fixed joint; SURVEY.md §8 a16 robot filter 0b1 vs table 0)
+NO_TABLE_CONTACT = {"shoulder_link", "upper_arm_link"}
+
+
+def build_model(scene, pool_names=None):
+    m = HaModel()
+    rob = scene["robot"]
+    links, dofs = rob["links"], rob["dofs"]
+    assert len(links) <= MAX_LINKS and len(dofs) <= MAX_DOFS
+    m.n_links, m.n_dofs = len(links), len(dofs)
+    for i, l in enumerate(links):
+        m.link_parent[i] = l["parent"]
+        m.link_dof[i] = l["dof"]
+        m.link_table_collide[i] = 0 if l["name"] in NO_TABLE_CONTACT else 1
+        m.link_origin_pos[i][:] = l["origin_pos"]
+        m.link_origin_quat[i][:] = l["origin_quat"]
+        m.link_axis[i][:] = l["axis"]
+        m.link_mass[i] = l["mass"]
+        m.link_com[i][:] = l["com"]
+        m.link_inertia[i][:] = l["inertia"]
+    for d, rec in enumerate(dofs):
+        m.dof_lower[d], m.dof_upper[d], m.dof_effort[d] = rec["lower"], rec["upper"], rec["effort"]
+        m.dof_kp[d], m.dof_kd[d] = rec["kp"], rec["kd"]
+    m.base_pos[:] = rob["base_pos"]
+    m.base_quat[:] = rob["base_quat"]
+    objects = scene["objects"]
+    if pool_names is not None:
+        byname = {o["name"]: o for o in objects}
+        objects = [byname[n] for n in pool_names]
+    hulls = [(h, h["index"]) for h in scene["link_hulls"]] + [(o["hull"], -1) for o in objects] + \
+            [(scene["table"]["hull"], -1)]
+    assert len(hulls) <= MAX_HULLS
+    vs, ps = 0, 0
+    verts = np.ctypeslib.as_array(m.verts)
+    planes = np.ctypeslib.as_array(m.planes)
+    for k, (h, link) in enumerate(hulls):
+        v = np.asarray(h["verts"], np.float32)
+        p = np.asarray(h["planes"], np.float32)
+        assert len(v) <= 64, "hull vertex count must fit one wavefront"
+        m.hull_link[k] = link
+        m.hull_vert_start[k], m.hull_nverts[k] = vs, len(v)
+        m.hull_plane_start[k], m.hull_nplanes[k] = ps, len(p)
+        m.hull_center[k][:] = h["center"]
+        m.hull_radius[k] = h["radius"]
+        verts[vs:vs + len(v), :3] = v
+        planes[ps:ps + len(p)] = p
+        vs += len(v)
+        ps += len(p)
+    assert vs <= MAX_VERTS and ps <= MAX_PLANES
+    m.n_link_hulls = len(scene["link_hulls"])
+    m.n_pool = len(objects)
+    m.n_hulls = len(hulls)
+    for i, o in enumerate(objects):
+        m.pool_hull[i] = m.n_link_hulls + i
+        m.pool_mass[i] = o["mass"]
+        m.pool_com[i][:] = o["com"]
+        m.pool_inertia[i][:] = o["inertia"]
+        m.pool_bbox_pos[i][:] = o["bbox_from_origin_pos"]
+        m.pool_bbox_quat[i][:] = o["bbox_from_origin_quat"]
+        m.pool_bbox_ext[i][:] = o["bbox_extents"]
+    m.table_hull = len(hulls) - 1
+    m.table_pos[:] = scene["table"]["pos"]
+    m.table_quat[:] = scene["table"]["quat"]
+    # derived topology for the level-synchronous wave kernels
+    level = []
+    for i, l in enumerate(links):
+        assert l["parent"] < i, "links must be in depth-first (parent-first) order"
+        level.append(0 if l["parent"] < 0 else level[l["parent"]] + 1)
+        m.link_level[i] = level[-1]
+        if l["dof"] >= 0:
+            m.dof_link[l["dof"]] = i
+    m.max_level = max(level)
+    pairs = []
+    for d in range(len(dofs)):
+        j = m.dof_link[d]
+        while j >= 0:
+            if links[j]["dof"] >= 0:
+                pairs.append((d, links[j]["dof"]))
+            j = links[j]["parent"]
+    assert len(pairs) <= MAX_MPAIRS
+    m.n_mpairs = len(pairs)
+    for k, (d, e) in enumerate(pairs):
+        m.mpair[k][0], m.mpair[k][1] = d, e
+    return m
+
+
+# ----------------------------------------------------------------------------- splines (host)
+SPLINE_ORDER = ["thumb_proximal", "thumb_distal", "index_proximal", "index_distal", "middle_proximal",
+                "middle_distal", "ring_proximal", "ring_distal"]
+SPLINE_KNOTS = {   # ur5sih.py:442-455
+    "thumb_proximal": ([-1850, -1175, -975, -600, -225], [-1.51, -1.31, -1.175, -0.6, 0.]),
+    "thumb_distal": ([-1318.125, -906.25, -200], [-1.235, -0.855, 0.]),
+    "index_proximal": ([-1250, -250, 150, 350, 540, 730, 1085, 1400], [-1.53, -1.4425, -1.315, -1.25, -1.18, -1.15, -0.6, 0.]),
+    "index_distal": ([-408.606, 793.515, 1400], [-1.665, -0.735, 0]),
+    "middle_proximal": ([-500, 500, 1350, 1625, 1700, 1980, 2240], [-1.571, -1.445, -1.055, -0.91, -0.9, -0.48, 0.]),
+    "middle_distal": ([442.6, 1147, 1750.6, 2240], [-1.65, -1.125, -0.62, 0.]),
+    "ring_proximal": ([-1050, -500, -250, 0, 370, 500, 700, 940], [-1.571, -1.45, -1.35, -1.225, -0.95, -0.9, -0.533, 0.]),
+    "ring_distal": ([-719, 408.8, 686.8, 939.2], [-1.64, -0.69, -0.425, 0.]),
+}
+
+
+def natural_cubic_spline_table(knots, values):
+    """Coefficients of the natural cubic spline through (knots, values), in float32 and in the
+    operation order of torchcubicspline.natural_cubic_spline_coeffs (tridiagonal knot-derivative
+    system, Thomas algorithm).  Returns (5, pieces): piece start, a, b, two_c, three_d."""
+    F = np.float32
+    t = np.asarray(knots, F)
+    x = np.asarray(values, F)
+    n = len(t)
+    dt = t[1:] - t[:-1]
+    r = (F(1) / dt).astype(F)
+    r2 = (r ** 2).astype(F)
+    three = F(3) * (x[1:] - x[:-1])
+    six = F(2) * three
+    scaled = three * r2
+    diag = np.empty(n, F)
+    diag[:-1] = r
+    diag[-1] = 0
+    diag[1:] += r
+    diag *= F(2)
+    rhs = np.empty(n, F)
+    rhs[:-1] = scaled
+    rhs[-1] = 0
+    rhs[1:] += scaled
+    nb, nd, out = np.empty(n, F), np.empty(n, F), np.empty(n, F)
+    nb[0], nd[0] = rhs[0], diag[0]
+    for i in range(1, n):
+        w = r[i - 1] / nd[i - 1]
+        nd[i] = diag[i] - w * r[i - 1]
+        nb[i] = rhs[i] - w * nb[i - 1]
+    out[n - 1] = nb[n - 1] / nd[n - 1]
+    for i in range(n - 2, -1, -1):
+        out[i] = (nb[i] - r[i] * out[i + 1]) / nd[i]
+    two_c = (six * r - F(4) * out[:-1] - F(2) * out[1:]) * r
+    three_d = (-six * r + F(3) * (out[:-1] + out[1:])) * r2
+    return np.stack([t[:-1], x[:-1], out[:-1], two_c, three_d]).astype(F)
+
+
+DEFAULT_TASK = dict(
+    dt=0.016666667, substeps=2, control_freq_inv=3, solver_iters=8, gravity=(0.0, 0.0, -9.81),
+    friction=1.0, contact_margin=0.01, baumgarte=0.2, max_depen_vel=1.0, object_ang_damping=0.5,
+    joint_limit_margin=0.02, n_objects=3, num_initial_poses=1, max_episode_length=200,
+    sih_alpha=0.8, reward_reaching=1.0, reward_lifting=5.0, reward_goal=50.0, reward_success=50.0,
+    lifting_threshold=0.05, goal_threshold=0.05, goal_pos=(0.28, 0.58, 0.8), goal_noise=(0.15, 0.15, 0.1),
+    drop_pos=(0.28, 0.58, 1.5), drop_noise=(0.1, 0.1, 0.0), drop_num_steps=100,
+    reset_pose=(0.6985, -1.4106, 1.2932, 0.1174, 0.6983, 1.5708, 0., 0., 0., 0., 0., 0., 0., 0., -1.571, 0., 0.),
+    bringup_pose=(0., -1.571, 0., 0., 0., 0., 0., 0., 0., 0., 0., 0., 0., 0., -1.571, 0., 0.),
+    servo_lower=(0, -2000, -1250, -400, -1350), servo_upper=(2650, 250, 1450, 2300, 1000),
+    proximal_coef=(-625.0, -582.61, -600.0, -488.0), seed=42,
+)
+
+
+def build_params(cfg=None):
+    c = dict(DEFAULT_TASK)
+    if cfg:
+        c.update(cfg)
+    p = HaParams()
+    for k in ["dt", "substeps", "control_freq_inv", "solver_iters", "friction", "contact_margin", "baumgarte",
+              "max_depen_vel", "object_ang_damping", "joint_limit_margin", "n_objects", "num_initial_poses",
+              "max_episode_length", "sih_alpha", "reward_reaching", "reward_lifting", "reward_goal",
+              "reward_success", "lifting_threshold", "goal_threshold", "seed"]:
+        setattr(p, k, c[k])
+    p.gravity[:] = c["gravity"]
+    p.action_dt = c["dt"]                      # VecTask.dt = sim_params.dt (vec_task.py:267)
+    p.goal_pos[:] = c["goal_pos"]
+    p.goal_noise[:] = c["goal_noise"]
+    p.reset_pose[:len(c["reset_pose"])] = c["reset_pose"]
+    p.servo_lower[:] = c["servo_lower"]
+    p.servo_upper[:] = c["servo_upper"]
+    p.proximal_coef[:] = c["proximal_coef"]
+    sp = np.ctypeslib.as_array(p.spline)
+    for i, name in enumerate(SPLINE_ORDER):
+        tab = natural_cubic_spline_table(*SPLINE_KNOTS[name])
+        p.spline_pieces[i] = tab.shape[1]
+        sp[i, :, :tab.shape[1]] = tab
+    p.thumb_opposition_gain = np.float32(-1.571 / 2675)
+    return p, c

@@ -1,0 +1,61 @@
+"""Multi-GPU: envs are sharded one process per GPU; the only cross-rank traffic is the episode-stat
+reduction at log intervals. The reference logs each rank's stats separately
+(rlgames_utils.py:183-219); reducing the COUNTS before the EWMA update (multi_object_manipulation.py:
+324-351) gives every rank the global success rate, identical to a single-GPU run over all envs.
+"""
+import torch
+
+
+def world():
+    import torch.distributed as dist
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def reduce_episode_stats(env):
+    """All-reduce (sum) the pending per-step device counters of `env` across ranks, in place.
+
+    Payload: pending_steps x (2 + 2*pool) int32 + pending_steps x 4 float32 (a few KB); one collective
+    per log interval, launched on the current stream (RCCL over xGMI with the nccl backend, gloo on CPU).
+    """
+    if world() == 1:
+        return
+    import torch.distributed as dist
+    k = env._stat_pending
+    if k == 0:
+        return
+    R = env.sim.stats_ring
+    slots = torch.tensor([(env._stat_folded + s) % R for s in range(k)], device=env.sim.t["stats"].device)
+    stats = env.sim.t["stats"].index_select(0, slots)
+    terms = env.sim.t["term_sums"].index_select(0, slots)
+    dist.all_reduce(stats)
+    dist.all_reduce(terms)
+    env.sim.t["stats"].index_copy_(0, slots, stats)
+    env.sim.t["term_sums"].index_copy_(0, slots, terms)
+    env.stat_scale = world()          # EWMA alpha uses the GLOBAL number of envs
+
+
+def fold_counts(stats, terms, num_envs, ewma, obj_ewma, n_objects):
+    """Host EWMA update from (already reduced) per-step counters; returns log dict entries.
+
+    stats: (steps, 2 + 2*pool) ints, terms: (steps, 4) floats. Mirrors _update_success_rate."""
+    import numpy as np
+    log = {}
+    for st, ts in zip(stats, terms):
+        for j, name in enumerate(["reaching", "lifting", "goal", "success"]):
+            log["reward_terms/" + name] = float(np.float32(ts[j]) / np.float32(num_envs))
+        r, s = int(st[0]), int(st[1])
+        if r > 0:
+            alpha = np.float32(0.2) * (np.float32(r) / np.float32(num_envs))
+            ewma = float(alpha * (np.float32(s) / np.float32(r)) + (np.float32(1) - alpha) * np.float32(ewma))
+            log["success_rate_ewma/overall"] = ewma
+        for i in range(n_objects):
+            ri, si = int(st[2 + 2 * i]), int(st[3 + 2 * i])
+            if ri > 0:
+                alpha = np.float32(0.2) * (np.float32(ri) / np.float32(num_envs)) * np.float32(n_objects)
+                obj_ewma[i] = float(alpha * (np.float32(si) / np.float32(ri)) + (np.float32(1) - alpha) * np.float32(obj_ewma[i]))
+                log[i] = obj_ewma[i]
+    return log, ewma, obj_ewma
+
+
+__all__ = ["reduce_episode_stats", "fold_counts", "world"]
+_ = torch

@@ -1,0 +1,143 @@
+"""Gym-style simulation object over the HIP library: the lower surface the reference task code uses.
+
+``HandArmSim`` owns one ``ha_handle`` and every device tensor (torch, on ``device``). Method names and
+semantics follow the Isaac Gym tensor API the hand_arm task calls:
+
+  acquire_actor_root_state_tensor / acquire_rigid_body_state_tensor / acquire_dof_state_tensor /
+  acquire_net_contact_force_tensor   -> the live state tensors (zero-copy: they ARE the sim state)
+  refresh_*                          -> no-ops (the kernels write the tensors in place)
+  simulate(n)                        -> n gym.simulate() calls in ONE kernel launch
+  set_actor_root_state_tensor_indexed / set_dof_state_tensor_indexed /
+  set_dof_position_target_tensor(_indexed)  -> copy-in for the listed global actor indices (int32)
+
+Difference to Isaac Gym worth knowing: because the acquired tensors are the simulation state,
+writes into them take effect even without a set_*_indexed call (the reference always calls it).
+"""
+import ctypes as C
+
+import torch
+
+from . import _lib
+from . import model as HM
+
+TORCH_DTYPE = {"float32": torch.float32, "int64": torch.int64, "uint8": torch.uint8, "int32": torch.int32,
+               "uint32": torch.int32}
+
+
+class HandArmSim:
+    def __init__(self, num_envs, device="cuda:0", task_cfg=None, scene=None, pool_names=None, stats_ring=64):
+        if not str(device).startswith("cuda"):
+            raise _lib.HandArmError("libhandarm_hip runs on a HIP device only (device must be 'cuda:N')")
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        self.scene = scene if scene is not None else HM.load_scene()
+        self.model = HM.build_model(self.scene, pool_names)
+        self.params, self.cfg = HM.build_params(task_cfg)
+        self.num_envs = num_envs
+        self.n_obj = self.params.n_objects
+        self.num_dofs = self.model.n_dofs
+        self.num_links = self.model.n_links
+        self.num_actors = 3 + self.n_obj
+        self.num_bodies = 1 + self.num_links + 1 + self.n_obj
+        self.stats_ring = stats_ring
+        spec = HM.state_spec(num_envs, n_links=self.num_links, n_dofs=self.num_dofs, n_obj=self.n_obj,
+                             num_initial_poses=self.params.num_initial_poses)
+        spec["stats"] = ((stats_ring, HM.STAT_SIZE), spec["stats"][1])
+        spec["term_sums"] = ((stats_ring, 4), spec["term_sums"][1])
+        with torch.cuda.device(self.device):
+            self.t = {k: torch.zeros(shape, dtype=TORCH_DTYPE[dt.__name__], device=self.device)
+                      for k, (shape, dt) in spec.items()}
+        self.t["root_state"].view(num_envs, self.num_actors, 13)[..., 6] = 1.0
+        self.t["collision_enabled"].fill_(1)
+        h = C.c_void_p()
+        _lib.check(self.lib.ha_create(C.byref(self.model), C.byref(self.params), num_envs, C.byref(h)), "ha_create")
+        self.h = h
+        self.state = HM.HaState()
+        for k in HM.STATE_FIELDS:
+            setattr(self.state, k, self.t[k].data_ptr())
+        _lib.check(self.lib.ha_bind_state(self.h, C.byref(self.state)), "ha_bind_state")
+        _lib.check(self.lib.ha_set_stats_ring(self.h, stats_ring), "ha_set_stats_ring")
+
+    # -------------------------------------------------------------- helpers
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                self.lib.ha_destroy(self.h)
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------- Isaac Gym tensor API
+    def acquire_actor_root_state_tensor(self):
+        return self.t["root_state"]
+
+    def acquire_rigid_body_state_tensor(self):
+        return self.t["rigid_body_state"]
+
+    def acquire_dof_state_tensor(self):
+        return self.t["dof_state"]
+
+    def acquire_net_contact_force_tensor(self):
+        return self.t["net_contact_force"]
+
+    def refresh_actor_root_state_tensor(self):
+        _lib.check(self.lib.ha_refresh(self.h, self._stream()), "ha_refresh")
+
+    refresh_rigid_body_state_tensor = refresh_actor_root_state_tensor
+    refresh_dof_state_tensor = refresh_actor_root_state_tensor
+    refresh_net_contact_force_tensor = refresh_actor_root_state_tensor
+
+    def simulate(self, n_calls=1, flags=0):
+        _lib.check(self.lib.ha_simulate(self.h, n_calls, flags, self._stream()), "ha_simulate")
+
+    def fetch_results(self, wait=True):
+        if wait:
+            torch.cuda.current_stream(self.device).synchronize()
+
+    def _indexed(self, fn, data, idx, name):
+        idx = idx.to(device=self.device, dtype=torch.int32).contiguous()
+        data = data.contiguous()
+        _lib.check(fn(self.h, C.c_void_p(data.data_ptr()), C.c_void_p(idx.data_ptr()), idx.numel(), self._stream()),
+                   name)
+
+    def set_actor_root_state_tensor_indexed(self, root_state, actor_indices):
+        self._indexed(self.lib.ha_set_actor_root_state_indexed, root_state, actor_indices, "set_actor_root_state")
+
+    def set_dof_state_tensor_indexed(self, dof_state, actor_indices):
+        self._indexed(self.lib.ha_set_dof_state_indexed, dof_state, actor_indices, "set_dof_state")
+
+    def set_dof_position_target_tensor_indexed(self, targets, actor_indices):
+        self._indexed(self.lib.ha_set_dof_position_target_indexed, targets, actor_indices, "set_dof_target")
+
+    def set_dof_position_target_tensor(self, targets):
+        targets = targets.contiguous()
+        _lib.check(self.lib.ha_set_dof_position_target(self.h, C.c_void_p(targets.data_ptr()), self._stream()),
+                   "set_dof_position_target")
+
+    def set_object_collisions(self, enabled):
+        """enabled: (N, n_obj) bool/uint8 - replaces the per-env shape-filter loop (multi_object.py:693-703)."""
+        self.t["collision_enabled"].copy_(enabled.to(torch.uint8))
+
+    # -------------------------------------------------------------- fused task entry points
+    def task_step(self, flags=0):
+        _lib.check(self.lib.ha_task_step(self.h, flags, self._stream()), "ha_task_step")
+
+    def task_observe(self, flags=0):
+        _lib.check(self.lib.ha_task_observe(self.h, flags, self._stream()), "ha_task_observe")
+
+    def task_reset(self, flags=0):
+        _lib.check(self.lib.ha_task_reset(self.h, flags, self._stream()), "ha_task_reset")
+
+    def last_kernel_ms(self):
+        return float(self.lib.ha_last_kernel_ms(self.h))
+
+    def enable_kernel_timing(self, max_launches):
+        _lib.check(self.lib.ha_enable_kernel_timing(self.h, max_launches), "ha_enable_kernel_timing")
+
+    def kernel_times_ms(self, max_n=1 << 16):
+        buf = (C.c_float * max_n)()
+        n = C.c_int32()
+        _lib.check(self.lib.ha_kernel_times(self.h, buf, max_n, C.byref(n)), "ha_kernel_times")
+        return list(buf[:n.value])

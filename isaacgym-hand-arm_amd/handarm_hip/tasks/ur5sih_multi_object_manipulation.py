@@ -1,0 +1,356 @@
+"""Ur5SihMultiObjectManipulation with the IsaacGymEnvs VecTask surface, backed by libhandarm_hip.
+
+Drop-in for tasks/hand_arm/task/multi_object_manipulation.py:19 (registered as
+"Ur5SihMultiObjectManipulation" in tasks/__init__.py:122). The upper surface is the one
+rl_games' RLGPUEnv reads (utils/rlgames_utils.py:252-310): step / reset / reset_done / reset_idx,
+observation/action spaces, observation_keys, teacher observation space, log_data, extras.
+
+Everything per step runs in ONE fused kernel (ha_task_step): controllers -> [reset + its extra
+simulate] -> control_freq_inv x substeps physics -> refresh -> observables -> reward -> done.
+There are no host syncs on the step path; reward-term means and success EWMAs (the reference's
+.item() logging, multi_object_manipulation.py:311-351) are accumulated on the device and folded into
+``log_data`` lazily.
+"""
+import math
+import random
+
+import numpy as np
+import torch
+
+from .. import model as HM
+from ..sim import HandArmSim
+from ..torch_utils import randomize_rotation, torch_rand_float
+
+OBSERVATIONS = ["ur5_joint_pos", "ur5_flange_pose", "sih_fingertip_pos", "sih_fingertip_quat", "sih_fingertip_linvel",
+                "dof_position_targets", "object_pos", "object_bounding_box", "target_object_bounding_box",
+                "sih_fingertip_to_target_object_pos", "target_object_to_goal_pos"]
+OBS_SIZES = [6, 7, 15, 20, 15, 17, 9, 30, 10, 15, 3]
+ACTIONS = ["ur5_relative_joint_pos", "sih_smoothed_relative_servo_pos"]
+REWARD_TERMS = ["reaching", "lifting", "goal", "success"]
+DEFAULT_OBJECTS = ["015_peach", "005_tomato_soup_can", "006_mustard_bottle"]   # Ur5SihMultiObject.yaml:11
+
+
+class Box:
+    """Minimal gym.spaces.Box (openai-gym is not a dependency here)."""
+
+    def __init__(self, low, high):
+        self.low = np.asarray(low, dtype=np.float32)
+        self.high = np.asarray(high, dtype=np.float32)
+        self.shape = self.low.shape
+        self.dtype = np.float32
+
+    def __repr__(self):
+        return f"Box({self.shape})"
+
+
+def _get(cfg, path, default):
+    cur = cfg
+    for k in path.split("."):
+        if not isinstance(cur, dict) or k not in cur:
+            return default
+        cur = cur[k]
+    return cur
+
+
+class Ur5SihMultiObjectManipulation:
+    def __init__(self, cfg, rl_device="cuda:0", sim_device="cuda:0", graphics_device_id=-1, headless=True,
+                 virtual_screen_capture=False, force_render=False):
+        self.cfg = cfg
+        self.rl_device = rl_device
+        self.device = sim_device
+        self.headless = headless
+        env = cfg.get("env", {})
+        self.num_environments = int(env.get("numEnvs", 16384))
+        self.num_agents = 1
+        self.control_freq_inv = int(env.get("controlFrequencyInv", 3))
+        self.clip_obs = float(env.get("clipObservations", math.inf))
+        self.clip_actions = float(env.get("clipActions", math.inf))
+        self.max_episode_length = int(_get(cfg, "rl.reset.max_episode_length", 200))
+        objects = _get(cfg, "objects.dataset.ycb", DEFAULT_OBJECTS)
+        self.num_objects = int(_get(cfg, "objects.num_objects", 3))
+        self.num_initial_poses = int(_get(cfg, "objects.drop.num_initial_poses", 1))
+        task_cfg = dict(control_freq_inv=self.control_freq_inv, max_episode_length=self.max_episode_length,
+                        n_objects=self.num_objects, num_initial_poses=self.num_initial_poses,
+                        seed=int(cfg.get("seed", 42)))
+        rew = _get(cfg, "rl.reward", None)
+        if rew:
+            for k in REWARD_TERMS:
+                task_cfg["reward_" + k] = float(rew.get(k, 0.0))
+        self.sim = HandArmSim(self.num_environments, sim_device, task_cfg=task_cfg, pool_names=objects)
+        self.task_cfg = self.sim.cfg
+        self.objects = objects
+        t = self.sim.t
+        N, A, B, D = self.num_envs, self.sim.num_actors, self.sim.num_bodies, self.sim.num_dofs
+        self.num_actors, self.num_bodies, self.num_dofs = A, B, D
+        # gym tensors and the reference's views (observable_vec_task.py:123-155)
+        self.root_state = t["root_state"]
+        self.body_state = t["rigid_body_state"]
+        self.dof_state = t["dof_state"]
+        self.contact_force = t["net_contact_force"].view(N, B, 3)
+        self.root_pos = self.root_state.view(N, A, 13)[..., 0:3]
+        self.root_quat = self.root_state.view(N, A, 13)[..., 3:7]
+        self.root_linvel = self.root_state.view(N, A, 13)[..., 7:10]
+        self.root_angvel = self.root_state.view(N, A, 13)[..., 10:13]
+        self.body_pos = self.body_state.view(N, B, 13)[..., 0:3]
+        self.body_quat = self.body_state.view(N, B, 13)[..., 3:7]
+        self.body_linvel = self.body_state.view(N, B, 13)[..., 7:10]
+        self.body_angvel = self.body_state.view(N, B, 13)[..., 10:13]
+        self.dof_pos = self.dof_state.view(N, D, 2)[..., 0]
+        self.dof_vel = self.dof_state.view(N, D, 2)[..., 1]
+        # VecTask buffers (vec_task.py:329-354)
+        self.obs_buf = t["obs"]
+        self.teacher_obs_buf = t["teacher_obs"]
+        self.rew_buf = t["rew"]
+        self.reset_buf = t["reset_buf"]
+        self.progress_buf = t["progress_buf"]
+        self.timeout_buf = t["timeout_buf"]
+        self.goal_pos = t["goal_pos"]
+        self.goal_reached_before = t["goal_reached_before"]
+        self.target_object_index = t["target_object_index"]
+        self.object_configuration_indices = t["object_configuration_indices"]
+        self.dof_position_targets = t["dof_position_targets"]
+        self.actions_buf = t["actions"]
+        self.reset_buf.fill_(1)
+        self.states_buf = torch.zeros((N, 0), device=self.device)
+        self.num_observations = sum(OBS_SIZES)
+        self.num_teacher_observations = self.num_observations
+        self.num_states = 0
+        self.num_actions = 11
+        self.obs_space = Box(np.full(self.num_observations, -np.inf), np.full(self.num_observations, np.inf))
+        self.teacher_obs_space = self.obs_space
+        self.state_space = Box(np.zeros(0), np.zeros(0))
+        self.act_space = Box(-np.ones(self.num_actions), np.ones(self.num_actions))
+        start = np.cumsum([0] + OBS_SIZES)
+        self.observations_start_end = {n: (int(start[i]), int(start[i + 1])) for i, n in enumerate(OBSERVATIONS)}
+        self.teacher_observations_start_end = dict(self.observations_start_end)
+        self.extras = {}
+        self.obs_dict = {}
+        self._log_data = {}
+        self.control_steps = 0
+        self.total_train_env_frames = 0
+        self.dt = self.sim.params.dt
+        # actor layout: goal 0, robot 1, table 2, objects 3.. (multi_object.py:562-663)
+        ar = torch.arange(N, dtype=torch.int32, device=self.device)
+        self.goal_actor_indices = ar * A
+        self.ur5sih_actor_indices = ar * A + 1
+        self.object_actor_indices = ar[:, None] * A + 3 + torch.arange(self.num_objects, dtype=torch.int32,
+                                                                          device=self.device)[None]
+        self.object_actor_env_indices = [3 + i for i in range(self.num_objects)]
+        # per-env object subset: random.sample of the pool (multi_object.py:569)
+        pool = list(range(len(objects)))
+        idx = [random.sample(pool, self.num_objects) for _ in range(N)]
+        t["object_indices"].copy_(torch.tensor(idx, dtype=torch.int64))
+        self.object_indices = t["object_indices"]
+        # initial actor poses (create_actor start poses)
+        rs = self.root_state.view(N, A, 13)
+        rs[:, 1, 0:3] = torch.tensor(self.sim.model.base_pos[:], device=self.device)
+        rs[:, 2, 0:3] = torch.tensor(self.sim.model.table_pos[:], device=self.device)
+        rs[:, 3:, 0:3] = torch.tensor([0.0, 0.0, 0.5], device=self.device)   # ObjectAsset.start_pose
+        self.dof_pos[:] = torch.tensor(self.sim.params.reset_pose[:D], device=self.device)
+        t["sim_targets"].copy_(self.dof_pos)
+        self._sync_obs_cache()      # observables' post_step in ConfigurableVecTask.__init__
+        self.objects_dropped = False
+        self._stat_pending = 0
+        self._stat_folded = 0
+        self._success_rate_ewma = 0.0
+        self._object_ewma = [0.0] * len(objects)
+        self.total_num_resets = 0
+        self.total_num_successes = 0
+        self.sim_flags = 0
+
+    # ------------------------------------------------------------------ VecTask properties
+    @property
+    def num_envs(self):
+        return self.num_environments
+
+    @property
+    def num_obs(self):
+        return self.num_observations
+
+    @property
+    def num_acts(self):
+        return self.num_actions
+
+    @property
+    def num_teacher_obs(self):
+        return self.num_teacher_observations
+
+    @property
+    def observation_space(self):
+        return self.obs_space
+
+    def teacher_observation_space(self):
+        return self.teacher_obs_space
+
+    @property
+    def action_space(self):
+        return self.act_space
+
+    @property
+    def observation_start_end(self):
+        # reference quirk (vec_task.py:176 vs observable_vec_task.py:24): always None
+        return getattr(self, "_observation_start_end", None)
+
+    @property
+    def teacher_observation_start_end(self):
+        return getattr(self, "_teacher_observation_start_end", None)
+
+    @property
+    def observation_keys(self):
+        return ["obs"]
+
+    def get_number_of_agents(self):
+        return self.num_agents
+
+    def set_train_info(self, env_frames, *args, **kwargs):
+        self.total_train_env_frames = env_frames
+
+    def get_env_state(self):
+        return None
+
+    def set_env_state(self, env_state):
+        pass
+
+    def zero_actions(self):
+        return torch.zeros((self.num_envs, self.num_actions), dtype=torch.float32, device=self.rl_device)
+
+    # ------------------------------------------------------------------ internals
+    def _sync_obs_cache(self):
+        n, a = self.num_envs, self.num_actors
+        self.sim.t["obs_cache"].copy_(self.root_state.view(n, a, 13)[:, 3:, 0:7])
+
+    def _random_object_pos(self, n, key):
+        c = self.task_cfg
+        pos = torch.tensor(c[key + "_pos"], device=self.device).unsqueeze(0).repeat(n, 1)
+        noise = 2 * (torch.rand((n, 3), dtype=torch.float32, device=self.device) - 0.5)
+        return pos + noise * torch.tensor(c[key + "_noise"], device=self.device)
+
+    def _reset_ur5sih(self, pose):
+        self.dof_pos[:] = torch.tensor(pose, device=self.device)
+        self.dof_vel[:] = 0.0
+        self.sim.t["sim_targets"].copy_(self.dof_pos)
+        self.dof_position_targets.copy_(self.dof_pos)
+
+    def _drop_initialisation(self):
+        """First reset: find initial object poses by dropping (multi_object_manipulation.py:36-61, 93-173)."""
+        N, A, n_obj = self.num_envs, self.num_actors, self.num_objects
+        P = self.num_initial_poses
+        rs = self.root_state.view(N, A, 13)
+        self._reset_ur5sih(self.task_cfg["bringup_pose"])
+        bin_lo = torch.tensor([0.03, 0.28, 0.5], device=self.device)     # no_bin extent + bin.pos (multi_object.py:423)
+        bin_hi = torch.tensor([0.53, 0.78, 0.7], device=self.device)
+        pos_init = self.sim.t["object_pos_initial"]
+        quat_init = self.sim.t["object_quat_initial"]
+        for p in range(P):
+            enabled = torch.zeros((N, n_obj), dtype=torch.uint8, device=self.device)
+            self.sim.set_object_collisions(enabled)
+            rs[:, 3:, 0:3] = torch.tensor([1.1, 0.0, 0.5], device=self.device)        # _init_object_poses
+            rs[:, 3:, 7:13] = 0.0
+            self.sim.simulate(1)
+            in_bin = torch.zeros((N, n_obj), dtype=torch.bool, device=self.device)
+            while not bool(in_bin.all()):
+                for i in range(n_obj):
+                    enabled[:, i] = 1
+                    self.sim.set_object_collisions(enabled)
+                    env_ids = (~in_bin[:, i]).nonzero(as_tuple=False).squeeze(-1)
+                    if len(env_ids) > 0:
+                        rs[env_ids, 3 + i, 0:3] = self._random_object_pos(len(env_ids), "drop")
+                        rf = torch_rand_float(-1.0, 1.0, (len(env_ids), 2), device=self.device)
+                        rs[env_ids, 3 + i, 3:7] = randomize_rotation(rf[:, 0], rf[:, 1])
+                        rs[env_ids, 3 + i, 7:13] = 0.0
+                        self.sim.simulate(self.task_cfg["drop_num_steps"])
+                obj_pos = rs[:, 3:, 0:3]
+                in_bin = ((obj_pos >= bin_lo) & (obj_pos <= bin_hi)).all(-1)
+            for _ in range(600):                                                    # settle
+                self.sim.simulate(1)
+                if bool((rs[:, 3:, 7:10].norm(dim=2).max(dim=1).values < 0.01).all()):
+                    break
+            pos_init[:, p] = rs[:, 3:, 0:3]
+            quat_init[:, p] = rs[:, 3:, 3:7]
+            self._sync_obs_cache()
+        self.objects_dropped = True
+
+    def _fold_stats(self):
+        """Fold the device-side per-step counters into log_data (reference :311-351 semantics)."""
+        k = self._stat_pending
+        if k == 0:
+            return
+        R = self.sim.stats_ring
+        slots = [(self._stat_folded + s) % R for s in range(k)]
+        stats = self.sim.t["stats"].cpu().numpy()[slots]
+        terms = self.sim.t["term_sums"].cpu().numpy()[slots]
+        self._stat_pending = 0
+        self._stat_folded += k
+        N = self.num_envs * getattr(self, "stat_scale", 1)   # global env count after a cross-rank reduce
+        n_obj = len(self.objects)
+        for s in range(k):
+            st, ts = stats[s], terms[s]
+            for j, name in enumerate(REWARD_TERMS):
+                self._log_data["reward_terms/" + name] = float(np.float32(ts[j]) / np.float32(N))
+            num_resets, num_succ = int(st[0]), int(st[1])
+            if num_resets > 0:
+                rate = np.float32(num_succ) / np.float32(num_resets)
+                alpha = np.float32(0.2) * (np.float32(num_resets) / np.float32(N))
+                self._success_rate_ewma = float(alpha * rate + (np.float32(1) - alpha) * np.float32(self._success_rate_ewma))
+                self._log_data["success_rate_ewma/overall"] = self._success_rate_ewma
+                self.total_num_resets += num_resets
+                self.total_num_successes += num_succ
+            for i in range(n_obj):
+                r_i, s_i = int(st[2 + 2 * i]), int(st[3 + 2 * i])
+                if r_i > 0:
+                    rate = np.float32(s_i) / np.float32(r_i)
+                    alpha = np.float32(0.2) * (np.float32(r_i) / np.float32(N)) * np.float32(n_obj)
+                    self._object_ewma[i] = float(alpha * rate + (np.float32(1) - alpha) * np.float32(self._object_ewma[i]))
+                    self._log_data["success_rate_ewma/" + self.objects[i]] = self._object_ewma[i]
+        assert R >= k
+
+    @property
+    def log_data(self):
+        """Read (and cleared) by RLGPUAlgoObserver (rlgames_utils.py:212-219); device counters folded in."""
+        self._fold_stats()
+        return self._log_data
+
+    @log_data.setter
+    def log_data(self, value):
+        self._log_data = value
+
+    def log(self, data):
+        self._log_data.update(data)
+
+    # ------------------------------------------------------------------ VecTask API
+    def step(self, actions):
+        if not self.objects_dropped and bool(self.reset_buf.any()):
+            self._drop_initialisation()
+        action_tensor = torch.clamp(actions, -self.clip_actions, self.clip_actions)
+        self.actions_buf.copy_(action_tensor)
+        if self._stat_pending == self.sim.stats_ring:
+            self._fold_stats()
+        self.sim.task_step(self.sim_flags)
+        self._stat_pending += 1
+        self.control_steps += 1
+        self.extras["time_outs"] = self.timeout_buf.to(torch.bool).to(self.rl_device)
+        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        self.obs_dict["teacher"] = {"obs": torch.clamp(self.teacher_obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)}
+        return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras
+
+    def reset(self):
+        """VecTask.reset (vec_task.py:459-474): compute_observations only."""
+        self.sim.task_observe(HM.FLAG_OBS_ONLY)
+        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        self.obs_dict["teacher"] = {"obs": torch.clamp(self.teacher_obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)}
+        return self.obs_dict
+
+    def reset_idx(self, env_ids):
+        """Immediate reset of ALL envs (the reference asserts it, ur5sih.py:617)."""
+        assert len(env_ids) == self.num_envs, "All environments should be reset simultaneously."
+        if not self.objects_dropped:
+            self._drop_initialisation()
+        self.sim.task_reset(self.sim_flags)
+
+    def reset_done(self):
+        done_env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()
+        if len(done_env_ids) > 0:
+            self.reset_idx(done_env_ids)
+        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        return self.obs_dict, done_env_ids
+

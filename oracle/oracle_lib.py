@@ -1,0 +1,77 @@
+"""ORACLE (test infrastructure only): ctypes front-end of oracle/_build/libhandarm_oracle.so.
+
+Operates on host numpy buffers laid out exactly like the device tensors (handarm_hip.model.state_spec).
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from handarm_hip import model as HM
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "libhandarm_oracle.so")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def load():
+    build()   # make is a no-op when the library is up to date
+    lib = C.CDLL(LIB)
+    lib.hao_create.restype = C.c_void_p
+    lib.hao_create.argtypes = [C.POINTER(HM.HaModel), C.POINTER(HM.HaParams), C.c_int]
+    lib.hao_destroy.argtypes = [C.c_void_p]
+    lib.hao_simulate.argtypes = [C.c_void_p, C.POINTER(HM.HaState), C.c_int, C.c_int, C.c_int]
+    lib.hao_controller.argtypes = [C.c_void_p, C.POINTER(HM.HaState), C.c_int]
+    lib.hao_struct_sizes.argtypes = [C.POINTER(C.c_int32)] * 3
+    return lib
+
+
+class HostState:
+    """numpy buffers for every ha_state_t field."""
+
+    def __init__(self, num_envs, n_obj=3, num_initial_poses=1):
+        self.spec = HM.state_spec(num_envs, n_obj=n_obj, num_initial_poses=num_initial_poses)
+        self.arrays = {k: np.zeros(shape, dtype) for k, (shape, dtype) in self.spec.items()}
+        self.num_envs = num_envs
+
+    def __getitem__(self, k):
+        return self.arrays[k]
+
+    def ctypes(self):
+        s = HM.HaState()
+        for k in HM.STATE_FIELDS:
+            setattr(s, k, self.arrays[k].ctypes.data)
+        return s
+
+    def copy(self):
+        o = HostState.__new__(HostState)
+        o.spec, o.num_envs = self.spec, self.num_envs
+        o.arrays = {k: v.copy() for k, v in self.arrays.items()}
+        return o
+
+
+class Oracle:
+    def __init__(self, model, params, num_envs):
+        self.lib = load()
+        self.model, self.params = model, params
+        self.h = self.lib.hao_create(C.byref(model), C.byref(params), num_envs)
+        self.num_envs = num_envs
+
+    def simulate(self, st, n_calls=1, begin=0, end=None):
+        s = st.ctypes()
+        self.lib.hao_simulate(self.h, C.byref(s), n_calls, begin, self.num_envs if end is None else end)
+
+    def controller(self, st):
+        s = st.ctypes()
+        for e in range(self.num_envs):
+            self.lib.hao_controller(self.h, C.byref(s), e)
+
+    def __del__(self):
+        try:
+            self.lib.hao_destroy(self.h)
+        except Exception:
+            pass

@@ -1,0 +1,782 @@
+/*
+ * ORACLE (test infrastructure only) - scalar C restatement of the hand-arm simulator + task step.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library
+ * (oracle/_build/libhandarm_oracle.so), and only as the checker / CPU baseline; the product path
+ * (libhandarm_hip.so) never links or calls it.
+ *
+ * Physics: Isaac Gym / PhysX is a closed binary that is absent here, so PHYSICS
+ * PARITY VS PHYSX IS UNPINNED.  This file restates, one env at a time and in plain loops, the
+ * algorithm the HIP kernels implement (see DESIGN.md "Physics"):
+ *   - fixed-base articulation in reduced coordinates; world-frame spatial algebra; forward
+ *     kinematics; CRBA joint-space inertia; RNEA velocity-product (Coriolis) forces
+ *     (PhysX articulation semantics: gravity disabled on the robot, ur5sih.py:176);
+ *   - implicit PD position drives  (DOF_MODE_POS, kp/kd of Ur5SihBase.yaml:3-4, effort limit
+ *     from the URDF <limit effort>) folded into the joint-space inertia, saturating at the effort;
+ *   - free rigid objects (gravity, Isaac Gym default angular damping 0.5);
+ *   - convex-hull contact generation (SAT over face normals, reference-face / incident-vertex
+ *     manifold reduced to <= 4 points per pair), ground plane and table box;
+ *   - projected Gauss-Seidel on the Delassus system J M^-1 J^T (normal + 2 friction rows per
+ *     contact, joint-limit rows), Baumgarte + speculative contacts, `solver_iters` sweeps;
+ *   - symplectic Euler integration, `substeps` substeps per gym.simulate() call.
+ * Task math (controllers, reset, observations, reward, done) restates the reference exactly as
+ * oracle/task_oracle.py does; that file is the one pinned against reference-generated goldens.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/handarm_abi.h"
+
+#define MAXC 21          /* contacts per env (3 rows each -> 63 rows + limit rows <= 64) */
+#define MAXR 64
+#define NOBJ HA_MAX_OBJ
+
+typedef struct { float x, y, z; } v3;
+static v3 V(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static v3 add(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+static v3 sub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static v3 mul(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
+static float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static v3 crs(v3 a, v3 b) { return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+static v3 ld3(const float* p) { return V(p[0], p[1], p[2]); }
+static void st3(float* p, v3 a) { p[0] = a.x; p[1] = a.y; p[2] = a.z; }
+
+typedef struct { float x, y, z, w; } qt;
+static qt Q(float x, float y, float z, float w) { qt r = {x, y, z, w}; return r; }
+static qt ldq(const float* p) { return Q(p[0], p[1], p[2], p[3]); }
+static void stq(float* p, qt q) { p[0] = q.x; p[1] = q.y; p[2] = q.z; p[3] = q.w; }
+static qt qmul(qt a, qt b) {
+    return Q(a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y, a.w * b.y - a.x * b.z + a.y * b.w + a.z * b.x,
+             a.w * b.z + a.x * b.y - a.y * b.x + a.z * b.w, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z);
+}
+static v3 qrot(qt q, v3 v) {
+    v3 u = V(q.x, q.y, q.z);
+    v3 t = mul(crs(u, v), 2.0f);
+    return add(add(v, mul(t, q.w)), crs(u, t));
+}
+static qt qnorm(qt q) {
+    float n = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    return Q(q.x / n, q.y / n, q.z / n, q.w / n);
+}
+static qt qaxis(v3 a, float ang) {
+    float s = sinf(0.5f * ang), c = cosf(0.5f * ang);
+    return Q(a.x * s, a.y * s, a.z * s, c);
+}
+/* 3x3 rotation from quat */
+static void qmat(qt q, float R[9]) {
+    float x = q.x, y = q.y, z = q.z, w = q.w;
+    R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w); R[2] = 2 * (x * z + y * w);
+    R[3] = 2 * (x * y + z * w); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
+    R[6] = 2 * (x * z - y * w); R[7] = 2 * (y * z + x * w); R[8] = 1 - 2 * (x * x + y * y);
+}
+static v3 mv(const float M[9], v3 v) {
+    return V(M[0] * v.x + M[1] * v.y + M[2] * v.z, M[3] * v.x + M[4] * v.y + M[5] * v.z,
+             M[6] * v.x + M[7] * v.y + M[8] * v.z);
+}
+/* out = R A R^T */
+static void rart(const float R[9], const float A[9], float out[9]) {
+    float T[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) T[i * 3 + j] = R[i * 3] * A[j] + R[i * 3 + 1] * A[3 + j] + R[i * 3 + 2] * A[6 + j];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            out[i * 3 + j] = T[i * 3] * R[j * 3] + T[i * 3 + 1] * R[j * 3 + 1] + T[i * 3 + 2] * R[j * 3 + 2];
+}
+static int inv3(const float A[9], float out[9]) {
+    float c0 = A[4] * A[8] - A[5] * A[7], c1 = A[5] * A[6] - A[3] * A[8], c2 = A[3] * A[7] - A[4] * A[6];
+    float det = A[0] * c0 + A[1] * c1 + A[2] * c2;
+    if (fabsf(det) < 1e-30f) return -1;
+    float id = 1.0f / det;
+    out[0] = c0 * id; out[1] = (A[2] * A[7] - A[1] * A[8]) * id; out[2] = (A[1] * A[5] - A[2] * A[4]) * id;
+    out[3] = c1 * id; out[4] = (A[0] * A[8] - A[2] * A[6]) * id; out[5] = (A[2] * A[3] - A[0] * A[5]) * id;
+    out[6] = c2 * id; out[7] = (A[1] * A[6] - A[0] * A[7]) * id; out[8] = (A[0] * A[4] - A[1] * A[3]) * id;
+    return 0;
+}
+
+/* spatial inertia at the world origin: (m, h = m c, J = I_c + m(|c|^2 1 - c c^T)) */
+typedef struct { float m; v3 h; float J[9]; } sinert;
+typedef struct { v3 w, v; } twist;   /* (omega, velocity of the point at the world origin) */
+
+static void inert_apply(const sinert* I, twist t, v3* n, v3* f) {
+    *n = add(mv(I->J, t.w), crs(I->h, t.v));
+    *f = sub(mul(t.v, I->m), crs(I->h, t.w));
+}
+
+typedef struct {
+    int nr;                 /* rows */
+    float J[MAXR][HA_MAX_DOFS + 6 * NOBJ];
+    float Y[MAXR][HA_MAX_DOFS + 6 * NOBJ];
+    float vt[MAXR];         /* target velocity */
+    float lo[MAXR], hi[MAXR];
+    int fric_of[MAXR];      /* normal row index for friction rows, -1 otherwise */
+    int contact[MAXR];      /* contact index or -1 */
+} rows_t;
+
+typedef struct {
+    v3 x, n;      /* point, normal from B to A */
+    float sep;
+    int a, b;     /* body codes: -1 static, 0..NOBJ-1 object, 100+link robot */
+} contact_t;
+
+struct hao_s {
+    ha_model_t m;
+    ha_params_t p;
+    int N, A, B, D, NO;
+};
+typedef struct hao_s* hao_handle;
+
+/* ------------------------------------------------------------------ env scratch (one env) */
+typedef struct {
+    float q[HA_MAX_DOFS], qd[HA_MAX_DOFS], tgt[HA_MAX_DOFS];
+    v3 lp[HA_MAX_LINKS];      /* link origin world */
+    qt lq[HA_MAX_LINKS];      /* link rotation */
+    v3 ax[HA_MAX_DOFS], an[HA_MAX_DOFS];
+    /* objects */
+    v3 oc[NOBJ], ov[NOBJ], ow[NOBJ];
+    qt oq[NOBJ];
+    float om[NOBJ], oIinv[NOBJ][9];
+    int pool[NOBJ];
+    int coll[NOBJ];
+    float cforce[1 + HA_MAX_LINKS + 1 + NOBJ][3];
+} env_t;
+
+static int dofn(const hao_handle h) { return h->D; }
+
+static void fk(const hao_handle h, env_t* e) {
+    const ha_model_t* m = &h->m;
+    for (int i = 0; i < m->n_links; i++) {
+        int par = m->link_parent[i];
+        if (par < 0) {
+            e->lp[i] = ld3(m->base_pos);
+            e->lq[i] = ldq(m->base_quat);
+            continue;
+        }
+        e->lp[i] = add(e->lp[par], qrot(e->lq[par], ld3(m->link_origin_pos[i])));
+        qt r = qmul(e->lq[par], ldq(m->link_origin_quat[i]));
+        int d = m->link_dof[i];
+        if (d >= 0) {
+            r = qmul(r, qaxis(ld3(m->link_axis[i]), e->q[d]));
+            e->ax[d] = qrot(r, ld3(m->link_axis[i]));
+            e->an[d] = e->lp[i];
+        }
+        e->lq[i] = r;
+    }
+}
+
+static void link_inertia(const hao_handle h, const env_t* e, int i, sinert* I) {
+    const ha_model_t* m = &h->m;
+    float R[9], Iw[9];
+    qmat(e->lq[i], R);
+    v3 c = add(e->lp[i], qrot(e->lq[i], ld3(m->link_com[i])));
+    rart(R, m->link_inertia[i], Iw);
+    float mm = m->link_mass[i];
+    I->m = mm;
+    I->h = mul(c, mm);
+    float cc = dot(c, c);
+    float cv[3] = {c.x, c.y, c.z};
+    for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) I->J[a * 3 + b] = Iw[a * 3 + b] + mm * ((a == b ? cc : 0.0f) - cv[a] * cv[b]);
+}
+
+/* joint-space inertia M (D x D) and velocity-product forces C (D) */
+static void dynamics(const hao_handle h, env_t* e, float* M, float* C) {
+    const ha_model_t* m = &h->m;
+    int D = dofn(h), L = m->n_links;
+    sinert I[HA_MAX_LINKS], Ic[HA_MAX_LINKS];
+    twist Vl[HA_MAX_LINKS], Al[HA_MAX_LINKS];
+    v3 Fn[HA_MAX_LINKS], Ff[HA_MAX_LINKS];
+    for (int i = 0; i < L; i++) {
+        link_inertia(h, e, i, &I[i]);
+        Ic[i] = I[i];
+        int par = m->link_parent[i], d = m->link_dof[i];
+        twist vp = {V(0, 0, 0), V(0, 0, 0)}, ap = {V(0, 0, 0), V(0, 0, 0)};
+        if (par >= 0) { vp = Vl[par]; ap = Al[par]; }
+        Vl[i] = vp;
+        Al[i] = ap;
+        if (d >= 0) {
+            twist s = {mul(e->ax[d], e->qd[d]), mul(crs(e->an[d], e->ax[d]), e->qd[d])};
+            Vl[i].w = add(vp.w, s.w);
+            Vl[i].v = add(vp.v, s.v);
+            /* A += crm(V) s */
+            Al[i].w = add(ap.w, crs(Vl[i].w, s.w));
+            Al[i].v = add(ap.v, add(crs(Vl[i].w, s.v), crs(Vl[i].v, s.w)));
+        }
+        v3 n1, f1, n2, f2;
+        inert_apply(&I[i], Al[i], &n1, &f1);
+        inert_apply(&I[i], Vl[i], &n2, &f2);
+        /* crf(V) (n2,f2) = (w x n2 + v x f2, w x f2) */
+        Fn[i] = add(n1, add(crs(Vl[i].w, n2), crs(Vl[i].v, f2)));
+        Ff[i] = add(f1, crs(Vl[i].w, f2));
+    }
+    for (int i = 0; i < D; i++) C[i] = 0;
+    for (int i = L - 1; i >= 0; i--) {
+        int par = m->link_parent[i], d = m->link_dof[i];
+        if (d >= 0) C[d] = dot(e->ax[d], Fn[i]) + dot(crs(e->an[d], e->ax[d]), Ff[i]);
+        if (par >= 0) {
+            Fn[par] = add(Fn[par], Fn[i]);
+            Ff[par] = add(Ff[par], Ff[i]);
+            Ic[par].m += Ic[i].m;
+            Ic[par].h = add(Ic[par].h, Ic[i].h);
+            for (int k = 0; k < 9; k++) Ic[par].J[k] += Ic[i].J[k];
+        }
+    }
+    for (int i = 0; i < D * D; i++) M[i] = 0;
+    for (int i = 0; i < L; i++) {
+        int d = m->link_dof[i];
+        if (d < 0) continue;
+        twist s = {e->ax[d], crs(e->an[d], e->ax[d])};
+        v3 n, f;
+        inert_apply(&Ic[i], s, &n, &f);
+        for (int j = i; j >= 0; j = m->link_parent[j]) {
+            int dd = m->link_dof[j];
+            if (dd < 0) continue;
+            float v = dot(e->ax[dd], n) + dot(crs(e->an[dd], e->ax[dd]), f);
+            M[d * D + dd] = v;
+            M[dd * D + d] = v;
+        }
+    }
+}
+
+static int cholesky(float* A, int n) {
+    for (int j = 0; j < n; j++) {
+        float s = A[j * n + j];
+        for (int k = 0; k < j; k++) s -= A[j * n + k] * A[j * n + k];
+        if (s <= 0) return -1;
+        float l = sqrtf(s);
+        A[j * n + j] = l;
+        for (int i = j + 1; i < n; i++) {
+            float t = A[i * n + j];
+            for (int k = 0; k < j; k++) t -= A[i * n + k] * A[j * n + k];
+            A[i * n + j] = t / l;
+        }
+    }
+    return 0;
+}
+static void chol_solve(const float* L, int n, float* x) {
+    for (int i = 0; i < n; i++) {
+        float t = x[i];
+        for (int k = 0; k < i; k++) t -= L[i * n + k] * x[k];
+        x[i] = t / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; i--) {
+        float t = x[i];
+        for (int k = i + 1; k < n; k++) t -= L[k * n + i] * x[k];
+        x[i] = t / L[i * n + i];
+    }
+}
+
+/* ------------------------------------------------------------------ collision */
+typedef struct { v3 p; qt q; } pose_t;
+
+static v3 hull_vert(const ha_model_t* m, int hull, int i, pose_t P) {
+    const float* v = m->verts[m->hull_vert_start[hull] + i];
+    return add(P.p, qrot(P.q, V(v[0], v[1], v[2])));
+}
+static void hull_plane(const ha_model_t* m, int hull, int k, pose_t P, v3* n, float* d) {
+    const float* pl = m->planes[m->hull_plane_start[hull] + k];
+    *n = qrot(P.q, V(pl[0], pl[1], pl[2]));
+    *d = pl[3] - dot(*n, P.p);
+}
+
+/* reduce candidate list (points, sep) to <= 4 contacts; returns count appended */
+static int reduce_manifold(v3* pts, float* seps, int nc, v3 n, int* out_idx) {
+    if (nc <= 0) return 0;
+    int i0 = 0;
+    for (int i = 1; i < nc; i++)
+        if (seps[i] < seps[i0]) i0 = i;
+    out_idx[0] = i0;
+    if (nc == 1) return 1;
+    int i1 = -1;
+    float best = 1e-12f;
+    for (int i = 0; i < nc; i++) {
+        v3 d = sub(pts[i], pts[i0]);
+        float dd = dot(d, d);
+        if (dd > best) { best = dd; i1 = i; }
+    }
+    if (i1 < 0) return 1;
+    out_idx[1] = i1;
+    v3 e = sub(pts[i1], pts[i0]);
+    int i2 = -1, i3 = -1;
+    float bmax = 1e-12f, bmin = -1e-12f;
+    for (int i = 0; i < nc; i++) {
+        float s = dot(crs(e, sub(pts[i], pts[i0])), n);
+        if (s > bmax) { bmax = s; i2 = i; }
+        if (s < bmin) { bmin = s; i3 = i; }
+    }
+    int k = 2;
+    if (i2 >= 0) out_idx[k++] = i2;
+    if (i3 >= 0) out_idx[k++] = i3;
+    return k;
+}
+
+#define MAXCAND 128
+static int emit(contact_t* out, int* nout, int maxout, v3* pts, float* seps, int nc, v3 n, int a, int b) {
+    int idx[4];
+    int k = reduce_manifold(pts, seps, nc, n, idx);
+    for (int i = 0; i < k; i++) {
+        if (*nout >= maxout) {
+            /* replace the shallowest stored contact if this one is deeper */
+            int w = 0;
+            for (int j = 1; j < maxout; j++)
+                if (out[j].sep > out[w].sep) w = j;
+            if (out[w].sep <= seps[idx[i]]) continue;
+            out[w].x = pts[idx[i]]; out[w].n = n; out[w].sep = seps[idx[i]]; out[w].a = a; out[w].b = b;
+            continue;
+        }
+        contact_t* c = &out[(*nout)++];
+        c->x = pts[idx[i]]; c->n = n; c->sep = seps[idx[i]]; c->a = a; c->b = b;
+    }
+    return k;
+}
+
+/* hull A (body a) vs hull B (body b); contact normal from B to A */
+static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t PB, float margin, int a, int b,
+                          contact_t* out, int* nout, int maxout) {
+    int nva = m->hull_nverts[ha], nvb = m->hull_nverts[hb];
+    int npa = m->hull_nplanes[ha], npb = m->hull_nplanes[hb];
+    /* bounding spheres */
+    v3 ca = add(PA.p, qrot(PA.q, ld3(m->hull_center[ha]))), cb = add(PB.p, qrot(PB.q, ld3(m->hull_center[hb])));
+    v3 dc = sub(ca, cb);
+    float rr = m->hull_radius[ha] + m->hull_radius[hb] + margin;
+    if (dot(dc, dc) > rr * rr) return;
+    v3 va[64], vb[64];
+    for (int i = 0; i < nva; i++) va[i] = hull_vert(m, ha, i, PA);
+    for (int i = 0; i < nvb; i++) vb[i] = hull_vert(m, hb, i, PB);
+    /* SAT over face normals */
+    float sepA = -1e30f, sepB = -1e30f;
+    int kA = -1, kB = -1;
+    for (int k = 0; k < npa; k++) {
+        v3 n; float d;
+        hull_plane(m, ha, k, PA, &n, &d);
+        float mn = 1e30f;
+        for (int i = 0; i < nvb; i++) { float s = dot(n, vb[i]) + d; if (s < mn) mn = s; }
+        if (mn > sepA) { sepA = mn; kA = k; }
+    }
+    if (sepA > margin) return;
+    for (int k = 0; k < npb; k++) {
+        v3 n; float d;
+        hull_plane(m, hb, k, PB, &n, &d);
+        float mn = 1e30f;
+        for (int i = 0; i < nva; i++) { float s = dot(n, va[i]) + d; if (s < mn) mn = s; }
+        if (mn > sepB) { sepB = mn; kB = k; }
+    }
+    if (sepB > margin) return;
+    v3 pts[MAXCAND];
+    float seps[MAXCAND];
+    for (int pass = 0; pass < 2; pass++) {
+        int refB = (sepB >= sepA) ? (pass == 0) : (pass == 1);
+        int hr = refB ? hb : ha, hi = refB ? ha : hb, kr = refB ? kB : kA;
+        pose_t Pr = refB ? PB : PA;
+        v3* vi = refB ? va : vb;
+        int nvi = refB ? nva : nvb, npr = m->hull_nplanes[hr];
+        v3 nref; float dref;
+        hull_plane(m, hr, kr, Pr, &nref, &dref);
+        int nc = 0;
+        for (int i = 0; i < nvi && nc < MAXCAND; i++) {
+            float dist = dot(nref, vi[i]) + dref;
+            if (dist > margin) continue;
+            float mx = -1e30f;
+            for (int k = 0; k < npr; k++) {
+                if (k == kr) continue;
+                v3 n; float d;
+                hull_plane(m, hr, k, Pr, &n, &d);
+                float s = dot(n, vi[i]) + d;
+                if (s > mx) mx = s;
+            }
+            if (mx > margin) continue;
+            pts[nc] = sub(vi[i], mul(nref, 0.5f * dist));
+            seps[nc] = dist;
+            nc++;
+        }
+        if (nc > 0) {
+            v3 n = refB ? nref : mul(nref, -1.0f);
+            emit(out, nout, maxout, pts, seps, nc, n, a, b);
+            return;
+        }
+    }
+}
+
+static void collide_ground(const ha_model_t* m, int ha, pose_t PA, float margin, int a, contact_t* out, int* nout,
+                           int maxout) {
+    v3 c = add(PA.p, qrot(PA.q, ld3(m->hull_center[ha])));
+    if (c.z - m->hull_radius[ha] > margin) return;
+    v3 pts[64];
+    float seps[64];
+    int nc = 0;
+    for (int i = 0; i < m->hull_nverts[ha]; i++) {
+        v3 v = hull_vert(m, ha, i, PA);
+        if (v.z <= margin) { pts[nc] = sub(v, V(0, 0, 0.5f * v.z)); seps[nc] = v.z; nc++; }
+    }
+    emit(out, nout, maxout, pts, seps, nc, V(0, 0, 1), a, -1);
+}
+
+static int detect(const hao_handle h, const env_t* e, contact_t* out) {
+    const ha_model_t* m = &h->m;
+    const ha_params_t* p = &h->p;
+    int nout = 0;
+    float mg = p->contact_margin;
+    pose_t Ptab = {ld3(m->table_pos), ldq(m->table_quat)};
+    for (int o = 0; o < h->NO; o++) {
+        if (!e->coll[o]) continue;
+        int ho = m->pool_hull[e->pool[o]];
+        pose_t Po = {sub(e->oc[o], qrot(e->oq[o], ld3(m->pool_com[e->pool[o]]))), e->oq[o]};
+        collide_ground(m, ho, Po, mg, o, out, &nout, MAXC);
+        collide_hulls(m, ho, Po, m->table_hull, Ptab, mg, o, -1, out, &nout, MAXC);
+        for (int o2 = o + 1; o2 < h->NO; o2++) {
+            if (!e->coll[o2]) continue;
+            int h2 = m->pool_hull[e->pool[o2]];
+            pose_t P2 = {sub(e->oc[o2], qrot(e->oq[o2], ld3(m->pool_com[e->pool[o2]]))), e->oq[o2]};
+            collide_hulls(m, ho, Po, h2, P2, mg, o, o2, out, &nout, MAXC);
+        }
+        for (int k = 0; k < m->n_link_hulls; k++) {
+            int L = m->hull_link[k];
+            pose_t PL = {e->lp[L], e->lq[L]};
+            collide_hulls(m, k, PL, ho, Po, mg, 100 + L, o, out, &nout, MAXC);
+        }
+    }
+    for (int k = 0; k < m->n_link_hulls; k++) {
+        int L = m->hull_link[k];
+        if (!m->link_table_collide[L]) continue;
+        pose_t PL = {e->lp[L], e->lq[L]};
+        collide_hulls(m, k, PL, m->table_hull, Ptab, mg, 100 + L, -1, out, &nout, MAXC);
+    }
+    return nout;
+}
+
+/* Jacobian row: relative velocity of body a minus body b at point x along dir, into J (len D+6*NO) */
+static void jac_body(const hao_handle h, const env_t* e, int body, v3 x, v3 dir, float sgn, float* J) {
+    int D = dofn(h);
+    if (body < 0) return;
+    if (body < 100) {
+        int o = body;
+        v3 r = sub(x, e->oc[o]);
+        v3 ang = crs(r, dir);
+        float* Jo = J + D + 6 * o;
+        Jo[0] += sgn * dir.x; Jo[1] += sgn * dir.y; Jo[2] += sgn * dir.z;
+        Jo[3] += sgn * ang.x; Jo[4] += sgn * ang.y; Jo[5] += sgn * ang.z;
+        return;
+    }
+    int L = body - 100;
+    for (int j = L; j >= 0; j = h->m.link_parent[j]) {
+        int d = h->m.link_dof[j];
+        if (d < 0) continue;
+        J[d] += sgn * dot(e->ax[d], crs(sub(x, e->an[d]), dir));
+    }
+}
+
+/* Y = Minv J^T for one row */
+static void apply_minv(const hao_handle h, const env_t* e, const float* L, const float* J, float* Y) {
+    int D = dofn(h);
+    for (int i = 0; i < D; i++) Y[i] = J[i];
+    chol_solve(L, D, Y);
+    for (int o = 0; o < h->NO; o++) {
+        const float* Jo = J + D + 6 * o;
+        float* Yo = Y + D + 6 * o;
+        float im = 1.0f / e->om[o];
+        Yo[0] = Jo[0] * im; Yo[1] = Jo[1] * im; Yo[2] = Jo[2] * im;
+        v3 a = mv(e->oIinv[o], V(Jo[3], Jo[4], Jo[5]));
+        Yo[3] = a.x; Yo[4] = a.y; Yo[5] = a.z;
+    }
+}
+
+static void tangents(v3 n, v3* t1, v3* t2) {
+    v3 a = fabsf(n.x) < 0.9f ? V(1, 0, 0) : V(0, 1, 0);
+    v3 t = crs(n, a);
+    float l = sqrtf(dot(t, t));
+    *t1 = mul(t, 1.0f / l);
+    *t2 = crs(n, *t1);
+}
+
+static void substep(const hao_handle h, env_t* e, float hdt) {
+    const ha_model_t* m = &h->m;
+    const ha_params_t* p = &h->p;
+    int D = dofn(h), NO = h->NO, NV = D + 6 * NO;
+    static __thread float M[HA_MAX_DOFS * HA_MAX_DOFS];
+    float C[HA_MAX_DOFS], rhs[HA_MAX_DOFS];
+    fk(h, e);
+    dynamics(h, e, M, C);
+    /* implicit PD drives with effort saturation */
+    for (int d = 0; d < D; d++) {
+        float kp = m->dof_kp[d], kd = m->dof_kd[d], eff = m->dof_effort[d];
+        float fpred = kp * (e->tgt[d] - e->q[d] - hdt * e->qd[d]) - kd * e->qd[d];
+        float tau;
+        if (fabsf(fpred) > eff) {
+            tau = fpred > 0 ? eff : -eff;
+        } else {
+            tau = kp * (e->tgt[d] - e->q[d]) - kd * e->qd[d] - hdt * kp * e->qd[d];
+            M[d * D + d] += hdt * kd + hdt * hdt * kp;
+        }
+        rhs[d] = hdt * (tau - C[d]);
+    }
+    if (cholesky(M, D) != 0) return;
+    chol_solve(M, D, rhs);
+    float v[HA_MAX_DOFS + 6 * NOBJ];
+    for (int d = 0; d < D; d++) v[d] = e->qd[d] + rhs[d];
+    for (int o = 0; o < NO; o++) {
+        float damp = 1.0f / (1.0f + hdt * p->object_ang_damping);
+        v3 lv = add(e->ov[o], mul(ld3(p->gravity), hdt));
+        v3 av = mul(e->ow[o], damp);
+        float* vo = v + D + 6 * o;
+        vo[0] = lv.x; vo[1] = lv.y; vo[2] = lv.z; vo[3] = av.x; vo[4] = av.y; vo[5] = av.z;
+        /* world inverse inertia */
+        float R[9], Iw[9];
+        qmat(e->oq[o], R);
+        rart(R, m->pool_inertia[e->pool[o]], Iw);
+        inv3(Iw, e->oIinv[o]);
+        e->om[o] = m->pool_mass[e->pool[o]];
+    }
+    /* contacts -> rows */
+    contact_t cs[MAXC];
+    int nc = detect(h, e, cs);
+    static __thread rows_t R;
+    R.nr = 0;
+    for (int c = 0; c < nc && R.nr + 3 <= MAXR; c++) {
+        v3 t1, t2;
+        tangents(cs[c].n, &t1, &t2);
+        v3 dirs[3] = {cs[c].n, t1, t2};
+        int base = R.nr;
+        for (int k = 0; k < 3; k++) {
+            int r = R.nr++;
+            memset(R.J[r], 0, sizeof(float) * NV);
+            jac_body(h, e, cs[c].a, cs[c].x, dirs[k], 1.0f, R.J[r]);
+            jac_body(h, e, cs[c].b, cs[c].x, dirs[k], -1.0f, R.J[r]);
+            R.contact[r] = c;
+            if (k == 0) {
+                float s = cs[c].sep;
+                float vt = s > 0 ? -s / hdt : -p->baumgarte * s / hdt;
+                if (vt > p->max_depen_vel) vt = p->max_depen_vel;
+                R.vt[r] = vt; R.lo[r] = 0; R.hi[r] = 1e30f; R.fric_of[r] = -1;
+            } else {
+                R.vt[r] = 0; R.lo[r] = 0; R.hi[r] = 0; R.fric_of[r] = base;
+            }
+        }
+    }
+    for (int d = 0; d < D && R.nr < MAXR; d++) {
+        float lo = m->dof_lower[d], up = m->dof_upper[d];
+        for (int side = 0; side < 2 && R.nr < MAXR; side++) {
+            float s = side == 0 ? e->q[d] - lo : up - e->q[d];
+            if (s > p->joint_limit_margin) continue;
+            int r = R.nr++;
+            memset(R.J[r], 0, sizeof(float) * NV);
+            R.J[r][d] = side == 0 ? 1.0f : -1.0f;
+            float vt = s > 0 ? -s / hdt : -p->baumgarte * s / hdt;
+            R.vt[r] = vt; R.lo[r] = 0; R.hi[r] = 1e30f; R.fric_of[r] = -1; R.contact[r] = -1;
+        }
+    }
+    int nr = R.nr;
+    static __thread float Am[MAXR][MAXR];
+    float w[MAXR], lam[MAXR];
+    for (int r = 0; r < nr; r++) apply_minv(h, e, M, R.J[r], R.Y[r]);
+    for (int r = 0; r < nr; r++) {
+        for (int s = 0; s < nr; s++) {
+            float a = 0;
+            for (int k = 0; k < NV; k++) a += R.J[r][k] * R.Y[s][k];
+            Am[r][s] = a;
+        }
+        float b = 0;
+        for (int k = 0; k < NV; k++) b += R.J[r][k] * v[k];
+        w[r] = b - R.vt[r];
+        lam[r] = 0;
+        Am[r][r] += 1e-9f;
+    }
+    for (int it = 0; it < p->solver_iters; it++) {
+        for (int r = 0; r < nr; r++) {
+            float lo = R.lo[r], hi = R.hi[r];
+            if (R.fric_of[r] >= 0) {
+                hi = p->friction * lam[R.fric_of[r]];
+                lo = -hi;
+            }
+            float nl = lam[r] - w[r] / Am[r][r];
+            nl = nl < lo ? lo : (nl > hi ? hi : nl);
+            float dl = nl - lam[r];
+            if (dl != 0.0f) {
+                lam[r] = nl;
+                /* A is symmetric; Am[r][s] = J_r . M^-1 J_s^T is the entry the GPU lane s holds */
+                for (int s = 0; s < nr; s++) w[s] += Am[r][s] * dl;
+            }
+        }
+    }
+    for (int r = 0; r < nr; r++)
+        for (int k = 0; k < NV; k++) v[k] += R.Y[r][k] * lam[r];
+    /* contact forces per body (net_contact_force): the last substep's forces */
+    memset(e->cforce, 0, sizeof(e->cforce));
+    for (int c = 0; c < nc; c++) {
+        int r0 = 3 * c;
+        if (r0 + 2 >= nr) break;
+        v3 t1, t2;
+        tangents(cs[c].n, &t1, &t2);
+        v3 f = add(add(mul(cs[c].n, lam[r0]), mul(t1, lam[r0 + 1])), mul(t2, lam[r0 + 2]));
+        f = mul(f, 1.0f / hdt);
+        int bodies[2] = {cs[c].a, cs[c].b};
+        for (int s = 0; s < 2; s++) {
+            int bd = bodies[s];
+            float sg = s == 0 ? 1.0f : -1.0f;
+            int idx = -1;
+            if (bd >= 100) idx = 1 + (bd - 100);
+            else if (bd >= 0) idx = 1 + m->n_links + 1 + bd;
+            if (idx < 0) continue;
+            e->cforce[idx][0] += sg * f.x; e->cforce[idx][1] += sg * f.y; e->cforce[idx][2] += sg * f.z;
+        }
+    }
+    /* integrate */
+    for (int d = 0; d < D; d++) {
+        e->qd[d] = v[d];
+        e->q[d] += hdt * v[d];
+    }
+    for (int o = 0; o < NO; o++) {
+        float* vo = v + D + 6 * o;
+        e->ov[o] = V(vo[0], vo[1], vo[2]);
+        e->ow[o] = V(vo[3], vo[4], vo[5]);
+        e->oc[o] = add(e->oc[o], mul(e->ov[o], hdt));
+        qt dq = qmul(Q(e->ow[o].x, e->ow[o].y, e->ow[o].z, 0.0f), e->oq[o]);
+        qt q = e->oq[o];
+        e->oq[o] = qnorm(Q(q.x + 0.5f * hdt * dq.x, q.y + 0.5f * hdt * dq.y, q.z + 0.5f * hdt * dq.z,
+                           q.w + 0.5f * hdt * dq.w));
+    }
+}
+
+/* ------------------------------------------------------------------ state load/store */
+static void load_env(const hao_handle h, const ha_state_t* S, int env, env_t* e) {
+    const ha_model_t* m = &h->m;
+    int D = h->D, A = h->A;
+    for (int d = 0; d < D; d++) {
+        e->q[d] = S->dof_state[(env * D + d) * 2];
+        e->qd[d] = S->dof_state[(env * D + d) * 2 + 1];
+        e->tgt[d] = S->sim_targets[env * D + d];
+    }
+    for (int o = 0; o < h->NO; o++) {
+        const float* r = S->root_state + (env * A + 3 + o) * 13;
+        int pid = (int)S->object_indices[env * h->NO + o];
+        e->pool[o] = pid;
+        e->oq[o] = ldq(r + 3);
+        e->oc[o] = add(ld3(r), qrot(e->oq[o], ld3(m->pool_com[pid])));
+        e->ov[o] = ld3(r + 7);
+        e->ow[o] = ld3(r + 10);
+        e->coll[o] = S->collision_enabled ? S->collision_enabled[env * h->NO + o] : 1;
+    }
+    memset(e->cforce, 0, sizeof(e->cforce));
+}
+
+static void store_env(const hao_handle h, ha_state_t* S, int env, env_t* e) {
+    const ha_model_t* m = &h->m;
+    int D = h->D, A = h->A, B = h->B;
+    for (int d = 0; d < D; d++) {
+        S->dof_state[(env * D + d) * 2] = e->q[d];
+        S->dof_state[(env * D + d) * 2 + 1] = e->qd[d];
+    }
+    for (int o = 0; o < h->NO; o++) {
+        float* r = S->root_state + (env * A + 3 + o) * 13;
+        v3 pos = sub(e->oc[o], qrot(e->oq[o], ld3(m->pool_com[e->pool[o]])));
+        st3(r, pos); stq(r + 3, e->oq[o]); st3(r + 7, e->ov[o]); st3(r + 10, e->ow[o]);
+    }
+    /* rigid body states: goal, robot links, table, objects */
+    fk(h, e);
+    float* bs = S->rigid_body_state + (size_t)env * B * 13;
+    const float* goal = S->root_state + (env * A + 0) * 13;
+    memcpy(bs, goal, 13 * sizeof(float));
+    twist Vl[HA_MAX_LINKS];
+    for (int i = 0; i < m->n_links; i++) {
+        int par = m->link_parent[i], d = m->link_dof[i];
+        twist vp = {V(0, 0, 0), V(0, 0, 0)};
+        if (par >= 0) vp = Vl[par];
+        Vl[i] = vp;
+        if (d >= 0) {
+            Vl[i].w = add(vp.w, mul(e->ax[d], e->qd[d]));
+            Vl[i].v = add(vp.v, mul(crs(e->an[d], e->ax[d]), e->qd[d]));
+        }
+        float* b = bs + (1 + i) * 13;
+        v3 c = add(e->lp[i], qrot(e->lq[i], ld3(m->link_com[i])));
+        v3 lin = add(Vl[i].v, crs(Vl[i].w, c));
+        st3(b, e->lp[i]); stq(b + 3, e->lq[i]); st3(b + 7, lin); st3(b + 10, Vl[i].w);
+    }
+    memcpy(bs + (1 + m->n_links) * 13, S->root_state + (env * A + 2) * 13, 13 * sizeof(float));
+    for (int o = 0; o < h->NO; o++)
+        memcpy(bs + (1 + m->n_links + 1 + o) * 13, S->root_state + (env * A + 3 + o) * 13, 13 * sizeof(float));
+    for (int b = 0; b < B; b++)
+        for (int k = 0; k < 3; k++) S->net_contact_force[((size_t)env * B + b) * 3 + k] = e->cforce[b][k];
+}
+
+/* ------------------------------------------------------------------ public oracle API */
+hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int num_envs) {
+    hao_handle h = (hao_handle)calloc(1, sizeof(struct hao_s));
+    h->m = *model;
+    h->p = *params;
+    h->N = num_envs;
+    h->NO = params->n_objects;
+    h->A = 3 + h->NO;
+    h->D = model->n_dofs;
+    h->B = 1 + model->n_links + 1 + h->NO;
+    return h;
+}
+void hao_destroy(hao_handle h) { free(h); }
+int hao_struct_sizes(int32_t* model_size, int32_t* params_size, int32_t* state_size) {
+    *model_size = (int32_t)sizeof(ha_model_t);
+    *params_size = (int32_t)sizeof(ha_params_t);
+    *state_size = (int32_t)sizeof(ha_state_t);
+    return 0;
+}
+
+static void simulate_env(const hao_handle h, ha_state_t* S, int env, int n_calls) {
+    env_t e;
+    load_env(h, S, env, &e);
+    float hdt = h->p.dt / (float)h->p.substeps;
+    for (int c = 0; c < n_calls; c++)
+        for (int s = 0; s < h->p.substeps; s++) substep(h, &e, hdt);
+    /* net contact force of the last substep (PhysX reports the last substep's forces) */
+    store_env(h, S, env, &e);
+}
+
+void hao_simulate(hao_handle h, ha_state_t* S, int n_calls, int env_begin, int env_end) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int env = env_begin; env < env_end; env++) simulate_env(h, S, env, n_calls);
+}
+
+/* --------------------------------------------------------------- task math (see task_oracle.py) */
+static float spline_eval(const ha_params_t* p, int s, float t) {
+    int n = p->spline_pieces[s];
+    /* bucketize(t, knots) - 1 clamped to [0, n-1]; knots[k] = t0[k], knots[n] not needed */
+    int idx = 0;
+    for (int k = 1; k < n; k++)
+        if (t > p->spline[s][0][k]) idx = k;
+    float f = t - p->spline[s][0][idx];
+    float inner = 0.5f * p->spline[s][3][idx] + p->spline[s][4][idx] * f / 3.0f;
+    inner = p->spline[s][2][idx] + inner * f;
+    return p->spline[s][1][idx] + inner * f;
+}
+
+enum { D_INDEX = 6, D_IF_DISTAL, D_LF, D_LF_DISTAL, D_MIDDLE, D_MF_DISTAL, D_RING, D_RF_DISTAL, D_TH_OPP, D_TH_FLEX,
+       D_TH_DISTAL };
+
+void hao_controller(hao_handle h, ha_state_t* S, int env) {
+    const ha_params_t* p = &h->p;
+    const float* a = S->actions + env * 11;
+    float* ur5 = S->ur5_target + env * 6;
+    float* servo = S->servo + env * 5;
+    float* sm = S->smoothed + env * 5;
+    float* tgt = S->dof_position_targets + env * h->D;
+    const float* dof = S->dof_state + (size_t)env * h->D * 2;
+    for (int i = 0; i < 6; i++) ur5[i] = ur5[i] + p->action_dt * a[i];
+    float alpha = p->sih_alpha, beta = (float)(1.0 - (double)p->sih_alpha);
+    for (int i = 0; i < 5; i++) {
+        sm[i] = alpha * a[6 + i] + beta * sm[i];
+        float s = servo[i] + 100.0f * sm[i];
+        s = s < p->servo_lower[i] ? p->servo_lower[i] : s;
+        s = s > p->servo_upper[i] ? p->servo_upper[i] : s;
+        servo[i] = s;
+    }
+    for (int i = 0; i < 6; i++) tgt[i] = ur5[i];
+    tgt[D_TH_OPP] = p->thumb_opposition_gain * servo[0];
+    tgt[D_TH_FLEX] = -spline_eval(p, 0, servo[1]);
+    tgt[D_TH_DISTAL] = -spline_eval(p, 1, servo[1] + p->proximal_coef[0] * dof[2 * D_TH_FLEX]);
+    tgt[D_INDEX] = spline_eval(p, 2, servo[2]);
+    tgt[D_IF_DISTAL] = spline_eval(p, 3, servo[2] + p->proximal_coef[1] * dof[2 * D_INDEX]);
+    tgt[D_MIDDLE] = spline_eval(p, 4, servo[3]);
+    tgt[D_MF_DISTAL] = spline_eval(p, 5, servo[3] + p->proximal_coef[2] * dof[2 * D_MIDDLE]);
+    tgt[D_RING] = spline_eval(p, 6, servo[4]);
+    tgt[D_RF_DISTAL] = spline_eval(p, 7, servo[4] + p->proximal_coef[3] * dof[2 * D_RING]);
+    tgt[D_LF] = tgt[D_RING];
+    tgt[D_LF_DISTAL] = tgt[D_RF_DISTAL];
+    for (int d = 0; d < h->D; d++) S->sim_targets[env * h->D + d] = tgt[d];
+}

@@ -1,0 +1,45 @@
+"""Seeded synthetic scene states shared by the parity tests and bench.py's CPU-baseline leg.
+
+Layouts are the Isaac Gym tensor layouts of handarm_hip.model.state_spec (host numpy)."""
+import numpy as np
+
+RESET_POSE = np.array([0.6985, -1.4106, 1.2932, 0.1174, 0.6983, 1.5708, 0., 0., 0., 0., 0., 0., 0., 0., -1.571,
+                       0., 0.], np.float32)
+
+
+def rand_quat(rng, shape):
+    q = rng.standard_normal(shape + (4,)).astype(np.float32)
+    return (q / np.linalg.norm(q, axis=-1, keepdims=True)).astype(np.float32)
+
+
+def fill_scene(st, num_envs, seed=0, near_hand=0.3, n_obj=3, fingertip_pos=None):
+    """Robot near its reset pose, objects resting-ish on the table, some dropped into the hand."""
+    rng = np.random.default_rng(seed)
+    N, A = num_envs, 3 + n_obj
+    rs = st["root_state"].reshape(N, A, 13)
+    rs[:] = 0
+    rs[..., 6] = 1.0
+    rs[:, 0, 0:3] = [0.28, 0.58, 0.8]
+    rs[:, 1, 0:3] = [0.0, 0.0, 0.5]
+    rs[:, 2, 0:3] = [0.2925, 0.38, 0.25]
+    for o in range(n_obj):
+        rs[:, 3 + o, 0] = 0.08 + 0.17 * o + rng.uniform(-0.03, 0.03, N)
+        rs[:, 3 + o, 1] = rng.uniform(0.45, 0.75, N)
+        rs[:, 3 + o, 2] = rng.uniform(0.56, 0.62, N)
+        rs[:, 3 + o, 3:7] = rand_quat(rng, (N,))
+        rs[:, 3 + o, 7:10] = rng.uniform(-0.2, 0.2, (N, 3))
+        rs[:, 3 + o, 10:13] = rng.uniform(-1.0, 1.0, (N, 3))
+    if fingertip_pos is not None:
+        sel = rng.random(N) < near_hand
+        rs[sel, 3, 0:3] = fingertip_pos[sel] + rng.uniform(-0.02, 0.02, (int(sel.sum()), 3))
+    ds = st["dof_state"].reshape(N, 17, 2)
+    ds[..., 0] = RESET_POSE + rng.uniform(-0.05, 0.05, (N, 17)).astype(np.float32)
+    ds[..., 0, ] = np.clip(ds[..., 0], -6, 6)
+    ds[:, 6:14, 0] = np.clip(ds[:, 6:14, 0], -1.571, 0.0)
+    ds[:, 14, 0] = np.clip(ds[:, 14, 0], -1.571, 0.0)
+    ds[:, 15:17, 0] = np.clip(ds[:, 15:17, 0], 0.0, 1.571)
+    ds[..., 1] = rng.uniform(-0.3, 0.3, (N, 17))
+    st["sim_targets"][:] = RESET_POSE + rng.uniform(-0.3, 0.3, (N, 17)).astype(np.float32)
+    st["object_indices"][:] = np.stack([rng.permutation(3) for _ in range(N)])
+    st["collision_enabled"][:] = 1
+    return st
