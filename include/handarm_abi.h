@@ -116,6 +116,7 @@ typedef struct ha_params_t {
     int32_t max_episode_length;/* 200 */
     float action_dt;           /* dt used by the UR5 relative controller (VecTask.dt = sim dt) */
     float sih_alpha;           /* 0.8 */
+    float sih_beta;            /* 1 - alpha evaluated in double then rounded (python-float semantics) */
     float reward_reaching, reward_lifting, reward_goal, reward_success;
     float lifting_threshold, goal_threshold;
     float goal_pos[3], goal_noise[3];

@@ -37,6 +37,7 @@ struct EnvLDS {
     float Ic[HA_MAX_LINKS][13];                 // composite spatial inertia (m, h, J) at world origin
     float Vl[HA_MAX_LINKS][6], Al[HA_MAX_LINKS][6], Fl[HA_MAX_LINKS][6];
     float M[MAXD * MAXD];
+    float Minv[MAXD * MAXD];
     float Cb[MAXD], rhs[MAXD];
     float v[RS];
     float oc[NOBJ][4], oq[NOBJ][4], ov[NOBJ][4], ow[NOBJ][4], oIinv[NOBJ][12], om[NOBJ];
@@ -556,21 +557,8 @@ HD void substep(SimCtx& c, float hdt) {
     int NV = D + 6 * NO;
     fk(c);
     dynamics(c);
-    // implicit PD drives with effort saturation
-    if (lane < D) {
-        int d = lane;
-        float kp = m.dof_kp[d], kd = m.dof_kd[d], eff = m.dof_effort[d];
-        float q = s.q[d], qd = s.qd[d];
-        float fpred = kp * (s.tgt[d] - q - hdt * qd) - kd * qd;
-        float tau;
-        if (fabsf(fpred) > eff) {
-            tau = fpred > 0 ? eff : -eff;
-        } else {
-            tau = kp * (s.tgt[d] - q) - kd * qd - hdt * kp * qd;
-            s.M[d * D + d] += hdt * kd + hdt * hdt * kp;
-        }
-        s.rhs[d] = hdt * (tau - s.Cb[d]);
-    }
+    // free motion: velocity-product forces only (drives are constraint rows of the PGS below)
+    if (lane < D) s.rhs[lane] = -hdt * s.Cb[lane];
     wsync();
     cholesky(c);
     {
@@ -578,10 +566,18 @@ HD void substep(SimCtx& c, float hdt) {
 #pragma unroll
         for (int i = 0; i < MAXD; i++) x[i] = i < D ? s.rhs[i] : 0.0f;
         chol_solve_regs(c, x);
-        wsync();
 #pragma unroll
         for (int i = 0; i < MAXD; i++)
             if (i < D && lane == i) s.v[i] = s.qd[i] + x[i];
+        // explicit M^-1: lane k solves M x = e_k; row k of Minv = column k (symmetric)
+#pragma unroll
+        for (int i = 0; i < MAXD; i++) x[i] = (i == lane) ? 1.0f : 0.0f;
+        chol_solve_regs(c, x);
+        if (lane < D) {
+#pragma unroll
+            for (int i = 0; i < MAXD; i++)
+                if (i < D) s.Minv[lane * MAXD + i] = x[i];
+        }
     }
     if (lane < NO) {
         int o = lane;
@@ -717,9 +713,45 @@ HD void substep(SimCtx& c, float hdt) {
             if (k == r) { A[k] += 1e-9f; rinv = A[k]; }
         lo = s.lo[r]; hi = s.hi[r]; fric_of = s.fric_of[r];
     }
-    // ---- projected Gauss-Seidel: row r's residual / impulse live in lane r
+    // generalized velocity: lane k owns v[k]
+    float vreg = lane < NV ? s.v[lane] : 0.0f;
+    // PD drive rows (lane d): soft implicit spring-damper, impulse bounded by effort * h
+    float dgam = 0.f, dbias = 0.f, dwinv = 0.f, dlim = 0.f, dlam = 0.f;
+    if (lane < D) {
+        float kp = m.dof_kp[lane], kd = m.dof_kd[lane];
+        float den = kd + hdt * kp;
+        dgam = 1.0f / (hdt * den);
+        dbias = kp / den * (s.q[lane] - s.tgt[lane]);
+        dwinv = 1.0f / (s.Minv[lane * MAXD + lane] + dgam);
+        dlim = m.dof_effort[lane] * hdt;
+    }
+    wsync();
+    // Y rows replace J rows in LDS (J is no longer needed): lane k reads Y[r][k] in the sweep
+    if (myrow) {
+#pragma unroll
+        for (int t = 0; t < RS; t++) Jr[t] = y[t];
+    }
+    wsync();
+    // ---- projected Gauss-Seidel: drive rows in velocity form (J = e_d, residual = v[d]),
+    //      contact/limit rows in Delassus form (row r's residual / impulse live in lane r)
     const float mu = p.friction;
+    const float* Y = s.J;
     for (int it = 0; it < p.solver_iters; it++) {
+#pragma unroll
+        for (int d = 0; d < MAXD; d++) {
+            if (d < D) {
+                float vd = bcast(vreg, d), ld = bcast(dlam, d);
+                float nl = ld - (vd + bcast(dbias, d) + bcast(dgam, d) * ld) * bcast(dwinv, d);
+                float lim = bcast(dlim, d);
+                nl = nl < -lim ? -lim : (nl > lim ? lim : nl);
+                float dl = nl - ld;
+                if (dl != 0.0f) {
+                    if (lane == d) dlam = nl;
+                    if (lane < D) vreg += s.Minv[d * MAXD + lane] * dl;
+                    w += y[d] * dl;
+                }
+            }
+        }
 #pragma unroll
         for (int k = 0; k < MAXR; k++) {
             if (k < nr) {
@@ -736,25 +768,14 @@ HD void substep(SimCtx& c, float hdt) {
                 if (dl != 0.0f) {
                     if (lane == k) lam = nl;
                     w += A[k] * dl;
+                    if (lane < NV) vreg += Y[k * RS + lane] * dl;
                 }
             }
         }
     }
-    wsync();
-    // ---- v += sum_r Y_r lam_r  (transpose through LDS, sequential sum in row order like the oracle)
-    float* T = s.J;    // [NV][64]
-    if (myrow) {
-#pragma unroll
-        for (int t = 0; t < RS; t++)
-            if (t < NV) T[t * 64 + r] = y[t] * lam;
-    }
     s.scratch[lane] = lam;
     wsync();
-    if (lane < NV) {
-        float acc = s.v[lane];
-        for (int k = 0; k < nr; k++) acc += T[lane * 64 + k];
-        s.v[lane] = acc;
-    }
+    if (lane < NV) s.v[lane] = vreg;
     // contact forces (last substep wins, like the oracle)
     if (lane == 0) {
         for (int b = 0; b < MAXB; b++) s.cforce[b][0] = s.cforce[b][1] = s.cforce[b][2] = 0.f;

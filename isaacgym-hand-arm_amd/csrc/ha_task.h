@@ -75,7 +75,7 @@ HD void controller_step(SimCtx& c, const ha_state_t& st, int env) {
         s.scratch[lane] = u;
     } else if (lane < 11) {
         int i = lane - 6;
-        float beta = (float)(1.0 - (double)p.sih_alpha);
+        float beta = p.sih_beta;
         float sm = p.sih_alpha * st.actions[env * NUM_ACT + lane] + beta * st.smoothed[env * 5 + i];
         st.smoothed[env * 5 + i] = sm;
         float sv = st.servo[env * 5 + i] + 100.0f * sm;

@@ -67,7 +67,7 @@ class HaParams(C.Structure):
         ("gravity", arr(f32, 3)), ("friction", f32), ("contact_margin", f32), ("baumgarte", f32),
         ("max_depen_vel", f32), ("object_ang_damping", f32), ("joint_limit_margin", f32),
         ("n_objects", i32), ("num_initial_poses", i32), ("max_episode_length", i32),
-        ("action_dt", f32), ("sih_alpha", f32),
+        ("action_dt", f32), ("sih_alpha", f32), ("sih_beta", f32),
         ("reward_reaching", f32), ("reward_lifting", f32), ("reward_goal", f32), ("reward_success", f32),
         ("lifting_threshold", f32), ("goal_threshold", f32),
         ("goal_pos", arr(f32, 3)), ("goal_noise", arr(f32, 3)), ("reset_pose", arr(f32, MAX_DOFS)),
@@ -280,6 +280,7 @@ def build_params(cfg=None):
         setattr(p, k, c[k])
     p.gravity[:] = c["gravity"]
     p.action_dt = c["dt"]                      # VecTask.dt = sim_params.dt (vec_task.py:267)
+    p.sih_beta = 1.0 - c["sih_alpha"]          # (1 - alpha) * s: python double, cast once (ur5sih.py:496)
     p.goal_pos[:] = c["goal_pos"]
     p.goal_noise[:] = c["goal_noise"]
     p.reset_pose[:len(c["reset_pose"])] = c["reset_pose"]

@@ -497,23 +497,32 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
     float C[HA_MAX_DOFS], rhs[HA_MAX_DOFS];
     fk(h, e);
     dynamics(h, e, M, C);
-    /* implicit PD drives with effort saturation */
-    for (int d = 0; d < D; d++) {
-        float kp = m->dof_kp[d], kd = m->dof_kd[d], eff = m->dof_effort[d];
-        float fpred = kp * (e->tgt[d] - e->q[d] - hdt * e->qd[d]) - kd * e->qd[d];
-        float tau;
-        if (fabsf(fpred) > eff) {
-            tau = fpred > 0 ? eff : -eff;
-        } else {
-            tau = kp * (e->tgt[d] - e->q[d]) - kd * e->qd[d] - hdt * kp * e->qd[d];
-            M[d * D + d] += hdt * kd + hdt * hdt * kp;
-        }
-        rhs[d] = hdt * (tau - C[d]);
-    }
+    /* free motion (velocity-product forces only; drives are constraint rows below) */
+    for (int d = 0; d < D; d++) rhs[d] = -hdt * C[d];
     if (cholesky(M, D) != 0) return;
     chol_solve(M, D, rhs);
     float v[HA_MAX_DOFS + 6 * NOBJ];
     for (int d = 0; d < D; d++) v[d] = e->qd[d] + rhs[d];
+    /* explicit M^-1 (column k = M^-1 e_k; symmetric) for the drive rows */
+    static __thread float Minv[HA_MAX_DOFS][HA_MAX_DOFS];
+    for (int k = 0; k < D; k++) {
+        float x[HA_MAX_DOFS];
+        for (int i = 0; i < D; i++) x[i] = i == k ? 1.0f : 0.0f;
+        chol_solve(M, D, x);
+        for (int i = 0; i < D; i++) Minv[k][i] = x[i];
+    }
+    /* PD position drives as soft, impulse-bounded constraint rows (PhysX articulation drive semantics:
+     * implicit spring-damper  gamma = 1/(h(kd + h kp)), bias = kp/(kd + h kp) (q - q*), |lambda| <= effort h) */
+    float dgam[HA_MAX_DOFS], dbias[HA_MAX_DOFS], dwinv[HA_MAX_DOFS], dlim[HA_MAX_DOFS], dlam[HA_MAX_DOFS];
+    for (int d = 0; d < D; d++) {
+        float kp = m->dof_kp[d], kd = m->dof_kd[d];
+        float den = kd + hdt * kp;
+        dgam[d] = 1.0f / (hdt * den);
+        dbias[d] = kp / den * (e->q[d] - e->tgt[d]);
+        dwinv[d] = 1.0f / (Minv[d][d] + dgam[d]);
+        dlim[d] = m->dof_effort[d] * hdt;
+        dlam[d] = 0.0f;
+    }
     for (int o = 0; o < NO; o++) {
         float damp = 1.0f / (1.0f + hdt * p->object_ang_damping);
         v3 lv = add(e->ov[o], mul(ld3(p->gravity), hdt));
@@ -581,7 +590,19 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
         lam[r] = 0;
         Am[r][r] += 1e-9f;
     }
+    /* projected Gauss-Seidel: drive rows (velocity form, J = e_d) then contact/limit rows (Delassus
+     * form).  v and the contact residuals w are both kept current after every row update. */
     for (int it = 0; it < p->solver_iters; it++) {
+        for (int d = 0; d < D; d++) {
+            float nl = dlam[d] - (v[d] + dbias[d] + dgam[d] * dlam[d]) * dwinv[d];
+            nl = nl < -dlim[d] ? -dlim[d] : (nl > dlim[d] ? dlim[d] : nl);
+            float dl = nl - dlam[d];
+            if (dl != 0.0f) {
+                dlam[d] = nl;
+                for (int k = 0; k < D; k++) v[k] += Minv[d][k] * dl;
+                for (int s = 0; s < nr; s++) w[s] += R.Y[s][d] * dl;
+            }
+        }
         for (int r = 0; r < nr; r++) {
             float lo = R.lo[r], hi = R.hi[r];
             if (R.fric_of[r] >= 0) {
@@ -595,11 +616,10 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
                 lam[r] = nl;
                 /* A is symmetric; Am[r][s] = J_r . M^-1 J_s^T is the entry the GPU lane s holds */
                 for (int s = 0; s < nr; s++) w[s] += Am[r][s] * dl;
+                for (int k = 0; k < NV; k++) v[k] += R.Y[r][k] * dl;
             }
         }
     }
-    for (int r = 0; r < nr; r++)
-        for (int k = 0; k < NV; k++) v[k] += R.Y[r][k] * lam[r];
     /* contact forces per body (net_contact_force): the last substep's forces */
     memset(e->cforce, 0, sizeof(e->cforce));
     for (int c = 0; c < nc; c++) {
@@ -758,7 +778,7 @@ void hao_controller(hao_handle h, ha_state_t* S, int env) {
     float* tgt = S->dof_position_targets + env * h->D;
     const float* dof = S->dof_state + (size_t)env * h->D * 2;
     for (int i = 0; i < 6; i++) ur5[i] = ur5[i] + p->action_dt * a[i];
-    float alpha = p->sih_alpha, beta = (float)(1.0 - (double)p->sih_alpha);
+    float alpha = p->sih_alpha, beta = p->sih_beta;
     for (int i = 0; i < 5; i++) {
         sm[i] = alpha * a[6 + i] + beta * sm[i];
         float s = servo[i] + 100.0f * sm[i];
