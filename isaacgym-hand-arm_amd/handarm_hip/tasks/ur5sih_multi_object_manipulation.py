@@ -13,6 +13,7 @@ There are no host syncs on the step path; reward-term means and success EWMAs (t
 """
 import math
 import random
+import sys
 
 import numpy as np
 import torch
@@ -150,6 +151,7 @@ class Ur5SihMultiObjectManipulation:
         t["sim_targets"].copy_(self.dof_pos)
         self._sync_obs_cache()      # observables' post_step in ConfigurableVecTask.__init__
         self.objects_dropped = False
+        self.max_drop_rounds = int(_get(cfg, "objects.drop.max_rounds", 30))
         self._stat_pending = 0
         self._stat_folded = 0
         self._success_rate_ewma = 0.0
@@ -248,7 +250,17 @@ class Ur5SihMultiObjectManipulation:
             rs[:, 3:, 7:13] = 0.0
             self.sim.simulate(1)
             in_bin = torch.zeros((N, n_obj), dtype=torch.bool, device=self.device)
+            rounds = 0
             while not bool(in_bin.all()):
+                if rounds == self.max_drop_rounds:
+                    # the reference loops until every object lands in the bin extent; cap it so a
+                    # rolling object cannot stall initialisation (remaining objects stay where they are)
+                    print(f"[handarm_hip] drop init: {int((~in_bin).sum())} objects outside the bin extent after "
+                          f"{rounds} rounds; keeping their resting poses", file=sys.stderr, flush=True)
+                    break
+                rounds += 1
+                print(f"[handarm_hip] drop init pose {p}: round {rounds}, {int((~in_bin).sum())} objects to drop",
+                      file=sys.stderr, flush=True)
                 for i in range(n_obj):
                     enabled[:, i] = 1
                     self.sim.set_object_collisions(enabled)
