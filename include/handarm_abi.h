@@ -95,6 +95,7 @@ typedef struct ha_model_t {
     int32_t dof_link[HA_MAX_DOFS];
     int32_t n_mpairs;                           /* (d, e) with e an ancestor-or-self DOF of d */
     int32_t mpair[HA_MAX_MPAIRS][2];
+    float table_half[3];                        /* table box half extents (broad phase) */
 } ha_model_t;
 
 /* Simulation + task parameters (Ur5SihBase.yaml, Ur5SihMultiObject*.yaml). */

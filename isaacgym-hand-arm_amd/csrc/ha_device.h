@@ -111,5 +111,8 @@ HD void wave_argmax(float& v, int& i) {
         if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
     }
 }
-HD float bcast(float x, int src) { return __shfl(x, src, 64); }
-HD int bcast_i(int x, int src) { return __shfl(x, src, 64); }
+// value of lane `src` in every lane; src must be wave-uniform (v_readlane_b32 -> SGPR)
+HD float bcast(float x, int src) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), src));
+}
+HD int bcast_i(int x, int src) { return __builtin_amdgcn_readlane(x, src); }

@@ -425,6 +425,17 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     }
 }
 
+// does a sphere (center c, radius r) reach the table box? Conservative for the hull inside the sphere,
+// so culling with it never removes a contact the narrow phase would produce.
+HD bool sphere_near_table(const ha_model_t& m, PoseF Ptab, f3 c, float r) {
+    qf qi = qf{-Ptab.q.x, -Ptab.q.y, -Ptab.q.z, Ptab.q.w};
+    f3 pl = qrot(qi, c - Ptab.p);
+    float dx = fmaxf(fabsf(pl.x) - m.table_half[0], 0.0f);
+    float dy = fmaxf(fabsf(pl.y) - m.table_half[1], 0.0f);
+    float dz = fmaxf(fabsf(pl.z) - m.table_half[2], 0.0f);
+    return dx * dx + dy * dy + dz * dz <= r * r;
+}
+
 // pair enumeration in the oracle's order (see detect() in physics_oracle.c)
 HD bool pair_desc(const SimCtx& c, int p, int& kind, int& A, int& B) {
     int NO = c.NO, NLH = c.m->n_link_hulls;
@@ -482,6 +493,7 @@ HD void detect(SimCtx& c) {
                         f3 dc = co - cbb;
                         float rr = ro + m.hull_radius[hb] + mg;
                         cand = dot3(dc, dc) <= rr * rr;
+                        if (kind == 1) cand = cand && sphere_near_table(m, Ptab, co, ro + mg);
                     }
                 }
             } else {
@@ -493,6 +505,8 @@ HD void detect(SimCtx& c) {
                     f3 dc = ch - ct;
                     float rr = m.hull_radius[A] + m.hull_radius[m.table_hull] + mg;
                     cand = dot3(dc, dc) <= rr * rr;
+                    // the table's bounding sphere (0.71 m) contains the whole hand: cull on the exact box
+                    cand = cand && sphere_near_table(m, Ptab, ch, m.hull_radius[A] + mg);
                 }
             }
         }

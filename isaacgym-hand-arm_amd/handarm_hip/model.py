@@ -57,7 +57,7 @@ class HaModel(C.Structure):
         ("pool_bbox_quat", arr(f32, MAX_POOL, 4)), ("pool_bbox_ext", arr(f32, MAX_POOL, 3)),
         ("table_hull", i32), ("table_pos", arr(f32, 3)), ("table_quat", arr(f32, 4)),
         ("link_level", arr(i32, MAX_LINKS)), ("max_level", i32), ("dof_link", arr(i32, MAX_DOFS)),
-        ("n_mpairs", i32), ("mpair", arr(i32, MAX_MPAIRS, 2)),
+        ("n_mpairs", i32), ("mpair", arr(i32, MAX_MPAIRS, 2)), ("table_half", arr(f32, 3)),
     ]
 
 
@@ -179,6 +179,7 @@ def build_model(scene, pool_names=None):
     m.table_hull = len(hulls) - 1
     m.table_pos[:] = scene["table"]["pos"]
     m.table_quat[:] = scene["table"]["quat"]
+    m.table_half[:] = scene["table"]["half_extents"]
     # derived topology for the level-synchronous wave kernels
     level = []
     for i, l in enumerate(links):

@@ -256,7 +256,15 @@ class Ur5SihMultiObjectManipulation:
                     # the reference loops until every object lands in the bin extent; cap it so a
                     # rolling object cannot stall initialisation (remaining objects stay where they are)
                     print(f"[handarm_hip] drop init: {int((~in_bin).sum())} objects outside the bin extent after "
-                          f"{rounds} rounds; keeping their resting poses", file=sys.stderr, flush=True)
+                          f"{rounds} rounds; placing them upright above the bin centre", file=sys.stderr, flush=True)
+                    bad = (~in_bin).nonzero(as_tuple=False)
+                    xy = torch.tensor([0.28, 0.53], device=self.device) + 0.1 * (
+                        torch.rand((len(bad), 2), device=self.device) - 0.5)
+                    rs[bad[:, 0], 3 + bad[:, 1], 0:2] = xy
+                    rs[bad[:, 0], 3 + bad[:, 1], 2] = 0.65
+                    rs[bad[:, 0], 3 + bad[:, 1], 3:7] = torch.tensor([0.0, 0.0, 0.0, 1.0], device=self.device)
+                    rs[bad[:, 0], 3 + bad[:, 1], 7:13] = 0.0
+                    self.sim.simulate(self.task_cfg["drop_num_steps"])
                     break
                 rounds += 1
                 print(f"[handarm_hip] drop init pose {p}: round {rounds}, {int((~in_bin).sum())} objects to drop",

@@ -412,6 +412,16 @@ static void collide_ground(const ha_model_t* m, int ha, pose_t PA, float margin,
     emit(out, nout, maxout, pts, seps, nc, V(0, 0, 1), a, -1);
 }
 
+/* sphere (center c, radius r) vs the table box: exact sphere-box overlap test (broad phase) */
+static int near_table(const ha_model_t* m, pose_t Ptab, v3 c, float r) {
+    qt qi = Q(-Ptab.q.x, -Ptab.q.y, -Ptab.q.z, Ptab.q.w);
+    v3 pl = qrot(qi, sub(c, Ptab.p));
+    float dx = fmaxf(fabsf(pl.x) - m->table_half[0], 0.0f);
+    float dy = fmaxf(fabsf(pl.y) - m->table_half[1], 0.0f);
+    float dz = fmaxf(fabsf(pl.z) - m->table_half[2], 0.0f);
+    return dx * dx + dy * dy + dz * dz <= r * r;
+}
+
 static int detect(const hao_handle h, const env_t* e, contact_t* out) {
     const ha_model_t* m = &h->m;
     const ha_params_t* p = &h->p;
@@ -423,7 +433,8 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
         int ho = m->pool_hull[e->pool[o]];
         pose_t Po = {sub(e->oc[o], qrot(e->oq[o], ld3(m->pool_com[e->pool[o]]))), e->oq[o]};
         collide_ground(m, ho, Po, mg, o, out, &nout, MAXC);
-        collide_hulls(m, ho, Po, m->table_hull, Ptab, mg, o, -1, out, &nout, MAXC);
+        if (near_table(m, Ptab, add(Po.p, qrot(Po.q, ld3(m->hull_center[ho]))), m->hull_radius[ho] + mg))
+            collide_hulls(m, ho, Po, m->table_hull, Ptab, mg, o, -1, out, &nout, MAXC);
         for (int o2 = o + 1; o2 < h->NO; o2++) {
             if (!e->coll[o2]) continue;
             int h2 = m->pool_hull[e->pool[o2]];
@@ -440,7 +451,8 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
         int L = m->hull_link[k];
         if (!m->link_table_collide[L]) continue;
         pose_t PL = {e->lp[L], e->lq[L]};
-        collide_hulls(m, k, PL, m->table_hull, Ptab, mg, 100 + L, -1, out, &nout, MAXC);
+        if (near_table(m, Ptab, add(PL.p, qrot(PL.q, ld3(m->hull_center[k]))), m->hull_radius[k] + mg))
+            collide_hulls(m, k, PL, m->table_hull, Ptab, mg, 100 + L, -1, out, &nout, MAXC);
     }
     return nout;
 }

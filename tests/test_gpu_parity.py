@@ -264,7 +264,9 @@ def test_vectask_episode_at_full_shard_size():
             torch.cuda.synchronize()
             assert torch.isfinite(obs_dict["obs"]).all() and torch.isfinite(rew).all()
             z = env.root_pos[:, 3:, 2]
-            assert (z > 0.3).all() and (z < 2.0).all()
+            assert (z > -0.01).all() and (z < 2.0).all()       # above the ground plane (random actions may
+            if step == 1:                                      # sweep objects off the table later on)
+                assert (z > 0.5).float().mean() > 0.99         # after the drop init they rest on the table
         if step == 199:
             assert (reset == 0).all()
         if step == 200:                 # done mask is exact: every env hits max_episode_length together
