@@ -563,14 +563,34 @@ HD void tangents(f3 n, f3& t1, f3& t2) {
     t2 = cross3(n, t1);
 }
 
+// Diagnostic phase timers (built only into libhandarm_hip_prof.so, -DHA_PROFILE): lane 0 of every
+// wave adds the s_memtime delta of each phase; read back with ha_profile_read().
+#ifdef HA_PROFILE
+__device__ unsigned long long g_prof[16];
+#define PROF_BEGIN() unsigned long long _pt = __builtin_amdgcn_s_memtime();
+#define PROF(i)                                                        \
+    do {                                                               \
+        wsync();                                                       \
+        unsigned long long _n = __builtin_amdgcn_s_memtime();          \
+        if (c.lane == 0) atomicAdd(&g_prof[i], _n - _pt);              \
+        _pt = _n;                                                      \
+    } while (0)
+#else
+#define PROF_BEGIN()
+#define PROF(i)
+#endif
+
 HD void substep(SimCtx& c, float hdt) {
+    PROF_BEGIN();
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     const ha_params_t& p = *c.p;
     int lane = c.lane, D = c.D, NO = c.NO;
     int NV = D + 6 * NO;
     fk(c);
+    PROF(0);
     dynamics(c);
+    PROF(1);
     // free motion: velocity-product forces only (drives are constraint rows of the PGS below)
     if (lane < D) s.rhs[lane] = -hdt * s.Cb[lane];
     wsync();
@@ -609,7 +629,9 @@ HD void substep(SimCtx& c, float hdt) {
         s.om[o] = m.pool_mass[s.pool[o]];
     }
     wsync();
+    PROF(2);
     detect(c);
+    PROF(3);
     // ---- rows: lane r owns row r
     int nc = s.nc;
     int ncrow = 3 * nc;    // nc <= MAXC = 21 -> <= 63 rows
@@ -676,6 +698,7 @@ HD void substep(SimCtx& c, float hdt) {
         s.vt[r] = vt; s.lo[r] = lo; s.hi[r] = hi; s.fric_of[r] = fric_of; s.rcontact[r] = rcont;
     }
     wsync();
+    PROF(4);
     // ---- Y_r = M^-1 J_r^T (registers) and the Delassus column A[:, r]
     float y[RS];
 #pragma unroll
@@ -746,6 +769,7 @@ HD void substep(SimCtx& c, float hdt) {
         for (int t = 0; t < RS; t++) Jr[t] = y[t];
     }
     wsync();
+    PROF(5);
     // ---- projected Gauss-Seidel: drive rows in velocity form (J = e_d, residual = v[d]),
     //      contact/limit rows in Delassus form (row r's residual / impulse live in lane r)
     const float mu = p.friction;
@@ -790,6 +814,7 @@ HD void substep(SimCtx& c, float hdt) {
     s.scratch[lane] = lam;
     wsync();
     if (lane < NV) s.v[lane] = vreg;
+    PROF(6);
     // contact forces (last substep wins, like the oracle)
     if (lane == 0) {
         for (int b = 0; b < MAXB; b++) s.cforce[b][0] = s.cforce[b][1] = s.cforce[b][2] = 0.f;
@@ -832,4 +857,5 @@ HD void substep(SimCtx& c, float hdt) {
                                    q.w + 0.5f * hdt * dq.w}));
     }
     wsync();
+    PROF(7);
 }
