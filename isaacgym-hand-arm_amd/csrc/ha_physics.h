@@ -2,19 +2,23 @@
 //
 // Algorithm (identical to oracle/physics_oracle.c, which is its scalar restatement):
 //   FK (level-synchronous over the link tree) -> CRBA joint-space inertia + RNEA velocity-product
-//   forces in world-frame spatial algebra -> implicit PD drives (effort-saturating) folded into the
-//   inertia -> Cholesky (lane i owns row i) -> convex-hull contacts (SAT + incident vertices, <= 4 per
-//   pair) -> one constraint row per lane: lane r builds J_r, solves Y_r = M^-1 J_r^T in registers and
-//   the column A[:, r] of the Delassus matrix J M^-1 J^T -> projected Gauss-Seidel sweeps where the
-//   residual w = A lambda + b lives one element per lane (no cross-lane reductions in the sweep) ->
-//   velocity update through an LDS transpose -> symplectic Euler.
+//   forces in world-frame spatial algebra -> Cholesky (lane i owns row i) -> triangular inverse
+//   (lane j owns column j) -> explicit M^-1 = L^-T L^-1 -> convex-hull contacts (SAT + incident vertices,
+//   <= 4 per pair) -> projected Gauss-Seidel in velocity form:
+//     * joint rows (PD drives as impulse-bounded soft constraints, joint limits) live in lane d and need
+//       no reduction (J = +-e_d, J v = v[d]);
+//     * contact rows (normal + 2 friction) keep J_r and Y_r = M^-1 J_r^T in LDS; J_r . v is one DPP
+//       row reduction + 4 v_readlane; the velocity update is one LDS read + FMA per lane.
+//   Generalised velocity v lives one coordinate per lane for the whole solve -> symplectic Euler.
+// Everything loops at run time (small code: the kernel must stay resident in the instruction cache),
+// and the phase-local scratch (dynamics, collision, rows) shares one LDS union.
 #pragma once
 #include "ha_device.h"
 #include "../../include/handarm_abi.h"
 
 #define MAXC 21
-#define MAXR 64
-#define RS 40
+#define MAXR (3 * MAXC)
+#define RS 36            /* row stride: D + 6 * n_obj <= 36 */
 #define NOBJ HA_MAX_OBJ
 #define MAXD 24
 #define MAXB (1 + HA_MAX_LINKS + 1 + NOBJ)
@@ -29,26 +33,38 @@ struct ObsIn {
     float pad[2];
 };
 
+struct DynScratch {
+    float Ic[HA_MAX_LINKS][13];                 // composite spatial inertia (m, h, J) at world origin
+    float Vl[HA_MAX_LINKS][6], Al[HA_MAX_LINKS][6], Fl[HA_MAX_LINKS][6];
+};
+struct ColScratch {
+    float wvA[64][4], wvB[64][4], wpR[128][4];
+};
+struct RowScratch {
+    float J[MAXR * RS];
+    float Y[MAXR * RS];
+};
+
 struct EnvLDS {
     ObsIn in;
     float q[MAXD], qd[MAXD], tgt[MAXD];
     float lp[HA_MAX_LINKS][4], lq[HA_MAX_LINKS][4];
     float ax[MAXD][4], an[MAXD][4];
-    float Ic[HA_MAX_LINKS][13];                 // composite spatial inertia (m, h, J) at world origin
-    float Vl[HA_MAX_LINKS][6], Al[HA_MAX_LINKS][6], Fl[HA_MAX_LINKS][6];
-    float M[MAXD * MAXD];
-    float Minv[MAXD * MAXD];
-    float Cb[MAXD], rhs[MAXD];
+    float M[MAXD * MAXD];                       // M, then its Cholesky factor L (stride D)
+    float Minv[MAXD * MAXD];                    // stride D
+    float Cb[MAXD];
     float v[RS];
     float oc[NOBJ][4], oq[NOBJ][4], ov[NOBJ][4], ow[NOBJ][4], oIinv[NOBJ][12], om[NOBJ];
     int pool[NOBJ], coll[NOBJ];
     float cx[MAXC][4], cn[MAXC][4], csep[MAXC];
     int ca[MAXC], cb[MAXC];
     int nc, nr, pad0, pad1;
-    float wvA[64][4], wvB[64][4], wpR[128][4];
-    float J[MAXR * RS];                         // rows; reused as the [NV][64] transpose after the solve
-    float vt[MAXR], lo[MAXR], hi[MAXR];
-    int fric_of[MAXR], rcontact[MAXR];
+    union {
+        DynScratch dyn;
+        float Linv[MAXD * MAXD];
+        ColScratch col;
+        RowScratch rows;
+    } u;
     float cforce[MAXB][3];
     float obs[160];
     float scratch[64];
@@ -60,6 +76,17 @@ struct SimCtx {
     EnvLDS* s;
     int lane, D, NO, L;
 };
+
+// 64-lane sum: DPP butterfly inside each 16-lane row (xor1, xor2, half-mirror, mirror), then the four
+// row sums via v_readlane. Every lane gets the same bits; the oracle emulates this exact tree.
+HD float wave_sum_rows(float x) {
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));   // quad_perm 1,0,3,2
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, true));  // row_half_mirror
+    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xF, 0xF, true));  // row_mirror
+    float r0 = bcast(x, 0), r1 = bcast(x, 16), r2 = bcast(x, 32), r3 = bcast(x, 48);
+    return (r0 + r1) + (r2 + r3);
+}
 
 // ----------------------------------------------------------------------------- kinematics
 HD void fk(SimCtx& c) {
@@ -125,13 +152,13 @@ HD void dynamics(SimCtx& c) {
         for (int a = 0; a < 3; a++)
 #pragma unroll
             for (int b = 0; b < 3; b++) I.J[a * 3 + b] = Iw[a * 3 + b] + mm * ((a == b ? ccd : 0.0f) - cv[a] * cv[b]);
-        float* ic = s.Ic[i];
+        float* ic = s.u.dyn.Ic[i];
         ic[0] = I.m; ic[1] = I.h.x; ic[2] = I.h.y; ic[3] = I.h.z;
 #pragma unroll
         for (int k = 0; k < 9; k++) ic[4 + k] = I.J[k];
         if (i == 0) {
 #pragma unroll
-            for (int k = 0; k < 6; k++) { s.Vl[0][k] = 0.f; s.Al[0][k] = 0.f; }
+            for (int k = 0; k < 6; k++) { s.u.dyn.Vl[0][k] = 0.f; s.u.dyn.Al[0][k] = 0.f; }
         }
     }
     // zero M
@@ -141,8 +168,8 @@ HD void dynamics(SimCtx& c) {
     for (int lev = 1; lev <= m.max_level; lev++) {
         if (own && m.link_level[lane] == lev) {
             int i = lane, par = m.link_parent[i], d = m.link_dof[i];
-            f3 vw = ld3(&s.Vl[par][0]), vv = ld3(&s.Vl[par][3]);
-            f3 aw = ld3(&s.Al[par][0]), av = ld3(&s.Al[par][3]);
+            f3 vw = ld3(&s.u.dyn.Vl[par][0]), vv = ld3(&s.u.dyn.Vl[par][3]);
+            f3 aw = ld3(&s.u.dyn.Al[par][0]), av = ld3(&s.u.dyn.Al[par][3]);
             if (d >= 0) {
                 f3 axd = ld3(s.ax[d]), and_ = ld3(s.an[d]);
                 float qd = s.qd[d];
@@ -152,21 +179,21 @@ HD void dynamics(SimCtx& c) {
                 aw = aw + cross3(vw, sw);
                 av = av + (cross3(vw, sv) + cross3(vv, sw));
             }
-            st3(&s.Vl[i][0], vw); st3(&s.Vl[i][3], vv);
-            st3(&s.Al[i][0], aw); st3(&s.Al[i][3], av);
+            st3(&s.u.dyn.Vl[i][0], vw); st3(&s.u.dyn.Vl[i][3], vv);
+            st3(&s.u.dyn.Al[i][0], aw); st3(&s.u.dyn.Al[i][3], av);
         }
         wsync();
     }
     if (own) {
         int i = lane;
-        f3 vw = ld3(&s.Vl[i][0]), vv = ld3(&s.Vl[i][3]);
-        f3 aw = ld3(&s.Al[i][0]), av = ld3(&s.Al[i][3]);
+        f3 vw = ld3(&s.u.dyn.Vl[i][0]), vv = ld3(&s.u.dyn.Vl[i][3]);
+        f3 aw = ld3(&s.u.dyn.Al[i][0]), av = ld3(&s.u.dyn.Al[i][3]);
         f3 n1, f1, n2, f2;
         inert_apply(I, aw, av, n1, f1);
         inert_apply(I, vw, vv, n2, f2);
         f3 fn = n1 + (cross3(vw, n2) + cross3(vv, f2));
         f3 ff = f1 + cross3(vw, f2);
-        st3(&s.Fl[i][0], fn); st3(&s.Fl[i][3], ff);
+        st3(&s.u.dyn.Fl[i][0], fn); st3(&s.u.dyn.Fl[i][3], ff);
     }
     wsync();
     // backward accumulation of forces and composite inertia, deepest level first
@@ -174,23 +201,23 @@ HD void dynamics(SimCtx& c) {
         if (own && m.link_level[lane] == lev) {
             int i = lane, par = m.link_parent[i];
 #pragma unroll
-            for (int k = 0; k < 6; k++) atomicAdd(&s.Fl[par][k], s.Fl[i][k]);
+            for (int k = 0; k < 6; k++) atomicAdd(&s.u.dyn.Fl[par][k], s.u.dyn.Fl[i][k]);
 #pragma unroll
-            for (int k = 0; k < 13; k++) atomicAdd(&s.Ic[par][k], s.Ic[i][k]);
+            for (int k = 0; k < 13; k++) atomicAdd(&s.u.dyn.Ic[par][k], s.u.dyn.Ic[i][k]);
         }
         wsync();
     }
     if (lane < D) {
         int i = m.dof_link[lane];
         f3 axd = ld3(s.ax[lane]), and_ = ld3(s.an[lane]);
-        s.Cb[lane] = dot3(axd, ld3(&s.Fl[i][0])) + dot3(cross3(and_, axd), ld3(&s.Fl[i][3]));
+        s.Cb[lane] = dot3(axd, ld3(&s.u.dyn.Fl[i][0])) + dot3(cross3(and_, axd), ld3(&s.u.dyn.Fl[i][3]));
     }
     for (int k = lane; k < m.n_mpairs; k += 64) {
         int d = m.mpair[k][0], e = m.mpair[k][1];
         int i = m.dof_link[d];
         f3 axd = ld3(s.ax[d]), and_ = ld3(s.an[d]);
         f3 n, f;
-        inert_apply_lds(s.Ic[i], axd, cross3(and_, axd), n, f);
+        inert_apply_lds(s.u.dyn.Ic[i], axd, cross3(and_, axd), n, f);
         f3 axe = ld3(s.ax[e]), ane = ld3(s.an[e]);
         float val = dot3(axe, n) + dot3(cross3(ane, axe), f);
         s.M[d * D + e] = val;
@@ -199,7 +226,8 @@ HD void dynamics(SimCtx& c) {
     wsync();
 }
 
-// in-place Cholesky of s.M (lower triangle), same operation order as the oracle (left-looking)
+
+// in-place Cholesky of s.M (lower triangle, stride D), left-looking like the oracle
 HD void cholesky(SimCtx& c) {
     EnvLDS& s = *c.s;
     int lane = c.lane, D = c.D;
@@ -220,29 +248,32 @@ HD void cholesky(SimCtx& c) {
     }
 }
 
-// x (registers, MAXD) <- M^-1 x using the factor in s.M
-HD void chol_solve_regs(const SimCtx& c, float (&x)[MAXD]) {
-    const float* Lm = c.s->M;
-    int D = c.D;
-#pragma unroll
-    for (int i = 0; i < MAXD; i++) {
-        if (i < D) {
-            float t = x[i];
-#pragma unroll
-            for (int k = 0; k < i; k++) t -= Lm[i * D + k] * x[k];
-            x[i] = t / Lm[i * D + i];
+// M^-1 = L^-T L^-1: lane j builds column j of L^-1 (forward substitution), lane i then row i of M^-1
+HD void inverse_from_cholesky(SimCtx& c) {
+    EnvLDS& s = *c.s;
+    int lane = c.lane, D = c.D;
+    const float* Lm = s.M;
+    float* Li = s.u.Linv;
+    if (lane < D) {
+        int j = lane;
+        Li[j * D + j] = 1.0f / Lm[j * D + j];
+        for (int i = j + 1; i < D; i++) {
+            float t = 0.0f;
+            for (int k = j; k < i; k++) t += Lm[i * D + k] * Li[k * D + j];
+            Li[i * D + j] = -t / Lm[i * D + i];
         }
     }
-#pragma unroll
-    for (int i = MAXD - 1; i >= 0; i--) {
-        if (i < D) {
-            float t = x[i];
-#pragma unroll
-            for (int k = i + 1; k < MAXD; k++)
-                if (k < D) t -= Lm[k * D + i] * x[k];
-            x[i] = t / Lm[i * D + i];
+    wsync();
+    if (lane < D) {
+        int i = lane;
+        for (int j = 0; j <= i; j++) {
+            float t = 0.0f;
+            for (int k = i; k < D; k++) t += Li[k * D + i] * Li[k * D + j];
+            s.Minv[i * D + j] = t;
+            s.Minv[j * D + i] = t;
         }
     }
+    wsync();
 }
 
 // ----------------------------------------------------------------------------- collision
@@ -354,8 +385,8 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     if (dot3(dc, dc) > rr * rr) return;
     int nva = m.hull_nverts[ha], nvb = m.hull_nverts[hb];
     int npa = m.hull_nplanes[ha], npb = m.hull_nplanes[hb];
-    if (lane < nva) st3(s.wvA[lane], PA.p + qrot(PA.q, ld3(m.verts[m.hull_vert_start[ha] + lane])));
-    if (lane < nvb) st3(s.wvB[lane], PB.p + qrot(PB.q, ld3(m.verts[m.hull_vert_start[hb] + lane])));
+    if (lane < nva) st3(s.u.col.wvA[lane], PA.p + qrot(PA.q, ld3(m.verts[m.hull_vert_start[ha] + lane])));
+    if (lane < nvb) st3(s.u.col.wvB[lane], PB.p + qrot(PB.q, ld3(m.verts[m.hull_vert_start[hb] + lane])));
     wsync();
     // SAT over the face normals of A (planes k = lane, lane + 64)
     float best = -3.0e38f;
@@ -364,7 +395,8 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         f3 n; float d;
         world_plane(m, ha, k, PA, n, d);
         float mn = 3.0e38f;
-        for (int i = 0; i < nvb; i++) mn = fminf(mn, dot3(n, ld3(s.wvB[i])) + d);
+#pragma unroll 2
+        for (int i = 0; i < nvb; i++) mn = fminf(mn, dot3(n, ld3(s.u.col.wvB[i])) + d);
         if (mn > best) { best = mn; bestk = k; }
     }
     wave_argmax(best, bestk);
@@ -377,7 +409,8 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         f3 n; float d;
         world_plane(m, hb, k, PB, n, d);
         float mn = 3.0e38f;
-        for (int i = 0; i < nva; i++) mn = fminf(mn, dot3(n, ld3(s.wvA[i])) + d);
+#pragma unroll 2
+        for (int i = 0; i < nva; i++) mn = fminf(mn, dot3(n, ld3(s.u.col.wvA[i])) + d);
         if (mn > best) { best = mn; bestk = k; }
     }
     wave_argmax(best, bestk);
@@ -393,23 +426,23 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         for (int k = lane; k < npr; k += 64) {
             f3 n; float d;
             world_plane(m, hr, k, Pr, n, d);
-            st3(s.wpR[k], n);
-            s.wpR[k][3] = d;
+            st3(s.u.col.wpR[k], n);
+            s.u.col.wpR[k][3] = d;
         }
         wsync();
-        f3 nref = ld3(s.wpR[kr]);
-        float dref = s.wpR[kr][3];
+        f3 nref = ld3(s.u.col.wpR[kr]);
+        float dref = s.u.col.wpR[kr][3];
         bool valid = false;
         f3 pt = mk3(0, 0, 0);
         float dist = 0;
         if (lane < nvi) {
-            f3 vi = ld3(refB ? s.wvA[lane] : s.wvB[lane]);
+            f3 vi = ld3(refB ? s.u.col.wvA[lane] : s.u.col.wvB[lane]);
             dist = dot3(nref, vi) + dref;
             if (dist <= mg) {
                 float mx = -3.0e38f;
                 for (int k = 0; k < npr; k++) {
                     if (k == kr) continue;
-                    mx = fmaxf(mx, dot3(ld3(s.wpR[k]), vi) + s.wpR[k][3]);
+                    mx = fmaxf(mx, dot3(ld3(s.u.col.wpR[k]), vi) + s.u.col.wpR[k][3]);
                 }
                 if (mx <= mg) {
                     valid = true;
@@ -516,20 +549,27 @@ HD void detect(SimCtx& c) {
             mask &= mask - 1;
             int q = base + bit;
             pair_desc(c, q, kind, A, B);
+            // one call site per narrow phase (keeps a single inlined copy: code size / VGPRs)
+            if (kind == 0) {
+                collide_ground(c, m.pool_hull[s.pool[A]], object_pose(c, A), A);
+                continue;
+            }
+            int h1, h2, b1, b2;
+            PoseF P1, P2;
             if (kind <= 3) {
                 int ho = m.pool_hull[s.pool[A]];
                 PoseF Po = object_pose(c, A);
-                if (kind == 0) collide_ground(c, ho, Po, A);
-                else if (kind == 1) collide_hulls(c, ho, Po, m.table_hull, Ptab, A, -1);
-                else if (kind == 2) collide_hulls(c, ho, Po, m.pool_hull[s.pool[B]], object_pose(c, B), A, B);
+                if (kind == 1) { h1 = ho; P1 = Po; b1 = A; h2 = m.table_hull; P2 = Ptab; b2 = -1; }
+                else if (kind == 2) { h1 = ho; P1 = Po; b1 = A; h2 = m.pool_hull[s.pool[B]]; P2 = object_pose(c, B); b2 = B; }
                 else {
                     int Lk = m.hull_link[B];
-                    collide_hulls(c, B, PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}, ho, Po, 100 + Lk, A);
+                    h1 = B; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = ho; P2 = Po; b2 = A;
                 }
             } else {
                 int Lk = m.hull_link[A];
-                collide_hulls(c, A, PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}, m.table_hull, Ptab, 100 + Lk, -1);
+                h1 = A; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = m.table_hull; P2 = Ptab; b2 = -1;
             }
+            collide_hulls(c, h1, P1, h2, P2, b1, b2);
         }
     }
     wsync();
@@ -563,6 +603,7 @@ HD void tangents(f3 n, f3& t1, f3& t2) {
     t2 = cross3(n, t1);
 }
 
+
 // Diagnostic phase timers (built only into libhandarm_hip_prof.so, -DHA_PROFILE): lane 0 of every
 // wave adds the s_memtime delta of each phase; read back with ha_profile_read().
 #ifdef HA_PROFILE
@@ -591,27 +632,13 @@ HD void substep(SimCtx& c, float hdt) {
     PROF(0);
     dynamics(c);
     PROF(1);
-    // free motion: velocity-product forces only (drives are constraint rows of the PGS below)
-    if (lane < D) s.rhs[lane] = -hdt * s.Cb[lane];
-    wsync();
     cholesky(c);
-    {
-        float x[MAXD];
-#pragma unroll
-        for (int i = 0; i < MAXD; i++) x[i] = i < D ? s.rhs[i] : 0.0f;
-        chol_solve_regs(c, x);
-#pragma unroll
-        for (int i = 0; i < MAXD; i++)
-            if (i < D && lane == i) s.v[i] = s.qd[i] + x[i];
-        // explicit M^-1: lane k solves M x = e_k; row k of Minv = column k (symmetric)
-#pragma unroll
-        for (int i = 0; i < MAXD; i++) x[i] = (i == lane) ? 1.0f : 0.0f;
-        chol_solve_regs(c, x);
-        if (lane < D) {
-#pragma unroll
-            for (int i = 0; i < MAXD; i++)
-                if (i < D) s.Minv[lane * MAXD + i] = x[i];
-        }
+    inverse_from_cholesky(c);
+    // free motion: velocity-product forces only (drives are constraint rows of the PGS below)
+    if (lane < D) {
+        float acc = 0.0f;
+        for (int j = 0; j < D; j++) acc += s.Minv[lane * D + j] * (-hdt * s.Cb[j]);
+        s.v[lane] = s.qd[lane] + acc;
     }
     if (lane < NO) {
         int o = lane;
@@ -632,15 +659,15 @@ HD void substep(SimCtx& c, float hdt) {
     PROF(2);
     detect(c);
     PROF(3);
-    // ---- rows: lane r owns row r
+    // ---- contact rows: lane r owns row r (normal, friction 1, friction 2 of contact r / 3)
     int nc = s.nc;
-    int ncrow = 3 * nc;    // nc <= MAXC = 21 -> <= 63 rows
+    int nr = 3 * nc;    // nc <= MAXC -> <= MAXR rows
     int r = lane;
-    float* Jr = s.J + r * RS;
-    for (int k = 0; k < RS; k++) Jr[k] = 0.0f;
-    float vt = 0.f, lo = 0.f, hi = 0.f;
-    int fric_of = -1, rcont = -1;
-    if (r < ncrow) {
+    float vt = 0.f, lo = 0.f, hi = 0.f, winv = 0.f, lam = 0.f;
+    int fric_of = -1;
+    if (r < nr) {
+        float* Jr = s.u.rows.J + r * RS;
+        for (int k = 0; k < RS; k++) Jr[k] = 0.0f;
         int ci = r / 3, k = r % 3;
         f3 n = ld3(s.cn[ci]), t1, t2;
         tangents(n, t1, t2);
@@ -648,7 +675,6 @@ HD void substep(SimCtx& c, float hdt) {
         f3 x = ld3(s.cx[ci]);
         jac_body(c, s.ca[ci], x, dir, 1.0f, Jr);
         jac_body(c, s.cb[ci], x, dir, -1.0f, Jr);
-        rcont = ci;
         if (k == 0) {
             float sp = s.csep[ci];
             vt = sp > 0 ? -sp / hdt : -p.baumgarte * sp / hdt;
@@ -657,157 +683,104 @@ HD void substep(SimCtx& c, float hdt) {
         } else {
             fric_of = r - k;
         }
-    }
-    // joint-limit rows, compacted after the contact rows in (dof, lower/upper) order
-    bool lim_lo = false, lim_up = false;
-    float s_lo = 0, s_up = 0;
-    if (lane < D) {
-        s_lo = s.q[lane] - m.dof_lower[lane];
-        s_up = m.dof_upper[lane] - s.q[lane];
-        lim_lo = s_lo <= p.joint_limit_margin;
-        lim_up = s_up <= p.joint_limit_margin;
-    }
-    int cnt = (int)lim_lo + (int)lim_up;
-    // exclusive prefix sum over lanes
-    int incl = cnt;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        int t = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += t;
-    }
-    int excl = incl - cnt;
-    int nlim = bcast_i(incl, 63);
-    int nr = ncrow + nlim;
-    if (nr > MAXR) nr = MAXR;
-    wsync();
-    for (int side = 0; side < 2; side++) {
-        bool act = side == 0 ? lim_lo : lim_up;
-        int rr = ncrow + excl + (side == 1 && lim_lo ? 1 : 0);
-        if (act && rr < MAXR) {
-            float* Jl = s.J + rr * RS;
-            Jl[lane] = side == 0 ? 1.0f : -1.0f;
-            float sp = side == 0 ? s_lo : s_up;
-            s.vt[rr] = sp > 0 ? -sp / hdt : -p.baumgarte * sp / hdt;
-            s.lo[rr] = 0.f;
-            s.hi[rr] = 3.0e38f;
-            s.fric_of[rr] = -1;
-            s.rcontact[rr] = -1;
+        // Y_r = M^-1 J_r^T (robot block through the explicit inverse, object blocks 1/m, I_w^-1)
+        float* Yr = s.u.rows.Y + r * RS;
+        for (int i = 0; i < D; i++) {
+            float acc = 0.0f;
+            for (int j = 0; j < D; j++) acc += s.Minv[i * D + j] * Jr[j];
+            Yr[i] = acc;
         }
+        for (int o = 0; o < NO; o++) {
+            const float* Jo = Jr + D + 6 * o;
+            float* Yo = Yr + D + 6 * o;
+            float im = 1.0f / s.om[o];
+            Yo[0] = Jo[0] * im; Yo[1] = Jo[1] * im; Yo[2] = Jo[2] * im;
+            f3 a = mv3(s.oIinv[o], mk3(Jo[3], Jo[4], Jo[5]));
+            Yo[3] = a.x; Yo[4] = a.y; Yo[5] = a.z;
+        }
+        for (int t = NV; t < RS; t++) Yr[t] = 0.0f;
+        float a = 0.0f;
+        for (int t = 0; t < NV; t++) a += Jr[t] * Yr[t];
+        winv = 1.0f / (a + 1e-9f);
     }
-    if (r < ncrow) {
-        s.vt[r] = vt; s.lo[r] = lo; s.hi[r] = hi; s.fric_of[r] = fric_of; s.rcontact[r] = rcont;
-    }
-    wsync();
     PROF(4);
-    // ---- Y_r = M^-1 J_r^T (registers) and the Delassus column A[:, r]
-    float y[RS];
-#pragma unroll
-    for (int k = 0; k < RS; k++) y[k] = 0.0f;
-    bool myrow = r < nr;
-    if (myrow) {
-        float x[MAXD];
-#pragma unroll
-        for (int i = 0; i < MAXD; i++) x[i] = i < D ? Jr[i] : 0.0f;
-        chol_solve_regs(c, x);
-#pragma unroll
-        for (int i = 0; i < MAXD; i++)
-            if (i < D) y[i] = x[i];
-        // object blocks: (J_lin / m, I_world^-1 J_ang)
-#pragma unroll
-        for (int t = 0; t < RS; t++) {
-            if (t >= D && t < NV) {
-                int o = (t - D) / 6, k = (t - D) - 6 * o;
-                const float* Jo = Jr + D + 6 * o;
-                if (k < 3) {
-                    y[t] = Jo[k] * (1.0f / s.om[o]);
-                } else {
-                    const float* Ir = s.oIinv[o] + 3 * (k - 3);
-                    y[t] = Ir[0] * Jo[3] + Ir[1] * Jo[4] + Ir[2] * Jo[5];
-                }
-            }
-        }
-    }
-    float A[MAXR];
-    float w = 0.f, lam = 0.f, rinv = 0.f;
-#pragma unroll
-    for (int k = 0; k < MAXR; k++) {
-        A[k] = 0.f;
-        if (k < nr && myrow) {
-            const float* Jk = s.J + k * RS;
-            float a = 0.f;
-#pragma unroll
-            for (int t = 0; t < RS; t++)
-                if (t < NV) a += Jk[t] * y[t];
-            A[k] = a;
-        }
-    }
-    if (myrow) {
-        float b = 0.f;
-        for (int t = 0; t < NV; t++) b += Jr[t] * s.v[t];
-        w = b - s.vt[r];
-#pragma unroll
-        for (int k = 0; k < MAXR; k++)
-            if (k == r) { A[k] += 1e-9f; rinv = A[k]; }
-        lo = s.lo[r]; hi = s.hi[r]; fric_of = s.fric_of[r];
-    }
-    // generalized velocity: lane k owns v[k]
-    float vreg = lane < NV ? s.v[lane] : 0.0f;
-    // PD drive rows (lane d): soft implicit spring-damper, impulse bounded by effort * h
+    // ---- joint rows, lane d: PD drive (soft implicit spring-damper, |impulse| <= effort h) and the
+    //      lower/upper joint limits (hard, unilateral)
     float dgam = 0.f, dbias = 0.f, dwinv = 0.f, dlim = 0.f, dlam = 0.f;
+    float lwinv = 0.f, vt_lo = 0.f, vt_up = 0.f, lam_lo = 0.f, lam_up = 0.f;
+    int act_lo = 0, act_up = 0;
     if (lane < D) {
         float kp = m.dof_kp[lane], kd = m.dof_kd[lane];
         float den = kd + hdt * kp;
+        float mii = s.Minv[lane * D + lane];
         dgam = 1.0f / (hdt * den);
         dbias = kp / den * (s.q[lane] - s.tgt[lane]);
-        dwinv = 1.0f / (s.Minv[lane * MAXD + lane] + dgam);
+        dwinv = 1.0f / (mii + dgam);
         dlim = m.dof_effort[lane] * hdt;
+        lwinv = 1.0f / (mii + 1e-9f);
+        float s_lo = s.q[lane] - m.dof_lower[lane], s_up = m.dof_upper[lane] - s.q[lane];
+        act_lo = s_lo <= p.joint_limit_margin;
+        act_up = s_up <= p.joint_limit_margin;
+        vt_lo = s_lo > 0 ? -s_lo / hdt : -p.baumgarte * s_lo / hdt;
+        vt_up = s_up > 0 ? -s_up / hdt : -p.baumgarte * s_up / hdt;
     }
-    wsync();
-    // Y rows replace J rows in LDS (J is no longer needed): lane k reads Y[r][k] in the sweep
-    if (myrow) {
-#pragma unroll
-        for (int t = 0; t < RS; t++) Jr[t] = y[t];
-    }
+    float vreg = lane < NV ? s.v[lane] : 0.0f;
     wsync();
     PROF(5);
-    // ---- projected Gauss-Seidel: drive rows in velocity form (J = e_d, residual = v[d]),
-    //      contact/limit rows in Delassus form (row r's residual / impulse live in lane r)
+    // ---- projected Gauss-Seidel (velocity form): joint rows d = 0..D-1 (drive, lower, upper), then
+    //      contact rows r = 0..nr-1.  Same row order and arithmetic as the oracle.
     const float mu = p.friction;
-    const float* Y = s.J;
+    const float* J = s.u.rows.J;
+    const float* Y = s.u.rows.Y;
     for (int it = 0; it < p.solver_iters; it++) {
-#pragma unroll
-        for (int d = 0; d < MAXD; d++) {
-            if (d < D) {
-                float vd = bcast(vreg, d), ld = bcast(dlam, d);
-                float nl = ld - (vd + bcast(dbias, d) + bcast(dgam, d) * ld) * bcast(dwinv, d);
-                float lim = bcast(dlim, d);
-                nl = nl < -lim ? -lim : (nl > lim ? lim : nl);
-                float dl = nl - ld;
-                if (dl != 0.0f) {
-                    if (lane == d) dlam = nl;
-                    if (lane < D) vreg += s.Minv[d * MAXD + lane] * dl;
-                    w += y[d] * dl;
+        for (int d = 0; d < D; d++) {
+            float mrow = lane < D ? s.Minv[d * D + lane] : 0.0f;
+            float vd = bcast(vreg, d), ld = bcast(dlam, d);
+            float nl = ld - (vd + bcast(dbias, d) + bcast(dgam, d) * ld) * bcast(dwinv, d);
+            float lim = bcast(dlim, d);
+            nl = nl < -lim ? -lim : (nl > lim ? lim : nl);
+            float dl = nl - ld;
+            if (dl != 0.0f) {
+                if (lane == d) dlam = nl;
+                vreg += mrow * dl;
+            }
+            if (bcast_i(act_lo, d)) {
+                float l0 = bcast(lam_lo, d);
+                float n0 = l0 - (bcast(vreg, d) - bcast(vt_lo, d)) * bcast(lwinv, d);
+                n0 = n0 < 0.0f ? 0.0f : n0;
+                float d0 = n0 - l0;
+                if (d0 != 0.0f) {
+                    if (lane == d) lam_lo = n0;
+                    vreg += mrow * d0;
+                }
+            }
+            if (bcast_i(act_up, d)) {
+                float l1 = bcast(lam_up, d);
+                float n1 = l1 - (-bcast(vreg, d) - bcast(vt_up, d)) * bcast(lwinv, d);
+                n1 = n1 < 0.0f ? 0.0f : n1;
+                float d1 = n1 - l1;
+                if (d1 != 0.0f) {
+                    if (lane == d) lam_up = n1;
+                    vreg -= mrow * d1;
                 }
             }
         }
-#pragma unroll
-        for (int k = 0; k < MAXR; k++) {
-            if (k < nr) {
-                float wk = bcast(w, k), lk = bcast(lam, k), akk = bcast(rinv, k);
-                float lok = bcast(lo, k), hik = bcast(hi, k);
-                int fo = bcast_i(fric_of, k);
-                if (fo >= 0) {
-                    hik = mu * bcast(lam, fo);
-                    lok = -hik;
-                }
-                float nl = lk - wk / akk;
-                nl = nl < lok ? lok : (nl > hik ? hik : nl);
-                float dl = nl - lk;
-                if (dl != 0.0f) {
-                    if (lane == k) lam = nl;
-                    w += A[k] * dl;
-                    if (lane < NV) vreg += Y[k * RS + lane] * dl;
-                }
+        for (int k = 0; k < nr; k++) {
+            float jk = lane < RS ? J[k * RS + lane] : 0.0f;
+            float jv = wave_sum_rows(jk * vreg);
+            float lk = bcast(lam, k);
+            float lok = bcast(lo, k), hik = bcast(hi, k);
+            int fo = bcast_i(fric_of, k);
+            if (fo >= 0) {
+                hik = mu * bcast(lam, fo);
+                lok = -hik;
+            }
+            float nl = lk - (jv - bcast(vt, k)) * bcast(winv, k);
+            nl = nl < lok ? lok : (nl > hik ? hik : nl);
+            float dl = nl - lk;
+            if (dl != 0.0f) {
+                if (lane == k) lam = nl;
+                if (lane < RS) vreg += Y[k * RS + lane] * dl;
             }
         }
     }
@@ -820,7 +793,6 @@ HD void substep(SimCtx& c, float hdt) {
         for (int b = 0; b < MAXB; b++) s.cforce[b][0] = s.cforce[b][1] = s.cforce[b][2] = 0.f;
         for (int ci = 0; ci < nc; ci++) {
             int r0 = 3 * ci;
-            if (r0 + 2 >= nr) break;
             f3 n = ld3(s.cn[ci]), t1, t2;
             tangents(n, t1, t2);
             f3 f = (n * s.scratch[r0] + t1 * s.scratch[r0 + 1]) + t2 * s.scratch[r0 + 2];

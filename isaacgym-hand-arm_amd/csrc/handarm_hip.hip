@@ -46,19 +46,19 @@ __device__ void store_env(SimCtx& c, const ha_state_t& st, int env, ObsIn* in) {
     int lane = c.lane, D = c.D, NO = c.NO, A = 3 + NO, L = c.L, B = 1 + L + 1 + NO;
     fk(c);
     // link twists (level-synchronous)
-    if (lane == 0) for (int k = 0; k < 6; k++) s.Vl[0][k] = 0.f;
+    if (lane == 0) for (int k = 0; k < 6; k++) s.u.dyn.Vl[0][k] = 0.f;
     wsync();
     for (int lev = 1; lev <= m.max_level; lev++) {
         if (lane < L && m.link_level[lane] == lev) {
             int i = lane, par = m.link_parent[i], d = m.link_dof[i];
-            f3 vw = ld3(&s.Vl[par][0]), vv = ld3(&s.Vl[par][3]);
+            f3 vw = ld3(&s.u.dyn.Vl[par][0]), vv = ld3(&s.u.dyn.Vl[par][3]);
             if (d >= 0) {
                 f3 axd = ld3(s.ax[d]);
                 vw = vw + axd * s.qd[d];
                 vv = vv + cross3(ld3(s.an[d]), axd) * s.qd[d];
             }
-            st3(&s.Vl[i][0], vw);
-            st3(&s.Vl[i][3], vv);
+            st3(&s.u.dyn.Vl[i][0], vw);
+            st3(&s.u.dyn.Vl[i][3], vv);
         }
         wsync();
     }
@@ -88,9 +88,9 @@ __device__ void store_env(SimCtx& c, const ha_state_t& st, int env, ObsIn* in) {
             else if (k < 7) v = s.lq[i][k - 3];
             else if (k < 10) {
                 f3 cc = ld3(s.lp[i]) + qrot(ldq(s.lq[i]), ld3(m.link_com[i]));
-                f3 lin = ld3(&s.Vl[i][3]) + cross3(ld3(&s.Vl[i][0]), cc);
+                f3 lin = ld3(&s.u.dyn.Vl[i][3]) + cross3(ld3(&s.u.dyn.Vl[i][0]), cc);
                 v = k == 7 ? lin.x : (k == 8 ? lin.y : lin.z);
-            } else v = s.Vl[i][k - 7];
+            } else v = s.u.dyn.Vl[i][k - 7];
         } else if (b == L + 1) v = rs[2 * 13 + k];
         else {
             int o = b - L - 2;
@@ -111,7 +111,7 @@ __device__ void store_env(SimCtx& c, const ha_state_t& st, int env, ObsIn* in) {
             else if (k < 7) v = s.lq[i][k - 3];
             else {
                 f3 cc = ld3(s.lp[i]) + qrot(ldq(s.lq[i]), ld3(m.link_com[i]));
-                f3 lin = ld3(&s.Vl[i][3]) + cross3(ld3(&s.Vl[i][0]), cc);
+                f3 lin = ld3(&s.u.dyn.Vl[i][3]) + cross3(ld3(&s.u.dyn.Vl[i][0]), cc);
                 v = k == 7 ? lin.x : (k == 8 ? lin.y : lin.z);
             }
             in->tip[t][k] = v;

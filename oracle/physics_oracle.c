@@ -239,32 +239,55 @@ static void dynamics(const hao_handle h, env_t* e, float* M, float* C) {
     }
 }
 
-static int cholesky(float* A, int n) {
+/* in-place Cholesky (lower triangle, stride n), left-looking; the pivot is floored at 1e-30 exactly like
+ * the GPU (isaacgym-hand-arm_amd/csrc/ha_physics.h cholesky) */
+static void cholesky(float* A, int n) {
     for (int j = 0; j < n; j++) {
         float s = A[j * n + j];
         for (int k = 0; k < j; k++) s -= A[j * n + k] * A[j * n + k];
-        if (s <= 0) return -1;
-        float l = sqrtf(s);
-        A[j * n + j] = l;
+        A[j * n + j] = sqrtf(fmaxf(s, 1e-30f));
         for (int i = j + 1; i < n; i++) {
             float t = A[i * n + j];
             for (int k = 0; k < j; k++) t -= A[i * n + k] * A[j * n + k];
-            A[i * n + j] = t / l;
+            A[i * n + j] = t / A[j * n + j];
         }
     }
-    return 0;
 }
-static void chol_solve(const float* L, int n, float* x) {
-    for (int i = 0; i < n; i++) {
-        float t = x[i];
-        for (int k = 0; k < i; k++) t -= L[i * n + k] * x[k];
-        x[i] = t / L[i * n + i];
+/* explicit M^-1 = L^-T L^-1 (stride n): column j of L^-1 by forward substitution, then
+ * Minv[i][j] = sum_{k>=i} Li[k][i] Li[k][j] for j <= i, mirrored (ha_physics.h inverse_from_cholesky) */
+static void inverse_from_cholesky(const float* Lm, int n, float* Li, float* Minv) {
+    for (int j = 0; j < n; j++) {
+        Li[j * n + j] = 1.0f / Lm[j * n + j];
+        for (int i = j + 1; i < n; i++) {
+            float t = 0.0f;
+            for (int k = j; k < i; k++) t += Lm[i * n + k] * Li[k * n + j];
+            Li[i * n + j] = -t / Lm[i * n + i];
+        }
     }
-    for (int i = n - 1; i >= 0; i--) {
-        float t = x[i];
-        for (int k = i + 1; k < n; k++) t -= L[k * n + i] * x[k];
-        x[i] = t / L[i * n + i];
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j <= i; j++) {
+            float t = 0.0f;
+            for (int k = i; k < n; k++) t += Li[k * n + i] * Li[k * n + j];
+            Minv[i * n + j] = t;
+            Minv[j * n + i] = t;
+        }
+}
+/* The GPU's 64-lane dot product (ha_physics.h wave_sum_rows): a DPP butterfly inside each 16-lane row
+ * gives ((x0+x1)+(x2+x3)) + ((x4+x5)+(x6+x7)) + ... as ((Q0+Q1)+(Q2+Q3)), then (R0+R1)+(R2+R3). Lanes
+ * beyond n contribute exact zeros. */
+static float wave_dot(const float* a, const float* b, int n) {
+    float x[64];
+    for (int i = 0; i < 64; i++) x[i] = i < n ? a[i] * b[i] : 0.0f;
+    float R[4];
+    for (int r = 0; r < 4; r++) {
+        float Q[4];
+        for (int q = 0; q < 4; q++) {
+            const float* y = x + 16 * r + 4 * q;
+            Q[q] = (y[0] + y[1]) + (y[2] + y[3]);
+        }
+        R[r] = (Q[0] + Q[1]) + (Q[2] + Q[3]);
     }
+    return (R[0] + R[1]) + (R[2] + R[3]);
 }
 
 /* ------------------------------------------------------------------ collision */
@@ -478,11 +501,14 @@ static void jac_body(const hao_handle h, const env_t* e, int body, v3 x, v3 dir,
     }
 }
 
-/* Y = Minv J^T for one row */
-static void apply_minv(const hao_handle h, const env_t* e, const float* L, const float* J, float* Y) {
+/* Y = M^-1 J^T for one row: robot block through the explicit inverse, object blocks 1/m and I_w^-1 */
+static void apply_minv(const hao_handle h, const env_t* e, const float* Minv, const float* J, float* Y) {
     int D = dofn(h);
-    for (int i = 0; i < D; i++) Y[i] = J[i];
-    chol_solve(L, D, Y);
+    for (int i = 0; i < D; i++) {
+        float acc = 0.0f;
+        for (int j = 0; j < D; j++) acc += Minv[i * D + j] * J[j];
+        Y[i] = acc;
+    }
     for (int o = 0; o < h->NO; o++) {
         const float* Jo = J + D + 6 * o;
         float* Yo = Y + D + 6 * o;
@@ -501,39 +527,24 @@ static void tangents(v3 n, v3* t1, v3* t2) {
     *t2 = crs(n, *t1);
 }
 
+/* One substep; the same operation order as ha_physics.h substep (the GPU lane-parallel version). */
 static void substep(const hao_handle h, env_t* e, float hdt) {
     const ha_model_t* m = &h->m;
     const ha_params_t* p = &h->p;
     int D = dofn(h), NO = h->NO, NV = D + 6 * NO;
-    static __thread float M[HA_MAX_DOFS * HA_MAX_DOFS];
-    float C[HA_MAX_DOFS], rhs[HA_MAX_DOFS];
+    static __thread float M[HA_MAX_DOFS * HA_MAX_DOFS], Li[HA_MAX_DOFS * HA_MAX_DOFS],
+        Minv[HA_MAX_DOFS * HA_MAX_DOFS];
+    float C[HA_MAX_DOFS];
     fk(h, e);
     dynamics(h, e, M, C);
-    /* free motion (velocity-product forces only; drives are constraint rows below) */
-    for (int d = 0; d < D; d++) rhs[d] = -hdt * C[d];
-    if (cholesky(M, D) != 0) return;
-    chol_solve(M, D, rhs);
+    cholesky(M, D);
+    inverse_from_cholesky(M, D, Li, Minv);
+    /* free motion: velocity-product forces only (drives are constraint rows of the PGS below) */
     float v[HA_MAX_DOFS + 6 * NOBJ];
-    for (int d = 0; d < D; d++) v[d] = e->qd[d] + rhs[d];
-    /* explicit M^-1 (column k = M^-1 e_k; symmetric) for the drive rows */
-    static __thread float Minv[HA_MAX_DOFS][HA_MAX_DOFS];
-    for (int k = 0; k < D; k++) {
-        float x[HA_MAX_DOFS];
-        for (int i = 0; i < D; i++) x[i] = i == k ? 1.0f : 0.0f;
-        chol_solve(M, D, x);
-        for (int i = 0; i < D; i++) Minv[k][i] = x[i];
-    }
-    /* PD position drives as soft, impulse-bounded constraint rows (PhysX articulation drive semantics:
-     * implicit spring-damper  gamma = 1/(h(kd + h kp)), bias = kp/(kd + h kp) (q - q*), |lambda| <= effort h) */
-    float dgam[HA_MAX_DOFS], dbias[HA_MAX_DOFS], dwinv[HA_MAX_DOFS], dlim[HA_MAX_DOFS], dlam[HA_MAX_DOFS];
-    for (int d = 0; d < D; d++) {
-        float kp = m->dof_kp[d], kd = m->dof_kd[d];
-        float den = kd + hdt * kp;
-        dgam[d] = 1.0f / (hdt * den);
-        dbias[d] = kp / den * (e->q[d] - e->tgt[d]);
-        dwinv[d] = 1.0f / (Minv[d][d] + dgam[d]);
-        dlim[d] = m->dof_effort[d] * hdt;
-        dlam[d] = 0.0f;
+    for (int i = 0; i < D; i++) {
+        float acc = 0.0f;
+        for (int j = 0; j < D; j++) acc += Minv[i * D + j] * (-hdt * C[j]);
+        v[i] = e->qd[i] + acc;
     }
     for (int o = 0; o < NO; o++) {
         float damp = 1.0f / (1.0f + hdt * p->object_ang_damping);
@@ -541,93 +552,109 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
         v3 av = mul(e->ow[o], damp);
         float* vo = v + D + 6 * o;
         vo[0] = lv.x; vo[1] = lv.y; vo[2] = lv.z; vo[3] = av.x; vo[4] = av.y; vo[5] = av.z;
-        /* world inverse inertia */
         float R[9], Iw[9];
         qmat(e->oq[o], R);
         rart(R, m->pool_inertia[e->pool[o]], Iw);
         inv3(Iw, e->oIinv[o]);
         e->om[o] = m->pool_mass[e->pool[o]];
     }
-    /* contacts -> rows */
+    /* contacts -> rows (normal, friction 1, friction 2 per contact) */
     contact_t cs[MAXC];
     int nc = detect(h, e, cs);
     static __thread rows_t R;
-    R.nr = 0;
-    for (int c = 0; c < nc && R.nr + 3 <= MAXR; c++) {
+    int nr = 3 * nc;
+    float winv[MAXR], lam[MAXR];
+    for (int r = 0; r < nr; r++) {
+        int c = r / 3, k = r % 3;
         v3 t1, t2;
         tangents(cs[c].n, &t1, &t2);
-        v3 dirs[3] = {cs[c].n, t1, t2};
-        int base = R.nr;
-        for (int k = 0; k < 3; k++) {
-            int r = R.nr++;
-            memset(R.J[r], 0, sizeof(float) * NV);
-            jac_body(h, e, cs[c].a, cs[c].x, dirs[k], 1.0f, R.J[r]);
-            jac_body(h, e, cs[c].b, cs[c].x, dirs[k], -1.0f, R.J[r]);
-            R.contact[r] = c;
-            if (k == 0) {
-                float s = cs[c].sep;
-                float vt = s > 0 ? -s / hdt : -p->baumgarte * s / hdt;
-                if (vt > p->max_depen_vel) vt = p->max_depen_vel;
-                R.vt[r] = vt; R.lo[r] = 0; R.hi[r] = 1e30f; R.fric_of[r] = -1;
-            } else {
-                R.vt[r] = 0; R.lo[r] = 0; R.hi[r] = 0; R.fric_of[r] = base;
-            }
-        }
-    }
-    for (int d = 0; d < D && R.nr < MAXR; d++) {
-        float lo = m->dof_lower[d], up = m->dof_upper[d];
-        for (int side = 0; side < 2 && R.nr < MAXR; side++) {
-            float s = side == 0 ? e->q[d] - lo : up - e->q[d];
-            if (s > p->joint_limit_margin) continue;
-            int r = R.nr++;
-            memset(R.J[r], 0, sizeof(float) * NV);
-            R.J[r][d] = side == 0 ? 1.0f : -1.0f;
+        v3 dir = k == 0 ? cs[c].n : (k == 1 ? t1 : t2);
+        memset(R.J[r], 0, sizeof(R.J[r]));
+        memset(R.Y[r], 0, sizeof(R.Y[r]));
+        jac_body(h, e, cs[c].a, cs[c].x, dir, 1.0f, R.J[r]);
+        jac_body(h, e, cs[c].b, cs[c].x, dir, -1.0f, R.J[r]);
+        R.contact[r] = c;
+        if (k == 0) {
+            float s = cs[c].sep;
             float vt = s > 0 ? -s / hdt : -p->baumgarte * s / hdt;
-            R.vt[r] = vt; R.lo[r] = 0; R.hi[r] = 1e30f; R.fric_of[r] = -1; R.contact[r] = -1;
+            if (vt > p->max_depen_vel) vt = p->max_depen_vel;
+            R.vt[r] = vt; R.lo[r] = 0; R.hi[r] = 3.0e38f; R.fric_of[r] = -1;
+        } else {
+            R.vt[r] = 0; R.lo[r] = 0; R.hi[r] = 0; R.fric_of[r] = r - k;
         }
+        apply_minv(h, e, Minv, R.J[r], R.Y[r]);
+        float a = 0.0f;
+        for (int t = 0; t < NV; t++) a += R.J[r][t] * R.Y[r][t];
+        winv[r] = 1.0f / (a + 1e-9f);
+        lam[r] = 0.0f;
     }
-    int nr = R.nr;
-    static __thread float Am[MAXR][MAXR];
-    float w[MAXR], lam[MAXR];
-    for (int r = 0; r < nr; r++) apply_minv(h, e, M, R.J[r], R.Y[r]);
-    for (int r = 0; r < nr; r++) {
-        for (int s = 0; s < nr; s++) {
-            float a = 0;
-            for (int k = 0; k < NV; k++) a += R.J[r][k] * R.Y[s][k];
-            Am[r][s] = a;
-        }
-        float b = 0;
-        for (int k = 0; k < NV; k++) b += R.J[r][k] * v[k];
-        w[r] = b - R.vt[r];
-        lam[r] = 0;
-        Am[r][r] += 1e-9f;
+    /* joint rows of dof d: PD drive as a soft, impulse-bounded constraint (PhysX articulation drive
+     * semantics: implicit spring-damper gamma = 1/(h(kd + h kp)), bias = kp/(kd + h kp)(q - q*),
+     * |lambda| <= effort h) and the hard lower/upper limits (active within joint_limit_margin) */
+    float dgam[HA_MAX_DOFS], dbias[HA_MAX_DOFS], dwinv[HA_MAX_DOFS], dlim[HA_MAX_DOFS], dlam[HA_MAX_DOFS];
+    float lwinv[HA_MAX_DOFS], vt_lo[HA_MAX_DOFS], vt_up[HA_MAX_DOFS], lam_lo[HA_MAX_DOFS], lam_up[HA_MAX_DOFS];
+    int act_lo[HA_MAX_DOFS], act_up[HA_MAX_DOFS];
+    for (int d = 0; d < D; d++) {
+        float kp = m->dof_kp[d], kd = m->dof_kd[d];
+        float den = kd + hdt * kp;
+        float mii = Minv[d * D + d];
+        dgam[d] = 1.0f / (hdt * den);
+        dbias[d] = kp / den * (e->q[d] - e->tgt[d]);
+        dwinv[d] = 1.0f / (mii + dgam[d]);
+        dlim[d] = m->dof_effort[d] * hdt;
+        dlam[d] = 0.0f;
+        lwinv[d] = 1.0f / (mii + 1e-9f);
+        float s_lo = e->q[d] - m->dof_lower[d], s_up = m->dof_upper[d] - e->q[d];
+        act_lo[d] = s_lo <= p->joint_limit_margin;
+        act_up[d] = s_up <= p->joint_limit_margin;
+        vt_lo[d] = s_lo > 0 ? -s_lo / hdt : -p->baumgarte * s_lo / hdt;
+        vt_up[d] = s_up > 0 ? -s_up / hdt : -p->baumgarte * s_up / hdt;
+        lam_lo[d] = lam_up[d] = 0.0f;
     }
-    /* projected Gauss-Seidel: drive rows (velocity form, J = e_d) then contact/limit rows (Delassus
-     * form).  v and the contact residuals w are both kept current after every row update. */
+    /* projected Gauss-Seidel, velocity form: joint rows d = 0..D-1 (drive, lower, upper), then the
+     * contact rows; v is updated after every row */
+    const float mu = p->friction;
     for (int it = 0; it < p->solver_iters; it++) {
         for (int d = 0; d < D; d++) {
+            const float* mrow = Minv + d * D;
             float nl = dlam[d] - (v[d] + dbias[d] + dgam[d] * dlam[d]) * dwinv[d];
             nl = nl < -dlim[d] ? -dlim[d] : (nl > dlim[d] ? dlim[d] : nl);
             float dl = nl - dlam[d];
             if (dl != 0.0f) {
                 dlam[d] = nl;
-                for (int k = 0; k < D; k++) v[k] += Minv[d][k] * dl;
-                for (int s = 0; s < nr; s++) w[s] += R.Y[s][d] * dl;
+                for (int k = 0; k < D; k++) v[k] += mrow[k] * dl;
+            }
+            if (act_lo[d]) {
+                float n0 = lam_lo[d] - (v[d] - vt_lo[d]) * lwinv[d];
+                n0 = n0 < 0.0f ? 0.0f : n0;
+                float d0 = n0 - lam_lo[d];
+                if (d0 != 0.0f) {
+                    lam_lo[d] = n0;
+                    for (int k = 0; k < D; k++) v[k] += mrow[k] * d0;
+                }
+            }
+            if (act_up[d]) {
+                float n1 = lam_up[d] - (-v[d] - vt_up[d]) * lwinv[d];
+                n1 = n1 < 0.0f ? 0.0f : n1;
+                float d1 = n1 - lam_up[d];
+                if (d1 != 0.0f) {
+                    lam_up[d] = n1;
+                    for (int k = 0; k < D; k++) v[k] -= mrow[k] * d1;
+                }
             }
         }
         for (int r = 0; r < nr; r++) {
+            float jv = wave_dot(R.J[r], v, NV);
             float lo = R.lo[r], hi = R.hi[r];
             if (R.fric_of[r] >= 0) {
-                hi = p->friction * lam[R.fric_of[r]];
+                hi = mu * lam[R.fric_of[r]];
                 lo = -hi;
             }
-            float nl = lam[r] - w[r] / Am[r][r];
+            float nl = lam[r] - (jv - R.vt[r]) * winv[r];
             nl = nl < lo ? lo : (nl > hi ? hi : nl);
             float dl = nl - lam[r];
             if (dl != 0.0f) {
                 lam[r] = nl;
-                /* A is symmetric; Am[r][s] = J_r . M^-1 J_s^T is the entry the GPU lane s holds */
-                for (int s = 0; s < nr; s++) w[s] += Am[r][s] * dl;
                 for (int k = 0; k < NV; k++) v[k] += R.Y[r][k] * dl;
             }
         }
@@ -636,7 +663,6 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
     memset(e->cforce, 0, sizeof(e->cforce));
     for (int c = 0; c < nc; c++) {
         int r0 = 3 * c;
-        if (r0 + 2 >= nr) break;
         v3 t1, t2;
         tangents(cs[c].n, &t1, &t2);
         v3 f = add(add(mul(cs[c].n, lam[r0]), mul(t1, lam[r0 + 1])), mul(t2, lam[r0 + 2]));
@@ -652,7 +678,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
             e->cforce[idx][0] += sg * f.x; e->cforce[idx][1] += sg * f.y; e->cforce[idx][2] += sg * f.z;
         }
     }
-    /* integrate */
+    /* integrate (symplectic Euler) */
     for (int d = 0; d < D; d++) {
         e->qd[d] = v[d];
         e->q[d] += hdt * v[d];

@@ -12,7 +12,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "isaacgym-hand-arm_amd")]
 from handarm_hip import _lib, build  # noqa: E402
 
 PROF_LIB = os.path.join(build.PKG, "libhandarm_hip_prof.so")
-PHASES = ["fk", "dynamics(CRBA+RNEA)", "chol+solves+Minv+objects", "detect", "rows", "Y+A build", "PGS",
+PHASES = ["fk", "dynamics(CRBA+RNEA)", "chol+Minv+free+objects", "detect", "contact rows J,Y", "joint rows", "PGS",
           "forces+integrate"]
 
 if __name__ == "__main__":
