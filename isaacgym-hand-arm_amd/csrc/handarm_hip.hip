@@ -151,10 +151,14 @@ __device__ void run_physics(SimCtx& c, int n_calls) {
         for (int sub = 0; sub < c.p->substeps; sub++) substep(c, hdt);
 }
 
-// ----------------------------------------------------------------------------- the kernel
-extern "C" __global__ void __launch_bounds__(64)
-ha_env_kernel(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params, ha_state_t st,
-              int num_envs, int mode, int n_calls, uint32_t flags, int stat_slot) {
+// ----------------------------------------------------------------------------- the kernels
+// One kernel per mode (one workgroup = one wavefront = one env): each is compiled with only its own
+// path, which keeps every kernel's code small enough to stay resident in the instruction cache, and
+// gives the profiler a distinct name for the env-step kernel.
+template <int MODE>
+__device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params,
+                                         const ha_state_t& st, int num_envs, int n_calls, uint32_t flags,
+                                         int stat_slot) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int env = blockIdx.x;
     if (env >= num_envs) return;
@@ -168,22 +172,22 @@ ha_env_kernel(const ha_model_t* __restrict__ model, const ha_params_t* __restric
     c.L = model->n_links;
     ObsIn& in = c.s->in;
     ha_state_t S = st;
-    if (mode == MODE_STEP || mode == MODE_OBSERVE) {
+    if (MODE == MODE_STEP || MODE == MODE_OBSERVE) {
         S.stats = st.stats + stat_slot * HA_STAT_SIZE;
         S.term_sums = st.term_sums + stat_slot * 4;
     }
-    if (mode == MODE_OBSERVE) {
+    if (MODE == MODE_OBSERVE) {
         snapshot_from_tensors(c, S, env, &in);
         post_step(c, S, env, in, (flags & HA_FLAG_OBS_ONLY) != 0);
         return;
     }
     load_env(c, S, env);
-    if (mode == MODE_SIMULATE) {
+    if (MODE == MODE_SIMULATE) {
         run_physics(c, n_calls);
         store_env(c, S, env, nullptr);
         return;
     }
-    if (mode == MODE_RESET) {
+    if (MODE == MODE_RESET) {
         task_reset(c, S, env, flags);
         if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics(c, 1);
         task_reset_finish(c, S, env);
@@ -193,16 +197,38 @@ ha_env_kernel(const ha_model_t* __restrict__ model, const ha_params_t* __restric
     // MODE_STEP: VecTask.step (vec_task.py:390-441) for Ur5SihMultiObjectManipulation
     bool do_reset = S.reset_buf[env] != 0;                   // configurable_vec_task.py:348
     controller_step(c, S, env);                               // :350-354
-    if (do_reset) {                                           // :356-357 -> reset_idx
-        task_reset(c, S, env, flags);
-        // reset_idx's extra gym.simulate (multi_object_manipulation.py:67). The reference resets every
-        // env on the same step (ur5sih.py:617 asserts it), so a per-env extra call is equivalent.
-        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics(c, 1);
-        task_reset_finish(c, S, env);
+    if (do_reset) task_reset(c, S, env, flags);               // :356-357 -> reset_idx
+    // phase 0 (reset envs only): reset_idx's extra gym.simulate (multi_object_manipulation.py:67). The
+    // reference resets every env on the same step (ur5sih.py:617 asserts it), so a per-env extra call is
+    // equivalent. Phase 1: the control_freq_inv physics calls (vec_task.py:409-412). One call site keeps
+    // a single copy of the physics code.
+    for (int ph = do_reset ? 0 : 1; ph < 2; ph++) {
+        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics(c, ph == 0 ? 1 : c.p->control_freq_inv);
+        if (ph == 0) task_reset_finish(c, S, env);
     }
-    if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics(c, c.p->control_freq_inv);   // vec_task.py:409-412
     store_env(c, S, env, &in);
     post_step(c, S, env, in, false);                           // configurable_vec_task.py:359-390
+}
+
+#define HA_KERNEL(name, MODE)                                                                                   \
+    extern "C" __global__ void __launch_bounds__(64)                                                          \
+        name(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params, ha_state_t st,       \
+             int num_envs, int n_calls, uint32_t flags, int stat_slot) {                                        \
+        env_body<MODE>(model, params, st, num_envs, n_calls, flags, stat_slot);                                \
+    }
+HA_KERNEL(ha_step_kernel, MODE_STEP)
+HA_KERNEL(ha_simulate_kernel, MODE_SIMULATE)
+HA_KERNEL(ha_observe_kernel, MODE_OBSERVE)
+HA_KERNEL(ha_reset_kernel, MODE_RESET)
+
+typedef void (*env_kernel_t)(const ha_model_t*, const ha_params_t*, ha_state_t, int, int, uint32_t, int);
+static env_kernel_t kernel_for(int mode) {
+    switch (mode) {
+        case MODE_STEP: return ha_step_kernel;
+        case MODE_SIMULATE: return ha_simulate_kernel;
+        case MODE_OBSERVE: return ha_observe_kernel;
+        default: return ha_reset_kernel;
+    }
 }
 
 // ----------------------------------------------------------------------------- indexed setters
@@ -276,8 +302,9 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     HIPCHK(hipMalloc(&h->d_params, sizeof(ha_params_t)));
     HIPCHK(hipMemcpy(h->d_model, model, sizeof(ha_model_t), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->d_params, params, sizeof(ha_params_t), hipMemcpyHostToDevice));
-    HIPCHK(hipFuncSetAttribute((const void*)ha_env_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)lds_bytes()));
+    for (int mode : {MODE_STEP, MODE_SIMULATE, MODE_OBSERVE, MODE_RESET})
+        HIPCHK(hipFuncSetAttribute((const void*)kernel_for(mode), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds_bytes()));
     HIPCHK(hipEventCreate(&h->ev0));
     HIPCHK(hipEventCreate(&h->ev1));
     *out = h;
@@ -310,8 +337,8 @@ static int launch(ha_handle h, int mode, int n_calls, uint32_t flags, int slot, 
     hipStream_t s = (hipStream_t)stream;
     bool rec = h->t_ev && h->t_count < h->t_max;
     (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count] : h->ev0, s);
-    hipLaunchKernelGGL(ha_env_kernel, dim3(h->N), dim3(64), lds_bytes(), s, h->d_model, h->d_params, h->st, h->N,
-                       mode, n_calls, flags, slot);
+    hipLaunchKernelGGL(kernel_for(mode), dim3(h->N), dim3(64), lds_bytes(), s, h->d_model, h->d_params, h->st,
+                       h->N, n_calls, flags, slot);
     HIPCHK(hipGetLastError());
     (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count + 1] : h->ev1, s);
     if (rec) {
