@@ -34,27 +34,35 @@ def reduce_episode_stats(env):
     env.stat_scale = world()          # EWMA alpha uses the GLOBAL number of envs
 
 
-def fold_counts(stats, terms, num_envs, ewma, obj_ewma, n_objects):
-    """Host EWMA update from (already reduced) per-step counters; returns log dict entries.
+def fold_counts(stats, terms, num_envs, ewma, obj_ewma, object_names):
+    """Host EWMA update from (already reduced) per-step counters; mirrors _update_success_rate and the
+    reward-term logging (multi_object_manipulation.py:305-351).
 
-    stats: (steps, 2 + 2*pool) ints, terms: (steps, 4) floats. Mirrors _update_success_rate."""
+    stats: (steps, 2 + 2*n_obj) ints [resets, successes, (resets_i, successes_i)...];
+    terms: (steps, 4) float reward-term sums; num_envs: GLOBAL env count.
+    Returns (log dict, ewma, obj_ewma, resets, successes)."""
     import numpy as np
-    log = {}
+    F = np.float32
+    log, obj_ewma = {}, list(obj_ewma)
+    n_obj = len(object_names)
+    total_r = total_s = 0
     for st, ts in zip(stats, terms):
-        for j, name in enumerate(["reaching", "lifting", "goal", "success"]):
-            log["reward_terms/" + name] = float(np.float32(ts[j]) / np.float32(num_envs))
+        for j, name in enumerate(("reaching", "lifting", "goal", "success")):
+            log["reward_terms/" + name] = float(F(ts[j]) / F(num_envs))
         r, s = int(st[0]), int(st[1])
         if r > 0:
-            alpha = np.float32(0.2) * (np.float32(r) / np.float32(num_envs))
-            ewma = float(alpha * (np.float32(s) / np.float32(r)) + (np.float32(1) - alpha) * np.float32(ewma))
+            alpha = F(0.2) * (F(r) / F(num_envs))
+            ewma = float(alpha * (F(s) / F(r)) + (F(1) - alpha) * F(ewma))
             log["success_rate_ewma/overall"] = ewma
-        for i in range(n_objects):
+            total_r += r
+            total_s += s
+        for i in range(n_obj):
             ri, si = int(st[2 + 2 * i]), int(st[3 + 2 * i])
             if ri > 0:
-                alpha = np.float32(0.2) * (np.float32(ri) / np.float32(num_envs)) * np.float32(n_objects)
-                obj_ewma[i] = float(alpha * (np.float32(si) / np.float32(ri)) + (np.float32(1) - alpha) * np.float32(obj_ewma[i]))
-                log[i] = obj_ewma[i]
-    return log, ewma, obj_ewma
+                alpha = F(0.2) * (F(ri) / F(num_envs)) * F(n_obj)
+                obj_ewma[i] = float(alpha * (F(si) / F(ri)) + (F(1) - alpha) * F(obj_ewma[i]))
+                log["success_rate_ewma/" + object_names[i]] = obj_ewma[i]
+    return log, ewma, obj_ewma, total_r, total_s
 
 
 __all__ = ["reduce_episode_stats", "fold_counts", "world"]

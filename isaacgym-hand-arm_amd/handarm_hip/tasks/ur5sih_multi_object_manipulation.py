@@ -19,6 +19,7 @@ import numpy as np
 import torch
 
 from .. import model as HM
+from .. import parallel
 from ..sim import HandArmSim
 from ..torch_utils import randomize_rotation, torch_rand_float
 
@@ -302,26 +303,11 @@ class Ur5SihMultiObjectManipulation:
         self._stat_pending = 0
         self._stat_folded += k
         N = self.num_envs * getattr(self, "stat_scale", 1)   # global env count after a cross-rank reduce
-        n_obj = len(self.objects)
-        for s in range(k):
-            st, ts = stats[s], terms[s]
-            for j, name in enumerate(REWARD_TERMS):
-                self._log_data["reward_terms/" + name] = float(np.float32(ts[j]) / np.float32(N))
-            num_resets, num_succ = int(st[0]), int(st[1])
-            if num_resets > 0:
-                rate = np.float32(num_succ) / np.float32(num_resets)
-                alpha = np.float32(0.2) * (np.float32(num_resets) / np.float32(N))
-                self._success_rate_ewma = float(alpha * rate + (np.float32(1) - alpha) * np.float32(self._success_rate_ewma))
-                self._log_data["success_rate_ewma/overall"] = self._success_rate_ewma
-                self.total_num_resets += num_resets
-                self.total_num_successes += num_succ
-            for i in range(n_obj):
-                r_i, s_i = int(st[2 + 2 * i]), int(st[3 + 2 * i])
-                if r_i > 0:
-                    rate = np.float32(s_i) / np.float32(r_i)
-                    alpha = np.float32(0.2) * (np.float32(r_i) / np.float32(N)) * np.float32(n_obj)
-                    self._object_ewma[i] = float(alpha * rate + (np.float32(1) - alpha) * np.float32(self._object_ewma[i]))
-                    self._log_data["success_rate_ewma/" + self.objects[i]] = self._object_ewma[i]
+        log, self._success_rate_ewma, self._object_ewma, r, sc = parallel.fold_counts(
+            stats, terms, N, self._success_rate_ewma, self._object_ewma, self.objects)
+        self._log_data.update(log)
+        self.total_num_resets += r
+        self.total_num_successes += sc
         assert R >= k
 
     @property

@@ -280,3 +280,39 @@ def test_vectask_episode_at_full_shard_size():
     torch.testing.assert_close(o[:, 63:80], env.dof_position_targets, rtol=0, atol=0)
     log = env.log_data
     assert "success_rate_ewma/overall" in log and "reward_terms/reaching" in log
+
+
+def test_gym_api_binding_matches_direct_abi():
+    """The reference-side binding (handarm_hip.gym_api) drives the same C ABI: Isaac Gym
+    call signatures with gymtorch.unwrap_tensor arguments give bit-identical state to HandArmSim calls."""
+    need_gpu()
+    from handarm_hip.gym_api import acquire_gym, gymtorch
+    n = 32
+    sim_a, _, st = _oracle_and_sim(n, 5)
+    gym = acquire_gym()
+    sim_b = gym.create_sim(n, "cuda:0")
+    assert gym.prepare_sim(sim_b)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim_b))
+    dof = gymtorch.wrap_tensor(gym.acquire_dof_state_tensor(sim_b))
+    for k in HM.STATE_FIELDS:
+        if k not in ("stats", "term_sums", "root_state", "dof_state"):
+            put(sim_b, k, st[k])
+    src_root = torch.as_tensor(st["root_state"]).cuda()
+    src_dof = torch.as_tensor(st["dof_state"]).cuda()
+    actors = torch.arange(n * 6, dtype=torch.int32, device="cuda:0")
+    robots = torch.arange(n, dtype=torch.int32, device="cuda:0") * 6 + 1
+    assert gym.set_actor_root_state_tensor_indexed(sim_b, gymtorch.unwrap_tensor(src_root),
+                                                   gymtorch.unwrap_tensor(actors), len(actors))
+    assert gym.set_dof_state_tensor_indexed(sim_b, gymtorch.unwrap_tensor(src_dof), gymtorch.unwrap_tensor(robots),
+                                            len(robots))
+    tgt = torch.as_tensor(st["sim_targets"]).cuda()
+    assert gym.set_dof_position_target_tensor(sim_b, gymtorch.unwrap_tensor(tgt))
+    sim_a.set_dof_position_target_tensor(tgt)
+    for _ in range(3):
+        gym.simulate(sim_b)
+        gym.fetch_results(sim_b, True)
+        sim_a.simulate(1)
+    gym.refresh_dof_state_tensor(sim_b)
+    gym.refresh_actor_root_state_tensor(sim_b)
+    torch.cuda.synchronize()
+    assert torch.equal(root, sim_a.t["root_state"]) and torch.equal(dof, sim_a.t["dof_state"])

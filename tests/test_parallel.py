@@ -1,0 +1,110 @@
+"""Multi-rank path on CPU (gloo, world size 2): the episode-stat all-reduce + EWMA fold.
+
+SURVEY.md §8e: envs shard with no data-path collective; the only exchange is the per-log-interval
+reduction of the success/reset counters, which must happen BEFORE the EWMA update
+(multi_object_manipulation.py:324-351) so every rank logs the global success rate a single process over
+all envs would log.
+"""
+import os
+import socket
+import types
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from handarm_hip import parallel
+
+OBJECTS = ["015_peach", "005_tomato_soup_can", "006_mustard_bottle"]
+N_LOCAL, RING = 64, 8
+
+
+def local_counts(rank, k, first_slot):
+    """Deterministic per-rank counters for k pending steps starting at ring slot first_slot."""
+    g = np.random.default_rng(100 + rank)
+    stats = np.zeros((RING, 2 + 2 * len(OBJECTS)), np.int32)
+    terms = np.zeros((RING, 4), np.float32)
+    for s in range(k):
+        slot = (first_slot + s) % RING
+        per_r = g.integers(0, 8, len(OBJECTS))
+        per_s = np.minimum(per_r, g.integers(0, 8, len(OBJECTS)))
+        stats[slot, 0], stats[slot, 1] = per_r.sum(), per_s.sum()
+        stats[slot, 2::2], stats[slot, 3::2] = per_r, per_s
+        terms[slot] = g.uniform(0, 50, 4).astype(np.float32)
+    return stats, terms
+
+
+def fake_env(rank, k, folded):
+    stats, terms = local_counts(rank, k, folded % RING)
+    sim = types.SimpleNamespace(stats_ring=RING, t={"stats": torch.from_numpy(stats), "term_sums": torch.from_numpy(terms)})
+    return types.SimpleNamespace(sim=sim, _stat_pending=k, _stat_folded=folded, num_envs=N_LOCAL)
+
+
+def _worker(rank, world, port, k, folded, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        env = fake_env(rank, k, folded)
+        parallel.reduce_episode_stats(env)
+        slots = [(folded + s) % RING for s in range(k)]
+        st = env.sim.t["stats"].numpy()[slots]
+        tm = env.sim.t["term_sums"].numpy()[slots]
+        log, ewma, obj, r, s = parallel.fold_counts(st, tm, env.num_envs * env.stat_scale, 0.0, [0.0] * 3, OBJECTS)
+        q.put((rank, env.stat_scale, st.tolist(), tm.tolist(), log, ewma, obj, r, s))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("k,folded", [(5, 0), (6, 6)])    # second case wraps around the ring
+def test_reduce_then_fold_matches_single_process(k, folded):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, k, folded, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single process over all envs: counters are sums over ranks, N = world * N_LOCAL
+    slots = [(folded + s) % RING for s in range(k)]
+    tot_st = sum(local_counts(r, k, folded % RING)[0] for r in range(world))[slots]
+    tot_tm = sum(local_counts(r, k, folded % RING)[1] for r in range(world))[slots]
+    ref = parallel.fold_counts(tot_st, tot_tm, world * N_LOCAL, 0.0, [0.0] * 3, OBJECTS)
+    for rank, scale, st, tm, log, ewma, obj, r, s in out:
+        assert scale == world
+        np.testing.assert_array_equal(np.array(st), tot_st)
+        np.testing.assert_allclose(np.array(tm, np.float32), tot_tm, rtol=1e-6)
+        assert ewma == pytest.approx(ref[1], rel=1e-6) and obj == pytest.approx(ref[2], rel=1e-6)
+        assert (r, s) == (ref[3], ref[4]) and r > 0
+        assert set(log) == set(ref[0])
+
+
+def test_single_rank_is_a_no_op():
+    env = fake_env(0, 3, 0)
+    before = env.sim.t["stats"].clone()
+    parallel.reduce_episode_stats(env)          # no process group -> untouched, no stat_scale
+    assert torch.equal(before, env.sim.t["stats"]) and not hasattr(env, "stat_scale")
+
+
+def test_fold_counts_ewma_arithmetic():
+    """Pins fold_counts to the reference update: alpha = 0.2 * resets / N (per object: x n_obj)."""
+    st = np.array([[4, 1, 2, 1, 1, 0, 1, 0]], np.int32)
+    tm = np.array([[1.0, 2.0, 3.0, 4.0]], np.float32)
+    log, ewma, obj, r, s = parallel.fold_counts(st, tm, 8, 0.5, [0.5, 0.5, 0.5], OBJECTS)
+    a = np.float32(0.2) * np.float32(4 / 8)
+    assert ewma == pytest.approx(float(a * np.float32(0.25) + (1 - a) * np.float32(0.5)), rel=1e-7)
+    a0 = np.float32(0.2) * np.float32(2 / 8) * 3
+    assert obj[0] == pytest.approx(float(a0 * np.float32(0.5) + (1 - a0) * np.float32(0.5)), rel=1e-7)
+    assert log["reward_terms/goal"] == pytest.approx(3.0 / 8)
+    assert (r, s) == (4, 1)
