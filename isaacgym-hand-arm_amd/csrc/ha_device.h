@@ -74,45 +74,52 @@ HD int lane_id() { return threadIdx.x & 63; }
 // Block == one wavefront: s_barrier is a no-op wait for lockstep lanes but orders the LDS traffic.
 HD void wsync() { __syncthreads(); }
 
-HD float wave_max(float x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x = fmaxf(x, __shfl_xor(x, off, 64));
-    return x;
-}
-HD float wave_min(float x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x = fminf(x, __shfl_xor(x, off, 64));
-    return x;
-}
-HD float wave_sum(float x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-    return x;
-}
-HD int wave_sum_i(int x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-    return x;
-}
-// arg-min / arg-max with ties broken toward the smaller index (matches a sequential strict-compare scan)
-HD void wave_argmin(float& v, int& i) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        float ov = __shfl_xor(v, off, 64);
-        int oi = __shfl_xor(i, off, 64);
-        if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; }
-    }
-}
-HD void wave_argmax(float& v, int& i) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        float ov = __shfl_xor(v, off, 64);
-        int oi = __shfl_xor(i, off, 64);
-        if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
-    }
-}
 // value of lane `src` in every lane; src must be wave-uniform (v_readlane_b32 -> SGPR)
 HD float bcast(float x, int src) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), src));
 }
 HD int bcast_i(int x, int src) { return __builtin_amdgcn_readlane(x, src); }
+
+// Reductions: DPP inside each 16-lane row (quad_perm xor1, xor2, row_half_mirror, row_mirror leave the
+// row's result in all 16 lanes), then the four row results via v_readlane. No LDS round trips
+// (a __shfl_xor is a ds_bpermute). Results are wave-uniform.
+#define HA_DPP(x, ctrl) __builtin_amdgcn_mov_dpp((x), (ctrl), 0xF, 0xF, true)
+template <int CTRL>
+HD float dpp_f(float x) { return __int_as_float(HA_DPP(__float_as_int(x), CTRL)); }
+template <int CTRL>
+HD int dpp_i(int x) { return HA_DPP(x, CTRL); }
+
+HD float wave_max(float x) {
+    x = fmaxf(x, dpp_f<0xB1>(x));
+    x = fmaxf(x, dpp_f<0x4E>(x));
+    x = fmaxf(x, dpp_f<0x141>(x));
+    x = fmaxf(x, dpp_f<0x140>(x));
+    return fmaxf(fmaxf(bcast(x, 0), bcast(x, 16)), fmaxf(bcast(x, 32), bcast(x, 48)));
+}
+HD float wave_min(float x) {
+    x = fminf(x, dpp_f<0xB1>(x));
+    x = fminf(x, dpp_f<0x4E>(x));
+    x = fminf(x, dpp_f<0x141>(x));
+    x = fminf(x, dpp_f<0x140>(x));
+    return fminf(fminf(bcast(x, 0), bcast(x, 16)), fminf(bcast(x, 32), bcast(x, 48)));
+}
+HD int wave_min_i(int x) {
+    x = min(x, dpp_i<0xB1>(x));
+    x = min(x, dpp_i<0x4E>(x));
+    x = min(x, dpp_i<0x141>(x));
+    x = min(x, dpp_i<0x140>(x));
+    return min(min(bcast_i(x, 0), bcast_i(x, 16)), min(bcast_i(x, 32), bcast_i(x, 48)));
+}
+// arg-min / arg-max with ties broken toward the smaller index (matches a sequential strict-compare
+// scan): the extreme value first, then the smallest index among the lanes that hold it.
+HD void wave_argmin(float& v, int& i) {
+    float m = wave_min(v);
+    i = wave_min_i(v == m ? i : 0x7fffffff);
+    v = m;
+}
+HD void wave_argmax(float& v, int& i) {
+    float m = wave_max(v);
+    i = wave_min_i(v == m ? i : 0x7fffffff);
+    v = m;
+}
+

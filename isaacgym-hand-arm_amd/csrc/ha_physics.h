@@ -38,7 +38,10 @@ struct DynScratch {
     float Vl[HA_MAX_LINKS][6], Al[HA_MAX_LINKS][6], Fl[HA_MAX_LINKS][6];
 };
 struct ColScratch {
-    float wvA[64][4], wvB[64][4], wpR[128][4];
+    float wvA[64][4], wvB[64][4];       // world vertices of both hulls
+    float wpA[128][4], wpB[128][4];     // world face planes (n, d) of both hulls
+    int cand[64];                       // clipping: candidate incident vertices
+    int cmax[64];                       // clipping: per-candidate max plane distance (order-preserving int)
 };
 struct RowScratch {
     float J[MAXR * RS];
@@ -87,6 +90,28 @@ HD float wave_sum_rows(float x) {
     float r0 = bcast(x, 0), r1 = bcast(x, 16), r2 = bcast(x, 32), r3 = bcast(x, 48);
     return (r0 + r1) + (r2 + r3);
 }
+
+// Diagnostic phase timers (built only into libhandarm_hip_prof.so, -DHA_PROFILE): lane 0 of every
+// wave adds the s_memtime delta of each phase; read back with ha_profile_read().
+#ifdef HA_PROFILE
+__device__ unsigned long long g_prof[32];
+#define PROF_BEGIN() unsigned long long _pt = __builtin_amdgcn_s_memtime();
+#define PROF_COUNT(i, v)                                               \
+    do {                                                               \
+        if (c.lane == 0) atomicAdd(&g_prof[i], (unsigned long long)(v)); \
+    } while (0)
+#define PROF(i)                                                        \
+    do {                                                               \
+        wsync();                                                       \
+        unsigned long long _n = __builtin_amdgcn_s_memtime();          \
+        if (c.lane == 0) atomicAdd(&g_prof[i], _n - _pt);              \
+        _pt = _n;                                                      \
+    } while (0)
+#else
+#define PROF_BEGIN()
+#define PROF(i)
+#define PROF_COUNT(i, v)
+#endif
 
 // ----------------------------------------------------------------------------- kinematics
 HD void fk(SimCtx& c) {
@@ -372,6 +397,61 @@ HD void collide_ground(SimCtx& c, int hull, PoseF P, int a) {
     emit_contacts(c, valid, pt, sep, mk3(0, 0, 1), a, -1);
 }
 
+// float <-> int mapping that preserves order (for LDS atomicMax over floats)
+HD int f2ord(float f) {
+    int i = __float_as_int(f);
+    return i >= 0 ? i : i ^ 0x7fffffff;
+}
+HD float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
+
+// SAT over the face planes wp[0..np) of one hull against the world vertices wv[0..nv) of the other:
+// sep = max_k min_i (n_k . v_i + d_k), k = its argmax (ties -> smaller k). Every (k, i) value is the
+// same expression as in the oracle; only the parallel order of the (exact) min/max differs.
+HD void sat_planes(const SimCtx& c, const float (*wp)[4], int np, const float (*wv)[4], int nv, float& sep, int& kbest) {
+    int lane = c.lane;
+    if (np <= 8) {
+        // few planes (boxes): lane = vertex, one wave min per plane
+        f3 v = mk3(0, 0, 0);
+        if (lane < nv) v = ld3(wv[lane]);
+        float best = -3.0e38f;
+        int bk = 1 << 20;
+        for (int k = 0; k < np; k++) {
+            f3 n = ld3(wp[k]);
+            float d = wp[k][3];
+            float mn = wave_min(lane < nv ? dot3(n, v) + d : 3.0e38f);
+            if (mn > best) { best = mn; bk = k; }
+        }
+        sep = best;
+        kbest = bk;
+        return;
+    }
+    // lane = plane (k = lane, lane + 64), loop over the vertices with batched LDS loads
+    float best = -3.0e38f;
+    int bk = 1 << 20;
+    for (int k = lane; k < np; k += 64) {
+        f3 n = ld3(wp[k]);
+        float d = wp[k][3];
+        float m0 = 3.0e38f, m1 = 3.0e38f;
+        int i = 0;
+        for (; i + 4 <= nv; i += 4) {
+            float4 a = *reinterpret_cast<const float4*>(wv[i]);
+            float4 b = *reinterpret_cast<const float4*>(wv[i + 1]);
+            float4 e = *reinterpret_cast<const float4*>(wv[i + 2]);
+            float4 f = *reinterpret_cast<const float4*>(wv[i + 3]);
+            m0 = fminf(m0, dot3(n, mk3(a.x, a.y, a.z)) + d);
+            m1 = fminf(m1, dot3(n, mk3(b.x, b.y, b.z)) + d);
+            m0 = fminf(m0, dot3(n, mk3(e.x, e.y, e.z)) + d);
+            m1 = fminf(m1, dot3(n, mk3(f.x, f.y, f.z)) + d);
+        }
+        for (; i < nv; i++) m0 = fminf(m0, dot3(n, ld3(wv[i])) + d);
+        float mn = fminf(m0, m1);
+        if (mn > best) { best = mn; bk = k; }
+    }
+    wave_argmax(best, bk);
+    sep = best;
+    kbest = bk;
+}
+
 // hull A (body a) vs hull B (body b); normal from B to A
 HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int b) {
     EnvLDS& s = *c.s;
@@ -385,76 +465,82 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     if (dot3(dc, dc) > rr * rr) return;
     int nva = m.hull_nverts[ha], nvb = m.hull_nverts[hb];
     int npa = m.hull_nplanes[ha], npb = m.hull_nplanes[hb];
-    if (lane < nva) st3(s.u.col.wvA[lane], PA.p + qrot(PA.q, ld3(m.verts[m.hull_vert_start[ha] + lane])));
-    if (lane < nvb) st3(s.u.col.wvB[lane], PB.p + qrot(PB.q, ld3(m.verts[m.hull_vert_start[hb] + lane])));
-    wsync();
-    // SAT over the face normals of A (planes k = lane, lane + 64)
-    float best = -3.0e38f;
-    int bestk = 1 << 20;
+    ColScratch& cs = s.u.col;
+    // world vertices and planes of both hulls, once
+    if (lane < nva) st3(cs.wvA[lane], PA.p + qrot(PA.q, ld3(m.verts[m.hull_vert_start[ha] + lane])));
+    if (lane < nvb) st3(cs.wvB[lane], PB.p + qrot(PB.q, ld3(m.verts[m.hull_vert_start[hb] + lane])));
     for (int k = lane; k < npa; k += 64) {
         f3 n; float d;
         world_plane(m, ha, k, PA, n, d);
-        float mn = 3.0e38f;
-#pragma unroll 2
-        for (int i = 0; i < nvb; i++) mn = fminf(mn, dot3(n, ld3(s.u.col.wvB[i])) + d);
-        if (mn > best) { best = mn; bestk = k; }
+        st3(cs.wpA[k], n);
+        cs.wpA[k][3] = d;
     }
-    wave_argmax(best, bestk);
-    float sepA = best;
-    int kA = bestk;
-    if (sepA > mg) return;
-    best = -3.0e38f;
-    bestk = 1 << 20;
     for (int k = lane; k < npb; k += 64) {
         f3 n; float d;
         world_plane(m, hb, k, PB, n, d);
-        float mn = 3.0e38f;
-#pragma unroll 2
-        for (int i = 0; i < nva; i++) mn = fminf(mn, dot3(n, ld3(s.u.col.wvA[i])) + d);
-        if (mn > best) { best = mn; bestk = k; }
+        st3(cs.wpB[k], n);
+        cs.wpB[k][3] = d;
     }
-    wave_argmax(best, bestk);
-    float sepB = best;
-    int kB = bestk;
+    wsync();
+    float sepA, sepB;
+    int kA, kB;
+    sat_planes(c, cs.wpA, npa, cs.wvB, nvb, sepA, kA);
+    if (sepA > mg) return;
+    sat_planes(c, cs.wpB, npb, cs.wvA, nva, sepB, kB);
     if (sepB > mg) return;
     for (int pass = 0; pass < 2; pass++) {
         bool refB = (sepB >= sepA) ? (pass == 0) : (pass == 1);
-        int hr = refB ? hb : ha, kr = refB ? kB : kA;
-        PoseF Pr = refB ? PB : PA;
-        int nvi = refB ? nva : nvb, npr = m.hull_nplanes[hr];
-        wsync();
-        for (int k = lane; k < npr; k += 64) {
-            f3 n; float d;
-            world_plane(m, hr, k, Pr, n, d);
-            st3(s.u.col.wpR[k], n);
-            s.u.col.wpR[k][3] = d;
+        int kr = refB ? kB : kA;
+        int nvi = refB ? nva : nvb, npr = refB ? npb : npa;
+        const float (*wpr)[4] = refB ? cs.wpB : cs.wpA;
+        const float (*wvi)[4] = refB ? cs.wvA : cs.wvB;
+        f3 nref = ld3(wpr[kr]);
+        float dref = wpr[kr][3];
+        // incident vertices within the margin of the reference face
+        f3 vi = mk3(0, 0, 0);
+        float dist = 0;
+        bool cand = false;
+        if (lane < nvi) {
+            vi = ld3(wvi[lane]);
+            dist = dot3(nref, vi) + dref;
+            cand = dist <= mg;
+        }
+        uint64_t cm = __ballot(cand);
+        int ncand = __popcll(cm);
+        int slot = __popcll(cm & ((1ull << lane) - 1ull));
+        if (cand) {
+            cs.cand[slot] = lane;
+            cs.cmax[slot] = f2ord(-3.0e38f);
         }
         wsync();
-        f3 nref = ld3(s.u.col.wpR[kr]);
-        float dref = s.u.col.wpR[kr][3];
+        // side planes of the reference face: max distance per candidate over (candidate, plane) pairs
+        // spread across the lanes (exact max -> order-independent)
+        int total = ncand * npr;
+        int j = lane / npr, k = lane - j * npr;
+        int step_j = 64 / npr, step_k = 64 - step_j * npr;
+        for (int w = lane; w < total; w += 64) {
+            if (k != kr) {
+                f3 v = ld3(wvi[cs.cand[j]]);
+                float val = dot3(ld3(wpr[k]), v) + wpr[k][3];
+                atomicMax(&cs.cmax[j], f2ord(val));
+            }
+            j += step_j;
+            k += step_k;
+            if (k >= npr) { k -= npr; j++; }
+        }
+        wsync();
         bool valid = false;
         f3 pt = mk3(0, 0, 0);
-        float dist = 0;
-        if (lane < nvi) {
-            f3 vi = ld3(refB ? s.u.col.wvA[lane] : s.u.col.wvB[lane]);
-            dist = dot3(nref, vi) + dref;
-            if (dist <= mg) {
-                float mx = -3.0e38f;
-                for (int k = 0; k < npr; k++) {
-                    if (k == kr) continue;
-                    mx = fmaxf(mx, dot3(ld3(s.u.col.wpR[k]), vi) + s.u.col.wpR[k][3]);
-                }
-                if (mx <= mg) {
-                    valid = true;
-                    pt = vi - nref * (0.5f * dist);
-                }
-            }
+        if (cand && ord2f(cs.cmax[slot]) <= mg) {
+            valid = true;
+            pt = vi - nref * (0.5f * dist);
         }
         if (__ballot(valid)) {
             f3 n = refB ? nref : nref * -1.0f;
             emit_contacts(c, valid, pt, dist, n, a, b);
             return;
         }
+        wsync();
     }
 }
 
@@ -569,7 +655,17 @@ HD void detect(SimCtx& c) {
                 int Lk = m.hull_link[A];
                 h1 = A; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = m.table_hull; P2 = Ptab; b2 = -1;
             }
+#ifdef HA_PROFILE
+            unsigned long long _k0 = __builtin_amdgcn_s_memtime();
+            int _nc0 = s.nc;
+#endif
             collide_hulls(c, h1, P1, h2, P2, b1, b2);
+#ifdef HA_PROFILE
+            wsync();
+            PROF_COUNT(10 + kind, __builtin_amdgcn_s_memtime() - _k0);
+            PROF_COUNT(15 + kind, 1);
+            PROF_COUNT(20 + kind, s.nc != _nc0);
+#endif
         }
     }
     wsync();
@@ -603,23 +699,6 @@ HD void tangents(f3 n, f3& t1, f3& t2) {
     t2 = cross3(n, t1);
 }
 
-
-// Diagnostic phase timers (built only into libhandarm_hip_prof.so, -DHA_PROFILE): lane 0 of every
-// wave adds the s_memtime delta of each phase; read back with ha_profile_read().
-#ifdef HA_PROFILE
-__device__ unsigned long long g_prof[16];
-#define PROF_BEGIN() unsigned long long _pt = __builtin_amdgcn_s_memtime();
-#define PROF(i)                                                        \
-    do {                                                               \
-        wsync();                                                       \
-        unsigned long long _n = __builtin_amdgcn_s_memtime();          \
-        if (c.lane == 0) atomicAdd(&g_prof[i], _n - _pt);              \
-        _pt = _n;                                                      \
-    } while (0)
-#else
-#define PROF_BEGIN()
-#define PROF(i)
-#endif
 
 HD void substep(SimCtx& c, float hdt) {
     PROF_BEGIN();
@@ -659,12 +738,13 @@ HD void substep(SimCtx& c, float hdt) {
     PROF(2);
     detect(c);
     PROF(3);
+    PROF_COUNT(8, s.nc);
+    PROF_COUNT(9, 1);
     // ---- contact rows: lane r owns row r (normal, friction 1, friction 2 of contact r / 3)
     int nc = s.nc;
     int nr = 3 * nc;    // nc <= MAXC -> <= MAXR rows
     int r = lane;
-    float vt = 0.f, lo = 0.f, hi = 0.f, winv = 0.f, lam = 0.f;
-    int fric_of = -1;
+    float vt = 0.f, winv = 0.f, lam = 0.f;
     if (r < nr) {
         float* Jr = s.u.rows.J + r * RS;
         for (int k = 0; k < RS; k++) Jr[k] = 0.0f;
@@ -679,9 +759,6 @@ HD void substep(SimCtx& c, float hdt) {
             float sp = s.csep[ci];
             vt = sp > 0 ? -sp / hdt : -p.baumgarte * sp / hdt;
             if (vt > p.max_depen_vel) vt = p.max_depen_vel;
-            hi = 3.0e38f;
-        } else {
-            fric_of = r - k;
         }
         // Y_r = M^-1 J_r^T (robot block through the explicit inverse, object blocks 1/m, I_w^-1)
         float* Yr = s.u.rows.Y + r * RS;
@@ -702,6 +779,24 @@ HD void substep(SimCtx& c, float hdt) {
         float a = 0.0f;
         for (int t = 0; t < NV; t++) a += Jr[t] * Yr[t];
         winv = 1.0f / (a + 1e-9f);
+    }
+    wsync();
+    // coupling inside each contact's 3-row block (Delassus entries J_ri . M^-1 J_rj^T, i > j): lane of
+    // friction row 1 holds a10, lane of friction row 2 holds a20 and a21
+    float ca0 = 0.f, ca1 = 0.f;
+    if (r < nr && r % 3 != 0) {
+        const float* Jr = s.u.rows.J + r * RS;
+        int r0 = r - r % 3;
+        const float* Y0 = s.u.rows.Y + r0 * RS;
+        float a = 0.0f;
+        for (int t = 0; t < NV; t++) a += Jr[t] * Y0[t];
+        ca0 = a;
+        if (r % 3 == 2) {
+            const float* Y1 = Y0 + RS;
+            float b = 0.0f;
+            for (int t = 0; t < NV; t++) b += Jr[t] * Y1[t];
+            ca1 = b;
+        }
     }
     PROF(4);
     // ---- joint rows, lane d: PD drive (soft implicit spring-damper, |impulse| <= effort h) and the
@@ -765,23 +860,45 @@ HD void substep(SimCtx& c, float hdt) {
                 }
             }
         }
-        for (int k = 0; k < nr; k++) {
-            float jk = lane < RS ? J[k * RS + lane] : 0.0f;
-            float jv = wave_sum_rows(jk * vreg);
-            float lk = bcast(lam, k);
-            float lok = bcast(lo, k), hik = bcast(hi, k);
-            int fo = bcast_i(fric_of, k);
-            if (fo >= 0) {
-                hik = mu * bcast(lam, fo);
-                lok = -hik;
+        // contact blocks: the three J.v reductions of a contact run together; the friction rows see the
+        // normal (and first friction) update through the block's Delassus entries, which equals
+        // re-reducing J.v after each row (row-by-row Gauss-Seidel) up to rounding
+        float j0n = 0.f, j1n = 0.f, j2n = 0.f, y0n = 0.f, y1n = 0.f, y2n = 0.f;
+        if (nc > 0 && lane < RS) {
+            j0n = J[lane]; j1n = J[RS + lane]; j2n = J[2 * RS + lane];
+            y0n = Y[lane]; y1n = Y[RS + lane]; y2n = Y[2 * RS + lane];
+        }
+        for (int ci = 0; ci < nc; ci++) {
+            int r0 = 3 * ci;
+            float j0 = j0n, j1 = j1n, j2 = j2n, y0 = y0n, y1 = y1n, y2 = y2n;
+            if (ci + 1 < nc && lane < RS) {
+                const float* Jn = J + (r0 + 3) * RS;
+                const float* Yn = Y + (r0 + 3) * RS;
+                j0n = Jn[lane]; j1n = Jn[RS + lane]; j2n = Jn[2 * RS + lane];
+                y0n = Yn[lane]; y1n = Yn[RS + lane]; y2n = Yn[2 * RS + lane];
             }
-            float nl = lk - (jv - bcast(vt, k)) * bcast(winv, k);
-            nl = nl < lok ? lok : (nl > hik ? hik : nl);
-            float dl = nl - lk;
-            if (dl != 0.0f) {
-                if (lane == k) lam = nl;
-                if (lane < RS) vreg += Y[k * RS + lane] * dl;
-            }
+            float jv0 = wave_sum_rows(j0 * vreg);
+            float jv1 = wave_sum_rows(j1 * vreg);
+            float jv2 = wave_sum_rows(j2 * vreg);
+            float l0 = bcast(lam, r0), l1 = bcast(lam, r0 + 1), l2 = bcast(lam, r0 + 2);
+            float n0 = l0 - (jv0 - bcast(vt, r0)) * bcast(winv, r0);
+            n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
+            float d0 = n0 - l0;
+            float hi = mu * n0;
+            jv1 = jv1 + bcast(ca0, r0 + 1) * d0;
+            float n1 = l1 - (jv1 - bcast(vt, r0 + 1)) * bcast(winv, r0 + 1);
+            n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
+            float d1 = n1 - l1;
+            jv2 = (jv2 + bcast(ca0, r0 + 2) * d0) + bcast(ca1, r0 + 2) * d1;
+            float n2 = l2 - (jv2 - bcast(vt, r0 + 2)) * bcast(winv, r0 + 2);
+            n2 = n2 < -hi ? -hi : (n2 > hi ? hi : n2);
+            float d2 = n2 - l2;
+            if (lane == r0) lam = n0;
+            if (lane == r0 + 1) lam = n1;
+            if (lane == r0 + 2) lam = n2;
+            if (d0 != 0.0f) vreg += y0 * d0;
+            if (d1 != 0.0f) vreg += y1 * d1;
+            if (d2 != 0.0f) vreg += y2 * d2;
         }
     }
     s.scratch[lane] = lam;

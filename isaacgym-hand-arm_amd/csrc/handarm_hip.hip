@@ -490,10 +490,10 @@ float ha_last_kernel_ms(ha_handle h) {
 
 #ifdef HA_PROFILE
 // diagnostic build only: per-phase s_memtime totals summed over waves (see PROF in ha_physics.h)
-extern "C" int ha_profile_read(unsigned long long* out16, int reset) {
-    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16) != hipSuccess) return HA_E_HIP;
+extern "C" int ha_profile_read(unsigned long long* out32, int reset) {
+    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 32) != hipSuccess) return HA_E_HIP;
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[32] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return HA_E_HIP;
     }
     return HA_OK;

@@ -588,6 +588,16 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
         winv[r] = 1.0f / (a + 1e-9f);
         lam[r] = 0.0f;
     }
+    /* coupling inside each contact's 3-row block: a10 = J_1 . Y_0, a20 = J_2 . Y_0, a21 = J_2 . Y_1 */
+    float a10[MAXC], a20[MAXC], a21[MAXC];
+    for (int c = 0; c < nc; c++) {
+        const float *J1 = R.J[3 * c + 1], *J2 = R.J[3 * c + 2], *Y0 = R.Y[3 * c], *Y1 = R.Y[3 * c + 1];
+        float x = 0.0f, y = 0.0f, z = 0.0f;
+        for (int t = 0; t < NV; t++) x += J1[t] * Y0[t];
+        for (int t = 0; t < NV; t++) y += J2[t] * Y0[t];
+        for (int t = 0; t < NV; t++) z += J2[t] * Y1[t];
+        a10[c] = x; a20[c] = y; a21[c] = z;
+    }
     /* joint rows of dof d: PD drive as a soft, impulse-bounded constraint (PhysX articulation drive
      * semantics: implicit spring-damper gamma = 1/(h(kd + h kp)), bias = kp/(kd + h kp)(q - q*),
      * |lambda| <= effort h) and the hard lower/upper limits (active within joint_limit_margin) */
@@ -643,20 +653,28 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
                 }
             }
         }
-        for (int r = 0; r < nr; r++) {
-            float jv = wave_dot(R.J[r], v, NV);
-            float lo = R.lo[r], hi = R.hi[r];
-            if (R.fric_of[r] >= 0) {
-                hi = mu * lam[R.fric_of[r]];
-                lo = -hi;
-            }
-            float nl = lam[r] - (jv - R.vt[r]) * winv[r];
-            nl = nl < lo ? lo : (nl > hi ? hi : nl);
-            float dl = nl - lam[r];
-            if (dl != 0.0f) {
-                lam[r] = nl;
-                for (int k = 0; k < NV; k++) v[k] += R.Y[r][k] * dl;
-            }
+        /* contact blocks (ha_physics.h): the three J.v reductions of a contact from the same v; the
+         * friction rows see the normal / first-friction update through the block's Delassus entries */
+        for (int c = 0; c < nc; c++) {
+            int r0 = 3 * c;
+            float jv0 = wave_dot(R.J[r0], v, NV), jv1 = wave_dot(R.J[r0 + 1], v, NV), jv2 = wave_dot(R.J[r0 + 2], v, NV);
+            float l0 = lam[r0], l1 = lam[r0 + 1], l2 = lam[r0 + 2];
+            float n0 = l0 - (jv0 - R.vt[r0]) * winv[r0];
+            n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
+            float d0 = n0 - l0;
+            float hi = mu * n0;
+            jv1 = jv1 + a10[c] * d0;
+            float n1 = l1 - (jv1 - R.vt[r0 + 1]) * winv[r0 + 1];
+            n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
+            float d1 = n1 - l1;
+            jv2 = (jv2 + a20[c] * d0) + a21[c] * d1;
+            float n2 = l2 - (jv2 - R.vt[r0 + 2]) * winv[r0 + 2];
+            n2 = n2 < -hi ? -hi : (n2 > hi ? hi : n2);
+            float d2 = n2 - l2;
+            lam[r0] = n0; lam[r0 + 1] = n1; lam[r0 + 2] = n2;
+            if (d0 != 0.0f) for (int k = 0; k < NV; k++) v[k] += R.Y[r0][k] * d0;
+            if (d1 != 0.0f) for (int k = 0; k < NV; k++) v[k] += R.Y[r0 + 1][k] * d1;
+            if (d2 != 0.0f) for (int k = 0; k < NV; k++) v[k] += R.Y[r0 + 2][k] * d2;
         }
     }
     /* contact forces per body (net_contact_force): the last substep's forces */

@@ -26,12 +26,41 @@ if __name__ == "__main__":
     from tools.perf_probe import run
     lib = _lib.load()
     lib.ha_profile_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    buf = (C.c_ulonglong * 16)()
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
-    for objects in (False, True):
-        lib.ha_profile_read(buf, 1)
-        run(n, "objects on" if objects else "objects off", objects=objects)
+    buf = (C.c_ulonglong * 32)()
+    args = [x for x in sys.argv[1:] if not x.startswith("--")]
+    n = int(args[0]) if args else 8192
+
+    def report(label):
         torch.cuda.synchronize()
         lib.ha_profile_read(buf, 1)
         tot = sum(buf[:8])
+        print(f"{label}: contacts/substep {buf[8] / max(buf[9], 1):.2f}", flush=True)
         print("  " + "  ".join(f"{PHASES[i]} {100.0 * buf[i] / tot:5.1f}%" for i in range(8)), flush=True)
+        sub = max(buf[9], 1)
+        for k, name in enumerate(["obj-ground", "obj-table", "obj-obj", "link-obj", "link-table"]):
+            print(f"    narrow {name:10s}: {buf[15 + k] / sub:6.2f} pairs/substep, {buf[20 + k] / sub:6.2f} with contacts, "
+                  f"{100.0 * buf[10 + k] / tot:5.1f}% of substep cycles", flush=True)
+
+    if "--bench-scene" in sys.argv:
+        # the bench workload: VecTask after drop initialisation, random actions
+        from handarm_hip.tasks import Ur5SihMultiObjectManipulation
+        env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}, "seed": 42}, "cuda:0", "cuda:0")
+        env.reset()
+        g = torch.Generator(device="cuda:0").manual_seed(42)
+        for _ in range(5):
+            env.step(torch.rand((n, 11), device="cuda:0", generator=g) * 2 - 1)
+        torch.cuda.synchronize()
+        lib.ha_profile_read(buf, 1)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            env.step(torch.rand((n, 11), device="cuda:0", generator=g) * 2 - 1)
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"bench scene n={n}: {e0.elapsed_time(e1) / 10:.3f} ms/step (profiled build)", flush=True)
+        report("bench scene")
+        sys.exit(0)
+    for objects in (False, True):
+        lib.ha_profile_read(buf, 1)
+        run(n, "objects on" if objects else "objects off", objects=objects)
+        report("objects on" if objects else "objects off")
