@@ -18,7 +18,7 @@
 
 #define MAXC 21
 #define MAXR (3 * MAXC)
-#define RS 36            /* row stride: D + 6 * n_obj <= 36 */
+#define RS 35            /* row stride: D + 6 * n_obj <= 35 */
 #define NOBJ HA_MAX_OBJ
 #define MAXD 24
 #define MAXB (1 + HA_MAX_LINKS + 1 + NOBJ)
@@ -47,30 +47,40 @@ struct RowScratch {
     float J[MAXR * RS];
     float Y[MAXR * RS];
 };
+// dynamics (M + spatial scratch) and, after the last substep, the refresh/observation staging. M sits at
+// offset 0 here and in InvScratch, so the Cholesky factor stays in place for the inverse. cforce is
+// written after each substep's PGS (nothing overlaps it until the next substep's rows phase).
+struct PostScratch {
+    float M[MAXD * MAXD];                       // M, then its Cholesky factor L (stride D)
+    DynScratch dyn;
+    ObsIn in;
+    float obs[160];
+    float cforce[MAXB][3];
+};
+struct InvScratch {
+    float M[MAXD * MAXD];
+    float Linv[MAXD * MAXD];
+};
 
 struct EnvLDS {
-    ObsIn in;
     float q[MAXD], qd[MAXD], tgt[MAXD];
-    float lp[HA_MAX_LINKS][4], lq[HA_MAX_LINKS][4];
-    float ax[MAXD][4], an[MAXD][4];
-    float M[MAXD * MAXD];                       // M, then its Cholesky factor L (stride D)
+    float lp[HA_MAX_LINKS][3], lq[HA_MAX_LINKS][4];
+    float ax[MAXD][3], an[MAXD][3];
     float Minv[MAXD * MAXD];                    // stride D
     float Cb[MAXD];
     float v[RS];
     float oc[NOBJ][4], oq[NOBJ][4], ov[NOBJ][4], ow[NOBJ][4], oIinv[NOBJ][12], om[NOBJ];
     int pool[NOBJ], coll[NOBJ];
-    float cx[MAXC][4], cn[MAXC][4], csep[MAXC];
+    float cx[MAXC][3], cn[MAXC][3], csep[MAXC];
     int ca[MAXC], cb[MAXC];
     int nc, nr, pad0, pad1;
     union {
-        DynScratch dyn;
-        float Linv[MAXD * MAXD];
+        PostScratch pd;
+        InvScratch inv;
         ColScratch col;
         RowScratch rows;
+        float xfer[64];     // lane exchange outside the physics phases (controller; PGS impulses -> forces)
     } u;
-    float cforce[MAXB][3];
-    float obs[160];
-    float scratch[64];
 };
 
 struct SimCtx {
@@ -177,24 +187,24 @@ HD void dynamics(SimCtx& c) {
         for (int a = 0; a < 3; a++)
 #pragma unroll
             for (int b = 0; b < 3; b++) I.J[a * 3 + b] = Iw[a * 3 + b] + mm * ((a == b ? ccd : 0.0f) - cv[a] * cv[b]);
-        float* ic = s.u.dyn.Ic[i];
+        float* ic = s.u.pd.dyn.Ic[i];
         ic[0] = I.m; ic[1] = I.h.x; ic[2] = I.h.y; ic[3] = I.h.z;
 #pragma unroll
         for (int k = 0; k < 9; k++) ic[4 + k] = I.J[k];
         if (i == 0) {
 #pragma unroll
-            for (int k = 0; k < 6; k++) { s.u.dyn.Vl[0][k] = 0.f; s.u.dyn.Al[0][k] = 0.f; }
+            for (int k = 0; k < 6; k++) { s.u.pd.dyn.Vl[0][k] = 0.f; s.u.pd.dyn.Al[0][k] = 0.f; }
         }
     }
     // zero M
-    for (int k = lane; k < D * D; k += 64) s.M[k] = 0.0f;
+    for (int k = lane; k < D * D; k += 64) s.u.pd.M[k] = 0.0f;
     wsync();
     // twists / bias accelerations, level by level
     for (int lev = 1; lev <= m.max_level; lev++) {
         if (own && m.link_level[lane] == lev) {
             int i = lane, par = m.link_parent[i], d = m.link_dof[i];
-            f3 vw = ld3(&s.u.dyn.Vl[par][0]), vv = ld3(&s.u.dyn.Vl[par][3]);
-            f3 aw = ld3(&s.u.dyn.Al[par][0]), av = ld3(&s.u.dyn.Al[par][3]);
+            f3 vw = ld3(&s.u.pd.dyn.Vl[par][0]), vv = ld3(&s.u.pd.dyn.Vl[par][3]);
+            f3 aw = ld3(&s.u.pd.dyn.Al[par][0]), av = ld3(&s.u.pd.dyn.Al[par][3]);
             if (d >= 0) {
                 f3 axd = ld3(s.ax[d]), and_ = ld3(s.an[d]);
                 float qd = s.qd[d];
@@ -204,21 +214,21 @@ HD void dynamics(SimCtx& c) {
                 aw = aw + cross3(vw, sw);
                 av = av + (cross3(vw, sv) + cross3(vv, sw));
             }
-            st3(&s.u.dyn.Vl[i][0], vw); st3(&s.u.dyn.Vl[i][3], vv);
-            st3(&s.u.dyn.Al[i][0], aw); st3(&s.u.dyn.Al[i][3], av);
+            st3(&s.u.pd.dyn.Vl[i][0], vw); st3(&s.u.pd.dyn.Vl[i][3], vv);
+            st3(&s.u.pd.dyn.Al[i][0], aw); st3(&s.u.pd.dyn.Al[i][3], av);
         }
         wsync();
     }
     if (own) {
         int i = lane;
-        f3 vw = ld3(&s.u.dyn.Vl[i][0]), vv = ld3(&s.u.dyn.Vl[i][3]);
-        f3 aw = ld3(&s.u.dyn.Al[i][0]), av = ld3(&s.u.dyn.Al[i][3]);
+        f3 vw = ld3(&s.u.pd.dyn.Vl[i][0]), vv = ld3(&s.u.pd.dyn.Vl[i][3]);
+        f3 aw = ld3(&s.u.pd.dyn.Al[i][0]), av = ld3(&s.u.pd.dyn.Al[i][3]);
         f3 n1, f1, n2, f2;
         inert_apply(I, aw, av, n1, f1);
         inert_apply(I, vw, vv, n2, f2);
         f3 fn = n1 + (cross3(vw, n2) + cross3(vv, f2));
         f3 ff = f1 + cross3(vw, f2);
-        st3(&s.u.dyn.Fl[i][0], fn); st3(&s.u.dyn.Fl[i][3], ff);
+        st3(&s.u.pd.dyn.Fl[i][0], fn); st3(&s.u.pd.dyn.Fl[i][3], ff);
     }
     wsync();
     // backward accumulation of forces and composite inertia, deepest level first
@@ -226,27 +236,27 @@ HD void dynamics(SimCtx& c) {
         if (own && m.link_level[lane] == lev) {
             int i = lane, par = m.link_parent[i];
 #pragma unroll
-            for (int k = 0; k < 6; k++) atomicAdd(&s.u.dyn.Fl[par][k], s.u.dyn.Fl[i][k]);
+            for (int k = 0; k < 6; k++) atomicAdd(&s.u.pd.dyn.Fl[par][k], s.u.pd.dyn.Fl[i][k]);
 #pragma unroll
-            for (int k = 0; k < 13; k++) atomicAdd(&s.u.dyn.Ic[par][k], s.u.dyn.Ic[i][k]);
+            for (int k = 0; k < 13; k++) atomicAdd(&s.u.pd.dyn.Ic[par][k], s.u.pd.dyn.Ic[i][k]);
         }
         wsync();
     }
     if (lane < D) {
         int i = m.dof_link[lane];
         f3 axd = ld3(s.ax[lane]), and_ = ld3(s.an[lane]);
-        s.Cb[lane] = dot3(axd, ld3(&s.u.dyn.Fl[i][0])) + dot3(cross3(and_, axd), ld3(&s.u.dyn.Fl[i][3]));
+        s.Cb[lane] = dot3(axd, ld3(&s.u.pd.dyn.Fl[i][0])) + dot3(cross3(and_, axd), ld3(&s.u.pd.dyn.Fl[i][3]));
     }
     for (int k = lane; k < m.n_mpairs; k += 64) {
         int d = m.mpair[k][0], e = m.mpair[k][1];
         int i = m.dof_link[d];
         f3 axd = ld3(s.ax[d]), and_ = ld3(s.an[d]);
         f3 n, f;
-        inert_apply_lds(s.u.dyn.Ic[i], axd, cross3(and_, axd), n, f);
+        inert_apply_lds(s.u.pd.dyn.Ic[i], axd, cross3(and_, axd), n, f);
         f3 axe = ld3(s.ax[e]), ane = ld3(s.an[e]);
         float val = dot3(axe, n) + dot3(cross3(ane, axe), f);
-        s.M[d * D + e] = val;
-        s.M[e * D + d] = val;
+        s.u.pd.M[d * D + e] = val;
+        s.u.pd.M[e * D + d] = val;
     }
     wsync();
 }
@@ -256,7 +266,7 @@ HD void dynamics(SimCtx& c) {
 HD void cholesky(SimCtx& c) {
     EnvLDS& s = *c.s;
     int lane = c.lane, D = c.D;
-    float* A = s.M;
+    float* A = s.u.pd.M;
     for (int j = 0; j < D; j++) {
         if (lane == j) {
             float t = A[j * D + j];
@@ -277,8 +287,8 @@ HD void cholesky(SimCtx& c) {
 HD void inverse_from_cholesky(SimCtx& c) {
     EnvLDS& s = *c.s;
     int lane = c.lane, D = c.D;
-    const float* Lm = s.M;
-    float* Li = s.u.Linv;
+    const float* Lm = s.u.inv.M;
+    float* Li = s.u.inv.Linv;
     if (lane < D) {
         int j = lane;
         Li[j * D + j] = 1.0f / Lm[j * D + j];
@@ -901,18 +911,18 @@ HD void substep(SimCtx& c, float hdt) {
             if (d2 != 0.0f) vreg += y2 * d2;
         }
     }
-    s.scratch[lane] = lam;
+    s.u.xfer[lane] = lam;
     wsync();
     if (lane < NV) s.v[lane] = vreg;
     PROF(6);
     // contact forces (last substep wins, like the oracle)
     if (lane == 0) {
-        for (int b = 0; b < MAXB; b++) s.cforce[b][0] = s.cforce[b][1] = s.cforce[b][2] = 0.f;
+        for (int b = 0; b < MAXB; b++) s.u.pd.cforce[b][0] = s.u.pd.cforce[b][1] = s.u.pd.cforce[b][2] = 0.f;
         for (int ci = 0; ci < nc; ci++) {
             int r0 = 3 * ci;
             f3 n = ld3(s.cn[ci]), t1, t2;
             tangents(n, t1, t2);
-            f3 f = (n * s.scratch[r0] + t1 * s.scratch[r0 + 1]) + t2 * s.scratch[r0 + 2];
+            f3 f = (n * s.u.xfer[r0] + t1 * s.u.xfer[r0 + 1]) + t2 * s.u.xfer[r0 + 2];
             f = f * (1.0f / hdt);
             int bodies[2] = {s.ca[ci], s.cb[ci]};
             for (int sd = 0; sd < 2; sd++) {
@@ -922,7 +932,7 @@ HD void substep(SimCtx& c, float hdt) {
                 if (bd >= 100) idx = 1 + (bd - 100);
                 else if (bd >= 0) idx = 1 + m.n_links + 1 + bd;
                 if (idx < 0) continue;
-                s.cforce[idx][0] += sg * f.x; s.cforce[idx][1] += sg * f.y; s.cforce[idx][2] += sg * f.z;
+                s.u.pd.cforce[idx][0] += sg * f.x; s.u.pd.cforce[idx][1] += sg * f.y; s.u.pd.cforce[idx][2] += sg * f.z;
             }
         }
     }

@@ -68,11 +68,11 @@ HD void controller_step(SimCtx& c, const ha_state_t& st, int env) {
     const ha_params_t& p = *c.p;
     int lane = c.lane, D = c.D;
     float* tgt = st.dof_position_targets + (size_t)env * D;
-    float* servo_sh = s.scratch + 8;
+    float* servo_sh = s.u.xfer + 8;
     if (lane < 6) {
         float u = st.ur5_target[env * 6 + lane] + p.action_dt * st.actions[env * NUM_ACT + lane];
         st.ur5_target[env * 6 + lane] = u;
-        s.scratch[lane] = u;
+        s.u.xfer[lane] = u;
     } else if (lane < 11) {
         int i = lane - 6;
         float beta = p.sih_beta;
@@ -88,7 +88,7 @@ HD void controller_step(SimCtx& c, const ha_state_t& st, int env) {
     if (lane < D) {
         int d = lane;
         float v = 0.0f;
-        if (d < 6) v = s.scratch[d];
+        if (d < 6) v = s.u.xfer[d];
         else if (d == DI_TH_OPP) v = p.thumb_opposition_gain * servo_sh[0];
         else if (d == DI_TH_FLEX) v = -spline_eval(p, 0, servo_sh[1]);
         else if (d == DI_TH_DISTAL) v = -spline_eval(p, 1, servo_sh[1] + p.proximal_coef[0] * s.q[DI_TH_FLEX]);
@@ -200,7 +200,7 @@ HD void post_step(SimCtx& c, const ha_state_t& st, int env, const ObsIn& in, boo
     const ha_model_t& m = *c.m;
     const ha_params_t& p = *c.p;
     int lane = c.lane, D = c.D, NO = c.NO;
-    float* ob = s.obs;
+    float* ob = s.u.pd.obs;
     int tgt = (int)st.target_object_index[env];
     int cfg = (int)st.object_configuration_indices[env];
     const float* goal = st.goal_pos + env * 3;

@@ -34,7 +34,7 @@ __device__ void load_env(SimCtx& c, const ha_state_t& st, int env) {
         st3(s.ow[o], ld3(r + 10));
         s.coll[o] = st.collision_enabled ? st.collision_enabled[(size_t)env * NO + o] : 1;
     }
-    for (int b = lane; b < MAXB; b += 64) s.cforce[b][0] = s.cforce[b][1] = s.cforce[b][2] = 0.0f;
+    for (int b = lane; b < MAXB; b += 64) s.u.pd.cforce[b][0] = s.u.pd.cforce[b][1] = s.u.pd.cforce[b][2] = 0.0f;
     wsync();
 }
 
@@ -46,19 +46,19 @@ __device__ void store_env(SimCtx& c, const ha_state_t& st, int env, ObsIn* in) {
     int lane = c.lane, D = c.D, NO = c.NO, A = 3 + NO, L = c.L, B = 1 + L + 1 + NO;
     fk(c);
     // link twists (level-synchronous)
-    if (lane == 0) for (int k = 0; k < 6; k++) s.u.dyn.Vl[0][k] = 0.f;
+    if (lane == 0) for (int k = 0; k < 6; k++) s.u.pd.dyn.Vl[0][k] = 0.f;
     wsync();
     for (int lev = 1; lev <= m.max_level; lev++) {
         if (lane < L && m.link_level[lane] == lev) {
             int i = lane, par = m.link_parent[i], d = m.link_dof[i];
-            f3 vw = ld3(&s.u.dyn.Vl[par][0]), vv = ld3(&s.u.dyn.Vl[par][3]);
+            f3 vw = ld3(&s.u.pd.dyn.Vl[par][0]), vv = ld3(&s.u.pd.dyn.Vl[par][3]);
             if (d >= 0) {
                 f3 axd = ld3(s.ax[d]);
                 vw = vw + axd * s.qd[d];
                 vv = vv + cross3(ld3(s.an[d]), axd) * s.qd[d];
             }
-            st3(&s.u.dyn.Vl[i][0], vw);
-            st3(&s.u.dyn.Vl[i][3], vv);
+            st3(&s.u.pd.dyn.Vl[i][0], vw);
+            st3(&s.u.pd.dyn.Vl[i][3], vv);
         }
         wsync();
     }
@@ -88,9 +88,9 @@ __device__ void store_env(SimCtx& c, const ha_state_t& st, int env, ObsIn* in) {
             else if (k < 7) v = s.lq[i][k - 3];
             else if (k < 10) {
                 f3 cc = ld3(s.lp[i]) + qrot(ldq(s.lq[i]), ld3(m.link_com[i]));
-                f3 lin = ld3(&s.u.dyn.Vl[i][3]) + cross3(ld3(&s.u.dyn.Vl[i][0]), cc);
+                f3 lin = ld3(&s.u.pd.dyn.Vl[i][3]) + cross3(ld3(&s.u.pd.dyn.Vl[i][0]), cc);
                 v = k == 7 ? lin.x : (k == 8 ? lin.y : lin.z);
-            } else v = s.u.dyn.Vl[i][k - 7];
+            } else v = s.u.pd.dyn.Vl[i][k - 7];
         } else if (b == L + 1) v = rs[2 * 13 + k];
         else {
             int o = b - L - 2;
@@ -101,7 +101,7 @@ __device__ void store_env(SimCtx& c, const ha_state_t& st, int env, ObsIn* in) {
         }
         bs[e] = v;
     }
-    for (int e = lane; e < B * 3; e += 64) st.net_contact_force[(size_t)env * B * 3 + e] = s.cforce[e / 3][e % 3];
+    for (int e = lane; e < B * 3; e += 64) st.net_contact_force[(size_t)env * B * 3 + e] = s.u.pd.cforce[e / 3][e % 3];
     if (in) {
         if (lane < 7) in->flange[lane] = lane < 3 ? s.lp[LINK_FLANGE][lane] : s.lq[LINK_FLANGE][lane - 3];
         if (lane < 50) {
@@ -111,7 +111,7 @@ __device__ void store_env(SimCtx& c, const ha_state_t& st, int env, ObsIn* in) {
             else if (k < 7) v = s.lq[i][k - 3];
             else {
                 f3 cc = ld3(s.lp[i]) + qrot(ldq(s.lq[i]), ld3(m.link_com[i]));
-                f3 lin = ld3(&s.u.dyn.Vl[i][3]) + cross3(ld3(&s.u.dyn.Vl[i][0]), cc);
+                f3 lin = ld3(&s.u.pd.dyn.Vl[i][3]) + cross3(ld3(&s.u.pd.dyn.Vl[i][0]), cc);
                 v = k == 7 ? lin.x : (k == 8 ? lin.y : lin.z);
             }
             in->tip[t][k] = v;
@@ -170,7 +170,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.D = model->n_dofs;
     c.NO = params->n_objects;
     c.L = model->n_links;
-    ObsIn& in = c.s->in;
+    ObsIn& in = c.s->u.pd.in;
     ha_state_t S = st;
     if (MODE == MODE_STEP || MODE == MODE_OBSERVE) {
         S.stats = st.stats + stat_slot * HA_STAT_SIZE;
