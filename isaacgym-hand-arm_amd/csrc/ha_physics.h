@@ -21,6 +21,7 @@
 #define RS 35            /* row stride: D + 6 * n_obj <= 35 */
 #define NOBJ HA_MAX_OBJ
 #define MAXD 24
+#define HA_ND 17         /* DOF count the kernels are compiled for (UR5 + SIH); checked by ha_create */
 #define MAXB (1 + HA_MAX_LINKS + 1 + NOBJ)
 
 // What the task observables read after refresh_simulation_tensors(): flange pose, fingertip states,
@@ -47,8 +48,7 @@ struct RowScratch {
     float J[MAXR * RS];
     float Y[MAXR * RS];
 };
-// dynamics (M + spatial scratch) and, after the last substep, the refresh/observation staging. M sits at
-// offset 0 here and in InvScratch, so the Cholesky factor stays in place for the inverse. cforce is
+// dynamics (M + spatial scratch) and, after the last substep, the refresh/observation staging. cforce is
 // written after each substep's PGS (nothing overlaps it until the next substep's rows phase).
 struct PostScratch {
     float M[MAXD * MAXD];                       // M, then its Cholesky factor L (stride D)
@@ -57,16 +57,12 @@ struct PostScratch {
     float obs[160];
     float cforce[MAXB][3];
 };
-struct InvScratch {
-    float M[MAXD * MAXD];
-    float Linv[MAXD * MAXD];
-};
 
 struct EnvLDS {
     float q[MAXD], qd[MAXD], tgt[MAXD];
     float lp[HA_MAX_LINKS][3], lq[HA_MAX_LINKS][4];
     float ax[MAXD][3], an[MAXD][3];
-    float Minv[MAXD * MAXD];                    // stride D
+    float Minv[MAXD * MAXD];                    // S ~ M^-1 (factor_inverse), stride D
     float Cb[MAXD];
     float v[RS];
     float oc[NOBJ][4], oq[NOBJ][4], ov[NOBJ][4], ow[NOBJ][4], oIinv[NOBJ][12], om[NOBJ];
@@ -76,7 +72,6 @@ struct EnvLDS {
     int nc, nr, pad0, pad1;
     union {
         PostScratch pd;
-        InvScratch inv;
         ColScratch col;
         RowScratch rows;
         float xfer[64];     // lane exchange outside the physics phases (controller; PGS impulses -> forces)
@@ -262,56 +257,57 @@ HD void dynamics(SimCtx& c) {
 }
 
 
-// in-place Cholesky of s.M (lower triangle, stride D), left-looking like the oracle
-HD void cholesky(SimCtx& c) {
+// M^-1 from M in registers, no LDS round trips or barriers (ND = compile-time DOF count):
+//   1. Cholesky M = L L^T, left-looking, lane i holds row i of L (row j of L via v_readlane);
+//   2. lane j builds column j of L^-1 by forward substitution;
+//   3. lane j back-substitutes L^T x = (L^-1 e_j) -> x = column j of M^-1.
+// Stored as S[j][i] = x_j[i] (row j of S = column j of M^-1; S is M^-1 up to rounding, not forced
+// symmetric). Every use below reads S the same way the oracle does.
+template <int ND>
+HD void factor_inverse(SimCtx& c) {
     EnvLDS& s = *c.s;
-    int lane = c.lane, D = c.D;
-    float* A = s.u.pd.M;
-    for (int j = 0; j < D; j++) {
-        if (lane == j) {
-            float t = A[j * D + j];
-            for (int k = 0; k < j; k++) t -= A[j * D + k] * A[j * D + k];
-            A[j * D + j] = sqrtf(fmaxf(t, 1e-30f));
-        }
-        wsync();
-        if (lane > j && lane < D) {
-            float t = A[lane * D + j];
-            for (int k = 0; k < j; k++) t -= A[lane * D + k] * A[j * D + k];
-            A[lane * D + j] = t / A[j * D + j];
-        }
-        wsync();
+    const int lane = c.lane;
+    const float* Mm = s.u.pd.M;
+    float a[ND];
+#pragma unroll
+    for (int k = 0; k < ND; k++) a[k] = (lane < ND && k <= lane) ? Mm[lane * ND + k] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < ND; j++) {
+        float t = a[j];
+#pragma unroll
+        for (int k = 0; k < j; k++) t -= a[k] * bcast(a[k], j);
+        float ljj = sqrtf(fmaxf(bcast(t, j), 1e-30f));
+        a[j] = lane == j ? ljj : (lane > j ? t / ljj : a[j]);
     }
-}
-
-// M^-1 = L^-T L^-1: lane j builds column j of L^-1 (forward substitution), lane i then row i of M^-1
-HD void inverse_from_cholesky(SimCtx& c) {
-    EnvLDS& s = *c.s;
-    int lane = c.lane, D = c.D;
-    const float* Lm = s.u.inv.M;
-    float* Li = s.u.inv.Linv;
-    if (lane < D) {
-        int j = lane;
-        Li[j * D + j] = 1.0f / Lm[j * D + j];
-        for (int i = j + 1; i < D; i++) {
-            float t = 0.0f;
-            for (int k = j; k < i; k++) t += Lm[i * D + k] * Li[k * D + j];
-            Li[i * D + j] = -t / Lm[i * D + i];
+    float rl[ND];
+#pragma unroll
+    for (int i = 0; i < ND; i++) rl[i] = 1.0f / bcast(a[i], i);
+    float y[ND];
+#pragma unroll
+    for (int i = 0; i < ND; i++) {
+        float t = 0.0f;
+#pragma unroll
+        for (int k = 0; k < i; k++) {
+            float lik = bcast(a[k], i);
+            t = k >= lane ? t + lik * y[k] : t;
         }
+        y[i] = i == lane ? rl[i] : (i > lane ? -t * rl[i] : 0.0f);
+    }
+    float x[ND];
+#pragma unroll
+    for (int i = ND - 1; i >= 0; i--) {
+        float t = y[i];
+#pragma unroll
+        for (int k = i + 1; k < ND; k++) t -= bcast(a[i], k) * x[k];
+        x[i] = t * rl[i];
+    }
+    if (lane < ND) {
+#pragma unroll
+        for (int i = 0; i < ND; i++) s.Minv[lane * ND + i] = x[i];
     }
     wsync();
-    if (lane < D) {
-        int i = lane;
-        for (int j = 0; j <= i; j++) {
-            float t = 0.0f;
-            for (int k = i; k < D; k++) t += Li[k * D + i] * Li[k * D + j];
-            s.Minv[i * D + j] = t;
-            s.Minv[j * D + i] = t;
-        }
-    }
-    wsync();
 }
 
-// ----------------------------------------------------------------------------- collision
 struct PoseF { f3 p; qf q; };
 
 HD PoseF object_pose(const SimCtx& c, int o) {
@@ -710,6 +706,7 @@ HD void tangents(f3 n, f3& t1, f3& t2) {
 }
 
 
+template <int ND>
 HD void substep(SimCtx& c, float hdt) {
     PROF_BEGIN();
     EnvLDS& s = *c.s;
@@ -721,8 +718,7 @@ HD void substep(SimCtx& c, float hdt) {
     PROF(0);
     dynamics(c);
     PROF(1);
-    cholesky(c);
-    inverse_from_cholesky(c);
+    factor_inverse<ND>(c);
     // free motion: velocity-product forces only (drives are constraint rows of the PGS below)
     if (lane < D) {
         float acc = 0.0f;

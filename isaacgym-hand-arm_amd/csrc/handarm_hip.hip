@@ -148,7 +148,7 @@ __device__ void snapshot_from_tensors(SimCtx& c, const ha_state_t& st, int env, 
 __device__ void run_physics(SimCtx& c, int n_calls) {
     float hdt = c.p->dt / (float)c.p->substeps;
     for (int k = 0; k < n_calls; k++)
-        for (int sub = 0; sub < c.p->substeps; sub++) substep(c, hdt);
+        for (int sub = 0; sub < c.p->substeps; sub++) substep<HA_ND>(c, hdt);
 }
 
 // ----------------------------------------------------------------------------- the kernels
@@ -167,7 +167,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.p = params;
     c.s = reinterpret_cast<EnvLDS*>(smem);
     c.lane = threadIdx.x;
-    c.D = model->n_dofs;
+    c.D = HA_ND;                  // == model->n_dofs (ha_create); a constant, so loops over D unroll
     c.NO = params->n_objects;
     c.L = model->n_links;
     ObsIn& in = c.s->u.pd.in;
@@ -283,7 +283,7 @@ int ha_struct_sizes(int32_t* model_size, int32_t* params_size, int32_t* state_si
 
 int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_envs, ha_handle* out) {
     if (!model || !params || !out || num_envs <= 0) return HA_E_ARG;
-    if (model->n_dofs > MAXD || model->n_links > HA_MAX_LINKS || params->n_objects > NOBJ ||
+    if (model->n_dofs != HA_ND || model->n_links > HA_MAX_LINKS || params->n_objects > NOBJ ||
         model->n_dofs + 6 * params->n_objects > RS || model->n_link_hulls + model->n_pool + 1 > HA_MAX_HULLS)
         return HA_E_MODEL;
     for (int k = 0; k < model->n_hulls; k++)

@@ -253,24 +253,30 @@ static void cholesky(float* A, int n) {
         }
     }
 }
-/* explicit M^-1 = L^-T L^-1 (stride n): column j of L^-1 by forward substitution, then
- * Minv[i][j] = sum_{k>=i} Li[k][i] Li[k][j] for j <= i, mirrored (ha_physics.h inverse_from_cholesky) */
-static void inverse_from_cholesky(const float* Lm, int n, float* Li, float* Minv) {
+/* M^-1 from the Cholesky factor (ha_physics.h factor_inverse): rl[i] = 1 / L[i][i]; column j of L^-1 by
+ * forward substitution (Li[j][j] = rl[j], Li[i][j] = -(sum_{k=j}^{i-1} L[i][k] Li[k][j]) rl[i]); then
+ * x = L^-T (L^-1 e_j) by back substitution. Stored as S[j][i] = x_j[i] (row j = column j of M^-1). */
+static void inverse_from_cholesky(const float* Lm, int n, float* Li, float* S) {
+    float rl[HA_MAX_DOFS];
+    for (int i = 0; i < n; i++) rl[i] = 1.0f / Lm[i * n + i];
     for (int j = 0; j < n; j++) {
-        Li[j * n + j] = 1.0f / Lm[j * n + j];
+        for (int i = 0; i < j; i++) Li[i * n + j] = 0.0f;
+        Li[j * n + j] = rl[j];
         for (int i = j + 1; i < n; i++) {
             float t = 0.0f;
             for (int k = j; k < i; k++) t += Lm[i * n + k] * Li[k * n + j];
-            Li[i * n + j] = -t / Lm[i * n + i];
+            Li[i * n + j] = -t * rl[i];
         }
     }
-    for (int i = 0; i < n; i++)
-        for (int j = 0; j <= i; j++) {
-            float t = 0.0f;
-            for (int k = i; k < n; k++) t += Li[k * n + i] * Li[k * n + j];
-            Minv[i * n + j] = t;
-            Minv[j * n + i] = t;
+    for (int j = 0; j < n; j++) {
+        float x[HA_MAX_DOFS];
+        for (int i = n - 1; i >= 0; i--) {
+            float t = Li[i * n + j];
+            for (int k = i + 1; k < n; k++) t -= Lm[k * n + i] * x[k];
+            x[i] = t * rl[i];
         }
+        for (int i = 0; i < n; i++) S[j * n + i] = x[i];
+    }
 }
 /* The GPU's 64-lane dot product (ha_physics.h wave_sum_rows): a DPP butterfly inside each 16-lane row
  * gives ((x0+x1)+(x2+x3)) + ((x4+x5)+(x6+x7)) + ... as ((Q0+Q1)+(Q2+Q3)), then (R0+R1)+(R2+R3). Lanes
