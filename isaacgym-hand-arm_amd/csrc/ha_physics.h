@@ -118,6 +118,18 @@ __device__ unsigned long long g_prof[32];
 #define PROF_COUNT(i, v)
 #endif
 
+// three independent wave_sum_rows, interleaved step by step so the DPP read-after-write wait states of
+// one chain are filled by the others (same reduction tree per value)
+HD void wave_sum_rows3(float& a, float& b, float& c) {
+    a += dpp_f<0xB1>(a); b += dpp_f<0xB1>(b); c += dpp_f<0xB1>(c);
+    a += dpp_f<0x4E>(a); b += dpp_f<0x4E>(b); c += dpp_f<0x4E>(c);
+    a += dpp_f<0x141>(a); b += dpp_f<0x141>(b); c += dpp_f<0x141>(c);
+    a += dpp_f<0x140>(a); b += dpp_f<0x140>(b); c += dpp_f<0x140>(c);
+    a = (bcast(a, 0) + bcast(a, 16)) + (bcast(a, 32) + bcast(a, 48));
+    b = (bcast(b, 0) + bcast(b, 16)) + (bcast(b, 32) + bcast(b, 48));
+    c = (bcast(c, 0) + bcast(c, 16)) + (bcast(c, 32) + bcast(c, 48));
+}
+
 // ----------------------------------------------------------------------------- kinematics
 HD void fk(SimCtx& c) {
     EnvLDS& s = *c.s;
@@ -472,6 +484,12 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     int nva = m.hull_nverts[ha], nvb = m.hull_nverts[hb];
     int npa = m.hull_nplanes[ha], npb = m.hull_nplanes[hb];
     ColScratch& cs = s.u.col;
+#ifdef HA_PROFILE
+    unsigned long long _h0 = __builtin_amdgcn_s_memtime();
+#define HPROF(i) do { wsync(); unsigned long long _h1 = __builtin_amdgcn_s_memtime(); PROF_COUNT(i, _h1 - _h0); _h0 = _h1; } while (0)
+#else
+#define HPROF(i)
+#endif
     // world vertices and planes of both hulls, once
     if (lane < nva) st3(cs.wvA[lane], PA.p + qrot(PA.q, ld3(m.verts[m.hull_vert_start[ha] + lane])));
     if (lane < nvb) st3(cs.wvB[lane], PB.p + qrot(PB.q, ld3(m.verts[m.hull_vert_start[hb] + lane])));
@@ -488,11 +506,14 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         cs.wpB[k][3] = d;
     }
     wsync();
+    HPROF(25);
     float sepA, sepB;
     int kA, kB;
     sat_planes(c, cs.wpA, npa, cs.wvB, nvb, sepA, kA);
+    HPROF(26);
     if (sepA > mg) return;
     sat_planes(c, cs.wpB, npb, cs.wvA, nva, sepB, kB);
+    HPROF(27);
     if (sepB > mg) return;
     for (int pass = 0; pass < 2; pass++) {
         bool refB = (sepB >= sepA) ? (pass == 0) : (pass == 1);
@@ -535,6 +556,7 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
             if (k >= npr) { k -= npr; j++; }
         }
         wsync();
+        HPROF(28);
         bool valid = false;
         f3 pt = mk3(0, 0, 0);
         if (cand && ord2f(cs.cmax[slot]) <= mg) {
@@ -544,11 +566,13 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         if (__ballot(valid)) {
             f3 n = refB ? nref : nref * -1.0f;
             emit_contacts(c, valid, pt, dist, n, a, b);
+            HPROF(29);
             return;
         }
         wsync();
     }
 }
+#undef HPROF
 
 // does a sphere (center c, radius r) reach the table box? Conservative for the hull inside the sphere,
 // so culling with it never removes a contact the narrow phase would produce.
@@ -883,9 +907,8 @@ HD void substep(SimCtx& c, float hdt) {
                 j0n = Jn[lane]; j1n = Jn[RS + lane]; j2n = Jn[2 * RS + lane];
                 y0n = Yn[lane]; y1n = Yn[RS + lane]; y2n = Yn[2 * RS + lane];
             }
-            float jv0 = wave_sum_rows(j0 * vreg);
-            float jv1 = wave_sum_rows(j1 * vreg);
-            float jv2 = wave_sum_rows(j2 * vreg);
+            float jv0 = j0 * vreg, jv1 = j1 * vreg, jv2 = j2 * vreg;
+            wave_sum_rows3(jv0, jv1, jv2);
             float l0 = bcast(lam, r0), l1 = bcast(lam, r0 + 1), l2 = bcast(lam, r0 + 2);
             float n0 = l0 - (jv0 - bcast(vt, r0)) * bcast(winv, r0);
             n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);

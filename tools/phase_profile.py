@@ -40,6 +40,8 @@ if __name__ == "__main__":
         for k, name in enumerate(["obj-ground", "obj-table", "obj-obj", "link-obj", "link-table"]):
             print(f"    narrow {name:10s}: {buf[15 + k] / sub:6.2f} pairs/substep, {buf[20 + k] / sub:6.2f} with contacts, "
                   f"{100.0 * buf[10 + k] / tot:5.1f}% of substep cycles", flush=True)
+        print("    hull-hull split: " + "  ".join(f"{nm} {100.0 * buf[25 + i] / tot:5.1f}%" for i, nm in
+              enumerate(["setup", "SAT A", "SAT B", "clip", "emit"])), flush=True)
 
     if "--bench-scene" in sys.argv:
         # the bench workload: VecTask after drop initialisation, random actions
