@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 1
+#define HA_ABI_VERSION 2
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -47,6 +47,11 @@ extern "C" {
 #define HA_MAX_SPLINE_PIECES 8
 #define HA_N_SPLINES 8
 #define HA_MAX_MPAIRS 192
+#define HA_DRAW_STRIDE 48     /* floats of reset_draws per env (replayed host RNG draws) */
+
+/* tasks (ha_params_t.task) */
+#define HA_TASK_UR5SIH 0        /* Ur5SihMultiObjectManipulation (tasks/hand_arm/task/multi_object_manipulation.py) */
+#define HA_TASK_ALLEGRO_HAND 1  /* AllegroHand in-hand reorientation (tasks/allegro_hand.py) */
 
 /* error codes */
 #define HA_OK 0
@@ -96,6 +101,11 @@ typedef struct ha_model_t {
     int32_t n_mpairs;                           /* (d, e) with e an ancestor-or-self DOF of d */
     int32_t mpair[HA_MAX_MPAIRS][2];
     float table_half[3];                        /* table box half extents (broad phase) */
+    /* v2: joint armature (added to the joint-space inertia diagonal; PhysX use_physx_armature) */
+    float dof_armature[HA_MAX_DOFS];
+    /* v2: env layout of the gym tensors (actor / rigid-body creation order); -1 = absent */
+    int32_t n_actors, actor_robot, actor_object0, actor_goal, actor_table;
+    int32_t n_bodies, body_robot0, body_object0, body_goal, body_table;
 } ha_model_t;
 
 /* Simulation + task parameters (Ur5SihBase.yaml, Ur5SihMultiObject*.yaml). */
@@ -129,6 +139,20 @@ typedef struct ha_params_t {
     float spline[HA_N_SPLINES][5][HA_MAX_SPLINE_PIECES];
     float thumb_opposition_gain;  /* -1.571 / 2675 */
     uint64_t seed;
+    /* v2 */
+    int32_t task;              /* HA_TASK_* */
+    int32_t num_actions, num_obs;
+    /* AllegroHand (cfg/task/AllegroHand.yaml:7-52, tasks/allegro_hand.py:44-80) */
+    float ah_dist_reward_scale, ah_rot_reward_scale, ah_rot_eps, ah_action_penalty_scale;
+    float ah_success_tolerance, ah_reach_goal_bonus, ah_fall_dist, ah_fall_penalty;
+    int32_t ah_max_consecutive_successes;
+    float ah_av_factor;
+    float ah_reset_position_noise, ah_reset_dof_pos_noise, ah_reset_dof_vel_noise;
+    float ah_act_moving_average;
+    float ah_vel_obs_scale, ah_force_torque_obs_scale;
+    float ah_object_init[7];   /* object start pose (pos, quat xyzw) */
+    float ah_goal_init[3];     /* goal_init_state position (object start - 0.04 z) */
+    float ah_goal_displacement[3];
 } ha_params_t;
 
 /* Device buffers (caller-allocated). Layouts match the Isaac Gym tensors exactly. */
@@ -158,12 +182,19 @@ typedef struct ha_state_t {
     float* servo;               /* [N][5] */
     float* smoothed;            /* [N][5] */
     float* obs_cache;           /* [N][n_obj][7] object pose seen by the previous observable refresh */
-    float* reset_draws;         /* [N][5] cfg-draw, target-draw (as float ints), goal u[3] (replay mode) */
+    float* reset_draws;         /* [N][HA_DRAW_STRIDE] replayed reset draws; Ur5Sih: cfg-draw, target-draw
+                                 * (as float ints), goal u[3]; AllegroHand: see ah_task.h */
     uint32_t* episode;          /* [N] episode counter (device RNG stream) */
     int32_t* stats;             /* [S] per-step counters, see HA_STAT_* */
     float* term_sums;           /* [4] reward term sums for the step */
     int32_t* flags;             /* [4] device flags: [0] any env needs reset (written by the step kernel) */
     uint8_t* collision_enabled; /* [N][n_obj] object collision filter (drop init) */
+    /* v2 */
+    float* dof_force;           /* [N][D] joint force of the last substep (drive + limit impulses / h) */
+    int64_t* reset_goal_buf;    /* [N] AllegroHand goal resets */
+    float* successes;           /* [N] AllegroHand consecutive successes in the episode */
+    float* goal_state;          /* [N][7] AllegroHand goal_states[:, 0:7] */
+    float* consecutive_successes; /* [1] AllegroHand global average (device EWMA) */
 } ha_state_t;
 
 /* stats layout (int32): [0] num_resets, [1] num_successes, then per pool object

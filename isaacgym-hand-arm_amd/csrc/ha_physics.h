@@ -56,6 +56,7 @@ struct PostScratch {
     ObsIn in;
     float obs[160];
     float cforce[MAXB][3];
+    float dforce[MAXD];                         // joint force of the last substep (drive + limits) / h
 };
 
 struct EnvLDS {
@@ -262,6 +263,7 @@ HD void dynamics(SimCtx& c) {
         inert_apply_lds(s.u.pd.dyn.Ic[i], axd, cross3(and_, axd), n, f);
         f3 axe = ld3(s.ax[e]), ane = ld3(s.an[e]);
         float val = dot3(axe, n) + dot3(cross3(ane, axe), f);
+        if (d == e) val += m.dof_armature[d];
         s.u.pd.M[d * D + e] = val;
         s.u.pd.M[e * D + d] = val;
     }
@@ -623,7 +625,7 @@ HD void detect(SimCtx& c) {
         if (p < npairs && pair_desc(c, p, kind, A, B)) {
             float mg = c.p->contact_margin;
             if (kind <= 3) {
-                cand = s.coll[A] != 0;
+                cand = s.coll[A] != 0 && (kind != 1 || m.table_hull >= 0);
                 if (kind == 2) cand = cand && s.coll[B] != 0;
                 if (cand) {
                     int ho = m.pool_hull[s.pool[A]];
@@ -647,7 +649,7 @@ HD void detect(SimCtx& c) {
                 }
             } else {
                 int Lk = m.hull_link[A];
-                cand = m.link_table_collide[Lk] != 0;
+                cand = m.table_hull >= 0 && m.link_table_collide[Lk] != 0;
                 if (cand) {
                     f3 ch = ld3(s.lp[Lk]) + qrot(ldq(s.lq[Lk]), ld3(m.hull_center[A]));
                     f3 ct = Ptab.p + qrot(Ptab.q, ld3(m.hull_center[m.table_hull]));
@@ -931,6 +933,7 @@ HD void substep(SimCtx& c, float hdt) {
         }
     }
     s.u.xfer[lane] = lam;
+    if (lane < D) s.u.pd.dforce[lane] = ((dlam + lam_lo) - lam_up) / hdt;
     wsync();
     if (lane < NV) s.v[lane] = vreg;
     PROF(6);
@@ -948,8 +951,8 @@ HD void substep(SimCtx& c, float hdt) {
                 int bd = bodies[sd];
                 float sg = sd == 0 ? 1.0f : -1.0f;
                 int idx = -1;
-                if (bd >= 100) idx = 1 + (bd - 100);
-                else if (bd >= 0) idx = 1 + m.n_links + 1 + bd;
+                if (bd >= 100) idx = m.body_robot0 + (bd - 100);
+                else if (bd >= 0) idx = m.body_object0 + bd;
                 if (idx < 0) continue;
                 s.u.pd.cforce[idx][0] += sg * f.x; s.u.pd.cforce[idx][1] += sg * f.y; s.u.pd.cforce[idx][2] += sg * f.z;
             }

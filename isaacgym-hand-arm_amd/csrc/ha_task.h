@@ -125,7 +125,7 @@ HD void task_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags) {
     float dr[5];
     if (flags & HA_FLAG_REPLAY_DRAWS) {
 #pragma unroll
-        for (int k = 0; k < 5; k++) dr[k] = st.reset_draws[env * 5 + k];
+        for (int k = 0; k < 5; k++) dr[k] = st.reset_draws[env * HA_DRAW_STRIDE + k];
     } else {
         uint32_t ep = st.episode[env];
         float u0 = uniform01(p.seed, env, ep, 0), u1 = uniform01(p.seed, env, ep, 1);
@@ -160,8 +160,8 @@ HD void task_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags) {
     } else if (lane == 12) {
         st.target_object_index[env] = tgt_obj;
         st.object_configuration_indices[env] = cfg;
-        st.reset_draws[env * 5 + 0] = dr[0];
-        st.reset_draws[env * 5 + 1] = dr[1];
+        st.reset_draws[env * HA_DRAW_STRIDE + 0] = dr[0];
+        st.reset_draws[env * HA_DRAW_STRIDE + 1] = dr[1];
     } else if (lane >= 16 && lane < 21) {
         int i = lane - 16;
         st.servo[env * 5 + i] = p.servo_upper[i];

@@ -14,22 +14,25 @@
 enum { MODE_SIMULATE = 0, MODE_STEP = 1, MODE_OBSERVE = 2, MODE_RESET = 3 };
 
 // ----------------------------------------------------------------------------- state load/store
+// Generic over the env layout in ha_model_t (actor / rigid-body creation order of the task).
 __device__ void load_env(SimCtx& c, const ha_state_t& st, int env) {
     EnvLDS& s = *c.s;
-    int lane = c.lane, D = c.D, NO = c.NO, A = 3 + NO;
+    const ha_model_t& m = *c.m;
+    int lane = c.lane, D = c.D, NO = c.NO, A = m.n_actors;
     if (lane < D) {
         s.q[lane] = st.dof_state[((size_t)env * D + lane) * 2];
         s.qd[lane] = st.dof_state[((size_t)env * D + lane) * 2 + 1];
         s.tgt[lane] = st.sim_targets[(size_t)env * D + lane];
+        s.u.pd.dforce[lane] = 0.0f;
     }
     if (lane < NO) {
         int o = lane;
-        const float* r = st.root_state + ((size_t)env * A + 3 + o) * 13;
+        const float* r = st.root_state + ((size_t)env * A + m.actor_object0 + o) * 13;
         int pid = (int)st.object_indices[(size_t)env * NO + o];
         s.pool[o] = pid;
         qf q = ldq(r + 3);
         stq(s.oq[o], q);
-        st3(s.oc[o], ld3(r) + qrot(q, ld3(c.m->pool_com[pid])));
+        st3(s.oc[o], ld3(r) + qrot(q, ld3(m.pool_com[pid])));
         st3(s.ov[o], ld3(r + 7));
         st3(s.ow[o], ld3(r + 10));
         s.coll[o] = st.collision_enabled ? st.collision_enabled[(size_t)env * NO + o] : 1;
@@ -38,14 +41,11 @@ __device__ void load_env(SimCtx& c, const ha_state_t& st, int env) {
     wsync();
 }
 
-// writes dof_state, object root states, rigid_body_state, net_contact_force; fills the observation
-// snapshot from the same (final) kinematics.
-__device__ void store_env(SimCtx& c, const ha_state_t& st, int env, ObsIn* in) {
+// link twists into s.u.pd.dyn.Vl (level-synchronous); needs fk()
+__device__ void link_twists(SimCtx& c) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
-    int lane = c.lane, D = c.D, NO = c.NO, A = 3 + NO, L = c.L, B = 1 + L + 1 + NO;
-    fk(c);
-    // link twists (level-synchronous)
+    int lane = c.lane, L = c.L;
     if (lane == 0) for (int k = 0; k < 6; k++) s.u.pd.dyn.Vl[0][k] = 0.f;
     wsync();
     for (int lev = 1; lev <= m.max_level; lev++) {
@@ -62,71 +62,76 @@ __device__ void store_env(SimCtx& c, const ha_state_t& st, int env, ObsIn* in) {
         }
         wsync();
     }
+}
+
+// rigid-body row k (13 floats: pos, quat, COM linvel, angvel) of robot link i from LDS
+__device__ float link_state(const SimCtx& c, int i, int k) {
+    const EnvLDS& s = *c.s;
+    if (k < 3) return s.lp[i][k];
+    if (k < 7) return s.lq[i][k - 3];
+    if (k < 10) {
+        f3 cc = ld3(s.lp[i]) + qrot(ldq(s.lq[i]), ld3(c.m->link_com[i]));
+        f3 lin = ld3(&s.u.pd.dyn.Vl[i][3]) + cross3(ld3(&s.u.pd.dyn.Vl[i][0]), cc);
+        return k == 7 ? lin.x : (k == 8 ? lin.y : lin.z);
+    }
+    return s.u.pd.dyn.Vl[i][k - 7];
+}
+// root-state row k of object o (origin pose, not COM) from LDS
+__device__ float object_state(const SimCtx& c, int o, int k) {
+    const EnvLDS& s = *c.s;
+    if (k < 3) {
+        f3 pos = ld3(s.oc[o]) - qrot(ldq(s.oq[o]), ld3(c.m->pool_com[s.pool[o]]));
+        return k == 0 ? pos.x : (k == 1 ? pos.y : pos.z);
+    }
+    if (k < 7) return s.oq[o][k - 3];
+    if (k < 10) return s.ov[o][k - 7];
+    return s.ow[o][k - 10];
+}
+
+// writes dof_state, dof_force, sim targets, object root states, rigid_body_state and net_contact_force
+// (the refresh_* tensors). Leaves the link twists in s.u.pd.dyn.Vl for the task's observation snapshot.
+__device__ void store_env(SimCtx& c, const ha_state_t& st, int env) {
+    EnvLDS& s = *c.s;
+    const ha_model_t& m = *c.m;
+    int lane = c.lane, D = c.D, NO = c.NO, A = m.n_actors, L = c.L, B = m.n_bodies;
+    fk(c);
+    link_twists(c);
     if (lane < D) {
         st.dof_state[((size_t)env * D + lane) * 2] = s.q[lane];
         st.dof_state[((size_t)env * D + lane) * 2 + 1] = s.qd[lane];
         st.sim_targets[(size_t)env * D + lane] = s.tgt[lane];
+        if (st.dof_force) st.dof_force[(size_t)env * D + lane] = s.u.pd.dforce[lane];
     }
-    if (lane < NO) {
-        int o = lane;
-        float* r = st.root_state + ((size_t)env * A + 3 + o) * 13;
-        qf q = ldq(s.oq[o]);
-        f3 pos = ld3(s.oc[o]) - qrot(q, ld3(m.pool_com[s.pool[o]]));
-        st3(r, pos); stq(r + 3, q); st3(r + 7, ld3(s.ov[o])); st3(r + 10, ld3(s.ow[o]));
-    }
+    for (int e = lane; e < NO * 13; e += 64)
+        st.root_state[((size_t)env * A + m.actor_object0 + e / 13) * 13 + e % 13] = object_state(c, e / 13, e % 13);
     wsync();
     float* bs = st.rigid_body_state + (size_t)env * B * 13;
     const float* rs = st.root_state + (size_t)env * A * 13;
-    // rigid bodies: goal(0), robot links 1..L, table L+1, objects L+2.. ; 13 floats each
     for (int e = lane; e < B * 13; e += 64) {
         int b = e / 13, k = e % 13;
         float v;
-        if (b == 0) v = rs[k];
-        else if (b <= L) {
-            int i = b - 1;
-            if (k < 3) v = s.lp[i][k];
-            else if (k < 7) v = s.lq[i][k - 3];
-            else if (k < 10) {
-                f3 cc = ld3(s.lp[i]) + qrot(ldq(s.lq[i]), ld3(m.link_com[i]));
-                f3 lin = ld3(&s.u.pd.dyn.Vl[i][3]) + cross3(ld3(&s.u.pd.dyn.Vl[i][0]), cc);
-                v = k == 7 ? lin.x : (k == 8 ? lin.y : lin.z);
-            } else v = s.u.pd.dyn.Vl[i][k - 7];
-        } else if (b == L + 1) v = rs[2 * 13 + k];
-        else {
-            int o = b - L - 2;
-            if (k < 3) { f3 pos = ld3(s.oc[o]) - qrot(ldq(s.oq[o]), ld3(m.pool_com[s.pool[o]])); v = k == 0 ? pos.x : (k == 1 ? pos.y : pos.z); }
-            else if (k < 7) v = s.oq[o][k - 3];
-            else if (k < 10) v = s.ov[o][k - 7];
-            else v = s.ow[o][k - 10];
-        }
+        if (b >= m.body_robot0 && b < m.body_robot0 + L) v = link_state(c, b - m.body_robot0, k);
+        else if (b >= m.body_object0 && b < m.body_object0 + NO) v = object_state(c, b - m.body_object0, k);
+        else if (b == m.body_goal) v = rs[m.actor_goal * 13 + k];
+        else v = rs[m.actor_table * 13 + k];
         bs[e] = v;
     }
     for (int e = lane; e < B * 3; e += 64) st.net_contact_force[(size_t)env * B * 3 + e] = s.u.pd.cforce[e / 3][e % 3];
-    if (in) {
-        if (lane < 7) in->flange[lane] = lane < 3 ? s.lp[LINK_FLANGE][lane] : s.lq[LINK_FLANGE][lane - 3];
-        if (lane < 50) {
-            int t = lane / 10, k = lane % 10, i = c_tip_links[t];
-            float v;
-            if (k < 3) v = s.lp[i][k];
-            else if (k < 7) v = s.lq[i][k - 3];
-            else {
-                f3 cc = ld3(s.lp[i]) + qrot(ldq(s.lq[i]), ld3(m.link_com[i]));
-                f3 lin = ld3(&s.u.pd.dyn.Vl[i][3]) + cross3(ld3(&s.u.pd.dyn.Vl[i][0]), cc);
-                v = k == 7 ? lin.x : (k == 8 ? lin.y : lin.z);
-            }
-            in->tip[t][k] = v;
-        }
-        if (lane < D) in->dofpos[lane] = s.q[lane];
-        for (int e = lane; e < NO * 13; e += 64) {
-            int o = e / 13, k = e % 13;
-            float v;
-            if (k < 3) { f3 pos = ld3(s.oc[o]) - qrot(ldq(s.oq[o]), ld3(m.pool_com[s.pool[o]])); v = k == 0 ? pos.x : (k == 1 ? pos.y : pos.z); }
-            else if (k < 7) v = s.oq[o][k - 3];
-            else if (k < 10) v = s.ov[o][k - 7];
-            else v = s.ow[o][k - 10];
-            in->obj[o][k] = v;
-        }
+    wsync();
+}
+
+// Ur5Sih observation snapshot (what the observables read after refresh_*): from the LDS state after
+// store_env (same final kinematics)
+__device__ void ur5sih_obs_in(SimCtx& c, ObsIn* in) {
+    EnvLDS& s = *c.s;
+    int lane = c.lane, D = c.D, NO = c.NO;
+    if (lane < 7) in->flange[lane] = lane < 3 ? s.lp[LINK_FLANGE][lane] : s.lq[LINK_FLANGE][lane - 3];
+    if (lane < 50) {
+        int t = lane / 10, k = lane % 10;
+        in->tip[t][k] = link_state(c, c_tip_links[t], k);
     }
+    if (lane < D) in->dofpos[lane] = s.q[lane];
+    for (int e = lane; e < NO * 13; e += 64) in->obj[e / 13][e % 13] = object_state(c, e / 13, e % 13);
     wsync();
 }
 
@@ -184,14 +189,14 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     load_env(c, S, env);
     if (MODE == MODE_SIMULATE) {
         run_physics(c, n_calls);
-        store_env(c, S, env, nullptr);
+        store_env(c, S, env);
         return;
     }
     if (MODE == MODE_RESET) {
         task_reset(c, S, env, flags);
         if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics(c, 1);
         task_reset_finish(c, S, env);
-        store_env(c, S, env, nullptr);
+        store_env(c, S, env);
         return;
     }
     // MODE_STEP: VecTask.step (vec_task.py:390-441) for Ur5SihMultiObjectManipulation
@@ -206,7 +211,8 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
         if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics(c, ph == 0 ? 1 : c.p->control_freq_inv);
         if (ph == 0) task_reset_finish(c, S, env);
     }
-    store_env(c, S, env, &in);
+    store_env(c, S, env);
+    ur5sih_obs_in(c, &in);
     post_step(c, S, env, in, false);                           // configurable_vec_task.py:359-390
 }
 

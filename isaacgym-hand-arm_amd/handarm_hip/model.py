@@ -22,6 +22,8 @@ MAX_LINKS, MAX_DOFS, MAX_HULLS, MAX_VERTS, MAX_PLANES = 32, 24, 64, 4096, 8192
 MAX_POOL, MAX_OBJ, MAX_INIT_POSES, MAX_SPLINE_PIECES, N_SPLINES = 32, 3, 4, 8, 8
 MAX_MPAIRS = 192
 STAT_SIZE = 2 + 2 * MAX_POOL
+DRAW_STRIDE = 48
+TASK_UR5SIH, TASK_ALLEGRO_HAND = 0, 1
 
 FLAG_NO_PHYSICS = 1
 FLAG_REPLAY_DRAWS = 2
@@ -58,6 +60,9 @@ class HaModel(C.Structure):
         ("table_hull", i32), ("table_pos", arr(f32, 3)), ("table_quat", arr(f32, 4)),
         ("link_level", arr(i32, MAX_LINKS)), ("max_level", i32), ("dof_link", arr(i32, MAX_DOFS)),
         ("n_mpairs", i32), ("mpair", arr(i32, MAX_MPAIRS, 2)), ("table_half", arr(f32, 3)),
+        ("dof_armature", arr(f32, MAX_DOFS)),
+        ("n_actors", i32), ("actor_robot", i32), ("actor_object0", i32), ("actor_goal", i32), ("actor_table", i32),
+        ("n_bodies", i32), ("body_robot0", i32), ("body_object0", i32), ("body_goal", i32), ("body_table", i32),
     ]
 
 
@@ -74,6 +79,13 @@ class HaParams(C.Structure):
         ("servo_lower", arr(f32, 5)), ("servo_upper", arr(f32, 5)), ("proximal_coef", arr(f32, 4)),
         ("spline_pieces", arr(i32, N_SPLINES)), ("spline", arr(f32, N_SPLINES, 5, MAX_SPLINE_PIECES)),
         ("thumb_opposition_gain", f32), ("seed", C.c_uint64),
+        ("task", i32), ("num_actions", i32), ("num_obs", i32),
+        ("ah_dist_reward_scale", f32), ("ah_rot_reward_scale", f32), ("ah_rot_eps", f32),
+        ("ah_action_penalty_scale", f32), ("ah_success_tolerance", f32), ("ah_reach_goal_bonus", f32),
+        ("ah_fall_dist", f32), ("ah_fall_penalty", f32), ("ah_max_consecutive_successes", i32), ("ah_av_factor", f32),
+        ("ah_reset_position_noise", f32), ("ah_reset_dof_pos_noise", f32), ("ah_reset_dof_vel_noise", f32),
+        ("ah_act_moving_average", f32), ("ah_vel_obs_scale", f32), ("ah_force_torque_obs_scale", f32),
+        ("ah_object_init", arr(f32, 7)), ("ah_goal_init", arr(f32, 3)), ("ah_goal_displacement", arr(f32, 3)),
     ]
 
 
@@ -85,12 +97,16 @@ STATE_FIELDS = ["root_state", "rigid_body_state", "dof_state", "net_contact_forc
                 "timeout_buf", "goal_reached_before", "goal_pos", "target_object_index",
                 "object_configuration_indices", "object_indices", "object_pos_initial", "object_quat_initial",
                 "ur5_target", "servo", "smoothed", "obs_cache", "reset_draws", "episode", "stats", "term_sums",
-                "flags", "collision_enabled"]
+                "flags", "collision_enabled", "dof_force", "reset_goal_buf", "successes", "goal_state",
+                "consecutive_successes"]
 
 
-def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, num_actions=11, num_obs=147):
+def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, num_actions=11, num_obs=147,
+               n_actors=None, n_bodies=None):
     """name -> (shape, numpy dtype) of every ha_state_t buffer (Isaac Gym tensor layouts)."""
-    N, D, A, B, P = num_envs, n_dofs, 3 + n_obj, 1 + n_links + 1 + n_obj, num_initial_poses
+    N, D, P = num_envs, n_dofs, num_initial_poses
+    A = n_actors if n_actors is not None else 3 + n_obj
+    B = n_bodies if n_bodies is not None else 1 + n_links + 1 + n_obj
     f, i64, u8, i32, u32 = np.float32, np.int64, np.uint8, np.int32, np.uint32
     return {
         "root_state": ((N * A, 13), f), "rigid_body_state": ((N * B, 13), f), "dof_state": ((N * D, 2), f),
@@ -101,8 +117,10 @@ def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, nu
         "object_configuration_indices": ((N,), i64), "object_indices": ((N, n_obj), i64),
         "object_pos_initial": ((N, P, n_obj, 3), f), "object_quat_initial": ((N, P, n_obj, 4), f),
         "ur5_target": ((N, 6), f), "servo": ((N, 5), f), "smoothed": ((N, 5), f), "obs_cache": ((N, n_obj, 7), f),
-        "reset_draws": ((N, 5), f), "episode": ((N,), u32), "stats": ((STAT_SIZE,), i32), "term_sums": ((4,), f),
-        "flags": ((4,), i32), "collision_enabled": ((N, n_obj), u8),
+        "reset_draws": ((N, DRAW_STRIDE), f), "episode": ((N,), u32), "stats": ((STAT_SIZE,), i32),
+        "term_sums": ((4,), f), "flags": ((4,), i32), "collision_enabled": ((N, n_obj), u8),
+        "dof_force": ((N, D), f), "reset_goal_buf": ((N,), i64), "successes": ((N,), f), "goal_state": ((N, 7), f),
+        "consecutive_successes": ((1,), f),
     }
 
 
@@ -139,14 +157,16 @@ def build_model(scene, pool_names=None):
     for d, rec in enumerate(dofs):
         m.dof_lower[d], m.dof_upper[d], m.dof_effort[d] = rec["lower"], rec["upper"], rec["effort"]
         m.dof_kp[d], m.dof_kd[d] = rec["kp"], rec["kd"]
+        m.dof_armature[d] = rec.get("armature", 0.0)
     m.base_pos[:] = rob["base_pos"]
     m.base_quat[:] = rob["base_quat"]
     objects = scene["objects"]
     if pool_names is not None:
         byname = {o["name"]: o for o in objects}
         objects = [byname[n] for n in pool_names]
+    table = scene.get("table")
     hulls = [(h, h["index"]) for h in scene["link_hulls"]] + [(o["hull"], -1) for o in objects] + \
-            [(scene["table"]["hull"], -1)]
+            ([(table["hull"], -1)] if table else [])
     assert len(hulls) <= MAX_HULLS
     vs, ps = 0, 0
     verts = np.ctypeslib.as_array(m.verts)
@@ -173,13 +193,26 @@ def build_model(scene, pool_names=None):
         m.pool_mass[i] = o["mass"]
         m.pool_com[i][:] = o["com"]
         m.pool_inertia[i][:] = o["inertia"]
-        m.pool_bbox_pos[i][:] = o["bbox_from_origin_pos"]
-        m.pool_bbox_quat[i][:] = o["bbox_from_origin_quat"]
-        m.pool_bbox_ext[i][:] = o["bbox_extents"]
-    m.table_hull = len(hulls) - 1
-    m.table_pos[:] = scene["table"]["pos"]
-    m.table_quat[:] = scene["table"]["quat"]
-    m.table_half[:] = scene["table"]["half_extents"]
+        m.pool_bbox_pos[i][:] = o.get("bbox_from_origin_pos", (0, 0, 0))
+        m.pool_bbox_quat[i][:] = o.get("bbox_from_origin_quat", (0, 0, 0, 1))
+        m.pool_bbox_ext[i][:] = o.get("bbox_extents", (0, 0, 0))
+    if table:
+        m.table_hull = len(hulls) - 1
+        m.table_pos[:] = table["pos"]
+        m.table_quat[:] = table["quat"]
+        m.table_half[:] = table["half_extents"]
+    else:
+        m.table_hull = -1
+        m.table_quat[:] = (0, 0, 0, 1)
+    # gym tensor layout (actor and rigid-body creation order). Default: Ur5SihMultiObject (multi_object.py:
+    # 562-663): goal 0, robot 1, table 2, objects 3..; bodies goal, robot links, table, objects.
+    L = len(links)
+    n_obj = scene.get("objects_per_env", 3)
+    lay = scene.get("layout") or dict(n_actors=3 + n_obj, actor_robot=1, actor_object0=3, actor_goal=0, actor_table=2,
+                                      n_bodies=1 + L + 1 + n_obj, body_robot0=1, body_object0=L + 2, body_goal=0,
+                                      body_table=L + 1)
+    for k, v in lay.items():
+        setattr(m, k, v)
     # derived topology for the level-synchronous wave kernels
     level = []
     for i, l in enumerate(links):
@@ -294,4 +327,7 @@ def build_params(cfg=None):
         p.spline_pieces[i] = tab.shape[1]
         sp[i, :, :tab.shape[1]] = tab
     p.thumb_opposition_gain = np.float32(-1.571 / 2675)
+    p.task = c.get("task", TASK_UR5SIH)
+    p.num_actions = c.get("num_actions", 11)
+    p.num_obs = c.get("num_obs", 147)
     return p, c

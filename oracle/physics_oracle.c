@@ -140,6 +140,7 @@ typedef struct {
     int pool[NOBJ];
     int coll[NOBJ];
     float cforce[1 + HA_MAX_LINKS + 1 + NOBJ][3];
+    float dforce[HA_MAX_DOFS];      /* joint force of the last substep: (drive + lower - upper impulse) / h */
 } env_t;
 
 static int dofn(const hao_handle h) { return h->D; }
@@ -233,6 +234,7 @@ static void dynamics(const hao_handle h, env_t* e, float* M, float* C) {
             int dd = m->link_dof[j];
             if (dd < 0) continue;
             float v = dot(e->ax[dd], n) + dot(crs(e->an[dd], e->ax[dd]), f);
+            if (dd == d) v += m->dof_armature[d];
             M[d * D + dd] = v;
             M[dd * D + d] = v;
         }
@@ -462,7 +464,7 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
         int ho = m->pool_hull[e->pool[o]];
         pose_t Po = {sub(e->oc[o], qrot(e->oq[o], ld3(m->pool_com[e->pool[o]]))), e->oq[o]};
         collide_ground(m, ho, Po, mg, o, out, &nout, MAXC);
-        if (near_table(m, Ptab, add(Po.p, qrot(Po.q, ld3(m->hull_center[ho]))), m->hull_radius[ho] + mg))
+        if (m->table_hull >= 0 && near_table(m, Ptab, add(Po.p, qrot(Po.q, ld3(m->hull_center[ho]))), m->hull_radius[ho] + mg))
             collide_hulls(m, ho, Po, m->table_hull, Ptab, mg, o, -1, out, &nout, MAXC);
         for (int o2 = o + 1; o2 < h->NO; o2++) {
             if (!e->coll[o2]) continue;
@@ -478,7 +480,7 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
     }
     for (int k = 0; k < m->n_link_hulls; k++) {
         int L = m->hull_link[k];
-        if (!m->link_table_collide[L]) continue;
+        if (m->table_hull < 0 || !m->link_table_collide[L]) continue;
         pose_t PL = {e->lp[L], e->lq[L]};
         if (near_table(m, Ptab, add(PL.p, qrot(PL.q, ld3(m->hull_center[k]))), m->hull_radius[k] + mg))
             collide_hulls(m, k, PL, m->table_hull, Ptab, mg, 100 + L, -1, out, &nout, MAXC);
@@ -683,6 +685,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
             if (d2 != 0.0f) for (int k = 0; k < NV; k++) v[k] += R.Y[r0 + 2][k] * d2;
         }
     }
+    for (int d = 0; d < D; d++) e->dforce[d] = ((dlam[d] + lam_lo[d]) - lam_up[d]) / hdt;
     /* contact forces per body (net_contact_force): the last substep's forces */
     memset(e->cforce, 0, sizeof(e->cforce));
     for (int c = 0; c < nc; c++) {
@@ -696,8 +699,8 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
             int bd = bodies[s];
             float sg = s == 0 ? 1.0f : -1.0f;
             int idx = -1;
-            if (bd >= 100) idx = 1 + (bd - 100);
-            else if (bd >= 0) idx = 1 + m->n_links + 1 + bd;
+            if (bd >= 100) idx = m->body_robot0 + (bd - 100);
+            else if (bd >= 0) idx = m->body_object0 + bd;
             if (idx < 0) continue;
             e->cforce[idx][0] += sg * f.x; e->cforce[idx][1] += sg * f.y; e->cforce[idx][2] += sg * f.z;
         }
@@ -729,7 +732,7 @@ static void load_env(const hao_handle h, const ha_state_t* S, int env, env_t* e)
         e->tgt[d] = S->sim_targets[env * D + d];
     }
     for (int o = 0; o < h->NO; o++) {
-        const float* r = S->root_state + (env * A + 3 + o) * 13;
+        const float* r = S->root_state + (env * A + m->actor_object0 + o) * 13;
         int pid = (int)S->object_indices[env * h->NO + o];
         e->pool[o] = pid;
         e->oq[o] = ldq(r + 3);
@@ -739,6 +742,7 @@ static void load_env(const hao_handle h, const ha_state_t* S, int env, env_t* e)
         e->coll[o] = S->collision_enabled ? S->collision_enabled[env * h->NO + o] : 1;
     }
     memset(e->cforce, 0, sizeof(e->cforce));
+    memset(e->dforce, 0, sizeof(e->dforce));
 }
 
 static void store_env(const hao_handle h, ha_state_t* S, int env, env_t* e) {
@@ -747,17 +751,18 @@ static void store_env(const hao_handle h, ha_state_t* S, int env, env_t* e) {
     for (int d = 0; d < D; d++) {
         S->dof_state[(env * D + d) * 2] = e->q[d];
         S->dof_state[(env * D + d) * 2 + 1] = e->qd[d];
+        if (S->dof_force) S->dof_force[env * D + d] = e->dforce[d];
     }
     for (int o = 0; o < h->NO; o++) {
-        float* r = S->root_state + (env * A + 3 + o) * 13;
+        float* r = S->root_state + (env * A + m->actor_object0 + o) * 13;
         v3 pos = sub(e->oc[o], qrot(e->oq[o], ld3(m->pool_com[e->pool[o]])));
         st3(r, pos); stq(r + 3, e->oq[o]); st3(r + 7, e->ov[o]); st3(r + 10, e->ow[o]);
     }
-    /* rigid body states: goal, robot links, table, objects */
+    /* rigid body states in the env's layout: robot links, objects, goal and table copied from the roots */
     fk(h, e);
     float* bs = S->rigid_body_state + (size_t)env * B * 13;
-    const float* goal = S->root_state + (env * A + 0) * 13;
-    memcpy(bs, goal, 13 * sizeof(float));
+    const float* rs = S->root_state + (size_t)env * A * 13;
+    if (m->body_goal >= 0) memcpy(bs + m->body_goal * 13, rs + m->actor_goal * 13, 13 * sizeof(float));
     twist Vl[HA_MAX_LINKS];
     for (int i = 0; i < m->n_links; i++) {
         int par = m->link_parent[i], d = m->link_dof[i];
@@ -768,14 +773,14 @@ static void store_env(const hao_handle h, ha_state_t* S, int env, env_t* e) {
             Vl[i].w = add(vp.w, mul(e->ax[d], e->qd[d]));
             Vl[i].v = add(vp.v, mul(crs(e->an[d], e->ax[d]), e->qd[d]));
         }
-        float* b = bs + (1 + i) * 13;
+        float* b = bs + (m->body_robot0 + i) * 13;
         v3 c = add(e->lp[i], qrot(e->lq[i], ld3(m->link_com[i])));
         v3 lin = add(Vl[i].v, crs(Vl[i].w, c));
         st3(b, e->lp[i]); stq(b + 3, e->lq[i]); st3(b + 7, lin); st3(b + 10, Vl[i].w);
     }
-    memcpy(bs + (1 + m->n_links) * 13, S->root_state + (env * A + 2) * 13, 13 * sizeof(float));
+    if (m->body_table >= 0) memcpy(bs + m->body_table * 13, rs + m->actor_table * 13, 13 * sizeof(float));
     for (int o = 0; o < h->NO; o++)
-        memcpy(bs + (1 + m->n_links + 1 + o) * 13, S->root_state + (env * A + 3 + o) * 13, 13 * sizeof(float));
+        memcpy(bs + (m->body_object0 + o) * 13, rs + (m->actor_object0 + o) * 13, 13 * sizeof(float));
     for (int b = 0; b < B; b++)
         for (int k = 0; k < 3; k++) S->net_contact_force[((size_t)env * B + b) * 3 + k] = e->cforce[b][k];
 }
@@ -787,9 +792,9 @@ hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int nu
     h->p = *params;
     h->N = num_envs;
     h->NO = params->n_objects;
-    h->A = 3 + h->NO;
+    h->A = model->n_actors;
     h->D = model->n_dofs;
-    h->B = 1 + model->n_links + 1 + h->NO;
+    h->B = model->n_bodies;
     return h;
 }
 void hao_destroy(hao_handle h) { free(h); }

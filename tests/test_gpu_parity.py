@@ -107,7 +107,7 @@ def test_reset_against_reference_goldens():
     put(sim, "object_pos_initial", d["object_pos_initial"])
     put(sim, "object_quat_initial", d["object_quat_initial"])
     put(sim, "object_indices", np.tile(np.arange(3), (n, 1)))
-    draws = np.zeros((n, 5), np.float32)
+    draws = np.zeros((n, HM.DRAW_STRIDE), np.float32)
     draws[:, 0], draws[:, 1], draws[:, 2:5] = d["draw_cfg"], d["draw_target"], d["draw_goal"]
     put(sim, "reset_draws", draws)
     sim.t["progress_buf"].fill_(200)
