@@ -9,7 +9,9 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "ha_task.h"
+#include "ah_task.h"
+
+#define HA_ND 17         /* Ur5Sih DOF count (UR5 + SIH); AH_ND = 16 (Allegro) */
 
 enum { MODE_SIMULATE = 0, MODE_STEP = 1, MODE_OBSERVE = 2, MODE_RESET = 3 };
 
@@ -150,20 +152,46 @@ __device__ void snapshot_from_tensors(SimCtx& c, const ha_state_t& st, int env, 
     wsync();
 }
 
+template <int ND>
 __device__ void run_physics(SimCtx& c, int n_calls) {
     float hdt = c.p->dt / (float)c.p->substeps;
     for (int k = 0; k < n_calls; k++)
-        for (int sub = 0; sub < c.p->substeps; sub++) substep<HA_ND>(c, hdt);
+        for (int sub = 0; sub < c.p->substeps; sub++) substep<ND>(c, hdt);
+}
+
+// AllegroHand observation staging
+__device__ void ah_in_from_lds(SimCtx& c, AhIn* in) {
+    EnvLDS& s = *c.s;
+    int lane = c.lane, D = c.D;
+    if (lane < D) {
+        in->q[lane] = s.q[lane];
+        in->qd[lane] = s.qd[lane];
+        in->f[lane] = s.u.pd.dforce[lane];
+    }
+    if (lane < 13) in->obj[lane] = object_state(c, 0, lane);
+    wsync();
+}
+__device__ void ah_in_from_tensors(SimCtx& c, const ha_state_t& st, int env, AhIn* in) {
+    const ha_model_t& m = *c.m;
+    int lane = c.lane, D = c.D;
+    if (lane < D) {
+        in->q[lane] = st.dof_state[((size_t)env * D + lane) * 2];
+        in->qd[lane] = st.dof_state[((size_t)env * D + lane) * 2 + 1];
+        in->f[lane] = st.dof_force[(size_t)env * D + lane];
+    }
+    if (lane < 13) in->obj[lane] = st.root_state[((size_t)env * m.n_actors + m.actor_object0) * 13 + lane];
+    wsync();
 }
 
 // ----------------------------------------------------------------------------- the kernels
-// One kernel per mode (one workgroup = one wavefront = one env): each is compiled with only its own
-// path, which keeps every kernel's code small enough to stay resident in the instruction cache, and
-// gives the profiler a distinct name for the env-step kernel.
-template <int MODE>
+// One kernel per (task, mode) (one workgroup = one wavefront = one env): each is compiled with only its
+// own path, which keeps every kernel's code small, gives the DOF count to the compiler as a constant, and
+// gives the profiler a distinct name per kernel.
+template <int TASK, int MODE>
 __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params,
                                          const ha_state_t& st, int num_envs, int n_calls, uint32_t flags,
                                          int stat_slot) {
+    constexpr int ND = TASK == HA_TASK_ALLEGRO_HAND ? AH_ND : HA_ND;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int env = blockIdx.x;
     if (env >= num_envs) return;
@@ -172,29 +200,51 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.p = params;
     c.s = reinterpret_cast<EnvLDS*>(smem);
     c.lane = threadIdx.x;
-    c.D = HA_ND;                  // == model->n_dofs (ha_create); a constant, so loops over D unroll
+    c.D = ND;                     // == model->n_dofs (ha_create); a constant, so loops over D unroll
     c.NO = params->n_objects;
     c.L = model->n_links;
     ObsIn& in = c.s->u.pd.in;
+    AhIn& ain = *reinterpret_cast<AhIn*>(&c.s->u.pd.in);
     ha_state_t S = st;
     if (MODE == MODE_STEP || MODE == MODE_OBSERVE) {
         S.stats = st.stats + stat_slot * HA_STAT_SIZE;
         S.term_sums = st.term_sums + stat_slot * 4;
     }
     if (MODE == MODE_OBSERVE) {
-        snapshot_from_tensors(c, S, env, &in);
-        post_step(c, S, env, in, (flags & HA_FLAG_OBS_ONLY) != 0);
+        if (TASK == HA_TASK_ALLEGRO_HAND) {
+            ah_in_from_tensors(c, S, env, &ain);
+            ah_post(c, S, env, ain, (flags & HA_FLAG_OBS_ONLY) != 0);
+        } else {
+            snapshot_from_tensors(c, S, env, &in);
+            post_step(c, S, env, in, (flags & HA_FLAG_OBS_ONLY) != 0);
+        }
         return;
     }
     load_env(c, S, env);
     if (MODE == MODE_SIMULATE) {
-        run_physics(c, n_calls);
+        run_physics<ND>(c, n_calls);
         store_env(c, S, env);
+        return;
+    }
+    if (TASK == HA_TASK_ALLEGRO_HAND) {
+        // pre_physics_step (allegro_hand.py:586-625): goal / env resets, then targets from the actions
+        bool goal = S.reset_goal_buf[env] != 0, full = S.reset_buf[env] != 0;
+        if (goal || full) ah_reset(c, S, env, flags, goal, full);
+        if (MODE == MODE_RESET) {
+            store_env(c, S, env);
+            return;
+        }
+        ah_controller(c, S, env);
+        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<ND>(c, c.p->control_freq_inv);   // vec_task.py:409-412
+        store_env(c, S, env);
+        if (c.lane == 0) S.progress_buf[env] = S.progress_buf[env] + 1;                // allegro_hand.py:629
+        ah_in_from_lds(c, &ain);
+        ah_post(c, S, env, ain, false);
         return;
     }
     if (MODE == MODE_RESET) {
         task_reset(c, S, env, flags);
-        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics(c, 1);
+        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<ND>(c, 1);
         task_reset_finish(c, S, env);
         store_env(c, S, env);
         return;
@@ -208,7 +258,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     // equivalent. Phase 1: the control_freq_inv physics calls (vec_task.py:409-412). One call site keeps
     // a single copy of the physics code.
     for (int ph = do_reset ? 0 : 1; ph < 2; ph++) {
-        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics(c, ph == 0 ? 1 : c.p->control_freq_inv);
+        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<ND>(c, ph == 0 ? 1 : c.p->control_freq_inv);
         if (ph == 0) task_reset_finish(c, S, env);
     }
     store_env(c, S, env);
@@ -216,19 +266,31 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     post_step(c, S, env, in, false);                           // configurable_vec_task.py:359-390
 }
 
-#define HA_KERNEL(name, MODE)                                                                                   \
+#define HA_KERNEL(name, TASK, MODE)                                                                             \
     extern "C" __global__ void __launch_bounds__(64)                                                          \
         name(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params, ha_state_t st,       \
              int num_envs, int n_calls, uint32_t flags, int stat_slot) {                                        \
-        env_body<MODE>(model, params, st, num_envs, n_calls, flags, stat_slot);                                \
+        env_body<TASK, MODE>(model, params, st, num_envs, n_calls, flags, stat_slot);                          \
     }
-HA_KERNEL(ha_step_kernel, MODE_STEP)
-HA_KERNEL(ha_simulate_kernel, MODE_SIMULATE)
-HA_KERNEL(ha_observe_kernel, MODE_OBSERVE)
-HA_KERNEL(ha_reset_kernel, MODE_RESET)
+HA_KERNEL(ha_step_kernel, HA_TASK_UR5SIH, MODE_STEP)
+HA_KERNEL(ha_simulate_kernel, HA_TASK_UR5SIH, MODE_SIMULATE)
+HA_KERNEL(ha_observe_kernel, HA_TASK_UR5SIH, MODE_OBSERVE)
+HA_KERNEL(ha_reset_kernel, HA_TASK_UR5SIH, MODE_RESET)
+HA_KERNEL(ah_step_kernel, HA_TASK_ALLEGRO_HAND, MODE_STEP)
+HA_KERNEL(ah_simulate_kernel, HA_TASK_ALLEGRO_HAND, MODE_SIMULATE)
+HA_KERNEL(ah_observe_kernel, HA_TASK_ALLEGRO_HAND, MODE_OBSERVE)
+HA_KERNEL(ah_reset_kernel, HA_TASK_ALLEGRO_HAND, MODE_RESET)
 
 typedef void (*env_kernel_t)(const ha_model_t*, const ha_params_t*, ha_state_t, int, int, uint32_t, int);
-static env_kernel_t kernel_for(int mode) {
+static env_kernel_t kernel_for(int task, int mode) {
+    if (task == HA_TASK_ALLEGRO_HAND) {
+        switch (mode) {
+            case MODE_STEP: return ah_step_kernel;
+            case MODE_SIMULATE: return ah_simulate_kernel;
+            case MODE_OBSERVE: return ah_observe_kernel;
+            default: return ah_reset_kernel;
+        }
+    }
     switch (mode) {
         case MODE_STEP: return ha_step_kernel;
         case MODE_SIMULATE: return ha_simulate_kernel;
@@ -253,7 +315,7 @@ struct ha_handle_s {
     ha_model_t* d_model;
     ha_params_t* d_params;
     ha_params_t h_params;
-    int N, NO, D, L, A, B;
+    int N, NO, D, L, A, B, task;
     ha_state_t st;
     int bound;
     int stat_slots;
@@ -289,7 +351,11 @@ int ha_struct_sizes(int32_t* model_size, int32_t* params_size, int32_t* state_si
 
 int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_envs, ha_handle* out) {
     if (!model || !params || !out || num_envs <= 0) return HA_E_ARG;
-    if (model->n_dofs != HA_ND || model->n_links > HA_MAX_LINKS || params->n_objects > NOBJ ||
+    if (params->task != HA_TASK_UR5SIH && params->task != HA_TASK_ALLEGRO_HAND) return HA_E_ARG;
+    // the kernels are compiled for the task's DOF count (register-resident factorization)
+    if (model->n_dofs != (params->task == HA_TASK_ALLEGRO_HAND ? AH_ND : HA_ND)) return HA_E_MODEL;
+    if (model->n_actors < 1 || model->n_bodies < model->n_links + params->n_objects) return HA_E_MODEL;
+    if (model->n_links > HA_MAX_LINKS || params->n_objects > NOBJ ||
         model->n_dofs + 6 * params->n_objects > RS || model->n_link_hulls + model->n_pool + 1 > HA_MAX_HULLS)
         return HA_E_MODEL;
     for (int k = 0; k < model->n_hulls; k++)
@@ -300,8 +366,9 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     h->NO = params->n_objects;
     h->D = model->n_dofs;
     h->L = model->n_links;
-    h->A = 3 + h->NO;
-    h->B = 1 + h->L + 1 + h->NO;
+    h->A = model->n_actors;
+    h->B = model->n_bodies;
+    h->task = params->task;
     h->h_params = *params;
     h->stat_slots = 1;
     HIPCHK(hipMalloc(&h->d_model, sizeof(ha_model_t)));
@@ -309,7 +376,7 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     HIPCHK(hipMemcpy(h->d_model, model, sizeof(ha_model_t), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->d_params, params, sizeof(ha_params_t), hipMemcpyHostToDevice));
     for (int mode : {MODE_STEP, MODE_SIMULATE, MODE_OBSERVE, MODE_RESET})
-        HIPCHK(hipFuncSetAttribute((const void*)kernel_for(mode), hipFuncAttributeMaxDynamicSharedMemorySize,
+        HIPCHK(hipFuncSetAttribute((const void*)kernel_for(h->task, mode), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds_bytes()));
     HIPCHK(hipEventCreate(&h->ev0));
     HIPCHK(hipEventCreate(&h->ev1));
@@ -343,7 +410,7 @@ static int launch(ha_handle h, int mode, int n_calls, uint32_t flags, int slot, 
     hipStream_t s = (hipStream_t)stream;
     bool rec = h->t_ev && h->t_count < h->t_max;
     (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count] : h->ev0, s);
-    hipLaunchKernelGGL(kernel_for(mode), dim3(h->N), dim3(64), lds_bytes(), s, h->d_model, h->d_params, h->st,
+    hipLaunchKernelGGL(kernel_for(h->task, mode), dim3(h->N), dim3(64), lds_bytes(), s, h->d_model, h->d_params, h->st,
                        h->N, n_calls, flags, slot);
     HIPCHK(hipGetLastError());
     (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count + 1] : h->ev1, s);
@@ -443,7 +510,15 @@ int ha_task_step(ha_handle h, uint32_t flags, void* stream) {
     h->step_counter++;
     HIPCHK(hipMemsetAsync(h->st.stats + slot * HA_STAT_SIZE, 0, sizeof(int32_t) * HA_STAT_SIZE, (hipStream_t)stream));
     HIPCHK(hipMemsetAsync(h->st.term_sums + slot * 4, 0, sizeof(float) * 4, (hipStream_t)stream));
-    return launch(h, MODE_STEP, 0, flags, slot, stream);
+    int rc = launch(h, MODE_STEP, 0, flags, slot, stream);
+    if (rc == HA_OK && h->task == HA_TASK_ALLEGRO_HAND && h->st.consecutive_successes) {
+        // consecutive_successes EWMA over the shard's resets of this step (allegro_hand.py:714-717)
+        hipLaunchKernelGGL(ah_consecutive_successes_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                           h->st.stats + slot * HA_STAT_SIZE, h->st.term_sums + slot * 4, h->st.consecutive_successes,
+                           h->h_params.ah_av_factor);
+        HIPCHK(hipGetLastError());
+    }
+    return rc;
 }
 
 int ha_task_observe(ha_handle h, uint32_t flags, void* stream) {

@@ -17,6 +17,7 @@ import os
 import numpy as np
 
 ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "ur5sih_scene.json")
+ALLEGRO_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "allegro_hand_scene.json")
 
 MAX_LINKS, MAX_DOFS, MAX_HULLS, MAX_VERTS, MAX_PLANES = 32, 24, 64, 4096, 8192
 MAX_POOL, MAX_OBJ, MAX_INIT_POSES, MAX_SPLINE_PIECES, N_SPLINES = 32, 3, 4, 8, 8
@@ -302,8 +303,28 @@ DEFAULT_TASK = dict(
 )
 
 
-def build_params(cfg=None):
-    c = dict(DEFAULT_TASK)
+# AllegroHand (config C3): cfg/task/AllegroHand.yaml + tasks/allegro_hand.py
+ALLEGRO_TASK = dict(
+    DEFAULT_TASK, task=TASK_ALLEGRO_HAND, num_actions=16, num_obs=88, n_objects=1,
+    dt=0.01667, substeps=2, control_freq_inv=2, solver_iters=8,          # AllegroHand.yaml:23,160-173
+    contact_margin=0.002, max_depen_vel=1000.0,                          # contact_offset, max_depenetration_velocity
+    max_episode_length=600,                                              # episodeLength
+    dist_reward_scale=-10.0, rot_reward_scale=1.0, rot_eps=0.1, action_penalty_scale=-0.0002,
+    success_tolerance=0.1, reach_goal_bonus=250.0, fall_dist=0.24, fall_penalty=0.0,
+    max_consecutive_successes=0, av_factor=0.1,                          # allegro_hand.py:79 averFactor default
+    reset_position_noise=0.01, reset_dof_pos_noise=0.2, reset_dof_vel_noise=0.0, act_moving_average=1.0,
+    vel_obs_scale=0.2, force_torque_obs_scale=10.0,                      # allegro_hand.py:57-58
+    clip_observations=5.0, clip_actions=1.0,
+    # hand at (0, 0, 0.5); object at hand + (0, -0.2, 0.06); goal_states = object - 0.04 z; goal actor at
+    # goal_states + displacement (allegro_hand.py:284-300,363-365)
+    object_init=(0.0, -0.2, 0.56, 0.0, 0.0, 0.0, 1.0), goal_init=(0.0, -0.2, 0.52),
+    goal_displacement=(-0.2, -0.06, 0.12),
+)
+
+
+def build_params(cfg=None, task=None):
+    c = dict(ALLEGRO_TASK if (task == TASK_ALLEGRO_HAND or (cfg or {}).get("task") == TASK_ALLEGRO_HAND)
+             else DEFAULT_TASK)
     if cfg:
         c.update(cfg)
     p = HaParams()
@@ -330,4 +351,16 @@ def build_params(cfg=None):
     p.task = c.get("task", TASK_UR5SIH)
     p.num_actions = c.get("num_actions", 11)
     p.num_obs = c.get("num_obs", 147)
+    if p.task == TASK_ALLEGRO_HAND:
+        for k in ["dist_reward_scale", "rot_reward_scale", "rot_eps", "action_penalty_scale", "success_tolerance",
+                  "reach_goal_bonus", "fall_dist", "fall_penalty", "max_consecutive_successes", "av_factor",
+                  "reset_position_noise", "reset_dof_pos_noise", "reset_dof_vel_noise", "act_moving_average",
+                  "vel_obs_scale", "force_torque_obs_scale"]:
+            setattr(p, "ah_" + k, c[k])
+        p.ah_object_init[:] = c["object_init"]
+        p.ah_goal_init[:] = c["goal_init"]
+        p.ah_goal_displacement[:] = c["goal_displacement"]
+        # (1.0 - act_moving_average) * prev_targets: python double, cast once (allegro_hand.py:612-613)
+        p.sih_beta = 1.0 - c["act_moving_average"]
+        p.action_dt = c["dt"]
     return p, c

@@ -25,29 +25,36 @@ TORCH_DTYPE = {"float32": torch.float32, "int64": torch.int64, "uint8": torch.ui
 
 
 class HandArmSim:
-    def __init__(self, num_envs, device="cuda:0", task_cfg=None, scene=None, pool_names=None, stats_ring=64):
+    def __init__(self, num_envs, device="cuda:0", task_cfg=None, scene=None, pool_names=None, stats_ring=64,
+                 task=None):
         if not str(device).startswith("cuda"):
             raise _lib.HandArmError("libhandarm_hip runs on a HIP device only (device must be 'cuda:N')")
         self.lib = _lib.load()
         self.device = torch.device(device)
-        self.scene = scene if scene is not None else HM.load_scene()
+        if task is None:
+            task = (task_cfg or {}).get("task", HM.TASK_UR5SIH)
+        self.task = task
+        default_scene = HM.ALLEGRO_ASSET if task == HM.TASK_ALLEGRO_HAND else HM.ASSET
+        self.scene = scene if scene is not None else HM.load_scene(default_scene)
         self.model = HM.build_model(self.scene, pool_names)
-        self.params, self.cfg = HM.build_params(task_cfg)
+        self.params, self.cfg = HM.build_params(task_cfg, task=task)
         self.num_envs = num_envs
         self.n_obj = self.params.n_objects
         self.num_dofs = self.model.n_dofs
         self.num_links = self.model.n_links
-        self.num_actors = 3 + self.n_obj
-        self.num_bodies = 1 + self.num_links + 1 + self.n_obj
+        self.num_actors = self.model.n_actors
+        self.num_bodies = self.model.n_bodies
         self.stats_ring = stats_ring
         spec = HM.state_spec(num_envs, n_links=self.num_links, n_dofs=self.num_dofs, n_obj=self.n_obj,
-                             num_initial_poses=self.params.num_initial_poses)
+                             num_initial_poses=self.params.num_initial_poses, num_actions=self.params.num_actions,
+                             num_obs=self.params.num_obs, n_actors=self.num_actors, n_bodies=self.num_bodies)
         spec["stats"] = ((stats_ring, HM.STAT_SIZE), spec["stats"][1])
         spec["term_sums"] = ((stats_ring, 4), spec["term_sums"][1])
         with torch.cuda.device(self.device):
             self.t = {k: torch.zeros(shape, dtype=TORCH_DTYPE[dt.__name__], device=self.device)
                       for k, (shape, dt) in spec.items()}
         self.t["root_state"].view(num_envs, self.num_actors, 13)[..., 6] = 1.0
+        self.t["goal_state"][:, 6] = 1.0
         self.t["collision_enabled"].fill_(1)
         h = C.c_void_p()
         _lib.check(self.lib.ha_create(C.byref(self.model), C.byref(self.params), num_envs, C.byref(h)), "ha_create")

@@ -348,6 +348,155 @@ def box_hull(half):
     return {"verts": verts, "planes": planes, "center": [0, 0, 0], "radius": float(np.linalg.norm(half))}
 
 
+# ----------------------------------------------------------------------------- AllegroHand (config C3)
+ALLEGRO_URDF = os.path.join(REF, "assets", "urdf", "kuka_allegro_description", "allegro_touch_sensor.urdf")
+ALLEGRO_OUT = os.path.join(os.path.dirname(__file__), "..", "isaacgym-hand-arm_amd", "handarm_hip",
+                           "assets", "allegro_hand_scene.json")
+
+
+def quat_mul_np(a, b):
+    ax, ay, az, aw = a
+    bx, by, bz, bw = b
+    return np.array([aw * bx + ax * bw + ay * bz - az * by, aw * by - ax * bz + ay * bw + az * bx,
+                     aw * bz + ax * by - ay * bx + az * bw, aw * bw - ax * bx - ay * by - az * bz])
+
+
+def quat_axis_angle(axis, angle):
+    a = np.asarray(axis, float) / np.linalg.norm(axis)
+    return np.concatenate([a * math.sin(angle / 2), [math.cos(angle / 2)]])
+
+
+def build_allegro():
+    """allegro_touch_sensor.urdf loaded like tasks/allegro_hand.py:232-268: fix_base_link,
+    collapse_fixed_joints (fixed children merged into their parent body, which keeps the parent's
+    frame), disable_gravity, DOF_MODE_POS with stiffness 3, damping 0.1, effort 0.5, armature 0.001
+    (:264-268). Mass properties come from the URDF inertials (no override_com/inertia), combined with
+    the parallel-axis rule when bodies merge."""
+    base_dir = os.path.join(REF, "assets", "urdf")
+    root = ET.parse(ALLEGRO_URDF).getroot()
+    links = {l.get("name"): l for l in root.findall("link")}
+    parent_joint = {j.find("child").get("link"): j for j in root.findall("joint")}
+    children = {}
+    for j in root.findall("joint"):
+        children.setdefault(j.find("parent").get("link"), []).append(j.find("child").get("link"))
+
+    def T_of(j):
+        o, R = parse_origin(j.find("origin"))
+        T = np.eye(4)
+        T[:3, :3], T[:3, 3] = R, o
+        return T
+    # body of each link (collapse fixed joints) and the link frame in its body frame
+    body_of, T_in_body = {}, {}
+    rootname = [n for n in links if n not in parent_joint][0]
+
+    def visit(n, body, T):
+        body_of[n], T_in_body[n] = body, T
+        for c in children.get(n, []):
+            j = parent_joint[c]
+            if j.get("type") == "fixed":
+                visit(c, body, T @ T_of(j))
+            else:
+                visit(c, c, np.eye(4))
+    visit(rootname, rootname, np.eye(4))
+    bodies = []
+
+    def dfs(b):
+        bodies.append(b)
+        kids = sorted({c for n in links if body_of[n] == b for c in children.get(n, [])
+                       if parent_joint[c].get("type") != "fixed"})
+        for c in kids:
+            dfs(c)
+    dfs(rootname)
+    bidx = {b: i for i, b in enumerate(bodies)}
+    out_links, dofs, hulls = [], [], []
+    for b in bodies:
+        rec = {"name": b, "parent": -1, "joint": None, "type": "fixed", "origin_pos": [0, 0, 0],
+               "origin_quat": [0, 0, 0, 1], "axis": [0, 0, 1], "dof": -1}
+        j = parent_joint.get(b)
+        if j is not None:
+            plink = j.find("parent").get("link")
+            T = T_in_body[plink] @ T_of(j)
+            rec.update(parent=bidx[body_of[plink]], joint=j.get("name"), type=j.get("type"),
+                       origin_pos=T[:3, 3].tolist(), origin_quat=matrix_to_quat(T[:3, :3]).tolist())
+            a = np.array([float(t) for t in j.find("axis").get("xyz").split()])
+            rec["axis"] = (a / np.linalg.norm(a)).tolist()
+            lim = j.find("limit")
+            rec["dof"] = len(dofs)
+            dofs.append({"name": j.get("name"), "link": bidx[b], "lower": float(lim.get("lower")),
+                         "upper": float(lim.get("upper")), "effort": 0.5, "velocity": float(lim.get("velocity")),
+                         "kp": 3.0, "kd": 0.1, "armature": 0.001})
+        mass, mc, Isum = 0.0, np.zeros(3), np.zeros((3, 3))
+        parts = []
+        for n in links:
+            if body_of[n] != b:
+                continue
+            T = T_in_body[n]
+            el = links[n]
+            inn = el.find("inertial")
+            if inn is not None:
+                o, R = parse_origin(inn.find("origin"))
+                m_ = float(inn.find("mass").get("value"))
+                ie = inn.find("inertia")
+                I = np.array([[float(ie.get("ixx")), float(ie.get("ixy")), float(ie.get("ixz"))],
+                              [float(ie.get("ixy")), float(ie.get("iyy")), float(ie.get("iyz"))],
+                              [float(ie.get("ixz")), float(ie.get("iyz")), float(ie.get("izz"))]])
+                Rb = T[:3, :3] @ R
+                parts.append((m_, T[:3, :3] @ o + T[:3, 3], Rb @ I @ Rb.T))
+            for c in el.findall("collision"):
+                g = c.find("geometry/mesh")
+                if g is None:
+                    continue
+                fn = g.get("filename")     # relative to the URDF's directory or to the asset root
+                path = os.path.join(os.path.dirname(ALLEGRO_URDF), fn)
+                if not os.path.exists(path):
+                    path = os.path.join(base_dir, fn)
+                v, _ = load_mesh(path, [float(t) for t in g.get("scale", "1 1 1").split()])
+                o, R = parse_origin(c.find("origin"))
+                v = (v @ R.T + o) @ T[:3, :3].T + T[:3, 3]
+                h = hull_record(v, MAX_LINK_VERTS)
+                h.update(owner="link", index=bidx[b])
+                hulls.append(h)
+        for m_, c_, _ in parts:
+            mass += m_
+            mc += m_ * c_
+        com = mc / mass
+        for m_, c_, I_ in parts:
+            d = c_ - com
+            Isum += I_ + m_ * (np.dot(d, d) * np.eye(3) - np.outer(d, d))
+        rec.update(mass=float(mass), com=com.tolist(), inertia=Isum.reshape(-1).tolist())
+        out_links.append(rec)
+    # hand_start_pose (allegro_hand.py:284-286): p = (0, 0, 0.5), r = Qy(pi) * Qx(0.47 pi) * Qz(0.25 pi)
+    q = quat_mul_np(quat_mul_np(quat_axis_angle([0, 1, 0], math.pi), quat_axis_angle([1, 0, 0], 0.47 * math.pi)),
+                    quat_axis_angle([0, 0, 1], 0.25 * math.pi))
+    robot = {"links": out_links, "dofs": dofs, "base_pos": [0.0, 0.0, 0.5], "base_quat": q.tolist()}
+    return robot, hulls
+
+
+def build_cube(size=0.065, density=400.0):
+    """cube_multicolor_allegro.urdf: box 0.065, density 400 (the URDF gives no mass)."""
+    half = [size / 2] * 3
+    mass = density * size ** 3
+    I = mass / 6.0 * size ** 2
+    return {"name": "cube_multicolor_allegro", "mass": mass, "com": [0, 0, 0],
+            "inertia": [I, 0, 0, 0, I, 0, 0, 0, I], "hull": box_hull(half)}
+
+
+def main_allegro():
+    robot, link_hulls = build_allegro()
+    L = len(robot["links"])
+    scene = {"robot": robot, "link_hulls": link_hulls, "objects": [build_cube()], "table": None,
+             "objects_per_env": 1,
+             # actors hand 0, object 1, goal 2; bodies hand links, object, goal (allegro_hand.py:330-357)
+             "layout": {"n_actors": 3, "actor_robot": 0, "actor_object0": 1, "actor_goal": 2, "actor_table": -1,
+                        "n_bodies": L + 2, "body_robot0": 0, "body_object0": L, "body_goal": L + 1,
+                        "body_table": -1},
+             "generator": "tools/build_model.py --allegro (reference assets @ /root/reference/assets/urdf)"}
+    with open(ALLEGRO_OUT, "w") as f:
+        json.dump(scene, f, indent=None, separators=(",", ":"))
+    print(f"allegro: links={L} dofs={len(robot['dofs'])} hulls={len(link_hulls)} "
+          f"dof order={[d['name'] for d in robot['dofs']]} -> {ALLEGRO_OUT}")
+
+
 def main():
     robot, link_hulls = build_robot()
     objects = [build_object(n) for n in YCB_POOL
@@ -367,4 +516,4 @@ def main():
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(main_allegro() if "--allegro" in sys.argv else main())
