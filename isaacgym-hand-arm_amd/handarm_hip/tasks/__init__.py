@@ -1,6 +1,8 @@
-"""Task registry mirroring isaacgymenvs/tasks/__init__.py (hand-arm path only)."""
+"""Task registry mirroring isaacgymenvs/tasks/__init__.py (the tasks on the BASELINE.json hot path)."""
+from .allegro_hand import AllegroHand
 from .ur5sih_multi_object_manipulation import Ur5SihMultiObjectManipulation
 
 isaacgym_task_map = {
     "Ur5SihMultiObjectManipulation": Ur5SihMultiObjectManipulation,
+    "AllegroHand": AllegroHand,
 }

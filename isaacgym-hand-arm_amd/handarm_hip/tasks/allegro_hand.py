@@ -1,0 +1,162 @@
+"""AllegroHand (in-hand cube reorientation) with the IsaacGymEnvs VecTask surface, backed by libhandarm_hip.
+
+Drop-in for tasks/allegro_hand.py:40 (registered as "AllegroHand" in tasks/__init__.py). Config
+cfg/task/AllegroHand.yaml: 16 DOF Allegro hand (allegro_touch_sensor.urdf, fixed base, gravity off),
+one 0.065 m cube, a goal cube that only carries a pose, observationType "full_state" (88 floats),
+controlFrequencyInv 2, episodeLength 600.
+
+One fused kernel per step (ha_task_step -> ah_step_kernel): goal resets, reset_idx, absolute targets
+with moving average, 2 x 2 physics substeps, refresh, full_state observations, compute_hand_reward; then a
+one-thread kernel updates the global consecutive_successes average (allegro_hand.py:714-717). No host
+syncs on the step path.
+"""
+import numpy as np
+import torch
+
+from .. import model as HM
+from ..sim import HandArmSim
+from .ur5sih_multi_object_manipulation import Box
+
+
+class AllegroHand:
+    def __init__(self, cfg, rl_device="cuda:0", sim_device="cuda:0", graphics_device_id=-1, headless=True,
+                 virtual_screen_capture=False, force_render=False):
+        self.cfg = cfg
+        self.rl_device = rl_device
+        self.device = sim_device
+        env = cfg.get("env", {})
+        c = HM.ALLEGRO_TASK
+        self.num_environments = int(env.get("numEnvs", 16384))
+        self.num_agents = 1
+        self.obs_type = env.get("observationType", "full_state")
+        if self.obs_type != "full_state":
+            raise NotImplementedError("observationType must be 'full_state' (the AllegroHand.yaml default)")
+        if env.get("objectType", "block") != "block" or env.get("useRelativeControl", False) \
+                or float(env.get("forceScale", 0.0)) != 0.0 or env.get("asymmetric_observations", False):
+            raise NotImplementedError("only the AllegroHand.yaml defaults (block, absolute control, no random "
+                                      "forces, symmetric observations) are implemented")
+        self.control_freq_inv = int(env.get("controlFrequencyInv", c["control_freq_inv"]))
+        self.clip_obs = float(env.get("clipObservations", c["clip_observations"]))
+        self.clip_actions = float(env.get("clipActions", c["clip_actions"]))
+        self.max_episode_length = int(env.get("episodeLength", c["max_episode_length"]))
+        task_cfg = dict(task=HM.TASK_ALLEGRO_HAND, control_freq_inv=self.control_freq_inv,
+                        max_episode_length=self.max_episode_length, seed=int(cfg.get("seed", 42)))
+        for key, name in [("distRewardScale", "dist_reward_scale"), ("rotRewardScale", "rot_reward_scale"),
+                          ("rotEps", "rot_eps"), ("actionPenaltyScale", "action_penalty_scale"),
+                          ("successTolerance", "success_tolerance"), ("reachGoalBonus", "reach_goal_bonus"),
+                          ("fallDistance", "fall_dist"), ("fallPenalty", "fall_penalty"),
+                          ("maxConsecutiveSuccesses", "max_consecutive_successes"), ("averFactor", "av_factor"),
+                          ("resetPositionNoise", "reset_position_noise"),
+                          ("resetDofPosRandomInterval", "reset_dof_pos_noise"),
+                          ("resetDofVelRandomInterval", "reset_dof_vel_noise"),
+                          ("actionsMovingAverage", "act_moving_average")]:
+            if key in env:
+                task_cfg[name] = type(c[name])(env[key])
+        self.sim = HandArmSim(self.num_environments, sim_device, task_cfg=task_cfg, task=HM.TASK_ALLEGRO_HAND)
+        self.sim_flags = 0
+        N, t = self.num_environments, self.sim.t
+        self.num_observations, self.num_actions, self.num_states = 88, 16, 0
+        self.obs_buf = t["obs"]
+        self.rew_buf = t["rew"]
+        self.reset_buf = t["reset_buf"]
+        self.reset_goal_buf = t["reset_goal_buf"]
+        self.progress_buf = t["progress_buf"]
+        self.timeout_buf = t["timeout_buf"]
+        self.successes = t["successes"]
+        self.consecutive_successes = t["consecutive_successes"]
+        self.actions_buf = t["actions"]
+        self.goal_states = t["goal_state"]
+        self.dof_state = t["dof_state"]
+        self.dof_force_tensor = t["dof_force"].view(N, 16)
+        self.root_state_tensor = t["root_state"]
+        self.rigid_body_states = t["rigid_body_state"].view(N, -1, 13)
+        self.prev_targets = t["dof_position_targets"]
+        self.shadow_hand_dof_lower_limits = torch.tensor(list(self.sim.model.dof_lower)[:16], device=sim_device)
+        self.shadow_hand_dof_upper_limits = torch.tensor(list(self.sim.model.dof_upper)[:16], device=sim_device)
+        # initial state (allegro_hand.py:282-375, vec_task.py:346-347): everything resets on the first step
+        r = self.root_state_tensor.view(N, 3, 13)
+        r[:, 0, 0:3] = torch.tensor(list(self.sim.model.base_pos), device=sim_device)
+        r[:, 0, 3:7] = torch.tensor(list(self.sim.model.base_quat), device=sim_device)
+        r[:, 1, 0:7] = torch.tensor(c["object_init"], device=sim_device)
+        self.goal_states[:, 0:3] = torch.tensor(c["goal_init"], device=sim_device)
+        self.goal_states[:, 3:7] = torch.tensor([0.0, 0.0, 0.0, 1.0], device=sim_device)
+        r[:, 2, 0:3] = self.goal_states[:, 0:3] + torch.tensor(c["goal_displacement"], device=sim_device)
+        r[:, 2, 6] = 1.0
+        self.reset_buf.fill_(1)
+        self.reset_goal_buf.fill_(1)
+        self.extras = {}
+        self.obs_dict = {}
+        self.control_steps = 0
+        self.total_successes = 0
+        self.total_resets = 0
+
+    # ---------------------------------------------------------------- VecTask surface
+    @property
+    def num_envs(self):
+        return self.num_environments
+
+    @property
+    def num_obs(self):
+        return self.num_observations
+
+    @property
+    def num_acts(self):
+        return self.num_actions
+
+    @property
+    def observation_space(self):
+        return Box(np.ones(self.num_obs) * -np.inf, np.ones(self.num_obs) * np.inf)
+
+    @property
+    def action_space(self):
+        return Box(np.ones(self.num_acts) * -1.0, np.ones(self.num_acts) * 1.0)
+
+    @property
+    def state_space(self):
+        return Box(np.ones(self.num_states) * -np.inf, np.ones(self.num_states) * np.inf)
+
+    def get_number_of_agents(self):
+        return self.num_agents
+
+    def set_train_info(self, env_frames, *args, **kwargs):
+        self.env_frames = env_frames
+
+    def get_env_state(self):
+        return None
+
+    def set_env_state(self, env_state):
+        pass
+
+    def zero_actions(self):
+        return torch.zeros((self.num_envs, self.num_actions), dtype=torch.float32, device=self.rl_device)
+
+    def step(self, actions):
+        """VecTask.step (vec_task.py:390-441) -> pre_physics_step / simulate x2 / post_physics_step, fused."""
+        self.actions_buf.copy_(torch.clamp(actions, -self.clip_actions, self.clip_actions))
+        self.sim.task_step(self.sim_flags)
+        self.control_steps += 1
+        self.extras["time_outs"] = self.timeout_buf.to(torch.bool).to(self.rl_device)
+        self.extras["consecutive_successes"] = self.consecutive_successes.mean()     # allegro_hand.py:393
+        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras
+
+    def reset(self):
+        """VecTask.reset (vec_task.py:459-474): compute_observations only."""
+        self.sim.task_observe(HM.FLAG_OBS_ONLY)
+        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        return self.obs_dict
+
+    def reset_idx(self, env_ids, goal_env_ids=None):
+        """reset_idx (allegro_hand.py:524-584) for the listed envs (and goal resets for goal_env_ids)."""
+        self.reset_buf[env_ids] = 1
+        if goal_env_ids is not None:
+            self.reset_goal_buf[goal_env_ids] = 1
+        self.sim.task_reset(self.sim_flags)
+
+    def reset_done(self):
+        done_env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()
+        if len(done_env_ids) > 0:
+            self.reset_idx(done_env_ids)
+        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        return self.obs_dict, done_env_ids
+

@@ -33,8 +33,14 @@ def load():
 class HostState:
     """numpy buffers for every ha_state_t field."""
 
-    def __init__(self, num_envs, n_obj=3, num_initial_poses=1):
-        self.spec = HM.state_spec(num_envs, n_obj=n_obj, num_initial_poses=num_initial_poses)
+    def __init__(self, num_envs, n_obj=3, num_initial_poses=1, model=None, params=None):
+        kw = {}
+        if model is not None:       # sizes/layout of the model's task (default: Ur5Sih)
+            kw = dict(n_links=model.n_links, n_dofs=model.n_dofs, n_actors=model.n_actors, n_bodies=model.n_bodies)
+        if params is not None:
+            kw.update(num_actions=params.num_actions, num_obs=params.num_obs)
+            n_obj = params.n_objects
+        self.spec = HM.state_spec(num_envs, n_obj=n_obj, num_initial_poses=num_initial_poses, **kw)
         self.arrays = {k: np.zeros(shape, dtype) for k, (shape, dtype) in self.spec.items()}
         self.num_envs = num_envs
 

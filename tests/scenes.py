@@ -43,3 +43,30 @@ def fill_scene(st, num_envs, seed=0, near_hand=0.3, n_obj=3, fingertip_pos=None)
     st["object_indices"][:] = np.stack([rng.permutation(3) for _ in range(N)])
     st["collision_enabled"][:] = 1
     return st
+
+
+def fill_allegro_scene(st, num_envs, lower, upper, seed=0, in_hand=1.0):
+    """AllegroHand: hand joints inside their limits, the cube resting on / just above the palm
+    (object start pose (0, -0.2, 0.56) +- noise, random orientation), random goal orientation."""
+    rng = np.random.default_rng(seed)
+    N = num_envs
+    rs = st["root_state"].reshape(N, 3, 13)
+    rs[:] = 0
+    rs[..., 6] = 1.0
+    rs[:, 1, 0:3] = np.array([0.0, -0.2, 0.56], np.float32) + rng.uniform(-0.01, 0.01, (N, 3))
+    lift = rng.random(N) >= in_hand
+    rs[lift, 1, 2] += 0.1
+    rs[:, 1, 3:7] = rand_quat(rng, (N,))
+    rs[:, 1, 7:10] = rng.uniform(-0.1, 0.1, (N, 3))
+    rs[:, 1, 10:13] = rng.uniform(-0.5, 0.5, (N, 3))
+    rs[:, 2, 0:3] = [-0.2, -0.26, 0.64]
+    rs[:, 2, 3:7] = rand_quat(rng, (N,))
+    st["goal_state"][:, 0:3] = [0.0, -0.2, 0.52]
+    st["goal_state"][:, 3:7] = rs[:, 2, 3:7]
+    ds = st["dof_state"].reshape(N, 16, 2)
+    ds[..., 0] = lower + (upper - lower) * rng.uniform(0.1, 0.9, (N, 16)).astype(np.float32)
+    ds[..., 1] = rng.uniform(-0.5, 0.5, (N, 16))
+    st["sim_targets"][:] = lower + (upper - lower) * rng.uniform(0.0, 1.0, (N, 16)).astype(np.float32)
+    st["object_indices"][:] = 0
+    st["collision_enabled"][:] = 1
+    return st

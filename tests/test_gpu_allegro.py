@@ -1,0 +1,156 @@
+"""GPU parity for the AllegroHand task (config C3), through the C ABI:
+* task math (observe / reward / resets / targets) against the reference-generated goldens
+  (bit-exact done masks and counters; float tolerances stated per check);
+* physics against the C oracle after one gym.simulate (1-ulp-sensitivity-calibrated tolerance, as for
+  Ur5Sih), and physical properties over a full-size episode.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from handarm_hip import model as HM
+from tests import scenes
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def make_sim(n, **cfg):
+    need_gpu()
+    from handarm_hip.sim import HandArmSim
+    cfg = dict(cfg, task=HM.TASK_ALLEGRO_HAND)
+    return HandArmSim(n, "cuda:0", task_cfg=cfg, task=HM.TASK_ALLEGRO_HAND)
+
+
+def put(sim, name, arr):
+    t = sim.t[name]
+    t.copy_(torch.as_tensor(np.ascontiguousarray(arr)).reshape(t.shape).to(t.dtype))
+
+
+def get(sim, name):
+    torch.cuda.synchronize()
+    return sim.t[name].cpu().numpy()
+
+
+def test_allegro_observe_and_reward_against_reference_goldens():
+    d = np.load(os.path.join(G, "allegro_obs_reward.npz"))
+    S, N = d["rew"].shape
+    sim = make_sim(N)
+    for s in range(S):
+        for k, g in [("dof_state", "dof_state"), ("dof_force", "dof_force"), ("root_state", "root_state"),
+                     ("goal_state", "goal_state"), ("actions", "actions"), ("reset_buf", "reset_in"),
+                     ("reset_goal_buf", "reset_goal_in"), ("progress_buf", "progress_in"),
+                     ("successes", "successes_in")]:
+            put(sim, k, d[g][s])
+        sim.task_observe(0)
+        np.testing.assert_allclose(get(sim, "obs"), d["obs"][s], rtol=1e-5, atol=2e-6)
+        np.testing.assert_array_equal(get(sim, "reset_buf"), d["reset"][s])
+        np.testing.assert_array_equal(get(sim, "reset_goal_buf"), d["reset_goal"][s])
+        np.testing.assert_array_equal(get(sim, "progress_buf"), d["progress"][s])
+        np.testing.assert_array_equal(get(sim, "successes"), d["successes"][s])
+        np.testing.assert_allclose(get(sim, "rew"), d["rew"][s], rtol=1e-5, atol=1e-4)
+        # consecutive_successes inputs of the step: number of resets and sum(successes * resets)
+        stats, terms = get(sim, "stats")[0], get(sim, "term_sums")[0]
+        assert stats[0] == d["reset"][s].sum()
+        np.testing.assert_allclose(terms[0], (d["successes"][s] * d["reset"][s]).sum(), rtol=1e-6)
+
+
+def test_allegro_step_with_resets_replayed_against_reference_goldens():
+    """The fused step kernel without physics: goal + env resets from the recorded reference draws,
+    targets from the actions, progress, full_state observations, reward, done, timeout, EWMA."""
+    d = np.load(os.path.join(G, "allegro_steps.npz"))
+    T, N = d["rew"].shape
+    sim = make_sim(N)
+    for k, g in [("dof_state", "dof_state"), ("goal_state", "goal_state"), ("dof_position_targets", "targets"),
+                 ("reset_buf", "reset_in"), ("reset_goal_buf", "reset_goal_in"), ("successes", "successes_in")]:
+        put(sim, k, d[g][0])
+    flags = HM.FLAG_NO_PHYSICS | HM.FLAG_REPLAY_DRAWS
+    for t in range(T):
+        put(sim, "root_state", d["root_state"][t])       # the generator's stand-in for physics between steps
+        put(sim, "progress_buf", d["progress_in"][t])
+        put(sim, "actions", d["actions"][t])
+        put(sim, "reset_draws", d["draws"][t])
+        sim.task_step(flags)
+        np.testing.assert_array_equal(get(sim, "reset_buf"), d["reset"][t])
+        np.testing.assert_array_equal(get(sim, "reset_goal_buf"), d["reset_goal"][t])
+        np.testing.assert_array_equal(get(sim, "progress_buf"), d["progress"][t])
+        np.testing.assert_array_equal(get(sim, "successes"), d["successes"][t])
+        np.testing.assert_array_equal(get(sim, "timeout_buf").astype(bool), d["timeout"][t])
+        np.testing.assert_allclose(get(sim, "dof_position_targets"), d["targets_after"][t], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(get(sim, "sim_targets"), d["targets_after"][t], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(get(sim, "dof_state"), d["dof_after"][t], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(get(sim, "root_state"), d["root_after"][t], rtol=1e-5, atol=2e-6)
+        np.testing.assert_allclose(get(sim, "obs"), d["obs"][t], rtol=1e-5, atol=2e-6)
+        np.testing.assert_allclose(get(sim, "rew"), d["rew"][t], rtol=1e-5, atol=1e-4)
+        np.testing.assert_allclose(get(sim, "consecutive_successes")[0], d["cons"][t][0], rtol=1e-6)
+
+
+def _oracle_and_sim(n, seed):
+    from oracle.oracle_lib import HostState, Oracle
+    sim = make_sim(n)
+    lo = np.array(sim.model.dof_lower[:16], np.float32)
+    up = np.array(sim.model.dof_upper[:16], np.float32)
+    st = HostState(n, model=sim.model, params=sim.params)
+    scenes.fill_allegro_scene(st, n, lo, up, seed=seed)
+    for k in HM.STATE_FIELDS:
+        if k not in ("stats", "term_sums"):
+            put(sim, k, st[k])
+    return sim, Oracle(sim.model, sim.params, n), st
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_allegro_simulate_single_call_matches_oracle(seed):
+    n = 128
+    sim, orc, st = _oracle_and_sim(n, seed)
+    pert = st.copy()
+    pd = pert["dof_state"].reshape(n, 16, 2)
+    pd[..., 0] = np.nextafter(pd[..., 0], np.float32(10))
+    sim.simulate(1)
+    orc.simulate(st, 1)
+    orc.simulate(pert, 1)
+    gd, od, sd = (x.reshape(n, 16, 2) for x in (get(sim, "dof_state"), st["dof_state"], pert["dof_state"]))
+    gr, orr, sr = (x.reshape(n, 3, 13) for x in (get(sim, "root_state"), st["root_state"], pert["root_state"]))
+    assert np.isfinite(gd).all() and np.isfinite(gr).all()
+    for a, b, c_, floor in [(gd[..., 0], od[..., 0], sd[..., 0], 1e-6), (gd[..., 1], od[..., 1], sd[..., 1], 1e-4),
+                            (gr[:, 1, 0:3], orr[:, 1, 0:3], sr[:, 1, 0:3], 1e-6),
+                            (gr[:, 1, 7:13], orr[:, 1, 7:13], sr[:, 1, 7:13], 1e-4)]:
+        err = np.abs(a - b).reshape(n, -1).max(1)
+        sens = np.abs(c_ - b).reshape(n, -1).max(1)
+        print("err max %.2e sens max %.2e" % (err.max(), sens.max()))
+        assert np.mean(err <= 10.0 * np.maximum(sens, floor)) >= 0.95, (err.max(), sens.max())
+    np.testing.assert_allclose(get(sim, "dof_force"), st["dof_force"], rtol=1e-3, atol=2e-3)
+
+
+def test_allegro_vectask_episode_at_full_size():
+    """C3 size (16384 envs): reset -> 120 random-action steps; everything finite, cube mostly held or
+    dropped onto the ground, fall resets fire, consecutive_successes stays a finite average."""
+    need_gpu()
+    from handarm_hip.tasks import AllegroHand
+    n = 16384
+    env = AllegroHand({"env": {"numEnvs": n}}, "cuda:0", "cuda:0")
+    obs = env.reset()["obs"]
+    assert obs.shape == (n, 88)
+    g = torch.Generator(device="cuda:0").manual_seed(42)
+    resets = 0
+    for step in range(120):
+        a = torch.rand((n, 16), device="cuda:0", generator=g) * 2 - 1
+        obs_dict, rew, reset, extras = env.step(a)
+        resets += int(reset.sum())
+    torch.cuda.synchronize()
+    o = obs_dict["obs"]
+    assert torch.isfinite(o).all() and torch.isfinite(rew).all()
+    assert o.abs().max() <= 5.0                                   # clipObservations
+    z = env.root_state_tensor.view(n, 3, 13)[:, 1, 2]
+    assert (z > 0.0).all() and (z < 1.0).all()
+    assert resets > 0                                             # the first step resets every env; falls later
+    cs = float(extras["consecutive_successes"])
+    assert np.isfinite(cs) and cs >= 0.0
+    print(f"allegro full-size: resets {resets}, consecutive_successes {cs:.3f}, "
+          f"cube z in [{float(z.min()):.3f}, {float(z.max()):.3f}]")
