@@ -51,6 +51,68 @@ def algorithmic_bytes_per_env_step(n_links=29, n_dofs=17, n_obj=3, num_obs=147, 
     return sum(reads.values()) + sum(writes.values()), reads, writes
 
 
+def allegro_bytes_per_env_step(n_links=17, n_dofs=16, num_obs=88, num_act=16):
+    """B_api of the AllegroHand step, per env."""
+    f, i64 = 4, 8
+    B = n_links + 2
+    reads = {"dof_state": n_dofs * 2 * f, "prev_targets": n_dofs * f, "object_root": 13 * f, "goal_root": 13 * f,
+             "goal_state": 7 * f, "actions": num_act * f, "reset_progress_goal": 3 * i64, "successes": f}
+    writes = {"dof_state": n_dofs * 2 * f, "dof_force": n_dofs * f, "sim_targets": n_dofs * f,
+              "prev_targets": n_dofs * f, "object_root": 13 * f, "rigid_body_state": B * 13 * f,
+              "net_contact_force": B * 3 * f, "obs": num_obs * f, "rew": f, "reset_progress_goal": 3 * i64,
+              "successes": f, "timeout": 1}
+    return sum(reads.values()) + sum(writes.values()), reads, writes
+
+
+def cpu_baseline_allegro(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0):
+    """AllegroHand on the host: C oracle physics (OpenMP over envs) + numpy task oracle."""
+    from oracle import allegro_oracle as AO
+    from oracle.oracle_lib import HostState, Oracle
+    from handarm_hip import model as HM
+    from tests import scenes
+    model = HM.build_model(HM.load_scene(HM.ALLEGRO_ASSET))
+    params, _ = HM.build_params(task=HM.TASK_ALLEGRO_HAND)
+    lo, up = np.array(model.dof_lower[:16], np.float32), np.array(model.dof_upper[:16], np.float32)
+    orc = Oracle(model, params, num_envs)
+    st = HostState(num_envs, model=model, params=params)
+    scenes.fill_allegro_scene(st, num_envs, lo, up, seed=seed)
+    rng = np.random.default_rng(seed)
+    N = num_envs
+    reset = np.zeros(N, np.int64)
+    goal = np.zeros(N, np.int64)
+    prog = np.zeros(N, np.int64)
+    succ = np.zeros(N, np.float32)
+    cons = np.float32(0)
+    t0 = time.perf_counter()
+    steps = 0
+    while steps < max_steps and (steps < 2 or time.perf_counter() - t0 < min_seconds):
+        steps += 1
+        a = rng.uniform(-1, 1, (N, 16)).astype(np.float32)
+        st["sim_targets"][:] = AO.targets_from_actions(a, st["sim_targets"], lo, up)
+        orc.simulate(st, 2)
+        dof = st["dof_state"].reshape(N, 16, 2)
+        obj = st["root_state"].reshape(N, 3, 13)[:, 1]
+        AO.observations(dof[..., 0], dof[..., 1], st["dof_force"], obj, st["goal_state"], a, lo, up)
+        prog += 1
+        _, reset, goal, prog, succ, cons = AO.reward(obj, st["goal_state"], a, reset, goal, prog, succ, cons)
+        # pre_physics_step of the next step: goal resets and reset_idx for the done envs
+        root = st["root_state"].reshape(N, 3, 13)
+        for e in np.nonzero(reset | goal)[0]:
+            dr = rng.uniform(-1, 1, AO.DRAW_RESET_GOAL + 4).astype(np.float32)
+            base = AO.DRAW_RESET_GOAL if reset[e] else AO.DRAW_GOAL
+            AO.goal_reset(st["goal_state"], root, e, dr[base], dr[base + 1])
+            goal[e] = 0
+            if reset[e]:
+                AO.env_reset(root, dof[..., 0], dof[..., 1], st["sim_targets"], e, dr[AO.DRAW_RESET:AO.DRAW_RESET + 37],
+                             lo, up)
+                reset[e], prog[e], succ[e] = 0, 0, 0
+    dt = time.perf_counter() - t0
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": num_envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{num_envs} envs x {steps} env-steps of the AllegroHand step (C oracle physics, "
+                      f"OpenMP {threads} threads, + numpy task oracle), {dt:.1f} s"}
+
+
 def cpu_baseline(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0):
     """The C oracle (scalar restatement, OpenMP over envs) + numpy task oracle, timed on host cores.
 
@@ -97,11 +159,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--envs", type=int, default=8192, help="envs per GPU")
+    ap.add_argument("--task", choices=["ur5sih", "allegro_hand"], default="ur5sih",
+                    help="ur5sih: BASELINE config 4 shard (default); allegro_hand: config 3")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (8192 ur5sih, 16384 allegro_hand)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-envs", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
+    allegro = args.task == "allegro_hand"
+    if args.envs is None:
+        args.envs = 16384 if allegro else 8192
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -117,12 +184,13 @@ def main():
     random.seed(seed)
     torch.manual_seed(seed)
 
-    from handarm_hip.tasks import Ur5SihMultiObjectManipulation
+    from handarm_hip.tasks import AllegroHand, Ur5SihMultiObjectManipulation
     from handarm_hip import parallel
-    env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": args.envs}, "seed": seed}, device, device)
+    cls = AllegroHand if allegro else Ur5SihMultiObjectManipulation
+    env = cls({"env": {"numEnvs": args.envs}, "seed": seed}, device, device)
     env.reset()
     gen = torch.Generator(device=device).manual_seed(seed)
-    pool = [torch.rand((args.envs, 11), device=device, generator=gen) * 2 - 1 for _ in range(8)]
+    pool = [torch.rand((args.envs, env.num_acts), device=device, generator=gen) * 2 - 1 for _ in range(8)]
     for k in range(args.warmup):
         env.step(pool[k % len(pool)])
     torch.cuda.synchronize()
@@ -138,7 +206,7 @@ def main():
         ev[k][0].record()
         env.step(pool[k % len(pool)])
         ev[k][1].record()
-        if (k + 1) % LOG_INTERVAL == 0:
+        if (k + 1) % LOG_INTERVAL == 0 and not allegro:
             parallel.reduce_episode_stats(env)       # RCCL all-reduce of the episode counters (N > 1)
     torch.cuda.synchronize()
     if world > 1:
@@ -150,15 +218,16 @@ def main():
         elapsed = float(t.item())
     step_ms = [a.elapsed_time(b) for a, b in ev]
     kern_ms = env.sim.kernel_times_ms(args.steps)
-    log = env.log_data
+    log = {} if allegro else env.log_data
     if rank == 0:
         total_env_steps = world * args.envs * args.steps
         value = total_env_steps / elapsed
-        bytes_env, _, _ = algorithmic_bytes_per_env_step()
+        bytes_env, _, _ = allegro_bytes_per_env_step() if allegro else algorithmic_bytes_per_env_step()
+        kernel = "ah_step_kernel" if allegro else "ha_step_kernel"
         kavg = statistics.mean(kern_ms) if kern_ms else float("nan")
         achieved = bytes_env * args.envs / (kavg * 1e-3) / 1e9
         traffic = None
-        tf = os.path.join(ROOT, "profiles", "traffic_step_kernel.json")
+        tf = os.path.join(ROOT, "profiles", "traffic_ah_step_kernel.json" if allegro else "traffic_step_kernel.json")
         if os.path.exists(tf):
             with open(tf) as f:
                 tj = json.load(f)
@@ -166,22 +235,25 @@ def main():
                 traffic = tj.get("hbm_bytes_per_launch")
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args.cpu_envs, args.cpu_seconds)
+            cpu = (cpu_baseline_allegro if allegro else cpu_baseline)(args.cpu_envs, args.cpu_seconds)
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "p50_ms_per_step": statistics.median(step_ms), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded U[-1,1] actions, YCB scene of "
-            "Ur5SihMultiObject.yaml, objects dropped at init)",
-            "config": {"workload": "HandArm Ur5SihMultiObjectManipulation VecTask.step, 3x2 substeps, "
-                                   f"{args.envs} envs/GPU (BASELINE config 4 shard)",
+            "vs_baseline": None, "dtype": "f32",
+            "data": ("synthetic (seeded U[-1,1] actions, AllegroHand.yaml cube scene)" if allegro else
+                     "synthetic (seeded U[-1,1] actions, YCB scene of Ur5SihMultiObject.yaml, objects dropped at init)"),
+            "config": {"workload": (f"AllegroHand VecTask.step, 2x2 substeps, {args.envs} envs/GPU (BASELINE config 3)"
+                                    if allegro else "HandArm Ur5SihMultiObjectManipulation VecTask.step, 3x2 substeps, "
+                                   f"{args.envs} envs/GPU (BASELINE config 4 shard)"),
                        "envs_per_gpu": args.envs, "total_envs": world * args.envs, "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "ha_step_kernel", "kernel_avg_ms": kavg,
+                         "kernel": kernel, "kernel_avg_ms": kavg,
                          "algorithmic_bytes_per_env_step": bytes_env},
             "cpu_baseline": cpu,
             "success_rate_ewma": log.get("success_rate_ewma/overall"),
+            "consecutive_successes": float(env.consecutive_successes.item()) if allegro else None,
         }
         print(json.dumps(out))
     if world > 1:
