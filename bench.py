@@ -30,7 +30,7 @@ HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 LOG_INTERVAL = 16                # rl_games horizon_length (train/Ur5SihMultiObjectManipulationPPO.yaml:65)
 
 
-def algorithmic_bytes_per_env_step(n_links=29, n_dofs=17, n_obj=3, num_obs=147, num_act=11, P=1):
+def algorithmic_bytes_per_env_step(n_links=29, n_dofs=17, n_obj=3, num_obs=147, num_act=11, P=1, dr=False):
     """HBM bytes one env-step of the fused kernel must move (state in + state/obs out), per env.
     B_api of SURVEY.md §8(d): the reference surface materialises body states and contact forces."""
     f, i64 = 4, 8
@@ -42,6 +42,8 @@ def algorithmic_bytes_per_env_step(n_links=29, n_dofs=17, n_obj=3, num_obs=147, 
         "goal_pos": 3 * f, "target_cfg_index": 2 * i64, "obs_cache": n_obj * 7 * f, "goal_reached": 1,
         "object_pos_initial_target": 3 * f, "dof_position_targets": n_dofs * f,
     }
+    if dr:      # per-env DR row: link + object mass scales and frictions
+        reads["dr_scale"] = (2 * n_links + 2 * n_obj) * f
     writes = {
         "dof_state": n_dofs * 2 * f, "sim_targets": n_dofs * f, "object_root_states": n_obj * 13 * f,
         "rigid_body_state": B * 13 * f, "net_contact_force": B * 3 * f, "dof_position_targets": n_dofs * f,
@@ -163,6 +165,7 @@ def main():
                     help="ur5sih: BASELINE config 4 shard (default); allegro_hand: config 3")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (8192 ur5sih, 16384 allegro_hand)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dr", action="store_true", help="ur5sih: domain randomization off")
     ap.add_argument("--cpu-envs", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
@@ -187,7 +190,9 @@ def main():
     from handarm_hip.tasks import AllegroHand, Ur5SihMultiObjectManipulation
     from handarm_hip import parallel
     cls = AllegroHand if allegro else Ur5SihMultiObjectManipulation
-    env = cls({"env": {"numEnvs": args.envs}, "seed": seed}, device, device)
+    # config 4 is quoted with domain randomization on (BASELINE.json configs[3]); --no-dr turns it off
+    env = cls({"env": {"numEnvs": args.envs}, "seed": seed, "task": {"randomize": not (allegro or args.no_dr)}},
+              device, device)
     env.reset()
     gen = torch.Generator(device=device).manual_seed(seed)
     pool = [torch.rand((args.envs, env.num_acts), device=device, generator=gen) * 2 - 1 for _ in range(8)]
@@ -222,7 +227,7 @@ def main():
     if rank == 0:
         total_env_steps = world * args.envs * args.steps
         value = total_env_steps / elapsed
-        bytes_env, _, _ = allegro_bytes_per_env_step() if allegro else algorithmic_bytes_per_env_step()
+        bytes_env, _, _ = allegro_bytes_per_env_step() if allegro else algorithmic_bytes_per_env_step(dr=not args.no_dr)
         kernel = "ah_step_kernel" if allegro else "ha_step_kernel"
         kavg = statistics.mean(kern_ms) if kern_ms else float("nan")
         achieved = bytes_env * args.envs / (kavg * 1e-3) / 1e9
@@ -245,7 +250,8 @@ def main():
                      "synthetic (seeded U[-1,1] actions, YCB scene of Ur5SihMultiObject.yaml, objects dropped at init)"),
             "config": {"workload": (f"AllegroHand VecTask.step, 2x2 substeps, {args.envs} envs/GPU (BASELINE config 3)"
                                     if allegro else "HandArm Ur5SihMultiObjectManipulation VecTask.step, 3x2 substeps, "
-                                   f"{args.envs} envs/GPU (BASELINE config 4 shard)"),
+                                   f"{args.envs} envs/GPU (BASELINE config 4 shard, DR "
+                                   f"{'off' if args.no_dr else 'on'})"),
                        "envs_per_gpu": args.envs, "total_envs": world * args.envs, "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

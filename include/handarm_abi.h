@@ -48,6 +48,12 @@ extern "C" {
 #define HA_N_SPLINES 8
 #define HA_MAX_MPAIRS 192
 #define HA_DRAW_STRIDE 48     /* floats of reset_draws per env (replayed host RNG draws) */
+/* per-env domain-randomization samples (ha_state_t.dr_scale rows) */
+#define HA_DR_LINK_MASS 0      /* [HA_MAX_LINKS] robot link mass (and inertia) scale */
+#define HA_DR_OBJ_MASS 32      /* [HA_MAX_OBJ] object mass (and inertia) scale */
+#define HA_DR_LINK_FRIC 36     /* [HA_MAX_LINKS] robot link friction */
+#define HA_DR_OBJ_FRIC 68      /* [HA_MAX_OBJ] object friction */
+#define HA_DR_SIZE 72
 
 /* tasks (ha_params_t.task) */
 #define HA_TASK_UR5SIH 0        /* Ur5SihMultiObjectManipulation (tasks/hand_arm/task/multi_object_manipulation.py) */
@@ -153,6 +159,15 @@ typedef struct ha_params_t {
     float ah_object_init[7];   /* object start pose (pos, quat xyzw) */
     float ah_goal_init[3];     /* goal_init_state position (object start - 0.04 z) */
     float ah_goal_displacement[3];
+    /* v2: domain randomization (BASELINE config 4 "DR on"; ranges of cfg/task/AllegroKuka.yaml:121-207,
+     * sampled per env at reset on the device). Contact friction = mean of the two bodies' frictions
+     * (PhysX average combine); static geometry keeps `friction`. */
+    int32_t dr_enable;
+    float dr_mass_lo, dr_mass_hi;      /* uniform scaling of link / object mass and inertia */
+    float dr_fric_lo, dr_fric_hi;      /* uniform scaling of friction, then bucketed */
+    int32_t dr_fric_buckets;           /* 250 */
+    float dr_obs_noise;                /* additive gaussian sigma on obs each step */
+    float dr_act_noise;                /* additive gaussian sigma on actions (applied by the host wrapper) */
 } ha_params_t;
 
 /* Device buffers (caller-allocated). Layouts match the Isaac Gym tensors exactly. */
@@ -195,6 +210,7 @@ typedef struct ha_state_t {
     float* successes;           /* [N] AllegroHand consecutive successes in the episode */
     float* goal_state;          /* [N][7] AllegroHand goal_states[:, 0:7] */
     float* consecutive_successes; /* [1] AllegroHand global average (device EWMA) */
+    float* dr_scale;            /* [N][HA_DR_SIZE] per-env DR samples (read when dr_enable) */
 } ha_state_t;
 
 /* stats layout (int32): [0] num_resets, [1] num_successes, then per pool object

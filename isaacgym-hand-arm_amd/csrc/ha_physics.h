@@ -68,7 +68,7 @@ struct EnvLDS {
     float v[RS];
     float oc[NOBJ][4], oq[NOBJ][4], ov[NOBJ][4], ow[NOBJ][4], oIinv[NOBJ][12], om[NOBJ];
     int pool[NOBJ], coll[NOBJ];
-    float cx[MAXC][3], cn[MAXC][3], csep[MAXC];
+    float cx[MAXC][3], cn[MAXC][3], csep[MAXC], cmu[MAXC];
     int ca[MAXC], cb[MAXC];
     int nc, nr, pad0, pad1;
     union {
@@ -84,7 +84,15 @@ struct SimCtx {
     const ha_params_t* __restrict__ p;
     EnvLDS* s;
     int lane, D, NO, L;
+    const float* dr;        // this env's domain-randomization row (HA_DR_*), or null when DR is off
 };
+
+// friction of a contact body (link 100+L, object o, static -1) and of a contact (PhysX average combine)
+HD float body_friction(const SimCtx& c, int b) {
+    if (!c.dr || b < 0) return c.p->friction;
+    return b >= 100 ? c.dr[HA_DR_LINK_FRIC + (b - 100)] : c.dr[HA_DR_OBJ_FRIC + b];
+}
+HD float contact_friction(const SimCtx& c, int a, int b) { return 0.5f * (body_friction(c, a) + body_friction(c, b)); }
 
 // 64-lane sum: DPP butterfly inside each 16-lane row (xor1, xor2, half-mirror, mirror), then the four
 // row sums via v_readlane. Every lane gets the same bits; the oracle emulates this exact tree.
@@ -186,7 +194,10 @@ HD void dynamics(SimCtx& c) {
         qmat(lq, R);
         f3 cc = ld3(s.lp[i]) + qrot(lq, ld3(m.link_com[i]));
         rart3(R, m.link_inertia[i], Iw);
-        float mm = m.link_mass[i];
+        float sc = c.dr ? c.dr[HA_DR_LINK_MASS + i] : 1.0f;     // DR: mass and inertia scale together
+#pragma unroll
+        for (int k = 0; k < 9; k++) Iw[k] = Iw[k] * sc;
+        float mm = m.link_mass[i] * sc;
         I.m = mm;
         I.h = cc * mm;
         float ccd = dot3(cc, cc);
@@ -390,6 +401,7 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
             st3(s.cx[slot], P[t]);
             st3(s.cn[slot], n);
             s.csep[slot] = S[t];
+            s.cmu[slot] = contact_friction(c, a, b);
             s.ca[slot] = a;
             s.cb[slot] = b;
         }
@@ -761,10 +773,13 @@ HD void substep(SimCtx& c, float hdt) {
         float R[9], Iw[9], Ii[9];
         qmat(ldq(s.oq[o]), R);
         rart3(R, m.pool_inertia[s.pool[o]], Iw);
+        float sc = c.dr ? c.dr[HA_DR_OBJ_MASS + o] : 1.0f;
+#pragma unroll
+        for (int k = 0; k < 9; k++) Iw[k] = Iw[k] * sc;
         inv3(Iw, Ii);
 #pragma unroll
         for (int k = 0; k < 9; k++) s.oIinv[o][k] = Ii[k];
-        s.om[o] = m.pool_mass[s.pool[o]];
+        s.om[o] = m.pool_mass[s.pool[o]] * sc;
     }
     wsync();
     PROF(2);
@@ -776,8 +791,9 @@ HD void substep(SimCtx& c, float hdt) {
     int nc = s.nc;
     int nr = 3 * nc;    // nc <= MAXC -> <= MAXR rows
     int r = lane;
-    float vt = 0.f, winv = 0.f, lam = 0.f;
+    float vt = 0.f, winv = 0.f, lam = 0.f, cmu = 0.f;
     if (r < nr) {
+        cmu = s.cmu[r / 3];
         float* Jr = s.u.rows.J + r * RS;
         for (int k = 0; k < RS; k++) Jr[k] = 0.0f;
         int ci = r / 3, k = r % 3;
@@ -856,7 +872,6 @@ HD void substep(SimCtx& c, float hdt) {
     PROF(5);
     // ---- projected Gauss-Seidel (velocity form): joint rows d = 0..D-1 (drive, lower, upper), then
     //      contact rows r = 0..nr-1.  Same row order and arithmetic as the oracle.
-    const float mu = p.friction;
     const float* J = s.u.rows.J;
     const float* Y = s.u.rows.Y;
     for (int it = 0; it < p.solver_iters; it++) {
@@ -915,7 +930,7 @@ HD void substep(SimCtx& c, float hdt) {
             float n0 = l0 - (jv0 - bcast(vt, r0)) * bcast(winv, r0);
             n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
             float d0 = n0 - l0;
-            float hi = mu * n0;
+            float hi = bcast(cmu, r0) * n0;
             jv1 = jv1 + bcast(ca0, r0 + 1) * d0;
             float n1 = l1 - (jv1 - bcast(vt, r0 + 1)) * bcast(winv, r0 + 1);
             n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);

@@ -114,6 +114,41 @@ HD float uniform01(uint64_t seed, uint32_t env, uint32_t episode, uint32_t k) {
     return (h >> 8) * (1.0f / 16777216.0f);
 }
 
+// standard normal by Box-Muller from two counter-based uniforms
+HD float gauss01(uint64_t seed, uint32_t env, uint32_t ctr, uint32_t k) {
+    float u1 = uniform01(seed ^ 0x9E3779B97F4A7C15ULL, env, ctr, 2 * k);
+    float u2 = uniform01(seed ^ 0x9E3779B97F4A7C15ULL, env, ctr, 2 * k + 1);
+    u1 = fmaxf(u1, 1.0f / 16777216.0f);
+    return sqrtf(-2.0f * logf(u1)) * cosf(6.28318530717958647692f * u2);
+}
+
+// Domain randomization samples of one env at reset (BASELINE config 4 "DR on"; dr_utils.py:71-147 semantics:
+// uniform scaling per rigid body, friction scaling then bucketing into num_buckets values over the range)
+HD float dr_bucket(float v, float lo, float hi, int nb) {
+    float w = hi - lo;
+    int i = (int)floorf((v - lo) / w * (float)nb);
+    i = i < 0 ? 0 : (i >= nb ? nb - 1 : i);
+    return w * (float)i / (float)nb + lo;
+}
+HD void dr_sample(const SimCtx& c, const ha_state_t& st, int env) {
+    const ha_params_t& p = *c.p;
+    if (!p.dr_enable || !st.dr_scale) return;
+    int lane = c.lane;
+    float* row = st.dr_scale + (size_t)env * HA_DR_SIZE;
+    uint32_t ep = st.episode[env];
+    auto u = [&](int k, float lo, float hi) { return lo + (hi - lo) * uniform01(p.seed, env, ep, 1000 + k); };
+    if (lane < HA_MAX_LINKS) {
+        row[HA_DR_LINK_MASS + lane] = u(lane, p.dr_mass_lo, p.dr_mass_hi);
+        row[HA_DR_LINK_FRIC + lane] = dr_bucket(p.friction * u(100 + lane, p.dr_fric_lo, p.dr_fric_hi), p.dr_fric_lo,
+                                                p.dr_fric_hi, p.dr_fric_buckets);
+    }
+    if (lane < NOBJ) {
+        row[HA_DR_OBJ_MASS + lane] = u(50 + lane, p.dr_mass_lo, p.dr_mass_hi);
+        row[HA_DR_OBJ_FRIC + lane] = dr_bucket(p.friction * u(150 + lane, p.dr_fric_lo, p.dr_fric_hi), p.dr_fric_lo,
+                                               p.dr_fric_hi, p.dr_fric_buckets);
+    }
+}
+
 // ----------------------------------------------------------------------------- reset_idx (steady state)
 // multi_object_manipulation.py:62-71 + _reset_objects :73-91, _reset_target_object :193-209,
 // _reset_goal :211-230 + _get_random_object_pos :175-184, Ur5Sih._reset_ur5sih (ur5sih.py:616-632),
@@ -134,6 +169,7 @@ HD void task_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags) {
 #pragma unroll
         for (int k = 0; k < 3; k++) dr[2 + k] = uniform01(p.seed, env, ep, 2 + k);
     }
+    dr_sample(c, st, env);
     int cfg = (int)dr[0], tgt_obj = (int)dr[1];
     cfg = cfg < 0 ? 0 : (cfg >= P ? P - 1 : cfg);
     tgt_obj = tgt_obj < 0 ? 0 : (tgt_obj >= NO ? NO - 1 : tgt_obj);
@@ -238,9 +274,15 @@ HD void post_step(SimCtx& c, const ha_state_t& st, int env, const ObsIn& in, boo
         ob[e] = v;
     }
     wsync();
+    // DR observation noise (vec_task.py:427-428: applied to obs_buf after post_physics_step, not to the
+    // teacher observations and not in VecTask.reset)
+    bool noise = !obs_only && p.dr_enable;
+    uint32_t nctr = (st.episode[env] << 12) ^ (uint32_t)st.progress_buf[env];
     for (int e = lane; e < NUM_OBS; e += 64) {
-        st.obs[(size_t)env * NUM_OBS + e] = ob[e];
-        st.teacher_obs[(size_t)env * NUM_OBS + e] = ob[e];
+        float v = ob[e];
+        st.teacher_obs[(size_t)env * NUM_OBS + e] = v;
+        if (noise) v = v + p.dr_obs_noise * gauss01(p.seed, env, nctr, e);
+        st.obs[(size_t)env * NUM_OBS + e] = v;
     }
     if (obs_only) return;     // VecTask.reset(): compute_observations without a refresh
     // refresh the observable cache with the current object pose

@@ -203,6 +203,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.D = ND;                     // == model->n_dofs (ha_create); a constant, so loops over D unroll
     c.NO = params->n_objects;
     c.L = model->n_links;
+    c.dr = (params->dr_enable && st.dr_scale) ? st.dr_scale + (size_t)env * HA_DR_SIZE : nullptr;
     ObsIn& in = c.s->u.pd.in;
     AhIn& ain = *reinterpret_cast<AhIn*>(&c.s->u.pd.in);
     ha_state_t S = st;

@@ -24,6 +24,8 @@ MAX_POOL, MAX_OBJ, MAX_INIT_POSES, MAX_SPLINE_PIECES, N_SPLINES = 32, 3, 4, 8, 8
 MAX_MPAIRS = 192
 STAT_SIZE = 2 + 2 * MAX_POOL
 DRAW_STRIDE = 48
+DR_SIZE = 72
+DR_LINK_MASS, DR_OBJ_MASS, DR_LINK_FRIC, DR_OBJ_FRIC = 0, 32, 36, 68
 TASK_UR5SIH, TASK_ALLEGRO_HAND = 0, 1
 
 FLAG_NO_PHYSICS = 1
@@ -87,6 +89,8 @@ class HaParams(C.Structure):
         ("ah_reset_position_noise", f32), ("ah_reset_dof_pos_noise", f32), ("ah_reset_dof_vel_noise", f32),
         ("ah_act_moving_average", f32), ("ah_vel_obs_scale", f32), ("ah_force_torque_obs_scale", f32),
         ("ah_object_init", arr(f32, 7)), ("ah_goal_init", arr(f32, 3)), ("ah_goal_displacement", arr(f32, 3)),
+        ("dr_enable", i32), ("dr_mass_lo", f32), ("dr_mass_hi", f32), ("dr_fric_lo", f32), ("dr_fric_hi", f32),
+        ("dr_fric_buckets", i32), ("dr_obs_noise", f32), ("dr_act_noise", f32),
     ]
 
 
@@ -99,7 +103,7 @@ STATE_FIELDS = ["root_state", "rigid_body_state", "dof_state", "net_contact_forc
                 "object_configuration_indices", "object_indices", "object_pos_initial", "object_quat_initial",
                 "ur5_target", "servo", "smoothed", "obs_cache", "reset_draws", "episode", "stats", "term_sums",
                 "flags", "collision_enabled", "dof_force", "reset_goal_buf", "successes", "goal_state",
-                "consecutive_successes"]
+                "consecutive_successes", "dr_scale"]
 
 
 def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, num_actions=11, num_obs=147,
@@ -121,7 +125,7 @@ def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, nu
         "reset_draws": ((N, DRAW_STRIDE), f), "episode": ((N,), u32), "stats": ((STAT_SIZE,), i32),
         "term_sums": ((4,), f), "flags": ((4,), i32), "collision_enabled": ((N, n_obj), u8),
         "dof_force": ((N, D), f), "reset_goal_buf": ((N,), i64), "successes": ((N,), f), "goal_state": ((N, 7), f),
-        "consecutive_successes": ((1,), f),
+        "consecutive_successes": ((1,), f), "dr_scale": ((N, DR_SIZE), f),
     }
 
 
@@ -295,6 +299,8 @@ DEFAULT_TASK = dict(
     joint_limit_margin=0.02, n_objects=3, num_initial_poses=1, max_episode_length=200,
     sih_alpha=0.8, reward_reaching=1.0, reward_lifting=5.0, reward_goal=50.0, reward_success=50.0,
     lifting_threshold=0.05, goal_threshold=0.05, goal_pos=(0.28, 0.58, 0.8), goal_noise=(0.15, 0.15, 0.1),
+    dr_enable=0, dr_mass=(0.5, 1.5), dr_friction=(0.7, 1.3), dr_friction_buckets=250, dr_obs_noise=0.002,
+    dr_act_noise=0.05,     # BASELINE config 4 "DR on" (ranges of AllegroKuka.yaml:121-207)
     drop_pos=(0.28, 0.58, 1.5), drop_noise=(0.1, 0.1, 0.0), drop_num_steps=100,
     reset_pose=(0.6985, -1.4106, 1.2932, 0.1174, 0.6983, 1.5708, 0., 0., 0., 0., 0., 0., 0., 0., -1.571, 0., 0.),
     bringup_pose=(0., -1.571, 0., 0., 0., 0., 0., 0., 0., 0., 0., 0., 0., 0., -1.571, 0., 0.),
@@ -348,6 +354,12 @@ def build_params(cfg=None, task=None):
         p.spline_pieces[i] = tab.shape[1]
         sp[i, :, :tab.shape[1]] = tab
     p.thumb_opposition_gain = np.float32(-1.571 / 2675)
+    p.dr_enable = int(c.get("dr_enable", 0))
+    p.dr_mass_lo, p.dr_mass_hi = c.get("dr_mass", (0.5, 1.5))
+    p.dr_fric_lo, p.dr_fric_hi = c.get("dr_friction", (0.7, 1.3))
+    p.dr_fric_buckets = int(c.get("dr_friction_buckets", 250))
+    p.dr_obs_noise = c.get("dr_obs_noise", 0.002)
+    p.dr_act_noise = c.get("dr_act_noise", 0.05)
     p.task = c.get("task", TASK_UR5SIH)
     p.num_actions = c.get("num_actions", 11)
     p.num_obs = c.get("num_obs", 147)

@@ -56,6 +56,13 @@ class HandArmSim:
         self.t["root_state"].view(num_envs, self.num_actors, 13)[..., 6] = 1.0
         self.t["goal_state"][:, 6] = 1.0
         self.t["collision_enabled"].fill_(1)
+        # domain-randomization rows start at the nominal values (mass scale 1, friction) until the first
+        # reset samples them (ha_task.h dr_sample)
+        dr = self.t["dr_scale"]
+        dr[:, HM.DR_LINK_MASS:HM.DR_LINK_MASS + HM.MAX_LINKS] = 1.0
+        dr[:, HM.DR_OBJ_MASS:HM.DR_OBJ_MASS + HM.MAX_OBJ] = 1.0
+        dr[:, HM.DR_LINK_FRIC:HM.DR_LINK_FRIC + HM.MAX_LINKS] = self.params.friction
+        dr[:, HM.DR_OBJ_FRIC:HM.DR_OBJ_FRIC + HM.MAX_OBJ] = self.params.friction
         h = C.c_void_p()
         _lib.check(self.lib.ha_create(C.byref(self.model), C.byref(self.params), num_envs, C.byref(h)), "ha_create")
         self.h = h

@@ -74,6 +74,11 @@ class Ur5SihMultiObjectManipulation:
         task_cfg = dict(control_freq_inv=self.control_freq_inv, max_episode_length=self.max_episode_length,
                         n_objects=self.num_objects, num_initial_poses=self.num_initial_poses,
                         seed=int(cfg.get("seed", 42)))
+        # BASELINE config 4 "DR on": device-side domain randomization (mass / friction resampled at reset,
+        # observation noise in the step kernel, action noise below). The reference's Ur5Sih `randomize`
+        # flag has no consumer, so this is the build's own switch: cfg["task"]["randomize"].
+        self.randomize = bool(_get(cfg, "task.randomize", False))
+        task_cfg["dr_enable"] = int(self.randomize)
         rew = _get(cfg, "rl.reward", None)
         if rew:
             for k in REWARD_TERMS:
@@ -327,6 +332,8 @@ class Ur5SihMultiObjectManipulation:
     def step(self, actions):
         if not self.objects_dropped and bool(self.reset_buf.any()):
             self._drop_initialisation()
+        if self.randomize:      # action noise before the clamp (vec_task.py:400-404)
+            actions = actions + self.sim.params.dr_act_noise * torch.randn_like(actions)
         action_tensor = torch.clamp(actions, -self.clip_actions, self.clip_actions)
         self.actions_buf.copy_(action_tensor)
         if self._stat_pending == self.sim.stats_ring:

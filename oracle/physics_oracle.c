@@ -141,7 +141,10 @@ typedef struct {
     int coll[NOBJ];
     float cforce[1 + HA_MAX_LINKS + 1 + NOBJ][3];
     float dforce[HA_MAX_DOFS];      /* joint force of the last substep: (drive + lower - upper impulse) / h */
+    const float* dr;                /* this env's DR row (HA_DR_*) or NULL (ha_physics.h SimCtx::dr) */
 } env_t;
+
+static float body_friction(const hao_handle h, const env_t* e, int b);
 
 static int dofn(const hao_handle h) { return h->D; }
 
@@ -172,7 +175,9 @@ static void link_inertia(const hao_handle h, const env_t* e, int i, sinert* I) {
     qmat(e->lq[i], R);
     v3 c = add(e->lp[i], qrot(e->lq[i], ld3(m->link_com[i])));
     rart(R, m->link_inertia[i], Iw);
-    float mm = m->link_mass[i];
+    float sc = e->dr ? e->dr[HA_DR_LINK_MASS + i] : 1.0f;
+    for (int k = 0; k < 9; k++) Iw[k] = Iw[k] * sc;
+    float mm = m->link_mass[i] * sc;
     I->m = mm;
     I->h = mul(c, mm);
     float cc = dot(c, c);
@@ -536,6 +541,12 @@ static void tangents(v3 n, v3* t1, v3* t2) {
 }
 
 /* One substep; the same operation order as ha_physics.h substep (the GPU lane-parallel version). */
+/* friction of a contact body: link 100+L, object o, static -1 (PhysX average combine per contact) */
+static float body_friction(const hao_handle h, const env_t* e, int b) {
+    if (!e->dr || b < 0) return h->p.friction;
+    return b >= 100 ? e->dr[HA_DR_LINK_FRIC + (b - 100)] : e->dr[HA_DR_OBJ_FRIC + b];
+}
+
 static void substep(const hao_handle h, env_t* e, float hdt) {
     const ha_model_t* m = &h->m;
     const ha_params_t* p = &h->p;
@@ -563,8 +574,10 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
         float R[9], Iw[9];
         qmat(e->oq[o], R);
         rart(R, m->pool_inertia[e->pool[o]], Iw);
+        float sc = e->dr ? e->dr[HA_DR_OBJ_MASS + o] : 1.0f;
+        for (int k = 0; k < 9; k++) Iw[k] = Iw[k] * sc;
         inv3(Iw, e->oIinv[o]);
-        e->om[o] = m->pool_mass[e->pool[o]];
+        e->om[o] = m->pool_mass[e->pool[o]] * sc;
     }
     /* contacts -> rows (normal, friction 1, friction 2 per contact) */
     contact_t cs[MAXC];
@@ -631,7 +644,6 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
     }
     /* projected Gauss-Seidel, velocity form: joint rows d = 0..D-1 (drive, lower, upper), then the
      * contact rows; v is updated after every row */
-    const float mu = p->friction;
     for (int it = 0; it < p->solver_iters; it++) {
         for (int d = 0; d < D; d++) {
             const float* mrow = Minv + d * D;
@@ -670,7 +682,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
             float n0 = l0 - (jv0 - R.vt[r0]) * winv[r0];
             n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
             float d0 = n0 - l0;
-            float hi = mu * n0;
+            float hi = (0.5f * (body_friction(h, e, cs[c].a) + body_friction(h, e, cs[c].b))) * n0;
             jv1 = jv1 + a10[c] * d0;
             float n1 = l1 - (jv1 - R.vt[r0 + 1]) * winv[r0 + 1];
             n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
@@ -808,6 +820,7 @@ int hao_struct_sizes(int32_t* model_size, int32_t* params_size, int32_t* state_s
 static void simulate_env(const hao_handle h, ha_state_t* S, int env, int n_calls) {
     env_t e;
     load_env(h, S, env, &e);
+    e.dr = (h->p.dr_enable && S->dr_scale) ? S->dr_scale + (size_t)env * HA_DR_SIZE : NULL;
     float hdt = h->p.dt / (float)h->p.substeps;
     for (int c = 0; c < n_calls; c++)
         for (int s = 0; s < h->p.substeps; s++) substep(h, &e, hdt);
