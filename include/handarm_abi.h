@@ -23,6 +23,8 @@
  *                                  (vec_task.py:390-441 -> configurable_vec_task.py:347-414)
  *   ha_task_observe                post_step callbacks + compute_reward + compute_observations alone
  *   ha_task_reset                  reset_idx steady state (multi_object_manipulation.py:33-71)
+ * The fused entry points serve three tasks (ha_params_t.task): Ur5Sih (above), AllegroHand
+ * (allegro_hand.py:586-633) and AllegroKuka (allegro_kuka_base.py:1355-1447).
  */
 #ifndef HANDARM_ABI_H
 #define HANDARM_ABI_H
@@ -33,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 2
+#define HA_ABI_VERSION 3
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -47,7 +49,7 @@ extern "C" {
 #define HA_MAX_SPLINE_PIECES 8
 #define HA_N_SPLINES 8
 #define HA_MAX_MPAIRS 192
-#define HA_DRAW_STRIDE 48     /* floats of reset_draws per env (replayed host RNG draws) */
+#define HA_DRAW_STRIDE 80     /* floats of reset_draws per env (replayed host RNG draws) */
 /* per-env domain-randomization samples (ha_state_t.dr_scale rows) */
 #define HA_DR_LINK_MASS 0      /* [HA_MAX_LINKS] robot link mass (and inertia) scale */
 #define HA_DR_OBJ_MASS 32      /* [HA_MAX_OBJ] object mass (and inertia) scale */
@@ -58,6 +60,23 @@ extern "C" {
 /* tasks (ha_params_t.task) */
 #define HA_TASK_UR5SIH 0        /* Ur5SihMultiObjectManipulation (tasks/hand_arm/task/multi_object_manipulation.py) */
 #define HA_TASK_ALLEGRO_HAND 1  /* AllegroHand in-hand reorientation (tasks/allegro_hand.py) */
+#define HA_TASK_ALLEGRO_KUKA 2  /* AllegroKuka regrasping / reorientation (tasks/allegro_kuka/) */
+
+/* AllegroKuka per-env task state (ha_state_t.task_state rows, floats; allegro_kuka_base.py:330-389) */
+#define HA_AK_LIFTED 0          /* lifted_object (0/1) */
+#define HA_AK_CLOSEST_KP 1      /* closest_keypoint_max_dist (-1 = unset) */
+#define HA_AK_CLOSEST_FT 2      /* [4] closest_fingertip_dist */
+#define HA_AK_FURTHEST 6        /* furthest_hand_dist */
+#define HA_AK_NEAR_GOAL 7       /* near_goal_steps */
+#define HA_AK_PREV_SUCC 8       /* prev_episode_successes */
+#define HA_AK_TRUE_OBJ 9        /* true_objective */
+#define HA_AK_PREV_TRUE_OBJ 10  /* prev_episode_true_objective */
+#define HA_AK_FORCE_PROB 11     /* random_force_prob */
+#define HA_AK_RB_FORCE 12       /* [3] rb_forces of the object (LOCAL_SPACE) */
+#define HA_AK_RNG 15            /* per-env step counter of the device RNG (uint32 bits) */
+#define HA_AK_REW_EP 16         /* [12] rewards_episode, in the reference's reward_keys order */
+#define HA_AK_KP 32             /* [4][3] object_keypoint_offsets (static per env, host-computed) */
+#define HA_AK_TS 48
 
 /* error codes */
 #define HA_OK 0
@@ -168,6 +187,32 @@ typedef struct ha_params_t {
     int32_t dr_fric_buckets;           /* 250 */
     float dr_obs_noise;                /* additive gaussian sigma on obs each step */
     float dr_act_noise;                /* additive gaussian sigma on actions (applied by the host wrapper) */
+    /* v3: AllegroKuka (cfg/task/AllegroKuka.yaml:9-94, env/regrasping.yaml, allegro_kuka_base.py:53-400) */
+    int32_t ak_subtask;                /* 0 regrasping, 1 reorientation */
+    int32_t ak_num_keypoints;          /* 1 (regrasping) or 4 */
+    float ak_keypoints[4][3];          /* unit keypoint offsets (_object_keypoint_offsets) */
+    float ak_object_base_size, ak_keypoint_scale;
+    float ak_initial_tolerance, ak_target_tolerance;
+    float ak_lifting_rew_scale, ak_lifting_bonus, ak_lifting_bonus_threshold;
+    float ak_keypoint_rew_scale, ak_distance_delta_rew_scale, ak_reach_goal_bonus;
+    float ak_kuka_actions_penalty_scale, ak_allegro_actions_penalty_scale;
+    int32_t ak_success_steps, ak_max_consecutive_successes;
+    float ak_bonus_rew;                /* reach_goal_bonus / success_steps (python float, rounded) */
+    float ak_reset_noise[3];           /* resetPositionNoiseX/Y/Z */
+    float ak_dof_noise_arm, ak_dof_noise_fingers, ak_dof_vel_noise;
+    float ak_force_scale, ak_force_prob_lo, ak_force_prob_hi;
+    float ak_force_decay_step;         /* force_decay ** (dt / force_decay_interval) in fp32 (torch.pow) */
+    float ak_object_rb_mass;           /* object_rb_masses: env 0's object mass (allegro_kuka_base.py:734-735) */
+    float ak_dof_speed_scale;          /* arm relative-target speed (dofSpeedScale) */
+    float ak_act_moving_average, ak_one_minus_ama;
+    float ak_clamp_abs_obs;
+    float ak_object_init[3];           /* object_start_pose position (identity rotation) */
+    float ak_goal_init[3];             /* reorientation goal start position */
+    float ak_target_origin[3], ak_target_lo[3], ak_target_size[3];   /* target volume (min corner, size) */
+    float ak_palm_offset[3];
+    float ak_fingertip_offsets[4][3];
+    int32_t ak_palm_link, ak_fingertip_links[4];
+    int32_t ak_num_arm_dofs;           /* 7 */
 } ha_params_t;
 
 /* Device buffers (caller-allocated). Layouts match the Isaac Gym tensors exactly. */
@@ -211,6 +256,14 @@ typedef struct ha_state_t {
     float* goal_state;          /* [N][7] AllegroHand goal_states[:, 0:7] */
     float* consecutive_successes; /* [1] AllegroHand global average (device EWMA) */
     float* dr_scale;            /* [N][HA_DR_SIZE] per-env DR samples (read when dr_enable) */
+    /* v3 */
+    float* object_scale;        /* [N][n_obj][3] per-env object dimension scale of the pool hull (null = 1);
+                                 * mass scales with the volume, inertia with the scaled second moments */
+    float* object_force;        /* [N][n_obj][3] world force at the object COM for the next ha_simulate
+                                 * (gym.apply_rigid_body_force_tensors; consumed, i.e. zeroed, by it) */
+    float* task_state;          /* [N][HA_AK_TS] AllegroKuka per-env task state */
+    float* task_scalars;        /* [4] AllegroKuka host-curriculum scalars: success_tolerance,
+                                 * tolerance objective, 1 if tolerance > target, keypoint success tolerance */
 } ha_state_t;
 
 /* stats layout (int32): [0] num_resets, [1] num_successes, then per pool object

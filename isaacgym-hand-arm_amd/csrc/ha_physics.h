@@ -68,6 +68,8 @@ struct EnvLDS {
     float v[RS];
     float oc[NOBJ][4], oq[NOBJ][4], ov[NOBJ][4], ow[NOBJ][4], oIinv[NOBJ][12], om[NOBJ];
     int pool[NOBJ], coll[NOBJ];
+    float osc[NOBJ][4];     // per-env object dimension scale of the pool hull; [3] = 1 when scaled
+    float ofx[NOBJ][4];     // world force on the object COM for this physics call (apply_rigid_body_force)
     float cx[MAXC][3], cn[MAXC][3], csep[MAXC], cmu[MAXC];
     int ca[MAXC], cb[MAXC];
     int nc, nr, pad0, pad1;
@@ -335,16 +337,46 @@ HD void factor_inverse(SimCtx& c) {
 
 struct PoseF { f3 p; qf q; };
 
+// Per-env object dimensions (AllegroKuka's cuboid family): the pool hull of object o is scaled by
+// diag(osc[o]) in its body frame. Unscaled bodies (links, static geometry, objects without a scale) take
+// the unscaled expressions, bit for bit.
+HD bool body_scaled(const SimCtx& c, int b) { return b >= 0 && b < c.NO && c.s->osc[b][3] != 0.0f; }
+HD f3 scale3(const SimCtx& c, int b, f3 v) {
+    if (!body_scaled(c, b)) return v;
+    const float* sc = c.s->osc[b];
+    return mk3(v.x * sc[0], v.y * sc[1], v.z * sc[2]);
+}
+HD float scale_radius(const SimCtx& c, int b, float r) {
+    if (!body_scaled(c, b)) return r;
+    const float* sc = c.s->osc[b];
+    return r * fmaxf(fmaxf(sc[0], sc[1]), sc[2]);
+}
+
 HD PoseF object_pose(const SimCtx& c, int o) {
     const EnvLDS& s = *c.s;
     qf q = ldq(s.oq[o]);
-    return PoseF{ld3(s.oc[o]) - qrot(q, ld3(c.m->pool_com[s.pool[o]])), q};
+    return PoseF{ld3(s.oc[o]) - qrot(q, scale3(c, o, ld3(c.m->pool_com[s.pool[o]]))), q};
 }
 
-HD void world_plane(const ha_model_t& m, int hull, int k, PoseF P, f3& n, float& d) {
+// face plane k of a hull in world space; for a scaled body (inv_sc = 1 / scale, read once per hull pair by
+// the caller) n' = S^-1 n / |S^-1 n|, d' = d / |S^-1 n|
+HD void world_plane(const ha_model_t& m, int hull, int k, PoseF P, bool scaled, f3 inv_sc, f3& n, float& d) {
     const float* pl = m.planes[m.hull_plane_start[hull] + k];
-    n = qrot(P.q, mk3(pl[0], pl[1], pl[2]));
-    d = pl[3] - dot3(n, P.p);
+    f3 nl = mk3(pl[0], pl[1], pl[2]);
+    float dl = pl[3];
+    if (scaled) {
+        nl = mk3(pl[0] * inv_sc.x, pl[1] * inv_sc.y, pl[2] * inv_sc.z);
+        float inv = 1.0f / sqrtf(dot3(nl, nl));
+        nl = nl * inv;
+        dl = dl * inv;
+    }
+    n = qrot(P.q, nl);
+    d = dl - dot3(n, P.p);
+}
+HD f3 inv_scale(const SimCtx& c, int b) {
+    if (!body_scaled(c, b)) return mk3(1, 1, 1);
+    const float* sc = c.s->osc[b];
+    return mk3(1.0f / sc[0], 1.0f / sc[1], 1.0f / sc[2]);
 }
 
 // append up to 4 reduced contacts (lane 0 does the list bookkeeping, same policy as the oracle)
@@ -412,14 +444,14 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
 HD void collide_ground(SimCtx& c, int hull, PoseF P, int a) {
     const ha_model_t& m = *c.m;
     float mg = c.p->contact_margin;
-    f3 ctr = P.p + qrot(P.q, ld3(m.hull_center[hull]));
-    if (ctr.z - m.hull_radius[hull] > mg) return;
+    f3 ctr = P.p + qrot(P.q, scale3(c, a, ld3(m.hull_center[hull])));
+    if (ctr.z - scale_radius(c, a, m.hull_radius[hull]) > mg) return;
     int lane = c.lane;
     bool valid = false;
     f3 pt = mk3(0, 0, 0);
     float sep = 0;
     if (lane < m.hull_nverts[hull]) {
-        f3 v = P.p + qrot(P.q, ld3(m.verts[m.hull_vert_start[hull] + lane]));
+        f3 v = P.p + qrot(P.q, scale3(c, a, ld3(m.verts[m.hull_vert_start[hull] + lane])));
         if (v.z <= mg) {
             valid = true;
             pt = v - mk3(0, 0, 0.5f * v.z);
@@ -490,10 +522,10 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     const ha_model_t& m = *c.m;
     float mg = c.p->contact_margin;
     int lane = c.lane;
-    f3 ca = PA.p + qrot(PA.q, ld3(m.hull_center[ha]));
-    f3 cb = PB.p + qrot(PB.q, ld3(m.hull_center[hb]));
+    f3 ca = PA.p + qrot(PA.q, scale3(c, a, ld3(m.hull_center[ha])));
+    f3 cb = PB.p + qrot(PB.q, scale3(c, b, ld3(m.hull_center[hb])));
     f3 dc = ca - cb;
-    float rr = m.hull_radius[ha] + m.hull_radius[hb] + mg;
+    float rr = scale_radius(c, a, m.hull_radius[ha]) + scale_radius(c, b, m.hull_radius[hb]) + mg;
     if (dot3(dc, dc) > rr * rr) return;
     int nva = m.hull_nverts[ha], nvb = m.hull_nverts[hb];
     int npa = m.hull_nplanes[ha], npb = m.hull_nplanes[hb];
@@ -505,17 +537,19 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
 #define HPROF(i)
 #endif
     // world vertices and planes of both hulls, once
-    if (lane < nva) st3(cs.wvA[lane], PA.p + qrot(PA.q, ld3(m.verts[m.hull_vert_start[ha] + lane])));
-    if (lane < nvb) st3(cs.wvB[lane], PB.p + qrot(PB.q, ld3(m.verts[m.hull_vert_start[hb] + lane])));
+    if (lane < nva) st3(cs.wvA[lane], PA.p + qrot(PA.q, scale3(c, a, ld3(m.verts[m.hull_vert_start[ha] + lane]))));
+    if (lane < nvb) st3(cs.wvB[lane], PB.p + qrot(PB.q, scale3(c, b, ld3(m.verts[m.hull_vert_start[hb] + lane]))));
+    bool scA = body_scaled(c, a), scB = body_scaled(c, b);
+    f3 isA = inv_scale(c, a), isB = inv_scale(c, b);
     for (int k = lane; k < npa; k += 64) {
         f3 n; float d;
-        world_plane(m, ha, k, PA, n, d);
+        world_plane(m, ha, k, PA, scA, isA, n, d);
         st3(cs.wpA[k], n);
         cs.wpA[k][3] = d;
     }
     for (int k = lane; k < npb; k += 64) {
         f3 n; float d;
-        world_plane(m, hb, k, PB, n, d);
+        world_plane(m, hb, k, PB, scB, isB, n, d);
         st3(cs.wpB[k], n);
         cs.wpB[k][3] = d;
     }
@@ -642,8 +676,8 @@ HD void detect(SimCtx& c) {
                 if (cand) {
                     int ho = m.pool_hull[s.pool[A]];
                     PoseF Po = object_pose(c, A);
-                    f3 co = Po.p + qrot(Po.q, ld3(m.hull_center[ho]));
-                    float ro = m.hull_radius[ho];
+                    f3 co = Po.p + qrot(Po.q, scale3(c, A, ld3(m.hull_center[ho])));
+                    float ro = scale_radius(c, A, m.hull_radius[ho]);
                     if (kind == 0) {
                         cand = co.z - ro <= mg;
                     } else {
@@ -652,9 +686,10 @@ HD void detect(SimCtx& c) {
                         if (kind == 1) { hb = m.table_hull; Pb = Ptab; }
                         else if (kind == 2) { hb = m.pool_hull[s.pool[B]]; Pb = object_pose(c, B); }
                         else { hb = B; int Lk = m.hull_link[B]; Pb = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; }
-                        f3 cbb = Pb.p + qrot(Pb.q, ld3(m.hull_center[hb]));
+                        int bb = kind == 2 ? B : -1;
+                        f3 cbb = Pb.p + qrot(Pb.q, scale3(c, bb, ld3(m.hull_center[hb])));
                         f3 dc = co - cbb;
-                        float rr = ro + m.hull_radius[hb] + mg;
+                        float rr = ro + scale_radius(c, bb, m.hull_radius[hb]) + mg;
                         cand = dot3(dc, dc) <= rr * rr;
                         if (kind == 1) cand = cand && sphere_near_table(m, Ptab, co, ro + mg);
                     }
@@ -766,20 +801,44 @@ HD void substep(SimCtx& c, float hdt) {
     if (lane < NO) {
         int o = lane;
         float damp = 1.0f / (1.0f + hdt * p.object_ang_damping);
-        f3 lv = ld3(s.ov[o]) + ld3(p.gravity) * hdt;
-        f3 av = ld3(s.ow[o]) * damp;
-        float* vo = s.v + D + 6 * o;
-        vo[0] = lv.x; vo[1] = lv.y; vo[2] = lv.z; vo[3] = av.x; vo[4] = av.y; vo[5] = av.z;
-        float R[9], Iw[9], Ii[9];
-        qmat(ldq(s.oq[o]), R);
-        rart3(R, m.pool_inertia[s.pool[o]], Iw);
+        float R[9], Iw[9], Ii[9], Il[9];
+        const float* I0 = m.pool_inertia[s.pool[o]];
         float sc = c.dr ? c.dr[HA_DR_OBJ_MASS + o] : 1.0f;
+        float mass = m.pool_mass[s.pool[o]];
+#pragma unroll
+        for (int k = 0; k < 9; k++) Il[k] = I0[k];
+        if (body_scaled(c, o)) {
+            // uniform density scaled by S: C = tr(I)/2 Id - I (second moments), C' = det(S) S C S,
+            // I' = tr(C') Id - C', m' = det(S) m
+            const float* sv = s.osc[o];
+            float det = (sv[0] * sv[1]) * sv[2];
+            float h = 0.5f * ((I0[0] + I0[4]) + I0[8]);
+            float Cs[9];
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+#pragma unroll
+                for (int j = 0; j < 3; j++) Cs[3 * i + j] = det * (sv[i] * (((i == j ? h : 0.0f) - I0[3 * i + j]) * sv[j]));
+            float tr = (Cs[0] + Cs[4]) + Cs[8];
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+#pragma unroll
+                for (int j = 0; j < 3; j++) Il[3 * i + j] = (i == j ? tr : 0.0f) - Cs[3 * i + j];
+            mass = mass * det;
+        }
+        qmat(ldq(s.oq[o]), R);
+        rart3(R, Il, Iw);
 #pragma unroll
         for (int k = 0; k < 9; k++) Iw[k] = Iw[k] * sc;
         inv3(Iw, Ii);
 #pragma unroll
         for (int k = 0; k < 9; k++) s.oIinv[o][k] = Ii[k];
-        s.om[o] = m.pool_mass[s.pool[o]] * sc;
+        mass = mass * sc;
+        s.om[o] = mass;
+        // external force (zero unless a task applied one): constant over the call's substeps
+        f3 lv = (ld3(s.ov[o]) + ld3(p.gravity) * hdt) + ld3(s.ofx[o]) * (hdt / mass);
+        f3 av = ld3(s.ow[o]) * damp;
+        float* vo = s.v + D + 6 * o;
+        vo[0] = lv.x; vo[1] = lv.y; vo[2] = lv.z; vo[3] = av.x; vo[4] = av.y; vo[5] = av.z;
     }
     wsync();
     PROF(2);

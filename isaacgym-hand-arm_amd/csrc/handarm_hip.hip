@@ -9,7 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "ah_task.h"
+#include "ak_task.h"
 
 #define HA_ND 17         /* Ur5Sih DOF count (UR5 + SIH); AH_ND = 16 (Allegro) */
 
@@ -17,7 +17,8 @@ enum { MODE_SIMULATE = 0, MODE_STEP = 1, MODE_OBSERVE = 2, MODE_RESET = 3 };
 
 // ----------------------------------------------------------------------------- state load/store
 // Generic over the env layout in ha_model_t (actor / rigid-body creation order of the task).
-__device__ void load_env(SimCtx& c, const ha_state_t& st, int env) {
+// take_force: consume st.object_force (ha_simulate = gym.simulate after apply_rigid_body_force_tensors)
+__device__ void load_env(SimCtx& c, const ha_state_t& st, int env, bool take_force = false) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     int lane = c.lane, D = c.D, NO = c.NO, A = m.n_actors;
@@ -32,9 +33,22 @@ __device__ void load_env(SimCtx& c, const ha_state_t& st, int env) {
         const float* r = st.root_state + ((size_t)env * A + m.actor_object0 + o) * 13;
         int pid = (int)st.object_indices[(size_t)env * NO + o];
         s.pool[o] = pid;
+        if (st.object_scale) {
+            const float* sc = st.object_scale + ((size_t)env * NO + o) * 3;
+            s.osc[o][0] = sc[0]; s.osc[o][1] = sc[1]; s.osc[o][2] = sc[2]; s.osc[o][3] = 1.0f;
+        } else {
+            s.osc[o][0] = s.osc[o][1] = s.osc[o][2] = 1.0f;
+            s.osc[o][3] = 0.0f;
+        }
+        s.ofx[o][0] = s.ofx[o][1] = s.ofx[o][2] = s.ofx[o][3] = 0.0f;
+        if (take_force && st.object_force) {
+            float* fo = st.object_force + ((size_t)env * NO + o) * 3;
+            s.ofx[o][0] = fo[0]; s.ofx[o][1] = fo[1]; s.ofx[o][2] = fo[2];
+            fo[0] = fo[1] = fo[2] = 0.0f;
+        }
         qf q = ldq(r + 3);
         stq(s.oq[o], q);
-        st3(s.oc[o], ld3(r) + qrot(q, ld3(m.pool_com[pid])));
+        st3(s.oc[o], ld3(r) + qrot(q, scale3(c, o, ld3(m.pool_com[pid]))));
         st3(s.ov[o], ld3(r + 7));
         st3(s.ow[o], ld3(r + 10));
         s.coll[o] = st.collision_enabled ? st.collision_enabled[(size_t)env * NO + o] : 1;
@@ -76,13 +90,13 @@ __device__ float link_state(const SimCtx& c, int i, int k) {
         f3 lin = ld3(&s.u.pd.dyn.Vl[i][3]) + cross3(ld3(&s.u.pd.dyn.Vl[i][0]), cc);
         return k == 7 ? lin.x : (k == 8 ? lin.y : lin.z);
     }
-    return s.u.pd.dyn.Vl[i][k - 7];
+    return s.u.pd.dyn.Vl[i][k - 10];        // angular velocity: Vl = (w, v at the world origin)
 }
 // root-state row k of object o (origin pose, not COM) from LDS
 __device__ float object_state(const SimCtx& c, int o, int k) {
     const EnvLDS& s = *c.s;
     if (k < 3) {
-        f3 pos = ld3(s.oc[o]) - qrot(ldq(s.oq[o]), ld3(c.m->pool_com[s.pool[o]]));
+        f3 pos = ld3(s.oc[o]) - qrot(ldq(s.oq[o]), scale3(c, o, ld3(c.m->pool_com[s.pool[o]])));
         return k == 0 ? pos.x : (k == 1 ? pos.y : pos.z);
     }
     if (k < 7) return s.oq[o][k - 3];
@@ -183,6 +197,40 @@ __device__ void ah_in_from_tensors(SimCtx& c, const ha_state_t& st, int env, AhI
     wsync();
 }
 
+// AllegroKuka observation staging (palm = iiwa7_link_7, fingertips = *_link_3)
+__device__ void ak_in_from_lds(SimCtx& c, AkIn* in) {
+    EnvLDS& s = *c.s;
+    const ha_params_t& p = *c.p;
+    int lane = c.lane, D = c.D;
+    if (lane < D) {
+        in->q[lane] = s.q[lane];
+        in->qd[lane] = s.qd[lane];
+    }
+    if (lane < 13) {
+        in->palm[lane] = link_state(c, p.ak_palm_link, lane);
+        in->obj[lane] = object_state(c, 0, lane);
+    }
+    if (lane < 28) in->tip[lane / 7][lane % 7] = link_state(c, p.ak_fingertip_links[lane / 7], lane % 7);
+    wsync();
+}
+__device__ void ak_in_from_tensors(SimCtx& c, const ha_state_t& st, int env, AkIn* in) {
+    const ha_model_t& m = *c.m;
+    const ha_params_t& p = *c.p;
+    int lane = c.lane, D = c.D;
+    const float* bs = st.rigid_body_state + (size_t)env * m.n_bodies * 13;
+    if (lane < D) {
+        in->q[lane] = st.dof_state[((size_t)env * D + lane) * 2];
+        in->qd[lane] = st.dof_state[((size_t)env * D + lane) * 2 + 1];
+    }
+    if (lane < 13) {
+        in->palm[lane] = bs[(m.body_robot0 + p.ak_palm_link) * 13 + lane];
+        in->obj[lane] = st.root_state[((size_t)env * m.n_actors + m.actor_object0) * 13 + lane];
+    }
+    if (lane < 28) in->tip[lane / 7][lane % 7] = bs[(m.body_robot0 + p.ak_fingertip_links[lane / 7]) * 13 + lane % 7];
+    wsync();
+}
+static_assert(sizeof(AkPost) <= sizeof(PostScratch) - offsetof(PostScratch, in), "AkPost must fit after pd.dyn");
+
 // ----------------------------------------------------------------------------- the kernels
 // One kernel per (task, mode) (one workgroup = one wavefront = one env): each is compiled with only its
 // own path, which keeps every kernel's code small, gives the DOF count to the compiler as a constant, and
@@ -191,7 +239,7 @@ template <int TASK, int MODE>
 __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params,
                                          const ha_state_t& st, int num_envs, int n_calls, uint32_t flags,
                                          int stat_slot) {
-    constexpr int ND = TASK == HA_TASK_ALLEGRO_HAND ? AH_ND : HA_ND;
+    constexpr int ND = TASK == HA_TASK_ALLEGRO_HAND ? AH_ND : (TASK == HA_TASK_ALLEGRO_KUKA ? AK_ND : HA_ND);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int env = blockIdx.x;
     if (env >= num_envs) return;
@@ -206,13 +254,17 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.dr = (params->dr_enable && st.dr_scale) ? st.dr_scale + (size_t)env * HA_DR_SIZE : nullptr;
     ObsIn& in = c.s->u.pd.in;
     AhIn& ain = *reinterpret_cast<AhIn*>(&c.s->u.pd.in);
+    AkPost& akp = *reinterpret_cast<AkPost*>(&c.s->u.pd.in);
     ha_state_t S = st;
     if (MODE == MODE_STEP || MODE == MODE_OBSERVE) {
         S.stats = st.stats + stat_slot * HA_STAT_SIZE;
         S.term_sums = st.term_sums + stat_slot * 4;
     }
     if (MODE == MODE_OBSERVE) {
-        if (TASK == HA_TASK_ALLEGRO_HAND) {
+        if (TASK == HA_TASK_ALLEGRO_KUKA) {
+            ak_in_from_tensors(c, S, env, &akp.in);
+            ak_post(c, S, env, akp, (flags & HA_FLAG_OBS_ONLY) != 0);
+        } else if (TASK == HA_TASK_ALLEGRO_HAND) {
             ah_in_from_tensors(c, S, env, &ain);
             ah_post(c, S, env, ain, (flags & HA_FLAG_OBS_ONLY) != 0);
         } else {
@@ -221,10 +273,32 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
         }
         return;
     }
-    load_env(c, S, env);
+    load_env(c, S, env, MODE == MODE_SIMULATE);
     if (MODE == MODE_SIMULATE) {
         run_physics<ND>(c, n_calls);
         store_env(c, S, env);
+        return;
+    }
+    if (TASK == HA_TASK_ALLEGRO_KUKA) {
+        // pre_physics_step (allegro_kuka_base.py:1355-1424). Lane k holds task_state field k in tsv; it goes
+        // back to HBM before the physics (whose LDS union overwrites everything) and ak_post reloads it.
+        float* tsg = S.task_state + (size_t)env * HA_AK_TS;
+        float tsv = c.lane < HA_AK_TS ? tsg[c.lane] : 0.0f;
+        bool goal = S.reset_goal_buf[env] != 0, full = S.reset_buf[env] != 0;
+        if (goal || full) ak_reset(c, S, env, flags, goal, full, tsv);
+        if (MODE == MODE_RESET) {
+            if (c.lane < AK_TS_KP) tsg[c.lane] = tsv;
+            store_env(c, S, env);
+            return;
+        }
+        ak_controller(c, S, env);
+        ak_forces(c, S, env, flags, tsv);
+        if (c.lane < AK_TS_KP) tsg[c.lane] = tsv;
+        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<ND>(c, c.p->control_freq_inv);   // vec_task.py:409-412
+        store_env(c, S, env);
+        if (c.lane == 0) S.progress_buf[env] = S.progress_buf[env] + 1;                // allegro_kuka_base.py:1429
+        ak_in_from_lds(c, &akp.in);
+        ak_post(c, S, env, akp, false);
         return;
     }
     if (TASK == HA_TASK_ALLEGRO_HAND) {
@@ -281,9 +355,21 @@ HA_KERNEL(ah_step_kernel, HA_TASK_ALLEGRO_HAND, MODE_STEP)
 HA_KERNEL(ah_simulate_kernel, HA_TASK_ALLEGRO_HAND, MODE_SIMULATE)
 HA_KERNEL(ah_observe_kernel, HA_TASK_ALLEGRO_HAND, MODE_OBSERVE)
 HA_KERNEL(ah_reset_kernel, HA_TASK_ALLEGRO_HAND, MODE_RESET)
+HA_KERNEL(ak_step_kernel, HA_TASK_ALLEGRO_KUKA, MODE_STEP)
+HA_KERNEL(ak_simulate_kernel, HA_TASK_ALLEGRO_KUKA, MODE_SIMULATE)
+HA_KERNEL(ak_observe_kernel, HA_TASK_ALLEGRO_KUKA, MODE_OBSERVE)
+HA_KERNEL(ak_reset_kernel, HA_TASK_ALLEGRO_KUKA, MODE_RESET)
 
 typedef void (*env_kernel_t)(const ha_model_t*, const ha_params_t*, ha_state_t, int, int, uint32_t, int);
 static env_kernel_t kernel_for(int task, int mode) {
+    if (task == HA_TASK_ALLEGRO_KUKA) {
+        switch (mode) {
+            case MODE_STEP: return ak_step_kernel;
+            case MODE_SIMULATE: return ak_simulate_kernel;
+            case MODE_OBSERVE: return ak_observe_kernel;
+            default: return ak_reset_kernel;
+        }
+    }
     if (task == HA_TASK_ALLEGRO_HAND) {
         switch (mode) {
             case MODE_STEP: return ah_step_kernel;
@@ -352,9 +438,19 @@ int ha_struct_sizes(int32_t* model_size, int32_t* params_size, int32_t* state_si
 
 int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_envs, ha_handle* out) {
     if (!model || !params || !out || num_envs <= 0) return HA_E_ARG;
-    if (params->task != HA_TASK_UR5SIH && params->task != HA_TASK_ALLEGRO_HAND) return HA_E_ARG;
+    if (params->task != HA_TASK_UR5SIH && params->task != HA_TASK_ALLEGRO_HAND && params->task != HA_TASK_ALLEGRO_KUKA)
+        return HA_E_ARG;
     // the kernels are compiled for the task's DOF count (register-resident factorization)
-    if (model->n_dofs != (params->task == HA_TASK_ALLEGRO_HAND ? AH_ND : HA_ND)) return HA_E_MODEL;
+    int nd = params->task == HA_TASK_ALLEGRO_HAND ? AH_ND : (params->task == HA_TASK_ALLEGRO_KUKA ? AK_ND : HA_ND);
+    if (model->n_dofs != nd) return HA_E_MODEL;
+    if (params->task == HA_TASK_ALLEGRO_KUKA) {
+        if (params->n_objects != 1 || params->ak_num_keypoints < 1 || params->ak_num_keypoints > 4 ||
+            params->num_obs > AK_MAX_OBS || params->num_obs != 93 + 6 * params->ak_num_keypoints)
+            return HA_E_ARG;
+        if (params->ak_palm_link < 0 || params->ak_palm_link >= model->n_links) return HA_E_MODEL;
+        for (int i = 0; i < 4; i++)
+            if (params->ak_fingertip_links[i] < 0 || params->ak_fingertip_links[i] >= model->n_links) return HA_E_MODEL;
+    }
     if (model->n_actors < 1 || model->n_bodies < model->n_links + params->n_objects) return HA_E_MODEL;
     if (model->n_links > HA_MAX_LINKS || params->n_objects > NOBJ ||
         model->n_dofs + 6 * params->n_objects > RS || model->n_link_hulls + model->n_pool + 1 > HA_MAX_HULLS)
@@ -505,8 +601,18 @@ int ha_set_stats_ring(ha_handle h, int32_t n_slots) {
     return HA_OK;
 }
 
+// the task buffers a fused entry point needs besides the physics tensors
+static bool task_bound(ha_handle h) {
+    const ha_state_t& s = h->st;
+    if (h->task == HA_TASK_ALLEGRO_KUKA)
+        return s.task_state && s.task_scalars && s.object_scale && s.goal_state && s.successes && s.reset_goal_buf &&
+               s.dof_position_targets && s.reset_buf && s.progress_buf && s.rew && s.timeout_buf && s.episode;
+    return true;
+}
+
 int ha_task_step(ha_handle h, uint32_t flags, void* stream) {
-    if (!h || !h->bound || !h->st.actions || !h->st.obs || !h->st.stats || !h->st.term_sums) return HA_E_STATE;
+    if (!h || !h->bound || !h->st.actions || !h->st.obs || !h->st.stats || !h->st.term_sums || !task_bound(h))
+        return HA_E_STATE;
     int slot = (int)(h->step_counter % h->stat_slots);
     h->step_counter++;
     HIPCHK(hipMemsetAsync(h->st.stats + slot * HA_STAT_SIZE, 0, sizeof(int32_t) * HA_STAT_SIZE, (hipStream_t)stream));
@@ -523,14 +629,14 @@ int ha_task_step(ha_handle h, uint32_t flags, void* stream) {
 }
 
 int ha_task_observe(ha_handle h, uint32_t flags, void* stream) {
-    if (!h || !h->bound || !h->st.obs) return HA_E_STATE;
+    if (!h || !h->bound || !h->st.obs || !task_bound(h)) return HA_E_STATE;
     HIPCHK(hipMemsetAsync(h->st.stats, 0, sizeof(int32_t) * HA_STAT_SIZE, (hipStream_t)stream));
     HIPCHK(hipMemsetAsync(h->st.term_sums, 0, sizeof(float) * 4, (hipStream_t)stream));
     return launch(h, MODE_OBSERVE, 0, flags, 0, stream);
 }
 
 int ha_task_reset(ha_handle h, uint32_t flags, void* stream) {
-    if (!h || !h->bound) return HA_E_STATE;
+    if (!h || !h->bound || !task_bound(h)) return HA_E_STATE;
     return launch(h, MODE_RESET, 0, flags, 0, stream);
 }
 

@@ -18,15 +18,24 @@ import numpy as np
 
 ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "ur5sih_scene.json")
 ALLEGRO_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "allegro_hand_scene.json")
+KUKA_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "kuka_allegro_scene.json")
 
 MAX_LINKS, MAX_DOFS, MAX_HULLS, MAX_VERTS, MAX_PLANES = 32, 24, 64, 4096, 8192
 MAX_POOL, MAX_OBJ, MAX_INIT_POSES, MAX_SPLINE_PIECES, N_SPLINES = 32, 3, 4, 8, 8
 MAX_MPAIRS = 192
 STAT_SIZE = 2 + 2 * MAX_POOL
-DRAW_STRIDE = 48
+DRAW_STRIDE = 80
 DR_SIZE = 72
 DR_LINK_MASS, DR_OBJ_MASS, DR_LINK_FRIC, DR_OBJ_FRIC = 0, 32, 36, 68
-TASK_UR5SIH, TASK_ALLEGRO_HAND = 0, 1
+TASK_UR5SIH, TASK_ALLEGRO_HAND, TASK_ALLEGRO_KUKA = 0, 1, 2
+# AllegroKuka task_state row (HA_AK_* in handarm_abi.h)
+AK_TS = 48
+AK_LIFTED, AK_CLOSEST_KP, AK_CLOSEST_FT, AK_FURTHEST, AK_NEAR_GOAL = 0, 1, 2, 6, 7
+AK_PREV_SUCC, AK_TRUE_OBJ, AK_PREV_TRUE_OBJ, AK_FORCE_PROB, AK_RB_FORCE, AK_RNG, AK_REW_EP, AK_KP = \
+    8, 9, 10, 11, 12, 15, 16, 32
+AK_REWARD_KEYS = ["raw_fingertip_delta_rew", "raw_hand_delta_penalty", "raw_lifting_rew", "raw_keypoint_rew",
+                  "fingertip_delta_rew", "hand_delta_penalty", "lifting_rew", "lift_bonus_rew", "keypoint_rew",
+                  "bonus_rew", "kuka_actions_penalty", "allegro_actions_penalty"]   # allegro_kuka_base.py:361-374
 
 FLAG_NO_PHYSICS = 1
 FLAG_REPLAY_DRAWS = 2
@@ -91,6 +100,20 @@ class HaParams(C.Structure):
         ("ah_object_init", arr(f32, 7)), ("ah_goal_init", arr(f32, 3)), ("ah_goal_displacement", arr(f32, 3)),
         ("dr_enable", i32), ("dr_mass_lo", f32), ("dr_mass_hi", f32), ("dr_fric_lo", f32), ("dr_fric_hi", f32),
         ("dr_fric_buckets", i32), ("dr_obs_noise", f32), ("dr_act_noise", f32),
+        ("ak_subtask", i32), ("ak_num_keypoints", i32), ("ak_keypoints", arr(f32, 4, 3)),
+        ("ak_object_base_size", f32), ("ak_keypoint_scale", f32), ("ak_initial_tolerance", f32),
+        ("ak_target_tolerance", f32), ("ak_lifting_rew_scale", f32), ("ak_lifting_bonus", f32),
+        ("ak_lifting_bonus_threshold", f32), ("ak_keypoint_rew_scale", f32), ("ak_distance_delta_rew_scale", f32),
+        ("ak_reach_goal_bonus", f32), ("ak_kuka_actions_penalty_scale", f32), ("ak_allegro_actions_penalty_scale", f32),
+        ("ak_success_steps", i32), ("ak_max_consecutive_successes", i32), ("ak_bonus_rew", f32),
+        ("ak_reset_noise", arr(f32, 3)), ("ak_dof_noise_arm", f32), ("ak_dof_noise_fingers", f32),
+        ("ak_dof_vel_noise", f32), ("ak_force_scale", f32), ("ak_force_prob_lo", f32), ("ak_force_prob_hi", f32),
+        ("ak_force_decay_step", f32), ("ak_object_rb_mass", f32), ("ak_dof_speed_scale", f32),
+        ("ak_act_moving_average", f32), ("ak_one_minus_ama", f32), ("ak_clamp_abs_obs", f32),
+        ("ak_object_init", arr(f32, 3)), ("ak_goal_init", arr(f32, 3)), ("ak_target_origin", arr(f32, 3)),
+        ("ak_target_lo", arr(f32, 3)), ("ak_target_size", arr(f32, 3)), ("ak_palm_offset", arr(f32, 3)),
+        ("ak_fingertip_offsets", arr(f32, 4, 3)), ("ak_palm_link", i32), ("ak_fingertip_links", arr(i32, 4)),
+        ("ak_num_arm_dofs", i32),
     ]
 
 
@@ -103,7 +126,7 @@ STATE_FIELDS = ["root_state", "rigid_body_state", "dof_state", "net_contact_forc
                 "object_configuration_indices", "object_indices", "object_pos_initial", "object_quat_initial",
                 "ur5_target", "servo", "smoothed", "obs_cache", "reset_draws", "episode", "stats", "term_sums",
                 "flags", "collision_enabled", "dof_force", "reset_goal_buf", "successes", "goal_state",
-                "consecutive_successes", "dr_scale"]
+                "consecutive_successes", "dr_scale", "object_scale", "object_force", "task_state", "task_scalars"]
 
 
 def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, num_actions=11, num_obs=147,
@@ -126,11 +149,19 @@ def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, nu
         "term_sums": ((4,), f), "flags": ((4,), i32), "collision_enabled": ((N, n_obj), u8),
         "dof_force": ((N, D), f), "reset_goal_buf": ((N,), i64), "successes": ((N,), f), "goal_state": ((N, 7), f),
         "consecutive_successes": ((1,), f), "dr_scale": ((N, DR_SIZE), f),
+        "object_scale": ((N, n_obj, 3), f), "object_force": ((N, n_obj, 3), f), "task_state": ((N, AK_TS), f),
+        "task_scalars": ((4,), f),
     }
 
 
 class HaState(C.Structure):
     _fields_ = [(n, P) for n in STATE_FIELDS]
+
+
+def null_fields(task):
+    """State buffers left NULL for a task: object_scale switches the physics to per-env scaled object
+    geometry, which only AllegroKuka's cuboid family uses (bit-identical unscaled path otherwise)."""
+    return set() if task == TASK_ALLEGRO_KUKA else {"object_scale"}
 
 
 def load_scene(path=ASSET):
@@ -328,9 +359,69 @@ ALLEGRO_TASK = dict(
 )
 
 
+# AllegroKuka (config C2): cfg/task/AllegroKuka.yaml:9-94,210-231 + env/regrasping.yaml (default subtask here:
+# BASELINE.json config 2 "Arm+Allegro cube grasp") or env/reorientation.yaml; allegro_kuka_base.py:53-400
+def _f32(x):
+    return float(np.float32(x))
+
+
+ALLEGRO_KUKA_TASK = dict(
+    DEFAULT_TASK, task=TASK_ALLEGRO_KUKA, num_actions=23, n_objects=1, subtask="regrasping",
+    dt=0.01667, substeps=2, control_freq_inv=1, solver_iters=8,          # AllegroKuka.yaml:27,210-223
+    contact_margin=0.002, max_depen_vel=1000.0,                          # :226-229
+    episode_length={"regrasping": 300, "reorientation": 600}, success_steps={"regrasping": 30, "reorientation": 1},
+    reset_position_noise=(0.1, 0.1, 0.02), reset_dof_pos_noise_fingers=0.1, reset_dof_pos_noise_arm=0.1,
+    reset_dof_vel_noise=0.5, force_scale=2.0, force_prob_range=(0.001, 0.1), force_decay=0.99,
+    force_decay_interval=0.08, lifting_rew_scale=20.0, lifting_bonus=300.0, lifting_bonus_threshold=0.15,
+    keypoint_rew_scale=200.0, distance_delta_rew_scale=50.0, reach_goal_bonus=1000.0,
+    kuka_actions_penalty_scale=0.003, allegro_actions_penalty_scale=0.0003, dof_speed_scale=10.0,
+    act_moving_average=1.0, keypoint_scale=1.5, object_base_size=0.05, success_tolerance=0.075,
+    target_success_tolerance=0.01, tolerance_curriculum_increment=0.9, tolerance_curriculum_interval=3000,
+    max_consecutive_successes=50, clamp_abs_observations=10.0,
+    # desired_kuka_pos pose v1 (allegro_kuka_base.py:316-319), fingers 0
+    reset_pose=(-1.571, 1.571, -0.000, 1.376, -0.000, 1.485, 2.358) + (0.0,) * 16,
+    # allegro_pose (0, 0.8, 0) in gymapi.Vec3 (float32); object_start_pose = allegro_pose + (0, -0.8, 0.38 + 0.25)
+    # computed by Vec3 arithmetic (allegro_kuka_base.py:401-413,608-628)
+    object_init=(0.0, _f32(_f32(0.8) + -0.8), _f32(0.0 + (0.38 + 0.25))),
+    target_volume_origin=(0.0, 0.05, 0.8), target_volume_extent=((-0.4, 0.4), (-0.05, 0.3), (-0.12, 0.25)),
+    palm_offset=(-0.00, -0.02, 0.16), fingertip_offsets=((0.05, 0.005, 0), (0.05, 0.005, 0), (0.05, 0.005, 0),
+                                                        (0.06, 0.005, 0)),
+    palm_link="iiwa7_link_7", fingertip_links=("index_link_3", "middle_link_3", "ring_link_3", "thumb_link_3"),
+    num_arm_dofs=7,
+)
+AK_KEYPOINTS = {"regrasping": [[0, 0, 0]],                                          # allegro_kuka_regrasping.py:46-48
+                "reorientation": [[1, 1, 1], [1, 1, -1], [-1, -1, 1], [-1, -1, -1]]}   # reorientation.py:48-54
+
+
+def kuka_tolerance_scalars(success_tolerance, c):
+    """task_scalars for the device: success_tolerance, tolerance_successes_objective's tolerance term and
+    branch, keypoint success tolerance (python double arithmetic, allegro_kuka_utils.py:122-163,
+    allegro_kuka_base.py:862), each rounded once to float32 like a python scalar in a tensor op."""
+    ini, tgt = c["success_tolerance"], c["target_success_tolerance"]
+    tol_obj = (ini - success_tolerance) / (ini - tgt) if ini > tgt else 1.0
+    return np.array([success_tolerance, tol_obj, 1.0 if success_tolerance > tgt else 0.0,
+                     success_tolerance * c["keypoint_scale"]], np.float32)
+
+
+def kuka_env_tables(num_envs, scene, c):
+    """Per-env object scales (env i gets object_dims[i % len], allegro_kuka_base.py:687-707) and keypoint
+    offsets (:708-715, python double, rounded once by to_torch)."""
+    dims = scene["object_dims"]
+    kps = AK_KEYPOINTS[c["subtask"]]
+    scales = np.zeros((num_envs, 1, 3), np.float32)
+    offs = np.zeros((num_envs, 4, 3), np.float32)
+    for i in range(num_envs):
+        sc = dims[i % len(dims)]
+        scales[i, 0] = sc
+        for j, kp in enumerate(kps):
+            offs[i, j] = [kp[k] * (sc[k] * c["object_base_size"] * c["keypoint_scale"] / 2) for k in range(3)]
+    return scales, offs
+
+
 def build_params(cfg=None, task=None):
-    c = dict(ALLEGRO_TASK if (task == TASK_ALLEGRO_HAND or (cfg or {}).get("task") == TASK_ALLEGRO_HAND)
-             else DEFAULT_TASK)
+    want = task if task is not None else (cfg or {}).get("task")
+    c = dict(ALLEGRO_TASK if want == TASK_ALLEGRO_HAND else (ALLEGRO_KUKA_TASK if want == TASK_ALLEGRO_KUKA
+                                                             else DEFAULT_TASK))
     if cfg:
         c.update(cfg)
     p = HaParams()
@@ -375,4 +466,59 @@ def build_params(cfg=None, task=None):
         # (1.0 - act_moving_average) * prev_targets: python double, cast once (allegro_hand.py:612-613)
         p.sih_beta = 1.0 - c["act_moving_average"]
         p.action_dt = c["dt"]
+    if p.task == TASK_ALLEGRO_KUKA:
+        _kuka_params(p, c)
     return p, c
+
+
+def _kuka_params(p, c):
+    import torch
+    sub = c["subtask"]
+    assert sub in AK_KEYPOINTS, sub
+    kps = AK_KEYPOINTS[sub]
+    p.ak_subtask = 0 if sub == "regrasping" else 1
+    p.ak_num_keypoints = len(kps)
+    for j, kp in enumerate(kps):
+        p.ak_keypoints[j][:] = kp
+    p.num_obs = 93 + 6 * len(kps)                      # full_state_size (allegro_kuka_base.py:185-220)
+    p.num_actions = 23
+    p.max_episode_length = c.get("max_episode_length_override") or c["episode_length"][sub]
+    p.ak_success_steps = c["success_steps"][sub] if isinstance(c["success_steps"], dict) else c["success_steps"]
+    for k in ["object_base_size", "keypoint_scale", "lifting_rew_scale", "lifting_bonus", "lifting_bonus_threshold",
+              "keypoint_rew_scale", "distance_delta_rew_scale", "reach_goal_bonus", "kuka_actions_penalty_scale",
+              "allegro_actions_penalty_scale", "max_consecutive_successes", "force_scale", "act_moving_average"]:
+        setattr(p, "ak_" + k, c[k])
+    p.ak_initial_tolerance = c["success_tolerance"]
+    p.ak_target_tolerance = c["target_success_tolerance"]
+    p.ak_bonus_rew = c["reach_goal_bonus"] / p.ak_success_steps
+    p.ak_reset_noise[:] = c["reset_position_noise"]
+    p.ak_dof_noise_arm = c["reset_dof_pos_noise_arm"]
+    p.ak_dof_noise_fingers = c["reset_dof_pos_noise_fingers"]
+    p.ak_dof_vel_noise = c["reset_dof_vel_noise"]
+    p.ak_force_prob_lo, p.ak_force_prob_hi = c["force_prob_range"]
+    # torch.pow(force_decay (fp32 tensor), dt / force_decay_interval) (allegro_kuka_base.py:1402)
+    p.ak_force_decay_step = float(torch.pow(torch.tensor(c["force_decay"], dtype=torch.float32),
+                                            c["dt"] / c["force_decay_interval"]))
+    p.ak_dof_speed_scale = c["dof_speed_scale"] * c["dt"]          # python double, rounded by the tensor op
+    p.ak_one_minus_ama = 1.0 - c["act_moving_average"]
+    p.ak_clamp_abs_obs = c["clamp_abs_observations"]
+    p.ak_object_init[:] = c["object_init"]
+    p.ak_goal_init[:] = (c["object_init"][0], c["object_init"][1], np.float32(c["object_init"][2]) - np.float32(0.04))
+    o = np.asarray(c["target_volume_origin"], np.float32)
+    ext = np.asarray(c["target_volume_extent"], np.float32)
+    lo, hi = o + ext[:, 0], o + ext[:, 1]
+    p.ak_target_origin[:] = o
+    p.ak_target_lo[:] = lo
+    p.ak_target_size[:] = hi - lo
+    p.ak_palm_offset[:] = c["palm_offset"]
+    for i in range(4):
+        p.ak_fingertip_offsets[i][:] = c["fingertip_offsets"][i]
+    p.ak_num_arm_dofs = c["num_arm_dofs"]
+    scene = load_scene(c.get("scene_path", KUKA_ASSET))
+    names = [l["name"] for l in scene["robot"]["links"]]
+    p.ak_palm_link = names.index(c["palm_link"])                    # find_asset_rigid_body_index (:642-644)
+    p.ak_fingertip_links[:] = [names.index(n) for n in c["fingertip_links"]]
+    # object_rb_masses: the object of env 0 (allegro_kuka_base.py:734-735), box of density 400
+    d0 = scene["object_dims"][0]
+    p.ak_object_rb_mass = 400.0 * (c["object_base_size"] * d0[0]) * (c["object_base_size"] * d0[1]) * \
+        (c["object_base_size"] * d0[2])

@@ -34,7 +34,7 @@ class HandArmSim:
         if task is None:
             task = (task_cfg or {}).get("task", HM.TASK_UR5SIH)
         self.task = task
-        default_scene = HM.ALLEGRO_ASSET if task == HM.TASK_ALLEGRO_HAND else HM.ASSET
+        default_scene = {HM.TASK_ALLEGRO_HAND: HM.ALLEGRO_ASSET, HM.TASK_ALLEGRO_KUKA: HM.KUKA_ASSET}.get(task, HM.ASSET)
         self.scene = scene if scene is not None else HM.load_scene(default_scene)
         self.model = HM.build_model(self.scene, pool_names)
         self.params, self.cfg = HM.build_params(task_cfg, task=task)
@@ -63,14 +63,48 @@ class HandArmSim:
         dr[:, HM.DR_OBJ_MASS:HM.DR_OBJ_MASS + HM.MAX_OBJ] = 1.0
         dr[:, HM.DR_LINK_FRIC:HM.DR_LINK_FRIC + HM.MAX_LINKS] = self.params.friction
         dr[:, HM.DR_OBJ_FRIC:HM.DR_OBJ_FRIC + HM.MAX_OBJ] = self.params.friction
+        if task == HM.TASK_ALLEGRO_KUKA:
+            self._init_kuka()
         h = C.c_void_p()
         _lib.check(self.lib.ha_create(C.byref(self.model), C.byref(self.params), num_envs, C.byref(h)), "ha_create")
         self.h = h
         self.state = HM.HaState()
+        null = HM.null_fields(task)
         for k in HM.STATE_FIELDS:
-            setattr(self.state, k, self.t[k].data_ptr())
+            setattr(self.state, k, None if k in null else self.t[k].data_ptr())
         _lib.check(self.lib.ha_bind_state(self.h, C.byref(self.state)), "ha_bind_state")
         _lib.check(self.lib.ha_set_stats_ring(self.h, stats_ring), "ha_set_stats_ring")
+
+    def _init_kuka(self):
+        """AllegroKuka buffers at env creation: per-env object dims and keypoint offsets, goal_states
+        (object start - 0.04 z, allegro_kuka_base.py:738-740), object/goal root states, the tolerance
+        scalars, random_force_prob drawn at __init__ (:339-343) and the -1 'unset' markers (:356-360).
+        reset_buf / reset_goal_buf start at 1 (vec_task.py allocate_buffers), so the first step resets all."""
+        N, c, p = self.num_envs, self.cfg, self.params
+        scales, offs = HM.kuka_env_tables(N, self.scene, c)
+        self.t["object_scale"].copy_(torch.from_numpy(scales))
+        ts = self.t["task_state"]
+        ts[:, HM.AK_KP:HM.AK_KP + 12] = torch.from_numpy(offs.reshape(N, 12)).to(self.device)
+        ts[:, HM.AK_CLOSEST_KP] = -1.0
+        ts[:, HM.AK_CLOSEST_FT:HM.AK_CLOSEST_FT + 4] = -1.0
+        ts[:, HM.AK_FURTHEST] = -1.0
+        g = torch.Generator(device=self.device).manual_seed(int(p.seed))
+        lo, hi = torch.log(torch.tensor(c["force_prob_range"], device=self.device))
+        ts[:, HM.AK_FORCE_PROB] = torch.exp((lo - hi) * torch.rand(N, device=self.device, generator=g) + hi)
+        init = torch.tensor(list(p.ak_object_init), device=self.device)
+        self.t["goal_state"][:, 0:3] = init
+        self.t["goal_state"][:, 2] -= 0.04
+        root = self.t["root_state"].view(N, self.num_actors, 13)
+        root[:, self.model.actor_object0, 0:3] = init
+        root[:, self.model.actor_goal, 0:3] = self.t["goal_state"][:, 0:3]
+        root[:, self.model.actor_table, 0:3] = torch.tensor(list(self.model.table_pos), device=self.device)
+        self.t["task_scalars"].copy_(torch.from_numpy(HM.kuka_tolerance_scalars(c["success_tolerance"], c)))
+        self.t["reset_buf"].fill_(1)
+        self.t["reset_goal_buf"].fill_(1)
+        self.t["dof_state"].view(N, self.num_dofs, 2)[..., 0] = torch.tensor(list(p.reset_pose)[:self.num_dofs],
+                                                                              device=self.device)
+        self.t["dof_position_targets"].copy_(self.t["dof_state"].view(N, self.num_dofs, 2)[..., 0])
+        self.t["sim_targets"].copy_(self.t["dof_position_targets"])
 
     # -------------------------------------------------------------- helpers
     def _stream(self):

@@ -41,6 +41,7 @@ class HostState:
             kw.update(num_actions=params.num_actions, num_obs=params.num_obs)
             n_obj = params.n_objects
         self.spec = HM.state_spec(num_envs, n_obj=n_obj, num_initial_poses=num_initial_poses, **kw)
+        self.null = HM.null_fields(params.task if params is not None else HM.TASK_UR5SIH)
         self.arrays = {k: np.zeros(shape, dtype) for k, (shape, dtype) in self.spec.items()}
         self.num_envs = num_envs
 
@@ -50,12 +51,12 @@ class HostState:
     def ctypes(self):
         s = HM.HaState()
         for k in HM.STATE_FIELDS:
-            setattr(s, k, self.arrays[k].ctypes.data)
+            setattr(s, k, None if k in self.null else self.arrays[k].ctypes.data)
         return s
 
     def copy(self):
         o = HostState.__new__(HostState)
-        o.spec, o.num_envs = self.spec, self.num_envs
+        o.spec, o.num_envs, o.null = self.spec, self.num_envs, self.null
         o.arrays = {k: v.copy() for k, v in self.arrays.items()}
         return o
 

@@ -139,6 +139,9 @@ typedef struct {
     float om[NOBJ], oIinv[NOBJ][9];
     int pool[NOBJ];
     int coll[NOBJ];
+    float osc[NOBJ][3];             /* per-env object dimension scale (ha_state_t.object_scale) */
+    int oscaled[NOBJ];
+    v3 ofx[NOBJ];                   /* world force on the object COM for this call (object_force) */
     float cforce[1 + HA_MAX_LINKS + 1 + NOBJ][3];
     float dforce[HA_MAX_DOFS];      /* joint force of the last substep: (drive + lower - upper impulse) / h */
     const float* dr;                /* this env's DR row (HA_DR_*) or NULL (ha_physics.h SimCtx::dr) */
@@ -306,14 +309,28 @@ static float wave_dot(const float* a, const float* b, int n) {
 /* ------------------------------------------------------------------ collision */
 typedef struct { v3 p; qt q; } pose_t;
 
-static v3 hull_vert(const ha_model_t* m, int hull, int i, pose_t P) {
+/* Per-env object dimensions: sc = diag scale of the hull in its body frame, or NULL (unscaled). Mirrors
+ * scale3 / scale_radius / world_plane in ha_physics.h. */
+static v3 scl(const float* sc, v3 v) { return sc ? V(v.x * sc[0], v.y * sc[1], v.z * sc[2]) : v; }
+static float scl_r(const float* sc, float r) { return sc ? r * fmaxf(fmaxf(sc[0], sc[1]), sc[2]) : r; }
+static const float* env_scale(const env_t* e, int b) { return (b >= 0 && b < NOBJ && e->oscaled[b]) ? e->osc[b] : NULL; }
+
+static v3 hull_vert(const ha_model_t* m, int hull, int i, pose_t P, const float* sc) {
     const float* v = m->verts[m->hull_vert_start[hull] + i];
-    return add(P.p, qrot(P.q, V(v[0], v[1], v[2])));
+    return add(P.p, qrot(P.q, scl(sc, V(v[0], v[1], v[2]))));
 }
-static void hull_plane(const ha_model_t* m, int hull, int k, pose_t P, v3* n, float* d) {
+static void hull_plane(const ha_model_t* m, int hull, int k, pose_t P, const float* sc, v3* n, float* d) {
     const float* pl = m->planes[m->hull_plane_start[hull] + k];
-    *n = qrot(P.q, V(pl[0], pl[1], pl[2]));
-    *d = pl[3] - dot(*n, P.p);
+    v3 nl = V(pl[0], pl[1], pl[2]);
+    float dl = pl[3];
+    if (sc) {
+        nl = V(pl[0] * (1.0f / sc[0]), pl[1] * (1.0f / sc[1]), pl[2] * (1.0f / sc[2]));
+        float inv = 1.0f / sqrtf(dot(nl, nl));
+        nl = mul(nl, inv);
+        dl = dl * inv;
+    }
+    *n = qrot(P.q, nl);
+    *d = dl - dot(*n, P.p);
 }
 
 /* reduce candidate list (points, sep) to <= 4 contacts; returns count appended */
@@ -369,23 +386,24 @@ static int emit(contact_t* out, int* nout, int maxout, v3* pts, float* seps, int
 
 /* hull A (body a) vs hull B (body b); contact normal from B to A */
 static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t PB, float margin, int a, int b,
-                          contact_t* out, int* nout, int maxout) {
+                          const float* sca, const float* scb, contact_t* out, int* nout, int maxout) {
     int nva = m->hull_nverts[ha], nvb = m->hull_nverts[hb];
     int npa = m->hull_nplanes[ha], npb = m->hull_nplanes[hb];
     /* bounding spheres */
-    v3 ca = add(PA.p, qrot(PA.q, ld3(m->hull_center[ha]))), cb = add(PB.p, qrot(PB.q, ld3(m->hull_center[hb])));
+    v3 ca = add(PA.p, qrot(PA.q, scl(sca, ld3(m->hull_center[ha]))));
+    v3 cb = add(PB.p, qrot(PB.q, scl(scb, ld3(m->hull_center[hb]))));
     v3 dc = sub(ca, cb);
-    float rr = m->hull_radius[ha] + m->hull_radius[hb] + margin;
+    float rr = scl_r(sca, m->hull_radius[ha]) + scl_r(scb, m->hull_radius[hb]) + margin;
     if (dot(dc, dc) > rr * rr) return;
     v3 va[64], vb[64];
-    for (int i = 0; i < nva; i++) va[i] = hull_vert(m, ha, i, PA);
-    for (int i = 0; i < nvb; i++) vb[i] = hull_vert(m, hb, i, PB);
+    for (int i = 0; i < nva; i++) va[i] = hull_vert(m, ha, i, PA, sca);
+    for (int i = 0; i < nvb; i++) vb[i] = hull_vert(m, hb, i, PB, scb);
     /* SAT over face normals */
     float sepA = -1e30f, sepB = -1e30f;
     int kA = -1, kB = -1;
     for (int k = 0; k < npa; k++) {
         v3 n; float d;
-        hull_plane(m, ha, k, PA, &n, &d);
+        hull_plane(m, ha, k, PA, sca, &n, &d);
         float mn = 1e30f;
         for (int i = 0; i < nvb; i++) { float s = dot(n, vb[i]) + d; if (s < mn) mn = s; }
         if (mn > sepA) { sepA = mn; kA = k; }
@@ -393,7 +411,7 @@ static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t
     if (sepA > margin) return;
     for (int k = 0; k < npb; k++) {
         v3 n; float d;
-        hull_plane(m, hb, k, PB, &n, &d);
+        hull_plane(m, hb, k, PB, scb, &n, &d);
         float mn = 1e30f;
         for (int i = 0; i < nva; i++) { float s = dot(n, va[i]) + d; if (s < mn) mn = s; }
         if (mn > sepB) { sepB = mn; kB = k; }
@@ -405,10 +423,11 @@ static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t
         int refB = (sepB >= sepA) ? (pass == 0) : (pass == 1);
         int hr = refB ? hb : ha, hi = refB ? ha : hb, kr = refB ? kB : kA;
         pose_t Pr = refB ? PB : PA;
+        const float* scr = refB ? scb : sca;
         v3* vi = refB ? va : vb;
         int nvi = refB ? nva : nvb, npr = m->hull_nplanes[hr];
         v3 nref; float dref;
-        hull_plane(m, hr, kr, Pr, &nref, &dref);
+        hull_plane(m, hr, kr, Pr, scr, &nref, &dref);
         int nc = 0;
         for (int i = 0; i < nvi && nc < MAXCAND; i++) {
             float dist = dot(nref, vi[i]) + dref;
@@ -417,7 +436,7 @@ static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t
             for (int k = 0; k < npr; k++) {
                 if (k == kr) continue;
                 v3 n; float d;
-                hull_plane(m, hr, k, Pr, &n, &d);
+                hull_plane(m, hr, k, Pr, scr, &n, &d);
                 float s = dot(n, vi[i]) + d;
                 if (s > mx) mx = s;
             }
@@ -434,15 +453,15 @@ static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t
     }
 }
 
-static void collide_ground(const ha_model_t* m, int ha, pose_t PA, float margin, int a, contact_t* out, int* nout,
-                           int maxout) {
-    v3 c = add(PA.p, qrot(PA.q, ld3(m->hull_center[ha])));
-    if (c.z - m->hull_radius[ha] > margin) return;
+static void collide_ground(const ha_model_t* m, int ha, pose_t PA, float margin, int a, const float* sca,
+                           contact_t* out, int* nout, int maxout) {
+    v3 c = add(PA.p, qrot(PA.q, scl(sca, ld3(m->hull_center[ha]))));
+    if (c.z - scl_r(sca, m->hull_radius[ha]) > margin) return;
     v3 pts[64];
     float seps[64];
     int nc = 0;
     for (int i = 0; i < m->hull_nverts[ha]; i++) {
-        v3 v = hull_vert(m, ha, i, PA);
+        v3 v = hull_vert(m, ha, i, PA, sca);
         if (v.z <= margin) { pts[nc] = sub(v, V(0, 0, 0.5f * v.z)); seps[nc] = v.z; nc++; }
     }
     emit(out, nout, maxout, pts, seps, nc, V(0, 0, 1), a, -1);
@@ -467,20 +486,23 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
     for (int o = 0; o < h->NO; o++) {
         if (!e->coll[o]) continue;
         int ho = m->pool_hull[e->pool[o]];
-        pose_t Po = {sub(e->oc[o], qrot(e->oq[o], ld3(m->pool_com[e->pool[o]]))), e->oq[o]};
-        collide_ground(m, ho, Po, mg, o, out, &nout, MAXC);
-        if (m->table_hull >= 0 && near_table(m, Ptab, add(Po.p, qrot(Po.q, ld3(m->hull_center[ho]))), m->hull_radius[ho] + mg))
-            collide_hulls(m, ho, Po, m->table_hull, Ptab, mg, o, -1, out, &nout, MAXC);
+        const float* so = env_scale(e, o);
+        pose_t Po = {sub(e->oc[o], qrot(e->oq[o], scl(so, ld3(m->pool_com[e->pool[o]])))), e->oq[o]};
+        collide_ground(m, ho, Po, mg, o, so, out, &nout, MAXC);
+        if (m->table_hull >= 0 &&
+            near_table(m, Ptab, add(Po.p, qrot(Po.q, scl(so, ld3(m->hull_center[ho])))), scl_r(so, m->hull_radius[ho]) + mg))
+            collide_hulls(m, ho, Po, m->table_hull, Ptab, mg, o, -1, so, NULL, out, &nout, MAXC);
         for (int o2 = o + 1; o2 < h->NO; o2++) {
             if (!e->coll[o2]) continue;
             int h2 = m->pool_hull[e->pool[o2]];
-            pose_t P2 = {sub(e->oc[o2], qrot(e->oq[o2], ld3(m->pool_com[e->pool[o2]]))), e->oq[o2]};
-            collide_hulls(m, ho, Po, h2, P2, mg, o, o2, out, &nout, MAXC);
+            const float* s2 = env_scale(e, o2);
+            pose_t P2 = {sub(e->oc[o2], qrot(e->oq[o2], scl(s2, ld3(m->pool_com[e->pool[o2]])))), e->oq[o2]};
+            collide_hulls(m, ho, Po, h2, P2, mg, o, o2, so, s2, out, &nout, MAXC);
         }
         for (int k = 0; k < m->n_link_hulls; k++) {
             int L = m->hull_link[k];
             pose_t PL = {e->lp[L], e->lq[L]};
-            collide_hulls(m, k, PL, ho, Po, mg, 100 + L, o, out, &nout, MAXC);
+            collide_hulls(m, k, PL, ho, Po, mg, 100 + L, o, NULL, so, out, &nout, MAXC);
         }
     }
     for (int k = 0; k < m->n_link_hulls; k++) {
@@ -488,7 +510,7 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
         if (m->table_hull < 0 || !m->link_table_collide[L]) continue;
         pose_t PL = {e->lp[L], e->lq[L]};
         if (near_table(m, Ptab, add(PL.p, qrot(PL.q, ld3(m->hull_center[k]))), m->hull_radius[k] + mg))
-            collide_hulls(m, k, PL, m->table_hull, Ptab, mg, 100 + L, -1, out, &nout, MAXC);
+            collide_hulls(m, k, PL, m->table_hull, Ptab, mg, 100 + L, -1, NULL, NULL, out, &nout, MAXC);
     }
     return nout;
 }
@@ -567,17 +589,34 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
     }
     for (int o = 0; o < NO; o++) {
         float damp = 1.0f / (1.0f + hdt * p->object_ang_damping);
-        v3 lv = add(e->ov[o], mul(ld3(p->gravity), hdt));
+        float R[9], Iw[9], Il[9];
+        const float* I0 = m->pool_inertia[e->pool[o]];
+        float sc = e->dr ? e->dr[HA_DR_OBJ_MASS + o] : 1.0f;
+        float mass = m->pool_mass[e->pool[o]];
+        for (int k = 0; k < 9; k++) Il[k] = I0[k];
+        if (e->oscaled[o]) {
+            /* uniform density scaled by S: C = tr(I)/2 Id - I, C' = det(S) S C S, I' = tr(C') Id - C' */
+            const float* sv = e->osc[o];
+            float det = (sv[0] * sv[1]) * sv[2];
+            float hh = 0.5f * ((I0[0] + I0[4]) + I0[8]);
+            float Cs[9];
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++) Cs[3 * i + j] = det * (sv[i] * (((i == j ? hh : 0.0f) - I0[3 * i + j]) * sv[j]));
+            float tr = (Cs[0] + Cs[4]) + Cs[8];
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++) Il[3 * i + j] = (i == j ? tr : 0.0f) - Cs[3 * i + j];
+            mass = mass * det;
+        }
+        qmat(e->oq[o], R);
+        rart(R, Il, Iw);
+        for (int k = 0; k < 9; k++) Iw[k] = Iw[k] * sc;
+        inv3(Iw, e->oIinv[o]);
+        mass = mass * sc;
+        e->om[o] = mass;
+        v3 lv = add(add(e->ov[o], mul(ld3(p->gravity), hdt)), mul(e->ofx[o], hdt / mass));
         v3 av = mul(e->ow[o], damp);
         float* vo = v + D + 6 * o;
         vo[0] = lv.x; vo[1] = lv.y; vo[2] = lv.z; vo[3] = av.x; vo[4] = av.y; vo[5] = av.z;
-        float R[9], Iw[9];
-        qmat(e->oq[o], R);
-        rart(R, m->pool_inertia[e->pool[o]], Iw);
-        float sc = e->dr ? e->dr[HA_DR_OBJ_MASS + o] : 1.0f;
-        for (int k = 0; k < 9; k++) Iw[k] = Iw[k] * sc;
-        inv3(Iw, e->oIinv[o]);
-        e->om[o] = m->pool_mass[e->pool[o]] * sc;
     }
     /* contacts -> rows (normal, friction 1, friction 2 per contact) */
     contact_t cs[MAXC];
@@ -735,7 +774,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
 }
 
 /* ------------------------------------------------------------------ state load/store */
-static void load_env(const hao_handle h, const ha_state_t* S, int env, env_t* e) {
+static void load_env(const hao_handle h, const ha_state_t* S, int env, env_t* e, int take_force) {
     const ha_model_t* m = &h->m;
     int D = h->D, A = h->A;
     for (int d = 0; d < D; d++) {
@@ -747,8 +786,16 @@ static void load_env(const hao_handle h, const ha_state_t* S, int env, env_t* e)
         const float* r = S->root_state + (env * A + m->actor_object0 + o) * 13;
         int pid = (int)S->object_indices[env * h->NO + o];
         e->pool[o] = pid;
+        e->oscaled[o] = S->object_scale != NULL;
+        for (int k = 0; k < 3; k++) e->osc[o][k] = S->object_scale ? S->object_scale[(env * h->NO + o) * 3 + k] : 1.0f;
+        e->ofx[o] = V(0, 0, 0);
+        if (take_force && S->object_force) {
+            float* fo = S->object_force + (env * h->NO + o) * 3;
+            e->ofx[o] = ld3(fo);
+            fo[0] = fo[1] = fo[2] = 0.0f;
+        }
         e->oq[o] = ldq(r + 3);
-        e->oc[o] = add(ld3(r), qrot(e->oq[o], ld3(m->pool_com[pid])));
+        e->oc[o] = add(ld3(r), qrot(e->oq[o], scl(env_scale(e, o), ld3(m->pool_com[pid]))));
         e->ov[o] = ld3(r + 7);
         e->ow[o] = ld3(r + 10);
         e->coll[o] = S->collision_enabled ? S->collision_enabled[env * h->NO + o] : 1;
@@ -767,7 +814,7 @@ static void store_env(const hao_handle h, ha_state_t* S, int env, env_t* e) {
     }
     for (int o = 0; o < h->NO; o++) {
         float* r = S->root_state + (env * A + m->actor_object0 + o) * 13;
-        v3 pos = sub(e->oc[o], qrot(e->oq[o], ld3(m->pool_com[e->pool[o]])));
+        v3 pos = sub(e->oc[o], qrot(e->oq[o], scl(env_scale(e, o), ld3(m->pool_com[e->pool[o]]))));
         st3(r, pos); stq(r + 3, e->oq[o]); st3(r + 7, e->ov[o]); st3(r + 10, e->ow[o]);
     }
     /* rigid body states in the env's layout: robot links, objects, goal and table copied from the roots */
@@ -819,7 +866,7 @@ int hao_struct_sizes(int32_t* model_size, int32_t* params_size, int32_t* state_s
 
 static void simulate_env(const hao_handle h, ha_state_t* S, int env, int n_calls) {
     env_t e;
-    load_env(h, S, env, &e);
+    load_env(h, S, env, &e, 1);
     e.dr = (h->p.dr_enable && S->dr_scale) ? S->dr_scale + (size_t)env * HA_DR_SIZE : NULL;
     float hdt = h->p.dt / (float)h->p.substeps;
     for (int c = 0; c < n_calls; c++)

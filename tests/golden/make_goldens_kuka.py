@@ -1,0 +1,460 @@
+#!/usr/bin/env python3
+"""Golden vectors for the AllegroKuka tasks (config C2) by RUNNING THE REFERENCE
+(tasks/allegro_kuka/allegro_kuka_base.py + allegro_kuka_regrasping.py / allegro_kuka_reorientation.py).
+
+Run in the build container only (needs /root/reference):  python tests/golden/make_goldens_kuka.py
+Writes ``kuka_*.npz`` (data only) next to this file.
+
+Reference code exercised, unmodified, through a fake ``self`` carrying what ``__init__`` /
+``_create_envs`` / ``VecTask.__init__`` would have allocated (values from cfg/task/AllegroKuka.yaml and
+cfg/task/env/<subtask>.yaml, read here with yaml.safe_load):
+  * the cuboid family: ``generate_*`` (generate_cuboids.py) into a temporary directory, then
+    ``_box_asset_files_and_scales`` / ``_main_object_assets_and_scales`` (allegro_kuka_base.py:411-512):
+    ``kuka_object_dims.npz`` pins the per-env object dimensions the build's scene JSON carries;
+  * ``post_physics_step`` (:1426-1447) -> ``compute_observations`` (:991-1089) -> ``compute_full_state``
+    (:1091-1172) -> ``compute_kuka_reward`` (:854-930): ``kuka_obs_reward_<subtask>.npz``;
+  * ``pre_physics_step`` (:1355-1424) with ``reset_target_pose`` / ``_reset_target`` / ``reset_object_pose``
+    / ``reset_idx`` and the random object forces, then ``post_physics_step`` and VecTask.step's timeout rule
+    (vec_task.py:424), over several steps: ``kuka_steps_<subtask>.npz``. Every random draw
+    (torch_rand_float, torch.rand, torch.randn) is recorded per env in the slot the device replays
+    (ak_task.h AK_DRAW_*).
+``gym.simulate`` is not run: between pre- and post-physics the rigid-body tensor is refreshed from the dof
+state by the build's own forward kinematics (the C oracle with zero substeps), which is what the device's
+no-physics step does too; these goldens pin the task math, not the physics.
+"""
+import json
+import os
+import sys
+import tempfile
+from unittest import mock
+
+import numpy as np
+import torch
+import yaml
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "isaacgym-hand-arm_amd"))
+import refload  # noqa: E402
+
+from handarm_hip import model as HM  # noqa: E402
+
+REF_CFG = "/root/reference/isaacgymenvs/cfg/task"
+SCENE = HM.KUKA_ASSET
+CLS = {"regrasping": "AllegroKukaRegrasping", "reorientation": "AllegroKukaReorientation"}
+L, OBJ_BODY, TABLE_BODY, GOAL_BODY, NB = 24, 24, 25, 26, 27
+
+
+def env_cfg(sub):
+    base = yaml.safe_load(open(os.path.join(REF_CFG, "AllegroKuka.yaml")))["env"]
+    base.update(yaml.safe_load(open(os.path.join(REF_CFG, "env", sub + ".yaml"))))
+    return base
+
+
+def reference_object_scales(base, t):
+    """The reference's own asset generation and ordering (files written to a temp dir)."""
+    with tempfile.TemporaryDirectory() as d:
+        files, scales = t._main_object_assets_and_scales("/root/reference/assets", d)
+    return np.array(scales, np.float64), [os.path.basename(f) for f in files]
+
+
+def make_task(sub, N):
+    mod = refload.load("isaacgymenvs.tasks.allegro_kuka.allegro_kuka_" + sub)
+    base = refload.load("isaacgymenvs.tasks.allegro_kuka.allegro_kuka_base")
+    scene = json.load(open(SCENE))
+    dofs = scene["robot"]["dofs"]
+    cfg = env_cfg(sub)
+    t = object.__new__(getattr(mod, CLS[sub]))
+    t.cfg = {"env": cfg, "task": {"randomize": False}}
+    e = cfg
+    # AllegroKukaBase.__init__ (allegro_kuka_base.py:53-400), field by field
+    t.frame_since_restart = 0
+    t.clamp_abs_observations = e["clampAbsObservations"]
+    t.privileged_actions = e["privilegedActions"]
+    t.num_arm_dofs, t.num_finger_dofs, t.num_allegro_fingertips = 7, 4, 4
+    t.num_hand_dofs, t.num_hand_arm_dofs, t.num_allegro_kuka_actions = 16, 23, 23
+    t.randomize = False
+    t.distance_delta_rew_scale = e["distanceDeltaRewScale"]
+    t.lifting_rew_scale, t.lifting_bonus = e["liftingRewScale"], e["liftingBonus"]
+    t.lifting_bonus_threshold, t.keypoint_rew_scale = e["liftingBonusThreshold"], e["keypointRewScale"]
+    t.kuka_actions_penalty_scale = e["kukaActionsPenaltyScale"]
+    t.allegro_actions_penalty_scale = e["allegroActionsPenaltyScale"]
+    t.initial_tolerance = t.success_tolerance = e["successTolerance"]
+    t.target_tolerance = e["targetSuccessTolerance"]
+    t.tolerance_curriculum_increment = e["toleranceCurriculumIncrement"]
+    t.tolerance_curriculum_interval = e["toleranceCurriculumInterval"]
+    t.save_states, t.should_load_initial_states = False, False
+    t.reach_goal_bonus, t.fall_dist, t.fall_penalty = e["reachGoalBonus"], e["fallDistance"], e["fallPenalty"]
+    t.reset_position_noise_x, t.reset_position_noise_y = e["resetPositionNoiseX"], e["resetPositionNoiseY"]
+    t.reset_position_noise_z, t.reset_rotation_noise = e["resetPositionNoiseZ"], e["resetRotationNoise"]
+    t.reset_dof_pos_noise_fingers = e["resetDofPosRandomIntervalFingers"]
+    t.reset_dof_pos_noise_arm = e["resetDofPosRandomIntervalArm"]
+    t.reset_dof_vel_noise = e["resetDofVelRandomInterval"]
+    t.force_scale, t.force_decay_interval = e["forceScale"], e["forceDecayInterval"]
+    t.hand_dof_speed_scale, t.use_relative_control = e["dofSpeedScale"], e["useRelativeControl"]
+    t.act_moving_average, t.debug_viz = e["actionsMovingAverage"], False
+    t.max_episode_length, t.reset_time = e["episodeLength"], -1.0
+    t.max_consecutive_successes, t.success_steps = e["maxConsecutiveSuccesses"], e["successSteps"]
+    t.keypoint_scale, t.object_base_size = e["keypointScale"], e["objectBaseSize"]
+    t.randomize_object_dimensions = e["randomizeObjectDimensions"]
+    t.with_small_cuboids, t.with_big_cuboids, t.with_sticks = e["withSmallCuboids"], e["withBigCuboids"], e["withSticks"]
+    t.with_dof_force_sensors = t.with_fingertip_force_sensors = False
+    t.object_type = e["objectType"]
+    t.asset_files_dict = {"block": "urdf/objects/cube_multicolor.urdf", "table": "urdf/table_narrow.urdf"}
+    t.keypoints_offsets = t._object_keypoint_offsets()
+    t.num_keypoints = len(t.keypoints_offsets)
+    t.allegro_fingertips = ["index_link_3", "middle_link_3", "ring_link_3", "thumb_link_3"]
+    t.fingertip_offsets = np.array([[0.05, 0.005, 0], [0.05, 0.005, 0], [0.05, 0.005, 0], [0.06, 0.005, 0]],
+                                   dtype=np.float32)
+    t.palm_offset = np.array([-0.00, -0.02, 0.16], dtype=np.float32)
+    t.obs_type = "full_state"
+    t.full_state_size = 23 + 23 + 3 + 10 + 10 + 12 + 6 * t.num_keypoints + 3 + 1 + 1 + 2 + 4 + 1
+    t.num_environments, t.device, t.dt, t.control_freq_inv = N, "cpu", 0.01667, 1
+    t.viewer, t.eval_stats, t.up_axis_idx = None, False, 2
+    t.gym, t.sim = mock.MagicMock(), None
+    t.target_volume_origin = torch.from_numpy(np.array([0, 0.05, 0.8], dtype=np.float32))
+    t.target_volume_extent = torch.from_numpy(np.array([[-0.4, 0.4], [-0.05, 0.3], [-0.12, 0.25]], dtype=np.float32))
+    # _create_envs: per-env objects (i % len) with their scales and keypoint offsets (:655-715)
+    scales, names = reference_object_scales(base, t)
+    t.object_asset_scales = [[float(x) for x in s] for s in scales]   # python floats, as parsed (:509)
+    t.arm_hand_dof_lower_limits = torch.tensor([d["lower"] for d in dofs], dtype=torch.float32)
+    t.arm_hand_dof_upper_limits = torch.tensor([d["upper"] for d in dofs], dtype=torch.float32)
+    from copy import copy
+    object_scales, object_keypoint_offsets = [], []
+    for i in range(N):
+        object_scale = t.object_asset_scales[i % len(scales)]
+        object_scales.append(object_scale)
+        object_offsets = []
+        for keypoint in t.keypoints_offsets:
+            keypoint = copy(keypoint)
+            for coord_idx in range(3):
+                keypoint[coord_idx] *= object_scale[coord_idx] * t.object_base_size * t.keypoint_scale / 2
+            object_offsets.append(keypoint)
+        object_keypoint_offsets.append(object_offsets)
+    t.object_scales = torch.tensor(object_scales, dtype=torch.float)
+    t.object_keypoint_offsets = torch.tensor(object_keypoint_offsets, dtype=torch.float)
+    # gymapi.Vec3 is float32: object_start_pose = allegro_pose (0, 0.8, 0) + (0, -0.8, 0.38 + 0.25)
+    oy = float(np.float32(float(np.float32(0.8)) + -0.8))
+    oz = float(np.float32(0.0 + (0.38 + 0.25)))
+    t.object_init_state = torch.tensor([0.0, oy, oz, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0]).repeat(N, 1)
+    t.goal_states = t.object_init_state.clone()
+    t.goal_states[:, 2] -= 0.04
+    t.goal_init_state = t.goal_states.clone()
+    t.allegro_fingertip_handles = torch.tensor([11, 15, 19, 23], dtype=torch.long)
+    t.allegro_palm_handle = 7
+    t.object_rb_handles = torch.tensor([OBJ_BODY], dtype=torch.long)
+    s0 = t.object_asset_scales[0]
+    t.object_rb_masses = torch.tensor([400.0 * (0.05 * s0[0]) * (0.05 * s0[1]) * (0.05 * s0[2])], dtype=torch.float)
+    t.allegro_hand_indices = torch.arange(N) * 4
+    t.object_indices = torch.arange(N) * 4 + 1
+    t.goal_object_indices = torch.arange(N) * 4 + 3
+    t.set_actor_root_state_object_indices = []
+    # __init__ tensors after VecTask.__init__ (:262-389)
+    t.dof_state = torch.zeros(N * 23, 2)
+    t.hand_arm_default_dof_pos = torch.zeros(23)
+    t.hand_arm_default_dof_pos[:7] = torch.tensor([-1.571, 1.571, -0.000, 1.376, -0.000, 1.485, 2.358])
+    t.arm_hand_dof_state = t.dof_state.view(N, -1, 2)[:, :23]
+    t.arm_hand_dof_pos = t.arm_hand_dof_state[..., 0]
+    t.arm_hand_dof_vel = t.arm_hand_dof_state[..., 1]
+    t.rigid_body_states = torch.zeros(N, NB, 13)
+    t.num_bodies = NB
+    t.root_state_tensor = torch.zeros(N * 4, 13)
+    t.root_state_tensor[:, 6] = 1.0
+    t.num_dofs = 23
+    t.prev_targets = torch.zeros(N, 23)
+    t.cur_targets = torch.zeros(N, 23)
+    t.reset_buf = torch.ones(N, dtype=torch.long)
+    t.reset_goal_buf = t.reset_buf.clone()
+    t.successes = torch.zeros(N)
+    t.prev_episode_successes = torch.zeros(N)
+    t.true_objective = torch.zeros(N)
+    t.prev_episode_true_objective = torch.zeros(N)
+    t.force_decay = torch.tensor(e["forceDecay"], dtype=torch.float)
+    t.force_prob_range = torch.tensor(e["forceProbRange"], dtype=torch.float)
+    t.random_force_prob = torch.exp((torch.log(t.force_prob_range[0]) - torch.log(t.force_prob_range[1]))
+                                    * torch.rand(N) + torch.log(t.force_prob_range[1]))
+    t.rb_forces = torch.zeros(N, NB, 3)
+    t.action_torques = torch.zeros(N, NB, 3)
+    t.obj_keypoint_pos = torch.zeros(N, t.num_keypoints, 3)
+    t.goal_keypoint_pos = torch.zeros(N, t.num_keypoints, 3)
+    t.near_goal_steps = torch.zeros(N, dtype=torch.int)
+    t.lifted_object = torch.zeros(N, dtype=torch.bool)
+    t.closest_keypoint_max_dist = -torch.ones(N)
+    t.closest_fingertip_dist = -torch.ones(N, 4)
+    t.furthest_hand_dist = -torch.ones(N)
+    t.finger_rew_coeffs = torch.ones(N, 4)
+    t.rewards_episode = {k: torch.zeros(N) for k in HM.AK_REWARD_KEYS}
+    t.last_curriculum_update = 0
+    t.obs_buf = torch.zeros(N, t.full_state_size)
+    t.rew_buf = torch.zeros(N)
+    t.progress_buf = torch.zeros(N, dtype=torch.long)
+    t.randomize_buf = torch.zeros(N, dtype=torch.long)
+    t.timeout_buf = torch.zeros(N, dtype=torch.long)
+    t.extras = {}
+    return mod, base, t, scales, names
+
+
+def pack_task_state(t):
+    """The reference's per-env task tensors in the device's task_state row layout (HA_AK_*)."""
+    N = t.num_environments
+    ts = np.zeros((N, HM.AK_TS), np.float32)
+    ts[:, HM.AK_LIFTED] = t.lifted_object.float().numpy()
+    ts[:, HM.AK_CLOSEST_KP] = t.closest_keypoint_max_dist.numpy()
+    ts[:, HM.AK_CLOSEST_FT:HM.AK_CLOSEST_FT + 4] = t.closest_fingertip_dist.numpy()
+    ts[:, HM.AK_FURTHEST] = t.furthest_hand_dist.numpy()
+    ts[:, HM.AK_NEAR_GOAL] = t.near_goal_steps.float().numpy()
+    ts[:, HM.AK_PREV_SUCC] = t.prev_episode_successes.numpy()
+    ts[:, HM.AK_TRUE_OBJ] = t.true_objective.numpy()
+    ts[:, HM.AK_PREV_TRUE_OBJ] = t.prev_episode_true_objective.numpy()
+    ts[:, HM.AK_FORCE_PROB] = t.random_force_prob.numpy()
+    ts[:, HM.AK_RB_FORCE:HM.AK_RB_FORCE + 3] = t.rb_forces[:, OBJ_BODY].numpy()
+    for k, name in enumerate(HM.AK_REWARD_KEYS):
+        ts[:, HM.AK_REW_EP + k] = t.rewards_episode[name].numpy()
+    kp = t.object_keypoint_offsets.numpy()
+    ts[:, HM.AK_KP:HM.AK_KP + 3 * kp.shape[1]] = kp.reshape(N, -1)
+    return ts
+
+
+def randomize_state(t, g, scene_lo, scene_hi):
+    """Arbitrary but physically plausible inputs: dof / body / object / goal states and episode counters."""
+    N = t.num_environments
+    t.arm_hand_dof_pos[:] = scene_lo + (scene_hi - scene_lo) * torch.rand(N, 23, generator=g)
+    t.arm_hand_dof_vel[:] = torch.randn(N, 23, generator=g)
+    r = t.root_state_tensor.view(N, 4, 13)
+    base = torch.tensor([0.0, 0.0, 0.6])
+    r[:, 1, 0:3] = base + 0.1 * torch.randn(N, 3, generator=g)
+    r[:4, 1, 2] = torch.tensor([0.05, 0.09, 0.75, 0.9])       # falls and lifts
+    qo = torch.randn(N, 4, generator=g)
+    r[:, 1, 3:7] = qo / qo.norm(dim=-1, keepdim=True)
+    r[:, 1, 7:13] = torch.randn(N, 6, generator=g)
+    # palm / fingertip bodies near the object
+    rb = t.rigid_body_states
+    rb[:] = 0
+    rb[:, :, 0:3] = r[:, 1:2, 0:3] + 0.08 * torch.randn(N, NB, 3, generator=g)
+    q = torch.randn(N, NB, 4, generator=g)
+    rb[:, :, 3:7] = q / q.norm(dim=-1, keepdim=True)
+    rb[:, :, 7:13] = torch.randn(N, NB, 6, generator=g)
+    rb[:, OBJ_BODY] = r[:, 1]
+    t.goal_states[:, 0:3] = r[:, 1, 0:3] + 0.05 * torch.randn(N, 3, generator=g)
+    near = torch.rand(N, generator=g) < 0.3
+    t.goal_states[near, 0:3] = r[near, 1, 0:3] + 0.01 * torch.randn(int(near.sum()), 3, generator=g)
+    gq = torch.randn(N, 4, generator=g)
+    t.goal_states[:, 3:7] = gq / gq.norm(dim=-1, keepdim=True)
+    t.goal_states[near, 3:7] = r[near, 1, 3:7]
+    t.progress_buf[:] = torch.randint(0, t.max_episode_length, (N,), generator=g)
+    t.progress_buf[:3] = t.max_episode_length - 2
+    t.successes[:] = torch.randint(0, 5, (N,), generator=g).float()
+    t.successes[3:5] = t.max_consecutive_successes - 1
+    t.near_goal_steps[:] = torch.randint(0, t.success_steps + 1, (N,), generator=g).int()
+    t.lifted_object[:] = torch.rand(N, generator=g) < 0.4
+    unset = torch.rand(N, generator=g) < 0.3
+    t.closest_keypoint_max_dist[:] = torch.where(unset, -1.0, 0.2 * torch.rand(N, generator=g))
+    t.closest_fingertip_dist[:] = torch.where(unset[:, None], -1.0, 0.2 * torch.rand(N, 4, generator=g))
+    t.furthest_hand_dist[:] = torch.where(unset, -1.0, 0.2 * torch.rand(N, generator=g))
+    for k in HM.AK_REWARD_KEYS:
+        t.rewards_episode[k][:] = torch.randn(N, generator=g)
+    t.reset_buf[:] = (torch.rand(N, generator=g) < 0.1).long()
+
+
+def obs_reward(sub, N=48, steps=4, seed=1):
+    mod, base, t, _, _ = make_task(sub, N)
+    g = torch.Generator().manual_seed(seed)
+    lo, hi = t.arm_hand_dof_lower_limits, t.arm_hand_dof_upper_limits
+    out = {}
+
+    def rec(k, v):
+        out.setdefault(k, []).append(np.array(v, copy=True))
+    for s in range(steps):
+        randomize_state(t, g, lo, hi)
+        rec("dof_state", t.dof_state.numpy())
+        rec("root_state", t.root_state_tensor.numpy())
+        rec("rigid_body_state", t.rigid_body_states.reshape(N * NB, 13).numpy())
+        rec("goal_state", t.goal_states[:, 0:7].numpy())
+        rec("task_state_in", pack_task_state(t))
+        rec("progress_in", (t.progress_buf + 1).numpy())      # post_physics_step increments first (:1429)
+        rec("successes_in", t.successes.numpy())
+        rec("reset_in", t.reset_buf.numpy())
+        t.post_physics_step()
+        rec("obs", t.obs_buf.numpy())
+        rec("rew", t.rew_buf.numpy())
+        rec("reset", t.reset_buf.numpy())
+        rec("reset_goal", t.reset_goal_buf.numpy())
+        rec("progress", t.progress_buf.numpy())
+        rec("successes", t.successes.numpy())
+        rec("task_state", pack_task_state(t))
+    res = {k: np.stack(v) for k, v in out.items()}
+    res["object_scale"] = t.object_scales.numpy()
+    np.savez_compressed(os.path.join(HERE, f"kuka_obs_reward_{sub}.npz"), **res)
+
+
+def refresh_bodies(t, orc, st):
+    """Rigid-body tensor from the dof / root state by the build's FK (oracle simulate with 0 calls)."""
+    N = t.num_environments
+    st["dof_state"][:] = t.dof_state.numpy()
+    st["root_state"][:] = t.root_state_tensor.numpy()
+    orc.simulate(st, 0)
+    t.rigid_body_states[:] = torch.from_numpy(st["rigid_body_state"].reshape(N, NB, 13))
+
+
+def steps(sub, N=32, T=8, seed=2):
+    from oracle.oracle_lib import HostState, Oracle
+    mod, base, t, _, _ = make_task(sub, N)
+    model = HM.build_model(HM.load_scene(SCENE))
+    params, cfg = HM.build_params({"subtask": sub}, task=HM.TASK_ALLEGRO_KUKA)
+    st = HostState(N, model=model, params=params)
+    st["object_scale"][:] = t.object_scales.numpy()[:, None, :]
+    st["collision_enabled"][:] = 1
+    orc = Oracle(model, params, N)
+    torch.manual_seed(seed)
+    g = torch.Generator().manual_seed(seed)
+    draws = np.zeros((T, N, HM.DRAW_STRIDE), np.float32)
+    cur = {"step": 0, "ids": None, "phase": "pre", "in_target": False, "in_reset": False, "u": None}
+    cursor = np.zeros(N, np.int64)
+
+    def put(ids, v):
+        ids = ids.numpy().reshape(-1)
+        if len(ids) == 0:
+            return
+        v = v.reshape(len(ids), -1).numpy()
+        for j in range(v.shape[1]):
+            draws[cur["step"], ids, cursor[ids] + j] = v[:, j]
+        cursor[ids] += v.shape[1]
+
+    real_trf = base.torch_rand_float
+    orig_mod_trf = mod.torch_rand_float
+
+    def trf(lower, upper, shape, device):
+        v = real_trf(lower, upper, shape, device)
+        put(cur["ids"], v)
+        return v
+    base.torch_rand_float = trf
+    mod.torch_rand_float = trf
+    real_rand, real_randn = torch.rand, torch.randn
+
+    def rand(*a, **kw):
+        v = real_rand(*a, **kw)
+        if cur["phase"] == "force":
+            draws[cur["step"], :, 71] = v.numpy()
+            cur["u"] = v
+        elif cur["in_reset"]:
+            put(cur["ids"], v)                       # random_force_prob draw of reset_idx
+        return v
+
+    def randn(*a, **kw):
+        v = real_randn(*a, **kw)
+        if cur["phase"] == "force":
+            idx = (cur["u"] < t.random_force_prob).nonzero().reshape(-1).numpy()
+            if len(idx) == 0:
+                return v
+            draws[cur["step"], idx, 72:75] = v.reshape(len(idx), 3).numpy()
+        return v
+    o_rtp, o_rt, o_rop, o_ri, o_set = (t.reset_target_pose, t._reset_target, t.reset_object_pose, t.reset_idx,
+                                       t.set_actor_root_state_tensor_indexed)
+
+    def rtp(env_ids):
+        cur["ids"] = env_ids
+        return o_rtp(env_ids)
+
+    def rt(env_ids):
+        cur["in_target"] = True
+        try:
+            return o_rt(env_ids)
+        finally:
+            cur["in_target"] = False
+
+    def rop(env_ids):
+        if cur["in_reset"] and not cur["in_target"]:
+            cursor[env_ids.numpy()] = 18             # reset_idx's own reset_object_pose (AK_DRAW_OBJ)
+        cur["ids"] = env_ids
+        return o_rop(env_ids)
+
+    def ri(env_ids):
+        cur["in_reset"], cur["ids"] = True, env_ids
+        cursor[env_ids.numpy()] = 9                  # AK_DRAW_RESET_GOAL
+        try:
+            return o_ri(env_ids)
+        finally:
+            cur["in_reset"] = False
+
+    def setter():
+        cur["phase"] = "force"                       # everything after the resets is the per-step force draw
+        return o_set()
+    t.reset_target_pose, t._reset_target, t.reset_object_pose, t.reset_idx = rtp, rt, rop, ri
+    t.set_actor_root_state_tensor_indexed = setter
+    keys_in = ["dof_state", "root_state", "goal_state", "targets", "actions", "reset_in", "reset_goal_in",
+               "progress_in", "successes_in", "task_state_in"]
+    out = {}
+
+    def rec(k, v):
+        out.setdefault(k, []).append(np.array(v, copy=True))
+    with mock.patch.object(torch, "rand", rand), mock.patch.object(torch, "randn", randn):
+        for s in range(T):
+            cur["step"], cur["phase"] = s, "pre"
+            cursor[:] = 0
+            if s > 0:   # stand-in for physics between steps: move the object so lifts / falls / successes happen
+                r = t.root_state_tensor.view(N, 4, 13)
+                r[:, 1, 0:3] += 0.05 * real_randn(N, 3, generator=g)
+                lift = real_rand(N, generator=g) < 0.25
+                r[lift, 1, 2] += 0.2
+                at_goal = real_rand(N, generator=g) < 0.25
+                r[at_goal, 1, 0:3] = t.goal_states[at_goal, 0:3]
+                r[at_goal, 1, 3:7] = t.goal_states[at_goal, 3:7]
+                fall = real_rand(N, generator=g) < 0.05
+                r[fall, 1, 2] = 0.05
+                t.arm_hand_dof_vel[:] = 0.3 * real_randn(N, 23, generator=g)
+                t.progress_buf[real_rand(N, generator=g) < 0.1] = t.max_episode_length - 2
+            actions = 2 * real_rand(N, 23, generator=g) - 1
+            rec("dof_state", t.dof_state.numpy())
+            rec("root_state", t.root_state_tensor.numpy())
+            rec("goal_state", t.goal_states[:, 0:7].numpy())
+            rec("targets", t.prev_targets.numpy())
+            rec("actions", actions.numpy())
+            rec("reset_in", t.reset_buf.numpy())
+            rec("reset_goal_in", t.reset_goal_buf.numpy())
+            rec("progress_in", t.progress_buf.numpy())
+            rec("successes_in", t.successes.numpy())
+            rec("task_state_in", pack_task_state(t))
+            t.pre_physics_step(actions)
+            cur["phase"] = "post"
+            refresh_bodies(t, orc, st)
+            t.post_physics_step()
+            t.timeout_buf = (t.progress_buf >= t.max_episode_length - 1) & (t.reset_buf != 0)   # vec_task.py:424
+            for k, v in [("obs", t.obs_buf), ("rew", t.rew_buf), ("reset", t.reset_buf),
+                         ("reset_goal", t.reset_goal_buf), ("progress", t.progress_buf), ("successes", t.successes),
+                         ("timeout", t.timeout_buf), ("targets_after", t.prev_targets), ("dof_after", t.dof_state),
+                         ("root_after", t.root_state_tensor), ("goal_after", t.goal_states[:, 0:7])]:
+                rec(k, v.numpy())
+            rec("task_state", pack_task_state(t))
+    base.torch_rand_float, mod.torch_rand_float = real_trf, orig_mod_trf
+    res = {k: np.stack(v) for k, v in out.items()}
+    res["draws"] = draws
+    res["object_scale"] = t.object_scales.numpy()
+    assert set(keys_in) <= set(res)
+    np.savez_compressed(os.path.join(HERE, f"kuka_steps_{sub}.npz"), **res)
+
+
+def object_dims_and_curriculum():
+    mod, base, t, scales, names = make_task("regrasping", 4)
+    utils = refload.load("isaacgymenvs.tasks.allegro_kuka.allegro_kuka_utils")
+    cases, results = [], []
+    for last, frame, succ, tol in [(0, 2999, 5.0, 0.075), (0, 3000, 2.0, 0.075), (0, 3000, 3.5, 0.075),
+                                   (3000, 6500, 4.0, 0.0675), (0, 3000, 9.0, 0.0105), (100, 3100, 3.0, 0.02)]:
+        prev = torch.full((8,), succ)
+        new_tol, new_last = utils.tolerance_curriculum(last, frame, 3000, prev, tol, 0.075, 0.01, 0.9)
+        obj = utils.tolerance_successes_objective(new_tol, 0.075, 0.01, torch.tensor([0.0, 3.0, 50.0]))
+        cases.append([last, frame, succ, tol])
+        results.append([new_tol, new_last] + obj.tolist())
+    np.savez_compressed(os.path.join(HERE, "kuka_object_dims.npz"), scales=scales,
+                        names=np.array(names), curriculum_in=np.array(cases, np.float64),
+                        curriculum_out=np.array(results, np.float64))
+
+
+if __name__ == "__main__":
+    refload.install()
+    object_dims_and_curriculum()
+    for sub in ("regrasping", "reorientation"):
+        obs_reward(sub)
+        steps(sub)
+    print("wrote kuka_object_dims.npz, kuka_obs_reward_*.npz, kuka_steps_*.npz")

@@ -70,3 +70,36 @@ def fill_allegro_scene(st, num_envs, lower, upper, seed=0, in_hand=1.0):
     st["object_indices"][:] = 0
     st["collision_enabled"][:] = 1
     return st
+
+
+def fill_kuka_scene(st, num_envs, lower, upper, reset_pose, scales, table_pos, seed=0, object_force=0.0):
+    """AllegroKuka: arm near its default pose (reset_pose +- 0.1), fingers inside their limits, the cuboid
+    (per-env dimensions `scales`) resting on / dropping onto the table top with a random orientation, goal
+    somewhere in the target volume, optional random object forces."""
+    rng = np.random.default_rng(seed)
+    N = num_envs
+    rs = st["root_state"].reshape(N, 4, 13)
+    rs[:] = 0
+    rs[..., 6] = 1.0
+    half_z = 0.025 * scales[:, 0, :].max(-1)
+    rs[:, 1, 0:2] = rng.uniform(-0.08, 0.08, (N, 2))
+    rs[:, 1, 2] = 0.53 + half_z + rng.uniform(0.0, 0.05, N)
+    rs[:, 1, 3:7] = rand_quat(rng, (N,))
+    rs[:, 1, 7:10] = rng.uniform(-0.1, 0.1, (N, 3))
+    rs[:, 1, 10:13] = rng.uniform(-0.5, 0.5, (N, 3))
+    rs[:, 2, 0:3] = table_pos
+    rs[:, 3, 0:3] = rng.uniform([-0.4, 0.0, 0.68], [0.4, 0.35, 1.05], (N, 3))
+    st["goal_state"][:, 0:3] = rs[:, 3, 0:3]
+    st["goal_state"][:, 6] = 1.0
+    D = len(lower)
+    ds = st["dof_state"].reshape(N, D, 2)
+    base = np.array(reset_pose[:D], np.float32)
+    ds[..., 0] = np.clip(base + rng.uniform(-0.1, 0.1, (N, D)), lower, upper)
+    ds[:, 7:, 0] = lower[7:] + (upper[7:] - lower[7:]) * rng.uniform(0.1, 0.9, (N, D - 7)).astype(np.float32)
+    ds[..., 1] = rng.uniform(-0.3, 0.3, (N, D))
+    st["sim_targets"][:] = np.clip(ds[..., 0] + rng.uniform(-0.2, 0.2, (N, D)), lower, upper)
+    st["object_indices"][:] = 0
+    st["object_scale"][:] = scales
+    st["collision_enabled"][:] = 1
+    st["object_force"][:] = object_force * rng.standard_normal((N, 1, 3))
+    return st

@@ -76,7 +76,9 @@ def test_allegro_step_with_resets_replayed_against_reference_goldens():
         put(sim, "root_state", d["root_state"][t])       # the generator's stand-in for physics between steps
         put(sim, "progress_buf", d["progress_in"][t])
         put(sim, "actions", d["actions"][t])
-        put(sim, "reset_draws", d["draws"][t])
+        dr = np.zeros((N, HM.DRAW_STRIDE), np.float32)        # goldens hold the 48 AllegroHand slots
+        dr[:, :d["draws"].shape[-1]] = d["draws"][t]
+        put(sim, "reset_draws", dr)
         sim.task_step(flags)
         np.testing.assert_array_equal(get(sim, "reset_buf"), d["reset"][t])
         np.testing.assert_array_equal(get(sim, "reset_goal_buf"), d["reset_goal"][t])

@@ -366,14 +366,14 @@ def quat_axis_angle(axis, angle):
     return np.concatenate([a * math.sin(angle / 2), [math.cos(angle / 2)]])
 
 
-def build_allegro():
-    """allegro_touch_sensor.urdf loaded like tasks/allegro_hand.py:232-268: fix_base_link,
-    collapse_fixed_joints (fixed children merged into their parent body, which keeps the parent's
-    frame), disable_gravity, DOF_MODE_POS with stiffness 3, damping 0.1, effort 0.5, armature 0.001
-    (:264-268). Mass properties come from the URDF inertials (no override_com/inertia), combined with
-    the parallel-axis rule when bodies merge."""
-    base_dir = os.path.join(REF, "assets", "urdf")
-    root = ET.parse(ALLEGRO_URDF).getroot()
+def build_collapsed(urdf, dof_props, base_pos, base_quat):
+    """A URDF loaded with fix_base_link + collapse_fixed_joints (fixed children merged into their parent
+    body, which keeps the parent's frame). Mass properties come from the URDF inertials (no
+    override_com/inertia), combined with the parallel-axis rule when bodies merge. dof_props(name) gives
+    the drive settings of a joint. Mesh paths resolve against the URDF's directory, its parent, then the
+    asset root (the order Isaac Gym's URDF importer tries)."""
+    asset_root = os.path.join(REF, "assets")
+    root = ET.parse(urdf).getroot()
     links = {l.get("name"): l for l in root.findall("link")}
     parent_joint = {j.find("child").get("link"): j for j in root.findall("joint")}
     children = {}
@@ -422,9 +422,10 @@ def build_allegro():
             rec["axis"] = (a / np.linalg.norm(a)).tolist()
             lim = j.find("limit")
             rec["dof"] = len(dofs)
-            dofs.append({"name": j.get("name"), "link": bidx[b], "lower": float(lim.get("lower")),
-                         "upper": float(lim.get("upper")), "effort": 0.5, "velocity": float(lim.get("velocity")),
-                         "kp": 3.0, "kd": 0.1, "armature": 0.001})
+            d = {"name": j.get("name"), "link": bidx[b], "lower": float(lim.get("lower")),
+                 "upper": float(lim.get("upper")), "velocity": float(lim.get("velocity"))}
+            d.update(dof_props(j.get("name")))
+            dofs.append(d)
         mass, mc, Isum = 0.0, np.zeros(3), np.zeros((3, 3))
         parts = []
         for n in links:
@@ -446,10 +447,11 @@ def build_allegro():
                 g = c.find("geometry/mesh")
                 if g is None:
                     continue
-                fn = g.get("filename")     # relative to the URDF's directory or to the asset root
-                path = os.path.join(os.path.dirname(ALLEGRO_URDF), fn)
-                if not os.path.exists(path):
-                    path = os.path.join(base_dir, fn)
+                fn = g.get("filename")
+                for base in (os.path.dirname(urdf), os.path.dirname(os.path.dirname(urdf)), asset_root):
+                    path = os.path.join(base, fn)
+                    if os.path.exists(path):
+                        break
                 v, _ = load_mesh(path, [float(t) for t in g.get("scale", "1 1 1").split()])
                 o, R = parse_origin(c.find("origin"))
                 v = (v @ R.T + o) @ T[:3, :3].T + T[:3, 3]
@@ -459,17 +461,25 @@ def build_allegro():
         for m_, c_, _ in parts:
             mass += m_
             mc += m_ * c_
-        com = mc / mass
+        com = mc / mass if mass > 0 else np.zeros(3)
         for m_, c_, I_ in parts:
             d = c_ - com
             Isum += I_ + m_ * (np.dot(d, d) * np.eye(3) - np.outer(d, d))
         rec.update(mass=float(mass), com=com.tolist(), inertia=Isum.reshape(-1).tolist())
         out_links.append(rec)
+    robot = {"links": out_links, "dofs": dofs, "base_pos": list(base_pos), "base_quat": list(base_quat)}
+    return robot, hulls
+
+
+def build_allegro():
+    """allegro_touch_sensor.urdf loaded like tasks/allegro_hand.py:232-268: fix_base_link,
+    collapse_fixed_joints, disable_gravity, DOF_MODE_POS with stiffness 3, damping 0.1, effort 0.5,
+    armature 0.001 (:264-268)."""
     # hand_start_pose (allegro_hand.py:284-286): p = (0, 0, 0.5), r = Qy(pi) * Qx(0.47 pi) * Qz(0.25 pi)
     q = quat_mul_np(quat_mul_np(quat_axis_angle([0, 1, 0], math.pi), quat_axis_angle([1, 0, 0], 0.47 * math.pi)),
                     quat_axis_angle([0, 0, 1], 0.25 * math.pi))
-    robot = {"links": out_links, "dofs": dofs, "base_pos": [0.0, 0.0, 0.5], "base_quat": q.tolist()}
-    return robot, hulls
+    return build_collapsed(ALLEGRO_URDF, lambda name: {"effort": 0.5, "kp": 3.0, "kd": 0.1, "armature": 0.001},
+                           [0.0, 0.0, 0.5], q.tolist())
 
 
 def build_cube(size=0.065, density=400.0):
@@ -497,6 +507,92 @@ def main_allegro():
           f"dof order={[d['name'] for d in robot['dofs']]} -> {ALLEGRO_OUT}")
 
 
+# ----------------------------------------------------------------------------- AllegroKuka (config C2)
+KUKA_URDF = os.path.join(REF, "assets", "urdf", "kuka_allegro_description", "kuka_allegro_touch_sensor.urdf")
+KUKA_OUT = os.path.join(os.path.dirname(__file__), "..", "isaacgym-hand-arm_amd", "handarm_hip",
+                        "assets", "kuka_allegro_scene.json")
+
+
+def kuka_object_dims():
+    """The procedurally generated cuboid family (allegro_kuka/generate_cuboids.py:37-137) as per-axis
+    scales of the 0.05 m base cube, in the order envs receive them: file names sorted, then shuffled
+    with numpy default_rng(42) (allegro_kuka_base.py:411-428, 485-512). Files of the four generators
+    share one directory, so equal names overwrite each other exactly as on disk."""
+    files = set()
+
+    def gen(scales, min_volume, max_volume, filters):
+        idx = 0
+        for x in scales:
+            for y in scales:
+                for z in scales:
+                    volume = x * y * z / (100 * 100 * 100)
+                    if volume > max_volume or volume < min_volume:
+                        continue
+                    cs = sorted([x, y, z])
+                    if any(f(cs) for f in filters):
+                        continue
+                    files.add(f"{idx:03d}_cube_{x}_{y}_{z}.urdf")
+                    idx += 1
+
+    def thin(s):
+        s = sorted(s)
+        return s[0] * 3 <= s[1]
+
+    def non_elongated(s):
+        s = sorted(s)
+        return s[2] <= s[0] * 3 or s[2] <= s[1] * 3
+    gen([100], 1.0, 1.0, [])                                                          # default cube
+    gen([100, 50, 66, 75, 90, 110, 125, 150, 175, 200, 250, 300], 1.0, 2.5, [])       # withSmallCuboids
+    gen([100, 125, 150, 200, 250, 300, 350], 2.5, 15.0, [thin])                       # withBigCuboids
+    gen([100, 50, 75, 200, 300, 400, 500, 600], 2.5, 6.0, [thin, non_elongated])     # withSticks
+    names = sorted(files)
+    scales = [[float(t) / 100 for t in os.path.splitext(f)[0].split("_")[2:]] for f in names]
+    pairs = list(zip(names, scales))
+    np.random.default_rng(42).shuffle(pairs)
+    return [p[1] for p in pairs]
+
+
+def build_kuka_allegro():
+    """kuka_allegro_touch_sensor.urdf loaded like allegro_kuka_base.py:559-575 (fix_base_link,
+    collapse_fixed_joints, disable_gravity, DOF_MODE_POS), DOF props from populate_dof_properties
+    (allegro_kuka_utils.py:66-83) with AllegroKuka.yaml:56-71: stiffness 40 / damping 5 for all DOFs,
+    effort 300 (arm) / 0.35 (hand), armature 0. Arm pose (0, 0.8, 0), identity (:608-610)."""
+    def props(name):
+        arm = name.startswith("iiwa7_joint")
+        return {"effort": 300.0 if arm else 0.35, "kp": 40.0, "kd": 5.0, "armature": 0.0}
+    return build_collapsed(KUKA_URDF, props, [0.0, 0.8, 0.0], [0.0, 0.0, 0.0, 1.0])
+
+
+def build_box_object(size=0.05, density=400.0):
+    """cube_multicolor_allegro.urdf.template at scale 1: box of objectBaseSize 0.05 m, density 400
+    (the template gives no mass). Per-env dimensions scale this hull and its mass properties."""
+    half = [size / 2] * 3
+    mass = density * size ** 3
+    I = mass / 6.0 * size ** 2
+    return {"name": "cuboid_base", "mass": mass, "com": [0, 0, 0],
+            "inertia": [I, 0, 0, 0, I, 0, 0, 0, I], "hull": box_hull(half)}
+
+
+def main_kuka():
+    robot, link_hulls = build_kuka_allegro()
+    L = len(robot["links"])
+    # table_narrow.urdf: box 0.475 x 0.4 x 0.3 at allegro_pose + (0, -0.8, 0.38) (allegro_kuka_base.py:622-628)
+    table = {"pos": [0.0, 0.0, 0.38], "quat": [0, 0, 0, 1], "half_extents": [0.2375, 0.2, 0.15]}
+    table["hull"] = box_hull(table["half_extents"])
+    scene = {"robot": robot, "link_hulls": link_hulls, "objects": [build_box_object()], "table": table,
+             "objects_per_env": 1, "object_dims": kuka_object_dims(),
+             # actors allegro 0, object 1, table 2, goal 3 (allegro_kuka_base.py:660-730); bodies likewise
+             "layout": {"n_actors": 4, "actor_robot": 0, "actor_object0": 1, "actor_goal": 3, "actor_table": 2,
+                        "n_bodies": L + 3, "body_robot0": 0, "body_object0": L, "body_goal": L + 2,
+                        "body_table": L + 1},
+             "generator": "tools/build_model.py --kuka (reference assets @ /root/reference/assets/urdf)"}
+    with open(KUKA_OUT, "w") as f:
+        json.dump(scene, f, indent=None, separators=(",", ":"))
+    print(f"kuka_allegro: links={L} dofs={len(robot['dofs'])} hulls={len(link_hulls)} "
+          f"objects dims={len(scene['object_dims'])} bodies={[l['name'] for l in robot['links']]} "
+          f"dof order={[d['name'] for d in robot['dofs']]} -> {KUKA_OUT} ({os.path.getsize(KUKA_OUT)} B)")
+
+
 def main():
     robot, link_hulls = build_robot()
     objects = [build_object(n) for n in YCB_POOL
@@ -516,4 +612,6 @@ def main():
 
 
 if __name__ == "__main__":
-    sys.exit(main_allegro() if "--allegro" in sys.argv else main())
+    if "--allegro" in sys.argv:
+        sys.exit(main_allegro())
+    sys.exit(main_kuka() if "--kuka" in sys.argv else main())
