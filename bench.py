@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
-"""bench.py - env-steps/s of the fused HandArm (Ur5SihMultiObjectManipulation) VecTask.step on MI355X.
+"""bench.py - env-steps/s of the fused VecTask.step on MI355X.
 
-Workload (BASELINE.json config 4 per GPU): 8192 envs per GPU = one shard of the 65 536-env HandArmGrasp
-node config, weak scaling (per-GPU work fixed as N grows). A step = one VecTask.step() for every env
-(3 gym.simulate calls x 2 substeps + controllers + observables + reward + done + resets) on synthetic
-i.i.d. U[-1,1] actions (seed 42 + rank). Multi-GPU: one process per GPU (torchrun), envs sharded, the
-only collective is the per-log-interval RCCL all-reduce of episode counters.
+Default workload (BASELINE.json configs[1], the metric's 4096-env point): AllegroKuka ("Arm+Allegro cube
+grasp", regrasping subtask, 23 DOF), 4096 envs per GPU, weak scaling (per-GPU work fixed as N grows). A step =
+one VecTask.step() for every env (pre_physics_step with resets, random object forces and targets, 1 gym.simulate
+call x 2 substeps, refresh, full_state observations, compute_kuka_reward, resets) on synthetic i.i.d. U[-1,1]
+actions (seed 42 + rank). --task ur5sih: config 4 shard (HandArm, 8192 envs/GPU, DR on); --task allegro_hand:
+config 3 (16384 envs). Multi-GPU: one process per GPU (torchrun), envs sharded, the only collective is the
+per-log-interval RCCL all-reduce of episode statistics.
 
 Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 """
@@ -64,6 +66,76 @@ def allegro_bytes_per_env_step(n_links=17, n_dofs=16, num_obs=88, num_act=16):
               "net_contact_force": B * 3 * f, "obs": num_obs * f, "rew": f, "reset_progress_goal": 3 * i64,
               "successes": f, "timeout": 1}
     return sum(reads.values()) + sum(writes.values()), reads, writes
+
+
+def kuka_bytes_per_env_step(n_links=24, n_dofs=23, num_obs=99, num_act=23, ts_read=48, ts_write=32):
+    """B_api of the AllegroKuka step, per env: the state the step must read and the
+    refreshed tensors / observations it must write (the task_state row is counted once each way)."""
+    f, i64 = 4, 8
+    B = n_links + 3
+    reads = {"dof_state": n_dofs * 2 * f, "prev_targets": n_dofs * f, "object_root": 13 * f, "goal_state": 7 * f,
+             "table_goal_rows": 2 * 13 * f, "actions": num_act * f, "reset_progress_goal": 3 * i64,
+             "successes": f, "task_state": ts_read * f, "object_scale": 3 * f, "object_index": i64, "episode": 4}
+    writes = {"dof_state": n_dofs * 2 * f, "dof_force": n_dofs * f, "sim_targets": n_dofs * f,
+              "prev_targets": n_dofs * f, "object_root": 13 * f, "rigid_body_state": B * 13 * f,
+              "net_contact_force": B * 3 * f, "obs": num_obs * f, "rew": f, "reset_progress_goal": 3 * i64,
+              "successes": f, "timeout": 1, "task_state": ts_write * f}
+    return sum(reads.values()) + sum(writes.values()), reads, writes
+
+
+def cpu_baseline_kuka(num_envs=512, min_seconds=12.0, max_steps=4000, seed=0, subtask="regrasping"):
+    """AllegroKuka on the host: C oracle physics (OpenMP over envs) + numpy task oracle (resets with host
+    draws, targets, random forces, observations, reward)."""
+    from oracle import kuka_oracle as KO
+    from oracle.oracle_lib import HostState, Oracle
+    from handarm_hip import model as HM
+    scene = HM.load_scene(HM.KUKA_ASSET)
+    model = HM.build_model(scene)
+    params, cfg = HM.build_params({"subtask": subtask}, task=HM.TASK_ALLEGRO_KUKA)
+    N = num_envs
+    lo, up = np.array(model.dof_lower[:23], np.float32), np.array(model.dof_upper[:23], np.float32)
+    scales, offs = HM.kuka_env_tables(N, scene, cfg)
+    hs = HostState(N, model=model, params=params)
+    hs["object_scale"][:] = scales
+    hs["collision_enabled"][:] = 1
+    st = dict(dof=np.zeros((N, 23, 2), np.float32), root=np.zeros((N, 4, 13), np.float32),
+              goal=np.zeros((N, 7), np.float32), targets=np.zeros((N, 23), np.float32), reset=np.ones(N, np.int64),
+              reset_goal=np.ones(N, np.int64), progress=np.zeros(N, np.int64), successes=np.zeros(N, np.float32),
+              ts=np.zeros((N, HM.AK_TS), np.float32))
+    st["root"][..., 6] = 1.0
+    st["root"][:, 2, 0:3] = list(model.table_pos)
+    st["goal"][:, 6] = 1.0
+    st["ts"][:, HM.AK_KP:HM.AK_KP + 12] = offs.reshape(N, 12)
+    scal = HM.kuka_tolerance_scalars(cfg["success_tolerance"], cfg)
+    orc = Oracle(model, params, N)
+    rng = np.random.default_rng(seed)
+    t0 = time.perf_counter()
+    steps = 0
+    while steps < max_steps and (steps < 2 or time.perf_counter() - t0 < min_seconds):
+        steps += 1
+        dr = rng.random((N, 80), dtype=np.float32)
+        for a_, b_ in ((3, 6), (12, 15), (18, 21), (48, 71)):
+            dr[:, a_:b_] = dr[:, a_:b_] * 2 - 1
+        dr[:, 72:75] = rng.standard_normal((N, 3))
+        a = rng.uniform(-1, 1, (N, 23)).astype(np.float32)
+        KO.pre(params, st, a, dr, lo, up)
+        hs["dof_state"][:] = st["dof"].reshape(-1, 2)
+        hs["root_state"][:] = st["root"].reshape(-1, 13)
+        hs["sim_targets"][:] = st["targets"]
+        hs["object_force"][:] = KO.quat_rotate(st["root"][:, 1, 3:7],
+                                               st["ts"][:, HM.AK_RB_FORCE:HM.AK_RB_FORCE + 3])[:, None]   # LOCAL_SPACE
+        orc.simulate(hs, 1)
+        st["dof"] = hs["dof_state"].reshape(N, 23, 2).copy()
+        st["root"] = hs["root_state"].reshape(N, 4, 13).copy()
+        rb = hs["rigid_body_state"].reshape(N, 27, 13)
+        _, _, st["reset"], st["reset_goal"], st["progress"], st["successes"] = KO.post(
+            params, st["ts"], st["dof"][..., 0], st["dof"][..., 1], rb, st["root"][:, 1], st["goal"],
+            st["progress"] + 1, st["successes"], st["reset"], scales[:, 0], scal, lo, up)
+    dt = time.perf_counter() - t0
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": N * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{N} envs x {steps} env-steps of the AllegroKuka {subtask} step (C oracle physics, "
+                      f"OpenMP {threads} threads, + numpy task oracle), {dt:.1f} s"}
 
 
 def cpu_baseline_allegro(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0):
@@ -161,17 +233,20 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--task", choices=["ur5sih", "allegro_hand"], default="ur5sih",
-                    help="ur5sih: BASELINE config 4 shard (default); allegro_hand: config 3")
-    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (8192 ur5sih, 16384 allegro_hand)")
+    ap.add_argument("--task", choices=["allegro_kuka", "ur5sih", "allegro_hand"], default="allegro_kuka",
+                    help="allegro_kuka: BASELINE config 2 (default); ur5sih: config 4 shard; allegro_hand: config 3")
+    ap.add_argument("--subtask", choices=["regrasping", "reorientation"], default="regrasping")
+    ap.add_argument("--envs", type=int, default=None,
+                    help="envs per GPU (4096 allegro_kuka, 8192 ur5sih, 16384 allegro_hand)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dr", action="store_true", help="ur5sih: domain randomization off")
     ap.add_argument("--cpu-envs", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
     allegro = args.task == "allegro_hand"
+    kuka = args.task == "allegro_kuka"
     if args.envs is None:
-        args.envs = 16384 if allegro else 8192
+        args.envs = {"allegro_kuka": 4096, "ur5sih": 8192, "allegro_hand": 16384}[args.task]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -187,17 +262,28 @@ def main():
     random.seed(seed)
     torch.manual_seed(seed)
 
-    from handarm_hip.tasks import AllegroHand, Ur5SihMultiObjectManipulation
+    from handarm_hip.tasks import AllegroHand, AllegroKuka, Ur5SihMultiObjectManipulation
     from handarm_hip import parallel
-    cls = AllegroHand if allegro else Ur5SihMultiObjectManipulation
-    # config 4 is quoted with domain randomization on (BASELINE.json configs[3]); --no-dr turns it off
-    env = cls({"env": {"numEnvs": args.envs}, "seed": seed, "task": {"randomize": not (allegro or args.no_dr)}},
-              device, device)
+    if kuka:
+        env = AllegroKuka({"env": {"numEnvs": args.envs, "subtask": args.subtask}, "seed": seed}, device, device)
+    else:
+        cls = AllegroHand if allegro else Ur5SihMultiObjectManipulation
+        # config 4 is quoted with domain randomization on (BASELINE.json configs[3]); --no-dr turns it off
+        env = cls({"env": {"numEnvs": args.envs}, "seed": seed, "task": {"randomize": not (allegro or args.no_dr)}},
+                  device, device)
     env.reset()
     gen = torch.Generator(device=device).manual_seed(seed)
     pool = [torch.rand((args.envs, env.num_acts), device=device, generator=gen) * 2 - 1 for _ in range(8)]
+    def log_interval():
+        if kuka:
+            return parallel.reduce_kuka_episode_stats(env)   # RCCL all-reduce, 3 floats (N > 1)
+        if not allegro:
+            parallel.reduce_episode_stats(env)       # RCCL all-reduce of the episode counters (N > 1)
+        return {}
     for k in range(args.warmup):
         env.step(pool[k % len(pool)])
+        if (k + 1) % LOG_INTERVAL == 0 or k == args.warmup - 1:
+            log_interval()                          # lazy initialisation of the logging path stays untimed
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -207,12 +293,14 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
+    host_t = []
     for k in range(args.steps):
         ev[k][0].record()
         env.step(pool[k % len(pool)])
         ev[k][1].record()
-        if (k + 1) % LOG_INTERVAL == 0 and not allegro:
-            parallel.reduce_episode_stats(env)       # RCCL all-reduce of the episode counters (N > 1)
+        host_t.append(time.perf_counter())
+        if (k + 1) % LOG_INTERVAL == 0:
+            log_interval()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -222,17 +310,29 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     step_ms = [a.elapsed_time(b) for a, b in ev]
+    if os.environ.get("BENCH_DEBUG"):
+        gaps = [(b - a) * 1e3 for a, b in zip([t0] + host_t[:-1], host_t)]
+        print("host ms/step issue:", [round(x, 3) for x in gaps], "\ngpu ms/step:", [round(x, 3) for x in step_ms],
+              file=sys.stderr)
     kern_ms = env.sim.kernel_times_ms(args.steps)
-    log = {} if allegro else env.log_data
+    log = {} if (allegro or kuka) else env.log_data
+    kstats = parallel.reduce_kuka_episode_stats(env) if kuka else {}
     if rank == 0:
         total_env_steps = world * args.envs * args.steps
         value = total_env_steps / elapsed
-        bytes_env, _, _ = allegro_bytes_per_env_step() if allegro else algorithmic_bytes_per_env_step(dr=not args.no_dr)
-        kernel = "ah_step_kernel" if allegro else "ha_step_kernel"
+        if kuka:
+            bytes_env, _, _ = kuka_bytes_per_env_step(num_obs=env.num_obs)
+        elif allegro:
+            bytes_env, _, _ = allegro_bytes_per_env_step()
+        else:
+            bytes_env, _, _ = algorithmic_bytes_per_env_step(dr=not args.no_dr)
+        kernel = {"allegro_kuka": "ak_step_kernel", "allegro_hand": "ah_step_kernel", "ur5sih": "ha_step_kernel"}[args.task]
         kavg = statistics.mean(kern_ms) if kern_ms else float("nan")
         achieved = bytes_env * args.envs / (kavg * 1e-3) / 1e9
         traffic = None
-        tf = os.path.join(ROOT, "profiles", "traffic_ah_step_kernel.json" if allegro else "traffic_step_kernel.json")
+        tf = os.path.join(ROOT, "profiles", {"allegro_kuka": "traffic_ak_step_kernel.json",
+                                             "allegro_hand": "traffic_ah_step_kernel.json",
+                                             "ur5sih": "traffic_ha_step_kernel.json"}[args.task])
         if os.path.exists(tf):
             with open(tf) as f:
                 tj = json.load(f)
@@ -240,18 +340,26 @@ def main():
                 traffic = tj.get("hbm_bytes_per_launch")
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = (cpu_baseline_allegro if allegro else cpu_baseline)(args.cpu_envs, args.cpu_seconds)
+            if kuka:
+                cpu = cpu_baseline_kuka(min(args.cpu_envs, 512), args.cpu_seconds, subtask=args.subtask)
+            else:
+                cpu = (cpu_baseline_allegro if allegro else cpu_baseline)(args.cpu_envs, args.cpu_seconds)
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "p50_ms_per_step": statistics.median(step_ms), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32",
-            "data": ("synthetic (seeded U[-1,1] actions, AllegroHand.yaml cube scene)" if allegro else
-                     "synthetic (seeded U[-1,1] actions, YCB scene of Ur5SihMultiObject.yaml, objects dropped at init)"),
-            "config": {"workload": (f"AllegroHand VecTask.step, 2x2 substeps, {args.envs} envs/GPU (BASELINE config 3)"
-                                    if allegro else "HandArm Ur5SihMultiObjectManipulation VecTask.step, 3x2 substeps, "
-                                   f"{args.envs} envs/GPU (BASELINE config 4 shard, DR "
-                                   f"{'off' if args.no_dr else 'on'})"),
+            "data": {"allegro_kuka": "synthetic (seeded U[-1,1] actions, AllegroKuka.yaml procedural cuboid family, "
+                                     "random object forces on)",
+                     "allegro_hand": "synthetic (seeded U[-1,1] actions, AllegroHand.yaml cube scene)",
+                     "ur5sih": "synthetic (seeded U[-1,1] actions, YCB scene of Ur5SihMultiObject.yaml, objects "
+                               "dropped at init)"}[args.task],
+            "config": {"workload": {
+                "allegro_kuka": f"AllegroKuka{args.subtask.capitalize()} VecTask.step, 1x2 substeps, {args.envs} envs/GPU "
+                                "(BASELINE config 2, Arm+Allegro cube grasp)",
+                "allegro_hand": f"AllegroHand VecTask.step, 2x2 substeps, {args.envs} envs/GPU (BASELINE config 3)",
+                "ur5sih": "HandArm Ur5SihMultiObjectManipulation VecTask.step, 3x2 substeps, "
+                          f"{args.envs} envs/GPU (BASELINE config 4 shard, DR {'off' if args.no_dr else 'on'})"}[args.task],
                        "envs_per_gpu": args.envs, "total_envs": world * args.envs, "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -260,6 +368,7 @@ def main():
             "cpu_baseline": cpu,
             "success_rate_ewma": log.get("success_rate_ewma/overall"),
             "consecutive_successes": float(env.consecutive_successes.item()) if allegro else None,
+            "episode_successes_mean": float(kstats["successes"]) if kuka else None,
         }
         print(json.dumps(out))
     if world > 1:

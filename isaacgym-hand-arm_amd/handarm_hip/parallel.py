@@ -34,6 +34,20 @@ def reduce_episode_stats(env):
     env.stat_scale = world()          # EWMA alpha uses the GLOBAL number of envs
 
 
+def reduce_kuka_episode_stats(env):
+    """AllegroKuka: global means of the logged per-env scalars (prev_episode_successes, true_objective) over
+    all ranks' envs. One all-reduce of a 3-float payload (sums and env count) per log interval; returns
+    {"successes": .., "true_objective_mean": ..} as device tensors (no host sync)."""
+    ts = env.task_state
+    from . import model as HM
+    v = torch.full((3,), float(ts.shape[0]), device=ts.device)       # device fill: no host->device copy/sync
+    v[0:2] = ts[:, HM.AK_PREV_SUCC:HM.AK_TRUE_OBJ + 1].sum(0)        # adjacent fields (8, 9): a slice, no index copy
+    if world() > 1:
+        import torch.distributed as dist
+        dist.all_reduce(v)
+    return {"successes": v[0] / v[2], "true_objective_mean": v[1] / v[2]}
+
+
 def fold_counts(stats, terms, num_envs, ewma, obj_ewma, object_names):
     """Host EWMA update from (already reduced) per-step counters; mirrors _update_success_rate and the
     reward-term logging (multi_object_manipulation.py:305-351).
@@ -65,5 +79,5 @@ def fold_counts(stats, terms, num_envs, ewma, obj_ewma, object_names):
     return log, ewma, obj_ewma, total_r, total_s
 
 
-__all__ = ["reduce_episode_stats", "fold_counts", "world"]
+__all__ = ["reduce_episode_stats", "reduce_kuka_episode_stats", "fold_counts", "world"]
 _ = torch
