@@ -172,3 +172,33 @@ def test_kuka_vectask_episode_at_full_size(sub):
     lifted = float(env.lifted_object.mean())
     q = [float(torch.quantile(z, f)) for f in (0.0, 0.01, 0.5, 0.99, 1.0)]
     print(f"kuka {sub} full-size: resets {resets}, lifted {lifted:.3f}, z quantiles 0/1/50/99/100% {q}")
+
+
+def test_apply_rigid_body_force_tensors_local_space():
+    """gym.apply_rigid_body_force_tensors(LOCAL_SPACE) through gym_api: a free cuboid (clear of the scene)
+    gains R(q) F / m dt on top of gravity in one simulate call, and the force is consumed by it."""
+    need_gpu()
+    from handarm_hip.gym_api import acquire_gym, gymapi, gymtorch
+    n = 64
+    gym = acquire_gym()
+    sim = gym.create_sim(n, "cuda:0", task=HM.TASK_ALLEGRO_KUKA)
+    rng = np.random.default_rng(0)
+    root = gymtorch.wrap_tensor(gym.acquire_actor_root_state_tensor(sim)).view(n, 4, 13)
+    q = rng.standard_normal((n, 4)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    root[:, 1, 0:3] = torch.tensor([0.0, -0.6, 1.5], device="cuda:0")
+    root[:, 1, 3:7] = torch.from_numpy(q).cuda()
+    root[:, 1, 7:13] = 0
+    f_local = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+    forces = torch.zeros((n * 27, 3), device="cuda:0")
+    forces.view(n, 27, 3)[:, 24] = torch.from_numpy(f_local).cuda()
+    gym.apply_rigid_body_force_tensors(sim, gymtorch.unwrap_tensor(forces), None, gymapi.LOCAL_SPACE)
+    gym.simulate(sim)
+    v = get(sim, "root_state").reshape(n, 4, 13)[:, 1, 7:10]
+    from scipy.spatial.transform import Rotation
+    f_world = Rotation.from_quat(q).apply(f_local)
+    mass = 400.0 * 0.05 ** 3 * get(sim, "object_scale").reshape(n, 3).prod(-1)
+    dt = sim.params.dt
+    exp = f_world / mass[:, None] * dt + np.array([0.0, 0.0, -9.81]) * dt
+    np.testing.assert_allclose(v, exp, rtol=1e-3, atol=1e-5)
+    assert np.all(get(sim, "object_force") == 0)
