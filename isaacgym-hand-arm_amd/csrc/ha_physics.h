@@ -18,7 +18,7 @@
 
 #define MAXC 21
 #define MAXR (3 * MAXC)
-#define RS 35            /* row stride: D + 6 * n_obj <= 35 */
+#define RS 35            /* max row stride: D + 6 * n_obj <= 35 (Ur5Sih); see row_stride<ND>() */
 #define NOBJ HA_MAX_OBJ
 #define MAXD 24
 #define HA_ND 17         /* DOF count the kernels are compiled for (UR5 + SIH); checked by ha_create */
@@ -80,6 +80,18 @@ struct EnvLDS {
         float xfer[64];     // lane exchange outside the physics phases (controller; PGS impulses -> forces)
     } u;
 };
+
+// Constraint-row stride of a task's kernels: D + 6 x (objects per env). Ur5Sih (17 DOF) has 3 objects and
+// uses the full RS; the one-object tasks (AllegroHand 16, AllegroKuka 23 DOF) pack their rows tighter, which
+// shrinks their LDS footprint (AllegroKuka: 8 workgroups per CU instead of 7).
+template <int ND>
+__host__ __device__ constexpr int row_stride() { return ND == HA_ND ? RS : ND + 6; }
+__host__ __device__ inline size_t task_lds_bytes(int rs) {
+    size_t rows = 2 * (size_t)MAXR * rs * sizeof(float);
+    size_t u = sizeof(PostScratch) > sizeof(ColScratch) ? sizeof(PostScratch) : sizeof(ColScratch);
+    if (rows > u) u = rows;
+    return offsetof(EnvLDS, u) + u;
+}
 
 struct SimCtx {
     const ha_model_t* __restrict__ m;
@@ -781,6 +793,7 @@ HD void tangents(f3 n, f3& t1, f3& t2) {
 
 template <int ND>
 HD void substep(SimCtx& c, float hdt) {
+    constexpr int RSN = row_stride<ND>();
     PROF_BEGIN();
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
@@ -846,15 +859,18 @@ HD void substep(SimCtx& c, float hdt) {
     PROF(3);
     PROF_COUNT(8, s.nc);
     PROF_COUNT(9, 1);
-    // ---- contact rows: lane r owns row r (normal, friction 1, friction 2 of contact r / 3)
+    // ---- contact rows: lane r owns row r (normal, friction 1, friction 2 of contact r / 3). Rows are packed
+    //      with the task's stride (J then Y), so a one-object task needs less LDS (row_stride, task_lds_bytes)
+    float* Jb = s.u.rows.J;
+    float* Yb = Jb + MAXR * RSN;
     int nc = s.nc;
     int nr = 3 * nc;    // nc <= MAXC -> <= MAXR rows
     int r = lane;
     float vt = 0.f, winv = 0.f, lam = 0.f, cmu = 0.f;
     if (r < nr) {
         cmu = s.cmu[r / 3];
-        float* Jr = s.u.rows.J + r * RS;
-        for (int k = 0; k < RS; k++) Jr[k] = 0.0f;
+        float* Jr = Jb + r * RSN;
+        for (int k = 0; k < RSN; k++) Jr[k] = 0.0f;
         int ci = r / 3, k = r % 3;
         f3 n = ld3(s.cn[ci]), t1, t2;
         tangents(n, t1, t2);
@@ -868,7 +884,7 @@ HD void substep(SimCtx& c, float hdt) {
             if (vt > p.max_depen_vel) vt = p.max_depen_vel;
         }
         // Y_r = M^-1 J_r^T (robot block through the explicit inverse, object blocks 1/m, I_w^-1)
-        float* Yr = s.u.rows.Y + r * RS;
+        float* Yr = Yb + r * RSN;
         for (int i = 0; i < D; i++) {
             float acc = 0.0f;
             for (int j = 0; j < D; j++) acc += s.Minv[i * D + j] * Jr[j];
@@ -882,7 +898,7 @@ HD void substep(SimCtx& c, float hdt) {
             f3 a = mv3(s.oIinv[o], mk3(Jo[3], Jo[4], Jo[5]));
             Yo[3] = a.x; Yo[4] = a.y; Yo[5] = a.z;
         }
-        for (int t = NV; t < RS; t++) Yr[t] = 0.0f;
+        for (int t = NV; t < RSN; t++) Yr[t] = 0.0f;
         float a = 0.0f;
         for (int t = 0; t < NV; t++) a += Jr[t] * Yr[t];
         winv = 1.0f / (a + 1e-9f);
@@ -892,14 +908,14 @@ HD void substep(SimCtx& c, float hdt) {
     // friction row 1 holds a10, lane of friction row 2 holds a20 and a21
     float ca0 = 0.f, ca1 = 0.f;
     if (r < nr && r % 3 != 0) {
-        const float* Jr = s.u.rows.J + r * RS;
+        const float* Jr = Jb + r * RSN;
         int r0 = r - r % 3;
-        const float* Y0 = s.u.rows.Y + r0 * RS;
+        const float* Y0 = Yb + r0 * RSN;
         float a = 0.0f;
         for (int t = 0; t < NV; t++) a += Jr[t] * Y0[t];
         ca0 = a;
         if (r % 3 == 2) {
-            const float* Y1 = Y0 + RS;
+            const float* Y1 = Y0 + RSN;
             float b = 0.0f;
             for (int t = 0; t < NV; t++) b += Jr[t] * Y1[t];
             ca1 = b;
@@ -931,8 +947,8 @@ HD void substep(SimCtx& c, float hdt) {
     PROF(5);
     // ---- projected Gauss-Seidel (velocity form): joint rows d = 0..D-1 (drive, lower, upper), then
     //      contact rows r = 0..nr-1.  Same row order and arithmetic as the oracle.
-    const float* J = s.u.rows.J;
-    const float* Y = s.u.rows.Y;
+    const float* J = Jb;
+    const float* Y = Yb;
     for (int it = 0; it < p.solver_iters; it++) {
         for (int d = 0; d < D; d++) {
             float mrow = lane < D ? s.Minv[d * D + lane] : 0.0f;
@@ -970,18 +986,18 @@ HD void substep(SimCtx& c, float hdt) {
         // normal (and first friction) update through the block's Delassus entries, which equals
         // re-reducing J.v after each row (row-by-row Gauss-Seidel) up to rounding
         float j0n = 0.f, j1n = 0.f, j2n = 0.f, y0n = 0.f, y1n = 0.f, y2n = 0.f;
-        if (nc > 0 && lane < RS) {
-            j0n = J[lane]; j1n = J[RS + lane]; j2n = J[2 * RS + lane];
-            y0n = Y[lane]; y1n = Y[RS + lane]; y2n = Y[2 * RS + lane];
+        if (nc > 0 && lane < RSN) {
+            j0n = J[lane]; j1n = J[RSN + lane]; j2n = J[2 * RSN + lane];
+            y0n = Y[lane]; y1n = Y[RSN + lane]; y2n = Y[2 * RSN + lane];
         }
         for (int ci = 0; ci < nc; ci++) {
             int r0 = 3 * ci;
             float j0 = j0n, j1 = j1n, j2 = j2n, y0 = y0n, y1 = y1n, y2 = y2n;
-            if (ci + 1 < nc && lane < RS) {
-                const float* Jn = J + (r0 + 3) * RS;
-                const float* Yn = Y + (r0 + 3) * RS;
-                j0n = Jn[lane]; j1n = Jn[RS + lane]; j2n = Jn[2 * RS + lane];
-                y0n = Yn[lane]; y1n = Yn[RS + lane]; y2n = Yn[2 * RS + lane];
+            if (ci + 1 < nc && lane < RSN) {
+                const float* Jn = J + (r0 + 3) * RSN;
+                const float* Yn = Y + (r0 + 3) * RSN;
+                j0n = Jn[lane]; j1n = Jn[RSN + lane]; j2n = Jn[2 * RSN + lane];
+                y0n = Yn[lane]; y1n = Yn[RSN + lane]; y2n = Yn[2 * RSN + lane];
             }
             float jv0 = j0 * vreg, jv1 = j1 * vreg, jv2 = j2 * vreg;
             wave_sum_rows3(jv0, jv1, jv2);

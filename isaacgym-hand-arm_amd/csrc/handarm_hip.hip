@@ -230,6 +230,7 @@ __device__ void ak_in_from_tensors(SimCtx& c, const ha_state_t& st, int env, AkI
     wsync();
 }
 static_assert(sizeof(AkPost) <= sizeof(PostScratch) - offsetof(PostScratch, in), "AkPost must fit after pd.dyn");
+static_assert(row_stride<HA_ND>() == RS, "Ur5Sih rows use the full stride");
 
 // ----------------------------------------------------------------------------- the kernels
 // One kernel per (task, mode) (one workgroup = one wavefront = one env): each is compiled with only its
@@ -422,7 +423,16 @@ struct ha_handle_s {
         }                                                                             \
     } while (0)
 
-static size_t lds_bytes() { return sizeof(EnvLDS); }
+// dynamic LDS of a task's kernels: the EnvLDS prefix plus the largest phase scratch at the task's row stride
+static size_t lds_bytes(int task) {
+    if (task == HA_TASK_ALLEGRO_KUKA) return task_lds_bytes(row_stride<AK_ND>());
+    if (task == HA_TASK_ALLEGRO_HAND) return task_lds_bytes(row_stride<AH_ND>());
+    return task_lds_bytes(row_stride<HA_ND>());
+}
+static int task_row_stride(int task) {
+    return task == HA_TASK_ALLEGRO_KUKA ? row_stride<AK_ND>()
+                                        : (task == HA_TASK_ALLEGRO_HAND ? row_stride<AH_ND>() : row_stride<HA_ND>());
+}
 
 extern "C" {
 
@@ -453,7 +463,8 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     }
     if (model->n_actors < 1 || model->n_bodies < model->n_links + params->n_objects) return HA_E_MODEL;
     if (model->n_links > HA_MAX_LINKS || params->n_objects > NOBJ ||
-        model->n_dofs + 6 * params->n_objects > RS || model->n_link_hulls + model->n_pool + 1 > HA_MAX_HULLS)
+        model->n_dofs + 6 * params->n_objects > task_row_stride(params->task) ||
+        model->n_link_hulls + model->n_pool + 1 > HA_MAX_HULLS)
         return HA_E_MODEL;
     for (int k = 0; k < model->n_hulls; k++)
         if (model->hull_nverts[k] > 64 || model->hull_nplanes[k] > 128) return HA_E_MODEL;
@@ -474,7 +485,7 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     HIPCHK(hipMemcpy(h->d_params, params, sizeof(ha_params_t), hipMemcpyHostToDevice));
     for (int mode : {MODE_STEP, MODE_SIMULATE, MODE_OBSERVE, MODE_RESET})
         HIPCHK(hipFuncSetAttribute((const void*)kernel_for(h->task, mode), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds_bytes()));
+                                   (int)lds_bytes(h->task)));
     HIPCHK(hipEventCreate(&h->ev0));
     HIPCHK(hipEventCreate(&h->ev1));
     *out = h;
@@ -507,7 +518,7 @@ static int launch(ha_handle h, int mode, int n_calls, uint32_t flags, int slot, 
     hipStream_t s = (hipStream_t)stream;
     bool rec = h->t_ev && h->t_count < h->t_max;
     (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count] : h->ev0, s);
-    hipLaunchKernelGGL(kernel_for(h->task, mode), dim3(h->N), dim3(64), lds_bytes(), s, h->d_model, h->d_params, h->st,
+    hipLaunchKernelGGL(kernel_for(h->task, mode), dim3(h->N), dim3(64), lds_bytes(h->task), s, h->d_model, h->d_params, h->st,
                        h->N, n_calls, flags, slot);
     HIPCHK(hipGetLastError());
     (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count + 1] : h->ev1, s);
