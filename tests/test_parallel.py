@@ -108,3 +108,40 @@ def test_fold_counts_ewma_arithmetic():
     assert obj[0] == pytest.approx(float(a0 * np.float32(0.5) + (1 - a0) * np.float32(0.5)), rel=1e-7)
     assert log["reward_terms/goal"] == pytest.approx(3.0 / 8)
     assert (r, s) == (4, 1)
+
+
+def _kuka_worker(rank, world, port, q):
+    from handarm_hip import model as HM
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(7 + rank)
+        ts = torch.zeros((N_LOCAL + 8 * rank, HM.AK_TS))           # ranks may hold different env counts
+        ts[:, HM.AK_PREV_SUCC] = torch.randint(0, 9, (ts.shape[0],), generator=g).float()
+        ts[:, HM.AK_TRUE_OBJ] = torch.rand(ts.shape[0], generator=g)
+        out = parallel.reduce_kuka_episode_stats(types.SimpleNamespace(task_state=ts))
+        q.put((rank, float(out["successes"]), float(out["true_objective_mean"]), ts.numpy().tolist()))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_kuka_episode_stats_are_global_means():
+    """AllegroKuka: extras["successes"] / true_objective_mean after the all-reduce equal the means over the
+    union of all ranks' envs (what one process over all envs reports)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_kuka_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from handarm_hip import model as HM
+    allts = np.concatenate([np.array(o[3], np.float32) for o in out])
+    for rank, succ, tobj, _ in out:
+        np.testing.assert_allclose(succ, allts[:, HM.AK_PREV_SUCC].mean(), rtol=1e-6)
+        np.testing.assert_allclose(tobj, allts[:, HM.AK_TRUE_OBJ].mean(), rtol=1e-6)

@@ -43,20 +43,25 @@ if __name__ == "__main__":
         print("    hull-hull split: " + "  ".join(f"{nm} {100.0 * buf[25 + i] / tot:5.1f}%" for i, nm in
               enumerate(["setup", "SAT A", "SAT B", "clip", "emit"])), flush=True)
 
-    if "--bench-scene" in sys.argv:
-        # the bench workload: VecTask after drop initialisation, random actions
-        from handarm_hip.tasks import Ur5SihMultiObjectManipulation
-        env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}, "seed": 42}, "cuda:0", "cuda:0")
+    if "--bench-scene" in sys.argv or "--kuka" in sys.argv:
+        # the bench workload: VecTask after its first (reset) steps, random actions
+        from handarm_hip.tasks import AllegroKuka, Ur5SihMultiObjectManipulation
+        if "--kuka" in sys.argv:
+            n = int(args[0]) if args else 4096
+            env = AllegroKuka({"env": {"numEnvs": n}, "seed": 42}, "cuda:0", "cuda:0")
+        else:
+            env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}, "seed": 42}, "cuda:0", "cuda:0")
         env.reset()
+        na = env.num_acts
         g = torch.Generator(device="cuda:0").manual_seed(42)
-        for _ in range(5):
-            env.step(torch.rand((n, 11), device="cuda:0", generator=g) * 2 - 1)
+        for _ in range(20):
+            env.step(torch.rand((n, na), device="cuda:0", generator=g) * 2 - 1)
         torch.cuda.synchronize()
         lib.ha_profile_read(buf, 1)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(10):
-            env.step(torch.rand((n, 11), device="cuda:0", generator=g) * 2 - 1)
+            env.step(torch.rand((n, na), device="cuda:0", generator=g) * 2 - 1)
         e1.record()
         torch.cuda.synchronize()
         print(f"bench scene n={n}: {e0.elapsed_time(e1) / 10:.3f} ms/step (profiled build)", flush=True)
