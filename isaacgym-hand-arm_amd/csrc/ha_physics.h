@@ -81,11 +81,29 @@ struct EnvLDS {
     } u;
 };
 
-// Constraint-row stride of a task's kernels: D + 6 x (objects per env). Ur5Sih (17 DOF) has 3 objects and
-// uses the full RS; the one-object tasks (AllegroHand 16, AllegroKuka 23 DOF) pack their rows tighter, which
-// shrinks their LDS footprint (AllegroKuka: 8 workgroups per CU instead of 7).
+// Compact constraint rows: a contact touches at most two free objects, so a row stores the robot block (D)
+// plus one 6-wide block per object slot (slot 0 = the lower object index, slot 1 = the other), instead of
+// all D + 6 x n_obj coordinates. Ur5Sih (3 objects): stride 17 + 12; one-object tasks (AllegroHand 16,
+// AllegroKuka 23 DOF): D + 6. Dot products over a compact row visit the nonzero terms in the same order as
+// the dense row, so results are unchanged; the LDS saving is what lets these kernels run 8 workgroups per CU.
 template <int ND>
-__host__ __device__ constexpr int row_stride() { return ND == HA_ND ? RS : ND + 6; }
+__host__ __device__ constexpr int row_slots() { return ND == HA_ND ? 2 : 1; }
+template <int ND>
+__host__ __device__ constexpr int row_stride() { return ND + 6 * row_slots<ND>(); }
+// object slots of a contact between bodies a and b (codes: -1 static, 0..NOBJ-1 object, 100+ link)
+HD void contact_slots(int a, int b, int& so0, int& so1) {
+    int oa = (a >= 0 && a < 100) ? a : -1, ob = (b >= 0 && b < 100) ? b : -1;
+    so0 = oa < 0 ? ob : (ob < 0 ? oa : (oa < ob ? oa : ob));
+    so1 = (oa >= 0 && ob >= 0) ? (oa < ob ? ob : oa) : -1;
+}
+// index of generalized coordinate `lane` in a compact row (-1: not touched by the contact)
+HD int compact_index(int lane, int D, int so0, int so1) {
+    if (lane < D) return lane;
+    int t = lane - D;
+    if (so0 >= 0 && t >= 6 * so0 && t < 6 * so0 + 6) return D + t - 6 * so0;
+    if (so1 >= 0 && t >= 6 * so1 && t < 6 * so1 + 6) return D + 6 + t - 6 * so1;
+    return -1;
+}
 __host__ __device__ inline size_t task_lds_bytes(int rs) {
     size_t rows = 2 * (size_t)MAXR * rs * sizeof(float);
     size_t u = sizeof(PostScratch) > sizeof(ColScratch) ? sizeof(PostScratch) : sizeof(ColScratch);
@@ -763,14 +781,15 @@ HD void detect(SimCtx& c) {
 }
 
 // ----------------------------------------------------------------------------- constraint rows
-HD void jac_body(const SimCtx& c, int body, f3 x, f3 dir, float sgn, float* J) {
+// Jacobian of body `body` into the compact row J (object blocks at their slot: so0 -> 0, else 1)
+HD void jac_body(const SimCtx& c, int body, f3 x, f3 dir, float sgn, float* J, int so0) {
     const EnvLDS& s = *c.s;
     int D = c.D;
     if (body < 0) return;
     if (body < 100) {
         f3 r = x - ld3(s.oc[body]);
         f3 ang = cross3(r, dir);
-        float* Jo = J + D + 6 * body;
+        float* Jo = J + D + (body == so0 ? 0 : 6);
         Jo[0] += sgn * dir.x; Jo[1] += sgn * dir.y; Jo[2] += sgn * dir.z;
         Jo[3] += sgn * ang.x; Jo[4] += sgn * ang.y; Jo[5] += sgn * ang.z;
         return;
@@ -876,8 +895,10 @@ HD void substep(SimCtx& c, float hdt) {
         tangents(n, t1, t2);
         f3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
         f3 x = ld3(s.cx[ci]);
-        jac_body(c, s.ca[ci], x, dir, 1.0f, Jr);
-        jac_body(c, s.cb[ci], x, dir, -1.0f, Jr);
+        int so0, so1;
+        contact_slots(s.ca[ci], s.cb[ci], so0, so1);
+        jac_body(c, s.ca[ci], x, dir, 1.0f, Jr, so0);
+        jac_body(c, s.cb[ci], x, dir, -1.0f, Jr, so0);
         if (k == 0) {
             float sp = s.csep[ci];
             vt = sp > 0 ? -sp / hdt : -p.baumgarte * sp / hdt;
@@ -890,17 +911,21 @@ HD void substep(SimCtx& c, float hdt) {
             for (int j = 0; j < D; j++) acc += s.Minv[i * D + j] * Jr[j];
             Yr[i] = acc;
         }
-        for (int o = 0; o < NO; o++) {
-            const float* Jo = Jr + D + 6 * o;
-            float* Yo = Yr + D + 6 * o;
+        for (int sl = 0; sl < row_slots<ND>(); sl++) {
+            int o = sl == 0 ? so0 : so1;
+            const float* Jo = Jr + D + 6 * sl;
+            float* Yo = Yr + D + 6 * sl;
+            if (o < 0) {
+                for (int t = 0; t < 6; t++) Yo[t] = 0.0f;
+                continue;
+            }
             float im = 1.0f / s.om[o];
             Yo[0] = Jo[0] * im; Yo[1] = Jo[1] * im; Yo[2] = Jo[2] * im;
             f3 a = mv3(s.oIinv[o], mk3(Jo[3], Jo[4], Jo[5]));
             Yo[3] = a.x; Yo[4] = a.y; Yo[5] = a.z;
         }
-        for (int t = NV; t < RSN; t++) Yr[t] = 0.0f;
         float a = 0.0f;
-        for (int t = 0; t < NV; t++) a += Jr[t] * Yr[t];
+        for (int t = 0; t < RSN; t++) a += Jr[t] * Yr[t];
         winv = 1.0f / (a + 1e-9f);
     }
     wsync();
@@ -912,12 +937,12 @@ HD void substep(SimCtx& c, float hdt) {
         int r0 = r - r % 3;
         const float* Y0 = Yb + r0 * RSN;
         float a = 0.0f;
-        for (int t = 0; t < NV; t++) a += Jr[t] * Y0[t];
+        for (int t = 0; t < RSN; t++) a += Jr[t] * Y0[t];
         ca0 = a;
         if (r % 3 == 2) {
             const float* Y1 = Y0 + RSN;
             float b = 0.0f;
-            for (int t = 0; t < NV; t++) b += Jr[t] * Y1[t];
+            for (int t = 0; t < RSN; t++) b += Jr[t] * Y1[t];
             ca1 = b;
         }
     }
@@ -985,19 +1010,37 @@ HD void substep(SimCtx& c, float hdt) {
         // contact blocks: the three J.v reductions of a contact run together; the friction rows see the
         // normal (and first friction) update through the block's Delassus entries, which equals
         // re-reducing J.v after each row (row-by-row Gauss-Seidel) up to rounding
+        // lane = generalized coordinate; its entry of a compact row is at compact_index (or absent -> 0)
         float j0n = 0.f, j1n = 0.f, j2n = 0.f, y0n = 0.f, y1n = 0.f, y2n = 0.f;
-        if (nc > 0 && lane < RSN) {
-            j0n = J[lane]; j1n = J[RSN + lane]; j2n = J[2 * RSN + lane];
-            y0n = Y[lane]; y1n = Y[RSN + lane]; y2n = Y[2 * RSN + lane];
+        if (nc > 0) {
+            int ix = lane < RSN ? lane : -1;       // one slot: the compact row is the dense row
+            if constexpr (row_slots<ND>() == 2) {
+                int so0, so1;
+                contact_slots(s.ca[0], s.cb[0], so0, so1);
+                ix = compact_index(lane, D, so0, so1);
+            }
+            if (ix >= 0) {
+                j0n = J[ix]; j1n = J[RSN + ix]; j2n = J[2 * RSN + ix];
+                y0n = Y[ix]; y1n = Y[RSN + ix]; y2n = Y[2 * RSN + ix];
+            }
         }
         for (int ci = 0; ci < nc; ci++) {
             int r0 = 3 * ci;
             float j0 = j0n, j1 = j1n, j2 = j2n, y0 = y0n, y1 = y1n, y2 = y2n;
-            if (ci + 1 < nc && lane < RSN) {
+            if (ci + 1 < nc) {
+                int ix = lane < RSN ? lane : -1;
+                if constexpr (row_slots<ND>() == 2) {
+                    int so0, so1;
+                    contact_slots(s.ca[ci + 1], s.cb[ci + 1], so0, so1);
+                    ix = compact_index(lane, D, so0, so1);
+                }
                 const float* Jn = J + (r0 + 3) * RSN;
                 const float* Yn = Y + (r0 + 3) * RSN;
-                j0n = Jn[lane]; j1n = Jn[RSN + lane]; j2n = Jn[2 * RSN + lane];
-                y0n = Yn[lane]; y1n = Yn[RSN + lane]; y2n = Yn[2 * RSN + lane];
+                j0n = 0.f; j1n = 0.f; j2n = 0.f; y0n = 0.f; y1n = 0.f; y2n = 0.f;
+                if (ix >= 0) {
+                    j0n = Jn[ix]; j1n = Jn[RSN + ix]; j2n = Jn[2 * RSN + ix];
+                    y0n = Yn[ix]; y1n = Yn[RSN + ix]; y2n = Yn[2 * RSN + ix];
+                }
             }
             float jv0 = j0 * vreg, jv1 = j1 * vreg, jv2 = j2 * vreg;
             wave_sum_rows3(jv0, jv1, jv2);
