@@ -94,10 +94,10 @@ HD void ah_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags, bool 
         if (lane < 13) r[lane] = lane < 3 ? pos[lane] : (lane < 7 ? rot[lane - 3] : 0.0f);
         if (lane == 0) {
             qf q = qf{rot[0], rot[1], rot[2], rot[3]};
-            stq(s.oq[0], q);
-            st3(s.oc[0], mk3(pos[0], pos[1], pos[2]) + qrot(q, ld3(m.pool_com[s.pool[0]])));
-            st3(s.ov[0], mk3(0, 0, 0));
-            st3(s.ow[0], mk3(0, 0, 0));
+            stq(c.o[0].oq, q);
+            st3(c.o[0].oc, mk3(pos[0], pos[1], pos[2]) + qrot(q, ld3(m.pool_com[c.o[0].pool])));
+            st3(c.o[0].ov, mk3(0, 0, 0));
+            st3(c.o[0].ow, mk3(0, 0, 0));
         }
         if (lane < D) {
             float lo = m.dof_lower[lane], up = m.dof_upper[lane];

@@ -97,10 +97,10 @@ HD void ak_reset_object_pose(SimCtx& c, const ha_state_t& st, int env, uint32_t 
     if (lane < 13) r[lane] = lane < 3 ? pos[lane] : (lane < 7 ? q[lane - 3] : 0.0f);
     if (lane == 0) {
         qf qq = qf{q[0], q[1], q[2], q[3]};
-        stq(s.oq[0], qq);
-        st3(s.oc[0], mk3(pos[0], pos[1], pos[2]) + qrot(qq, scale3(c, 0, ld3(m.pool_com[s.pool[0]]))));
-        st3(s.ov[0], mk3(0, 0, 0));
-        st3(s.ow[0], mk3(0, 0, 0));
+        stq(c.o[0].oq, qq);
+        st3(c.o[0].oc, mk3(pos[0], pos[1], pos[2]) + qrot(qq, scale3(c, 0, ld3(m.pool_com[c.o[0].pool]))));
+        st3(c.o[0].ov, mk3(0, 0, 0));
+        st3(c.o[0].ow, mk3(0, 0, 0));
     }
     if (lane >= HA_AK_CLOSEST_FT && lane < HA_AK_CLOSEST_FT + 4) tsv = -1.0f;
     if (lane == HA_AK_FURTHEST) tsv = -1.0f;
@@ -231,7 +231,7 @@ HD void ak_forces(SimCtx& c, const ha_state_t& st, int env, uint32_t flags, floa
     }
     if (lane == HA_AK_RNG) tsv = __uint_as_float(ctr + 1u);
     f3 fl = mk3(bcast(tsv, HA_AK_RB_FORCE), bcast(tsv, HA_AK_RB_FORCE + 1), bcast(tsv, HA_AK_RB_FORCE + 2));
-    if (lane == 0) st3(s.ofx[0], qrot(ldq(s.oq[0]), fl));
+    if (lane == 0) st3(c.o[0].ofx, qrot(ldq(c.o[0].oq), fl));
     wsync();
 }
 

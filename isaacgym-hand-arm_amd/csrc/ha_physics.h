@@ -59,6 +59,18 @@ struct PostScratch {
     float dforce[MAXD];                         // joint force of the last substep (drive + limits) / h
 };
 
+// One free object's state (LDS). These live after the EnvLDS block, one per object slot of the task
+// (Ur5Sih 3, bin-picking 7, AllegroHand / AllegroKuka 1), so the object capacity costs only the tasks
+// that use it.
+struct ObjLDS {
+    float oc[4], oq[4], ov[4], ow[4];   // COM position, orientation, linear / angular velocity
+    float oIinv[12];                    // world inverse inertia (3x3, padded)
+    float osc[4];                       // per-env dimension scale of the pool hull; [3] = 1 when scaled
+    float ofx[4];                       // world force on the COM for this physics call (apply_rigid_body_force)
+    float om;                           // mass
+    int pool, coll, pad;                // pool id, collision enabled
+};
+
 struct EnvLDS {
     float q[MAXD], qd[MAXD], tgt[MAXD];
     float lp[HA_MAX_LINKS][3], lq[HA_MAX_LINKS][4];
@@ -66,10 +78,6 @@ struct EnvLDS {
     float Minv[MAXD * MAXD];                    // S ~ M^-1 (factor_inverse), stride D
     float Cb[MAXD];
     float v[RS];
-    float oc[NOBJ][4], oq[NOBJ][4], ov[NOBJ][4], ow[NOBJ][4], oIinv[NOBJ][12], om[NOBJ];
-    int pool[NOBJ], coll[NOBJ];
-    float osc[NOBJ][4];     // per-env object dimension scale of the pool hull; [3] = 1 when scaled
-    float ofx[NOBJ][4];     // world force on the object COM for this physics call (apply_rigid_body_force)
     float cx[MAXC][3], cn[MAXC][3], csep[MAXC], cmu[MAXC];
     int ca[MAXC], cb[MAXC];
     int nc, nr, pad0, pad1;
@@ -104,17 +112,23 @@ HD int compact_index(int lane, int D, int so0, int so1) {
     if (so1 >= 0 && t >= 6 * so1 && t < 6 * so1 + 6) return D + 6 + t - 6 * so1;
     return -1;
 }
-__host__ __device__ inline size_t task_lds_bytes(int rs) {
+// LDS block of one env: EnvLDS up to the phase union, the union at the task's row stride, then the object
+// slots (ObjLDS x capacity), 16-byte aligned
+__host__ __device__ inline size_t obj_lds_offset(int rs) {
     size_t rows = 2 * (size_t)MAXR * rs * sizeof(float);
     size_t u = sizeof(PostScratch) > sizeof(ColScratch) ? sizeof(PostScratch) : sizeof(ColScratch);
     if (rows > u) u = rows;
-    return offsetof(EnvLDS, u) + u;
+    return (offsetof(EnvLDS, u) + u + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t task_lds_bytes(int rs, int obj_capacity) {
+    return obj_lds_offset(rs) + (size_t)obj_capacity * sizeof(ObjLDS);
 }
 
 struct SimCtx {
     const ha_model_t* __restrict__ m;
     const ha_params_t* __restrict__ p;
     EnvLDS* s;
+    ObjLDS* o;              // the env's object slots (after the EnvLDS block, see task_lds_bytes)
     int lane, D, NO, L;
     const float* dr;        // this env's domain-randomization row (HA_DR_*), or null when DR is off
 };
@@ -370,22 +384,22 @@ struct PoseF { f3 p; qf q; };
 // Per-env object dimensions (AllegroKuka's cuboid family): the pool hull of object o is scaled by
 // diag(osc[o]) in its body frame. Unscaled bodies (links, static geometry, objects without a scale) take
 // the unscaled expressions, bit for bit.
-HD bool body_scaled(const SimCtx& c, int b) { return b >= 0 && b < c.NO && c.s->osc[b][3] != 0.0f; }
+HD bool body_scaled(const SimCtx& c, int b) { return b >= 0 && b < c.NO && c.o[b].osc[3] != 0.0f; }
 HD f3 scale3(const SimCtx& c, int b, f3 v) {
     if (!body_scaled(c, b)) return v;
-    const float* sc = c.s->osc[b];
+    const float* sc = c.o[b].osc;
     return mk3(v.x * sc[0], v.y * sc[1], v.z * sc[2]);
 }
 HD float scale_radius(const SimCtx& c, int b, float r) {
     if (!body_scaled(c, b)) return r;
-    const float* sc = c.s->osc[b];
+    const float* sc = c.o[b].osc;
     return r * fmaxf(fmaxf(sc[0], sc[1]), sc[2]);
 }
 
 HD PoseF object_pose(const SimCtx& c, int o) {
     const EnvLDS& s = *c.s;
-    qf q = ldq(s.oq[o]);
-    return PoseF{ld3(s.oc[o]) - qrot(q, scale3(c, o, ld3(c.m->pool_com[s.pool[o]]))), q};
+    qf q = ldq(c.o[o].oq);
+    return PoseF{ld3(c.o[o].oc) - qrot(q, scale3(c, o, ld3(c.m->pool_com[c.o[o].pool]))), q};
 }
 
 // face plane k of a hull in world space; for a scaled body (inv_sc = 1 / scale, read once per hull pair by
@@ -405,7 +419,7 @@ HD void world_plane(const ha_model_t& m, int hull, int k, PoseF P, bool scaled, 
 }
 HD f3 inv_scale(const SimCtx& c, int b) {
     if (!body_scaled(c, b)) return mk3(1, 1, 1);
-    const float* sc = c.s->osc[b];
+    const float* sc = c.o[b].osc;
     return mk3(1.0f / sc[0], 1.0f / sc[1], 1.0f / sc[2]);
 }
 
@@ -701,10 +715,10 @@ HD void detect(SimCtx& c) {
         if (p < npairs && pair_desc(c, p, kind, A, B)) {
             float mg = c.p->contact_margin;
             if (kind <= 3) {
-                cand = s.coll[A] != 0 && (kind != 1 || m.table_hull >= 0);
-                if (kind == 2) cand = cand && s.coll[B] != 0;
+                cand = c.o[A].coll != 0 && (kind != 1 || m.table_hull >= 0);
+                if (kind == 2) cand = cand && c.o[B].coll != 0;
                 if (cand) {
-                    int ho = m.pool_hull[s.pool[A]];
+                    int ho = m.pool_hull[c.o[A].pool];
                     PoseF Po = object_pose(c, A);
                     f3 co = Po.p + qrot(Po.q, scale3(c, A, ld3(m.hull_center[ho])));
                     float ro = scale_radius(c, A, m.hull_radius[ho]);
@@ -714,7 +728,7 @@ HD void detect(SimCtx& c) {
                         int hb;
                         PoseF Pb;
                         if (kind == 1) { hb = m.table_hull; Pb = Ptab; }
-                        else if (kind == 2) { hb = m.pool_hull[s.pool[B]]; Pb = object_pose(c, B); }
+                        else if (kind == 2) { hb = m.pool_hull[c.o[B].pool]; Pb = object_pose(c, B); }
                         else { hb = B; int Lk = m.hull_link[B]; Pb = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; }
                         int bb = kind == 2 ? B : -1;
                         f3 cbb = Pb.p + qrot(Pb.q, scale3(c, bb, ld3(m.hull_center[hb])));
@@ -746,16 +760,16 @@ HD void detect(SimCtx& c) {
             pair_desc(c, q, kind, A, B);
             // one call site per narrow phase (keeps a single inlined copy: code size / VGPRs)
             if (kind == 0) {
-                collide_ground(c, m.pool_hull[s.pool[A]], object_pose(c, A), A);
+                collide_ground(c, m.pool_hull[c.o[A].pool], object_pose(c, A), A);
                 continue;
             }
             int h1, h2, b1, b2;
             PoseF P1, P2;
             if (kind <= 3) {
-                int ho = m.pool_hull[s.pool[A]];
+                int ho = m.pool_hull[c.o[A].pool];
                 PoseF Po = object_pose(c, A);
                 if (kind == 1) { h1 = ho; P1 = Po; b1 = A; h2 = m.table_hull; P2 = Ptab; b2 = -1; }
-                else if (kind == 2) { h1 = ho; P1 = Po; b1 = A; h2 = m.pool_hull[s.pool[B]]; P2 = object_pose(c, B); b2 = B; }
+                else if (kind == 2) { h1 = ho; P1 = Po; b1 = A; h2 = m.pool_hull[c.o[B].pool]; P2 = object_pose(c, B); b2 = B; }
                 else {
                     int Lk = m.hull_link[B];
                     h1 = B; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = ho; P2 = Po; b2 = A;
@@ -787,7 +801,7 @@ HD void jac_body(const SimCtx& c, int body, f3 x, f3 dir, float sgn, float* J, i
     int D = c.D;
     if (body < 0) return;
     if (body < 100) {
-        f3 r = x - ld3(s.oc[body]);
+        f3 r = x - ld3(c.o[body].oc);
         f3 ang = cross3(r, dir);
         float* Jo = J + D + (body == so0 ? 0 : 6);
         Jo[0] += sgn * dir.x; Jo[1] += sgn * dir.y; Jo[2] += sgn * dir.z;
@@ -834,15 +848,15 @@ HD void substep(SimCtx& c, float hdt) {
         int o = lane;
         float damp = 1.0f / (1.0f + hdt * p.object_ang_damping);
         float R[9], Iw[9], Ii[9], Il[9];
-        const float* I0 = m.pool_inertia[s.pool[o]];
+        const float* I0 = m.pool_inertia[c.o[o].pool];
         float sc = c.dr ? c.dr[HA_DR_OBJ_MASS + o] : 1.0f;
-        float mass = m.pool_mass[s.pool[o]];
+        float mass = m.pool_mass[c.o[o].pool];
 #pragma unroll
         for (int k = 0; k < 9; k++) Il[k] = I0[k];
         if (body_scaled(c, o)) {
             // uniform density scaled by S: C = tr(I)/2 Id - I (second moments), C' = det(S) S C S,
             // I' = tr(C') Id - C', m' = det(S) m
-            const float* sv = s.osc[o];
+            const float* sv = c.o[o].osc;
             float det = (sv[0] * sv[1]) * sv[2];
             float h = 0.5f * ((I0[0] + I0[4]) + I0[8]);
             float Cs[9];
@@ -857,18 +871,18 @@ HD void substep(SimCtx& c, float hdt) {
                 for (int j = 0; j < 3; j++) Il[3 * i + j] = (i == j ? tr : 0.0f) - Cs[3 * i + j];
             mass = mass * det;
         }
-        qmat(ldq(s.oq[o]), R);
+        qmat(ldq(c.o[o].oq), R);
         rart3(R, Il, Iw);
 #pragma unroll
         for (int k = 0; k < 9; k++) Iw[k] = Iw[k] * sc;
         inv3(Iw, Ii);
 #pragma unroll
-        for (int k = 0; k < 9; k++) s.oIinv[o][k] = Ii[k];
+        for (int k = 0; k < 9; k++) c.o[o].oIinv[k] = Ii[k];
         mass = mass * sc;
-        s.om[o] = mass;
+        c.o[o].om = mass;
         // external force (zero unless a task applied one): constant over the call's substeps
-        f3 lv = (ld3(s.ov[o]) + ld3(p.gravity) * hdt) + ld3(s.ofx[o]) * (hdt / mass);
-        f3 av = ld3(s.ow[o]) * damp;
+        f3 lv = (ld3(c.o[o].ov) + ld3(p.gravity) * hdt) + ld3(c.o[o].ofx) * (hdt / mass);
+        f3 av = ld3(c.o[o].ow) * damp;
         float* vo = s.v + D + 6 * o;
         vo[0] = lv.x; vo[1] = lv.y; vo[2] = lv.z; vo[3] = av.x; vo[4] = av.y; vo[5] = av.z;
     }
@@ -919,9 +933,9 @@ HD void substep(SimCtx& c, float hdt) {
                 for (int t = 0; t < 6; t++) Yo[t] = 0.0f;
                 continue;
             }
-            float im = 1.0f / s.om[o];
+            float im = 1.0f / c.o[o].om;
             Yo[0] = Jo[0] * im; Yo[1] = Jo[1] * im; Yo[2] = Jo[2] * im;
-            f3 a = mv3(s.oIinv[o], mk3(Jo[3], Jo[4], Jo[5]));
+            f3 a = mv3(c.o[o].oIinv, mk3(Jo[3], Jo[4], Jo[5]));
             Yo[3] = a.x; Yo[4] = a.y; Yo[5] = a.z;
         }
         float a = 0.0f;
@@ -1102,12 +1116,12 @@ HD void substep(SimCtx& c, float hdt) {
         int o = lane;
         const float* vo = s.v + D + 6 * o;
         f3 lv = mk3(vo[0], vo[1], vo[2]), av = mk3(vo[3], vo[4], vo[5]);
-        st3(s.ov[o], lv);
-        st3(s.ow[o], av);
-        st3(s.oc[o], ld3(s.oc[o]) + lv * hdt);
-        qf q = ldq(s.oq[o]);
+        st3(c.o[o].ov, lv);
+        st3(c.o[o].ow, av);
+        st3(c.o[o].oc, ld3(c.o[o].oc) + lv * hdt);
+        qf q = ldq(c.o[o].oq);
         qf dq = qmul(qf{av.x, av.y, av.z, 0.0f}, q);
-        stq(s.oq[o], qnormalize(qf{q.x + 0.5f * hdt * dq.x, q.y + 0.5f * hdt * dq.y, q.z + 0.5f * hdt * dq.z,
+        stq(c.o[o].oq, qnormalize(qf{q.x + 0.5f * hdt * dq.x, q.y + 0.5f * hdt * dq.y, q.z + 0.5f * hdt * dq.z,
                                    q.w + 0.5f * hdt * dq.w}));
     }
     wsync();

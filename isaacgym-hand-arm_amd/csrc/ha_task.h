@@ -182,10 +182,10 @@ HD void task_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags) {
         r[3] = quat0[0]; r[4] = quat0[1]; r[5] = quat0[2]; r[6] = quat0[3];
         for (int k = 7; k < 13; k++) r[k] = 0.0f;
         qf q = ldq(quat0);
-        stq(s.oq[o], q);
-        st3(s.oc[o], ld3(pos0) + qrot(q, ld3(c.m->pool_com[s.pool[o]])));
-        st3(s.ov[o], mk3(0, 0, 0));
-        st3(s.ow[o], mk3(0, 0, 0));
+        stq(c.o[o].oq, q);
+        st3(c.o[o].oc, ld3(pos0) + qrot(q, ld3(c.m->pool_com[c.o[o].pool])));
+        st3(c.o[o].ov, mk3(0, 0, 0));
+        st3(c.o[o].ow, mk3(0, 0, 0));
     } else if (lane >= 8 && lane < 11) {
         int k = lane - 8;
         float noise = 2.0f * (dr[2 + k] - 0.5f);
@@ -256,7 +256,7 @@ HD void post_step(SimCtx& c, const ha_state_t& st, int env, const ObsIn& in, boo
             // see oracle/task_oracle.py observations())
             int o = e < 119 ? (e - 89) / 10 : tgt;
             int k = e < 119 ? (e - 89) % 10 : e - 119;
-            int pid = s.pool[o];
+            int pid = c.o[o].pool;
             const float* cq = cache + o * 7;
             if (k < 3) {
                 float r3[3];
@@ -332,7 +332,7 @@ HD void post_step(SimCtx& c, const ha_state_t& st, int env, const ObsIn& in, boo
         bool before = st.goal_reached_before[env] != 0 || reached;
         st.goal_reached_before[env] = before;
         // device-side log accumulators (the reference does these with .item() host syncs)
-        int pid = s.pool[tgt];
+        int pid = c.o[tgt].pool;
         if (rb != 0) {
             atomicAdd(&st.stats[0], 1);
             atomicAdd(&st.stats[2 + 2 * pid], 1);

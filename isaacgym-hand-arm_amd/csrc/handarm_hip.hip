@@ -15,6 +15,15 @@
 
 enum { MODE_SIMULATE = 0, MODE_STEP = 1, MODE_OBSERVE = 2, MODE_RESET = 3 };
 
+template <int TASK>
+__host__ __device__ constexpr int task_nd() {
+    return TASK == HA_TASK_ALLEGRO_HAND ? AH_ND : (TASK == HA_TASK_ALLEGRO_KUKA ? AK_ND : HA_ND);
+}
+// object slots in LDS per env (objects per env the task's kernels support)
+template <int TASK>
+__host__ __device__ constexpr int task_obj_capacity() { return TASK == HA_TASK_UR5SIH ? 3 : 1; }
+
+
 // ----------------------------------------------------------------------------- state load/store
 // Generic over the env layout in ha_model_t (actor / rigid-body creation order of the task).
 // take_force: consume st.object_force (ha_simulate = gym.simulate after apply_rigid_body_force_tensors)
@@ -32,26 +41,26 @@ __device__ void load_env(SimCtx& c, const ha_state_t& st, int env, bool take_for
         int o = lane;
         const float* r = st.root_state + ((size_t)env * A + m.actor_object0 + o) * 13;
         int pid = (int)st.object_indices[(size_t)env * NO + o];
-        s.pool[o] = pid;
+        c.o[o].pool = pid;
         if (st.object_scale) {
             const float* sc = st.object_scale + ((size_t)env * NO + o) * 3;
-            s.osc[o][0] = sc[0]; s.osc[o][1] = sc[1]; s.osc[o][2] = sc[2]; s.osc[o][3] = 1.0f;
+            c.o[o].osc[0] = sc[0]; c.o[o].osc[1] = sc[1]; c.o[o].osc[2] = sc[2]; c.o[o].osc[3] = 1.0f;
         } else {
-            s.osc[o][0] = s.osc[o][1] = s.osc[o][2] = 1.0f;
-            s.osc[o][3] = 0.0f;
+            c.o[o].osc[0] = c.o[o].osc[1] = c.o[o].osc[2] = 1.0f;
+            c.o[o].osc[3] = 0.0f;
         }
-        s.ofx[o][0] = s.ofx[o][1] = s.ofx[o][2] = s.ofx[o][3] = 0.0f;
+        c.o[o].ofx[0] = c.o[o].ofx[1] = c.o[o].ofx[2] = c.o[o].ofx[3] = 0.0f;
         if (take_force && st.object_force) {
             float* fo = st.object_force + ((size_t)env * NO + o) * 3;
-            s.ofx[o][0] = fo[0]; s.ofx[o][1] = fo[1]; s.ofx[o][2] = fo[2];
+            c.o[o].ofx[0] = fo[0]; c.o[o].ofx[1] = fo[1]; c.o[o].ofx[2] = fo[2];
             fo[0] = fo[1] = fo[2] = 0.0f;
         }
         qf q = ldq(r + 3);
-        stq(s.oq[o], q);
-        st3(s.oc[o], ld3(r) + qrot(q, scale3(c, o, ld3(m.pool_com[pid]))));
-        st3(s.ov[o], ld3(r + 7));
-        st3(s.ow[o], ld3(r + 10));
-        s.coll[o] = st.collision_enabled ? st.collision_enabled[(size_t)env * NO + o] : 1;
+        stq(c.o[o].oq, q);
+        st3(c.o[o].oc, ld3(r) + qrot(q, scale3(c, o, ld3(m.pool_com[pid]))));
+        st3(c.o[o].ov, ld3(r + 7));
+        st3(c.o[o].ow, ld3(r + 10));
+        c.o[o].coll = st.collision_enabled ? st.collision_enabled[(size_t)env * NO + o] : 1;
     }
     for (int b = lane; b < MAXB; b += 64) s.u.pd.cforce[b][0] = s.u.pd.cforce[b][1] = s.u.pd.cforce[b][2] = 0.0f;
     wsync();
@@ -96,12 +105,12 @@ __device__ float link_state(const SimCtx& c, int i, int k) {
 __device__ float object_state(const SimCtx& c, int o, int k) {
     const EnvLDS& s = *c.s;
     if (k < 3) {
-        f3 pos = ld3(s.oc[o]) - qrot(ldq(s.oq[o]), scale3(c, o, ld3(c.m->pool_com[s.pool[o]])));
+        f3 pos = ld3(c.o[o].oc) - qrot(ldq(c.o[o].oq), scale3(c, o, ld3(c.m->pool_com[c.o[o].pool])));
         return k == 0 ? pos.x : (k == 1 ? pos.y : pos.z);
     }
-    if (k < 7) return s.oq[o][k - 3];
-    if (k < 10) return s.ov[o][k - 7];
-    return s.ow[o][k - 10];
+    if (k < 7) return c.o[o].oq[k - 3];
+    if (k < 10) return c.o[o].ov[k - 7];
+    return c.o[o].ow[k - 10];
 }
 
 // writes dof_state, dof_force, sim targets, object root states, rigid_body_state and net_contact_force
@@ -162,7 +171,7 @@ __device__ void snapshot_from_tensors(SimCtx& c, const ha_state_t& st, int env, 
     }
     if (lane < D) in->dofpos[lane] = st.dof_state[((size_t)env * D + lane) * 2];
     for (int e = lane; e < NO * 13; e += 64) in->obj[e / 13][e % 13] = st.root_state[((size_t)env * A + 3) * 13 + e];
-    if (lane < NO) c.s->pool[lane] = (int)st.object_indices[(size_t)env * NO + lane];
+    if (lane < NO) c.o[lane].pool = (int)st.object_indices[(size_t)env * NO + lane];
     wsync();
 }
 
@@ -240,7 +249,7 @@ template <int TASK, int MODE>
 __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params,
                                          const ha_state_t& st, int num_envs, int n_calls, uint32_t flags,
                                          int stat_slot) {
-    constexpr int ND = TASK == HA_TASK_ALLEGRO_HAND ? AH_ND : (TASK == HA_TASK_ALLEGRO_KUKA ? AK_ND : HA_ND);
+    constexpr int ND = task_nd<TASK>();
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int env = blockIdx.x;
     if (env >= num_envs) return;
@@ -248,6 +257,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.m = model;
     c.p = params;
     c.s = reinterpret_cast<EnvLDS*>(smem);
+    c.o = reinterpret_cast<ObjLDS*>(smem + obj_lds_offset(row_stride<ND>()));
     c.lane = threadIdx.x;
     c.D = ND;                     // == model->n_dofs (ha_create); a constant, so loops over D unroll
     c.NO = params->n_objects;
@@ -424,10 +434,17 @@ struct ha_handle_s {
     } while (0)
 
 // dynamic LDS of a task's kernels: the EnvLDS prefix plus the largest phase scratch at the task's row stride
+static int obj_capacity(int task) {
+    return task == HA_TASK_UR5SIH ? task_obj_capacity<HA_TASK_UR5SIH>()
+                                  : (task == HA_TASK_ALLEGRO_HAND ? task_obj_capacity<HA_TASK_ALLEGRO_HAND>()
+                                                                   : task_obj_capacity<HA_TASK_ALLEGRO_KUKA>());
+}
 static size_t lds_bytes(int task) {
-    if (task == HA_TASK_ALLEGRO_KUKA) return task_lds_bytes(row_stride<AK_ND>());
-    if (task == HA_TASK_ALLEGRO_HAND) return task_lds_bytes(row_stride<AH_ND>());
-    return task_lds_bytes(row_stride<HA_ND>());
+    if (task == HA_TASK_ALLEGRO_KUKA)
+        return task_lds_bytes(row_stride<AK_ND>(), task_obj_capacity<HA_TASK_ALLEGRO_KUKA>());
+    if (task == HA_TASK_ALLEGRO_HAND)
+        return task_lds_bytes(row_stride<AH_ND>(), task_obj_capacity<HA_TASK_ALLEGRO_HAND>());
+    return task_lds_bytes(row_stride<HA_ND>(), task_obj_capacity<HA_TASK_UR5SIH>());
 }
 static int task_row_stride(int task) {
     return task == HA_TASK_ALLEGRO_KUKA ? row_stride<AK_ND>()
@@ -462,7 +479,7 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
             if (params->ak_fingertip_links[i] < 0 || params->ak_fingertip_links[i] >= model->n_links) return HA_E_MODEL;
     }
     if (model->n_actors < 1 || model->n_bodies < model->n_links + params->n_objects) return HA_E_MODEL;
-    if (model->n_links > HA_MAX_LINKS || params->n_objects > NOBJ ||
+    if (model->n_links > HA_MAX_LINKS || params->n_objects > obj_capacity(params->task) ||
         model->n_dofs + 6 * (params->n_objects < 2 ? params->n_objects : 2) > task_row_stride(params->task) ||
         model->n_dofs + 6 * params->n_objects > RS ||
         model->n_link_hulls + model->n_pool + 1 > HA_MAX_HULLS)
