@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 3
+#define HA_ABI_VERSION 4
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -44,7 +44,8 @@ extern "C" {
 #define HA_MAX_VERTS 4096
 #define HA_MAX_PLANES 8192
 #define HA_MAX_POOL 32
-#define HA_MAX_OBJ 3           /* objects per env (Ur5SihMultiObject.yaml:2) */
+#define HA_MAX_OBJ 8           /* objects per env: 3 in Ur5SihMultiObject.yaml:2, up to 7 for bin-picking */
+#define HA_MAX_STATIC 10       /* static boxes per env (table, or table-with-hole walls + bin pieces) */
 #define HA_MAX_INIT_POSES 4    /* objects.drop.num_initial_poses */
 #define HA_MAX_SPLINE_PIECES 8
 #define HA_N_SPLINES 8
@@ -53,9 +54,9 @@ extern "C" {
 /* per-env domain-randomization samples (ha_state_t.dr_scale rows) */
 #define HA_DR_LINK_MASS 0      /* [HA_MAX_LINKS] robot link mass (and inertia) scale */
 #define HA_DR_OBJ_MASS 32      /* [HA_MAX_OBJ] object mass (and inertia) scale */
-#define HA_DR_LINK_FRIC 36     /* [HA_MAX_LINKS] robot link friction */
-#define HA_DR_OBJ_FRIC 68      /* [HA_MAX_OBJ] object friction */
-#define HA_DR_SIZE 72
+#define HA_DR_LINK_FRIC 40     /* [HA_MAX_LINKS] robot link friction */
+#define HA_DR_OBJ_FRIC 72      /* [HA_MAX_OBJ] object friction */
+#define HA_DR_SIZE 80
 
 /* tasks (ha_params_t.task) */
 #define HA_TASK_UR5SIH 0        /* Ur5SihMultiObjectManipulation (tasks/hand_arm/task/multi_object_manipulation.py) */
@@ -131,6 +132,12 @@ typedef struct ha_model_t {
     /* v2: env layout of the gym tensors (actor / rigid-body creation order); -1 = absent */
     int32_t n_actors, actor_robot, actor_object0, actor_goal, actor_table;
     int32_t n_bodies, body_robot0, body_object0, body_goal, body_table;
+    /* v4: static boxes, collided with the objects and (link_table_collide) the robot links; static 0 is the
+     * table of table_* when there is one. Pairs are enumerated object by object (ground, statics, objects,
+     * link hulls), then link hull by link hull over the statics. */
+    int32_t n_static;
+    int32_t static_hull[HA_MAX_STATIC];
+    float static_pos[HA_MAX_STATIC][3], static_quat[HA_MAX_STATIC][4], static_half[HA_MAX_STATIC][3];
 } ha_model_t;
 
 /* Simulation + task parameters (Ur5SihBase.yaml, Ur5SihMultiObject*.yaml). */

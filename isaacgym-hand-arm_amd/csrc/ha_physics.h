@@ -22,7 +22,8 @@
 #define NOBJ HA_MAX_OBJ
 #define MAXD 24
 #define HA_ND 17         /* DOF count the kernels are compiled for (UR5 + SIH); checked by ha_create */
-#define MAXB (1 + HA_MAX_LINKS + 1 + NOBJ)
+#define MAXB 48          /* rigid bodies per env (contact-force rows): robot links + objects + statics */
+#define MAXV 64          /* generalized velocity coordinates: D + 6 x objects <= one wavefront */
 
 // What the task observables read after refresh_simulation_tensors(): flange pose, fingertip states,
 // dof positions, object root states (filled from FK in the fused step, or from the state tensors).
@@ -77,7 +78,7 @@ struct EnvLDS {
     float ax[MAXD][3], an[MAXD][3];
     float Minv[MAXD * MAXD];                    // S ~ M^-1 (factor_inverse), stride D
     float Cb[MAXD];
-    float v[RS];
+    float v[MAXV];
     float cx[MAXC][3], cn[MAXC][3], csep[MAXC], cmu[MAXC];
     int ca[MAXC], cb[MAXC];
     int nc, nr, pad0, pad1;
@@ -668,31 +669,34 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
 
 // does a sphere (center c, radius r) reach the table box? Conservative for the hull inside the sphere,
 // so culling with it never removes a contact the narrow phase would produce.
-HD bool sphere_near_table(const ha_model_t& m, PoseF Ptab, f3 c, float r) {
-    qf qi = qf{-Ptab.q.x, -Ptab.q.y, -Ptab.q.z, Ptab.q.w};
-    f3 pl = qrot(qi, c - Ptab.p);
-    float dx = fmaxf(fabsf(pl.x) - m.table_half[0], 0.0f);
-    float dy = fmaxf(fabsf(pl.y) - m.table_half[1], 0.0f);
-    float dz = fmaxf(fabsf(pl.z) - m.table_half[2], 0.0f);
+HD bool sphere_near_box(const float* half, PoseF Pb, f3 c, float r) {
+    qf qi = qf{-Pb.q.x, -Pb.q.y, -Pb.q.z, Pb.q.w};
+    f3 pl = qrot(qi, c - Pb.p);
+    float dx = fmaxf(fabsf(pl.x) - half[0], 0.0f);
+    float dy = fmaxf(fabsf(pl.y) - half[1], 0.0f);
+    float dz = fmaxf(fabsf(pl.z) - half[2], 0.0f);
     return dx * dx + dy * dy + dz * dz <= r * r;
 }
+HD PoseF static_pose(const ha_model_t& m, int k) { return PoseF{ld3(m.static_pos[k]), ldq(m.static_quat[k])}; }
 
 // pair enumeration in the oracle's order (see detect() in physics_oracle.c)
+// pair p -> (kind, A, B): kinds 0 object-ground, 1 object-static B, 2 object-object, 3 link hull B - object,
+// 4 link hull A - static B
 HD bool pair_desc(const SimCtx& c, int p, int& kind, int& A, int& B) {
-    int NO = c.NO, NLH = c.m->n_link_hulls;
+    int NO = c.NO, NLH = c.m->n_link_hulls, NS = c.m->n_static;
     for (int o = 0; o < NO; o++) {
-        int n = 2 + (NO - 1 - o) + NLH;
+        int n = 1 + NS + (NO - 1 - o) + NLH;
         if (p < n) {
             A = o;
             if (p == 0) { kind = 0; B = -1; }
-            else if (p == 1) { kind = 1; B = -1; }
-            else if (p < 2 + (NO - 1 - o)) { kind = 2; B = o + 1 + (p - 2); }
-            else { kind = 3; B = p - 2 - (NO - 1 - o); }
+            else if (p < 1 + NS) { kind = 1; B = p - 1; }
+            else if (p < 1 + NS + (NO - 1 - o)) { kind = 2; B = o + 1 + (p - 1 - NS); }
+            else { kind = 3; B = p - 1 - NS - (NO - 1 - o); }
             return true;
         }
         p -= n;
     }
-    if (p < NLH) { kind = 4; A = p; B = -1; return true; }
+    if (p < NLH * NS) { kind = 4; A = p / NS; B = p - A * NS; return true; }
     return false;
 }
 
@@ -701,11 +705,10 @@ HD void detect(SimCtx& c) {
     const ha_model_t& m = *c.m;
     int lane = c.lane;
     if (lane == 0) s.nc = 0;
-    int NO = c.NO, NLH = m.n_link_hulls;
+    int NO = c.NO, NLH = m.n_link_hulls, NS = m.n_static;
     int npairs = 0;
-    for (int o = 0; o < NO; o++) npairs += 2 + (NO - 1 - o) + NLH;
-    npairs += NLH;
-    PoseF Ptab{ld3(m.table_pos), ldq(m.table_quat)};
+    for (int o = 0; o < NO; o++) npairs += 1 + NS + (NO - 1 - o) + NLH;
+    npairs += NLH * NS;
     wsync();
     for (int base = 0; base < npairs; base += 64) {
         // parallel broad phase: one pair per lane
@@ -715,7 +718,7 @@ HD void detect(SimCtx& c) {
         if (p < npairs && pair_desc(c, p, kind, A, B)) {
             float mg = c.p->contact_margin;
             if (kind <= 3) {
-                cand = c.o[A].coll != 0 && (kind != 1 || m.table_hull >= 0);
+                cand = c.o[A].coll != 0;
                 if (kind == 2) cand = cand && c.o[B].coll != 0;
                 if (cand) {
                     int ho = m.pool_hull[c.o[A].pool];
@@ -727,7 +730,7 @@ HD void detect(SimCtx& c) {
                     } else {
                         int hb;
                         PoseF Pb;
-                        if (kind == 1) { hb = m.table_hull; Pb = Ptab; }
+                        if (kind == 1) { hb = m.static_hull[B]; Pb = static_pose(m, B); }
                         else if (kind == 2) { hb = m.pool_hull[c.o[B].pool]; Pb = object_pose(c, B); }
                         else { hb = B; int Lk = m.hull_link[B]; Pb = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; }
                         int bb = kind == 2 ? B : -1;
@@ -735,20 +738,22 @@ HD void detect(SimCtx& c) {
                         f3 dc = co - cbb;
                         float rr = ro + scale_radius(c, bb, m.hull_radius[hb]) + mg;
                         cand = dot3(dc, dc) <= rr * rr;
-                        if (kind == 1) cand = cand && sphere_near_table(m, Ptab, co, ro + mg);
+                        if (kind == 1) cand = cand && sphere_near_box(m.static_half[B], Pb, co, ro + mg);
                     }
                 }
             } else {
                 int Lk = m.hull_link[A];
-                cand = m.table_hull >= 0 && m.link_table_collide[Lk] != 0;
+                cand = m.link_table_collide[Lk] != 0;
                 if (cand) {
+                    PoseF Pst = static_pose(m, B);
+                    int hs = m.static_hull[B];
                     f3 ch = ld3(s.lp[Lk]) + qrot(ldq(s.lq[Lk]), ld3(m.hull_center[A]));
-                    f3 ct = Ptab.p + qrot(Ptab.q, ld3(m.hull_center[m.table_hull]));
+                    f3 ct = Pst.p + qrot(Pst.q, ld3(m.hull_center[hs]));
                     f3 dc = ch - ct;
-                    float rr = m.hull_radius[A] + m.hull_radius[m.table_hull] + mg;
+                    float rr = m.hull_radius[A] + m.hull_radius[hs] + mg;
                     cand = dot3(dc, dc) <= rr * rr;
-                    // the table's bounding sphere (0.71 m) contains the whole hand: cull on the exact box
-                    cand = cand && sphere_near_table(m, Ptab, ch, m.hull_radius[A] + mg);
+                    // a table's bounding sphere (0.71 m) contains the whole hand: cull on the exact box
+                    cand = cand && sphere_near_box(m.static_half[B], Pst, ch, m.hull_radius[A] + mg);
                 }
             }
         }
@@ -768,7 +773,7 @@ HD void detect(SimCtx& c) {
             if (kind <= 3) {
                 int ho = m.pool_hull[c.o[A].pool];
                 PoseF Po = object_pose(c, A);
-                if (kind == 1) { h1 = ho; P1 = Po; b1 = A; h2 = m.table_hull; P2 = Ptab; b2 = -1; }
+                if (kind == 1) { h1 = ho; P1 = Po; b1 = A; h2 = m.static_hull[B]; P2 = static_pose(m, B); b2 = -1; }
                 else if (kind == 2) { h1 = ho; P1 = Po; b1 = A; h2 = m.pool_hull[c.o[B].pool]; P2 = object_pose(c, B); b2 = B; }
                 else {
                     int Lk = m.hull_link[B];
@@ -776,7 +781,8 @@ HD void detect(SimCtx& c) {
                 }
             } else {
                 int Lk = m.hull_link[A];
-                h1 = A; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = m.table_hull; P2 = Ptab; b2 = -1;
+                h1 = A; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = m.static_hull[B];
+                P2 = static_pose(m, B); b2 = -1;
             }
 #ifdef HA_PROFILE
             unsigned long long _k0 = __builtin_amdgcn_s_memtime();

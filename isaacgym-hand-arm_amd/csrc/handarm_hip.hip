@@ -239,7 +239,7 @@ __device__ void ak_in_from_tensors(SimCtx& c, const ha_state_t& st, int env, AkI
     wsync();
 }
 static_assert(sizeof(AkPost) <= sizeof(PostScratch) - offsetof(PostScratch, in), "AkPost must fit after pd.dyn");
-static_assert(HA_ND + 6 * HA_MAX_OBJ <= RS, "the generalized velocity must fit EnvLDS::v");
+static_assert(HA_ND + 6 * 7 <= MAXV, "bin-picking (7 objects) must fit the generalized velocity in one wavefront");
 
 // ----------------------------------------------------------------------------- the kernels
 // One kernel per (task, mode) (one workgroup = one wavefront = one env): each is compiled with only its
@@ -481,7 +481,8 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     if (model->n_actors < 1 || model->n_bodies < model->n_links + params->n_objects) return HA_E_MODEL;
     if (model->n_links > HA_MAX_LINKS || params->n_objects > obj_capacity(params->task) ||
         model->n_dofs + 6 * (params->n_objects < 2 ? params->n_objects : 2) > task_row_stride(params->task) ||
-        model->n_dofs + 6 * params->n_objects > RS ||
+        model->n_dofs + 6 * params->n_objects > MAXV || model->n_bodies > MAXB ||
+        model->n_static < 0 || model->n_static > HA_MAX_STATIC ||
         model->n_link_hulls + model->n_pool + 1 > HA_MAX_HULLS)
         return HA_E_MODEL;
     for (int k = 0; k < model->n_hulls; k++)

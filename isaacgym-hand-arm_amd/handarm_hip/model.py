@@ -21,12 +21,13 @@ ALLEGRO_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets
 KUKA_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "kuka_allegro_scene.json")
 
 MAX_LINKS, MAX_DOFS, MAX_HULLS, MAX_VERTS, MAX_PLANES = 32, 24, 64, 4096, 8192
-MAX_POOL, MAX_OBJ, MAX_INIT_POSES, MAX_SPLINE_PIECES, N_SPLINES = 32, 3, 4, 8, 8
+MAX_POOL, MAX_OBJ, MAX_INIT_POSES, MAX_SPLINE_PIECES, N_SPLINES = 32, 8, 4, 8, 8
+MAX_STATIC = 10
 MAX_MPAIRS = 192
 STAT_SIZE = 2 + 2 * MAX_POOL
 DRAW_STRIDE = 80
-DR_SIZE = 72
-DR_LINK_MASS, DR_OBJ_MASS, DR_LINK_FRIC, DR_OBJ_FRIC = 0, 32, 36, 68
+DR_SIZE = 80
+DR_LINK_MASS, DR_OBJ_MASS, DR_LINK_FRIC, DR_OBJ_FRIC = 0, 32, 40, 72
 TASK_UR5SIH, TASK_ALLEGRO_HAND, TASK_ALLEGRO_KUKA = 0, 1, 2
 # AllegroKuka task_state row (HA_AK_* in handarm_abi.h)
 AK_TS = 48
@@ -75,6 +76,8 @@ class HaModel(C.Structure):
         ("dof_armature", arr(f32, MAX_DOFS)),
         ("n_actors", i32), ("actor_robot", i32), ("actor_object0", i32), ("actor_goal", i32), ("actor_table", i32),
         ("n_bodies", i32), ("body_robot0", i32), ("body_object0", i32), ("body_goal", i32), ("body_table", i32),
+        ("n_static", i32), ("static_hull", arr(i32, MAX_STATIC)), ("static_pos", arr(f32, MAX_STATIC, 3)),
+        ("static_quat", arr(f32, MAX_STATIC, 4)), ("static_half", arr(f32, MAX_STATIC, 3)),
     ]
 
 
@@ -201,8 +204,11 @@ def build_model(scene, pool_names=None):
         byname = {o["name"]: o for o in objects}
         objects = [byname[n] for n in pool_names]
     table = scene.get("table")
+    # static boxes: the table (static 0) and any extra pieces (table-with-hole walls, bin parts)
+    statics = ([table] if table else []) + list(scene.get("statics", []))
+    assert len(statics) <= MAX_STATIC
     hulls = [(h, h["index"]) for h in scene["link_hulls"]] + [(o["hull"], -1) for o in objects] + \
-            ([(table["hull"], -1)] if table else [])
+            [(st["hull"], -1) for st in statics]
     assert len(hulls) <= MAX_HULLS
     vs, ps = 0, 0
     verts = np.ctypeslib.as_array(m.verts)
@@ -232,8 +238,15 @@ def build_model(scene, pool_names=None):
         m.pool_bbox_pos[i][:] = o.get("bbox_from_origin_pos", (0, 0, 0))
         m.pool_bbox_quat[i][:] = o.get("bbox_from_origin_quat", (0, 0, 0, 1))
         m.pool_bbox_ext[i][:] = o.get("bbox_extents", (0, 0, 0))
+    first_static = len(hulls) - len(statics)
+    m.n_static = len(statics)
+    for k, st in enumerate(statics):
+        m.static_hull[k] = first_static + k
+        m.static_pos[k][:] = st["pos"]
+        m.static_quat[k][:] = st["quat"]
+        m.static_half[k][:] = st["half_extents"]
     if table:
-        m.table_hull = len(hulls) - 1
+        m.table_hull = first_static
         m.table_pos[:] = table["pos"]
         m.table_quat[:] = table["quat"]
         m.table_half[:] = table["half_extents"]

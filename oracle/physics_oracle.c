@@ -468,30 +468,34 @@ static void collide_ground(const ha_model_t* m, int ha, pose_t PA, float margin,
 }
 
 /* sphere (center c, radius r) vs the table box: exact sphere-box overlap test (broad phase) */
-static int near_table(const ha_model_t* m, pose_t Ptab, v3 c, float r) {
-    qt qi = Q(-Ptab.q.x, -Ptab.q.y, -Ptab.q.z, Ptab.q.w);
-    v3 pl = qrot(qi, sub(c, Ptab.p));
-    float dx = fmaxf(fabsf(pl.x) - m->table_half[0], 0.0f);
-    float dy = fmaxf(fabsf(pl.y) - m->table_half[1], 0.0f);
-    float dz = fmaxf(fabsf(pl.z) - m->table_half[2], 0.0f);
+/* sphere (center c, radius r) vs static box k: exact sphere-box overlap test (broad phase) */
+static int near_box(const float* half, pose_t Pb, v3 c, float r) {
+    qt qi = Q(-Pb.q.x, -Pb.q.y, -Pb.q.z, Pb.q.w);
+    v3 pl = qrot(qi, sub(c, Pb.p));
+    float dx = fmaxf(fabsf(pl.x) - half[0], 0.0f);
+    float dy = fmaxf(fabsf(pl.y) - half[1], 0.0f);
+    float dz = fmaxf(fabsf(pl.z) - half[2], 0.0f);
     return dx * dx + dy * dy + dz * dz <= r * r;
 }
+static pose_t static_pose(const ha_model_t* m, int k) { pose_t P = {ld3(m->static_pos[k]), ldq(m->static_quat[k])}; return P; }
 
 static int detect(const hao_handle h, const env_t* e, contact_t* out) {
     const ha_model_t* m = &h->m;
     const ha_params_t* p = &h->p;
     int nout = 0;
     float mg = p->contact_margin;
-    pose_t Ptab = {ld3(m->table_pos), ldq(m->table_quat)};
     for (int o = 0; o < h->NO; o++) {
         if (!e->coll[o]) continue;
         int ho = m->pool_hull[e->pool[o]];
         const float* so = env_scale(e, o);
         pose_t Po = {sub(e->oc[o], qrot(e->oq[o], scl(so, ld3(m->pool_com[e->pool[o]])))), e->oq[o]};
         collide_ground(m, ho, Po, mg, o, so, out, &nout, MAXC);
-        if (m->table_hull >= 0 &&
-            near_table(m, Ptab, add(Po.p, qrot(Po.q, scl(so, ld3(m->hull_center[ho])))), scl_r(so, m->hull_radius[ho]) + mg))
-            collide_hulls(m, ho, Po, m->table_hull, Ptab, mg, o, -1, so, NULL, out, &nout, MAXC);
+        for (int st = 0; st < m->n_static; st++) {
+            pose_t Pst = static_pose(m, st);
+            if (near_box(m->static_half[st], Pst, add(Po.p, qrot(Po.q, scl(so, ld3(m->hull_center[ho])))),
+                         scl_r(so, m->hull_radius[ho]) + mg))
+                collide_hulls(m, ho, Po, m->static_hull[st], Pst, mg, o, -1, so, NULL, out, &nout, MAXC);
+        }
         for (int o2 = o + 1; o2 < h->NO; o2++) {
             if (!e->coll[o2]) continue;
             int h2 = m->pool_hull[e->pool[o2]];
@@ -507,10 +511,13 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
     }
     for (int k = 0; k < m->n_link_hulls; k++) {
         int L = m->hull_link[k];
-        if (m->table_hull < 0 || !m->link_table_collide[L]) continue;
+        if (!m->link_table_collide[L]) continue;
         pose_t PL = {e->lp[L], e->lq[L]};
-        if (near_table(m, Ptab, add(PL.p, qrot(PL.q, ld3(m->hull_center[k]))), m->hull_radius[k] + mg))
-            collide_hulls(m, k, PL, m->table_hull, Ptab, mg, 100 + L, -1, NULL, NULL, out, &nout, MAXC);
+        for (int st = 0; st < m->n_static; st++) {
+            pose_t Pst = static_pose(m, st);
+            if (near_box(m->static_half[st], Pst, add(PL.p, qrot(PL.q, ld3(m->hull_center[k]))), m->hull_radius[k] + mg))
+                collide_hulls(m, k, PL, m->static_hull[st], Pst, mg, 100 + L, -1, NULL, NULL, out, &nout, MAXC);
+        }
     }
     return nout;
 }
