@@ -6,7 +6,8 @@ grasp", regrasping subtask, 23 DOF), 4096 envs per GPU, weak scaling (per-GPU wo
 one VecTask.step() for every env (pre_physics_step with resets, random object forces and targets, 1 gym.simulate
 call x 2 substeps, refresh, full_state observations, compute_kuka_reward, resets) on synthetic i.i.d. U[-1,1]
 actions (seed 42 + rank). --task ur5sih: config 4 shard (HandArm, 8192 envs/GPU, DR on); --task allegro_hand:
-config 3 (16384 envs). Multi-GPU: one process per GPU (torchrun), envs sharded, the only collective is the
+config 3 (16384 envs); --task binpick: config 5 shard (HandArm bin-picking: hard_bin tote, 8 objects per env,
+8192 envs/GPU). Multi-GPU: one process per GPU (torchrun), envs sharded, the only collective is the
 per-log-interval RCCL all-reduce of episode statistics.
 
 Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
@@ -32,11 +33,13 @@ HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 LOG_INTERVAL = 16                # rl_games horizon_length (train/Ur5SihMultiObjectManipulationPPO.yaml:65)
 
 
-def algorithmic_bytes_per_env_step(n_links=29, n_dofs=17, n_obj=3, num_obs=147, num_act=11, P=1, dr=False):
+def algorithmic_bytes_per_env_step(n_links=29, n_dofs=17, n_obj=3, num_obs=147, num_act=11, P=1, dr=False,
+                                   n_static_bodies=1):
     """HBM bytes one env-step of the fused kernel must move (state in + state/obs out), per env.
-    B_api of SURVEY.md §8(d): the reference surface materialises body states and contact forces."""
+    B_api of SURVEY.md §8(d): the reference surface materialises body states and contact forces.
+    Bin-picking: 8 objects, 6 static bodies (table-with-hole links, bin), obs 212."""
     f, i64 = 4, 8
-    B = 1 + n_links + 1 + n_obj
+    B = 1 + n_links + n_static_bodies + n_obj
     reads = {
         "dof_state": n_dofs * 2 * f, "sim_targets": n_dofs * f, "object_root_states": n_obj * 13 * f,
         "goal_and_table_rows": 2 * 13 * f, "object_indices": n_obj * i64, "collision_enabled": n_obj,
@@ -187,7 +190,7 @@ def cpu_baseline_allegro(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0
                       f"OpenMP {threads} threads, + numpy task oracle), {dt:.1f} s"}
 
 
-def cpu_baseline(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0):
+def cpu_baseline(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0, binpick=False):
     """The C oracle (scalar restatement, OpenMP over envs) + numpy task oracle, timed on host cores.
 
     Bounded sample: env-steps of the full batch are repeated until ``min_seconds`` of wall time have
@@ -196,17 +199,23 @@ def cpu_baseline(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0):
     from oracle.oracle_lib import HostState, Oracle
     from handarm_hip import model as HM
     from tests import scenes
-    model = HM.build_model(HM.load_scene())
-    params, _ = HM.build_params()
+    scene = HM.load_scene(HM.BIN_ASSET if binpick else HM.ASSET)
+    model = HM.build_model(scene)
+    params, _ = HM.build_params({"n_objects": 8} if binpick else None)
     orc = Oracle(model, params, num_envs)
-    st = HostState(num_envs)
-    scenes.fill_scene(st, num_envs, seed=seed)
+    st = HostState(num_envs, model=model, params=params)
+    if binpick:
+        scenes.fill_bin_scene(st, num_envs, scene, seed=seed)
+    else:
+        scenes.fill_scene(st, num_envs, seed=seed)
+    A, B, no, a0 = model.n_actors, model.n_bodies, params.n_objects, model.actor_object0
+    actors = list(range(a0, a0 + no))
     rng = np.random.default_rng(seed)
     st["ur5_target"][:] = st["dof_state"].reshape(num_envs, 17, 2)[:, 0:6, 0]
     bbox_p = np.array([[model.pool_bbox_pos[i][:] for i in r] for r in st["object_indices"]], np.float32)
     bbox_q = np.array([[model.pool_bbox_quat[i][:] for i in r] for r in st["object_indices"]], np.float32)
     bbox_e = np.array([[model.pool_bbox_ext[i][:] for i in r] for r in st["object_indices"]], np.float32)
-    prev = st["root_state"].reshape(num_envs, 6, 13)[:, 3:, 0:7].copy()
+    prev = st["root_state"].reshape(num_envs, A, 13)[:, a0:a0 + no, 0:7].copy()
     t0 = time.perf_counter()
     steps = 0
     while steps < max_steps and (steps < 2 or time.perf_counter() - t0 < min_seconds):
@@ -214,17 +223,18 @@ def cpu_baseline(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0):
         st["actions"][:] = rng.uniform(-1, 1, (num_envs, 11))
         orc.controller(st)
         orc.simulate(st, 3)
-        root = st["root_state"].reshape(num_envs, 6, 13)
-        body = st["rigid_body_state"].reshape(num_envs, 34, 13)
+        root = st["root_state"].reshape(num_envs, A, 13)
+        body = st["rigid_body_state"].reshape(num_envs, B, 13)
         O.observations(root, body, st["dof_state"].reshape(num_envs, 17, 2), st["dof_position_targets"],
-                       st["goal_pos"], st["target_object_index"], bbox_p, bbox_q, bbox_e, prev)
+                       st["goal_pos"], st["target_object_index"], bbox_p, bbox_q, bbox_e, prev, object_actors=actors)
         O.reward(root, body, st["goal_pos"], st["target_object_index"], st["object_configuration_indices"],
-                 st["object_pos_initial"].reshape(num_envs, 1, 3, 3))
-        prev = root[:, 3:, 0:7].copy()
+                 st["object_pos_initial"].reshape(num_envs, 1, no, 3), object_actors=actors)
+        prev = root[:, a0:a0 + no, 0:7].copy()
     dt = time.perf_counter() - t0
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return {"value": num_envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{num_envs} envs x {steps} env-steps of the same HandArm step (C oracle physics, "
+            "sample": f"{num_envs} envs x {steps} env-steps of the same HandArm{' bin-picking' if binpick else ''} step "
+                      f"(C oracle physics, "
                       f"OpenMP {threads} threads, + numpy task oracle), {dt:.1f} s"}
 
 
@@ -233,11 +243,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--task", choices=["allegro_kuka", "ur5sih", "allegro_hand"], default="allegro_kuka",
-                    help="allegro_kuka: BASELINE config 2 (default); ur5sih: config 4 shard; allegro_hand: config 3")
+    ap.add_argument("--task", choices=["allegro_kuka", "ur5sih", "allegro_hand", "binpick"], default="allegro_kuka",
+                    help="allegro_kuka: BASELINE config 2 (default); ur5sih: config 4 shard; allegro_hand: config 3; "
+                         "binpick: config 5 shard")
     ap.add_argument("--subtask", choices=["regrasping", "reorientation"], default="regrasping")
     ap.add_argument("--envs", type=int, default=None,
-                    help="envs per GPU (4096 allegro_kuka, 8192 ur5sih, 16384 allegro_hand)")
+                    help="envs per GPU (4096 allegro_kuka, 8192 ur5sih, 16384 allegro_hand, 8192 binpick)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dr", action="store_true", help="ur5sih: domain randomization off")
     ap.add_argument("--cpu-envs", type=int, default=1024)
@@ -245,8 +256,9 @@ def main():
     args = ap.parse_args()
     allegro = args.task == "allegro_hand"
     kuka = args.task == "allegro_kuka"
+    binpick = args.task == "binpick"
     if args.envs is None:
-        args.envs = {"allegro_kuka": 4096, "ur5sih": 8192, "allegro_hand": 16384}[args.task]
+        args.envs = {"allegro_kuka": 4096, "ur5sih": 8192, "allegro_hand": 16384, "binpick": 8192}[args.task]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -266,6 +278,12 @@ def main():
     from handarm_hip import parallel
     if kuka:
         env = AllegroKuka({"env": {"numEnvs": args.envs, "subtask": args.subtask}, "seed": seed}, device, device)
+    elif binpick:
+        # config 5: Ur5SihMultiObject with bin.asset hard_bin and 8 objects from the YCB pool
+        from handarm_hip import model as HM
+        pool = [o["name"] for o in HM.load_scene()["objects"]]
+        env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": args.envs}, "seed": seed, "bin": {"asset": "hard_bin"},
+                                             "objects": {"num_objects": 8, "dataset": {"ycb": pool}}}, device, device)
     else:
         cls = AllegroHand if allegro else Ur5SihMultiObjectManipulation
         # config 4 is quoted with domain randomization on (BASELINE.json configs[3]); --no-dr turns it off
@@ -324,15 +342,19 @@ def main():
             bytes_env, _, _ = kuka_bytes_per_env_step(num_obs=env.num_obs)
         elif allegro:
             bytes_env, _, _ = allegro_bytes_per_env_step()
+        elif binpick:
+            bytes_env, _, _ = algorithmic_bytes_per_env_step(n_obj=8, num_obs=env.num_obs, n_static_bodies=6)
         else:
             bytes_env, _, _ = algorithmic_bytes_per_env_step(dr=not args.no_dr)
-        kernel = {"allegro_kuka": "ak_step_kernel", "allegro_hand": "ah_step_kernel", "ur5sih": "ha_step_kernel"}[args.task]
+        kernel = {"allegro_kuka": "ak_step_kernel", "allegro_hand": "ah_step_kernel", "ur5sih": "ha_step_kernel",
+                  "binpick": "hb_step_kernel"}[args.task]
         kavg = statistics.mean(kern_ms) if kern_ms else float("nan")
         achieved = bytes_env * args.envs / (kavg * 1e-3) / 1e9
         traffic = None
         tf = os.path.join(ROOT, "profiles", {"allegro_kuka": "traffic_ak_step_kernel.json",
                                              "allegro_hand": "traffic_ah_step_kernel.json",
-                                             "ur5sih": "traffic_ha_step_kernel.json"}[args.task])
+                                             "ur5sih": "traffic_ha_step_kernel.json",
+                                             "binpick": "traffic_hb_step_kernel.json"}[args.task])
         if os.path.exists(tf):
             with open(tf) as f:
                 tj = json.load(f)
@@ -342,8 +364,10 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             if kuka:
                 cpu = cpu_baseline_kuka(min(args.cpu_envs, 512), args.cpu_seconds, subtask=args.subtask)
+            elif allegro:
+                cpu = cpu_baseline_allegro(args.cpu_envs, args.cpu_seconds)
             else:
-                cpu = (cpu_baseline_allegro if allegro else cpu_baseline)(args.cpu_envs, args.cpu_seconds)
+                cpu = cpu_baseline(args.cpu_envs, args.cpu_seconds, binpick=binpick)
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
@@ -353,13 +377,17 @@ def main():
                                      "random object forces on)",
                      "allegro_hand": "synthetic (seeded U[-1,1] actions, AllegroHand.yaml cube scene)",
                      "ur5sih": "synthetic (seeded U[-1,1] actions, YCB scene of Ur5SihMultiObject.yaml, objects "
-                               "dropped at init)"}[args.task],
+                               "dropped at init)",
+                     "binpick": "synthetic (seeded U[-1,1] actions, hard_bin tote + 8 YCB objects per env from the "
+                                "16-object pool, dropped into the bin at init)"}[args.task],
             "config": {"workload": {
                 "allegro_kuka": f"AllegroKuka{args.subtask.capitalize()} VecTask.step, 1x2 substeps, {args.envs} envs/GPU "
                                 "(BASELINE config 2, Arm+Allegro cube grasp)",
                 "allegro_hand": f"AllegroHand VecTask.step, 2x2 substeps, {args.envs} envs/GPU (BASELINE config 3)",
                 "ur5sih": "HandArm Ur5SihMultiObjectManipulation VecTask.step, 3x2 substeps, "
-                          f"{args.envs} envs/GPU (BASELINE config 4 shard, DR {'off' if args.no_dr else 'on'})"}[args.task],
+                          f"{args.envs} envs/GPU (BASELINE config 4 shard, DR {'off' if args.no_dr else 'on'})",
+                "binpick": "HandArm bin-picking Ur5SihMultiObjectManipulation VecTask.step, 3x2 substeps, 8 objects, "
+                           f"{args.envs} envs/GPU (BASELINE config 5 shard)"}[args.task],
                        "envs_per_gpu": args.envs, "total_envs": world * args.envs, "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

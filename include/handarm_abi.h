@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 4
+#define HA_ABI_VERSION 5
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -44,8 +44,10 @@ extern "C" {
 #define HA_MAX_VERTS 4096
 #define HA_MAX_PLANES 8192
 #define HA_MAX_POOL 32
-#define HA_MAX_OBJ 8           /* objects per env: 3 in Ur5SihMultiObject.yaml:2, up to 7 for bin-picking */
+#define HA_MAX_OBJ 8           /* objects per env: 3 in Ur5SihMultiObject.yaml:2, 8 for bin-picking (config 5) */
 #define HA_MAX_STATIC 10       /* static boxes per env (table, or table-with-hole walls + bin pieces) */
+#define HA_MAX_FIXED_BODIES 8  /* fixed rigid bodies with a model pose (table-with-hole links, bin) */
+#define HA_MAX_CONTACTS 42     /* contacts per env and substep: 21 (<= 3 objects), 42 (clutter, > 3 objects) */
 #define HA_MAX_INIT_POSES 4    /* objects.drop.num_initial_poses */
 #define HA_MAX_SPLINE_PIECES 8
 #define HA_N_SPLINES 8
@@ -138,6 +140,11 @@ typedef struct ha_model_t {
     int32_t n_static;
     int32_t static_hull[HA_MAX_STATIC];
     float static_pos[HA_MAX_STATIC][3], static_quat[HA_MAX_STATIC][4], static_half[HA_MAX_STATIC][3];
+    /* v5: fixed rigid bodies whose rigid_body_state rows come from the model (world pose, zero velocity):
+     * bodies [body_fixed0, body_fixed0 + n_fixed_bodies), e.g. the table-with-hole links and the bin
+     * (multi_object.py:626-637). 0 = the table row copies the table actor's root state (earlier scenes). */
+    int32_t n_fixed_bodies, body_fixed0;
+    float body_fixed_pose[HA_MAX_FIXED_BODIES][7];
 } ha_model_t;
 
 /* Simulation + task parameters (Ur5SihBase.yaml, Ur5SihMultiObject*.yaml). */

@@ -16,14 +16,14 @@
 #include "ha_device.h"
 #include "../../include/handarm_abi.h"
 
-#define MAXC 21
+#define MAXC 21          /* contacts per chunk: 3 rows each -> 63 rows, one per lane (lane 63 idle) */
 #define MAXR (3 * MAXC)
 #define RS 35            /* max row stride: D + 6 * n_obj <= 35 (Ur5Sih); see row_stride<ND>() */
 #define NOBJ HA_MAX_OBJ
 #define MAXD 24
 #define HA_ND 17         /* DOF count the kernels are compiled for (UR5 + SIH); checked by ha_create */
 #define MAXB 48          /* rigid bodies per env (contact-force rows): robot links + objects + statics */
-#define MAXV 64          /* generalized velocity coordinates: D + 6 x objects <= one wavefront */
+#define MAXV 72          /* generalized velocity coordinates D + 6 x objects (17 + 6 x 8 = 65 for bin-picking) */
 
 // What the task observables read after refresh_simulation_tensors(): flange pose, fingertip states,
 // dof positions, object root states (filled from FK in the fused step, or from the state tensors).
@@ -55,7 +55,7 @@ struct PostScratch {
     float M[MAXD * MAXD];                       // M, then its Cholesky factor L (stride D)
     DynScratch dyn;
     ObsIn in;
-    float obs[160];
+    float obs[216];                             // Ur5Sih: 108 + 13 x objects (212 at 8 objects)
     float cforce[MAXB][3];
     float dforce[MAXD];                         // joint force of the last substep (drive + limits) / h
 };
@@ -72,6 +72,13 @@ struct ObjLDS {
     int pool, coll, pad;                // pool id, collision enabled
 };
 
+// One contact point (LDS, after the object slots): up to MAXC x chunks per env (task_lds_bytes).
+struct ContactLDS {
+    float x[3], n[3];                   // world point, normal from body b to body a
+    float sep, mu;                      // separation (< 0: penetration), combined friction
+    int a, b;                           // body codes: -1 static, 0..NOBJ-1 object, 100 + link
+};
+
 struct EnvLDS {
     float q[MAXD], qd[MAXD], tgt[MAXD];
     float lp[HA_MAX_LINKS][3], lq[HA_MAX_LINKS][4];
@@ -79,14 +86,12 @@ struct EnvLDS {
     float Minv[MAXD * MAXD];                    // S ~ M^-1 (factor_inverse), stride D
     float Cb[MAXD];
     float v[MAXV];
-    float cx[MAXC][3], cn[MAXC][3], csep[MAXC], cmu[MAXC];
-    int ca[MAXC], cb[MAXC];
     int nc, nr, pad0, pad1;
     union {
         PostScratch pd;
         ColScratch col;
         RowScratch rows;
-        float xfer[64];     // lane exchange outside the physics phases (controller; PGS impulses -> forces)
+        float xfer[128];    // lane exchange outside the physics phases (controller; PGS impulses -> forces)
     } u;
 };
 
@@ -113,24 +118,39 @@ HD int compact_index(int lane, int D, int so0, int so1) {
     if (so1 >= 0 && t >= 6 * so1 && t < 6 * so1 + 6) return D + 6 + t - 6 * so1;
     return -1;
 }
-// LDS block of one env: EnvLDS up to the phase union, the union at the task's row stride, then the object
-// slots (ObjLDS x capacity), 16-byte aligned
-__host__ __device__ inline size_t obj_lds_offset(int rs) {
-    size_t rows = 2 * (size_t)MAXR * rs * sizeof(float);
+// LDS block of one env: EnvLDS up to the phase union, the union at the task's row stride and contact
+// chunks (J and Y of MAXR x chunks rows), then the object slots (ObjLDS x capacity), then the contact list
+// (ContactLDS x MAXC x chunks), 16-byte aligned
+__host__ __device__ inline size_t obj_lds_offset(int rs, int nch) {
+    size_t rows = 2 * (size_t)MAXR * nch * rs * sizeof(float);
     size_t u = sizeof(PostScratch) > sizeof(ColScratch) ? sizeof(PostScratch) : sizeof(ColScratch);
     if (rows > u) u = rows;
     return (offsetof(EnvLDS, u) + u + 15) & ~(size_t)15;
 }
-__host__ __device__ inline size_t task_lds_bytes(int rs, int obj_capacity) {
-    return obj_lds_offset(rs) + (size_t)obj_capacity * sizeof(ObjLDS);
+__host__ __device__ inline size_t contact_lds_offset(int rs, int obj_capacity, int nch) {
+    return obj_lds_offset(rs, nch) + (size_t)obj_capacity * sizeof(ObjLDS);
 }
+__host__ __device__ inline size_t task_lds_bytes(int rs, int obj_capacity, int nch) {
+    return contact_lds_offset(rs, obj_capacity, nch) + (size_t)MAXC * nch * sizeof(ContactLDS);
+}
+
+// Compile-time shape of a kernel family's physics: DOF count, object slots, contact chunks (MAXC contacts
+// each) and velocity words per lane (coordinates lane and lane + 64 when D + 6 x objects > 64).
+template <int ND, int OCAP, int NCH>
+struct PhysCfg {
+    static constexpr int nd = ND, ocap = OCAP, nch = NCH;
+    static constexpr int vw = ND + 6 * OCAP > 64 ? 2 : 1;
+    static_assert(ND + 6 * OCAP <= MAXV, "generalized velocity exceeds MAXV");
+};
 
 struct SimCtx {
     const ha_model_t* __restrict__ m;
     const ha_params_t* __restrict__ p;
     EnvLDS* s;
     ObjLDS* o;              // the env's object slots (after the EnvLDS block, see task_lds_bytes)
+    ContactLDS* k;          // the env's contact list (after the object slots)
     int lane, D, NO, L;
+    int maxc;               // contact capacity (MAXC x chunks of the kernel family)
     const float* dr;        // this env's domain-randomization row (HA_DR_*), or null when DR is off
 };
 
@@ -466,21 +486,22 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
     if (lane == 0) {
         for (int t = 0; t < k; t++) {
             int slot;
-            if (s.nc >= MAXC) {
+            if (s.nc >= c.maxc) {
                 int w = 0;
-                for (int j = 1; j < MAXC; j++)
-                    if (s.csep[j] > s.csep[w]) w = j;
-                if (s.csep[w] <= S[t]) continue;
+                for (int j = 1; j < c.maxc; j++)
+                    if (c.k[j].sep > c.k[w].sep) w = j;
+                if (c.k[w].sep <= S[t]) continue;
                 slot = w;
             } else {
                 slot = s.nc++;
             }
-            st3(s.cx[slot], P[t]);
-            st3(s.cn[slot], n);
-            s.csep[slot] = S[t];
-            s.cmu[slot] = contact_friction(c, a, b);
-            s.ca[slot] = a;
-            s.cb[slot] = b;
+            ContactLDS& ct = c.k[slot];
+            st3(ct.x, P[t]);
+            st3(ct.n, n);
+            ct.sep = S[t];
+            ct.mu = contact_friction(c, a, b);
+            ct.a = a;
+            ct.b = b;
         }
     }
     wsync();
@@ -830,8 +851,9 @@ HD void tangents(f3 n, f3& t1, f3& t2) {
 }
 
 
-template <int ND>
+template <class PC>
 HD void substep(SimCtx& c, float hdt) {
+    constexpr int ND = PC::nd, NCH = PC::nch, VW = PC::vw;
     constexpr int RSN = row_stride<ND>();
     PROF_BEGIN();
     EnvLDS& s = *c.s;
@@ -898,72 +920,84 @@ HD void substep(SimCtx& c, float hdt) {
     PROF(3);
     PROF_COUNT(8, s.nc);
     PROF_COUNT(9, 1);
-    // ---- contact rows: lane r owns row r (normal, friction 1, friction 2 of contact r / 3). Rows are packed
-    //      with the task's stride (J then Y), so a one-object task needs less LDS (row_stride, task_lds_bytes)
+    // ---- contact rows: in chunk ch, lane r < MAXR owns global row MAXR ch + r (normal, friction 1, friction 2
+    //      of contact MAXC ch + r / 3). Rows are packed with the task's stride (J then Y), so a one-object task
+    //      needs less LDS (row_stride, task_lds_bytes)
     float* Jb = s.u.rows.J;
-    float* Yb = Jb + MAXR * RSN;
+    float* Yb = Jb + MAXR * NCH * RSN;
     int nc = s.nc;
-    int nr = 3 * nc;    // nc <= MAXC -> <= MAXR rows
-    int r = lane;
-    float vt = 0.f, winv = 0.f, lam = 0.f, cmu = 0.f;
-    if (r < nr) {
-        cmu = s.cmu[r / 3];
-        float* Jr = Jb + r * RSN;
-        for (int k = 0; k < RSN; k++) Jr[k] = 0.0f;
-        int ci = r / 3, k = r % 3;
-        f3 n = ld3(s.cn[ci]), t1, t2;
-        tangents(n, t1, t2);
-        f3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
-        f3 x = ld3(s.cx[ci]);
-        int so0, so1;
-        contact_slots(s.ca[ci], s.cb[ci], so0, so1);
-        jac_body(c, s.ca[ci], x, dir, 1.0f, Jr, so0);
-        jac_body(c, s.cb[ci], x, dir, -1.0f, Jr, so0);
-        if (k == 0) {
-            float sp = s.csep[ci];
-            vt = sp > 0 ? -sp / hdt : -p.baumgarte * sp / hdt;
-            if (vt > p.max_depen_vel) vt = p.max_depen_vel;
-        }
-        // Y_r = M^-1 J_r^T (robot block through the explicit inverse, object blocks 1/m, I_w^-1)
-        float* Yr = Yb + r * RSN;
-        for (int i = 0; i < D; i++) {
-            float acc = 0.0f;
-            for (int j = 0; j < D; j++) acc += s.Minv[i * D + j] * Jr[j];
-            Yr[i] = acc;
-        }
-        for (int sl = 0; sl < row_slots<ND>(); sl++) {
-            int o = sl == 0 ? so0 : so1;
-            const float* Jo = Jr + D + 6 * sl;
-            float* Yo = Yr + D + 6 * sl;
-            if (o < 0) {
-                for (int t = 0; t < 6; t++) Yo[t] = 0.0f;
-                continue;
+    int nr = 3 * nc;    // nc <= MAXC x NCH -> <= MAXR x NCH rows
+    float vt[NCH], winv[NCH], lam[NCH], cmu[NCH];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+        vt[ch] = 0.f; winv[ch] = 0.f; lam[ch] = 0.f; cmu[ch] = 0.f;
+        int r = MAXR * ch + lane;
+        if (lane < MAXR && r < nr) {
+            const ContactLDS& ct = c.k[r / 3];
+            cmu[ch] = ct.mu;
+            float* Jr = Jb + r * RSN;
+            for (int k = 0; k < RSN; k++) Jr[k] = 0.0f;
+            int k = r % 3;
+            f3 n = ld3(ct.n), t1, t2;
+            tangents(n, t1, t2);
+            f3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
+            f3 x = ld3(ct.x);
+            int so0, so1;
+            contact_slots(ct.a, ct.b, so0, so1);
+            jac_body(c, ct.a, x, dir, 1.0f, Jr, so0);
+            jac_body(c, ct.b, x, dir, -1.0f, Jr, so0);
+            if (k == 0) {
+                float sp = ct.sep;
+                float v0 = sp > 0 ? -sp / hdt : -p.baumgarte * sp / hdt;
+                if (v0 > p.max_depen_vel) v0 = p.max_depen_vel;
+                vt[ch] = v0;
             }
-            float im = 1.0f / c.o[o].om;
-            Yo[0] = Jo[0] * im; Yo[1] = Jo[1] * im; Yo[2] = Jo[2] * im;
-            f3 a = mv3(c.o[o].oIinv, mk3(Jo[3], Jo[4], Jo[5]));
-            Yo[3] = a.x; Yo[4] = a.y; Yo[5] = a.z;
+            // Y_r = M^-1 J_r^T (robot block through the explicit inverse, object blocks 1/m, I_w^-1)
+            float* Yr = Yb + r * RSN;
+            for (int i = 0; i < D; i++) {
+                float acc = 0.0f;
+                for (int j = 0; j < D; j++) acc += s.Minv[i * D + j] * Jr[j];
+                Yr[i] = acc;
+            }
+            for (int sl = 0; sl < row_slots<ND>(); sl++) {
+                int o = sl == 0 ? so0 : so1;
+                const float* Jo = Jr + D + 6 * sl;
+                float* Yo = Yr + D + 6 * sl;
+                if (o < 0) {
+                    for (int t = 0; t < 6; t++) Yo[t] = 0.0f;
+                    continue;
+                }
+                float im = 1.0f / c.o[o].om;
+                Yo[0] = Jo[0] * im; Yo[1] = Jo[1] * im; Yo[2] = Jo[2] * im;
+                f3 a = mv3(c.o[o].oIinv, mk3(Jo[3], Jo[4], Jo[5]));
+                Yo[3] = a.x; Yo[4] = a.y; Yo[5] = a.z;
+            }
+            float a = 0.0f;
+            for (int t = 0; t < RSN; t++) a += Jr[t] * Yr[t];
+            winv[ch] = 1.0f / (a + 1e-9f);
         }
-        float a = 0.0f;
-        for (int t = 0; t < RSN; t++) a += Jr[t] * Yr[t];
-        winv = 1.0f / (a + 1e-9f);
     }
     wsync();
     // coupling inside each contact's 3-row block (Delassus entries J_ri . M^-1 J_rj^T, i > j): lane of
     // friction row 1 holds a10, lane of friction row 2 holds a20 and a21
-    float ca0 = 0.f, ca1 = 0.f;
-    if (r < nr && r % 3 != 0) {
-        const float* Jr = Jb + r * RSN;
-        int r0 = r - r % 3;
-        const float* Y0 = Yb + r0 * RSN;
-        float a = 0.0f;
-        for (int t = 0; t < RSN; t++) a += Jr[t] * Y0[t];
-        ca0 = a;
-        if (r % 3 == 2) {
-            const float* Y1 = Y0 + RSN;
-            float b = 0.0f;
-            for (int t = 0; t < RSN; t++) b += Jr[t] * Y1[t];
-            ca1 = b;
+    float ca0[NCH], ca1[NCH];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++) {
+        ca0[ch] = 0.f; ca1[ch] = 0.f;
+        int r = MAXR * ch + lane;
+        if (lane < MAXR && r < nr && r % 3 != 0) {
+            const float* Jr = Jb + r * RSN;
+            int r0 = r - r % 3;
+            const float* Y0 = Yb + r0 * RSN;
+            float a = 0.0f;
+            for (int t = 0; t < RSN; t++) a += Jr[t] * Y0[t];
+            ca0[ch] = a;
+            if (r % 3 == 2) {
+                const float* Y1 = Y0 + RSN;
+                float b = 0.0f;
+                for (int t = 0; t < RSN; t++) b += Jr[t] * Y1[t];
+                ca1[ch] = b;
+            }
         }
     }
     PROF(4);
@@ -987,7 +1021,9 @@ HD void substep(SimCtx& c, float hdt) {
         vt_lo = s_lo > 0 ? -s_lo / hdt : -p.baumgarte * s_lo / hdt;
         vt_up = s_up > 0 ? -s_up / hdt : -p.baumgarte * s_up / hdt;
     }
+    // generalized velocity: coordinate `lane` in vreg, coordinate 64 + lane in vregh (VW == 2 only)
     float vreg = lane < NV ? s.v[lane] : 0.0f;
+    float vregh = (VW == 2 && lane + 64 < NV) ? s.v[lane + 64] : 0.0f;
     wsync();
     PROF(5);
     // ---- projected Gauss-Seidel (velocity form): joint rows d = 0..D-1 (drive, lower, upper), then
@@ -1030,76 +1066,91 @@ HD void substep(SimCtx& c, float hdt) {
         // contact blocks: the three J.v reductions of a contact run together; the friction rows see the
         // normal (and first friction) update through the block's Delassus entries, which equals
         // re-reducing J.v after each row (row-by-row Gauss-Seidel) up to rounding
-        // lane = generalized coordinate; its entry of a compact row is at compact_index (or absent -> 0)
+        // lane = generalized coordinate; its entry of a compact row is at compact_index (or absent -> 0).
+        // The next contact's row entries are prefetched while the current one reduces.
         float j0n = 0.f, j1n = 0.f, j2n = 0.f, y0n = 0.f, y1n = 0.f, y2n = 0.f;
-        if (nc > 0) {
+        float h0n = 0.f, h1n = 0.f, h2n = 0.f, g0n = 0.f, g1n = 0.f, g2n = 0.f;   // coordinate 64 + lane
+        auto fetch = [&](int ci) {
             int ix = lane < RSN ? lane : -1;       // one slot: the compact row is the dense row
+            int ixh = -1;
             if constexpr (row_slots<ND>() == 2) {
                 int so0, so1;
-                contact_slots(s.ca[0], s.cb[0], so0, so1);
+                contact_slots(c.k[ci].a, c.k[ci].b, so0, so1);
                 ix = compact_index(lane, D, so0, so1);
+                if (VW == 2) ixh = compact_index(lane + 64, D, so0, so1);
             }
+            const float* Jn = J + 3 * ci * RSN;
+            const float* Yn = Y + 3 * ci * RSN;
+            j0n = 0.f; j1n = 0.f; j2n = 0.f; y0n = 0.f; y1n = 0.f; y2n = 0.f;
             if (ix >= 0) {
-                j0n = J[ix]; j1n = J[RSN + ix]; j2n = J[2 * RSN + ix];
-                y0n = Y[ix]; y1n = Y[RSN + ix]; y2n = Y[2 * RSN + ix];
+                j0n = Jn[ix]; j1n = Jn[RSN + ix]; j2n = Jn[2 * RSN + ix];
+                y0n = Yn[ix]; y1n = Yn[RSN + ix]; y2n = Yn[2 * RSN + ix];
             }
-        }
-        for (int ci = 0; ci < nc; ci++) {
-            int r0 = 3 * ci;
-            float j0 = j0n, j1 = j1n, j2 = j2n, y0 = y0n, y1 = y1n, y2 = y2n;
-            if (ci + 1 < nc) {
-                int ix = lane < RSN ? lane : -1;
-                if constexpr (row_slots<ND>() == 2) {
-                    int so0, so1;
-                    contact_slots(s.ca[ci + 1], s.cb[ci + 1], so0, so1);
-                    ix = compact_index(lane, D, so0, so1);
-                }
-                const float* Jn = J + (r0 + 3) * RSN;
-                const float* Yn = Y + (r0 + 3) * RSN;
-                j0n = 0.f; j1n = 0.f; j2n = 0.f; y0n = 0.f; y1n = 0.f; y2n = 0.f;
-                if (ix >= 0) {
-                    j0n = Jn[ix]; j1n = Jn[RSN + ix]; j2n = Jn[2 * RSN + ix];
-                    y0n = Yn[ix]; y1n = Yn[RSN + ix]; y2n = Yn[2 * RSN + ix];
+            if (VW == 2) {
+                h0n = 0.f; h1n = 0.f; h2n = 0.f; g0n = 0.f; g1n = 0.f; g2n = 0.f;
+                if (ixh >= 0) {
+                    h0n = Jn[ixh]; h1n = Jn[RSN + ixh]; h2n = Jn[2 * RSN + ixh];
+                    g0n = Yn[ixh]; g1n = Yn[RSN + ixh]; g2n = Yn[2 * RSN + ixh];
                 }
             }
-            float jv0 = j0 * vreg, jv1 = j1 * vreg, jv2 = j2 * vreg;
-            wave_sum_rows3(jv0, jv1, jv2);
-            float l0 = bcast(lam, r0), l1 = bcast(lam, r0 + 1), l2 = bcast(lam, r0 + 2);
-            float n0 = l0 - (jv0 - bcast(vt, r0)) * bcast(winv, r0);
-            n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
-            float d0 = n0 - l0;
-            float hi = bcast(cmu, r0) * n0;
-            jv1 = jv1 + bcast(ca0, r0 + 1) * d0;
-            float n1 = l1 - (jv1 - bcast(vt, r0 + 1)) * bcast(winv, r0 + 1);
-            n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
-            float d1 = n1 - l1;
-            jv2 = (jv2 + bcast(ca0, r0 + 2) * d0) + bcast(ca1, r0 + 2) * d1;
-            float n2 = l2 - (jv2 - bcast(vt, r0 + 2)) * bcast(winv, r0 + 2);
-            n2 = n2 < -hi ? -hi : (n2 > hi ? hi : n2);
-            float d2 = n2 - l2;
-            if (lane == r0) lam = n0;
-            if (lane == r0 + 1) lam = n1;
-            if (lane == r0 + 2) lam = n2;
-            if (d0 != 0.0f) vreg += y0 * d0;
-            if (d1 != 0.0f) vreg += y1 * d1;
-            if (d2 != 0.0f) vreg += y2 * d2;
+        };
+        if (nc > 0) fetch(0);
+#pragma unroll
+        for (int ch = 0; ch < NCH; ch++) {
+            int cend = nc < MAXC * (ch + 1) ? nc : MAXC * (ch + 1);
+            for (int ci = MAXC * ch; ci < cend; ci++) {
+                int r0 = 3 * (ci - MAXC * ch);      // row of this contact within the chunk (= its lane)
+                float j0 = j0n, j1 = j1n, j2 = j2n, y0 = y0n, y1 = y1n, y2 = y2n;
+                float h0 = h0n, h1 = h1n, h2 = h2n, g0 = g0n, g1 = g1n, g2 = g2n;
+                if (ci + 1 < nc) fetch(ci + 1);
+                float jv0 = j0 * vreg, jv1 = j1 * vreg, jv2 = j2 * vreg;
+                if (VW == 2) {
+                    jv0 = jv0 + h0 * vregh;
+                    jv1 = jv1 + h1 * vregh;
+                    jv2 = jv2 + h2 * vregh;
+                }
+                wave_sum_rows3(jv0, jv1, jv2);
+                float l0 = bcast(lam[ch], r0), l1 = bcast(lam[ch], r0 + 1), l2 = bcast(lam[ch], r0 + 2);
+                float n0 = l0 - (jv0 - bcast(vt[ch], r0)) * bcast(winv[ch], r0);
+                n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
+                float d0 = n0 - l0;
+                float hi = bcast(cmu[ch], r0) * n0;
+                jv1 = jv1 + bcast(ca0[ch], r0 + 1) * d0;
+                float n1 = l1 - (jv1 - bcast(vt[ch], r0 + 1)) * bcast(winv[ch], r0 + 1);
+                n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
+                float d1 = n1 - l1;
+                jv2 = (jv2 + bcast(ca0[ch], r0 + 2) * d0) + bcast(ca1[ch], r0 + 2) * d1;
+                float n2 = l2 - (jv2 - bcast(vt[ch], r0 + 2)) * bcast(winv[ch], r0 + 2);
+                n2 = n2 < -hi ? -hi : (n2 > hi ? hi : n2);
+                float d2 = n2 - l2;
+                if (lane == r0) lam[ch] = n0;
+                if (lane == r0 + 1) lam[ch] = n1;
+                if (lane == r0 + 2) lam[ch] = n2;
+                if (d0 != 0.0f) { vreg += y0 * d0; if (VW == 2) vregh += g0 * d0; }
+                if (d1 != 0.0f) { vreg += y1 * d1; if (VW == 2) vregh += g1 * d1; }
+                if (d2 != 0.0f) { vreg += y2 * d2; if (VW == 2) vregh += g2 * d2; }
+            }
         }
     }
-    s.u.xfer[lane] = lam;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ch++)
+        if (lane < MAXR) s.u.xfer[MAXR * ch + lane] = lam[ch];    // impulse of global row MAXR ch + lane
     if (lane < D) s.u.pd.dforce[lane] = ((dlam + lam_lo) - lam_up) / hdt;
     wsync();
     if (lane < NV) s.v[lane] = vreg;
+    if (VW == 2 && lane + 64 < NV) s.v[lane + 64] = vregh;
     PROF(6);
     // contact forces (last substep wins, like the oracle)
     if (lane == 0) {
         for (int b = 0; b < MAXB; b++) s.u.pd.cforce[b][0] = s.u.pd.cforce[b][1] = s.u.pd.cforce[b][2] = 0.f;
         for (int ci = 0; ci < nc; ci++) {
             int r0 = 3 * ci;
-            f3 n = ld3(s.cn[ci]), t1, t2;
+            const ContactLDS& ct = c.k[ci];
+            f3 n = ld3(ct.n), t1, t2;
             tangents(n, t1, t2);
             f3 f = (n * s.u.xfer[r0] + t1 * s.u.xfer[r0 + 1]) + t2 * s.u.xfer[r0 + 2];
             f = f * (1.0f / hdt);
-            int bodies[2] = {s.ca[ci], s.cb[ci]};
+            int bodies[2] = {ct.a, ct.b};
             for (int sd = 0; sd < 2; sd++) {
                 int bd = bodies[sd];
                 float sg = sd == 0 ? 1.0f : -1.0f;

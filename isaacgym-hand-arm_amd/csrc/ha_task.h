@@ -5,8 +5,10 @@
 #pragma once
 #include "ha_physics.h"
 
-#define NUM_OBS 147
 #define NUM_ACT 11
+// observation size for n objects: 80 + 3 n (object_pos) + 10 n (object_bounding_box) + 10 + 15 + 3
+// (Ur5SihMultiObjectManipulation.yaml:24-26 with num_objects = n; 147 at the default 3)
+HD constexpr int ur5sih_num_obs(int n_objects) { return 108 + 13 * n_objects; }
 // robot link indices (body index in env = 1 + link)
 #define LINK_FLANGE 9
 __constant__ int c_tip_links[5] = {28, 15, 21, 24, 18};   // thumb, index, middle, ring, little (ur5sih.py:613)
@@ -156,7 +158,8 @@ HD void dr_sample(const SimCtx& c, const ha_state_t& st, int env) {
 HD void task_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags) {
     EnvLDS& s = *c.s;
     const ha_params_t& p = *c.p;
-    int lane = c.lane, D = c.D, NO = c.NO, A = 3 + NO, P = p.num_initial_poses;
+    const ha_model_t& m = *c.m;
+    int lane = c.lane, D = c.D, NO = c.NO, A = m.n_actors, P = p.num_initial_poses;
     float dr[5];
     if (flags & HA_FLAG_REPLAY_DRAWS) {
 #pragma unroll
@@ -177,7 +180,7 @@ HD void task_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags) {
         int o = lane;
         const float* pos0 = st.object_pos_initial + (((size_t)env * P + cfg) * NO + o) * 3;
         const float* quat0 = st.object_quat_initial + (((size_t)env * P + cfg) * NO + o) * 4;
-        float* r = st.root_state + ((size_t)env * A + 3 + o) * 13;
+        float* r = st.root_state + ((size_t)env * A + m.actor_object0 + o) * 13;
         r[0] = pos0[0]; r[1] = pos0[1]; r[2] = pos0[2];
         r[3] = quat0[0]; r[4] = quat0[1]; r[5] = quat0[2]; r[6] = quat0[3];
         for (int k = 7; k < 13; k++) r[k] = 0.0f;
@@ -192,7 +195,7 @@ HD void task_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags) {
         noise = noise * p.goal_noise[k];
         float g = p.goal_pos[k] + noise;
         st.goal_pos[env * 3 + k] = g;
-        st.root_state[(size_t)env * A * 13 + k] = g;        // goal actor 0
+        st.root_state[((size_t)env * A + m.actor_goal) * 13 + k] = g;
     } else if (lane == 12) {
         st.target_object_index[env] = tgt_obj;
         st.object_configuration_indices[env] = cfg;
@@ -241,8 +244,11 @@ HD void post_step(SimCtx& c, const ha_state_t& st, int env, const ObsIn& in, boo
     int cfg = (int)st.object_configuration_indices[env];
     const float* goal = st.goal_pos + env * 3;
     const float* cache = st.obs_cache + (size_t)env * NO * 7;
-    // observation vector (Ur5SihMultiObjectManipulation.yaml:24-26), computed lane-parallel
-    for (int e = lane; e < NUM_OBS; e += 64) {
+    // observation vector (Ur5SihMultiObjectManipulation.yaml:24-26), computed lane-parallel; object blocks
+    // sized by the object count (multi_object.py:128,245)
+    const int NOBS = ur5sih_num_obs(NO);
+    const int e_bb = 80 + 3 * NO, e_tb = e_bb + 10 * NO, e_ft = e_tb + 10, e_tg = e_ft + 15;
+    for (int e = lane; e < NOBS; e += 64) {
         float v;
         if (e < 6) v = in.dofpos[e];
         else if (e < 13) v = in.flange[e - 6];
@@ -250,12 +256,12 @@ HD void post_step(SimCtx& c, const ha_state_t& st, int env, const ObsIn& in, boo
         else if (e < 48) { int t = (e - 28) / 4, k = (e - 28) % 4; v = in.tip[t][3 + k]; }
         else if (e < 63) { int t = (e - 48) / 3, k = (e - 48) % 3; v = in.tip[t][7 + k]; }
         else if (e < 80) v = st.dof_position_targets[(size_t)env * D + (e - 63)];
-        else if (e < 89) { int o = (e - 80) / 3, k = (e - 80) % 3; v = in.obj[o][k]; }
-        else if (e < 129) {
+        else if (e < e_bb) { int o = (e - 80) / 3, k = (e - 80) % 3; v = in.obj[o][k]; }
+        else if (e < e_ft) {
             // object bounding boxes from the PREVIOUS refresh's object pose (reference refresh order,
             // see oracle/task_oracle.py observations())
-            int o = e < 119 ? (e - 89) / 10 : tgt;
-            int k = e < 119 ? (e - 89) % 10 : e - 119;
+            int o = e < e_tb ? (e - e_bb) / 10 : tgt;
+            int k = e < e_tb ? (e - e_bb) % 10 : e - e_tb;
             int pid = c.o[o].pool;
             const float* cq = cache + o * 7;
             if (k < 3) {
@@ -269,8 +275,8 @@ HD void post_step(SimCtx& c, const ha_state_t& st, int env, const ObsIn& in, boo
             } else {
                 v = m.pool_bbox_ext[pid][k - 7];
             }
-        } else if (e < 144) { int t = (e - 129) / 3, k = (e - 129) % 3; v = in.obj[tgt][k] - in.tip[t][k]; }
-        else { int k = e - 144; v = goal[k] - in.obj[tgt][k]; }
+        } else if (e < e_tg) { int t = (e - e_ft) / 3, k = (e - e_ft) % 3; v = in.obj[tgt][k] - in.tip[t][k]; }
+        else { int k = e - e_tg; v = goal[k] - in.obj[tgt][k]; }
         ob[e] = v;
     }
     wsync();
@@ -278,11 +284,11 @@ HD void post_step(SimCtx& c, const ha_state_t& st, int env, const ObsIn& in, boo
     // teacher observations and not in VecTask.reset)
     bool noise = !obs_only && p.dr_enable;
     uint32_t nctr = (st.episode[env] << 12) ^ (uint32_t)st.progress_buf[env];
-    for (int e = lane; e < NUM_OBS; e += 64) {
+    for (int e = lane; e < NOBS; e += 64) {
         float v = ob[e];
-        st.teacher_obs[(size_t)env * NUM_OBS + e] = v;
+        st.teacher_obs[(size_t)env * NOBS + e] = v;
         if (noise) v = v + p.dr_obs_noise * gauss01(p.seed, env, nctr, e);
-        st.obs[(size_t)env * NUM_OBS + e] = v;
+        st.obs[(size_t)env * NOBS + e] = v;
     }
     if (obs_only) return;     // VecTask.reset(): compute_observations without a refresh
     // refresh the observable cache with the current object pose

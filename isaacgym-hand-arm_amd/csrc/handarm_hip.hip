@@ -15,13 +15,26 @@
 
 enum { MODE_SIMULATE = 0, MODE_STEP = 1, MODE_OBSERVE = 2, MODE_RESET = 3 };
 
-template <int TASK>
+// Kernel families: one per task, plus the Ur5Sih clutter family (bin-picking, BASELINE config 5: up to 8
+// objects, two contact chunks, a 65-coordinate velocity) that runs the same Ur5Sih task math. ha_create
+// picks the family from the task and the object count.
+#define FAM_UR5SIH_CLUTTER 3
+template <int FAM>
+__host__ __device__ constexpr int fam_task() { return FAM == FAM_UR5SIH_CLUTTER ? HA_TASK_UR5SIH : FAM; }
+template <int FAM>
 __host__ __device__ constexpr int task_nd() {
-    return TASK == HA_TASK_ALLEGRO_HAND ? AH_ND : (TASK == HA_TASK_ALLEGRO_KUKA ? AK_ND : HA_ND);
+    return FAM == HA_TASK_ALLEGRO_HAND ? AH_ND : (FAM == HA_TASK_ALLEGRO_KUKA ? AK_ND : HA_ND);
 }
-// object slots in LDS per env (objects per env the task's kernels support)
-template <int TASK>
-__host__ __device__ constexpr int task_obj_capacity() { return TASK == HA_TASK_UR5SIH ? 3 : 1; }
+// object slots in LDS per env (objects per env the family's kernels support)
+template <int FAM>
+__host__ __device__ constexpr int task_obj_capacity() {
+    return FAM == FAM_UR5SIH_CLUTTER ? HA_MAX_OBJ : (FAM == HA_TASK_UR5SIH ? 3 : 1);
+}
+// contact chunks (MAXC contacts each)
+template <int FAM>
+__host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5SIH_CLUTTER ? 2 : 1; }
+template <int FAM>
+using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>()>;
 
 
 // ----------------------------------------------------------------------------- state load/store
@@ -138,6 +151,7 @@ __device__ void store_env(SimCtx& c, const ha_state_t& st, int env) {
         if (b >= m.body_robot0 && b < m.body_robot0 + L) v = link_state(c, b - m.body_robot0, k);
         else if (b >= m.body_object0 && b < m.body_object0 + NO) v = object_state(c, b - m.body_object0, k);
         else if (b == m.body_goal) v = rs[m.actor_goal * 13 + k];
+        else if (b >= m.body_fixed0 && b < m.body_fixed0 + m.n_fixed_bodies) v = k < 7 ? m.body_fixed_pose[b - m.body_fixed0][k] : 0.0f;
         else v = rs[m.actor_table * 13 + k];
         bs[e] = v;
     }
@@ -162,24 +176,26 @@ __device__ void ur5sih_obs_in(SimCtx& c, ObsIn* in) {
 
 // observation snapshot straight from the (refreshed) state tensors
 __device__ void snapshot_from_tensors(SimCtx& c, const ha_state_t& st, int env, ObsIn* in) {
-    int lane = c.lane, D = c.D, NO = c.NO, A = 3 + NO, L = c.L, B = 1 + L + 1 + NO;
+    const ha_model_t& m = *c.m;
+    int lane = c.lane, D = c.D, NO = c.NO, A = m.n_actors, B = m.n_bodies, R0 = m.body_robot0;
     const float* bs = st.rigid_body_state + (size_t)env * B * 13;
-    if (lane < 7) in->flange[lane] = bs[(1 + LINK_FLANGE) * 13 + lane];
+    if (lane < 7) in->flange[lane] = bs[(R0 + LINK_FLANGE) * 13 + lane];
     if (lane < 50) {
         int t = lane / 10, k = lane % 10;
-        in->tip[t][k] = bs[(1 + c_tip_links[t]) * 13 + k];
+        in->tip[t][k] = bs[(R0 + c_tip_links[t]) * 13 + k];
     }
     if (lane < D) in->dofpos[lane] = st.dof_state[((size_t)env * D + lane) * 2];
-    for (int e = lane; e < NO * 13; e += 64) in->obj[e / 13][e % 13] = st.root_state[((size_t)env * A + 3) * 13 + e];
+    for (int e = lane; e < NO * 13; e += 64)
+        in->obj[e / 13][e % 13] = st.root_state[((size_t)env * A + m.actor_object0) * 13 + e];
     if (lane < NO) c.o[lane].pool = (int)st.object_indices[(size_t)env * NO + lane];
     wsync();
 }
 
-template <int ND>
+template <class PC>
 __device__ void run_physics(SimCtx& c, int n_calls) {
     float hdt = c.p->dt / (float)c.p->substeps;
     for (int k = 0; k < n_calls; k++)
-        for (int sub = 0; sub < c.p->substeps; sub++) substep<ND>(c, hdt);
+        for (int sub = 0; sub < c.p->substeps; sub++) substep<PC>(c, hdt);
 }
 
 // AllegroHand observation staging
@@ -239,17 +255,20 @@ __device__ void ak_in_from_tensors(SimCtx& c, const ha_state_t& st, int env, AkI
     wsync();
 }
 static_assert(sizeof(AkPost) <= sizeof(PostScratch) - offsetof(PostScratch, in), "AkPost must fit after pd.dyn");
-static_assert(HA_ND + 6 * 7 <= MAXV, "bin-picking (7 objects) must fit the generalized velocity in one wavefront");
+static_assert(HA_ND + 6 * HA_MAX_OBJ <= MAXV, "bin-picking (8 objects) must fit the generalized velocity (MAXV)");
 
 // ----------------------------------------------------------------------------- the kernels
 // One kernel per (task, mode) (one workgroup = one wavefront = one env): each is compiled with only its
 // own path, which keeps every kernel's code small, gives the DOF count to the compiler as a constant, and
 // gives the profiler a distinct name per kernel.
-template <int TASK, int MODE>
+template <int FAM, int MODE>
 __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params,
                                          const ha_state_t& st, int num_envs, int n_calls, uint32_t flags,
                                          int stat_slot) {
-    constexpr int ND = task_nd<TASK>();
+    constexpr int TASK = fam_task<FAM>();
+    constexpr int ND = task_nd<FAM>();
+    constexpr int NCH = task_contact_chunks<FAM>();
+    using PC = FamPhys<FAM>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int env = blockIdx.x;
     if (env >= num_envs) return;
@@ -257,7 +276,9 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.m = model;
     c.p = params;
     c.s = reinterpret_cast<EnvLDS*>(smem);
-    c.o = reinterpret_cast<ObjLDS*>(smem + obj_lds_offset(row_stride<ND>()));
+    c.o = reinterpret_cast<ObjLDS*>(smem + obj_lds_offset(row_stride<ND>(), NCH));
+    c.k = reinterpret_cast<ContactLDS*>(smem + contact_lds_offset(row_stride<ND>(), task_obj_capacity<FAM>(), NCH));
+    c.maxc = MAXC * NCH;
     c.lane = threadIdx.x;
     c.D = ND;                     // == model->n_dofs (ha_create); a constant, so loops over D unroll
     c.NO = params->n_objects;
@@ -286,7 +307,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     }
     load_env(c, S, env, MODE == MODE_SIMULATE);
     if (MODE == MODE_SIMULATE) {
-        run_physics<ND>(c, n_calls);
+        run_physics<PC>(c, n_calls);
         store_env(c, S, env);
         return;
     }
@@ -305,7 +326,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
         ak_controller(c, S, env);
         ak_forces(c, S, env, flags, tsv);
         if (c.lane < AK_TS_KP) tsg[c.lane] = tsv;
-        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<ND>(c, c.p->control_freq_inv);   // vec_task.py:409-412
+        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<PC>(c, c.p->control_freq_inv);   // vec_task.py:409-412
         store_env(c, S, env);
         if (c.lane == 0) S.progress_buf[env] = S.progress_buf[env] + 1;                // allegro_kuka_base.py:1429
         ak_in_from_lds(c, &akp.in);
@@ -321,7 +342,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
             return;
         }
         ah_controller(c, S, env);
-        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<ND>(c, c.p->control_freq_inv);   // vec_task.py:409-412
+        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<PC>(c, c.p->control_freq_inv);   // vec_task.py:409-412
         store_env(c, S, env);
         if (c.lane == 0) S.progress_buf[env] = S.progress_buf[env] + 1;                // allegro_hand.py:629
         ah_in_from_lds(c, &ain);
@@ -330,7 +351,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     }
     if (MODE == MODE_RESET) {
         task_reset(c, S, env, flags);
-        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<ND>(c, 1);
+        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<PC>(c, 1);
         task_reset_finish(c, S, env);
         store_env(c, S, env);
         return;
@@ -344,7 +365,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     // equivalent. Phase 1: the control_freq_inv physics calls (vec_task.py:409-412). One call site keeps
     // a single copy of the physics code.
     for (int ph = do_reset ? 0 : 1; ph < 2; ph++) {
-        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<ND>(c, ph == 0 ? 1 : c.p->control_freq_inv);
+        if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<PC>(c, ph == 0 ? 1 : c.p->control_freq_inv);
         if (ph == 0) task_reset_finish(c, S, env);
     }
     store_env(c, S, env);
@@ -352,16 +373,20 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     post_step(c, S, env, in, false);                           // configurable_vec_task.py:359-390
 }
 
-#define HA_KERNEL(name, TASK, MODE)                                                                             \
+#define HA_KERNEL(name, FAM, MODE)                                                                              \
     extern "C" __global__ void __launch_bounds__(64)                                                          \
         name(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params, ha_state_t st,       \
              int num_envs, int n_calls, uint32_t flags, int stat_slot) {                                        \
-        env_body<TASK, MODE>(model, params, st, num_envs, n_calls, flags, stat_slot);                          \
+        env_body<FAM, MODE>(model, params, st, num_envs, n_calls, flags, stat_slot);                           \
     }
 HA_KERNEL(ha_step_kernel, HA_TASK_UR5SIH, MODE_STEP)
 HA_KERNEL(ha_simulate_kernel, HA_TASK_UR5SIH, MODE_SIMULATE)
 HA_KERNEL(ha_observe_kernel, HA_TASK_UR5SIH, MODE_OBSERVE)
 HA_KERNEL(ha_reset_kernel, HA_TASK_UR5SIH, MODE_RESET)
+HA_KERNEL(hb_step_kernel, FAM_UR5SIH_CLUTTER, MODE_STEP)
+HA_KERNEL(hb_simulate_kernel, FAM_UR5SIH_CLUTTER, MODE_SIMULATE)
+HA_KERNEL(hb_observe_kernel, FAM_UR5SIH_CLUTTER, MODE_OBSERVE)
+HA_KERNEL(hb_reset_kernel, FAM_UR5SIH_CLUTTER, MODE_RESET)
 HA_KERNEL(ah_step_kernel, HA_TASK_ALLEGRO_HAND, MODE_STEP)
 HA_KERNEL(ah_simulate_kernel, HA_TASK_ALLEGRO_HAND, MODE_SIMULATE)
 HA_KERNEL(ah_observe_kernel, HA_TASK_ALLEGRO_HAND, MODE_OBSERVE)
@@ -372,8 +397,16 @@ HA_KERNEL(ak_observe_kernel, HA_TASK_ALLEGRO_KUKA, MODE_OBSERVE)
 HA_KERNEL(ak_reset_kernel, HA_TASK_ALLEGRO_KUKA, MODE_RESET)
 
 typedef void (*env_kernel_t)(const ha_model_t*, const ha_params_t*, ha_state_t, int, int, uint32_t, int);
-static env_kernel_t kernel_for(int task, int mode) {
-    if (task == HA_TASK_ALLEGRO_KUKA) {
+static env_kernel_t kernel_for(int fam, int mode) {
+    if (fam == FAM_UR5SIH_CLUTTER) {
+        switch (mode) {
+            case MODE_STEP: return hb_step_kernel;
+            case MODE_SIMULATE: return hb_simulate_kernel;
+            case MODE_OBSERVE: return hb_observe_kernel;
+            default: return hb_reset_kernel;
+        }
+    }
+    if (fam == HA_TASK_ALLEGRO_KUKA) {
         switch (mode) {
             case MODE_STEP: return ak_step_kernel;
             case MODE_SIMULATE: return ak_simulate_kernel;
@@ -381,7 +414,7 @@ static env_kernel_t kernel_for(int task, int mode) {
             default: return ak_reset_kernel;
         }
     }
-    if (task == HA_TASK_ALLEGRO_HAND) {
+    if (fam == HA_TASK_ALLEGRO_HAND) {
         switch (mode) {
             case MODE_STEP: return ah_step_kernel;
             case MODE_SIMULATE: return ah_simulate_kernel;
@@ -413,7 +446,7 @@ struct ha_handle_s {
     ha_model_t* d_model;
     ha_params_t* d_params;
     ha_params_t h_params;
-    int N, NO, D, L, A, B, task;
+    int N, NO, D, L, A, B, task, fam;
     ha_state_t st;
     int bound;
     int stat_slots;
@@ -433,22 +466,36 @@ struct ha_handle_s {
         }                                                                             \
     } while (0)
 
-// dynamic LDS of a task's kernels: the EnvLDS prefix plus the largest phase scratch at the task's row stride
-static int obj_capacity(int task) {
-    return task == HA_TASK_UR5SIH ? task_obj_capacity<HA_TASK_UR5SIH>()
-                                  : (task == HA_TASK_ALLEGRO_HAND ? task_obj_capacity<HA_TASK_ALLEGRO_HAND>()
-                                                                   : task_obj_capacity<HA_TASK_ALLEGRO_KUKA>());
+// per-family shape (object capacity, LDS bytes, row stride), from the same templates the kernels use
+template <int FAM>
+static size_t fam_lds_bytes() {
+    return task_lds_bytes(row_stride<task_nd<FAM>()>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>());
 }
-static size_t lds_bytes(int task) {
-    if (task == HA_TASK_ALLEGRO_KUKA)
-        return task_lds_bytes(row_stride<AK_ND>(), task_obj_capacity<HA_TASK_ALLEGRO_KUKA>());
-    if (task == HA_TASK_ALLEGRO_HAND)
-        return task_lds_bytes(row_stride<AH_ND>(), task_obj_capacity<HA_TASK_ALLEGRO_HAND>());
-    return task_lds_bytes(row_stride<HA_ND>(), task_obj_capacity<HA_TASK_UR5SIH>());
+static int obj_capacity(int fam) {
+    switch (fam) {
+        case FAM_UR5SIH_CLUTTER: return task_obj_capacity<FAM_UR5SIH_CLUTTER>();
+        case HA_TASK_ALLEGRO_HAND: return task_obj_capacity<HA_TASK_ALLEGRO_HAND>();
+        case HA_TASK_ALLEGRO_KUKA: return task_obj_capacity<HA_TASK_ALLEGRO_KUKA>();
+        default: return task_obj_capacity<HA_TASK_UR5SIH>();
+    }
+}
+static size_t lds_bytes(int fam) {
+    switch (fam) {
+        case FAM_UR5SIH_CLUTTER: return fam_lds_bytes<FAM_UR5SIH_CLUTTER>();
+        case HA_TASK_ALLEGRO_HAND: return fam_lds_bytes<HA_TASK_ALLEGRO_HAND>();
+        case HA_TASK_ALLEGRO_KUKA: return fam_lds_bytes<HA_TASK_ALLEGRO_KUKA>();
+        default: return fam_lds_bytes<HA_TASK_UR5SIH>();
+    }
 }
 static int task_row_stride(int task) {
     return task == HA_TASK_ALLEGRO_KUKA ? row_stride<AK_ND>()
                                         : (task == HA_TASK_ALLEGRO_HAND ? row_stride<AH_ND>() : row_stride<HA_ND>());
+}
+// kernel family of a task configuration: Ur5Sih with more objects than the dense family's 3 slots runs the
+// clutter family (bin-picking)
+static int family_of(const ha_params_t* p) {
+    if (p->task == HA_TASK_UR5SIH && p->n_objects > task_obj_capacity<HA_TASK_UR5SIH>()) return FAM_UR5SIH_CLUTTER;
+    return p->task;
 }
 
 extern "C" {
@@ -479,11 +526,19 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
             if (params->ak_fingertip_links[i] < 0 || params->ak_fingertip_links[i] >= model->n_links) return HA_E_MODEL;
     }
     if (model->n_actors < 1 || model->n_bodies < model->n_links + params->n_objects) return HA_E_MODEL;
-    if (model->n_links > HA_MAX_LINKS || params->n_objects > obj_capacity(params->task) ||
+    int fam = family_of(params);
+    if (params->task == HA_TASK_UR5SIH && params->num_obs != 108 + 13 * params->n_objects) return HA_E_ARG;
+    if (model->actor_object0 < 0 || model->actor_object0 + params->n_objects > model->n_actors ||
+        model->body_object0 < 0 || model->body_object0 + params->n_objects > model->n_bodies)
+        return HA_E_MODEL;
+    if (model->n_fixed_bodies < 0 || model->n_fixed_bodies > HA_MAX_FIXED_BODIES ||
+        (model->n_fixed_bodies > 0 && (model->body_fixed0 < 0 || model->body_fixed0 + model->n_fixed_bodies > model->n_bodies)))
+        return HA_E_MODEL;
+    if (model->n_links > HA_MAX_LINKS || params->n_objects < 1 || params->n_objects > obj_capacity(fam) ||
         model->n_dofs + 6 * (params->n_objects < 2 ? params->n_objects : 2) > task_row_stride(params->task) ||
         model->n_dofs + 6 * params->n_objects > MAXV || model->n_bodies > MAXB ||
         model->n_static < 0 || model->n_static > HA_MAX_STATIC ||
-        model->n_link_hulls + model->n_pool + 1 > HA_MAX_HULLS)
+        model->n_link_hulls + model->n_pool + model->n_static > HA_MAX_HULLS)
         return HA_E_MODEL;
     for (int k = 0; k < model->n_hulls; k++)
         if (model->hull_nverts[k] > 64 || model->hull_nplanes[k] > 128) return HA_E_MODEL;
@@ -496,6 +551,7 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     h->A = model->n_actors;
     h->B = model->n_bodies;
     h->task = params->task;
+    h->fam = fam;
     h->h_params = *params;
     h->stat_slots = 1;
     HIPCHK(hipMalloc(&h->d_model, sizeof(ha_model_t)));
@@ -503,8 +559,8 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     HIPCHK(hipMemcpy(h->d_model, model, sizeof(ha_model_t), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->d_params, params, sizeof(ha_params_t), hipMemcpyHostToDevice));
     for (int mode : {MODE_STEP, MODE_SIMULATE, MODE_OBSERVE, MODE_RESET})
-        HIPCHK(hipFuncSetAttribute((const void*)kernel_for(h->task, mode), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds_bytes(h->task)));
+        HIPCHK(hipFuncSetAttribute((const void*)kernel_for(h->fam, mode), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds_bytes(h->fam)));
     HIPCHK(hipEventCreate(&h->ev0));
     HIPCHK(hipEventCreate(&h->ev1));
     *out = h;
@@ -537,7 +593,7 @@ static int launch(ha_handle h, int mode, int n_calls, uint32_t flags, int slot, 
     hipStream_t s = (hipStream_t)stream;
     bool rec = h->t_ev && h->t_count < h->t_max;
     (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count] : h->ev0, s);
-    hipLaunchKernelGGL(kernel_for(h->task, mode), dim3(h->N), dim3(64), lds_bytes(h->task), s, h->d_model, h->d_params, h->st,
+    hipLaunchKernelGGL(kernel_for(h->fam, mode), dim3(h->N), dim3(64), lds_bytes(h->fam), s, h->d_model, h->d_params, h->st,
                        h->N, n_calls, flags, slot);
     HIPCHK(hipGetLastError());
     (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count + 1] : h->ev1, s);

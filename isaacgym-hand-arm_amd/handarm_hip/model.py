@@ -19,10 +19,12 @@ import numpy as np
 ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "ur5sih_scene.json")
 ALLEGRO_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "allegro_hand_scene.json")
 KUKA_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "kuka_allegro_scene.json")
+BIN_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "ur5sih_bin_scene.json")
 
 MAX_LINKS, MAX_DOFS, MAX_HULLS, MAX_VERTS, MAX_PLANES = 32, 24, 64, 4096, 8192
 MAX_POOL, MAX_OBJ, MAX_INIT_POSES, MAX_SPLINE_PIECES, N_SPLINES = 32, 8, 4, 8, 8
 MAX_STATIC = 10
+MAX_FIXED_BODIES = 8
 MAX_MPAIRS = 192
 STAT_SIZE = 2 + 2 * MAX_POOL
 DRAW_STRIDE = 80
@@ -78,6 +80,7 @@ class HaModel(C.Structure):
         ("n_bodies", i32), ("body_robot0", i32), ("body_object0", i32), ("body_goal", i32), ("body_table", i32),
         ("n_static", i32), ("static_hull", arr(i32, MAX_STATIC)), ("static_pos", arr(f32, MAX_STATIC, 3)),
         ("static_quat", arr(f32, MAX_STATIC, 4)), ("static_half", arr(f32, MAX_STATIC, 3)),
+        ("n_fixed_bodies", i32), ("body_fixed0", i32), ("body_fixed_pose", arr(f32, MAX_FIXED_BODIES, 7)),
     ]
 
 
@@ -168,8 +171,15 @@ def null_fields(task):
 
 
 def load_scene(path=ASSET):
+    """Scene JSON; an overlay scene names its base with "extends" (same directory) and replaces its keys."""
     with open(path) as f:
-        return json.load(f)
+        scene = json.load(f)
+    base = scene.pop("extends", None)
+    if base:
+        merged = load_scene(os.path.join(os.path.dirname(path), base))
+        merged.update(scene)
+        return merged
+    return scene
 
 
 # links whose hulls may touch the table (the base-mounted shoulder/upper arm sit on it and would
@@ -262,6 +272,13 @@ def build_model(scene, pool_names=None):
                                       body_table=L + 1)
     for k, v in lay.items():
         setattr(m, k, v)
+    # fixed bodies with a model pose (table-with-hole links, bin: multi_object.py:626-637)
+    fixed = scene.get("fixed_bodies", [])
+    assert len(fixed) <= MAX_FIXED_BODIES
+    m.n_fixed_bodies = len(fixed)
+    m.body_fixed0 = scene.get("body_fixed0", -1) if fixed else -1
+    for k, pose in enumerate(fixed):
+        m.body_fixed_pose[k][:] = pose
     # derived topology for the level-synchronous wave kernels
     level = []
     for i, l in enumerate(links):
@@ -431,6 +448,12 @@ def kuka_env_tables(num_envs, scene, c):
     return scales, offs
 
 
+def ur5sih_num_obs(n_objects):
+    """Ur5Sih observation size: 80 + 13 per object + 28 (object_pos 3 and object_bounding_box 10 per object,
+    multi_object.py:128,245; 147 at the default 3 objects)."""
+    return 108 + 13 * n_objects
+
+
 def build_params(cfg=None, task=None):
     want = task if task is not None else (cfg or {}).get("task")
     c = dict(ALLEGRO_TASK if want == TASK_ALLEGRO_HAND else (ALLEGRO_KUKA_TASK if want == TASK_ALLEGRO_KUKA
@@ -466,7 +489,7 @@ def build_params(cfg=None, task=None):
     p.dr_act_noise = c.get("dr_act_noise", 0.05)
     p.task = c.get("task", TASK_UR5SIH)
     p.num_actions = c.get("num_actions", 11)
-    p.num_obs = c.get("num_obs", 147)
+    p.num_obs = c.get("num_obs", ur5sih_num_obs(int(c["n_objects"])))
     if p.task == TASK_ALLEGRO_HAND:
         for k in ["dist_reward_scale", "rot_reward_scale", "rot_eps", "action_penalty_scale", "success_tolerance",
                   "reach_goal_bonus", "fall_dist", "fall_penalty", "max_consecutive_successes", "av_factor",

@@ -26,10 +26,20 @@ from ..torch_utils import randomize_rotation, torch_rand_float
 OBSERVATIONS = ["ur5_joint_pos", "ur5_flange_pose", "sih_fingertip_pos", "sih_fingertip_quat", "sih_fingertip_linvel",
                 "dof_position_targets", "object_pos", "object_bounding_box", "target_object_bounding_box",
                 "sih_fingertip_to_target_object_pos", "target_object_to_goal_pos"]
-OBS_SIZES = [6, 7, 15, 20, 15, 17, 9, 30, 10, 15, 3]
+OBS_SIZES = [6, 7, 15, 20, 15, 17, 9, 30, 10, 15, 3]     # at the default 3 objects (see obs_sizes)
 ACTIONS = ["ur5_relative_joint_pos", "sih_smoothed_relative_servo_pos"]
 REWARD_TERMS = ["reaching", "lifting", "goal", "success"]
 DEFAULT_OBJECTS = ["015_peach", "005_tomato_soup_can", "006_mustard_bottle"]   # Ur5SihMultiObject.yaml:11
+
+
+def obs_sizes(n_objects):
+    """Observation block sizes for n objects (object_pos 3 and object_bounding_box 10 per object,
+    multi_object.py:128,245)."""
+    return [6, 7, 15, 20, 15, 17, 3 * n_objects, 10 * n_objects, 10, 15, 3]
+
+
+# no_bin extent (multi_object.py:421-423) + bin.pos: the drop-init in-bin test without a bin
+NO_BIN_EXTENT = [[0.03, 0.28, 0.5], [0.53, 0.78, 0.7]]
 
 
 class Box:
@@ -83,7 +93,16 @@ class Ur5SihMultiObjectManipulation:
         if rew:
             for k in REWARD_TERMS:
                 task_cfg["reward_" + k] = float(rew.get(k, 0.0))
-        self.sim = HandArmSim(self.num_environments, sim_device, task_cfg=task_cfg, pool_names=objects)
+        # bin.asset (Ur5SihMultiObject.yaml:21-24): 'no_bin' (default) or 'hard_bin', the bin-picking scene of
+        # BASELINE config 5 (table with a hole, the tote as static boxes; tools/build_model.py --bin)
+        self.bin_asset = str(_get(cfg, "bin.asset", "no_bin"))
+        if self.bin_asset not in ("no_bin", "hard_bin"):
+            raise ValueError(f"bin.asset {self.bin_asset!r}: this build ships 'no_bin' and 'hard_bin'")
+        scene = HM.load_scene(HM.BIN_ASSET if self.bin_asset == "hard_bin" else HM.ASSET)
+        if len(objects) < self.num_objects:      # multi_object.py:567-568
+            raise ValueError("Number of objects per environment cannot be larger that the total number of objects used.")
+        self.scene = scene
+        self.sim = HandArmSim(self.num_environments, sim_device, task_cfg=task_cfg, scene=scene, pool_names=objects)
         self.task_cfg = self.sim.cfg
         self.objects = objects
         t = self.sim.t
@@ -119,7 +138,8 @@ class Ur5SihMultiObjectManipulation:
         self.actions_buf = t["actions"]
         self.reset_buf.fill_(1)
         self.states_buf = torch.zeros((N, 0), device=self.device)
-        self.num_observations = sum(OBS_SIZES)
+        sizes = obs_sizes(self.num_objects)
+        self.num_observations = sum(sizes)
         self.num_teacher_observations = self.num_observations
         self.num_states = 0
         self.num_actions = 11
@@ -127,7 +147,7 @@ class Ur5SihMultiObjectManipulation:
         self.teacher_obs_space = self.obs_space
         self.state_space = Box(np.zeros(0), np.zeros(0))
         self.act_space = Box(-np.ones(self.num_actions), np.ones(self.num_actions))
-        start = np.cumsum([0] + OBS_SIZES)
+        start = np.cumsum([0] + sizes)
         self.observations_start_end = {n: (int(start[i]), int(start[i + 1])) for i, n in enumerate(OBSERVATIONS)}
         self.teacher_observations_start_end = dict(self.observations_start_end)
         self.extras = {}
@@ -136,13 +156,16 @@ class Ur5SihMultiObjectManipulation:
         self.control_steps = 0
         self.total_train_env_frames = 0
         self.dt = self.sim.params.dt
-        # actor layout: goal 0, robot 1, table 2, objects 3.. (multi_object.py:562-663)
+        # actor layout: goal 0, robot 1, table 2, [bin 3,] objects (multi_object.py:562-663)
+        m = self.sim.model
+        self.actor_object0 = a0 = m.actor_object0
         ar = torch.arange(N, dtype=torch.int32, device=self.device)
-        self.goal_actor_indices = ar * A
-        self.ur5sih_actor_indices = ar * A + 1
-        self.object_actor_indices = ar[:, None] * A + 3 + torch.arange(self.num_objects, dtype=torch.int32,
-                                                                          device=self.device)[None]
-        self.object_actor_env_indices = [3 + i for i in range(self.num_objects)]
+        self.goal_actor_indices = ar * A + m.actor_goal
+        self.ur5sih_actor_indices = ar * A + m.actor_robot
+        self.object_actor_indices = ar[:, None] * A + a0 + torch.arange(self.num_objects, dtype=torch.int32,
+                                                                           device=self.device)[None]
+        self.object_actor_env_indices = [a0 + i for i in range(self.num_objects)]
+        self.bin_extent = scene.get("bin_extent", NO_BIN_EXTENT)
         # per-env object subset: random.sample of the pool (multi_object.py:569)
         pool = list(range(len(objects)))
         idx = [random.sample(pool, self.num_objects) for _ in range(N)]
@@ -150,9 +173,11 @@ class Ur5SihMultiObjectManipulation:
         self.object_indices = t["object_indices"]
         # initial actor poses (create_actor start poses)
         rs = self.root_state.view(N, A, 13)
-        rs[:, 1, 0:3] = torch.tensor(self.sim.model.base_pos[:], device=self.device)
-        rs[:, 2, 0:3] = torch.tensor(self.sim.model.table_pos[:], device=self.device)
-        rs[:, 3:, 0:3] = torch.tensor([0.0, 0.0, 0.5], device=self.device)   # ObjectAsset.start_pose
+        rs[:, m.actor_robot, 0:3] = torch.tensor(m.base_pos[:], device=self.device)
+        statics = scene.get("static_actors") or [{"actor": m.actor_table, "pose": list(m.table_pos) + [0, 0, 0, 1]}]
+        for sa in statics:                                                    # table (and bin) start poses
+            rs[:, sa["actor"], 0:7] = torch.tensor(sa["pose"], dtype=torch.float32, device=self.device)
+        rs[:, a0:a0 + self.num_objects, 0:3] = torch.tensor([0.0, 0.0, 0.5], device=self.device)   # ObjectAsset.start_pose
         self.dof_pos[:] = torch.tensor(self.sim.params.reset_pose[:D], device=self.device)
         t["sim_targets"].copy_(self.dof_pos)
         self._sync_obs_cache()      # observables' post_step in ConfigurableVecTask.__init__
@@ -224,8 +249,8 @@ class Ur5SihMultiObjectManipulation:
 
     # ------------------------------------------------------------------ internals
     def _sync_obs_cache(self):
-        n, a = self.num_envs, self.num_actors
-        self.sim.t["obs_cache"].copy_(self.root_state.view(n, a, 13)[:, 3:, 0:7])
+        n, a, a0 = self.num_envs, self.num_actors, self.actor_object0
+        self.sim.t["obs_cache"].copy_(self.root_state.view(n, a, 13)[:, a0:a0 + self.num_objects, 0:7])
 
     def _random_object_pos(self, n, key):
         c = self.task_cfg
@@ -243,17 +268,19 @@ class Ur5SihMultiObjectManipulation:
         """First reset: find initial object poses by dropping (multi_object_manipulation.py:36-61, 93-173)."""
         N, A, n_obj = self.num_envs, self.num_actors, self.num_objects
         P = self.num_initial_poses
-        rs = self.root_state.view(N, A, 13)
+        rs = self.root_state.view(N, A, 13)[:, self.actor_object0:self.actor_object0 + n_obj]   # the object rows
         self._reset_ur5sih(self.task_cfg["bringup_pose"])
-        bin_lo = torch.tensor([0.03, 0.28, 0.5], device=self.device)     # no_bin extent + bin.pos (multi_object.py:423)
-        bin_hi = torch.tensor([0.53, 0.78, 0.7], device=self.device)
+        # objects_in_bin extent (multi_object.py:705-718): no_bin default or the bin's bin_info.yaml + bin.pos
+        bin_lo = torch.tensor(self.bin_extent[0], device=self.device)
+        bin_hi = torch.tensor(self.bin_extent[1], device=self.device)
+        bin_mid = 0.5 * (bin_lo + bin_hi)
         pos_init = self.sim.t["object_pos_initial"]
         quat_init = self.sim.t["object_quat_initial"]
         for p in range(P):
             enabled = torch.zeros((N, n_obj), dtype=torch.uint8, device=self.device)
             self.sim.set_object_collisions(enabled)
-            rs[:, 3:, 0:3] = torch.tensor([1.1, 0.0, 0.5], device=self.device)        # _init_object_poses
-            rs[:, 3:, 7:13] = 0.0
+            rs[:, :, 0:3] = torch.tensor([1.1, 0.0, 0.5], device=self.device)        # _init_object_poses
+            rs[:, :, 7:13] = 0.0
             self.sim.simulate(1)
             in_bin = torch.zeros((N, n_obj), dtype=torch.bool, device=self.device)
             rounds = 0
@@ -264,12 +291,11 @@ class Ur5SihMultiObjectManipulation:
                     print(f"[handarm_hip] drop init: {int((~in_bin).sum())} objects outside the bin extent after "
                           f"{rounds} rounds; placing them upright above the bin centre", file=sys.stderr, flush=True)
                     bad = (~in_bin).nonzero(as_tuple=False)
-                    xy = torch.tensor([0.28, 0.53], device=self.device) + 0.1 * (
-                        torch.rand((len(bad), 2), device=self.device) - 0.5)
-                    rs[bad[:, 0], 3 + bad[:, 1], 0:2] = xy
-                    rs[bad[:, 0], 3 + bad[:, 1], 2] = 0.65
-                    rs[bad[:, 0], 3 + bad[:, 1], 3:7] = torch.tensor([0.0, 0.0, 0.0, 1.0], device=self.device)
-                    rs[bad[:, 0], 3 + bad[:, 1], 7:13] = 0.0
+                    xy = bin_mid[0:2] + 0.1 * (torch.rand((len(bad), 2), device=self.device) - 0.5)
+                    rs[bad[:, 0], bad[:, 1], 0:2] = xy
+                    rs[bad[:, 0], bad[:, 1], 2] = 0.65        # above the table top and the bin rim
+                    rs[bad[:, 0], bad[:, 1], 3:7] = torch.tensor([0.0, 0.0, 0.0, 1.0], device=self.device)
+                    rs[bad[:, 0], bad[:, 1], 7:13] = 0.0
                     self.sim.simulate(self.task_cfg["drop_num_steps"])
                     break
                 rounds += 1
@@ -280,19 +306,19 @@ class Ur5SihMultiObjectManipulation:
                     self.sim.set_object_collisions(enabled)
                     env_ids = (~in_bin[:, i]).nonzero(as_tuple=False).squeeze(-1)
                     if len(env_ids) > 0:
-                        rs[env_ids, 3 + i, 0:3] = self._random_object_pos(len(env_ids), "drop")
+                        rs[env_ids, i, 0:3] = self._random_object_pos(len(env_ids), "drop")
                         rf = torch_rand_float(-1.0, 1.0, (len(env_ids), 2), device=self.device)
-                        rs[env_ids, 3 + i, 3:7] = randomize_rotation(rf[:, 0], rf[:, 1])
-                        rs[env_ids, 3 + i, 7:13] = 0.0
+                        rs[env_ids, i, 3:7] = randomize_rotation(rf[:, 0], rf[:, 1])
+                        rs[env_ids, i, 7:13] = 0.0
                         self.sim.simulate(self.task_cfg["drop_num_steps"])
-                obj_pos = rs[:, 3:, 0:3]
+                obj_pos = rs[:, :, 0:3]
                 in_bin = ((obj_pos >= bin_lo) & (obj_pos <= bin_hi)).all(-1)
             for _ in range(600):                                                    # settle
                 self.sim.simulate(1)
-                if bool((rs[:, 3:, 7:10].norm(dim=2).max(dim=1).values < 0.01).all()):
+                if bool((rs[:, :, 7:10].norm(dim=2).max(dim=1).values < 0.01).all()):
                     break
-            pos_init[:, p] = rs[:, 3:, 0:3]
-            quat_init[:, p] = rs[:, 3:, 3:7]
+            pos_init[:, p] = rs[:, :, 0:3]
+            quat_init[:, p] = rs[:, :, 3:7]
             self._sync_obs_cache()
         self.objects_dropped = True
 

@@ -29,9 +29,11 @@
 
 #include "../include/handarm_abi.h"
 
-#define MAXC 21          /* contacts per env (3 rows each -> 63 rows + limit rows <= 64) */
-#define MAXR 64
+#define MAXC HA_MAX_CONTACTS   /* contact list capacity; a handle uses 21 (<= 3 objects) or 42 (clutter) */
+#define MAXR (3 * MAXC)
 #define NOBJ HA_MAX_OBJ
+#define MAXB 48                  /* rigid bodies per env (ha_physics.h MAXB) */
+#define MAXV (HA_MAX_DOFS + 6 * NOBJ)
 
 typedef struct { float x, y, z; } v3;
 static v3 V(float x, float y, float z) { v3 r = {x, y, z}; return r; }
@@ -106,8 +108,8 @@ static void inert_apply(const sinert* I, twist t, v3* n, v3* f) {
 
 typedef struct {
     int nr;                 /* rows */
-    float J[MAXR][HA_MAX_DOFS + 6 * NOBJ];
-    float Y[MAXR][HA_MAX_DOFS + 6 * NOBJ];
+    float J[MAXR][MAXV];
+    float Y[MAXR][MAXV];
     float vt[MAXR];         /* target velocity */
     float lo[MAXR], hi[MAXR];
     int fric_of[MAXR];      /* normal row index for friction rows, -1 otherwise */
@@ -124,6 +126,7 @@ struct hao_s {
     ha_model_t m;
     ha_params_t p;
     int N, A, B, D, NO;
+    int maxc;     /* contact capacity of the device kernel family (handarm_hip.hip family_of) */
 };
 typedef struct hao_s* hao_handle;
 
@@ -142,7 +145,7 @@ typedef struct {
     float osc[NOBJ][3];             /* per-env object dimension scale (ha_state_t.object_scale) */
     int oscaled[NOBJ];
     v3 ofx[NOBJ];                   /* world force on the object COM for this call (object_force) */
-    float cforce[1 + HA_MAX_LINKS + 1 + NOBJ][3];
+    float cforce[MAXB][3];
     float dforce[HA_MAX_DOFS];      /* joint force of the last substep: (drive + lower - upper impulse) / h */
     const float* dr;                /* this env's DR row (HA_DR_*) or NULL (ha_physics.h SimCtx::dr) */
 } env_t;
@@ -290,10 +293,13 @@ static void inverse_from_cholesky(const float* Lm, int n, float* Li, float* S) {
 }
 /* The GPU's 64-lane dot product (ha_physics.h wave_sum_rows): a DPP butterfly inside each 16-lane row
  * gives ((x0+x1)+(x2+x3)) + ((x4+x5)+(x6+x7)) + ... as ((Q0+Q1)+(Q2+Q3)), then (R0+R1)+(R2+R3). Lanes
- * beyond n contribute exact zeros. */
+ * beyond n contribute exact zeros. With more than 64 coordinates (bin-picking: 65), lane i also holds
+ * coordinate 64 + i and adds its product to its own first (ha_physics.h vregh). */
 static float wave_dot(const float* a, const float* b, int n) {
     float x[64];
     for (int i = 0; i < 64; i++) x[i] = i < n ? a[i] * b[i] : 0.0f;
+    if (n > 64)
+        for (int i = 0; i < 64; i++) x[i] = x[i] + (64 + i < n ? a[64 + i] * b[64 + i] : 0.0f * 0.0f);
     float R[4];
     for (int r = 0; r < 4; r++) {
         float Q[4];
@@ -489,24 +495,24 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
         int ho = m->pool_hull[e->pool[o]];
         const float* so = env_scale(e, o);
         pose_t Po = {sub(e->oc[o], qrot(e->oq[o], scl(so, ld3(m->pool_com[e->pool[o]])))), e->oq[o]};
-        collide_ground(m, ho, Po, mg, o, so, out, &nout, MAXC);
+        collide_ground(m, ho, Po, mg, o, so, out, &nout, h->maxc);
         for (int st = 0; st < m->n_static; st++) {
             pose_t Pst = static_pose(m, st);
             if (near_box(m->static_half[st], Pst, add(Po.p, qrot(Po.q, scl(so, ld3(m->hull_center[ho])))),
                          scl_r(so, m->hull_radius[ho]) + mg))
-                collide_hulls(m, ho, Po, m->static_hull[st], Pst, mg, o, -1, so, NULL, out, &nout, MAXC);
+                collide_hulls(m, ho, Po, m->static_hull[st], Pst, mg, o, -1, so, NULL, out, &nout, h->maxc);
         }
         for (int o2 = o + 1; o2 < h->NO; o2++) {
             if (!e->coll[o2]) continue;
             int h2 = m->pool_hull[e->pool[o2]];
             const float* s2 = env_scale(e, o2);
             pose_t P2 = {sub(e->oc[o2], qrot(e->oq[o2], scl(s2, ld3(m->pool_com[e->pool[o2]])))), e->oq[o2]};
-            collide_hulls(m, ho, Po, h2, P2, mg, o, o2, so, s2, out, &nout, MAXC);
+            collide_hulls(m, ho, Po, h2, P2, mg, o, o2, so, s2, out, &nout, h->maxc);
         }
         for (int k = 0; k < m->n_link_hulls; k++) {
             int L = m->hull_link[k];
             pose_t PL = {e->lp[L], e->lq[L]};
-            collide_hulls(m, k, PL, ho, Po, mg, 100 + L, o, NULL, so, out, &nout, MAXC);
+            collide_hulls(m, k, PL, ho, Po, mg, 100 + L, o, NULL, so, out, &nout, h->maxc);
         }
     }
     for (int k = 0; k < m->n_link_hulls; k++) {
@@ -516,7 +522,7 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
         for (int st = 0; st < m->n_static; st++) {
             pose_t Pst = static_pose(m, st);
             if (near_box(m->static_half[st], Pst, add(PL.p, qrot(PL.q, ld3(m->hull_center[k]))), m->hull_radius[k] + mg))
-                collide_hulls(m, k, PL, m->static_hull[st], Pst, mg, 100 + L, -1, NULL, NULL, out, &nout, MAXC);
+                collide_hulls(m, k, PL, m->static_hull[st], Pst, mg, 100 + L, -1, NULL, NULL, out, &nout, h->maxc);
         }
     }
     return nout;
@@ -588,7 +594,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
     cholesky(M, D);
     inverse_from_cholesky(M, D, Li, Minv);
     /* free motion: velocity-product forces only (drives are constraint rows of the PGS below) */
-    float v[HA_MAX_DOFS + 6 * NOBJ];
+    float v[MAXV];
     for (int i = 0; i < D; i++) {
         float acc = 0.0f;
         for (int j = 0; j < D; j++) acc += Minv[i * D + j] * (-hdt * C[j]);
@@ -845,6 +851,10 @@ static void store_env(const hao_handle h, ha_state_t* S, int env, env_t* e) {
         st3(b, e->lp[i]); stq(b + 3, e->lq[i]); st3(b + 7, lin); st3(b + 10, Vl[i].w);
     }
     if (m->body_table >= 0) memcpy(bs + m->body_table * 13, rs + m->actor_table * 13, 13 * sizeof(float));
+    for (int k = 0; k < m->n_fixed_bodies; k++) {      /* fixed bodies: model pose, zero velocity */
+        float* b = bs + (m->body_fixed0 + k) * 13;
+        for (int t = 0; t < 13; t++) b[t] = t < 7 ? m->body_fixed_pose[k][t] : 0.0f;
+    }
     for (int o = 0; o < h->NO; o++)
         memcpy(bs + (m->body_object0 + o) * 13, rs + (m->actor_object0 + o) * 13, 13 * sizeof(float));
     for (int b = 0; b < B; b++)
@@ -861,6 +871,7 @@ hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int nu
     h->A = model->n_actors;
     h->D = model->n_dofs;
     h->B = model->n_bodies;
+    h->maxc = (params->task == HA_TASK_UR5SIH && params->n_objects > 3) ? 2 * 21 : 21;
     return h;
 }
 void hao_destroy(hao_handle h) { free(h); }

@@ -225,12 +225,14 @@ OBS_LAYOUT = [("ur5_joint_pos", 6), ("ur5_flange_pose", 7), ("sih_fingertip_pos"
 
 
 def observations(root, body, dof, targets, goal_pos, target_idx, bbox_pos, bbox_quat, bbox_ext,
-                 prev_object_pose):
+                 prev_object_pose, object_actors=None):
     """post_step callbacks + compute_observations (Ur5SihMultiObjectManipulation.yaml:24-26,43-44).
 
     root (N,6,13) body (N,34,13) dof (N,17,2) targets (N,17) goal_pos (N,3) target_idx (N,) int
     bbox_pos (N,3,3) bbox_quat (N,3,4) bbox_ext (N,3,3); prev_object_pose (N,3,7) = the object
     pos/quat cached by the PREVIOUS post_step refresh. Returns obs (N,147), object_bbox (N,3,10).
+    With n objects (object_actors = their actor rows, e.g. 4..11 in the bin scene) the object blocks grow
+    to 3n and 10n: obs (N, 108 + 13 n).
 
     Reference quirk reproduced: the observable refresh order is the reversed networkx topological
     sort (observables.py:231-243) and ``object_bounding_box`` declares no ``requires``, so its
@@ -240,12 +242,14 @@ def observations(root, body, dof, targets, goal_pos, target_idx, bbox_pos, bbox_
     """
     n = root.shape[0]
     ar = np.arange(n)
-    object_pos = root[:, OBJECT_ACTORS, 0:3]
-    bbox = np.zeros((n, 3, 10), F)
+    actors = np.asarray(OBJECT_ACTORS if object_actors is None else object_actors)
+    no = len(actors)
+    object_pos = root[:, actors, 0:3]
+    bbox = np.zeros((n, no, 10), F)
     bbox[..., 0:3] = prev_object_pose[..., 0:3] + quat_apply(prev_object_pose[..., 3:7], bbox_pos)  # :771
     bbox[..., 3:7] = quat_mul(prev_object_pose[..., 3:7], bbox_quat)                              # :772
     bbox[..., 7:10] = bbox_ext
-    target_pos = root[ar, np.asarray(OBJECT_ACTORS)[target_idx], 0:3]        # multi_object.py:214
+    target_pos = root[ar, actors[target_idx], 0:3]        # multi_object.py:214
     tips = body[:, FINGERTIP_BODIES]
     parts = [dof[:, 0:6, 0],
              body[:, FLANGE_BODY, 0:7],
@@ -253,8 +257,8 @@ def observations(root, body, dof, targets, goal_pos, target_idx, bbox_pos, bbox_
              tips[..., 3:7].reshape(n, 20),
              tips[..., 7:10].reshape(n, 15),
              targets,
-             object_pos.reshape(n, 9),
-             bbox.reshape(n, 30),
+             object_pos.reshape(n, 3 * no),
+             bbox.reshape(n, 10 * no),
              bbox[ar, target_idx],
              (target_pos[:, None, :] - tips[..., 0:3]).reshape(n, 15),
              goal_pos - target_pos]
@@ -271,14 +275,15 @@ def norm3(x):
     return np.sqrt(np.sum(x * x, -1, dtype=F)).astype(F)
 
 
-def reward(root, body, goal_pos, target_idx, cfg_idx, object_pos_initial):
+def reward(root, body, goal_pos, target_idx, cfg_idx, object_pos_initial, object_actors=None):
     """_update_rew_buf (multi_object_manipulation.py:237-313) with its helpers :353-387.
 
     Returns rew (N,), goal_reached (N,) bool, per-term rewards dict.
     """
     n = root.shape[0]
     ar = np.arange(n)
-    target_pos = root[ar, np.asarray(OBJECT_ACTORS)[target_idx], 0:3]
+    actors = np.asarray(OBJECT_ACTORS if object_actors is None else object_actors)
+    target_pos = root[ar, actors[target_idx], 0:3]
     dist = norm3(target_pos - goal_pos)
     reached = dist < GOAL_THRESHOLD
     init = object_pos_initial[ar, cfg_idx][ar, target_idx]

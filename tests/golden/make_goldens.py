@@ -111,7 +111,9 @@ class FakeGym:
         return rec
 
 
-def make_task(num_envs, num_initial_poses=1, seed=0):
+def make_task(num_envs, num_initial_poses=1, seed=0, n_objects=None, bin_layout=False):
+    """n_objects / bin_layout: the bin-picking variant (BASELINE config 5): cfg objects.num_objects = n and
+    the actor layout with a bin actor (goal 0, robot 1, table 2, bin 3, objects 4..; multi_object.py:579-644)."""
     mom = refload.load("isaacgymenvs.tasks.hand_arm.task.multi_object_manipulation")
     avt = refload.load("isaacgymenvs.tasks.hand_arm.base.actionable_vec_task")
     obs_mod = refload.load("isaacgymenvs.tasks.hand_arm.utils.observables")
@@ -121,6 +123,8 @@ def make_task(num_envs, num_initial_poses=1, seed=0):
     cfg_task_raw = yaml.safe_load(open(os.path.join(REF_CFG, "Ur5SihMultiObjectManipulation.yaml")))
     cfg_task = wrap(cfg_task_raw)
     cfg_env.objects.drop.num_initial_poses = num_initial_poses
+    if n_objects is not None:
+        cfg_env.objects.num_objects = n_objects
     e = cfg_task_raw["env"]
     obs_list = e["proprioceptive_observations"] + e["object_observations"] + e["task_observations"]
 
@@ -159,15 +163,17 @@ def make_task(num_envs, num_initial_poses=1, seed=0):
     # _create_envs (multi_object.py:477-677): actor order goal, robot, table, objects
     g = torch.Generator().manual_seed(seed)
     n_obj = cfg_env.objects.num_objects
-    t.objects = [FakeObject(o) for o in scene["objects"][:3]]
+    t.objects = [FakeObject(o) for o in scene["objects"][:max(3, n_obj)]]
     t.object_indices = torch.stack([torch.randperm(len(t.objects), generator=g)[:n_obj] for _ in range(num_envs)])
-    t.num_actors, t.num_bodies, t.num_dofs = 3 + n_obj, 1 + len(links) + 1 + n_obj, len(dofs)
+    a0 = 4 if bin_layout else 3
+    n_static_bodies = 6 if bin_layout else 1      # table base_link + 4 walls, bin / the table box
+    t.num_actors, t.num_bodies, t.num_dofs = a0 + n_obj, 1 + len(links) + n_static_bodies + n_obj, len(dofs)
     A = t.num_actors
     t.ur5sih_actor_indices = torch.arange(num_envs, dtype=torch.int32) * A + 1
-    t.object_actor_indices = (torch.arange(num_envs, dtype=torch.int32)[:, None] * A + 3
+    t.object_actor_indices = (torch.arange(num_envs, dtype=torch.int32)[:, None] * A + a0
                               + torch.arange(n_obj, dtype=torch.int32)[None]).to(torch.int32)
     t.goal_actor_indices = torch.arange(num_envs, dtype=torch.int32) * A
-    t.object_actor_env_indices = [3 + i for i in range(n_obj)]
+    t.object_actor_env_indices = [a0 + i for i in range(n_obj)]
     t.goal_actor_env_index = 0
     t.ur5sih_rigid_body_env_indices = list(range(1, 1 + len(links)))
     t.object_configuration_indices = torch.zeros(num_envs, dtype=torch.int64)
@@ -231,8 +237,8 @@ def fill_random_state(t, g):
     t.contact_force[:] = torch.randn(N, B, 3, generator=g)
 
 
-def gen_obs_reward(path, N=16, steps=6, seed=1):
-    t, mom = make_task(N, num_initial_poses=2, seed=seed)
+def gen_obs_reward(path, N=16, steps=6, seed=1, n_objects=None, bin_layout=False):
+    t, mom = make_task(N, num_initial_poses=2, seed=seed, n_objects=n_objects, bin_layout=bin_layout)
     g = torch.Generator().manual_seed(seed + 100)
     n_obj, P = t.cfg_env.objects.num_objects, 2
     t.objects_dropped = True
@@ -380,6 +386,9 @@ def gen_quat(path, M=64, seed=4):
 
 
 if __name__ == "__main__":
+    if "--bin" in sys.argv:     # bin-picking variant only (8 objects, bin actor layout)
+        gen_obs_reward(os.path.join(HERE, "ur5sih_obs_reward_bin8.npz"), n_objects=8, bin_layout=True, seed=11)
+        sys.exit(0)
     gen_quat(os.path.join(HERE, "quat_utils.npz"))
     gen_controller(os.path.join(HERE, "ur5sih_controller.npz"))
     gen_obs_reward(os.path.join(HERE, "ur5sih_obs_reward.npz"))

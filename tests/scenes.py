@@ -103,3 +103,46 @@ def fill_kuka_scene(st, num_envs, lower, upper, reset_pose, scales, table_pos, s
     st["collision_enabled"][:] = 1
     st["object_force"][:] = object_force * rng.standard_normal((N, 1, 3))
     return st
+
+
+def bin_pool_ids(rng, n_envs, n_obj=8, pool=16):
+    """Per-env object subsets: random.sample of the pool (multi_object.py:569)."""
+    return np.stack([rng.permutation(pool)[:n_obj] for _ in range(n_envs)])
+
+
+def fill_bin_scene(st, num_envs, scene, seed=0, n_obj=8, spread=1.0, pool=16):
+    """Bin-picking (BASELINE config 5): the robot near its reset pose and n_obj objects on a 2 x 4 grid inside
+    the tote (bin extent of the scene), lower layer touching the floor, upper layer falling onto it, random
+    orientations and small velocities. Actor layout of the bin scene: goal 0, robot 1, table 2, bin 3,
+    objects 4.."""
+    rng = np.random.default_rng(seed)
+    N = num_envs
+    A = 4 + n_obj
+    lo, hi = np.array(scene["bin_extent"][0]), np.array(scene["bin_extent"][1])
+    rs = st["root_state"].reshape(N, A, 13)
+    rs[:] = 0
+    rs[..., 6] = 1.0
+    rs[:, 0, 0:3] = [0.28, 0.58, 0.8]
+    rs[:, 1, 0:3] = [0.0, 0.0, 0.5]
+    for sa in scene["static_actors"]:
+        rs[:, sa["actor"], 0:7] = sa["pose"]
+    cols = np.linspace(lo[0] + 0.09, hi[0] - 0.09, 2)
+    rows = np.linspace(lo[1] + 0.08, hi[1] - 0.08, 4)
+    for o in range(n_obj):
+        a = 4 + o
+        rs[:, a, 0] = cols[o % 2] + spread * rng.uniform(-0.02, 0.02, N)
+        rs[:, a, 1] = rows[(o // 2) % 4] + spread * rng.uniform(-0.02, 0.02, N)
+        rs[:, a, 2] = lo[2] + 0.06 + 0.1 * (o // 8) + rng.uniform(0.0, 0.03, N)
+        rs[:, a, 3:7] = rand_quat(rng, (N,))
+        rs[:, a, 7:10] = rng.uniform(-0.1, 0.1, (N, 3))
+        rs[:, a, 10:13] = rng.uniform(-0.5, 0.5, (N, 3))
+    ds = st["dof_state"].reshape(N, 17, 2)
+    ds[..., 0] = RESET_POSE + rng.uniform(-0.05, 0.05, (N, 17)).astype(np.float32)
+    ds[:, 6:14, 0] = np.clip(ds[:, 6:14, 0], -1.571, 0.0)
+    ds[:, 14, 0] = np.clip(ds[:, 14, 0], -1.571, 0.0)
+    ds[:, 15:17, 0] = np.clip(ds[:, 15:17, 0], 0.0, 1.571)
+    ds[..., 1] = rng.uniform(-0.3, 0.3, (N, 17))
+    st["sim_targets"][:] = RESET_POSE + rng.uniform(-0.3, 0.3, (N, 17)).astype(np.float32)
+    st["object_indices"][:] = bin_pool_ids(rng, N, n_obj, pool)
+    st["collision_enabled"][:] = 1
+    return st

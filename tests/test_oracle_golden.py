@@ -2,6 +2,7 @@
 import os
 
 import numpy as np
+import pytest
 
 from oracle import task_oracle as O
 
@@ -42,18 +43,27 @@ def test_controller_sequence():
         np.testing.assert_allclose(tgt, d["targets"][s], rtol=1e-6, atol=1e-6)
 
 
-def test_observations_reward_done_sequence():
-    d = load("ur5sih_obs_reward.npz")
+# (fixture, objects, actors, bodies, object actor rows): the default scene and the bin-picking variant
+# (BASELINE config 5: 8 objects, bin actor at 3, objects from actor 4; fixture made by make_goldens.py --bin)
+OBS_CASES = [("ur5sih_obs_reward.npz", 3, 6, 34, [3, 4, 5]),
+             ("ur5sih_obs_reward_bin8.npz", 8, 12, 44, list(range(4, 12)))]
+
+
+@pytest.mark.parametrize("fixture,no,A,B,actors", OBS_CASES, ids=["default3", "bin8"])
+def test_observations_reward_done_sequence(fixture, no, A, B, actors):
+    d = load(fixture)
     steps, n = d["rew"].shape
-    tracker = O.SuccessTracker(3, n)
-    prev = np.zeros((n, 3, 7), np.float32)   # make_task's init refresh saw an all-zero root state
+    tracker = O.SuccessTracker(no, n)
+    prev = np.zeros((n, no, 7), np.float32)   # make_task's init refresh saw an all-zero root state
     for s in range(steps):
-        root = d["root"][s].reshape(n, 6, 13)
-        body = d["body"][s].reshape(n, 34, 13)
+        root = d["root"][s].reshape(n, A, 13)
+        body = d["body"][s].reshape(n, B, 13)
         dof = d["dof"][s].reshape(n, 17, 2)
         obs, bbox = O.observations(root, body, dof, d["targets"][s], d["goal_pos"][s], d["target_idx"][s],
-                                   d["bbox_from_origin_pos"], d["bbox_from_origin_quat"], d["bbox"][s][..., 7:10], prev)
-        prev = root[:, O.OBJECT_ACTORS, 0:7].copy()
+                                   d["bbox_from_origin_pos"], d["bbox_from_origin_quat"], d["bbox"][s][..., 7:10], prev,
+                                   object_actors=actors)
+        assert obs.shape == (n, 108 + 13 * no)
+        prev = root[:, actors, 0:7].copy()
         np.testing.assert_allclose(obs, d["obs"][s], rtol=0, atol=2e-7)
         np.testing.assert_allclose(obs, d["teacher"][s], rtol=0, atol=2e-7)
         progress = d["progress_in"][s] + 1
@@ -62,14 +72,14 @@ def test_observations_reward_done_sequence():
         np.testing.assert_array_equal(reset, d["reset"][s])
         np.testing.assert_array_equal(timeout, d["timeout"][s])
         rew, reached, terms = O.reward(root, body, d["goal_pos"][s], d["target_idx"][s], d["cfg_idx"][s],
-                                       d["object_pos_initial"])
+                                       d["object_pos_initial"], object_actors=actors)
         np.testing.assert_allclose(rew, d["rew"][s], rtol=2e-6, atol=2e-6)
         np.testing.assert_allclose([terms[k].mean() for k in d["reward_terms"]], d["log_terms"][s], rtol=1e-5)
         reached_before = reached | d["reached_in"][s]
         np.testing.assert_array_equal(reached_before, d["reached"][s])
-        log = tracker.update(*O.success_counts(reset, reached_before, d["object_indices"], d["target_idx"][s], 3))
+        log = tracker.update(*O.success_counts(reset, reached_before, d["object_indices"], d["target_idx"][s], no))
         np.testing.assert_allclose(log.get("overall", np.nan), d["log_overall"][s], rtol=1e-6)
-        np.testing.assert_allclose([log.get(i, np.nan) for i in range(3)], d["log_obj"][s], rtol=1e-6)
+        np.testing.assert_allclose([log.get(i, np.nan) for i in range(no)], d["log_obj"][s], rtol=1e-6)
 
 
 def test_reset_steady_state():

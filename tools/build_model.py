@@ -63,6 +63,14 @@ def rpy_to_matrix(r, p, y):
                      [-sp, cp * sr, cp * cr]])
 
 
+def scipy_quat(R):
+    """Rotation matrix -> quaternion exactly as the reference converts the bounding-box frame
+    (scipy Rotation.from_matrix(...).as_quat(), multi_object.py:751-753): same rotation as matrix_to_quat but
+    scipy's sign choice, which the observed bounding-box quaternion (quat_mul with it) inherits."""
+    from scipy.spatial.transform import Rotation
+    return Rotation.from_matrix(np.asarray(R, float)).as_quat()
+
+
 def matrix_to_quat(R):
     """Rotation matrix -> quaternion (x, y, z, w), w >= 0."""
     t = np.trace(R)
@@ -337,7 +345,7 @@ def build_object(name):
     R, ctr, ext = min_volume_obb(reduce_points(v, 256))
     return {"name": name, "mass": mass, "com": com.tolist(),
             "inertia": (I_unit * mass / vol).reshape(-1).tolist(), "hull": hull,
-            "bbox_from_origin_pos": ctr.tolist(), "bbox_from_origin_quat": matrix_to_quat(R).tolist(),
+            "bbox_from_origin_pos": ctr.tolist(), "bbox_from_origin_quat": scipy_quat(R).tolist(),
             "bbox_extents": ext.tolist()}
 
 
@@ -611,7 +619,118 @@ def main():
           f"objects={[o['name'] for o in objects]} -> {OUT} ({os.path.getsize(OUT)} B)")
 
 
+# ----------------------------------------------------------------------------- bin-picking (config C5)
+BIN_OUT = os.path.join(os.path.dirname(__file__), "..", "isaacgym-hand-arm_amd", "handarm_hip", "assets",
+                       "ur5sih_bin_scene.json")
+BIN_POS = (0.28, 0.53, 0.0)                    # Ur5SihMultiObject.yaml bin.pos (z += table_height, multi_object.py:506)
+BIN_QUAT = (0.0, 0.0, -0.707, 0.707)           # bin.quat (gymapi.Quat, normalised by PhysX)
+HARD_BIN_EXTENT = [[-0.18, -0.2975, -0.19], [0.18, 0.2975, 0.065]]   # assets/hand_arm/hard_bin/bin_info.yaml
+
+
+def qrot_np(q, v):
+    x, y, z, w = q
+    u = np.array([x, y, z])
+    v = np.asarray(v, float)
+    t = 2.0 * np.cross(u, v)
+    return v + w * t + np.cross(u, t)
+
+
+def tote_boxes():
+    """Box decomposition of hard_bin/assets/tote.obj (the reference V-HACDs it, multi_object.py:497-504; no
+    V-HACD here, so the tote becomes five boxes): a 1 cm floor under the inner floor (mesh z 0.005) and four
+    1 cm walls whose inner faces run from the inner bottom corner (outer bottom |x| 0.286, |y| 0.163, minus the
+    wall) to the inner top edge of bin_info.yaml (|x| 0.2975, |y| 0.18 in the mesh frame) at the rim (z 0.1955),
+    i.e. tilted outward like the tote. Poses in the bin link frame (collision origin z -0.19, bin.urdf)."""
+    t, zb, zt, zo = 0.01, 0.005, 0.1955, -0.19
+    boxes = [([0.0, 0.0, zb - t / 2 + zo], [0, 0, 0, 1], [0.286, 0.163, t / 2])]
+    for axis, bot, top, length in ((0, 0.286 - t, 0.2975, 0.187), (1, 0.163 - t, 0.18, 0.308)):
+        dz = zt - zb
+        ang = math.atan2(top - bot, dz)
+        half_h = 0.5 * math.hypot(top - bot, dz)
+        for sgn in (1.0, -1.0):
+            up = np.zeros(3)
+            up[axis] = sgn * math.sin(ang)
+            up[2] = math.cos(ang)
+            out = np.zeros(3)                          # outward wall normal (perpendicular to up, in the plane)
+            out[axis] = sgn * math.cos(ang)
+            out[2] = -math.sin(ang)
+            inner_mid = np.zeros(3)
+            inner_mid[axis] = sgn * 0.5 * (bot + top)
+            inner_mid[2] = 0.5 * (zb + zt)
+            c = inner_mid + out * (t / 2)
+            c[2] += zo
+            # local z -> up: rotation about the other horizontal axis
+            rot_axis = [0.0, 1.0, 0.0] if axis == 0 else [1.0, 0.0, 0.0]
+            a = sgn * ang if axis == 0 else -sgn * ang
+            q = quat_axis_angle(rot_axis, a)
+            assert np.allclose(qrot_np(q, [0, 0, 1]), up, atol=1e-9)
+            half = [t / 2, length, half_h] if axis == 0 else [length, t / 2, half_h]
+            boxes.append((c.tolist(), q.tolist(), half))
+    return boxes
+
+
+def table_with_hole_boxes(height, hole_x, hole_y, x_range=(-0.095, 0.655), y_range=(-0.17, 0.93)):
+    """generate_table_with_hole (utils/urdf.py:125-210) as four boxes in the table frame (link origins of its
+    fixed joints); siblings in link-name order like the robot (back, front, left, right wall)."""
+    x0, x1 = x_range
+    y0, y1 = y_range
+    walls = {
+        "front_wall": ([x0 + 0.5 * (hole_x[0] - x0), y0 + 0.5 * (y1 - y0), 0.0], [hole_x[0] - x0, y1 - y0, height]),
+        "back_wall": ([(hole_x[1] + x1) / 2, y0 + 0.5 * (y1 - y0), 0.0], [x1 - hole_x[1], y1 - y0, height]),
+        "right_wall": ([x0 + 0.5 * (x1 - x0), y0 + 0.5 * (hole_y[0] - y0), 0.0], [x1 - x0, hole_y[0] - y0, height]),
+        "left_wall": ([x0 + 0.5 * (x1 - x0), (hole_y[1] + y1) / 2, 0.0], [x1 - x0, y1 - hole_y[1], height]),
+    }
+    return [(n, walls[n][0], [0.5 * v for v in walls[n][1]]) for n in sorted(walls)]
+
+
+def main_bin(n_objects=8):
+    """Ur5SihMultiObject with bin.asset hard_bin (BASELINE config 5): table with a hole
+    under the bin (multi_object.py:535-540), the bin actor (:497-507, 635-637) and n_objects YCB objects per
+    env. Actors: goal 0, robot 1, table 2, bin 3, objects 4.. (creation order, multi_object.py:579-644).
+    Bodies: goal, 29 robot links, table base_link + 4 walls, bin, objects."""
+    base = json.load(open(OUT))
+    L = len(base["robot"]["links"])
+    ext = HARD_BIN_EXTENT
+    hole_x = (ext[0][0] + BIN_POS[0], ext[1][0] + BIN_POS[0])
+    hole_y = (ext[0][1] + BIN_POS[1], ext[1][1] + BIN_POS[1])
+    table_pose = [0.0, 0.0, TABLE_HEIGHT / 2, 0, 0, 0, 1]              # multi_object.py:630
+    qn = np.asarray(BIN_QUAT, float)
+    qn = qn / np.linalg.norm(qn)
+    bin_pos = np.array([BIN_POS[0], BIN_POS[1], BIN_POS[2] + TABLE_HEIGHT])
+    statics, fixed = [], [table_pose]
+    for name, c, half in table_with_hole_boxes(TABLE_HEIGHT, hole_x, hole_y):
+        pos = [c[0], c[1], c[2] + TABLE_HEIGHT / 2]
+        statics.append({"name": "table_" + name, "pos": pos, "quat": [0, 0, 0, 1], "half_extents": half,
+                        "hull": box_hull(half)})
+        fixed.append(pos + [0, 0, 0, 1])
+    for k, (c, q, half) in enumerate(tote_boxes()):
+        pos = (bin_pos + qrot_np(qn, c)).tolist()
+        quat = quat_mul_np(qn, q)
+        statics.append({"name": f"bin_{k}", "pos": pos, "quat": (quat / np.linalg.norm(quat)).tolist(),
+                        "half_extents": half, "hull": box_hull(half)})
+    fixed.append(bin_pos.tolist() + qn.tolist())
+    n_obj = n_objects
+    body_table = 1 + L
+    scene = {
+        "extends": os.path.basename(OUT), "table": None, "statics": statics, "objects_per_env": n_obj,
+        "layout": {"n_actors": 4 + n_obj, "actor_robot": 1, "actor_object0": 4, "actor_goal": 0, "actor_table": 2,
+                   "n_bodies": 1 + L + 5 + 1 + n_obj, "body_robot0": 1, "body_object0": body_table + 6, "body_goal": 0,
+                   "body_table": body_table},
+        "fixed_bodies": fixed, "body_fixed0": body_table,
+        "static_actors": [{"actor": 2, "pose": table_pose}, {"actor": 3, "pose": bin_pos.tolist() + qn.tolist()}],
+        "bin_extent": [[hole_x[0], hole_y[0], ext[0][2] + TABLE_HEIGHT + BIN_POS[2]],    # objects_in_bin
+                       [hole_x[1], hole_y[1], ext[1][2] + TABLE_HEIGHT + BIN_POS[2]]],    # (multi_object.py:705-718)
+        "generator": "tools/build_model.py --bin (reference assets @ /root/reference/assets/hand_arm)",
+    }
+    with open(BIN_OUT, "w") as f:
+        json.dump(scene, f, indent=1)
+    print(f"bin scene: {len(statics)} static boxes, {len(fixed)} fixed bodies, {n_obj} objects/env, "
+          f"bin extent {scene['bin_extent']} -> {BIN_OUT}")
+
+
 if __name__ == "__main__":
+    if "--bin" in sys.argv:
+        sys.exit(main_bin())
     if "--allegro" in sys.argv:
         sys.exit(main_allegro())
     sys.exit(main_kuka() if "--kuka" in sys.argv else main())

@@ -37,18 +37,24 @@ if __name__ == "__main__":
         print(f"{label}: contacts/substep {buf[8] / max(buf[9], 1):.2f}", flush=True)
         print("  " + "  ".join(f"{PHASES[i]} {100.0 * buf[i] / tot:5.1f}%" for i in range(8)), flush=True)
         sub = max(buf[9], 1)
-        for k, name in enumerate(["obj-ground", "obj-table", "obj-obj", "link-obj", "link-table"]):
+        for k, name in enumerate(["obj-ground", "obj-static", "obj-obj", "link-obj", "link-static"]):
             print(f"    narrow {name:10s}: {buf[15 + k] / sub:6.2f} pairs/substep, {buf[20 + k] / sub:6.2f} with contacts, "
                   f"{100.0 * buf[10 + k] / tot:5.1f}% of substep cycles", flush=True)
         print("    hull-hull split: " + "  ".join(f"{nm} {100.0 * buf[25 + i] / tot:5.1f}%" for i, nm in
               enumerate(["setup", "SAT A", "SAT B", "clip", "emit"])), flush=True)
 
-    if "--bench-scene" in sys.argv or "--kuka" in sys.argv:
+    if "--bench-scene" in sys.argv or "--kuka" in sys.argv or "--bin" in sys.argv:
         # the bench workload: VecTask after its first (reset) steps, random actions
         from handarm_hip.tasks import AllegroKuka, Ur5SihMultiObjectManipulation
         if "--kuka" in sys.argv:
             n = int(args[0]) if args else 4096
             env = AllegroKuka({"env": {"numEnvs": n}, "seed": 42}, "cuda:0", "cuda:0")
+        elif "--bin" in sys.argv:       # bench --task binpick (config 5 shard)
+            from handarm_hip import model as HM
+            pool = [o["name"] for o in HM.load_scene()["objects"]]
+            env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}, "seed": 42, "bin": {"asset": "hard_bin"},
+                                                 "objects": {"num_objects": 8, "dataset": {"ycb": pool}}},
+                                                "cuda:0", "cuda:0")
         else:
             env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}, "seed": 42}, "cuda:0", "cuda:0")
         env.reset()
