@@ -211,25 +211,40 @@ HD void fk(SimCtx& c) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     int lane = c.lane;
+    // lane i owns link i: its model constants and its joint rotation (one sincos per lane) are loaded and
+    // computed before the level chain, so each level only waits on its parent's LDS pose
+    bool own = lane < c.L;
+    int lev = -1, par = 0, d = -1;
+    f3 op = mk3(0, 0, 0), ax = mk3(0, 0, 0);
+    qf oq = qf{0, 0, 0, 1}, qa = qf{0, 0, 0, 1};
+    if (own) {
+        lev = m.link_level[lane];
+        par = m.link_parent[lane];
+        d = m.link_dof[lane];
+        op = ld3(m.link_origin_pos[lane]);
+        oq = ldq(m.link_origin_quat[lane]);
+        if (d >= 0) {
+            ax = ld3(m.link_axis[lane]);
+            qa = qaxis(ax, s.q[d]);
+        }
+    }
     if (lane == 0) {
         st3(s.lp[0], ld3(m.base_pos));
         stq(s.lq[0], ldq(m.base_quat));
     }
     wsync();
-    for (int lev = 1; lev <= m.max_level; lev++) {
-        if (lane < c.L && m.link_level[lane] == lev) {
-            int i = lane, par = m.link_parent[i];
+    for (int l = 1; l <= m.max_level; l++) {
+        if (lev == l) {
             qf pq = ldq(s.lq[par]);
-            f3 p = ld3(s.lp[par]) + qrot(pq, ld3(m.link_origin_pos[i]));
-            qf r = qmul(pq, ldq(m.link_origin_quat[i]));
-            int d = m.link_dof[i];
+            f3 p = ld3(s.lp[par]) + qrot(pq, op);
+            qf r = qmul(pq, oq);
             if (d >= 0) {
-                r = qmul(r, qaxis(ld3(m.link_axis[i]), s.q[d]));
-                st3(s.ax[d], qrot(r, ld3(m.link_axis[i])));
+                r = qmul(r, qa);
+                st3(s.ax[d], qrot(r, ax));
                 st3(s.an[d], p);
             }
-            st3(s.lp[i], p);
-            stq(s.lq[i], r);
+            st3(s.lp[lane], p);
+            stq(s.lq[lane], r);
         }
         wsync();
     }
@@ -285,16 +300,24 @@ HD void dynamics(SimCtx& c) {
     // zero M
     for (int k = lane; k < D * D; k += 64) s.u.pd.M[k] = 0.0f;
     wsync();
-    // twists / bias accelerations, level by level
+    // twists / bias accelerations, level by level (per-lane link constants and joint axis read once)
+    int my_lev = own ? m.link_level[lane] : -1;
+    int my_par = own ? m.link_parent[lane] : 0;
+    int my_d = own ? m.link_dof[lane] : -1;
+    f3 my_sw = mk3(0, 0, 0), my_sv = mk3(0, 0, 0);
+    if (my_d >= 0) {
+        f3 axd = ld3(s.ax[my_d]), and_ = ld3(s.an[my_d]);
+        float qd = s.qd[my_d];
+        my_sw = axd * qd;
+        my_sv = cross3(and_, axd) * qd;
+    }
     for (int lev = 1; lev <= m.max_level; lev++) {
-        if (own && m.link_level[lane] == lev) {
-            int i = lane, par = m.link_parent[i], d = m.link_dof[i];
+        if (my_lev == lev) {
+            int i = lane, par = my_par, d = my_d;
             f3 vw = ld3(&s.u.pd.dyn.Vl[par][0]), vv = ld3(&s.u.pd.dyn.Vl[par][3]);
             f3 aw = ld3(&s.u.pd.dyn.Al[par][0]), av = ld3(&s.u.pd.dyn.Al[par][3]);
             if (d >= 0) {
-                f3 axd = ld3(s.ax[d]), and_ = ld3(s.an[d]);
-                float qd = s.qd[d];
-                f3 sw = axd * qd, sv = cross3(and_, axd) * qd;
+                f3 sw = my_sw, sv = my_sv;
                 vw = vw + sw;
                 vv = vv + sv;
                 aw = aw + cross3(vw, sw);
@@ -319,8 +342,8 @@ HD void dynamics(SimCtx& c) {
     wsync();
     // backward accumulation of forces and composite inertia, deepest level first
     for (int lev = m.max_level; lev >= 1; lev--) {
-        if (own && m.link_level[lane] == lev) {
-            int i = lane, par = m.link_parent[i];
+        if (my_lev == lev) {
+            int i = lane, par = my_par;
 #pragma unroll
             for (int k = 0; k < 6; k++) atomicAdd(&s.u.pd.dyn.Fl[par][k], s.u.pd.dyn.Fl[i][k]);
 #pragma unroll
@@ -448,20 +471,20 @@ HD f3 inv_scale(const SimCtx& c, int b) {
 HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int b) {
     EnvLDS& s = *c.s;
     int lane = c.lane;
-    int idx[4];
-    int k = 0;
+    // the chosen lanes live in scalars, never in an indexed private array (which would go to scratch)
     float v0 = valid ? sep : 3.0e38f;
     int i0 = valid ? lane : 1 << 20;
     wave_argmin(v0, i0);
     if (i0 >= (1 << 20)) return;
-    idx[k++] = i0;
+    int k = 1, j1 = 0, j2 = 0, j3 = 0;        // chosen lanes of points 1..3 (valid below k)
     f3 p0 = mk3(bcast(pt.x, i0), bcast(pt.y, i0), bcast(pt.z, i0));
     f3 dd = pt - p0;
     float v1 = valid ? dot3(dd, dd) : -1.0f;
     int i1 = lane;
     wave_argmax(v1, i1);
     if (v1 > 1e-12f) {
-        idx[k++] = i1;
+        j1 = i1;
+        k = 2;
         f3 p1 = mk3(bcast(pt.x, i1), bcast(pt.y, i1), bcast(pt.z, i1));
         f3 e = p1 - p0;
         float sv = dot3(cross3(e, pt - p0), n);
@@ -471,20 +494,24 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
         float v3 = valid ? sv : 3.0e38f;
         int i3 = lane;
         wave_argmin(v3, i3);
-        if (v2 > 1e-12f) idx[k++] = i2;
-        if (v3 < -1e-12f) idx[k++] = i3;
+        bool h2 = v2 > 1e-12f, h3 = v3 < -1e-12f;
+        j2 = h2 ? i2 : i3;
+        j3 = i3;
+        k = 2 + (h2 ? 1 : 0) + (h3 ? 1 : 0);
     }
     // gather the chosen points to every lane, lane 0 appends
     f3 P[4];
     float S[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
-        int src = t < k ? idx[t] : 0;
+        int src = t == 0 ? i0 : (t < k ? (t == 1 ? j1 : (t == 2 ? j2 : j3)) : 0);
         P[t] = mk3(bcast(pt.x, src), bcast(pt.y, src), bcast(pt.z, src));
         S[t] = bcast(sep, src);
     }
     if (lane == 0) {
-        for (int t = 0; t < k; t++) {
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            if (t >= k) break;
             int slot;
             if (s.nc >= c.maxc) {
                 int w = 0;

@@ -132,10 +132,10 @@ class AllegroHand:
 
     def step(self, actions):
         """VecTask.step (vec_task.py:390-441) -> pre_physics_step / simulate x2 / post_physics_step, fused."""
-        self.actions_buf.copy_(torch.clamp(actions, -self.clip_actions, self.clip_actions))
+        torch.clamp(actions, -self.clip_actions, self.clip_actions, out=self.actions_buf)
         self.sim.task_step(self.sim_flags)
         self.control_steps += 1
-        self.extras["time_outs"] = self.timeout_buf.to(torch.bool).to(self.rl_device)
+        self.extras["time_outs"] = self.timeout_buf.view(torch.bool).to(self.rl_device)
         self.extras["consecutive_successes"] = self.consecutive_successes.mean()     # allegro_hand.py:393
         self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
         return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras

@@ -185,12 +185,12 @@ class AllegroKuka:
 
     def step(self, actions):
         """VecTask.step (vec_task.py:390-441) -> pre_physics_step / simulate / post_physics_step, fused."""
-        self.actions_buf.copy_(torch.clamp(actions, -self.clip_actions, self.clip_actions))
+        torch.clamp(actions, -self.clip_actions, self.clip_actions, out=self.actions_buf)
         self.frame_since_restart += 1
         self._curriculum()
         self.sim.task_step(self.sim_flags)
         ex = self.extras
-        ex["time_outs"] = self.timeout_buf.to(torch.bool).to(self.rl_device)
+        ex["time_outs"] = self.timeout_buf.view(torch.bool).to(self.rl_device)
         ex["successes"] = self.prev_episode_successes.mean()                   # :908-917
         ex["true_objective"] = self.true_objective
         ex["true_objective_mean"] = self.true_objective.mean()

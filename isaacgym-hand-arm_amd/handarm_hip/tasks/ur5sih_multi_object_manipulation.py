@@ -367,7 +367,7 @@ class Ur5SihMultiObjectManipulation:
         self.sim.task_step(self.sim_flags)
         self._stat_pending += 1
         self.control_steps += 1
-        self.extras["time_outs"] = self.timeout_buf.to(torch.bool).to(self.rl_device)
+        self.extras["time_outs"] = self.timeout_buf.view(torch.bool).to(self.rl_device)
         self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
         self.obs_dict["teacher"] = {"obs": torch.clamp(self.teacher_obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)}
         return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras
