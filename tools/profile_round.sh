@@ -8,6 +8,7 @@ case $TASK in
   allegro_kuka) K=ak_step_kernel; ENVS=4096; SFX="" ;;
   ur5sih) K=ha_step_kernel; ENVS=8192; SFX="_ur5sih" ;;
   allegro_hand) K=ah_step_kernel; ENVS=16384; SFX="_allegro" ;;
+  binpick) K=hb_step_kernel; ENVS=8192; SFX="_binpick" ;;
   *) echo "unknown task $TASK"; exit 2 ;;
 esac
 P="cd /tmp && export TMPDIR=/tmp && rocprofv3"
