@@ -86,6 +86,31 @@ def kuka_bytes_per_env_step(n_links=24, n_dofs=23, num_obs=99, num_act=23, ts_re
     return sum(reads.values()) + sum(writes.values()), reads, writes
 
 
+def pointcloud_bytes_per_env(pcs):
+    """Algorithmic HBM bytes of one ha_pointclouds launch per env: every cloud point written once (16 B), the
+    pose rows it reads once (7 floats per object and per sampled robot link), the object pool ids, the target
+    index and goal_pos. Sample tables and the permutation are shared by all envs (L2-resident)."""
+    f, i64 = 4, 8
+    N, NO = pcs.sim.num_envs, pcs.sim.n_obj
+    writes = sum(t.numel() for t in pcs.outputs.values()) // N * f
+    obj = "object_synthetic_pointcloud" in pcs.outputs or "target_object_synthetic_pointcloud" in pcs.outputs
+    reads = (NO * 7 * f + NO * i64 + i64) if obj else 0
+    if "ur5sih_synthetic_pointcloud" in pcs.outputs:
+        reads += len(set(pcs.robot_body.tolist())) * 7 * f
+    if "sih_fingertip_pointcloud" in pcs.outputs:
+        reads += 5 * 3 * f
+    if "goal_synthetic_pointcloud" in pcs.outputs or "relative_goal_synthetic_pointcloud" in pcs.outputs:
+        reads += 3 * f
+    if "relative_goal_synthetic_pointcloud" in pcs.outputs:
+        reads += 7 * f
+    return writes + reads
+
+
+# the point-cloud student list (Ur5SihMultiObjectManipulation.yaml:45) that bench --pointclouds runs
+PC_STUDENT = ["goal_pos", "ur5_flange_pose", "dof_position_targets", "object_synthetic_pointcloud",
+              "ur5sih_synthetic_pointcloud", "goal_synthetic_pointcloud"]
+
+
 def cpu_baseline_kuka(num_envs=512, min_seconds=12.0, max_steps=4000, seed=0, subtask="regrasping"):
     """AllegroKuka on the host: C oracle physics (OpenMP over envs) + numpy task oracle (resets with host
     draws, targets, random forces, observations, reward)."""
@@ -251,6 +276,8 @@ def main():
                     help="envs per GPU (4096 allegro_kuka, 8192 ur5sih, 16384 allegro_hand, 8192 binpick)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dr", action="store_true", help="ur5sih: domain randomization off")
+    ap.add_argument("--pointclouds", action="store_true",
+                    help="ur5sih / binpick: the point-cloud student observation list (synthetic clouds every step)")
     ap.add_argument("--cpu-envs", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
@@ -282,12 +309,18 @@ def main():
         # config 5: Ur5SihMultiObject with bin.asset hard_bin and 8 objects from the YCB pool
         from handarm_hip import model as HM
         pool = [o["name"] for o in HM.load_scene()["objects"]]
-        env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": args.envs}, "seed": seed, "bin": {"asset": "hard_bin"},
+        envcfg = {"numEnvs": args.envs}
+        if args.pointclouds:
+            envcfg["observations"] = PC_STUDENT
+        env = Ur5SihMultiObjectManipulation({"env": envcfg, "seed": seed, "bin": {"asset": "hard_bin"},
                                              "objects": {"num_objects": 8, "dataset": {"ycb": pool}}}, device, device)
     else:
         cls = AllegroHand if allegro else Ur5SihMultiObjectManipulation
+        envcfg = {"numEnvs": args.envs}
+        if args.pointclouds and not allegro:
+            envcfg["observations"] = PC_STUDENT
         # config 4 is quoted with domain randomization on (BASELINE.json configs[3]); --no-dr turns it off
-        env = cls({"env": {"numEnvs": args.envs}, "seed": seed, "task": {"randomize": not (allegro or args.no_dr)}},
+        env = cls({"env": envcfg, "seed": seed, "task": {"randomize": not (allegro or args.no_dr)}},
                   device, device)
     env.reset()
     gen = torch.Generator(device=device).manual_seed(seed)
@@ -333,6 +366,8 @@ def main():
         print("host ms/step issue:", [round(x, 3) for x in gaps], "\ngpu ms/step:", [round(x, 3) for x in step_ms],
               file=sys.stderr)
     kern_ms = env.sim.kernel_times_ms(args.steps)
+    pcs = getattr(env, "pointclouds", None)
+    pc_ms = pcs.kernel_times_ms(args.steps) if pcs is not None else []
     log = {} if (allegro or kuka) else env.log_data
     kstats = parallel.reduce_kuka_episode_stats(env) if kuka else {}
     if rank == 0:
@@ -388,12 +423,20 @@ def main():
                           f"{args.envs} envs/GPU (BASELINE config 4 shard, DR {'off' if args.no_dr else 'on'})",
                 "binpick": "HandArm bin-picking Ur5SihMultiObjectManipulation VecTask.step, 3x2 substeps, 8 objects, "
                            f"{args.envs} envs/GPU (BASELINE config 5 shard)"}[args.task],
-                       "envs_per_gpu": args.envs, "total_envs": world * args.envs, "parallelism": f"env-shard x{world}"},
+                       "envs_per_gpu": args.envs, "total_envs": world * args.envs, "parallelism": f"env-shard x{world}",
+                       "observations": "point-cloud student list (Ur5SihMultiObjectManipulation.yaml:45)" if pcs is not None
+                       else "default"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": kernel, "kernel_avg_ms": kavg,
                          "algorithmic_bytes_per_env_step": bytes_env},
             "cpu_baseline": cpu,
+            "pointcloud_roofline": None if pcs is None else {
+                "bound": "hbm", "kernel": "ha_pointcloud_kernel", "observations": env.obs_names,
+                "kernel_avg_ms": statistics.mean(pc_ms), "algorithmic_bytes_per_env": pointcloud_bytes_per_env(pcs),
+                "achieved": pointcloud_bytes_per_env(pcs) * args.envs / (statistics.mean(pc_ms) * 1e-3) / 1e9,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": pointcloud_bytes_per_env(pcs) * args.envs / (statistics.mean(pc_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "success_rate_ewma": log.get("success_rate_ewma/overall"),
             "consecutive_successes": float(env.consecutive_successes.item()) if allegro else None,
             "episode_successes_mean": float(kstats["successes"]) if kuka else None,

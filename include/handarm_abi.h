@@ -23,6 +23,10 @@
  *                                  (vec_task.py:390-441 -> configurable_vec_task.py:347-414)
  *   ha_task_observe                post_step callbacks + compute_reward + compute_observations alone
  *   ha_task_reset                  reset_idx steady state (multi_object_manipulation.py:33-71)
+ *   ha_pointclouds                 synthetic point-cloud observables' post_step refresh
+ *                                  (multi_object.py:792-809, ur5sih.py:361-374)
+ *   ha_gather_obs                  compute_observations' torch.cat for a custom observation list
+ *                                  (observable_vec_task.py:183-203)
  * The fused entry points serve three tasks (ha_params_t.task): Ur5Sih (above), AllegroHand
  * (allegro_hand.py:586-633) and AllegroKuka (allegro_kuka_base.py:1355-1447).
  */
@@ -35,7 +39,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 5
+#define HA_ABI_VERSION 6
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -284,6 +288,47 @@ typedef struct ha_state_t {
  * [2 + 2*i] resets with pool object i as target, [3 + 2*i] successes */
 #define HA_STAT_SIZE (2 + 2 * HA_MAX_POOL)
 
+/* Synthetic point-cloud observables (SyntheticPointcloudObservable, hand_arm/utils/observables.py:199-216),
+ * computed from the refreshed state tensors bound with ha_bind_state. Each output is optional (NULL = skip)
+ * and is a dense float4 array (x, y, z, point type; utils/camera.py:43-47):
+ *   object_pc      [N][n_obj][P][4]  object_synthetic_pointcloud (multi_object.py:792-800): pool-frame
+ *                  samples posed by the object pose, padding points (w 0) zeroed, then the point axis
+ *                  permuted by perm (torch.randperm(P), one permutation for every env and object)
+ *   target_pc      [N][P][4]         target_object_synthetic_pointcloud (:802-804): the target object's
+ *                  row of object_pc with w *= 2 (PointType.TARGET)
+ *   robot_pc       [N][R][4]         ur5sih_synthetic_pointcloud (ur5sih.py:361-374): link-frame samples
+ *                  posed by rigid_body_state rows robot_body[r], w from the sample (1)
+ *   fingertip_pc   [N][5][4]         sih_fingertip_pointcloud (ur5sih.py:338-345): fingertip positions, w 3
+ *   goal_pc        [N][1][4]         goal_synthetic_pointcloud (multi_object.py:383-389): goal_pos, w 3
+ *   relative_goal_pc [N][1][4]       relative_goal_synthetic_pointcloud (:391-401, 806-809): goal_pos in
+ *                  the flange frame, w 3
+ * The object clouds pose their samples with object_pose rows when given ([N][n_obj][7]: the caller's snapshot
+ * of the previous observable refresh, for observation lists whose post-step order puts the cloud before
+ * object_pos, see handarm_hip/observables.py), else with this refresh's root_state rows. */
+#define HA_PC_MAX_LINKS 32      /* robot bodies a point-cloud launch reads (staged per env in LDS) */
+#define HA_PC_MAX_P 256         /* max_num_points per object cloud */
+#define HA_PC_MAX_R 2048        /* robot cloud points */
+typedef struct ha_pointcloud_t {
+    const float* object_samples;   /* [n_pool][P][4] pool-frame surface samples, w 1 (valid) / 0 (padding) */
+    const float* robot_samples;    /* [R][4] link-frame surface samples, w = point type */
+    const int32_t* robot_slot;     /* [R] index into links[] of each robot sample's body */
+    const int64_t* perm;           /* [P] object point permutation (torch.randperm output) */
+    const float* object_pose;      /* [N][n_obj][7] object poses (pos, quat) to use, or NULL = root_state */
+    float* object_pc;
+    float* target_pc;
+    float* robot_pc;
+    float* fingertip_pc;
+    float* goal_pc;
+    float* relative_goal_pc;
+    int32_t n_pool, P, R;
+    int32_t n_links;               /* <= HA_PC_MAX_LINKS */
+    int32_t links[HA_PC_MAX_LINKS];/* env-local rigid-body indices whose poses the clouds read */
+    int32_t fingertip_slot[5];     /* links[] slots of the five fingertips (thumb, index, middle, ring, little) */
+    int32_t flange_slot;           /* links[] slot of the UR5 flange */
+} ha_pointcloud_t;
+
+#define HA_MAX_OBS_SOURCES 4
+
 typedef struct ha_handle_s* ha_handle;
 
 int ha_abi_version(void);
@@ -316,6 +361,18 @@ float ha_last_kernel_ms(ha_handle h);
  * (0 disables); ha_kernel_times synchronises and returns the recorded durations in ms */
 int ha_enable_kernel_timing(ha_handle h, int32_t max_launches);
 int ha_kernel_times(ha_handle h, float* out_ms, int32_t max, int32_t* n_out);
+/* Synthetic point clouds (see ha_pointcloud_t) for all envs in one launch: replaces the post_step callbacks
+ * _refresh_object_synthetic_pointcloud / _refresh_target_object_synthetic_pointcloud (multi_object.py:792-804),
+ * _refresh_ur5sih_synthetic_pointcloud (ur5sih.py:361-374) and the goal / fingertip cloud get_state lambdas.
+ * Ur5Sih task only. If timing is enabled (ha_enable_kernel_timing) its launches are recorded separately
+ * (ha_pointcloud_times). */
+int ha_pointclouds(ha_handle h, const ha_pointcloud_t* pc, void* stream);
+int ha_pointcloud_times(ha_handle h, float* out_ms, int32_t max, int32_t* n_out);
+/* Observation vector of a custom observation list (observable_vec_task.py:183-192): out[N][n_cols], column k
+ * = sources[cols[2k]][env * strides[cols[2k]] + cols[2k+1]]. sources / strides are host arrays of n_sources
+ * (<= HA_MAX_OBS_SOURCES) device pointers / row strides in floats; cols is a device int32 array. */
+int ha_gather_obs(ha_handle h, const float* const* sources, const int32_t* strides, int32_t n_sources,
+                  const int32_t* cols, int32_t n_cols, float* out, void* stream);
 
 #ifdef __cplusplus
 }

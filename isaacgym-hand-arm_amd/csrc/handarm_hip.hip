@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include "ak_task.h"
+#include "ha_pointcloud.h"
 
 #define HA_ND 17         /* Ur5Sih DOF count (UR5 + SIH); AH_ND = 16 (Allegro) */
 
@@ -447,6 +448,7 @@ struct ha_handle_s {
     ha_params_t* d_params;
     ha_params_t h_params;
     int N, NO, D, L, A, B, task, fam;
+    int a0;               // actor_object0 (host copy)
     ha_state_t st;
     int bound;
     int stat_slots;
@@ -455,6 +457,8 @@ struct ha_handle_s {
     int timed;
     int t_max, t_count;
     hipEvent_t* t_ev;     // 2 * t_max events
+    int pc_count;
+    hipEvent_t* pc_ev;    // 2 * t_max events (ha_pointclouds launches)
 };
 
 #define HIPCHK(x)                                                                     \
@@ -550,6 +554,7 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     h->L = model->n_links;
     h->A = model->n_actors;
     h->B = model->n_bodies;
+    h->a0 = model->actor_object0;
     h->task = params->task;
     h->fam = fam;
     h->h_params = *params;
@@ -729,15 +734,23 @@ int ha_task_reset(ha_handle h, uint32_t flags, void* stream) {
 int ha_enable_kernel_timing(ha_handle h, int32_t max_launches) {
     if (!h || max_launches < 0) return HA_E_ARG;
     if (h->t_ev) {
-        for (int i = 0; i < 2 * h->t_max; i++) (void)hipEventDestroy(h->t_ev[i]);
+        for (int i = 0; i < 2 * h->t_max; i++) {
+            (void)hipEventDestroy(h->t_ev[i]);
+            (void)hipEventDestroy(h->pc_ev[i]);
+        }
         free(h->t_ev);
-        h->t_ev = nullptr;
+        free(h->pc_ev);
+        h->t_ev = h->pc_ev = nullptr;
     }
     h->t_max = max_launches;
-    h->t_count = 0;
+    h->t_count = h->pc_count = 0;
     if (max_launches == 0) return HA_OK;
     h->t_ev = (hipEvent_t*)calloc(2 * max_launches, sizeof(hipEvent_t));
-    for (int i = 0; i < 2 * max_launches; i++) HIPCHK(hipEventCreate(&h->t_ev[i]));
+    h->pc_ev = (hipEvent_t*)calloc(2 * max_launches, sizeof(hipEvent_t));
+    for (int i = 0; i < 2 * max_launches; i++) {
+        HIPCHK(hipEventCreate(&h->t_ev[i]));
+        HIPCHK(hipEventCreate(&h->pc_ev[i]));
+    }
     return HA_OK;
 }
 
@@ -749,6 +762,85 @@ int ha_kernel_times(ha_handle h, float* out_ms, int32_t max, int32_t* n_out) {
         HIPCHK(hipEventElapsedTime(&out_ms[i], h->t_ev[2 * i], h->t_ev[2 * i + 1]));
     }
     *n_out = n;
+    return HA_OK;
+}
+
+int ha_pointcloud_times(ha_handle h, float* out_ms, int32_t max, int32_t* n_out) {
+    if (!h || !out_ms || !n_out) return HA_E_ARG;
+    int n = h->pc_count < max ? h->pc_count : max;
+    for (int i = 0; i < n; i++) {
+        HIPCHK(hipEventSynchronize(h->pc_ev[2 * i + 1]));
+        HIPCHK(hipEventElapsedTime(&out_ms[i], h->pc_ev[2 * i], h->pc_ev[2 * i + 1]));
+    }
+    *n_out = n;
+    return HA_OK;
+}
+
+int ha_pointclouds(ha_handle h, const ha_pointcloud_t* pc, void* stream) {
+    if (!h || !h->bound || !pc) return HA_E_ARG;
+    if (h->task != HA_TASK_UR5SIH || !h->st.object_indices || !h->st.target_object_index || !h->st.goal_pos)
+        return HA_E_STATE;
+    PcLaunch L;
+    L.pc = *pc;
+    L.root = h->st.root_state;
+    L.body = h->st.rigid_body_state;
+    L.object_indices = h->st.object_indices;
+    L.target_index = h->st.target_object_index;
+    L.goal_pos = h->st.goal_pos;
+    L.N = h->N;
+    L.A = h->A;
+    L.B = h->B;
+    L.a0 = h->a0;
+    L.NO = h->NO;
+    // segment table; every index the kernel will form is checked here, on the host
+    bool obj = pc->object_pc || pc->target_pc;
+    if (obj && (!pc->object_samples || !pc->perm || pc->P < 1 || pc->P > HA_PC_MAX_P || pc->n_pool < 1))
+        return HA_E_ARG;
+    if (pc->robot_pc && pc->R > HA_PC_MAX_R) return HA_E_ARG;
+    if (pc->robot_pc && (!pc->robot_samples || !pc->robot_slot || pc->R < 1)) return HA_E_ARG;
+    if (pc->n_links < 0 || pc->n_links > HA_PC_MAX_LINKS || h->NO > HA_MAX_OBJ) return HA_E_ARG;
+    for (int l = 0; l < pc->n_links; l++)
+        if (pc->links[l] < 0 || pc->links[l] >= h->B) return HA_E_ARG;
+    for (int f = 0; f < 5 && pc->fingertip_pc; f++)
+        if (pc->fingertip_slot[f] < 0 || pc->fingertip_slot[f] >= pc->n_links) return HA_E_ARG;
+    if (pc->relative_goal_pc && (pc->flange_slot < 0 || pc->flange_slot >= pc->n_links)) return HA_E_ARG;
+    if (pc->robot_pc && pc->n_links < 1) return HA_E_ARG;   // robot_slot entries are validated by the caller
+    int len[6] = {pc->object_pc ? h->NO * pc->P : 0, pc->target_pc ? pc->P : 0, pc->robot_pc ? pc->R : 0,
+                  pc->fingertip_pc ? 5 : 0, pc->goal_pc ? 1 : 0, pc->relative_goal_pc ? 1 : 0};
+    L.seg[0] = 0;
+    for (int k = 0; k < 6; k++) L.seg[k + 1] = L.seg[k] + len[k];
+    int W = L.seg[PC_END];
+    if (W == 0) return HA_OK;
+    if ((long long)W * h->N >= (1ll << 31)) return HA_E_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    bool rec = h->pc_ev && h->pc_count < h->t_max;
+    if (rec) (void)hipEventRecord(h->pc_ev[2 * h->pc_count], s);
+    hipLaunchKernelGGL(ha_pointcloud_kernel, dim3(h->N), dim3(256), 0, s, L);
+    HIPCHK(hipGetLastError());
+    if (rec) (void)hipEventRecord(h->pc_ev[2 * h->pc_count++ + 1], s);
+    return HA_OK;
+}
+
+int ha_gather_obs(ha_handle h, const float* const* sources, const int32_t* strides, int32_t n_sources,
+                  const int32_t* cols, int32_t n_cols, float* out, void* stream) {
+    if (!h || !sources || !strides || !cols || !out || n_sources < 1 || n_sources > HA_MAX_OBS_SOURCES ||
+        n_cols < 0)
+        return HA_E_ARG;
+    if (n_cols == 0) return HA_OK;
+    if ((long long)n_cols * h->N >= (1ll << 31)) return HA_E_ARG;
+    ObsGather g;
+    for (int q = 0; q < HA_MAX_OBS_SOURCES; q++) {
+        g.src[q] = sources[q < n_sources ? q : 0];
+        g.stride[q] = strides[q < n_sources ? q : 0];
+        if (!g.src[q]) return HA_E_ARG;
+    }
+    g.cols = cols;
+    g.out = out;
+    g.N = h->N;
+    g.n_cols = n_cols;
+    unsigned total = (unsigned)n_cols * (unsigned)h->N;
+    hipLaunchKernelGGL(ha_obs_gather_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, g);
+    HIPCHK(hipGetLastError());
     return HA_OK;
 }
 

@@ -38,6 +38,9 @@ SIGNATURES = {
     "ha_last_kernel_ms": ([H], C.c_float),
     "ha_enable_kernel_timing": ([H, C.c_int32], C.c_int),
     "ha_kernel_times": ([H, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32)], C.c_int),
+    "ha_pointclouds": ([H, C.POINTER(HM.HaPointcloud), S], C.c_int),
+    "ha_pointcloud_times": ([H, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32)], C.c_int),
+    "ha_gather_obs": ([H, C.POINTER(C.c_void_p), C.POINTER(C.c_int32), C.c_int32, fp, C.c_int32, fp, S], C.c_int),
 }
 
 

@@ -164,6 +164,18 @@ class HaState(C.Structure):
     _fields_ = [(n, P) for n in STATE_FIELDS]
 
 
+PC_MAX_LINKS = 32
+
+
+class HaPointcloud(C.Structure):
+    """ha_pointcloud_t (include/handarm_abi.h): synthetic point-cloud inputs / outputs (device pointers)."""
+    _fields_ = [("object_samples", P), ("robot_samples", P), ("robot_slot", P), ("perm", P),
+                ("object_pose", P), ("object_pc", P), ("target_pc", P), ("robot_pc", P), ("fingertip_pc", P),
+                ("goal_pc", P), ("relative_goal_pc", P), ("n_pool", C.c_int32), ("P", C.c_int32), ("R", C.c_int32),
+                ("n_links", C.c_int32), ("links", C.c_int32 * PC_MAX_LINKS), ("fingertip_slot", C.c_int32 * 5),
+                ("flange_slot", C.c_int32)]
+
+
 def null_fields(task):
     """State buffers left NULL for a task: object_scale switches the physics to per-env scaled object
     geometry, which only AllegroKuka's cuboid family uses (bit-identical unscaled path otherwise)."""

@@ -18,8 +18,13 @@ import sys
 import numpy as np
 import torch
 
+import ctypes as C
+
+from .. import _lib
 from .. import model as HM
+from .. import observables as OB
 from .. import parallel
+from ..pointclouds import SyntheticPointclouds
 from ..sim import HandArmSim
 from ..torch_utils import randomize_rotation, torch_rand_float
 
@@ -150,6 +155,7 @@ class Ur5SihMultiObjectManipulation:
         start = np.cumsum([0] + sizes)
         self.observations_start_end = {n: (int(start[i]), int(start[i + 1])) for i, n in enumerate(OBSERVATIONS)}
         self.teacher_observations_start_end = dict(self.observations_start_end)
+        self._init_observation_lists(cfg, env, objects, N)
         self.extras = {}
         self.obs_dict = {}
         self._log_data = {}
@@ -191,6 +197,63 @@ class Ur5SihMultiObjectManipulation:
         self.total_num_successes = 0
         self.sim_flags = 0
 
+    def _init_observation_lists(self, cfg, env, objects, N):
+        """cfg["env"]["observations"] / ["teacher_observations"] (observable_vec_task.py:15-29). The default
+        lists are what the fused step kernel writes; a custom observation list (e.g. the point-cloud student
+        list, Ur5SihMultiObjectManipulation.yaml:45) is assembled on the device from the kernel's obs row and
+        goal_pos (ha_gather_obs), and its synthetic point clouds come from ONE ha_pointclouds launch per step
+        into obs_dict[name] (observables.py:199-210). The post-step order decides which object pose a cloud
+        sees (handarm_hip/observables.py)."""
+        self.obs_names = list(env.get("observations") or OB.DEFAULT_OBSERVATIONS)
+        teacher = list(env.get("teacher_observations") or OB.DEFAULT_OBSERVATIONS)
+        if teacher != OB.DEFAULT_OBSERVATIONS:
+            raise NotImplementedError("teacher_observations: this build writes the default teacher list "
+                                      f"{OB.DEFAULT_OBSERVATIONS}")
+        order = OB.post_step_order(self.obs_names, teacher)
+        if not OB.sees_previous_object_pose(order, "object_bounding_box"):
+            raise NotImplementedError("observation list refreshes object_bounding_box after object_pos; the step "
+                                      "kernel implements the default order (bbox sees the previous pose)")
+        self.custom_obs = self.obs_names != OB.DEFAULT_OBSERVATIONS
+        self.pointclouds = None
+        pc_names = [n for n in self.obs_names if n in OB.POINTCLOUDS]
+        if pc_names:
+            g = torch.Generator(device=self.device).manual_seed(int(cfg.get("seed", 42)))
+            self.pointclouds = SyntheticPointclouds(self.sim, pc_names, objects, _get(cfg, "pointclouds", {}), g)
+            if any(OB.sees_previous_object_pose(order, n) for n in
+                   ("object_synthetic_pointcloud", "target_object_synthetic_pointcloud") if n in order):
+                self.pointclouds.use_previous_object_pose()
+        if not self.custom_obs:
+            return
+        cols = OB.obs_columns(self.obs_names, self.num_objects)
+        self._obs_cols = torch.tensor(cols, dtype=torch.int32, device=self.device)
+        self.student_obs_buf = torch.zeros((N, len(cols)), dtype=torch.float32, device=self.device)
+        self._gather_src = (C.c_void_p * 2)(self.obs_buf.data_ptr(), self.goal_pos.data_ptr())
+        self._gather_stride = (C.c_int32 * 2)(self.obs_buf.shape[1], 3)
+        self.num_observations = len(cols)
+        self.obs_space = Box(np.full(self.num_observations, -np.inf), np.full(self.num_observations, np.inf))
+        start, self.observations_start_end = 0, {}
+        for n in self.obs_names:                  # _compute_num_observations: only key-"obs" observables
+            k = len(OB.obs_columns([n], self.num_objects))
+            if k:
+                self.observations_start_end[n] = (start, start + k)
+                start += k
+
+    def _observations(self):
+        """compute_observations (observable_vec_task.py:183-203) from the device buffers."""
+        obs = self.obs_buf
+        if self.custom_obs:
+            _lib.check(self.sim.lib.ha_gather_obs(self.sim.h, self._gather_src, self._gather_stride, 2,
+                                                  self._obs_cols.data_ptr(), len(self._obs_cols),
+                                                  self.student_obs_buf.data_ptr(), self.sim._stream()),
+                       "ha_gather_obs")
+            obs = self.student_obs_buf
+        self.obs_dict["obs"] = torch.clamp(obs, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        if self.pointclouds is not None:
+            for n, t in self.pointclouds.outputs.items():
+                self.obs_dict[n] = t.to(self.rl_device)
+        self.obs_dict["teacher"] = {"obs": torch.clamp(self.teacher_obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)}
+        return self.obs_dict
+
     # ------------------------------------------------------------------ VecTask properties
     @property
     def num_envs(self):
@@ -230,7 +293,13 @@ class Ur5SihMultiObjectManipulation:
 
     @property
     def observation_keys(self):
-        return ["obs"]
+        # observable_vec_task.py:205-211: "obs" for low-dimensional observables, the name for point clouds
+        keys = []
+        for n in self.obs_names:
+            k = n if n in OB.POINTCLOUDS else "obs"
+            if k not in keys:
+                keys.append(k)
+        return keys
 
     def get_number_of_agents(self):
         return self.num_agents
@@ -364,20 +433,21 @@ class Ur5SihMultiObjectManipulation:
         self.actions_buf.copy_(action_tensor)
         if self._stat_pending == self.sim.stats_ring:
             self._fold_stats()
+        if self.pointclouds is not None:           # object_pos as of the previous refresh (see observables.py)
+            self.pointclouds.snapshot_object_pose(self.sim.t["obs_cache"])
         self.sim.task_step(self.sim_flags)
+        if self.pointclouds is not None:           # the clouds' post_step refresh, one launch
+            self.pointclouds.refresh()
         self._stat_pending += 1
         self.control_steps += 1
         self.extras["time_outs"] = self.timeout_buf.view(torch.bool).to(self.rl_device)
-        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
-        self.obs_dict["teacher"] = {"obs": torch.clamp(self.teacher_obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)}
+        self._observations()
         return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras
 
     def reset(self):
         """VecTask.reset (vec_task.py:459-474): compute_observations only."""
         self.sim.task_observe(HM.FLAG_OBS_ONLY)
-        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
-        self.obs_dict["teacher"] = {"obs": torch.clamp(self.teacher_obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)}
-        return self.obs_dict
+        return self._observations()
 
     def reset_idx(self, env_ids):
         """Immediate reset of ALL envs (the reference asserts it, ur5sih.py:617)."""
@@ -390,6 +460,6 @@ class Ur5SihMultiObjectManipulation:
         done_env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()
         if len(done_env_ids) > 0:
             self.reset_idx(done_env_ids)
-        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        self._observations()
         return self.obs_dict, done_env_ids
 

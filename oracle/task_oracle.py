@@ -396,3 +396,56 @@ def reset_state(root, dof, draw_cfg, draw_target, draw_goal, object_pos_initial,
                 target_idx=np.asarray(draw_target), cfg_idx=np.asarray(draw_cfg),
                 servo=np.tile(SERVO_UPPER, (n, 1)), smoothed=np.zeros((n, 5), F),
                 ur5_target=dof[:, 0:6, 0].copy())
+
+
+# ----------------------------------------------------------------------------- synthetic point clouds (§8f #2)
+def object_pointcloud(pose, samples, perm):
+    """object_synthetic_pointcloud (multi_object.py:792-800): pose (N, n_obj, 7) object pos+quat,
+    samples (N, n_obj, P, 4) per-env pool-frame samples (w 1 / 0 padding), perm (P,).
+    ordered = pos + quat_apply(quat, samples); xyz *= w; then the point axis permuted. -> (N, n_obj*P, 4)"""
+    pose = np.asarray(pose, F)
+    samples = np.asarray(samples, F)
+    n, no, p = samples.shape[:3]
+    pos = np.broadcast_to(pose[:, :, None, 0:3], (n, no, p, 3))
+    quat = np.broadcast_to(pose[:, :, None, 3:7], (n, no, p, 4))
+    ordered = samples.copy()
+    ordered[..., 0:3] = pos + quat_apply(quat, samples[..., 0:3])
+    ordered[..., 0:3] *= ordered[..., 3:4]
+    return ordered[:, :, np.asarray(perm)].reshape(n, no * p, 4)
+
+
+def target_pointcloud(object_pc, target_idx, n_obj):
+    """target_object_synthetic_pointcloud (multi_object.py:802-804): gather the target row, w *= TARGET (2)."""
+    n = object_pc.shape[0]
+    pc = object_pc.reshape(n, n_obj, -1, 4)[np.arange(n), np.asarray(target_idx)].copy()
+    pc[..., 3] *= F(2)
+    return pc
+
+
+def robot_pointcloud(body, link_bodies, samples):
+    """ur5sih_synthetic_pointcloud (ur5sih.py:361-374, relative=False): body (N, B, 13) rigid-body states,
+    link_bodies (R,) env body index per sample, samples (R, 3) link-frame points. w = 1."""
+    body = np.asarray(body, F)
+    b = body[:, np.asarray(link_bodies)]
+    out = np.ones((body.shape[0], len(link_bodies), 4), F)
+    out[..., 0:3] = b[..., 0:3] + quat_apply(b[..., 3:7], np.broadcast_to(np.asarray(samples, F), b[..., 0:3].shape))
+    return out
+
+
+def fingertip_pointcloud(body, tip_bodies):
+    """sih_fingertip_pointcloud (ur5sih.py:337-345): fingertip positions with id 3."""
+    b = np.asarray(body, F)[:, np.asarray(tip_bodies), 0:3]
+    return np.concatenate([b, np.full(b.shape[:-1] + (1,), 3, F)], -1)
+
+
+def goal_pointcloud(goal_pos):
+    """goal_synthetic_pointcloud (multi_object.py:383-389)."""
+    g = np.asarray(goal_pos, F)
+    return np.concatenate([g, np.full((len(g), 1), 3, F)], -1)[:, None]
+
+
+def relative_goal_pointcloud(goal_pos, flange_pose):
+    """relative_goal_synthetic_pointcloud (multi_object.py:391-401, 806-809)."""
+    fl = np.asarray(flange_pose, F)
+    rel = quat_apply(quat_conjugate(fl[:, 3:7]), np.asarray(goal_pos, F) - fl[:, 0:3])
+    return np.concatenate([rel, np.full((len(rel), 1), 3, F)], -1)[:, None]

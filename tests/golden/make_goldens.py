@@ -111,9 +111,13 @@ class FakeGym:
         return rec
 
 
-def make_task(num_envs, num_initial_poses=1, seed=0, n_objects=None, bin_layout=False):
+def make_task(num_envs, num_initial_poses=1, seed=0, n_objects=None, bin_layout=False, student_obs=None, pc=None):
     """n_objects / bin_layout: the bin-picking variant (BASELINE config 5): cfg objects.num_objects = n and
-    the actor layout with a bin actor (goal 0, robot 1, table 2, bin 3, objects 4..; multi_object.py:579-644)."""
+    the actor layout with a bin actor (goal 0, robot 1, table 2, bin 3, objects 4..; multi_object.py:579-644).
+    student_obs: a custom cfg["env"]["observations"] list (the teacher list stays the default one).
+    pc: the committed surface samples (assets/ur5sih_pointclouds.npz) that the reference's point-cloud
+    acquisition draws through trimesh (absent here): FakeObject.sample_points_from_mesh / surface_area and a
+    stand-in trimesh.sample.sample_surface hand them to the reference's own code."""
     mom = refload.load("isaacgymenvs.tasks.hand_arm.task.multi_object_manipulation")
     avt = refload.load("isaacgymenvs.tasks.hand_arm.base.actionable_vec_task")
     obs_mod = refload.load("isaacgymenvs.tasks.hand_arm.utils.observables")
@@ -130,7 +134,7 @@ def make_task(num_envs, num_initial_poses=1, seed=0, n_objects=None, bin_layout=
 
     T = mom.Ur5SihMultiObjectManipulation
     t = object.__new__(T)
-    t.cfg = {"env": {"observations": list(obs_list), "teacher_observations": list(obs_list),
+    t.cfg = {"env": {"observations": list(student_obs or obs_list), "teacher_observations": list(obs_list),
                      "actions": list(e["actions"]), "numEnvs": num_envs}}
     t.cfg_base, t.cfg_env, t.cfg_task = cfg_base, cfg_env, cfg_task
     t.num_environments = num_envs
@@ -160,10 +164,28 @@ def make_task(num_envs, num_initial_poses=1, seed=0, n_objects=None, bin_layout=
     t.ur5sih_actuated_dof_upper_limits = t.ur5sih_dof_upper_limits[t.ur5sih_actuated_dof_indices]
     t.ur5sih_rigid_body_count = len(links)
     t.ur5sih_num_body_surface_samples = [1]   # synthetic robot point cloud: registered, never active
+    if pc is not None:
+        # _acquire_robot_urdf (ur5sih.py:70-91) with the committed samples: meshes keyed by link name, counts
+        # int(1500 * area) as stored; trimesh.sample.sample_surface returns the stored samples of that link
+        names = [str(n) for n in pc["robot_link_names"]]
+        counts = [int(c) for c in pc["robot_link_counts"]]
+        starts = np.cumsum([0] + counts)
+        t.ur5sih_body_meshes = {n: n for n in names}
+        t.ur5sih_body_areas = {n: c / 1500.0 for n, c in zip(names, counts)}
+        t.ur5sih_num_body_surface_samples = counts
+        by_link = {n: pc["robot_samples"][starts[i]:starts[i + 1]].astype(np.float64) for i, n in enumerate(names)}
+        sys.modules["trimesh"].sample.sample_surface = lambda mesh, count: (by_link[mesh][:count], None)
     # _create_envs (multi_object.py:477-677): actor order goal, robot, table, objects
     g = torch.Generator().manual_seed(seed)
     n_obj = cfg_env.objects.num_objects
     t.objects = [FakeObject(o) for o in scene["objects"][:max(3, n_obj)]]
+    if pc is not None:
+        names = [str(n) for n in pc["object_names"]]
+        for o in t.objects:
+            i = names.index(o.name)
+            o.surface_area = float(pc["object_areas"][i])
+            o.sample_points_from_mesh = (lambda smp: lambda num_samples: smp[:num_samples].astype(np.float64))(
+                pc["object_samples"][i])
     t.object_indices = torch.stack([torch.randperm(len(t.objects), generator=g)[:n_obj] for _ in range(num_envs)])
     a0 = 4 if bin_layout else 3
     n_static_bodies = 6 if bin_layout else 1      # table base_link + 4 walls, bin / the table box
@@ -185,7 +207,7 @@ def make_task(num_envs, num_initial_poses=1, seed=0, n_objects=None, bin_layout=
     t.register_observables()
     t._active_observations.add([t._registered_observables[n] for n in t.cfg["env"]["observations"]])
     t._active_observations.add([t._registered_observables[n] for n in t.cfg["env"]["teacher_observations"]])
-    t.cfg["env"]["numObservations"], t.observations_start_end = t._compute_num_observations(obs_list)
+    t.cfg["env"]["numObservations"], t.observations_start_end = t._compute_num_observations(t.cfg["env"]["observations"])
     t.cfg["env"]["numTeacherObservations"], t.teacher_observations_start_end = t._compute_num_observations(obs_list)
     t._sorted_observations = t._active_observations.sort(t._registered_observables)
     t.num_observations = t.cfg["env"]["numObservations"]
@@ -385,7 +407,75 @@ def gen_quat(path, M=64, seed=4):
     print("wrote", path)
 
 
+PC_ASSET = os.path.join(HERE, "..", "..", "isaacgym-hand-arm_amd", "handarm_hip", "assets", "ur5sih_pointclouds.npz")
+# the point-cloud student list of Ur5SihMultiObjectManipulation.yaml:45, and the same with every other synthetic
+# cloud this build produces
+PC_STUDENT = ["goal_pos", "ur5_flange_pose", "dof_position_targets", "object_synthetic_pointcloud",
+              "ur5sih_synthetic_pointcloud", "goal_synthetic_pointcloud"]
+PC_ALL = PC_STUDENT + ["target_object_synthetic_pointcloud", "sih_fingertip_pointcloud",
+                       "relative_goal_synthetic_pointcloud"]
+
+
+def gen_pointclouds(path, student, N=8, steps=4, seed=5):
+    """post_physics_step with point-cloud observables active (multi_object.py:774-809, ur5sih.py:347-374):
+    per step the state in, obs / teacher obs, every cloud in obs_dict, the torch.randperm drawn, and the
+    post-step order the reference's ActiveObservables.sort chose (it decides which object pose the clouds see)."""
+    pc = np.load(PC_ASSET)
+    t, mom = make_task(N, num_initial_poses=2, seed=seed, student_obs=student, pc=pc)
+    g = torch.Generator().manual_seed(seed + 100)
+    n_obj = t.cfg_env.objects.num_objects
+    t.objects_dropped = True
+    t.object_pos_initial = torch.rand(N, 2, n_obj, 3, generator=g) * 0.3 + torch.tensor([0.1, 0.4, 0.5])
+    t.object_quat_initial = rand_quat(g, (N, 2, n_obj))
+    clouds = [n for n in student if n.endswith("_pointcloud")]
+    out = {k: [] for k in ["root", "body", "dof", "targets", "goal_pos", "target_idx", "obs", "teacher", "perm"]
+           + clouds}
+    orig = torch.randperm
+    perms = []
+
+    def randperm(*a, **k):
+        r = orig(*a, **k)
+        perms.append(r.clone())
+        return r
+    torch.randperm = randperm
+    try:
+        for s in range(steps):
+            fill_random_state(t, g)
+            t.dof_position_targets[:] = torch.randn(N, 17, generator=g)
+            t.goal_pos[:] = torch.rand(N, 3, generator=g) * 0.3 + torch.tensor([0.13, 0.43, 0.7])
+            t.target_object_index[:] = torch.randint(n_obj, (N,), generator=g)
+            t.target_object_actor_env_index[:] = torch.tensor(t.object_actor_env_indices)[t.target_object_index]
+            t.progress_buf[:] = 5
+            t.reset_buf[:] = 0
+            for k, v in [("root", t.root_state), ("body", t.body_state), ("dof", t.dof_state),
+                         ("targets", t.dof_position_targets), ("goal_pos", t.goal_pos),
+                         ("target_idx", t.target_object_index)]:
+                out[k].append(v.clone())
+            perms.clear()
+            t.post_physics_step()
+            assert len(perms) == 1, len(perms)
+            out["perm"].append(perms[0])
+            out["obs"].append(t.obs_buf.clone())
+            out["teacher"].append(t.teacher_obs_buf.clone())
+            for c in clouds:
+                out[c].append(t.obs_dict[c].clone())
+    finally:
+        torch.randperm = orig
+    arrays = {k: torch.stack(v).numpy() for k, v in out.items()}
+    arrays["object_indices"] = t.object_indices.numpy()
+    arrays["pool"] = np.array([o.name for o in t.objects])
+    arrays["observations"] = np.array(student)
+    arrays["post_step_order"] = np.array(list(t._sorted_observations.keys()))
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, {k: v.shape for k, v in arrays.items()})
+    print("post-step order:", list(t._sorted_observations.keys()))
+
+
 if __name__ == "__main__":
+    if "--pointclouds" in sys.argv:
+        gen_pointclouds(os.path.join(HERE, "ur5sih_pointclouds_student.npz"), PC_STUDENT, seed=5)
+        gen_pointclouds(os.path.join(HERE, "ur5sih_pointclouds_all.npz"), PC_ALL, seed=6)
+        sys.exit(0)
     if "--bin" in sys.argv:     # bin-picking variant only (8 objects, bin actor layout)
         gen_obs_reward(os.path.join(HERE, "ur5sih_obs_reward_bin8.npz"), n_objects=8, bin_layout=True, seed=11)
         sys.exit(0)

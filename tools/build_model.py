@@ -728,7 +728,100 @@ def main_bin(n_objects=8):
           f"bin extent {scene['bin_extent']} -> {BIN_OUT}")
 
 
+# ----------------------------------------------------------------------------- synthetic point clouds (§8f #2)
+PC_OUT = os.path.join(os.path.dirname(__file__), "..", "isaacgym-hand-arm_amd", "handarm_hip", "assets",
+                      "ur5sih_pointclouds.npz")
+PC_MAX_POINTS = 128                  # Ur5SihMultiObject.yaml pointclouds.max_num_points
+ROBOT_PC_DENSITY = 1500.0            # samples per m^2 (ur5sih.py:90-91)
+# links whose collision meshes the reference samples: every link with a collision mesh in URDF order minus the
+# six UR5 arm links (ur5sih.py:70-88, use_reduced_robot)
+ROBOT_PC_SKIP = {"shoulder_link", "upper_arm_link", "forearm_link", "wrist_1_link", "wrist_2_link", "wrist_3_link"}
+
+
+def sample_surface(v, f, count, rng):
+    """trimesh.sample.sample_surface (trimesh==3.23.5, setup.py:28; absent here) restated: faces drawn with
+    probability proportional to area (searchsorted on the cumulative area), then a uniform point in the
+    triangle from two uniforms folded back into the triangle when their sum exceeds 1."""
+    tri = v[f]
+    area = 0.5 * np.linalg.norm(np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0]), axis=1)
+    cum = np.cumsum(area)
+    face = np.searchsorted(cum, rng.random(count) * cum[-1])
+    origins = tri[face, 0]
+    vecs = tri[face, 1:] - origins[:, None]
+    lengths = rng.random((count, 2, 1))
+    fold = lengths.sum(axis=1).reshape(-1) > 1.0
+    lengths[fold] -= 1.0
+    lengths = np.abs(lengths)
+    return (vecs * lengths).sum(axis=1) + origins, float(area.sum())
+
+
+def link_collision_mesh(link_el, base_dir, colls=None):
+    """urdfpy Link.collision_mesh: the link's collision meshes in the link frame, concatenated."""
+    vs, fs, n = [], [], 0
+    for c in (colls if colls is not None else link_el.findall("collision")):
+        g = c.find("geometry/mesh")
+        if g is None:
+            continue
+        path = os.path.join(base_dir, g.get("filename"))
+        if not os.path.exists(path):
+            return None
+        v, fa = load_mesh(path, [float(t) for t in g.get("scale", "1 1 1").split()])
+        o, R = parse_origin(c.find("origin"))
+        vs.append(v @ R.T + o)
+        fs.append(fa + n)
+        n += len(v)
+    if not vs:
+        return None
+    return np.concatenate(vs), np.concatenate(fs)
+
+
+def main_pointclouds(seed=0):
+    """Surface samples of the object pool and the reduced robot (multi_object.py:774-790, ur5sih.py:347-359).
+    Objects: PC_MAX_POINTS samples and the mesh area per pool object; the runtime takes the first
+    int(average_num_points * area / mean_area) of them for the configured pool ('area' sample mode) and pads
+    to max_num_points. Robot: int(1500 * area) samples per link in the link frame, with the link's index."""
+    rng = np.random.default_rng(seed)
+    scene = json.load(open(OUT))
+    names, samples, areas = [], [], []
+    for rec in scene["objects"]:
+        urdf = os.path.join(ASSETS, "object_sets", "urdf", "ycb", rec["name"] + ".urdf")
+        link = ET.parse(urdf).getroot().find("link")
+        v, f = link_collision_mesh(link, os.path.dirname(urdf))
+        pts, area = sample_surface(v, f, PC_MAX_POINTS, rng)
+        names.append(rec["name"])
+        samples.append(pts)
+        areas.append(area)
+    base_dir = os.path.dirname(ROBOT_URDF)
+    root = ET.parse(ROBOT_URDF).getroot()
+    link_index = {l["name"]: i for i, l in enumerate(scene["robot"]["links"])}
+    palm_colls = [l for l in ET.parse(PALM_URDF).getroot().findall("link") if l.get("name") == "palm"][0]
+    r_pts, r_link, r_names, r_counts = [], [], [], []
+    for el in root.findall("link"):                    # URDF document order (urdfpy URDF.links)
+        n = el.get("name")
+        if n in ROBOT_PC_SKIP or not el.findall("collision"):
+            continue
+        mesh = link_collision_mesh(el, base_dir, palm_colls.findall("collision") if n == "palm" else None)
+        if mesh is None:
+            continue
+        tri = mesh[0][mesh[1]]
+        area = float(0.5 * np.linalg.norm(np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0]), axis=1).sum())
+        count = int(ROBOT_PC_DENSITY * area)
+        pts, _ = sample_surface(mesh[0], mesh[1], count, rng)
+        r_pts.append(pts)
+        r_link += [link_index[n]] * count
+        r_names.append(n)
+        r_counts.append(count)
+    np.savez_compressed(PC_OUT, object_names=np.array(names), object_samples=np.array(samples, np.float32),
+                        object_areas=np.array(areas, np.float64), robot_samples=np.concatenate(r_pts).astype(np.float32),
+                        robot_link=np.array(r_link, np.int32), robot_link_names=np.array(r_names),
+                        robot_link_counts=np.array(r_counts, np.int32))
+    print(f"point clouds: {len(names)} objects x {PC_MAX_POINTS} samples, robot {sum(r_counts)} samples over "
+          f"{list(zip(r_names, r_counts))} -> {PC_OUT}")
+
+
 if __name__ == "__main__":
+    if "--pointclouds" in sys.argv:
+        sys.exit(main_pointclouds())
     if "--bin" in sys.argv:
         sys.exit(main_bin())
     if "--allegro" in sys.argv:
