@@ -508,28 +508,34 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
         P[t] = mk3(bcast(pt.x, src), bcast(pt.y, src), bcast(pt.z, src));
         S[t] = bcast(sep, src);
     }
-    if (lane == 0) {
+    // append, or (list full) replace the shallowest contact if this one is deeper: the shallowest is the first
+    // maximum of sep over the list (the oracle's sequential strict-compare scan), found by a wave arg-max over
+    // lanes = contacts instead of a scan on lane 0 (clutter scenes run with the list full)
+    float mu = contact_friction(c, a, b);
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            if (t >= k) break;
-            int slot;
-            if (s.nc >= c.maxc) {
-                int w = 0;
-                for (int j = 1; j < c.maxc; j++)
-                    if (c.k[j].sep > c.k[w].sep) w = j;
-                if (c.k[w].sep <= S[t]) continue;
-                slot = w;
-            } else {
-                slot = s.nc++;
-            }
+    for (int t = 0; t < 4; t++) {
+        if (t >= k) break;
+        int nc = s.nc, slot;
+        if (nc >= c.maxc) {
+            float sv = lane < c.maxc ? c.k[lane].sep : -3.0e38f;
+            int w = lane;
+            wave_argmax(sv, w);
+            if (sv <= S[t]) continue;
+            slot = w;
+        } else {
+            slot = nc;
+        }
+        if (lane == 0) {
+            if (slot == nc) s.nc = nc + 1;
             ContactLDS& ct = c.k[slot];
             st3(ct.x, P[t]);
             st3(ct.n, n);
             ct.sep = S[t];
-            ct.mu = contact_friction(c, a, b);
+            ct.mu = mu;
             ct.a = a;
             ct.b = b;
         }
+        wsync();
     }
     wsync();
 }
