@@ -27,6 +27,7 @@
  *                                  (multi_object.py:792-809, ur5sih.py:361-374)
  *   ha_gather_obs                  compute_observations' torch.cat for a custom observation list
  *                                  (observable_vec_task.py:183-203)
+ *   ha_render_camera               render_all_camera_sensors + camera image refresh (utils/camera.py:278-311)
  * The fused entry points serve three tasks (ha_params_t.task): Ur5Sih (above), AllegroHand
  * (allegro_hand.py:586-633) and AllegroKuka (allegro_kuka_base.py:1355-1447).
  */
@@ -329,6 +330,24 @@ typedef struct ha_pointcloud_t {
 
 #define HA_MAX_OBS_SOURCES 4
 
+/* Camera sensors (hand_arm/utils/camera.py:84-333; cameras of Ur5SihMultiObject.yaml:35-53). The camera looks along
+ * its local +X axis with +Z up (Isaac Gym camera frame); images are [N][height][width] like the reference's
+ * current_sensor_observation. Each output is optional (NULL = skip). */
+#define HA_CAM_FROM_DEPTH 1u    /* ha_render_camera flag: skip ray casting, compute the point cloud from `depth` */
+typedef struct ha_camera_t {
+    float pos[3], quat[4];      /* camera pose in the env frame (xyzw) */
+    float fovx_deg;             /* horizontal field of view (camera.py:144-153) */
+    int32_t width, height;      /* resolution [width, height] (camera.py:179-185) */
+    float max_depth;            /* 10: depth clamp and validity of the point cloud (camera.py:302-306) */
+    float workspace[4];         /* x0, x1, y0, y1 of the point cloud's in-workspace test (camera.py:303-309) */
+    float goal_radius;          /* goal sphere radius (rendered, collides with nothing) */
+    int32_t static_seg[HA_MAX_STATIC]; /* segmentation id of each static box (table links 0, bin pieces 2) */
+    float* depth;               /* [N][H][W] view-space z of the hit (negative), -inf where the ray hits nothing */
+    int32_t* segmentation;      /* [N][H][W] segmentation id of the hit actor (table 0, robot 1, bin 2, object i
+                                 * 3 + i, goal 3 + n_obj; 0 on a miss) */
+    float* pointcloud;          /* [N][H][W][4] xyz in the env frame + validity (depth_image_to_global_points) */
+} ha_camera_t;
+
 typedef struct ha_handle_s* ha_handle;
 
 int ha_abi_version(void);
@@ -373,6 +392,11 @@ int ha_pointcloud_times(ha_handle h, float* out_ms, int32_t max, int32_t* n_out)
  * (<= HA_MAX_OBS_SOURCES) device pointers / row strides in floats; cols is a device int32 array. */
 int ha_gather_obs(ha_handle h, const float* const* sources, const int32_t* strides, int32_t n_sources,
                   const int32_t* cols, int32_t n_cols, float* out, void* stream);
+/* One camera for all envs (render_all_camera_sensors + refresh_{depth,segmentation,pointcloud}, camera.py:278-311):
+ * depth and segmentation by ray casting the collision geometry of the bound state, then the point cloud.
+ * view_inv: the inverse view matrix (row-vector convention, 16 floats, host memory) the point cloud uses, as
+ * camera.py:68 multiplies by view_mat.inverse(). Ur5Sih task only. */
+int ha_render_camera(ha_handle h, const ha_camera_t* cam, const float* view_inv, uint32_t flags, void* stream);
 
 #ifdef __cplusplus
 }

@@ -11,6 +11,7 @@
 
 #include "ak_task.h"
 #include "ha_pointcloud.h"
+#include "ha_camera.h"
 
 #define HA_ND 17         /* Ur5Sih DOF count (UR5 + SIH); AH_ND = 16 (Allegro) */
 
@@ -840,6 +841,59 @@ int ha_gather_obs(ha_handle h, const float* const* sources, const int32_t* strid
     g.n_cols = n_cols;
     unsigned total = (unsigned)n_cols * (unsigned)h->N;
     hipLaunchKernelGGL(ha_obs_gather_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, g);
+    HIPCHK(hipGetLastError());
+    return HA_OK;
+}
+
+int ha_render_camera(ha_handle h, const ha_camera_t* cam, const float* view_inv, uint32_t flags, void* stream) {
+    if (!h || !h->bound || !cam || !view_inv) return HA_E_ARG;
+    if (h->task != HA_TASK_UR5SIH || !h->st.object_indices || !h->st.goal_pos) return HA_E_STATE;
+    if (cam->width < 1 || cam->height < 1 || (long long)cam->width * cam->height > (1 << 24) ||
+        !(cam->fovx_deg > 0.0f && cam->fovx_deg < 180.0f) || !(cam->max_depth > 0.0f))
+        return HA_E_ARG;
+    if ((flags & HA_CAM_FROM_DEPTH) && (!cam->depth || !cam->pointcloud)) return HA_E_ARG;
+    if (h->NO > HA_MAX_OBJ) return HA_E_ARG;
+    ha_model_t hm;      // the host copy of the few model fields the launch needs
+    HIPCHK(hipMemcpy(&hm.n_link_hulls, &h->d_model->n_link_hulls, sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&hm.n_static, &h->d_model->n_static, sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&hm.body_robot0, &h->d_model->body_robot0, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (hm.n_link_hulls + h->NO + hm.n_static > HA_CAM_MAX_HULLS || hm.n_link_hulls > 256) return HA_E_MODEL;
+    CamLaunch L;
+    L.cam = *cam;
+    L.m = h->d_model;
+    L.root = h->st.root_state;
+    L.body = h->st.rigid_body_state;
+    L.object_indices = h->st.object_indices;
+    L.goal_pos = h->st.goal_pos;
+    L.N = h->N;
+    L.A = h->A;
+    L.B = h->B;
+    L.a0 = h->a0;
+    L.NO = h->NO;
+    L.body_robot0 = hm.body_robot0;
+    L.n_link_hulls = hm.n_link_hulls;
+    L.n_static = hm.n_static;
+    // camera frame (Isaac Gym: +X forward, +Y left, +Z up) -> view axes (x right = -Y, y up = Z, z back = -X)
+    const float* q = cam->quat;
+    float qn = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    float x = q[0] / qn, y = q[1] / qn, z = q[2] / qn, w = q[3] / qn;
+    float Rc[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
+                   2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+                   2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)};
+    for (int r = 0; r < 3; r++) {
+        L.R[3 * r + 0] = -Rc[3 * r + 1];
+        L.R[3 * r + 1] = Rc[3 * r + 2];
+        L.R[3 * r + 2] = -Rc[3 * r + 0];
+    }
+    const float pi = 3.14159265358979f;
+    L.tanx = tanf(0.5f * cam->fovx_deg * pi / 180.0f);
+    L.tany = L.tanx * (float)cam->height / (float)cam->width;
+    L.fu = 2.0f * L.tanx;               // 2 / proj[0][0] (camera.py:317)
+    L.fv = 2.0f * L.tany;               // 2 / proj[1][1] (camera.py:318)
+    for (int k = 0; k < 16; k++) L.vinv[k] = view_inv[k];
+    L.flags = flags;
+    int pixels = cam->width * cam->height;
+    hipLaunchKernelGGL(ha_camera_kernel, dim3((pixels + 255) / 256, h->N), dim3(256), 0, (hipStream_t)stream, L);
     HIPCHK(hipGetLastError());
     return HA_OK;
 }

@@ -40,6 +40,7 @@ SIGNATURES = {
     "ha_kernel_times": ([H, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32)], C.c_int),
     "ha_pointclouds": ([H, C.POINTER(HM.HaPointcloud), S], C.c_int),
     "ha_pointcloud_times": ([H, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32)], C.c_int),
+    "ha_render_camera": ([H, C.POINTER(HM.HaCamera), C.POINTER(C.c_float), C.c_uint32, S], C.c_int),
     "ha_gather_obs": ([H, C.POINTER(C.c_void_p), C.POINTER(C.c_int32), C.c_int32, fp, C.c_int32, fp, S], C.c_int),
 }
 

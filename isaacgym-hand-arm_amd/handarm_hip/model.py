@@ -176,6 +176,16 @@ class HaPointcloud(C.Structure):
                 ("flange_slot", C.c_int32)]
 
 
+CAM_FROM_DEPTH = 1
+
+
+class HaCamera(C.Structure):
+    """ha_camera_t (include/handarm_abi.h)."""
+    _fields_ = [("pos", C.c_float * 3), ("quat", C.c_float * 4), ("fovx_deg", C.c_float), ("width", C.c_int32),
+                ("height", C.c_int32), ("max_depth", C.c_float), ("workspace", C.c_float * 4), ("goal_radius", C.c_float),
+                ("static_seg", C.c_int32 * MAX_STATIC), ("depth", P), ("segmentation", P), ("pointcloud", P)]
+
+
 def null_fields(task):
     """State buffers left NULL for a task: object_scale switches the physics to per-env scaled object
     geometry, which only AllegroKuka's cuboid family uses (bit-identical unscaled path otherwise)."""

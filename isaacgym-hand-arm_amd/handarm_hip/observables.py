@@ -82,7 +82,7 @@ def obs_columns(observations, n_objects):
     size = dict(zip(DEFAULT_OBSERVATIONS, sizes))
     cols = []
     for n in observations:
-        if n in POINTCLOUDS:
+        if n in POINTCLOUDS or n.endswith(("_depth", "_segmentation", "_pointcloud", "_color")):
             continue
         if n in start:
             cols += [(0, start[n] + k) for k in range(size[n])]

@@ -24,6 +24,7 @@ from .. import _lib
 from .. import model as HM
 from .. import observables as OB
 from .. import parallel
+from ..cameras import IMAGE_TYPES, CameraSensor
 from ..pointclouds import SyntheticPointclouds
 from ..sim import HandArmSim
 from ..torch_utils import randomize_rotation, torch_rand_float
@@ -209,7 +210,29 @@ class Ur5SihMultiObjectManipulation:
         if teacher != OB.DEFAULT_OBSERVATIONS:
             raise NotImplementedError("teacher_observations: this build writes the default teacher list "
                                       f"{OB.DEFAULT_OBSERVATIONS}")
-        order = OB.post_step_order(self.obs_names, teacher)
+        # camera observables `{camera}_{depth,segmentation,pointcloud}` (observable_vec_task.py:36-82): one sensor
+        # per camera of cfg["cameras"] that the list names; refreshed after every other observable
+        # (configurable_vec_task.py:91-114), so they do not enter the post-step order
+        self.cameras, self.camera_obs = {}, {}
+        for cam_name, cam_cfg in (_get(cfg, "cameras", {}) or {}).items():
+            kinds = [n[len(cam_name) + 1:] for n in self.obs_names if n.startswith(cam_name + "_")]
+            if not kinds:
+                continue
+            for k in kinds:
+                if k not in IMAGE_TYPES:
+                    raise NotImplementedError(f"camera observable {cam_name}_{k}: this build renders {IMAGE_TYPES}")
+            if "pos" not in cam_cfg:
+                raise NotImplementedError(f"camera {cam_name}: ROS cameras are out of scope")
+            self.cameras[cam_name] = CameraSensor(self.sim, cam_cfg["pos"], cam_cfg["quat"], cam_cfg.get("fovx", 87),
+                                                  cam_cfg.get("resolution", (160, 90)), kinds, self.scene)
+            for k in kinds:
+                self.camera_obs[f"{cam_name}_{k}"] = (cam_name, k)
+        for n in self.obs_names:
+            if n.endswith(("_pointcloud", "_depth", "_segmentation", "_color")) and n not in OB.POINTCLOUDS \
+                    and n not in self.camera_obs:
+                raise NotImplementedError(f"observable {n!r}: this build produces the synthetic clouds "
+                                          f"{OB.POINTCLOUDS} and camera images {IMAGE_TYPES} of cfg['cameras']")
+        order = OB.post_step_order([n for n in self.obs_names if n not in self.camera_obs], teacher)
         if not OB.sees_previous_object_pose(order, "object_bounding_box"):
             raise NotImplementedError("observation list refreshes object_bounding_box after object_pos; the step "
                                       "kernel implements the default order (bbox sees the previous pose)")
@@ -251,6 +274,10 @@ class Ur5SihMultiObjectManipulation:
         if self.pointclouds is not None:
             for n, t in self.pointclouds.outputs.items():
                 self.obs_dict[n] = t.to(self.rl_device)
+        for n, (cam, kind) in self.camera_obs.items():
+            img = self.cameras[cam].images[kind]
+            # PointcloudObservable's FlattenPointcloud transform (transforms.py:17-20): (N, H * W, 4)
+            self.obs_dict[n] = (img.flatten(1, 2) if kind == "pointcloud" else img).to(self.rl_device)
         self.obs_dict["teacher"] = {"obs": torch.clamp(self.teacher_obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)}
         return self.obs_dict
 
@@ -296,7 +323,7 @@ class Ur5SihMultiObjectManipulation:
         # observable_vec_task.py:205-211: "obs" for low-dimensional observables, the name for point clouds
         keys = []
         for n in self.obs_names:
-            k = n if n in OB.POINTCLOUDS else "obs"
+            k = n if (n in OB.POINTCLOUDS or n in self.camera_obs) else "obs"
             if k not in keys:
                 keys.append(k)
         return keys
@@ -438,6 +465,8 @@ class Ur5SihMultiObjectManipulation:
         self.sim.task_step(self.sim_flags)
         if self.pointclouds is not None:           # the clouds' post_step refresh, one launch
             self.pointclouds.refresh()
+        for cam in self.cameras.values():          # render_all_camera_sensors + image refresh, one launch each
+            cam.render()
         self._stat_pending += 1
         self.control_steps += 1
         self.extras["time_outs"] = self.timeout_buf.view(torch.bool).to(self.rl_device)

@@ -471,7 +471,43 @@ def gen_pointclouds(path, student, N=8, steps=4, seed=5):
     print("post-step order:", list(t._sorted_observations.keys()))
 
 
+def gen_camera_pointcloud(path, N=6, W=24, H=14, seed=7):
+    """IsaacGymCameraSensor._compute_pointcloud (utils/camera.py:302-311, with depth_image_to_global_points :50-69
+    and global_to_environment_points :72-81) run unmodified on synthetic depth images (misses = -inf, depths
+    beyond max_depth, points in and out of the workspace). Isaac Gym's view matrices are global: env i's camera
+    sits at its grid offset (num_per_row = max(int(sqrt(N)), 2), spacing 1), which global_to_environment_points
+    removes again, so the expected points are env-local like the build's."""
+    sys.path.insert(0, os.path.join(HERE, "..", "..", "isaacgym-hand-arm_amd"))
+    from handarm_hip import cameras as CAM
+    camera = refload.load("isaacgymenvs.tasks.hand_arm.utils.camera")
+    g = torch.Generator().manual_seed(seed)
+    pos, quat, fovx = [0.28, 1.05, 0.5], [0.213, 0.213, -0.674, 0.674], 87.0     # Ur5SihMultiObject.yaml topview
+    depth = -(0.2 + 1.2 * torch.rand(N, H, W, generator=g))
+    depth[torch.rand(N, H, W, generator=g) < 0.1] = -float("inf")
+    depth[torch.rand(N, H, W, generator=g) < 0.05] = -12.0
+    num_per_row = max(int(np.sqrt(N)), 2)
+    views = []
+    for i in range(N):
+        off = np.array([(i % num_per_row) * 2.0, (i // num_per_row) * 2.0, 0.0])
+        views.append(torch.from_numpy(CAM.view_matrix(np.asarray(pos) + off, quat)))
+    P = CAM.projection_matrix(fovx, W, H)
+    sensor = object.__new__(camera.IsaacGymCameraSensor)
+    sensor.device = "cpu"
+    sensor.current_sensor_observation = {camera.ImageType.DEPTH: depth.clone()}
+    proj = torch.from_numpy(P)
+    sensor._projection_matrix = torch.Tensor([[2 / proj[0, 0], 0., 0.], [0., 2 / proj[1, 1], 0.], [0., 0., 1.]])
+    sensor._view_matrix = torch.stack(views)
+    pc = sensor._compute_pointcloud()
+    arrays = dict(depth=depth.numpy(), pointcloud=pc.numpy(), view_local=CAM.view_matrix(pos, quat),
+                  proj=P, pos=np.array(pos), quat=np.array(quat), fovx=np.array(fovx))
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, {k: v.shape for k, v in arrays.items()})
+
+
 if __name__ == "__main__":
+    if "--camera" in sys.argv:
+        gen_camera_pointcloud(os.path.join(HERE, "camera_pointcloud.npz"))
+        sys.exit(0)
     if "--pointclouds" in sys.argv:
         gen_pointclouds(os.path.join(HERE, "ur5sih_pointclouds_student.npz"), PC_STUDENT, seed=5)
         gen_pointclouds(os.path.join(HERE, "ur5sih_pointclouds_all.npz"), PC_ALL, seed=6)
