@@ -346,6 +346,10 @@ typedef struct ha_camera_t {
     int32_t* segmentation;      /* [N][H][W] segmentation id of the hit actor (table 0, robot 1, bin 2, object i
                                  * 3 + i, goal 3 + n_obj; 0 on a miss) */
     float* pointcloud;          /* [N][H][W][4] xyz in the env frame + validity (depth_image_to_global_points) */
+    float* target_pc;           /* [N][P][4] {camera}_target_object_pointcloud (multi_object.py:837-855): the target
+                                 * object's points (segmentation 3 + target index); needs segmentation and pointcloud */
+    int32_t target_points;      /* P = pointclouds.max_num_points */
+    uint32_t rng_counter;       /* per-call counter of the random subset when more than P points are on the target */
 } ha_camera_t;
 
 typedef struct ha_handle_s* ha_handle;

@@ -175,3 +175,128 @@ extern "C" __global__ void __launch_bounds__(256) ha_camera_kernel(CamLaunch L) 
         reinterpret_cast<float4*>(cam.pointcloud)[out] = v4;
     }
 }
+
+// {camera}_target_object_pointcloud (_refresh_segmented_pointcloud, multi_object.py:837-855): the camera points
+// whose segmentation is the target object's (3 + target index), in pixel order; more than P of them -> a uniformly
+// random subset of P (the reference: torch.randperm(len)[:P]; here the P smallest per-pixel hash keys, exact
+// radix select, written in pixel order), fewer -> zero padding; then w *= TARGET (2).
+// One workgroup per env; thread t owns the contiguous pixel strip [t C, (t + 1) C), so block prefix sums keep
+// pixel order.
+struct CamTargetLaunch {
+    const float* pointcloud;      // [N][H*W][4]
+    const int32_t* segmentation;  // [N][H*W]
+    const int64_t* target_index;  // [N]
+    float* out;                   // [N][P][4]
+    int N, HW, P;
+    uint64_t seed;
+    uint32_t counter;
+};
+
+__device__ __forceinline__ uint32_t cam_key(uint64_t seed, uint32_t counter, uint32_t env, uint32_t pix) {
+    return mix32(mix32(mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + counter)) + env) + pix * 0x9E3779B9u);
+}
+
+// exclusive block prefix sum of one int per thread (256 threads); returns the total
+__device__ __forceinline__ int cam_block_scan(int v, int* sh, int& total) {
+    const int tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        int x = tid >= off ? sh[tid - off] : 0;
+        __syncthreads();
+        sh[tid] += x;
+        __syncthreads();
+    }
+    total = sh[255];
+    int excl = sh[tid] - v;
+    __syncthreads();
+    return excl;
+}
+
+extern "C" __global__ void __launch_bounds__(256) ha_camera_target_kernel(CamTargetLaunch L) {
+    __shared__ int sh[256];
+    __shared__ int hist[256];
+    __shared__ uint32_t s_prefix;
+    __shared__ int s_need;
+    const int env = blockIdx.x, tid = threadIdx.x;
+    const int C = (L.HW + 255) / 256;
+    const int p0 = tid * C, p1 = min(p0 + C, L.HW);
+    const int tgt = 3 + (int)L.target_index[env];
+    const int32_t* seg = L.segmentation + (size_t)env * L.HW;
+    const float4* pc = reinterpret_cast<const float4*>(L.pointcloud) + (size_t)env * L.HW;
+    float4* out = reinterpret_cast<float4*>(L.out) + (size_t)env * L.P;
+    int mine = 0;
+    for (int p = p0; p < p1; p++) mine += seg[p] == tgt;
+    int K;
+    int off = cam_block_scan(mine, sh, K);
+    if (K <= L.P) {
+        // all target points in pixel order, then zero padding (multi_object.py:848-850)
+        int j = off;
+        for (int p = p0; p < p1; p++)
+            if (seg[p] == tgt) {
+                float4 v = pc[p];
+                v.w *= 2.0f;
+                out[j++] = v;
+            }
+        for (int j2 = K + tid; j2 < L.P; j2 += 256) out[j2] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
+    // K > P: the P smallest keys among the target pixels (radix select over 4 bytes, most significant first)
+    uint32_t prefix = 0;
+    int need = L.P;                 // how many of the remaining candidates (keys with this prefix) to take
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        hist[tid] = 0;
+        __syncthreads();
+        const uint32_t hi_mask = shift == 24 ? 0u : (0xFFFFFFFFu << (shift + 8));
+        for (int p = p0; p < p1; p++) {
+            if (seg[p] != tgt) continue;
+            const uint32_t k = cam_key(L.seed, L.counter, env, p);
+            if ((k & hi_mask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int acc = 0, b = 0;
+            for (; b < 256; b++) {
+                if (acc + hist[b] >= need) break;
+                acc += hist[b];
+            }
+            s_prefix = prefix | ((uint32_t)b << shift);
+            s_need = need - acc;
+        }
+        __syncthreads();
+        prefix = s_prefix;
+        need = s_need;
+    }
+    // selected: key < T, plus the first `need` pixels (pixel order) whose key == T
+    const uint32_t T = prefix;
+    int lt = 0, eq = 0;
+    for (int p = p0; p < p1; p++) {
+        if (seg[p] != tgt) continue;
+        const uint32_t k = cam_key(L.seed, L.counter, env, p);
+        lt += k < T;
+        eq += k == T;
+    }
+    int nlt, neq;
+    const int off_lt = cam_block_scan(lt, sh, nlt);
+    const int off_eq = cam_block_scan(eq, sh, neq);
+    // output slots in pixel order: a selected pixel's slot = (selected pixels before it)
+    int sel_here = lt + max(0, min(eq, need - off_eq));
+    int tot;
+    int j = cam_block_scan(sel_here, sh, tot);
+    (void)off_lt;
+    int eq_seen = off_eq;
+    for (int p = p0; p < p1; p++) {
+        if (seg[p] != tgt) continue;
+        const uint32_t k = cam_key(L.seed, L.counter, env, p);
+        bool take = k < T;
+        if (k == T) {
+            take = eq_seen < need;
+            eq_seen++;
+        }
+        if (take) {
+            float4 v = pc[p];
+            v.w *= 2.0f;
+            out[j++] = v;
+        }
+    }
+}

@@ -893,8 +893,24 @@ int ha_render_camera(ha_handle h, const ha_camera_t* cam, const float* view_inv,
     for (int k = 0; k < 16; k++) L.vinv[k] = view_inv[k];
     L.flags = flags;
     int pixels = cam->width * cam->height;
+    if (cam->target_pc && (!cam->segmentation || !cam->pointcloud || cam->target_points < 1 || !h->st.target_object_index))
+        return HA_E_ARG;
     hipLaunchKernelGGL(ha_camera_kernel, dim3((pixels + 255) / 256, h->N), dim3(256), 0, (hipStream_t)stream, L);
     HIPCHK(hipGetLastError());
+    if (cam->target_pc) {
+        CamTargetLaunch T;
+        T.pointcloud = cam->pointcloud;
+        T.segmentation = cam->segmentation;
+        T.target_index = h->st.target_object_index;
+        T.out = cam->target_pc;
+        T.N = h->N;
+        T.HW = pixels;
+        T.P = cam->target_points;
+        T.seed = h->h_params.seed;
+        T.counter = cam->rng_counter;
+        hipLaunchKernelGGL(ha_camera_target_kernel, dim3(h->N), dim3(256), 0, (hipStream_t)stream, T);
+        HIPCHK(hipGetLastError());
+    }
     return HA_OK;
 }
 

@@ -20,7 +20,7 @@ import torch
 from . import _lib
 from . import model as HM
 
-IMAGE_TYPES = ("depth", "segmentation", "pointcloud")
+IMAGE_TYPES = ("depth", "segmentation", "pointcloud", "target_object_pointcloud")
 WORKSPACE = (-0.07, 0.63, 0.33, 0.83)     # camera.py:303-304 x_range, y_range
 MAX_DEPTH = 10.0                          # camera.py:302
 
@@ -67,7 +67,7 @@ class CameraSensor:
     segmentation (N, H, W) int32, pointcloud (N, H, W, 4) f32 - the reference's current_sensor_observation."""
 
     def __init__(self, sim, pos, quat, fovx=87, resolution=(160, 90), outputs=IMAGE_TYPES, scene=None,
-                 max_depth=MAX_DEPTH, workspace=WORKSPACE):
+                 max_depth=MAX_DEPTH, workspace=WORKSPACE, max_num_points=128):
         if sim.task != HM.TASK_UR5SIH:
             raise NotImplementedError("camera sensors are built for the Ur5Sih scenes")
         for k in outputs:
@@ -90,10 +90,14 @@ class CameraSensor:
         self.images = {}
         if "depth" in outputs or "pointcloud" in outputs:
             self.images["depth"] = torch.zeros((N, H, W), dtype=torch.float32, device=dev)
-        if "segmentation" in outputs:
+        target = "target_object_pointcloud" in outputs      # needs the segmentation and the point cloud
+        if "segmentation" in outputs or target:
             self.images["segmentation"] = torch.zeros((N, H, W), dtype=torch.int32, device=dev)
-        if "pointcloud" in outputs:
+        if "pointcloud" in outputs or target:
             self.images["pointcloud"] = torch.zeros((N, H, W, 4), dtype=torch.float32, device=dev)
+        if target:
+            self.images["target_object_pointcloud"] = torch.zeros((N, int(max_num_points), 4), dtype=torch.float32,
+                                                                  device=dev)
         c = HM.HaCamera()
         c.pos[:] = [float(v) for v in pos]
         c.quat[:] = [float(v) for v in quat]
@@ -108,6 +112,9 @@ class CameraSensor:
         c.depth = self.images["depth"].data_ptr() if "depth" in self.images else None
         c.segmentation = self.images["segmentation"].data_ptr() if "segmentation" in self.images else None
         c.pointcloud = self.images["pointcloud"].data_ptr() if "pointcloud" in self.images else None
+        c.target_pc = self.images["target_object_pointcloud"].data_ptr() if target else None
+        c.target_points = int(max_num_points)
+        c.rng_counter = 0
         self.args = c
         self._vinv = (C.c_float * 16)(*self.view_inv.reshape(-1).tolist())
 
@@ -120,5 +127,6 @@ class CameraSensor:
         """render_all_camera_sensors + refresh of every image (one launch). from_depth: only recompute the point
         cloud from images["depth"] (HA_CAM_FROM_DEPTH)."""
         flags = HM.CAM_FROM_DEPTH if from_depth else 0
+        self.args.rng_counter = (self.args.rng_counter + 1) & 0xFFFFFFFF     # a fresh random subset per refresh
         _lib.check(self.sim.lib.ha_render_camera(self.sim.h, C.byref(self.args), self._vinv, flags,
                                                  self.sim._stream()), "ha_render_camera")

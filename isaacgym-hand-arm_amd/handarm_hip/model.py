@@ -183,7 +183,8 @@ class HaCamera(C.Structure):
     """ha_camera_t (include/handarm_abi.h)."""
     _fields_ = [("pos", C.c_float * 3), ("quat", C.c_float * 4), ("fovx_deg", C.c_float), ("width", C.c_int32),
                 ("height", C.c_int32), ("max_depth", C.c_float), ("workspace", C.c_float * 4), ("goal_radius", C.c_float),
-                ("static_seg", C.c_int32 * MAX_STATIC), ("depth", P), ("segmentation", P), ("pointcloud", P)]
+                ("static_seg", C.c_int32 * MAX_STATIC), ("depth", P), ("segmentation", P), ("pointcloud", P),
+                ("target_pc", P), ("target_points", C.c_int32), ("rng_counter", C.c_uint32)]
 
 
 def null_fields(task):

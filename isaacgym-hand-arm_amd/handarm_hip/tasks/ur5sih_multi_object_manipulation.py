@@ -224,7 +224,8 @@ class Ur5SihMultiObjectManipulation:
             if "pos" not in cam_cfg:
                 raise NotImplementedError(f"camera {cam_name}: ROS cameras are out of scope")
             self.cameras[cam_name] = CameraSensor(self.sim, cam_cfg["pos"], cam_cfg["quat"], cam_cfg.get("fovx", 87),
-                                                  cam_cfg.get("resolution", (160, 90)), kinds, self.scene)
+                                                  cam_cfg.get("resolution", (160, 90)), kinds, self.scene,
+                                                  max_num_points=int(_get(cfg, "pointclouds.max_num_points", 128)))
             for k in kinds:
                 self.camera_obs[f"{cam_name}_{k}"] = (cam_name, k)
         for n in self.obs_names:

@@ -136,3 +136,16 @@ def pointcloud_from_depth(depth, fu, fv, view_inv, max_depth=10.0, workspace=(-0
     valid = ((depth > F(-max_depth)) & (xyz[..., 0] > F(workspace[0])) & (xyz[..., 0] < F(workspace[1]))
              & (xyz[..., 1] > F(workspace[2])) & (xyz[..., 1] < F(workspace[3])))
     return np.concatenate([xyz, valid[..., None].astype(F)], -1)
+
+
+def target_pointcloud(pointcloud, segmentation, target_index, P):
+    """{camera}_target_object_pointcloud (multi_object.py:837-855) where the target has <= P points: the target's
+    points in pixel order, zero padding, w *= 2. pointcloud (N, H*W, 4), segmentation (N, H*W)."""
+    N = pointcloud.shape[0]
+    out = np.zeros((N, P, 4), F)
+    for e in range(N):
+        pts = pointcloud[e][segmentation[e] == 3 + int(target_index[e])]
+        assert len(pts) <= P
+        out[e, :len(pts)] = pts
+    out[..., 3] *= F(2)
+    return out

@@ -107,3 +107,46 @@ def test_camera_observables_through_vectask():
     with pytest.raises(NotImplementedError):
         Ur5SihMultiObjectManipulation({"env": {"numEnvs": 4, "observations": ["topview_color"]},
                                        "cameras": {"topview": dict(TOPVIEW)}}, "cuda:0", "cuda:0")
+
+
+def test_target_object_pointcloud():
+    """<= P target points: exactly the oracle (pixel order, zero padding, w x 2); > P: P distinct target points
+    (a random subset: every selected point is a target pixel's point, no repeats), a different subset per refresh."""
+    need_gpu()
+    from handarm_hip.sim import HandArmSim
+    from tests import scenes
+    from oracle.oracle_lib import HostState
+    N, W, H = 8, 160, 90
+    sim = HandArmSim(N, "cuda:0")
+    st = HostState(N, model=sim.model, params=sim.params)
+    scenes.fill_scene(st, N, seed=4)
+    for k in ("root_state", "dof_state", "sim_targets", "object_indices", "goal_pos"):
+        sim.t[k].copy_(torch.from_numpy(np.ascontiguousarray(st[k])).reshape(sim.t[k].shape).to(sim.t[k].dtype))
+    sim.simulate(10)
+    for P in (4096, 64):
+        cam = CAM.CameraSensor(sim, TOPVIEW["pos"], TOPVIEW["quat"], TOPVIEW["fovx"], (W, H),
+                               ["target_object_pointcloud"], max_num_points=P)
+        for tgt in range(3):
+            sim.t["target_object_index"].fill_(tgt)
+            cam.render()
+            pc = cpu(cam.images["pointcloud"]).reshape(N, -1, 4)
+            seg = cpu(cam.images["segmentation"]).reshape(N, -1)
+            got = cpu(cam.images["target_object_pointcloud"])
+            counts = (seg == 3 + tgt).sum(1)
+            if P == 4096:
+                assert counts.max() <= P
+                np.testing.assert_array_equal(got, CO.target_pointcloud(pc, seg, np.full(N, tgt), P))
+                continue
+            first = got.copy()
+            cam.render()
+            again = cpu(cam.images["target_object_pointcloud"])
+            for e in range(N):
+                pts = pc[e][seg[e] == 3 + tgt].copy()
+                pts[:, 3] *= 2
+                k = min(counts[e], P)
+                rows = {tuple(r) for r in pts.tolist()}
+                assert all(tuple(r) in rows for r in first[e, :k].tolist())
+                assert len({tuple(r) for r in first[e, :k].tolist()}) == len({tuple(r) for r in pts.tolist()} & {tuple(r) for r in first[e, :k].tolist()})
+                assert np.all(first[e, k:] == 0)
+                if counts[e] > P + 16:
+                    assert not np.array_equal(first[e], again[e])
