@@ -121,27 +121,50 @@ HD int compact_index(int lane, int D, int so0, int so1) {
 // LDS block of one env: EnvLDS up to the phase union, the union at the task's row stride and contact
 // chunks (J and Y of MAXR x chunks rows), then the object slots (ObjLDS x capacity), then the contact list
 // (ContactLDS x MAXC x chunks), 16-byte aligned
-__host__ __device__ inline size_t obj_lds_offset(int rs, int nch) {
-    size_t rows = 2 * (size_t)MAXR * nch * rs * sizeof(float);
+__host__ __device__ inline size_t obj_lds_offset_rows(size_t rows) {
     size_t u = sizeof(PostScratch) > sizeof(ColScratch) ? sizeof(PostScratch) : sizeof(ColScratch);
     if (rows > u) u = rows;
     return (offsetof(EnvLDS, u) + u + 15) & ~(size_t)15;
 }
-__host__ __device__ inline size_t contact_lds_offset(int rs, int obj_capacity, int nch) {
-    return obj_lds_offset(rs, nch) + (size_t)obj_capacity * sizeof(ObjLDS);
-}
-__host__ __device__ inline size_t task_lds_bytes(int rs, int obj_capacity, int nch) {
-    return contact_lds_offset(rs, obj_capacity, nch) + (size_t)MAXC * nch * sizeof(ContactLDS);
-}
 
 // Compile-time shape of a kernel family's physics: DOF count, object slots, contact chunks (MAXC contacts
 // each) and velocity words per lane (coordinates lane and lane + 64 when D + 6 x objects > 64).
-template <int ND, int OCAP, int NCH>
+//
+// Split rows (the clutter family, split = true): most clutter contacts touch no robot link (object-bin,
+// object-object), and such a row's robot block is zero in J and in Y = M^-1 J^T. The rows then keep only
+// their two 6-wide object blocks in LDS (12 floats each of J and Y), and the robot blocks of the contacts that
+// do touch a link get a slot of their own: the first KL link contacts in LDS, the rest in a per-env global
+// spill area (ha_create allocates it; L2-resident, rare). Every dot product visits the nonzero terms in the
+// dense order and a skipped zero block adds exact zeros, so results are bit-identical to the dense rows.
+template <int ND, int OCAP, int NCH, int KL = 8>
 struct PhysCfg {
     static constexpr int nd = ND, ocap = OCAP, nch = NCH;
     static constexpr int vw = ND + 6 * OCAP > 64 ? 2 : 1;
+#ifdef HA_DENSE_ROWS    /* diagnostic build (tools/split_rows_check.py): every family on dense rows */
+    static constexpr bool split = false;
+#else
+    static constexpr bool split = OCAP > 3;
+#endif
+    static constexpr int kl = KL;
+    static constexpr int spill_floats = split ? 2 * 3 * (MAXC * NCH - KL) * ND : 0;   // per env: J then Y
     static_assert(ND + 6 * OCAP <= MAXV, "generalized velocity exceeds MAXV");
+    static_assert(!split || (row_slots<ND>() == 2 && MAXC * NCH <= 64), "split rows: two object slots, <= 64 contacts");
 };
+template <class PC>
+__host__ __device__ constexpr size_t pc_rows_bytes() {
+    return PC::split ? 2 * sizeof(float) * ((size_t)MAXR * PC::nch * 12 + 3 * (size_t)PC::kl * PC::nd)
+                     : 2 * sizeof(float) * (size_t)MAXR * PC::nch * row_stride<PC::nd>();
+}
+template <class PC>
+__host__ __device__ inline size_t obj_lds_offset() { return obj_lds_offset_rows(pc_rows_bytes<PC>()); }
+template <class PC>
+__host__ __device__ inline size_t contact_lds_offset() {
+    return obj_lds_offset<PC>() + (size_t)PC::ocap * sizeof(ObjLDS);
+}
+template <class PC>
+__host__ __device__ inline size_t task_lds_bytes() {
+    return contact_lds_offset<PC>() + (size_t)MAXC * PC::nch * sizeof(ContactLDS);
+}
 
 struct SimCtx {
     const ha_model_t* __restrict__ m;
@@ -152,6 +175,7 @@ struct SimCtx {
     int lane, D, NO, L;
     int maxc;               // contact capacity (MAXC x chunks of the kernel family)
     const float* dr;        // this env's domain-randomization row (HA_DR_*), or null when DR is off
+    float* spill;           // split rows: this env's global robot-block rows beyond the LDS slots (J, then Y)
 };
 
 // friction of a contact body (link 100+L, object o, static -1) and of a contact (PhysX average combine)
@@ -855,15 +879,15 @@ HD void detect(SimCtx& c) {
 }
 
 // ----------------------------------------------------------------------------- constraint rows
-// Jacobian of body `body` into the compact row J (object blocks at their slot: so0 -> 0, else 1)
-HD void jac_body(const SimCtx& c, int body, f3 x, f3 dir, float sgn, float* J, int so0) {
+// Jacobian of body `body` into a compact row: robot block J (D wide; only touched for a link) and object
+// blocks Job (slot so0 -> 0, else 1; Job = J + D for a dense row)
+HD void jac_body(const SimCtx& c, int body, f3 x, f3 dir, float sgn, float* J, float* Job, int so0) {
     const EnvLDS& s = *c.s;
-    int D = c.D;
     if (body < 0) return;
     if (body < 100) {
         f3 r = x - ld3(c.o[body].oc);
         f3 ang = cross3(r, dir);
-        float* Jo = J + D + (body == so0 ? 0 : 6);
+        float* Jo = Job + (body == so0 ? 0 : 6);
         Jo[0] += sgn * dir.x; Jo[1] += sgn * dir.y; Jo[2] += sgn * dir.z;
         Jo[3] += sgn * ang.x; Jo[4] += sgn * ang.y; Jo[5] += sgn * ang.z;
         return;
@@ -960,6 +984,23 @@ HD void substep(SimCtx& c, float hdt) {
     float* Yb = Jb + MAXR * NCH * RSN;
     int nc = s.nc;
     int nr = 3 * nc;    // nc <= MAXC x NCH -> <= MAXR x NCH rows
+    // split rows (PhysCfg): object blocks of every row (OW = 12 wide, J then Y), then the robot blocks of the
+    // first KL link contacts (J then Y), then the env's global spill area for the link contacts after those
+    constexpr int OW = 12, KL = PC::kl, SPJ = 3 * (MAXC * NCH - KL) * ND;
+    float* Ob = Jb;
+    float* ObY = Ob + MAXR * NCH * OW;
+    float* Rb = ObY + MAXR * NCH * OW;
+    float* RbY = Rb + 3 * KL * ND;
+    uint64_t lmask = 0;     // contacts that touch a robot link (split rows only)
+    if constexpr (PC::split) lmask = __ballot(lane < nc && (c.k[lane].a >= 100 || c.k[lane].b >= 100));
+    // robot-block slot of contact ci (-1: no link), and row k of its J or Y robot block
+    auto lslot = [&](int ci) -> int {
+        return ((lmask >> ci) & 1ull) ? (int)__popcll(lmask & ((1ull << ci) - 1ull)) : -1;
+    };
+    auto rrow = [&](int ls, int k, bool y) -> float* {
+        if (ls < KL) return (y ? RbY : Rb) + (3 * ls + k) * ND;
+        return c.spill + (y ? SPJ : 0) + (3 * (ls - KL) + k) * ND;
+    };
     float vt[NCH], winv[NCH], lam[NCH], cmu[NCH];
 #pragma unroll
     for (int ch = 0; ch < NCH; ch++) {
@@ -968,17 +1009,33 @@ HD void substep(SimCtx& c, float hdt) {
         if (lane < MAXR && r < nr) {
             const ContactLDS& ct = c.k[r / 3];
             cmu[ch] = ct.mu;
-            float* Jr = Jb + r * RSN;
-            for (int k = 0; k < RSN; k++) Jr[k] = 0.0f;
             int k = r % 3;
+            // robot block Jr / Yr (null: the contact touches no link, the block is zero) and object blocks Jo / Yo
+            float *Jr, *Yr, *Jo, *Yo;
+            if constexpr (PC::split) {
+                int ls = lslot(r / 3);
+                Jr = ls >= 0 ? rrow(ls, k, false) : nullptr;
+                Yr = ls >= 0 ? rrow(ls, k, true) : nullptr;
+                Jo = Ob + r * OW;
+                Yo = ObY + r * OW;
+                for (int t = 0; t < OW; t++) Jo[t] = 0.0f;
+                if (Jr)
+                    for (int t = 0; t < ND; t++) Jr[t] = 0.0f;
+            } else {
+                Jr = Jb + r * RSN;
+                Yr = Yb + r * RSN;
+                Jo = Jr + D;
+                Yo = Yr + D;
+                for (int t = 0; t < RSN; t++) Jr[t] = 0.0f;
+            }
             f3 n = ld3(ct.n), t1, t2;
             tangents(n, t1, t2);
             f3 dir = k == 0 ? n : (k == 1 ? t1 : t2);
             f3 x = ld3(ct.x);
             int so0, so1;
             contact_slots(ct.a, ct.b, so0, so1);
-            jac_body(c, ct.a, x, dir, 1.0f, Jr, so0);
-            jac_body(c, ct.b, x, dir, -1.0f, Jr, so0);
+            jac_body(c, ct.a, x, dir, 1.0f, Jr, Jo, so0);
+            jac_body(c, ct.b, x, dir, -1.0f, Jr, Jo, so0);
             if (k == 0) {
                 float sp = ct.sep;
                 float v0 = sp > 0 ? -sp / hdt : -p.baumgarte * sp / hdt;
@@ -986,27 +1043,31 @@ HD void substep(SimCtx& c, float hdt) {
                 vt[ch] = v0;
             }
             // Y_r = M^-1 J_r^T (robot block through the explicit inverse, object blocks 1/m, I_w^-1)
-            float* Yr = Yb + r * RSN;
-            for (int i = 0; i < D; i++) {
-                float acc = 0.0f;
-                for (int j = 0; j < D; j++) acc += s.Minv[i * D + j] * Jr[j];
-                Yr[i] = acc;
+            if (Jr) {
+                for (int i = 0; i < D; i++) {
+                    float acc = 0.0f;
+                    for (int j = 0; j < D; j++) acc += s.Minv[i * D + j] * Jr[j];
+                    Yr[i] = acc;
+                }
             }
             for (int sl = 0; sl < row_slots<ND>(); sl++) {
                 int o = sl == 0 ? so0 : so1;
-                const float* Jo = Jr + D + 6 * sl;
-                float* Yo = Yr + D + 6 * sl;
+                const float* Jos = Jo + 6 * sl;
+                float* Yos = Yo + 6 * sl;
                 if (o < 0) {
-                    for (int t = 0; t < 6; t++) Yo[t] = 0.0f;
+                    for (int t = 0; t < 6; t++) Yos[t] = 0.0f;
                     continue;
                 }
                 float im = 1.0f / c.o[o].om;
-                Yo[0] = Jo[0] * im; Yo[1] = Jo[1] * im; Yo[2] = Jo[2] * im;
-                f3 a = mv3(c.o[o].oIinv, mk3(Jo[3], Jo[4], Jo[5]));
-                Yo[3] = a.x; Yo[4] = a.y; Yo[5] = a.z;
+                Yos[0] = Jos[0] * im; Yos[1] = Jos[1] * im; Yos[2] = Jos[2] * im;
+                f3 a = mv3(c.o[o].oIinv, mk3(Jos[3], Jos[4], Jos[5]));
+                Yos[3] = a.x; Yos[4] = a.y; Yos[5] = a.z;
             }
+            // same term order as the dense row: robot block, then the object blocks
             float a = 0.0f;
-            for (int t = 0; t < RSN; t++) a += Jr[t] * Yr[t];
+            if (Jr)
+                for (int t = 0; t < D; t++) a += Jr[t] * Yr[t];
+            for (int t = 0; t < RSN - D; t++) a += Jo[t] * Yo[t];
             winv[ch] = 1.0f / (a + 1e-9f);
         }
     }
@@ -1019,16 +1080,33 @@ HD void substep(SimCtx& c, float hdt) {
         ca0[ch] = 0.f; ca1[ch] = 0.f;
         int r = MAXR * ch + lane;
         if (lane < MAXR && r < nr && r % 3 != 0) {
-            const float* Jr = Jb + r * RSN;
-            int r0 = r - r % 3;
-            const float* Y0 = Yb + r0 * RSN;
+            int k = r % 3, r0 = r - k;
+            const float *Jr, *Y0r, *Y1r, *Jo, *Y0o;
+            if constexpr (PC::split) {
+                int ls = lslot(r / 3);
+                Jr = ls >= 0 ? rrow(ls, k, false) : nullptr;
+                Y0r = ls >= 0 ? rrow(ls, 0, true) : nullptr;
+                Y1r = ls >= 0 ? rrow(ls, 1, true) : nullptr;
+                Jo = Ob + r * OW;
+                Y0o = ObY + r0 * OW;
+            } else {
+                Jr = Jb + r * RSN;
+                Y0r = Yb + r0 * RSN;
+                Y1r = Y0r + RSN;
+                Jo = Jr + D;
+                Y0o = Y0r + D;
+            }
+            const float* Y1o = Y0o + (PC::split ? OW : RSN);
             float a = 0.0f;
-            for (int t = 0; t < RSN; t++) a += Jr[t] * Y0[t];
+            if (Jr)
+                for (int t = 0; t < D; t++) a += Jr[t] * Y0r[t];
+            for (int t = 0; t < RSN - D; t++) a += Jo[t] * Y0o[t];
             ca0[ch] = a;
-            if (r % 3 == 2) {
-                const float* Y1 = Y0 + RSN;
+            if (k == 2) {
                 float b = 0.0f;
-                for (int t = 0; t < RSN; t++) b += Jr[t] * Y1[t];
+                if (Jr)
+                    for (int t = 0; t < D; t++) b += Jr[t] * Y1r[t];
+                for (int t = 0; t < RSN - D; t++) b += Jo[t] * Y1o[t];
                 ca1[ch] = b;
             }
         }
@@ -1112,15 +1190,40 @@ HD void substep(SimCtx& c, float hdt) {
                 ix = compact_index(lane, D, so0, so1);
                 if (VW == 2) ixh = compact_index(lane + 64, D, so0, so1);
             }
+            j0n = 0.f; j1n = 0.f; j2n = 0.f; y0n = 0.f; y1n = 0.f; y2n = 0.f;
+            h0n = 0.f; h1n = 0.f; h2n = 0.f; g0n = 0.f; g1n = 0.f; g2n = 0.f;
+            if constexpr (PC::split) {
+                // object coordinates from the LDS object blocks; robot coordinates from the contact's link slot
+                // (LDS for the first KL, else the global spill rows), absent -> 0
+                const float* On = Ob + 3 * ci * OW;
+                const float* OYn = ObY + 3 * ci * OW;
+                if (ix >= D) {
+                    int t = ix - D;
+                    j0n = On[t]; j1n = On[OW + t]; j2n = On[2 * OW + t];
+                    y0n = OYn[t]; y1n = OYn[OW + t]; y2n = OYn[2 * OW + t];
+                } else if (ix >= 0) {
+                    int ls = lslot(ci);
+                    if (ls >= 0) {
+                        const float* Rn = rrow(ls, 0, false);
+                        const float* RYn = rrow(ls, 0, true);
+                        j0n = Rn[ix]; j1n = Rn[ND + ix]; j2n = Rn[2 * ND + ix];
+                        y0n = RYn[ix]; y1n = RYn[ND + ix]; y2n = RYn[2 * ND + ix];
+                    }
+                }
+                if (VW == 2 && ixh >= D) {
+                    int t = ixh - D;
+                    h0n = On[t]; h1n = On[OW + t]; h2n = On[2 * OW + t];
+                    g0n = OYn[t]; g1n = OYn[OW + t]; g2n = OYn[2 * OW + t];
+                }
+                return;
+            }
             const float* Jn = J + 3 * ci * RSN;
             const float* Yn = Y + 3 * ci * RSN;
-            j0n = 0.f; j1n = 0.f; j2n = 0.f; y0n = 0.f; y1n = 0.f; y2n = 0.f;
             if (ix >= 0) {
                 j0n = Jn[ix]; j1n = Jn[RSN + ix]; j2n = Jn[2 * RSN + ix];
                 y0n = Yn[ix]; y1n = Yn[RSN + ix]; y2n = Yn[2 * RSN + ix];
             }
             if (VW == 2) {
-                h0n = 0.f; h1n = 0.f; h2n = 0.f; g0n = 0.f; g1n = 0.f; g2n = 0.f;
                 if (ixh >= 0) {
                     h0n = Jn[ixh]; h1n = Jn[RSN + ixh]; h2n = Jn[2 * RSN + ixh];
                     g0n = Yn[ixh]; g1n = Yn[RSN + ixh]; g2n = Yn[2 * RSN + ixh];

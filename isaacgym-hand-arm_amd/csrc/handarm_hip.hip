@@ -35,8 +35,13 @@ __host__ __device__ constexpr int task_obj_capacity() {
 // contact chunks (MAXC contacts each)
 template <int FAM>
 __host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5SIH_CLUTTER ? 2 : 1; }
+// clutter family: link contacts whose robot blocks stay in LDS (the rest use the global spill rows). 2 slots
+// keep the env block at <= 20 KB, i.e. 8 workgroups per CU (8 slots: 22.8 KB, 7 per CU)
+#ifndef HB_LINK_SLOTS
+#define HB_LINK_SLOTS 2
+#endif
 template <int FAM>
-using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>()>;
+using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>(), HB_LINK_SLOTS>;
 
 
 // ----------------------------------------------------------------------------- state load/store
@@ -266,7 +271,7 @@ static_assert(HA_ND + 6 * HA_MAX_OBJ <= MAXV, "bin-picking (8 objects) must fit 
 template <int FAM, int MODE>
 __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params,
                                          const ha_state_t& st, int num_envs, int n_calls, uint32_t flags,
-                                         int stat_slot) {
+                                         int stat_slot, float* __restrict__ spill) {
     constexpr int TASK = fam_task<FAM>();
     constexpr int ND = task_nd<FAM>();
     constexpr int NCH = task_contact_chunks<FAM>();
@@ -278,8 +283,9 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.m = model;
     c.p = params;
     c.s = reinterpret_cast<EnvLDS*>(smem);
-    c.o = reinterpret_cast<ObjLDS*>(smem + obj_lds_offset(row_stride<ND>(), NCH));
-    c.k = reinterpret_cast<ContactLDS*>(smem + contact_lds_offset(row_stride<ND>(), task_obj_capacity<FAM>(), NCH));
+    c.o = reinterpret_cast<ObjLDS*>(smem + obj_lds_offset<PC>());
+    c.k = reinterpret_cast<ContactLDS*>(smem + contact_lds_offset<PC>());
+    c.spill = PC::split ? spill + (size_t)env * PC::spill_floats : nullptr;
     c.maxc = MAXC * NCH;
     c.lane = threadIdx.x;
     c.D = ND;                     // == model->n_dofs (ha_create); a constant, so loops over D unroll
@@ -378,8 +384,8 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
 #define HA_KERNEL(name, FAM, MODE)                                                                              \
     extern "C" __global__ void __launch_bounds__(64)                                                          \
         name(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params, ha_state_t st,       \
-             int num_envs, int n_calls, uint32_t flags, int stat_slot) {                                        \
-        env_body<FAM, MODE>(model, params, st, num_envs, n_calls, flags, stat_slot);                           \
+             int num_envs, int n_calls, uint32_t flags, int stat_slot, float* spill) {                          \
+        env_body<FAM, MODE>(model, params, st, num_envs, n_calls, flags, stat_slot, spill);                    \
     }
 HA_KERNEL(ha_step_kernel, HA_TASK_UR5SIH, MODE_STEP)
 HA_KERNEL(ha_simulate_kernel, HA_TASK_UR5SIH, MODE_SIMULATE)
@@ -398,7 +404,7 @@ HA_KERNEL(ak_simulate_kernel, HA_TASK_ALLEGRO_KUKA, MODE_SIMULATE)
 HA_KERNEL(ak_observe_kernel, HA_TASK_ALLEGRO_KUKA, MODE_OBSERVE)
 HA_KERNEL(ak_reset_kernel, HA_TASK_ALLEGRO_KUKA, MODE_RESET)
 
-typedef void (*env_kernel_t)(const ha_model_t*, const ha_params_t*, ha_state_t, int, int, uint32_t, int);
+typedef void (*env_kernel_t)(const ha_model_t*, const ha_params_t*, ha_state_t, int, int, uint32_t, int, float*);
 static env_kernel_t kernel_for(int fam, int mode) {
     if (fam == FAM_UR5SIH_CLUTTER) {
         switch (mode) {
@@ -460,6 +466,7 @@ struct ha_handle_s {
     hipEvent_t* t_ev;     // 2 * t_max events
     int pc_count;
     hipEvent_t* pc_ev;    // 2 * t_max events (ha_pointclouds launches)
+    float* d_spill;       // split-row families: robot-block rows beyond the LDS slots, N x spill_floats
 };
 
 #define HIPCHK(x)                                                                     \
@@ -473,8 +480,9 @@ struct ha_handle_s {
 
 // per-family shape (object capacity, LDS bytes, row stride), from the same templates the kernels use
 template <int FAM>
-static size_t fam_lds_bytes() {
-    return task_lds_bytes(row_stride<task_nd<FAM>()>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>());
+static size_t fam_lds_bytes() { return task_lds_bytes<FamPhys<FAM>>(); }
+static size_t spill_floats(int fam) {
+    return fam == FAM_UR5SIH_CLUTTER ? (size_t)FamPhys<FAM_UR5SIH_CLUTTER>::spill_floats : 0;
 }
 static int obj_capacity(int fam) {
     switch (fam) {
@@ -564,6 +572,7 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     HIPCHK(hipMalloc(&h->d_params, sizeof(ha_params_t)));
     HIPCHK(hipMemcpy(h->d_model, model, sizeof(ha_model_t), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->d_params, params, sizeof(ha_params_t), hipMemcpyHostToDevice));
+    if (spill_floats(fam)) HIPCHK(hipMalloc(&h->d_spill, sizeof(float) * spill_floats(fam) * (size_t)num_envs));
     for (int mode : {MODE_STEP, MODE_SIMULATE, MODE_OBSERVE, MODE_RESET})
         HIPCHK(hipFuncSetAttribute((const void*)kernel_for(h->fam, mode), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds_bytes(h->fam)));
@@ -577,6 +586,7 @@ int ha_destroy(ha_handle h) {
     if (!h) return HA_E_ARG;
     (void)hipFree(h->d_model);
     (void)hipFree(h->d_params);
+    if (h->d_spill) (void)hipFree(h->d_spill);
     (void)hipEventDestroy(h->ev0);
     (void)hipEventDestroy(h->ev1);
     free(h);
@@ -600,7 +610,7 @@ static int launch(ha_handle h, int mode, int n_calls, uint32_t flags, int slot, 
     bool rec = h->t_ev && h->t_count < h->t_max;
     (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count] : h->ev0, s);
     hipLaunchKernelGGL(kernel_for(h->fam, mode), dim3(h->N), dim3(64), lds_bytes(h->fam), s, h->d_model, h->d_params, h->st,
-                       h->N, n_calls, flags, slot);
+                       h->N, n_calls, flags, slot, h->d_spill);
     HIPCHK(hipGetLastError());
     (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count + 1] : h->ev1, s);
     if (rec) {
