@@ -136,6 +136,9 @@ __host__ __device__ inline size_t obj_lds_offset_rows(size_t rows) {
 // do touch a link get a slot of their own: the first KL link contacts in LDS, the rest in a per-env global
 // spill area (ha_create allocates it; L2-resident, rare). Every dot product visits the nonzero terms in the
 // dense order and a skipped zero block adds exact zeros, so results are bit-identical to the dense rows.
+#ifndef HA_SPLIT_ABOVE_OCAP
+#define HA_SPLIT_ABOVE_OCAP 2   /* families with more object slots use split rows (Ur5Sih 3 objects, clutter) */
+#endif
 template <int ND, int OCAP, int NCH, int KL = 8>
 struct PhysCfg {
     static constexpr int nd = ND, ocap = OCAP, nch = NCH;
@@ -143,7 +146,7 @@ struct PhysCfg {
 #ifdef HA_DENSE_ROWS    /* diagnostic build (tools/split_rows_check.py): every family on dense rows */
     static constexpr bool split = false;
 #else
-    static constexpr bool split = OCAP > 3;
+    static constexpr bool split = OCAP > HA_SPLIT_ABOVE_OCAP;
 #endif
     static constexpr int kl = KL;
     static constexpr int spill_floats = split ? 2 * 3 * (MAXC * NCH - KL) * ND : 0;   // per env: J then Y

@@ -40,8 +40,18 @@ __host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5S
 #ifndef HB_LINK_SLOTS
 #define HB_LINK_SLOTS 2
 #endif
+#ifndef HA_LINK_SLOTS   /* the Ur5Sih 3-object family's LDS link slots (split rows, HA_SPLIT_ABOVE_OCAP) */
+#define HA_LINK_SLOTS 8
+#endif
+// minimum waves per SIMD asked of the Ur5Sih (3-object) kernels' register allocation: 3 (168 VGPRs, 72 B/lane
+// scratch) with split rows (15.1 KB LDS) runs 10 workgroups per CU instead of 8: C4 shard 5.01 -> 4.88 ms
+// (tools/ab_variants.sh ur5sih; 1 = the compiler's choice, 191 VGPRs)
+#ifndef HA_WAVES_PER_EU
+#define HA_WAVES_PER_EU 3
+#endif
 template <int FAM>
-using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>(), HB_LINK_SLOTS>;
+using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>(),
+                        FAM == FAM_UR5SIH_CLUTTER ? HB_LINK_SLOTS : HA_LINK_SLOTS>;
 
 
 // ----------------------------------------------------------------------------- state load/store
@@ -383,6 +393,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
 
 #define HA_KERNEL(name, FAM, MODE)                                                                              \
     extern "C" __global__ void __launch_bounds__(64)                                                          \
+        __attribute__((amdgpu_waves_per_eu(FAM == HA_TASK_UR5SIH ? HA_WAVES_PER_EU : 1)))                       \
         name(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params, ha_state_t st,       \
              int num_envs, int n_calls, uint32_t flags, int stat_slot, float* spill) {                          \
         env_body<FAM, MODE>(model, params, st, num_envs, n_calls, flags, stat_slot, spill);                    \
@@ -482,7 +493,12 @@ struct ha_handle_s {
 template <int FAM>
 static size_t fam_lds_bytes() { return task_lds_bytes<FamPhys<FAM>>(); }
 static size_t spill_floats(int fam) {
-    return fam == FAM_UR5SIH_CLUTTER ? (size_t)FamPhys<FAM_UR5SIH_CLUTTER>::spill_floats : 0;
+    switch (fam) {
+        case FAM_UR5SIH_CLUTTER: return FamPhys<FAM_UR5SIH_CLUTTER>::spill_floats;
+        case HA_TASK_ALLEGRO_HAND: return FamPhys<HA_TASK_ALLEGRO_HAND>::spill_floats;
+        case HA_TASK_ALLEGRO_KUKA: return FamPhys<HA_TASK_ALLEGRO_KUKA>::spill_floats;
+        default: return FamPhys<HA_TASK_UR5SIH>::spill_floats;
+    }
 }
 static int obj_capacity(int fam) {
     switch (fam) {

@@ -1,4 +1,4 @@
-"""Bit-identity check of the clutter family's split constraint rows (PhysCfg::split in csrc/ha_physics.h)
+"""Bit-identity check of the split constraint rows (clutter and Ur5Sih families) (PhysCfg::split in csrc/ha_physics.h)
 against a build that keeps every family on dense rows (-DHA_DENSE_ROWS).
 
     python tools/split_rows_check.py --build                  # here: libhandarm_hip_dense.so next to the product lib
@@ -8,7 +8,8 @@ against a build that keeps every family on dense rows (-DHA_DENSE_ROWS).
 
 Scenes (bin-picking, 8 objects, 256 envs, 3 gym.simulate calls each): the settled-clutter test scene; three
 objects on hand link hulls (more link contacts than the 8 LDS link slots -> global spill rows); eight objects
-on link hulls (contact list at capacity)."""
+on link hulls (contact list at capacity). Ur5Sih (3 objects, 256 envs, 3 calls): the test scene, and
+the three objects placed on hand link hulls (link contacts into the LDS link slots and beyond)."""
 import os
 import subprocess
 import sys
@@ -48,6 +49,29 @@ def run(kind, out):
             rs = st["root_state"].reshape(n, A, 13)
             rs[:, 4:4 + on_links, 0:3] = body[:, sim.model.body_robot0 + np.array(links), 0:3]
             rs[:, 4:4 + on_links, 7:13] = 0.0
+            for k, v in st.items():
+                sim.t[k].copy_(torch.as_tensor(v).reshape(sim.t[k].shape))
+        sim.simulate(3)
+        torch.cuda.synchronize()
+        for k in OUT_FIELDS:
+            res[f"{name}/{k}"] = sim.t[k].cpu().numpy().copy()
+        print(f"{kind} {name}: done", flush=True)
+    for name, on_links in [("ur5sih", 0), ("ur5sih_links", 3)]:
+        sim = HandArmSim(n, "cuda:0")
+        st = {k: sim.t[k].cpu().numpy().copy() for k in HM.STATE_FIELDS
+              if k not in ("stats", "term_sums") and k not in HM.null_fields(sim.task)}
+        scenes.fill_scene(st, n, seed=11, n_obj=sim.n_obj)
+        for k, v in st.items():
+            sim.t[k].copy_(torch.as_tensor(v).reshape(sim.t[k].shape))
+        if on_links:
+            sim.simulate(1)
+            torch.cuda.synchronize()
+            body = sim.t["rigid_body_state"].cpu().numpy().reshape(n, sim.num_bodies, 13)
+            hl = sorted({int(sim.model.hull_link[k]) for k in range(sim.model.n_link_hulls)})
+            links = [hl[-1 - 2 * i] for i in range(on_links)]
+            rs = st["root_state"].reshape(n, sim.num_actors, 13)
+            rs[:, 3:3 + on_links, 0:3] = body[:, sim.model.body_robot0 + np.array(links), 0:3]
+            rs[:, 3:3 + on_links, 7:13] = 0.0
             for k, v in st.items():
                 sim.t[k].copy_(torch.as_tensor(v).reshape(sim.t[k].shape))
         sim.simulate(3)
