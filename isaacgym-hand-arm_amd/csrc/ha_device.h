@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/ha_fmath.h"
+
 #define HD __device__ __forceinline__
 
 struct f3 { float x, y, z; };
@@ -34,8 +36,10 @@ HD qf qnormalize(qf q) {
     float n = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
     return qf{q.x / n, q.y / n, q.z / n, q.w / n};
 }
+// sin / cos from the shared ha_sincosf (include/ha_fmath.h): the same float32 operations as the C oracle
 HD qf qaxis(f3 a, float ang) {
-    float s = sinf(0.5f * ang), c = cosf(0.5f * ang);
+    float s, c;
+    ha_sincosf(0.5f * ang, &s, &c);
     return qf{a.x * s, a.y * s, a.z * s, c};
 }
 HD void qmat(qf q, float R[9]) {

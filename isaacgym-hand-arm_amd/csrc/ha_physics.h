@@ -367,14 +367,33 @@ HD void dynamics(SimCtx& c) {
         st3(&s.u.pd.dyn.Fl[i][0], fn); st3(&s.u.pd.dyn.Fl[i][3], ff);
     }
     wsync();
-    // backward accumulation of forces and composite inertia, deepest level first
-    for (int lev = m.max_level; lev >= 1; lev--) {
-        if (my_lev == lev) {
-            int i = lane, par = my_par;
+    // backward accumulation of forces and composite inertia, deepest level first. Each parent lane gathers
+    // its children itself, highest link index first: the oracle's order (it visits links L-1 .. 0 and adds
+    // each into its parent), so the float sums round identically. (LDS float atomics from the children
+    // would add in whatever order the hardware serialises them.)
+    uint32_t chm = 0;                           // this lane's child links (HA_MAX_LINKS = 32)
+    for (int j = 1; j < L; j++) chm |= (m.link_parent[j] == lane) ? (1u << j) : 0u;
+    for (int lev = m.max_level - 1; lev >= 0; lev--) {
+        if (my_lev == lev && chm) {
+            float* F = s.u.pd.dyn.Fl[lane];
+            float* C = s.u.pd.dyn.Ic[lane];
+            float f[6], ic[13];
 #pragma unroll
-            for (int k = 0; k < 6; k++) atomicAdd(&s.u.pd.dyn.Fl[par][k], s.u.pd.dyn.Fl[i][k]);
+            for (int k = 0; k < 6; k++) f[k] = F[k];
 #pragma unroll
-            for (int k = 0; k < 13; k++) atomicAdd(&s.u.pd.dyn.Ic[par][k], s.u.pd.dyn.Ic[i][k]);
+            for (int k = 0; k < 13; k++) ic[k] = C[k];
+            for (uint32_t mm = chm; mm;) {
+                int j = 31 - __clz(mm);
+                mm &= ~(1u << j);
+#pragma unroll
+                for (int k = 0; k < 6; k++) f[k] = f[k] + s.u.pd.dyn.Fl[j][k];
+#pragma unroll
+                for (int k = 0; k < 13; k++) ic[k] = ic[k] + s.u.pd.dyn.Ic[j][k];
+            }
+#pragma unroll
+            for (int k = 0; k < 6; k++) F[k] = f[k];
+#pragma unroll
+            for (int k = 0; k < 13; k++) C[k] = ic[k];
         }
         wsync();
     }

@@ -28,6 +28,7 @@
 #include <string.h>
 
 #include "../include/handarm_abi.h"
+#include "../include/ha_fmath.h"
 
 #define MAXC HA_MAX_CONTACTS   /* contact list capacity; a handle uses 21 (<= 3 objects) or 42 (clutter) */
 #define MAXR (3 * MAXC)
@@ -63,7 +64,8 @@ static qt qnorm(qt q) {
     return Q(q.x / n, q.y / n, q.z / n, q.w / n);
 }
 static qt qaxis(v3 a, float ang) {
-    float s = sinf(0.5f * ang), c = cosf(0.5f * ang);
+    float s, c;
+    ha_sincosf(0.5f * ang, &s, &c);     /* the kernels' sin / cos (include/ha_fmath.h), not libm */
     return Q(a.x * s, a.y * s, a.z * s, c);
 }
 /* 3x3 rotation from quat */

@@ -146,3 +146,22 @@ def fill_bin_scene(st, num_envs, scene, seed=0, n_obj=8, spread=1.0, pool=16):
     st["object_indices"][:] = bin_pool_ids(rng, N, n_obj, pool)
     st["collision_enabled"][:] = 1
     return st
+
+
+PHYSICS_OUTPUTS = ("dof_state", "root_state", "rigid_body_state", "net_contact_force", "dof_force")
+
+
+def assert_physics_bit_identical(sim, st, n, fields=PHYSICS_OUTPUTS, tag=""):
+    """Every physics output of every env is bit-identical between the HIP path (sim, through the C ABI) and
+    the C oracle (st): the kernels and oracle/physics_oracle.c evaluate the same float32 operations in the same
+    order (shared sin/cos in include/ha_fmath.h, the emulated DPP reduction tree, deterministic child sums,
+    correctly rounded division and square root on both sides, no contraction)."""
+    import torch
+    torch.cuda.synchronize()
+    for k in fields:
+        g = sim.t[k].cpu().numpy().reshape(n, -1)
+        o = np.asarray(st[k]).reshape(n, -1)
+        assert np.isfinite(g).all(), f"{tag} {k}: non-finite GPU output"
+        same = (g.view(np.uint32) == o.view(np.uint32)).all(1)
+        assert same.all(), (f"{tag} {k}: {int((~same).sum())}/{n} envs differ from the oracle, "
+                            f"max |d| {np.abs(g - o).max():.3e}")

@@ -117,29 +117,15 @@ def _oracle_and_sim(n, seed, force):
     return sim, O(sim.model, sim.params, n), st
 
 
-@pytest.mark.parametrize("seed,force", [(0, 0.0), (1, 0.5)])
-def test_kuka_simulate_single_call_matches_oracle(seed, force):
+@pytest.mark.parametrize("seed,force,calls", [(0, 0.0, 1), (1, 0.5, 1), (1, 0.5, 10)])
+def test_kuka_simulate_matches_oracle_bit_for_bit(seed, force, calls):
+    """AllegroKuka physics (per-env cuboid dimensions, object forces) vs the C oracle: bit-identical on every env."""
     n = 128
     sim, orc, st = _oracle_and_sim(n, seed, force)
-    pert = st.copy()
-    pd = pert["dof_state"].reshape(n, 23, 2)
-    pd[..., 0] = np.nextafter(pd[..., 0], np.float32(10))
-    sim.simulate(1)
-    orc.simulate(st, 1)
-    orc.simulate(pert, 1)
-    gd, od, sd = (x.reshape(n, 23, 2) for x in (get(sim, "dof_state"), st["dof_state"], pert["dof_state"]))
-    gr, orr, sr = (x.reshape(n, 4, 13) for x in (get(sim, "root_state"), st["root_state"], pert["root_state"]))
-    assert np.isfinite(gd).all() and np.isfinite(gr).all()
-    for a, b, c_, floor in [(gd[..., 0], od[..., 0], sd[..., 0], 1e-6), (gd[..., 1], od[..., 1], sd[..., 1], 1e-4),
-                            (gr[:, 1, 0:3], orr[:, 1, 0:3], sr[:, 1, 0:3], 1e-6),
-                            (gr[:, 1, 7:13], orr[:, 1, 7:13], sr[:, 1, 7:13], 1e-4)]:
-        err = np.abs(a - b).reshape(n, -1).max(1)
-        sens = np.abs(c_ - b).reshape(n, -1).max(1)
-        print("err max %.2e sens max %.2e" % (err.max(), sens.max()))
-        assert np.mean(err <= 10.0 * np.maximum(sens, floor)) >= 0.95, (err.max(), sens.max())
+    sim.simulate(calls)
+    orc.simulate(st, calls)
+    scenes.assert_physics_bit_identical(sim, st, n, tag=f"kuka seed {seed} force {force} calls {calls}")
     assert np.all(get(sim, "object_force") == 0)                 # consumed by the call, like the oracle
-    np.testing.assert_allclose(get(sim, "rigid_body_state").reshape(n, 27, 13)[:, :24, 0:3],
-                               st["rigid_body_state"].reshape(n, 27, 13)[:, :24, 0:3], atol=1e-4)
 
 
 @pytest.mark.parametrize("sub", ["regrasping", "reorientation"])
