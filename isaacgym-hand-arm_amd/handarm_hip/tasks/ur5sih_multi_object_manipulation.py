@@ -420,23 +420,11 @@ class Ur5SihMultiObjectManipulation:
         self.objects_dropped = True
 
     def _fold_stats(self):
-        """Fold the device-side per-step counters into log_data (reference :311-351 semantics)."""
-        k = self._stat_pending
-        if k == 0:
-            return
-        R = self.sim.stats_ring
-        slots = [(self._stat_folded + s) % R for s in range(k)]
-        stats = self.sim.t["stats"].cpu().numpy()[slots]
-        terms = self.sim.t["term_sums"].cpu().numpy()[slots]
-        self._stat_pending = 0
-        self._stat_folded += k
-        N = self.num_envs * getattr(self, "stat_scale", 1)   # global env count after a cross-rank reduce
-        log, self._success_rate_ewma, self._object_ewma, r, sc = parallel.fold_counts(
-            stats, terms, N, self._success_rate_ewma, self._object_ewma, self.objects)
-        self._log_data.update(log)
-        self.total_num_resets += r
-        self.total_num_successes += sc
-        assert R >= k
+        """Fold the device-side per-step counters into log_data (reference :311-351 semantics). With several
+        ranks only reduced slots are folded (parallel.reduce_episode_stats, a collective every rank runs at the
+        same step); rl_games reads log_data on rank 0 alone, so the fold here must not start a collective."""
+        if parallel.world() == 1:
+            parallel.fold_pending(self, self.num_envs)
 
     @property
     def log_data(self):
@@ -460,7 +448,7 @@ class Ur5SihMultiObjectManipulation:
         action_tensor = torch.clamp(actions, -self.clip_actions, self.clip_actions)
         self.actions_buf.copy_(action_tensor)
         if self._stat_pending == self.sim.stats_ring:
-            self._fold_stats()
+            parallel.reduce_episode_stats(self)      # ring full: reduce across ranks (if any), then fold
         if self.pointclouds is not None:           # object_pos as of the previous refresh (see observables.py)
             self.pointclouds.snapshot_object_pose(self.sim.t["obs_cache"])
         self.sim.task_step(self.sim_flags)

@@ -35,24 +35,42 @@ def local_counts(rank, k, first_slot):
     return stats, terms
 
 
+def shard_envs(rank):
+    return N_LOCAL + 16 * rank                      # unequal shards: the EWMA alpha needs the GLOBAL count
+
+
 def fake_env(rank, k, folded):
     stats, terms = local_counts(rank, k, folded % RING)
     sim = types.SimpleNamespace(stats_ring=RING, t={"stats": torch.from_numpy(stats), "term_sums": torch.from_numpy(terms)})
-    return types.SimpleNamespace(sim=sim, _stat_pending=k, _stat_folded=folded, num_envs=N_LOCAL)
+    return types.SimpleNamespace(sim=sim, _stat_pending=k, _stat_folded=folded, num_envs=shard_envs(rank),
+                                 objects=OBJECTS, _success_rate_ewma=0.0, _object_ewma=[0.0] * 3, _log_data={},
+                                 total_num_resets=0, total_num_successes=0)
 
 
-def _worker(rank, world, port, k, folded, q):
+def more_counts(rank, k2, first_slot):
+    """A second batch of pending steps (what the device writes between two log intervals)."""
+    return local_counts(rank + 10, k2, first_slot)
+
+
+def _worker(rank, world, port, k, folded, k2, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     try:
         env = fake_env(rank, k, folded)
         parallel.reduce_episode_stats(env)
-        slots = [(folded + s) % RING for s in range(k)]
-        st = env.sim.t["stats"].numpy()[slots]
-        tm = env.sim.t["term_sums"].numpy()[slots]
-        log, ewma, obj, r, s = parallel.fold_counts(st, tm, env.num_envs * env.stat_scale, 0.0, [0.0] * 3, OBJECTS)
-        q.put((rank, env.stat_scale, st.tolist(), tm.tolist(), log, ewma, obj, r, s))
+        assert env._stat_pending == 0 and env._stat_folded == folded + k
+        first = env.sim.t["stats"].numpy()[[(folded + s) % RING for s in range(k)]].copy()
+        parallel.reduce_episode_stats(env)          # nothing pending: no slot is reduced twice
+        again = env.sim.t["stats"].numpy()[[(folded + s) % RING for s in range(k)]].copy()
+        st2, tm2 = more_counts(rank, k2, (folded + k) % RING)
+        s2 = [(folded + k + s) % RING for s in range(k2)]
+        env.sim.t["stats"][s2] = torch.from_numpy(st2[s2])
+        env.sim.t["term_sums"][s2] = torch.from_numpy(tm2[s2])
+        env._stat_pending = k2
+        parallel.reduce_episode_stats(env)
+        q.put((rank, env._global_num_envs, first.tolist(), again.tolist(), env._success_rate_ewma, env._object_ewma,
+               env.total_num_resets, env.total_num_successes, sorted(env._log_data)))
     finally:
         torch.distributed.destroy_process_group()
 
@@ -63,38 +81,47 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("k,folded", [(5, 0), (6, 6)])    # second case wraps around the ring
-def test_reduce_then_fold_matches_single_process(k, folded):
+@pytest.mark.parametrize("k,folded,k2", [(5, 0, 3), (6, 6, 4)])    # second case wraps around the ring
+def test_reduce_then_fold_matches_single_process(k, folded, k2):
+    """Two log intervals on unequal shards: each slot is reduced exactly once, and the EWMA after both equals
+    one process folding the summed counters over all envs."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, k, folded, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, k, folded, k2, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = sorted(q.get(timeout=120) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # single process over all envs: counters are sums over ranks, N = world * N_LOCAL
+    n_all = sum(shard_envs(r) for r in range(world))
     slots = [(folded + s) % RING for s in range(k)]
+    slots2 = [(folded + k + s) % RING for s in range(k2)]
     tot_st = sum(local_counts(r, k, folded % RING)[0] for r in range(world))[slots]
     tot_tm = sum(local_counts(r, k, folded % RING)[1] for r in range(world))[slots]
-    ref = parallel.fold_counts(tot_st, tot_tm, world * N_LOCAL, 0.0, [0.0] * 3, OBJECTS)
-    for rank, scale, st, tm, log, ewma, obj, r, s in out:
-        assert scale == world
-        np.testing.assert_array_equal(np.array(st), tot_st)
-        np.testing.assert_allclose(np.array(tm, np.float32), tot_tm, rtol=1e-6)
-        assert ewma == pytest.approx(ref[1], rel=1e-6) and obj == pytest.approx(ref[2], rel=1e-6)
-        assert (r, s) == (ref[3], ref[4]) and r > 0
-        assert set(log) == set(ref[0])
+    tot_st2 = sum(more_counts(r, k2, (folded + k) % RING)[0] for r in range(world))[slots2]
+    tot_tm2 = sum(more_counts(r, k2, (folded + k) % RING)[1] for r in range(world))[slots2]
+    ref = parallel.fold_counts(tot_st, tot_tm, n_all, 0.0, [0.0] * 3, OBJECTS)
+    ref2 = parallel.fold_counts(tot_st2, tot_tm2, n_all, ref[1], ref[2], OBJECTS)
+    for rank, n_glob, first, again, ewma, obj, r, s, keys in out:
+        assert n_glob == n_all
+        np.testing.assert_array_equal(np.array(first), tot_st)
+        np.testing.assert_array_equal(np.array(again), tot_st)        # the empty second reduce changed nothing
+        assert ewma == pytest.approx(ref2[1], rel=1e-6) and obj == pytest.approx(ref2[2], rel=1e-6)
+        assert (r, s) == (ref[3] + ref2[3], ref[4] + ref2[4]) and r > 0
+        assert set(keys) == set(ref[0]) | set(ref2[0])
 
 
-def test_single_rank_is_a_no_op():
+def test_single_rank_folds_locally():
     env = fake_env(0, 3, 0)
     before = env.sim.t["stats"].clone()
-    parallel.reduce_episode_stats(env)          # no process group -> untouched, no stat_scale
-    assert torch.equal(before, env.sim.t["stats"]) and not hasattr(env, "stat_scale")
+    parallel.reduce_episode_stats(env)          # no process group: a plain local fold, counters untouched
+    assert torch.equal(before, env.sim.t["stats"]) and env._stat_pending == 0 and env._stat_folded == 3
+    st, tm = local_counts(0, 3, 0)
+    ref = parallel.fold_counts(st[:3], tm[:3], env.num_envs, 0.0, [0.0] * 3, OBJECTS)
+    assert env._success_rate_ewma == ref[1] and env.total_num_resets == ref[3]
 
 
 def test_fold_counts_ewma_arithmetic():
