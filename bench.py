@@ -215,7 +215,7 @@ def cpu_baseline_allegro(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0
                       f"OpenMP {threads} threads, + numpy task oracle), {dt:.1f} s"}
 
 
-def cpu_baseline(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0, binpick=False):
+def cpu_baseline(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0, binpick=False, pool16=False):
     """The C oracle (scalar restatement, OpenMP over envs) + numpy task oracle, timed on host cores.
 
     Bounded sample: env-steps of the full batch are repeated until ``min_seconds`` of wall time have
@@ -225,7 +225,8 @@ def cpu_baseline(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0, binpic
     from handarm_hip import model as HM
     from tests import scenes
     scene = HM.load_scene(HM.BIN_ASSET if binpick else HM.ASSET)
-    model = HM.build_model(scene)
+    pool = [o["name"] for o in HM.load_scene()["objects"]] if pool16 else None
+    model = HM.build_model(scene, pool)
     params, _ = HM.build_params({"n_objects": 8} if binpick else None)
     orc = Oracle(model, params, num_envs)
     st = HostState(num_envs, model=model, params=params)
@@ -233,6 +234,9 @@ def cpu_baseline(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0, binpic
         scenes.fill_bin_scene(st, num_envs, scene, seed=seed)
     else:
         scenes.fill_scene(st, num_envs, seed=seed)
+        if pool16:      # C4: each env's 3 objects are a random.sample of the 16-object pool (multi_object.py:569)
+            st["object_indices"][:] = np.stack([np.random.default_rng(seed + e).choice(len(pool), 3, replace=False)
+                                                for e in range(num_envs)])
     A, B, no, a0 = model.n_actors, model.n_bodies, params.n_objects, model.actor_object0
     actors = list(range(a0, a0 + no))
     rng = np.random.default_rng(seed)
@@ -263,78 +267,100 @@ def cpu_baseline(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0, binpic
                       f"OpenMP {threads} threads, + numpy task oracle), {dt:.1f} s"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--task", choices=["allegro_kuka", "ur5sih", "allegro_hand", "binpick"], default="allegro_kuka",
-                    help="allegro_kuka: BASELINE config 2 (default); ur5sih: config 4 shard; allegro_hand: config 3; "
-                         "binpick: config 5 shard")
-    ap.add_argument("--subtask", choices=["regrasping", "reorientation"], default="regrasping")
-    ap.add_argument("--envs", type=int, default=None,
-                    help="envs per GPU (4096 allegro_kuka, 8192 ur5sih, 16384 allegro_hand, 8192 binpick)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-dr", action="store_true", help="ur5sih: domain randomization off")
-    ap.add_argument("--pointclouds", action="store_true",
-                    help="ur5sih / binpick: the point-cloud student observation list (synthetic clouds every step)")
-    ap.add_argument("--cpu-envs", type=int, default=1024)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    args = ap.parse_args()
-    allegro = args.task == "allegro_hand"
-    kuka = args.task == "allegro_kuka"
-    binpick = args.task == "binpick"
-    if args.envs is None:
-        args.envs = {"allegro_kuka": 4096, "ur5sih": 8192, "allegro_hand": 16384, "binpick": 8192}[args.task]
+# BASELINE.json configs the bench runs on the GPU (configs[0] is the reference's CPU-pipeline plumbing case,
+# a parity-test size, not a bench line): key -> (task, envs per GPU, label)
+CONFIGS = {
+    "C2": ("allegro_kuka", 4096, "Arm+Allegro cube grasp (AllegroKuka regrasping), 4096 envs/GPU"),
+    "C3": ("allegro_hand", 16384, "In-hand cube reorientation (AllegroHand), 16384 envs/GPU"),
+    "C4": ("ur5sih", 8192, "HandArmGrasp shard, DR on, 3 objects per env sampled from the 16-object YCB pool, "
+                           "8192 envs/GPU (65536 at 8 GPUs)"),
+    "C5": ("binpick", 8192, "Multi-object bin-picking shard (hard_bin, 8 objects per env), 8192 envs/GPU "
+                            "(32768 at 4 GPUs)"),
+}
+STEP_KERNEL = {"allegro_kuka": "ak_step_kernel", "allegro_hand": "ah_step_kernel", "ur5sih": "ha_step_kernel",
+               "binpick": "hb_step_kernel"}
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md:54)
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
+NOMINAL_CLOCK_HZ = 2.4e9
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
-    device = f"cuda:{local_rank}"
-    torch.cuda.set_device(device)
+
+def pool16_names():
+    from handarm_hip import model as HM
+    return [o["name"] for o in HM.load_scene()["objects"]]
+
+
+def make_env(task, envs, seed, device, args):
+    from handarm_hip.tasks import AllegroHand, AllegroKuka, Ur5SihMultiObjectManipulation
+    if task == "allegro_kuka":
+        return AllegroKuka({"env": {"numEnvs": envs, "subtask": args.subtask}, "seed": seed}, device, device)
+    if task == "allegro_hand":
+        return AllegroHand({"env": {"numEnvs": envs}, "seed": seed}, device, device)
+    envcfg = {"numEnvs": envs}
+    if args.pointclouds:
+        envcfg["observations"] = PC_STUDENT
+    # C4 / C5 draw each env's objects by random.sample from the 16-object YCB pool (multi_object.py:569)
+    cfg = {"env": envcfg, "seed": seed, "objects": {"dataset": {"ycb": pool16_names()}}}
+    if task == "binpick":
+        # config 5: Ur5SihMultiObject with bin.asset hard_bin and 8 objects
+        cfg.update({"bin": {"asset": "hard_bin"}})
+        cfg["objects"]["num_objects"] = 8
+    else:
+        # config 4 is quoted with domain randomization on (BASELINE.json configs[3]); --no-dr turns it off
+        cfg["task"] = {"randomize": not args.no_dr}
+    return Ur5SihMultiObjectManipulation(cfg, device, device)
+
+
+def bytes_per_env_step(task, env, args):
+    if task == "allegro_kuka":
+        return kuka_bytes_per_env_step(num_obs=env.num_obs)[0]
+    if task == "allegro_hand":
+        return allegro_bytes_per_env_step()[0]
+    if task == "binpick":
+        return algorithmic_bytes_per_env_step(n_obj=8, num_obs=env.sim.params.num_obs, n_static_bodies=6)[0]
+    return algorithmic_bytes_per_env_step(dr=not args.no_dr)[0]
+
+
+def _profile_json(name, envs):
+    fn = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(fn):
+        return None
+    with open(fn) as f:
+        d = json.load(f)
+    return d if d.get("envs") == envs else None
+
+
+def compute_roofline(kernel, envs, kavg_ms):
+    """Second roofline: VALU issue. Wave-instructions per launch come from the committed
+    rocprofv3 SQ pass of the same workload (profiles/sq_<kernel>.json, tools/sq_summary.py); the kernel time is
+    this run's. Mean resident waves per SIMD = 4 x SQ_WAVE_CYCLES (quad-cycles) / (kernel cycles at the nominal
+    2.4 GHz) / 1024 SIMDs."""
+    sq = _profile_json(f"sq_{kernel}.json", envs)
+    if sq is None or not kavg_ms == kavg_ms:
+        return None
+    t = kavg_ms * 1e-3
+    rate = sq["valu_insts_per_launch"] / t
+    return {"bound": "valu", "achieved": rate, "peak": VALU_PEAK_WAVE_INSTS, "unit": "wave-instructions/s",
+            "frac": rate / VALU_PEAK_WAVE_INSTS, "valu_insts_per_launch": sq["valu_insts_per_launch"],
+            "waves_per_simd": 4 * sq["wave_cycles_per_launch"] / (t * NOMINAL_CLOCK_HZ) / 1024,
+            "valu_active_frac": sq.get("valu_active_frac"), "source": f"profiles/sq_{kernel}.json"}
+
+
+def run_config(task, envs, args, world, rank, device, log_interval_fn):
+    """Build the env, W warmup steps (the first includes the all-env reset and, for the HandArm tasks, drop
+    init), then exactly K timed steps between barrier + synchronize pairs; returns the record (rank 0 gets the
+    max over ranks)."""
+    from handarm_hip import parallel
     seed = 42 + rank                  # utils/utils.py:94 (seed + rank)
     random.seed(seed)
     torch.manual_seed(seed)
-
-    from handarm_hip.tasks import AllegroHand, AllegroKuka, Ur5SihMultiObjectManipulation
-    from handarm_hip import parallel
-    if kuka:
-        env = AllegroKuka({"env": {"numEnvs": args.envs, "subtask": args.subtask}, "seed": seed}, device, device)
-    elif binpick:
-        # config 5: Ur5SihMultiObject with bin.asset hard_bin and 8 objects from the YCB pool
-        from handarm_hip import model as HM
-        pool = [o["name"] for o in HM.load_scene()["objects"]]
-        envcfg = {"numEnvs": args.envs}
-        if args.pointclouds:
-            envcfg["observations"] = PC_STUDENT
-        env = Ur5SihMultiObjectManipulation({"env": envcfg, "seed": seed, "bin": {"asset": "hard_bin"},
-                                             "objects": {"num_objects": 8, "dataset": {"ycb": pool}}}, device, device)
-    else:
-        cls = AllegroHand if allegro else Ur5SihMultiObjectManipulation
-        envcfg = {"numEnvs": args.envs}
-        if args.pointclouds and not allegro:
-            envcfg["observations"] = PC_STUDENT
-        # config 4 is quoted with domain randomization on (BASELINE.json configs[3]); --no-dr turns it off
-        env = cls({"env": envcfg, "seed": seed, "task": {"randomize": not (allegro or args.no_dr)}},
-                  device, device)
+    env = make_env(task, envs, seed, device, args)
     env.reset()
     gen = torch.Generator(device=device).manual_seed(seed)
-    pool = [torch.rand((args.envs, env.num_acts), device=device, generator=gen) * 2 - 1 for _ in range(8)]
-    def log_interval():
-        if kuka:
-            return parallel.reduce_kuka_episode_stats(env)   # RCCL all-reduce, 3 floats (N > 1)
-        if not allegro:
-            parallel.reduce_episode_stats(env)       # RCCL all-reduce of the episode counters (N > 1)
-        return {}
+    pool = [torch.rand((envs, env.num_acts), device=device, generator=gen) * 2 - 1 for _ in range(8)]
     for k in range(args.warmup):
         env.step(pool[k % len(pool)])
         if (k + 1) % LOG_INTERVAL == 0 or k == args.warmup - 1:
-            log_interval()                          # lazy initialisation of the logging path stays untimed
+            log_interval_fn(task, env)               # lazy initialisation of the logging path stays untimed
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -344,14 +370,12 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
-    host_t = []
     for k in range(args.steps):
         ev[k][0].record()
         env.step(pool[k % len(pool)])
         ev[k][1].record()
-        host_t.append(time.perf_counter())
         if (k + 1) % LOG_INTERVAL == 0:
-            log_interval()
+            log_interval_fn(task, env)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -361,87 +385,167 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     step_ms = [a.elapsed_time(b) for a, b in ev]
-    if os.environ.get("BENCH_DEBUG"):
-        gaps = [(b - a) * 1e3 for a, b in zip([t0] + host_t[:-1], host_t)]
-        print("host ms/step issue:", [round(x, 3) for x in gaps], "\ngpu ms/step:", [round(x, 3) for x in step_ms],
-              file=sys.stderr)
     kern_ms = env.sim.kernel_times_ms(args.steps)
     pcs = getattr(env, "pointclouds", None)
     pc_ms = pcs.kernel_times_ms(args.steps) if pcs is not None else []
-    log = {} if (allegro or kuka) else env.log_data
-    kstats = parallel.reduce_kuka_episode_stats(env) if kuka else {}
-    if rank == 0:
-        total_env_steps = world * args.envs * args.steps
-        value = total_env_steps / elapsed
-        if kuka:
-            bytes_env, _, _ = kuka_bytes_per_env_step(num_obs=env.num_obs)
-        elif allegro:
-            bytes_env, _, _ = allegro_bytes_per_env_step()
-        elif binpick:
-            bytes_env, _, _ = algorithmic_bytes_per_env_step(n_obj=8, num_obs=env.num_obs, n_static_bodies=6)
+    extra = {}
+    if task == "allegro_kuka":
+        extra["episode_successes_mean"] = float(parallel.reduce_kuka_episode_stats(env)["successes"])
+    elif task == "allegro_hand":
+        extra["consecutive_successes"] = float(parallel.reduce_allegro_episode_stats(env)["consecutive_successes"])
+    else:
+        parallel.reduce_episode_stats(env)
+        extra["success_rate_ewma"] = env.log_data.get("success_rate_ewma/overall")
+        cs = env.contact_stats() if hasattr(env, "contact_stats") else None
+        if cs is not None:
+            extra["contacts"] = cs
+    kernel = STEP_KERNEL[task]
+    kavg = statistics.mean(kern_ms) if kern_ms else float("nan")
+    bytes_env = bytes_per_env_step(task, env, args)
+    achieved = bytes_env * envs / (kavg * 1e-3) / 1e9
+    tj = _profile_json(f"traffic_{kernel}.json", envs)
+    rec = {
+        "value": world * envs * args.steps / elapsed, "unit": "env-steps/s",
+        "ms_per_step": elapsed / args.steps * 1e3, "p50_ms_per_step": statistics.median(step_ms),
+        "envs_per_gpu": envs, "total_envs": world * envs,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": tj.get("hbm_bytes_per_launch") if tj else None,
+                     "kernel": kernel, "kernel_avg_ms": kavg, "algorithmic_bytes_per_env_step": bytes_env},
+        "compute_roofline": compute_roofline(kernel, envs, kavg),
+        **extra,
+    }
+    if pcs is not None:
+        pb = pointcloud_bytes_per_env(pcs)
+        pach = pb * envs / (statistics.mean(pc_ms) * 1e-3) / 1e9
+        rec["pointcloud_roofline"] = {"bound": "hbm", "kernel": "ha_pointcloud_kernel", "observations": env.obs_names,
+                                      "kernel_avg_ms": statistics.mean(pc_ms), "algorithmic_bytes_per_env": pb,
+                                      "achieved": pach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                      "frac": pach / HBM_PEAK_GBS}
+    del env, pool
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()
+    return rec
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def run_cpu_baseline(task, args, seconds, threads=None):
+    """Bounded CPU sample of the same workload (rank 0, N=1 only). threads: OpenMP threads of the C oracle
+    (None = OMP_NUM_THREADS / all)."""
+    from oracle import oracle_lib
+    lib = oracle_lib.load()
+    prev = lib.hao_get_threads()
+    if threads:
+        lib.hao_set_threads(threads)
+    try:
+        if task == "allegro_kuka":
+            r = cpu_baseline_kuka(min(args.cpu_envs, 512), seconds, subtask=args.subtask)
+        elif task == "allegro_hand":
+            r = cpu_baseline_allegro(args.cpu_envs, seconds)
         else:
-            bytes_env, _, _ = algorithmic_bytes_per_env_step(dr=not args.no_dr)
-        kernel = {"allegro_kuka": "ak_step_kernel", "allegro_hand": "ah_step_kernel", "ur5sih": "ha_step_kernel",
-                  "binpick": "hb_step_kernel"}[args.task]
-        kavg = statistics.mean(kern_ms) if kern_ms else float("nan")
-        achieved = bytes_env * args.envs / (kavg * 1e-3) / 1e9
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", {"allegro_kuka": "traffic_ak_step_kernel.json",
-                                             "allegro_hand": "traffic_ah_step_kernel.json",
-                                             "ur5sih": "traffic_ha_step_kernel.json",
-                                             "binpick": "traffic_hb_step_kernel.json"}[args.task])
-        if os.path.exists(tf):
-            with open(tf) as f:
-                tj = json.load(f)
-            if tj.get("envs") == args.envs:
-                traffic = tj.get("hbm_bytes_per_launch")
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            if kuka:
-                cpu = cpu_baseline_kuka(min(args.cpu_envs, 512), args.cpu_seconds, subtask=args.subtask)
-            elif allegro:
-                cpu = cpu_baseline_allegro(args.cpu_envs, args.cpu_seconds)
-            else:
-                cpu = cpu_baseline(args.cpu_envs, args.cpu_seconds, binpick=binpick)
-        out = {
-            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "p50_ms_per_step": statistics.median(step_ms), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32",
-            "data": {"allegro_kuka": "synthetic (seeded U[-1,1] actions, AllegroKuka.yaml procedural cuboid family, "
-                                     "random object forces on)",
-                     "allegro_hand": "synthetic (seeded U[-1,1] actions, AllegroHand.yaml cube scene)",
-                     "ur5sih": "synthetic (seeded U[-1,1] actions, YCB scene of Ur5SihMultiObject.yaml, objects "
-                               "dropped at init)",
-                     "binpick": "synthetic (seeded U[-1,1] actions, hard_bin tote + 8 YCB objects per env from the "
-                                "16-object pool, dropped into the bin at init)"}[args.task],
-            "config": {"workload": {
-                "allegro_kuka": f"AllegroKuka{args.subtask.capitalize()} VecTask.step, 1x2 substeps, {args.envs} envs/GPU "
-                                "(BASELINE config 2, Arm+Allegro cube grasp)",
-                "allegro_hand": f"AllegroHand VecTask.step, 2x2 substeps, {args.envs} envs/GPU (BASELINE config 3)",
-                "ur5sih": "HandArm Ur5SihMultiObjectManipulation VecTask.step, 3x2 substeps, "
-                          f"{args.envs} envs/GPU (BASELINE config 4 shard, DR {'off' if args.no_dr else 'on'})",
-                "binpick": "HandArm bin-picking Ur5SihMultiObjectManipulation VecTask.step, 3x2 substeps, 8 objects, "
-                           f"{args.envs} envs/GPU (BASELINE config 5 shard)"}[args.task],
-                       "envs_per_gpu": args.envs, "total_envs": world * args.envs, "parallelism": f"env-shard x{world}",
-                       "observations": "point-cloud student list (Ur5SihMultiObjectManipulation.yaml:45)" if pcs is not None
-                       else "default"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": kernel, "kernel_avg_ms": kavg,
-                         "algorithmic_bytes_per_env_step": bytes_env},
-            "cpu_baseline": cpu,
-            "pointcloud_roofline": None if pcs is None else {
-                "bound": "hbm", "kernel": "ha_pointcloud_kernel", "observations": env.obs_names,
-                "kernel_avg_ms": statistics.mean(pc_ms), "algorithmic_bytes_per_env": pointcloud_bytes_per_env(pcs),
-                "achieved": pointcloud_bytes_per_env(pcs) * args.envs / (statistics.mean(pc_ms) * 1e-3) / 1e9,
-                "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": pointcloud_bytes_per_env(pcs) * args.envs / (statistics.mean(pc_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS},
-            "success_rate_ewma": log.get("success_rate_ewma/overall"),
-            "consecutive_successes": float(env.consecutive_successes.item()) if allegro else None,
-            "episode_successes_mean": float(kstats["successes"]) if kuka else None,
-        }
-        print(json.dumps(out))
+            r = cpu_baseline(args.cpu_envs // (4 if task == "binpick" else 1), seconds, binpick=task == "binpick",
+                             pool16=task == "ur5sih")
+    finally:
+        lib.hao_set_threads(prev)
+    r["cores"] = threads or prev
+    r["cpu_model"] = cpu_model()
+    r["sample"] = r["sample"].replace(f"OpenMP {int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))} threads",
+                                      f"OpenMP {r['cores']} threads")
+    return r
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--task", choices=["all", "allegro_kuka", "ur5sih", "allegro_hand", "binpick"], default="all",
+                    help="all (default): the C2 headline (allegro_kuka) plus sub-records for C3 (allegro_hand), "
+                         "C4 (ur5sih shard) and C5 (binpick shard); or one of them alone")
+    ap.add_argument("--subtask", choices=["regrasping", "reorientation"], default="regrasping")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU of a single --task (default: its config)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dr", action="store_true", help="ur5sih: domain randomization off")
+    ap.add_argument("--pointclouds", action="store_true",
+                    help="ur5sih / binpick: the point-cloud student observation list (synthetic clouds every step)")
+    ap.add_argument("--cpu-envs", type=int, default=1024)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU sample of the headline config")
+    ap.add_argument("--cpu-seconds-sub", type=float, default=4.0, help="CPU sample of each sub-record")
+    args = ap.parse_args()
+
+    from handarm_hip import parallel
+    rank, local_rank, world, device = parallel.init_distributed("nccl")
+
+    def log_interval(task, env):
+        if task == "allegro_kuka":
+            return parallel.reduce_kuka_episode_stats(env)   # RCCL all-reduce, 3 floats (N > 1)
+        if task == "allegro_hand":
+            return parallel.reduce_allegro_episode_stats(env)
+        return parallel.reduce_episode_stats(env)            # RCCL all-reduce of the episode counters (N > 1)
+
+    if args.task == "all":
+        head, subs = "C2", ["C3", "C4", "C5"]
+    else:
+        head = next(k for k, v in CONFIGS.items() if v[0] == args.task)
+        subs = []
+    records = {}
+    for key in [head] + subs:
+        task, envs, _ = CONFIGS[key]
+        if key == head and args.envs:
+            envs = args.envs
+        records[key] = run_config(task, envs, args, world, rank, device, log_interval)
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        for key in [head] + subs:
+            task = CONFIGS[key][0]
+            records[key]["cpu_baseline"] = run_cpu_baseline(task, args, args.cpu_seconds if key == head
+                                                            else args.cpu_seconds_sub)
+        # the 1-thread run BASELINE.md plans, next to the all-cores one (headline config, short sample)
+        records[head]["cpu_baseline"]["one_thread"] = run_cpu_baseline(CONFIGS[head][0], args, 3.0, threads=1)
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    data = {"allegro_kuka": "synthetic (seeded U[-1,1] actions, AllegroKuka.yaml procedural cuboid family, random "
+                            "object forces on)",
+            "allegro_hand": "synthetic (seeded U[-1,1] actions, AllegroHand.yaml cube scene)",
+            "ur5sih": "synthetic (seeded U[-1,1] actions, YCB objects of the 16-object pool, dropped at init)",
+            "binpick": "synthetic (seeded U[-1,1] actions, hard_bin tote + 8 YCB objects per env from the 16-object "
+                       "pool, dropped into the bin at init)"}
+    h = records[head]
+    task, envs, label = CONFIGS[head]
+    envs = h["envs_per_gpu"]
+    out = {
+        "metric": METRIC, "value": h["value"], "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": h["ms_per_step"], "p50_ms_per_step": h["p50_ms_per_step"],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": data[task],
+        "config": {"workload": f"{head}: {label} - one VecTask.step() of every env per step",
+                   "envs_per_gpu": envs, "total_envs": world * envs, "parallelism": f"env-shard x{world}",
+                   "observations": "point-cloud student list (Ur5SihMultiObjectManipulation.yaml:45)"
+                   if args.pointclouds and task in ("ur5sih", "binpick") else "default"},
+        "roofline": h["roofline"], "compute_roofline": h["compute_roofline"], "cpu_baseline": h.get("cpu_baseline"),
+    }
+    for k in ("episode_successes_mean", "consecutive_successes", "success_rate_ewma", "contacts", "pointcloud_roofline"):
+        if k in h:
+            out[k] = h[k]
+    if subs:
+        out["configs"] = {}
+        for key in subs:
+            r = dict(records[key])
+            t = CONFIGS[key][0]
+            r["workload"] = CONFIGS[key][2]
+            r["data"] = data[t]
+            out["configs"][key] = r
+    print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -23,6 +23,7 @@
  * oracle/task_oracle.py does; that file is the one pinned against reference-generated goldens.
  */
 #include <math.h>
+#include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -429,7 +430,7 @@ static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t
     float seps[MAXCAND];
     for (int pass = 0; pass < 2; pass++) {
         int refB = (sepB >= sepA) ? (pass == 0) : (pass == 1);
-        int hr = refB ? hb : ha, hi = refB ? ha : hb, kr = refB ? kB : kA;
+        int hr = refB ? hb : ha, kr = refB ? kB : kA;
         pose_t Pr = refB ? PB : PA;
         const float* scr = refB ? scb : sca;
         v3* vi = refB ? va : vb;
@@ -877,6 +878,9 @@ hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int nu
     return h;
 }
 void hao_destroy(hao_handle h) { free(h); }
+/* OpenMP threads of hao_simulate (bench.py's cpu_baseline reports an all-cores and a 1-thread sample) */
+void hao_set_threads(int n) { if (n > 0) omp_set_num_threads(n); }
+int hao_get_threads(void) { return omp_get_max_threads(); }
 int hao_struct_sizes(int32_t* model_size, int32_t* params_size, int32_t* state_size) {
     *model_size = (int32_t)sizeof(ha_model_t);
     *params_size = (int32_t)sizeof(ha_params_t);

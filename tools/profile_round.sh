@@ -14,7 +14,7 @@ esac
 P="cd /tmp && export TMPDIR=/tmp && rocprofv3"
 B="python3 $R/bench.py --task $TASK --steps 20 --warmup 5 --no-cpu-baseline"
 bash "$R/tools/gpu_round.sh" \
-  "bench|600|python $R/bench.py --task $TASK > $O/${TAG}_bench${SFX}.json" \
+  "bench|600|python $R/bench.py --task $TASK --cpu-seconds 6 > $O/${TAG}_bench${SFX}.json" \
   "ks|400|$P --kernel-trace --stats --output-format csv -d $O/ks -- $B" \
   "ksx|60|cp $O/ks/*/*_kernel_stats.csv $O/${TAG}_bench${SFX}_kernel_stats.csv && rm -rf $O/ks" \
   "pmcf|400|$P --pmc FETCH_SIZE --output-format csv -d $O/pmcf -- $B" \
@@ -23,4 +23,5 @@ bash "$R/tools/gpu_round.sh" \
   "sq1|400|$P --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS --output-format csv -d $O/sq1 -- $B" \
   "sq1x|60|python $R/tools/pmc_extract.py $O/sq1 --kernel $K --out $O/${TAG}_sq1${SFX}.csv --delete > $O/${TAG}_sq1${SFX}_summary.txt" \
   "sq2|400|$P --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA --output-format csv -d $O/sq2 -- $B" \
-  "sq2x|60|python $R/tools/pmc_extract.py $O/sq2 --kernel $K --out $O/${TAG}_sq2${SFX}.csv --delete > $O/${TAG}_sq2${SFX}_summary.txt"
+  "sq2x|60|python $R/tools/pmc_extract.py $O/sq2 --kernel $K --out $O/${TAG}_sq2${SFX}.csv --delete > $O/${TAG}_sq2${SFX}_summary.txt" \
+  "sqsum|60|python $R/tools/sq_summary.py $O/${TAG}_sq1${SFX}.csv $O/${TAG}_sq2${SFX}.csv --kernel $K --envs $ENVS --out $O/sq_$K.json"
