@@ -82,6 +82,7 @@ class SyntheticPointclouds:
         self.robot_samples = torch.from_numpy(rs).to(dev)
         self.robot_slot = torch.from_numpy(slot).to(dev)
         self.gen = generator
+        self.reference_rng = False      # True: torch.randperm on the CPU global generator (ref_rng.py)
         self.perm = torch.arange(self.P, dtype=torch.int64, device=dev)
         self.prev_pose = None                      # snapshot buffer when the object clouds see the previous pose
         shapes = {"object_synthetic_pointcloud": (N, NO * self.P, 4), "target_object_synthetic_pointcloud": (N, self.P, 4),
@@ -138,7 +139,10 @@ class SyntheticPointclouds:
                 raise ValueError("perm must be a permutation of range(max_num_points)")
             self.perm.copy_(p)
         elif self._object_buf is not None:
-            self.perm.copy_(torch.randperm(self.P, generator=self.gen, device=self.sim.device))
+            if self.reference_rng:      # multi_object.py:806: torch.randperm without a device is a CPU draw
+                self.perm.copy_(torch.randperm(self.P))
+            else:
+                self.perm.copy_(torch.randperm(self.P, generator=self.gen, device=self.sim.device))
         _lib.check(self.sim.lib.ha_pointclouds(self.sim.h, C.byref(self.args), self.sim._stream()), "ha_pointclouds")
 
     def kernel_times_ms(self, max_n=1 << 16):

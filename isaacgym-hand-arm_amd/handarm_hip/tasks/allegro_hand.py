@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from .. import model as HM
+from .. import ref_rng as RR
 from ..sim import HandArmSim
 from .ur5sih_multi_object_manipulation import Box
 
@@ -84,6 +85,10 @@ class AllegroHand:
         r[:, 2, 6] = 1.0
         self.reset_buf.fill_(1)
         self.reset_goal_buf.fill_(1)
+        # seed-faithful draws (handarm_hip/ref_rng.py): every reset value from torch's global CPU generator in
+        # the reference's order (the __init__ random_force_prob draw happens here, as at allegro_hand.py:193)
+        self.reference_rng = bool(cfg.get("sim", {}).get("reference_rng", False))
+        self._rr = RR.AllegroDraws(N) if self.reference_rng else None
         self.extras = {}
         self.obs_dict = {}
         self.control_steps = 0
@@ -133,7 +138,7 @@ class AllegroHand:
     def step(self, actions):
         """VecTask.step (vec_task.py:390-441) -> pre_physics_step / simulate x2 / post_physics_step, fused."""
         torch.clamp(actions, -self.clip_actions, self.clip_actions, out=self.actions_buf)
-        self.sim.task_step(self.sim_flags)
+        self.sim.task_step(self.sim_flags | self._reference_draws())
         self.control_steps += 1
         self.extras["time_outs"] = self.timeout_buf.view(torch.bool).to(self.rl_device)
         self.extras["consecutive_successes"] = self.consecutive_successes.mean()     # allegro_hand.py:393
@@ -151,7 +156,16 @@ class AllegroHand:
         self.reset_buf[env_ids] = 1
         if goal_env_ids is not None:
             self.reset_goal_buf[goal_env_ids] = 1
-        self.sim.task_reset(self.sim_flags)
+        self.sim.task_reset(self.sim_flags | self._reference_draws())
+
+    def _reference_draws(self):
+        """reference_rng: this step's reset draws on the host (one read of the reset flags), uploaded for
+        HA_FLAG_REPLAY_DRAWS. Returns the extra launch flags."""
+        if self._rr is None:
+            return 0
+        d = self._rr.step(self.reset_buf.cpu(), self.reset_goal_buf.cpu())
+        self.sim.t["reset_draws"].copy_(d)
+        return HM.FLAG_REPLAY_DRAWS
 
     def reset_done(self):
         done_env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()

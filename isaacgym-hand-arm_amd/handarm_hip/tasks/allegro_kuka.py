@@ -16,6 +16,7 @@ import numpy as np
 import torch
 
 from .. import model as HM
+from .. import ref_rng as RR
 from ..sim import HandArmSim
 from .ur5sih_multi_object_manipulation import Box
 
@@ -124,6 +125,13 @@ class AllegroKuka:
         self.frame_since_restart = 0
         self.extras = {}
         self.obs_dict = {}
+        # seed-faithful draws (handarm_hip/ref_rng.py): every reset / force value from torch's global CPU
+        # generator in the reference's order; random_force_prob is drawn here, as at allegro_kuka_base.py:323-327
+        self.reference_rng = bool(cfg.get("sim", {}).get("reference_rng", False))
+        self._rr = None
+        if self.reference_rng:
+            self._rr = RR.KukaDraws(N, sub, tuple(self.tcfg["force_prob_range"]), float(self.tcfg["force_scale"]))
+            self.random_force_prob.copy_(self._rr.prob.to(sim_device))
 
     # ---------------------------------------------------------------- VecTask surface
     @property
@@ -188,7 +196,7 @@ class AllegroKuka:
         torch.clamp(actions, -self.clip_actions, self.clip_actions, out=self.actions_buf)
         self.frame_since_restart += 1
         self._curriculum()
-        self.sim.task_step(self.sim_flags)
+        self.sim.task_step(self.sim_flags | self._reference_draws())
         ex = self.extras
         ex["time_outs"] = self.timeout_buf.view(torch.bool).to(self.rl_device)
         ex["successes"] = self.prev_episode_successes.mean()                   # :908-917
@@ -212,7 +220,17 @@ class AllegroKuka:
     def reset_idx(self, env_ids):
         """reset_idx (allegro_kuka_base.py:1246-1353) for the listed envs."""
         self.reset_buf[env_ids] = 1
-        self.sim.task_reset(self.sim_flags)
+        self.sim.task_reset(self.sim_flags | self._reference_draws(forces=False))
+
+    def _reference_draws(self, forces=True):
+        """reference_rng: this step's draws on the host (one read of the reset flags), uploaded for
+        HA_FLAG_REPLAY_DRAWS. Returns the extra launch flags."""
+        if self._rr is None:
+            return 0
+        goal = self.reset_goal_buf.cpu() if forces else torch.zeros(self.num_envs, dtype=torch.int64)
+        d, _ = self._rr.step(self.reset_buf.cpu(), goal, forces=forces)
+        self.sim.t["reset_draws"].copy_(d)
+        return HM.FLAG_REPLAY_DRAWS
 
     def reset_done(self):
         done_env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()

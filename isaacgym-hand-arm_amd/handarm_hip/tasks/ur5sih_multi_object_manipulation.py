@@ -24,6 +24,7 @@ from .. import _lib
 from .. import model as HM
 from .. import observables as OB
 from .. import parallel
+from .. import ref_rng as RR
 from ..cameras import IMAGE_TYPES, CameraSensor
 from ..pointclouds import SyntheticPointclouds
 from ..sim import HandArmSim
@@ -94,6 +95,9 @@ class Ur5SihMultiObjectManipulation:
         # observation noise in the step kernel, action noise below). The reference's Ur5Sih `randomize`
         # flag has no consumer, so this is the build's own switch: cfg["task"]["randomize"].
         self.randomize = bool(_get(cfg, "task.randomize", False))
+        # seed-faithful draws (handarm_hip/ref_rng.py): resets, drops and cloud permutations from torch's global
+        # CPU generator in the reference's order, instead of the device counter hash
+        self.reference_rng = bool(_get(cfg, "sim.reference_rng", False))
         task_cfg["dr_enable"] = int(self.randomize)
         rew = _get(cfg, "rl.reward", None)
         if rew:
@@ -243,6 +247,7 @@ class Ur5SihMultiObjectManipulation:
         if pc_names:
             g = torch.Generator(device=self.device).manual_seed(int(cfg.get("seed", 42)))
             self.pointclouds = SyntheticPointclouds(self.sim, pc_names, objects, _get(cfg, "pointclouds", {}), g)
+            self.pointclouds.reference_rng = bool(_get(cfg, "sim.reference_rng", False))
             if any(OB.sees_previous_object_pose(order, n) for n in
                    ("object_synthetic_pointcloud", "target_object_synthetic_pointcloud") if n in order):
                 self.pointclouds.use_previous_object_pose()
@@ -403,9 +408,15 @@ class Ur5SihMultiObjectManipulation:
                     self.sim.set_object_collisions(enabled)
                     env_ids = (~in_bin[:, i]).nonzero(as_tuple=False).squeeze(-1)
                     if len(env_ids) > 0:
-                        rs[env_ids, i, 0:3] = self._random_object_pos(len(env_ids), "drop")
-                        rf = torch_rand_float(-1.0, 1.0, (len(env_ids), 2), device=self.device)
-                        rs[env_ids, i, 3:7] = randomize_rotation(rf[:, 0], rf[:, 1])
+                        if self.reference_rng:
+                            pos, quat = RR.ur5sih_drop_pose(len(env_ids), self.task_cfg["drop_pos"],
+                                                            self.task_cfg["drop_noise"])
+                            rs[env_ids, i, 0:3] = pos.to(self.device)
+                            rs[env_ids, i, 3:7] = quat.to(self.device)
+                        else:
+                            rs[env_ids, i, 0:3] = self._random_object_pos(len(env_ids), "drop")
+                            rf = torch_rand_float(-1.0, 1.0, (len(env_ids), 2), device=self.device)
+                            rs[env_ids, i, 3:7] = randomize_rotation(rf[:, 0], rf[:, 1])
                         rs[env_ids, i, 7:13] = 0.0
                         self.sim.simulate(self.task_cfg["drop_num_steps"])
                 obj_pos = rs[:, :, 0:3]
@@ -418,6 +429,21 @@ class Ur5SihMultiObjectManipulation:
             quat_init[:, p] = rs[:, :, 3:7]
             self._sync_obs_cache()
         self.objects_dropped = True
+
+    def _reference_draws(self, all_envs=False):
+        """reference_rng: if this step resets, draw its values on the host in the reference's order and hand them
+        to the kernel (HA_FLAG_REPLAY_DRAWS). One device->host read of reset_buf per step (the reference's
+        reset_buf.nonzero() in post_physics_step). Returns the extra launch flags."""
+        if not self.reference_rng:
+            return 0
+        if not all_envs:
+            reset = self.reset_buf.cpu()
+            if not bool(reset.any()):
+                return 0
+            assert bool(reset.all()), "All environments should be reset simultaneously."      # ur5sih.py:617
+        d = RR.ur5sih_reset_draws(self.num_envs, self.num_initial_poses, self.num_objects)
+        self.sim.t["reset_draws"][:, 0:5].copy_(d)
+        return HM.FLAG_REPLAY_DRAWS
 
     def _fold_stats(self):
         """Fold the device-side per-step counters into log_data (reference :311-351 semantics). With several
@@ -451,7 +477,7 @@ class Ur5SihMultiObjectManipulation:
             parallel.reduce_episode_stats(self)      # ring full: reduce across ranks (if any), then fold
         if self.pointclouds is not None:           # object_pos as of the previous refresh (see observables.py)
             self.pointclouds.snapshot_object_pose(self.sim.t["obs_cache"])
-        self.sim.task_step(self.sim_flags)
+        self.sim.task_step(self.sim_flags | self._reference_draws())
         if self.pointclouds is not None:           # the clouds' post_step refresh, one launch
             self.pointclouds.refresh()
         for cam in self.cameras.values():          # render_all_camera_sensors + image refresh, one launch each
@@ -472,7 +498,7 @@ class Ur5SihMultiObjectManipulation:
         assert len(env_ids) == self.num_envs, "All environments should be reset simultaneously."
         if not self.objects_dropped:
             self._drop_initialisation()
-        self.sim.task_reset(self.sim_flags)
+        self.sim.task_reset(self.sim_flags | self._reference_draws(all_envs=True))
 
     def reset_done(self):
         done_env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()

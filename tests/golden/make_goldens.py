@@ -383,6 +383,45 @@ def gen_reset(path, N=16, seed=3, P=2):
     print("wrote", path, {k: v.shape for k, v in arrays.items()})
 
 
+def gen_ref_rng(path, N=16, P=4, E=4, seed=77):
+    """Seed-faithful draws (handarm_hip/ref_rng.py): the reference's reset_idx over E episodes from
+    torch.manual_seed(seed) (multi_object_manipulation.py:33-91,193-230, objects already dropped), and the drop
+    draws (_get_random_object_pos(.., 'drop') + _get_random_quat, :107-110,175-191) for a scripted sequence of
+    env-id subsets from torch.manual_seed(seed + 1)."""
+    t, mom = make_task(N, num_initial_poses=P, seed=seed)
+    g = torch.Generator().manual_seed(seed + 100)
+    n_obj = t.cfg_env.objects.num_objects
+    t.objects_dropped = True
+    fill_random_state(t, g)
+    t.object_pos_initial = torch.rand(N, P, n_obj, 3, generator=g) * 0.3 + torch.tensor([0.1, 0.4, 0.5])
+    t.object_quat_initial = rand_quat(g, (N, P, n_obj))
+    out = {k: [] for k in ["target_idx", "cfg_idx", "goal_pos", "object_pos", "object_quat"]}
+    torch.manual_seed(seed)
+    for e in range(E):
+        t.reset_idx(torch.arange(N))
+        rs = t.root_state.view(N, t.num_actors, 13)[:, t.object_actor_env_indices]
+        out["target_idx"].append(t.target_object_index.clone()); out["cfg_idx"].append(t.object_configuration_indices.clone())
+        out["goal_pos"].append(t.goal_pos.clone())
+        out["object_pos"].append(rs[..., 0:3].clone()); out["object_quat"].append(rs[..., 3:7].clone())
+    arrays = {k: torch.stack(v).numpy() for k, v in out.items()}
+    # the drop loop's draws: round 1 drops every env's object i, later rounds the envs whose object missed
+    subsets = [torch.arange(N)] * n_obj + [torch.nonzero(torch.rand(N, generator=g) < 0.3).squeeze(-1)
+                                           for _ in range(2 * n_obj)]
+    torch.manual_seed(seed + 1)
+    pos, quat = [], []
+    for ids in subsets:
+        pos.append(t._get_random_object_pos(ids, "drop"))
+        quat.append(t._get_random_quat(ids))
+    arrays.update(drop_counts=np.array([len(i) for i in subsets]), drop_pos=torch.cat(pos).numpy(),
+                  drop_quat=torch.cat(quat).numpy(), object_pos_initial=t.object_pos_initial.numpy(),
+                  object_quat_initial=t.object_quat_initial.numpy(), object_indices=t.object_indices.numpy(),
+                  seed=np.array(seed), num_initial_poses=np.array(P),
+                  drop_cfg_pos=np.array(t.cfg_env.objects.drop.pos, np.float32),
+                  drop_cfg_noise=np.array(t.cfg_env.objects.drop.noise, np.float32))
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, {k: v.shape for k, v in arrays.items()})
+
+
 def gen_quat(path, M=64, seed=4):
     tu = refload.load("isaacgym.torch_utils")
     mom = refload.load("isaacgymenvs.tasks.hand_arm.task.multi_object_manipulation")
@@ -511,6 +550,9 @@ if __name__ == "__main__":
     if "--pointclouds" in sys.argv:
         gen_pointclouds(os.path.join(HERE, "ur5sih_pointclouds_student.npz"), PC_STUDENT, seed=5)
         gen_pointclouds(os.path.join(HERE, "ur5sih_pointclouds_all.npz"), PC_ALL, seed=6)
+        sys.exit(0)
+    if "--rng" in sys.argv:     # seed-faithful reset / drop draws only
+        gen_ref_rng(os.path.join(HERE, "ur5sih_ref_rng.npz"))
         sys.exit(0)
     if "--bin" in sys.argv:     # bin-picking variant only (8 objects, bin actor layout)
         gen_obs_reward(os.path.join(HERE, "ur5sih_obs_reward_bin8.npz"), n_objects=8, bin_layout=True, seed=11)

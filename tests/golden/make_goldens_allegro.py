@@ -94,7 +94,10 @@ def make_task(N, seed=0):
     t.successes = torch.zeros(N)
     t.consecutive_successes = torch.zeros(1)
     t.extras = {}
-    t.random_force_prob = torch.zeros(N)
+    # allegro_hand.py:191-194: the __init__ draw from the global generator (the first draw of a seeded run)
+    t.force_prob_range = torch.tensor([0.001, 0.1])
+    t.random_force_prob = torch.exp((torch.log(t.force_prob_range[0]) - torch.log(t.force_prob_range[1]))
+                                    * torch.rand(N) + torch.log(t.force_prob_range[1]))
     t.rb_forces = torch.zeros(N, 19, 3)
     t.object_rb_handles = torch.tensor([17])
     t.object_rb_masses = torch.tensor([0.10985])
@@ -102,6 +105,7 @@ def make_task(N, seed=0):
 
 
 def obs_reward(N=32, steps=5, seed=1):
+    torch.manual_seed(seed)
     mod, t = make_task(N)
     g = torch.Generator().manual_seed(seed)
     lo, up = t.shadow_hand_dof_lower_limits, t.shadow_hand_dof_upper_limits
@@ -145,8 +149,8 @@ def obs_reward(N=32, steps=5, seed=1):
 
 def steps(N=24, T=8, seed=2):
     """pre_physics_step -> (no physics) -> post_physics_step, with replayable draws."""
+    torch.manual_seed(seed)          # seeded before the task is built: __init__'s draw is part of the stream
     mod, t = make_task(N)
-    torch.manual_seed(seed)
     g = torch.Generator().manual_seed(seed)
     draws = np.zeros((T, N, DRAW_STRIDE), np.float32)
     cur = {"step": 0, "phase": None, "ids": None}
@@ -203,6 +207,7 @@ def steps(N=24, T=8, seed=2):
             out[k].append(v.clone().numpy())
     res = {k: np.stack(v) for k, v in out.items()}
     res["draws"] = draws
+    res["seed"] = np.array(seed)
     np.savez_compressed(os.path.join(HERE, "allegro_steps.npz"), **res)
 
 

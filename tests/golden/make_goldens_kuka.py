@@ -259,6 +259,7 @@ def randomize_state(t, g, scene_lo, scene_hi):
 
 
 def obs_reward(sub, N=48, steps=4, seed=1):
+    torch.manual_seed(seed)          # random_force_prob's __init__ draw (allegro_kuka_base.py:323-327) is seeded
     mod, base, t, _, _ = make_task(sub, N)
     g = torch.Generator().manual_seed(seed)
     lo, hi = t.arm_hand_dof_lower_limits, t.arm_hand_dof_upper_limits
@@ -300,14 +301,15 @@ def refresh_bodies(t, orc, st):
 
 def steps(sub, N=32, T=8, seed=2):
     from oracle.oracle_lib import HostState, Oracle
-    mod, base, t, _, _ = make_task(sub, N)
+    torch.manual_seed(seed)          # seeded before the task is built: __init__'s random_force_prob draw is the
+    mod, base, t, _, _ = make_task(sub, N)     # first draw of the stream (ref_rng.KukaDraws replays it)
+    prob_init = t.random_force_prob.clone()
     model = HM.build_model(HM.load_scene(SCENE))
     params, cfg = HM.build_params({"subtask": sub}, task=HM.TASK_ALLEGRO_KUKA)
     st = HostState(N, model=model, params=params)
     st["object_scale"][:] = t.object_scales.numpy()[:, None, :]
     st["collision_enabled"][:] = 1
     orc = Oracle(model, params, N)
-    torch.manual_seed(seed)
     g = torch.Generator().manual_seed(seed)
     draws = np.zeros((T, N, HM.DRAW_STRIDE), np.float32)
     cur = {"step": 0, "ids": None, "phase": "pre", "in_target": False, "in_reset": False, "u": None}
@@ -431,6 +433,8 @@ def steps(sub, N=32, T=8, seed=2):
     res = {k: np.stack(v) for k, v in out.items()}
     res["draws"] = draws
     res["object_scale"] = t.object_scales.numpy()
+    res["random_force_prob_init"] = prob_init.numpy()
+    res["seed"] = np.array(seed)
     assert set(keys_in) <= set(res)
     np.savez_compressed(os.path.join(HERE, f"kuka_steps_{sub}.npz"), **res)
 
