@@ -85,34 +85,57 @@ HD float bcast(float x, int src) {
 HD int bcast_i(int x, int src) { return __builtin_amdgcn_readlane(x, src); }
 
 // Reductions: DPP inside each 16-lane row (quad_perm xor1, xor2, row_half_mirror, row_mirror leave the
-// row's result in all 16 lanes), then the four row results via v_readlane. No LDS round trips
-// (a __shfl_xor is a ds_bpermute). Results are wave-uniform.
+// row's result in all 16 lanes), then across rows with row_bcast:15 (row 3 += row 2, row 1 += row 0) and
+// row_bcast:31 (rows 2, 3 += lane 31), and the result read from lane 63 (one v_readlane). Lane 63 holds
+// (r3 op r2) op (r1 op r0) of the four row results r0..r3, which for + is bitwise the (r0 + r1) + (r2 + r3)
+// the oracle's wave_dot emulates (IEEE addition is commutative). No LDS round trips (a __shfl_xor is a
+// ds_bpermute). Results are wave-uniform.
 #define HA_DPP(x, ctrl) __builtin_amdgcn_mov_dpp((x), (ctrl), 0xF, 0xF, true)
 template <int CTRL>
 HD float dpp_f(float x) { return __int_as_float(HA_DPP(__float_as_int(x), CTRL)); }
 template <int CTRL>
 HD int dpp_i(int x) { return HA_DPP(x, CTRL); }
+// cross-row steps: lanes outside the row mask get `old` (only lane 63's result is read)
+template <int CTRL, int RM>
+HD float dpp_row_f(float old, float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(x), CTRL, RM, 0xF, false));
+}
+template <int CTRL, int RM>
+HD int dpp_row_i(int old, int x) { return __builtin_amdgcn_update_dpp(old, x, CTRL, RM, 0xF, false); }
+HD float lane63(float x) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63)); }
 
+// sum of the four row results: (r3 + r2) + (r1 + r0) in lane 63
+HD float rows_sum(float x) {
+    x = x + dpp_row_f<0x142, 0xA>(0.0f, x);
+    x = x + dpp_row_f<0x143, 0xC>(0.0f, x);
+    return lane63(x);
+}
 HD float wave_max(float x) {
     x = fmaxf(x, dpp_f<0xB1>(x));
     x = fmaxf(x, dpp_f<0x4E>(x));
     x = fmaxf(x, dpp_f<0x141>(x));
     x = fmaxf(x, dpp_f<0x140>(x));
-    return fmaxf(fmaxf(bcast(x, 0), bcast(x, 16)), fmaxf(bcast(x, 32), bcast(x, 48)));
+    x = fmaxf(x, dpp_row_f<0x142, 0xA>(x, x));
+    x = fmaxf(x, dpp_row_f<0x143, 0xC>(x, x));
+    return lane63(x);
 }
 HD float wave_min(float x) {
     x = fminf(x, dpp_f<0xB1>(x));
     x = fminf(x, dpp_f<0x4E>(x));
     x = fminf(x, dpp_f<0x141>(x));
     x = fminf(x, dpp_f<0x140>(x));
-    return fminf(fminf(bcast(x, 0), bcast(x, 16)), fminf(bcast(x, 32), bcast(x, 48)));
+    x = fminf(x, dpp_row_f<0x142, 0xA>(x, x));
+    x = fminf(x, dpp_row_f<0x143, 0xC>(x, x));
+    return lane63(x);
 }
 HD int wave_min_i(int x) {
     x = min(x, dpp_i<0xB1>(x));
     x = min(x, dpp_i<0x4E>(x));
     x = min(x, dpp_i<0x141>(x));
     x = min(x, dpp_i<0x140>(x));
-    return min(min(bcast_i(x, 0), bcast_i(x, 16)), min(bcast_i(x, 32), bcast_i(x, 48)));
+    x = min(x, dpp_row_i<0x142, 0xA>(x, x));
+    x = min(x, dpp_row_i<0x143, 0xC>(x, x));
+    return __builtin_amdgcn_readlane(x, 63);
 }
 // arg-min / arg-max with ties broken toward the smaller index (matches a sequential strict-compare
 // scan): the extreme value first, then the smallest index among the lanes that hold it.

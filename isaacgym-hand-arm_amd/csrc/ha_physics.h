@@ -151,6 +151,7 @@ struct PhysCfg {
     static constexpr int kl = KL;
     static constexpr int spill_floats = split ? 2 * 3 * (MAXC * NCH - KL) * ND : 0;   // per env: J then Y
     static_assert(ND + 6 * OCAP <= MAXV, "generalized velocity exceeds MAXV");
+    static_assert(!split || (KL >= 0 && KL <= MAXC * NCH), "LDS link slots must not exceed the contact capacity");
     static_assert(!split || (row_slots<ND>() == 2 && MAXC * NCH <= 64), "split rows: two object slots, <= 64 contacts");
 };
 template <class PC>
@@ -179,6 +180,9 @@ struct SimCtx {
     int maxc;               // contact capacity (MAXC x chunks of the kernel family)
     const float* dr;        // this env's domain-randomization row (HA_DR_*), or null when DR is off
     float* spill;           // split rows: this env's global robot-block rows beyond the LDS slots (J, then Y)
+    // narrow-phase cache: (hull, body) whose world vertices / planes are in ColScratch side A / side B. Within one
+    // detect() the poses do not change, so consecutive pairs that share a side skip its setup (same values).
+    int colA_h, colA_b, colB_h, colB_b;
 };
 
 // friction of a contact body (link 100+L, object o, static -1) and of a contact (PhysX average combine)
@@ -195,8 +199,7 @@ HD float wave_sum_rows(float x) {
     x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
     x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, true));  // row_half_mirror
     x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xF, 0xF, true));  // row_mirror
-    float r0 = bcast(x, 0), r1 = bcast(x, 16), r2 = bcast(x, 32), r3 = bcast(x, 48);
-    return (r0 + r1) + (r2 + r3);
+    return rows_sum(x);     // (r3 + r2) + (r1 + r0) == (r0 + r1) + (r2 + r3) bitwise
 }
 
 // Diagnostic phase timers (built only into libhandarm_hip_prof.so, -DHA_PROFILE): lane 0 of every
@@ -228,9 +231,9 @@ HD void wave_sum_rows3(float& a, float& b, float& c) {
     a += dpp_f<0x4E>(a); b += dpp_f<0x4E>(b); c += dpp_f<0x4E>(c);
     a += dpp_f<0x141>(a); b += dpp_f<0x141>(b); c += dpp_f<0x141>(c);
     a += dpp_f<0x140>(a); b += dpp_f<0x140>(b); c += dpp_f<0x140>(c);
-    a = (bcast(a, 0) + bcast(a, 16)) + (bcast(a, 32) + bcast(a, 48));
-    b = (bcast(b, 0) + bcast(b, 16)) + (bcast(b, 32) + bcast(b, 48));
-    c = (bcast(c, 0) + bcast(c, 16)) + (bcast(c, 32) + bcast(c, 48));
+    a = a + dpp_row_f<0x142, 0xA>(0.0f, a); b = b + dpp_row_f<0x142, 0xA>(0.0f, b); c = c + dpp_row_f<0x142, 0xA>(0.0f, c);
+    a = a + dpp_row_f<0x143, 0xC>(0.0f, a); b = b + dpp_row_f<0x143, 0xC>(0.0f, b); c = c + dpp_row_f<0x143, 0xC>(0.0f, c);
+    a = lane63(a); b = lane63(b); c = lane63(c);
 }
 
 // ----------------------------------------------------------------------------- kinematics
@@ -661,8 +664,9 @@ HD void sat_planes(const SimCtx& c, const float (*wp)[4], int np, const float (*
     kbest = bk;
 }
 
-// hull A (body a) vs hull B (body b); normal from B to A
-HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int b) {
+// hull A (body a) vs hull B (body b); normal from B to A. keyA / keyB identify the posed hull of each side for
+// the ColScratch cache (the body code, or -100 - k for static body k: statics may share a hull)
+HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int b, int keyA, int keyB) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     float mg = c.p->contact_margin;
@@ -681,24 +685,33 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
 #else
 #define HPROF(i)
 #endif
-    // world vertices and planes of both hulls, once
-    if (lane < nva) st3(cs.wvA[lane], PA.p + qrot(PA.q, scale3(c, a, ld3(m.verts[m.hull_vert_start[ha] + lane]))));
-    if (lane < nvb) st3(cs.wvB[lane], PB.p + qrot(PB.q, scale3(c, b, ld3(m.verts[m.hull_vert_start[hb] + lane]))));
-    bool scA = body_scaled(c, a), scB = body_scaled(c, b);
-    f3 isA = inv_scale(c, a), isB = inv_scale(c, b);
-    for (int k = lane; k < npa; k += 64) {
-        f3 n; float d;
-        world_plane(m, ha, k, PA, scA, isA, n, d);
-        st3(cs.wpA[k], n);
-        cs.wpA[k][3] = d;
+    // world vertices and planes of both hulls, unless this side's (hull, body) is already in ColScratch
+    bool needA = ha != c.colA_h || keyA != c.colA_b, needB = hb != c.colB_h || keyB != c.colB_b;
+    if (needA) {
+        if (lane < nva) st3(cs.wvA[lane], PA.p + qrot(PA.q, scale3(c, a, ld3(m.verts[m.hull_vert_start[ha] + lane]))));
+        bool scA = body_scaled(c, a);
+        f3 isA = inv_scale(c, a);
+        for (int k = lane; k < npa; k += 64) {
+            f3 n; float d;
+            world_plane(m, ha, k, PA, scA, isA, n, d);
+            st3(cs.wpA[k], n);
+            cs.wpA[k][3] = d;
+        }
+        c.colA_h = ha; c.colA_b = keyA;
     }
-    for (int k = lane; k < npb; k += 64) {
-        f3 n; float d;
-        world_plane(m, hb, k, PB, scB, isB, n, d);
-        st3(cs.wpB[k], n);
-        cs.wpB[k][3] = d;
+    if (needB) {
+        if (lane < nvb) st3(cs.wvB[lane], PB.p + qrot(PB.q, scale3(c, b, ld3(m.verts[m.hull_vert_start[hb] + lane]))));
+        bool scB = body_scaled(c, b);
+        f3 isB = inv_scale(c, b);
+        for (int k = lane; k < npb; k += 64) {
+            f3 n; float d;
+            world_plane(m, hb, k, PB, scB, isB, n, d);
+            st3(cs.wpB[k], n);
+            cs.wpB[k][3] = d;
+        }
+        c.colB_h = hb; c.colB_b = keyB;
     }
-    wsync();
+    if (needA || needB) wsync();
     HPROF(25);
     float sepA, sepB;
     int kA, kB;
@@ -805,6 +818,8 @@ HD void detect(SimCtx& c) {
     const ha_model_t& m = *c.m;
     int lane = c.lane;
     if (lane == 0) s.nc = 0;
+    c.colA_h = c.colB_h = -1;       // poses changed since the last detect(): no cached hull sides
+    c.colA_b = c.colB_b = -1000;
     int NO = c.NO, NLH = m.n_link_hulls, NS = m.n_static;
     int npairs = 0;
     for (int o = 0; o < NO; o++) npairs += 1 + NS + (NO - 1 - o) + NLH;
@@ -868,12 +883,13 @@ HD void detect(SimCtx& c) {
                 collide_ground(c, m.pool_hull[c.o[A].pool], object_pose(c, A), A);
                 continue;
             }
-            int h1, h2, b1, b2;
+            int h1, h2, b1, b2, k2;
             PoseF P1, P2;
             if (kind <= 3) {
                 int ho = m.pool_hull[c.o[A].pool];
                 PoseF Po = object_pose(c, A);
-                if (kind == 1) { h1 = ho; P1 = Po; b1 = A; h2 = m.static_hull[B]; P2 = static_pose(m, B); b2 = -1; }
+                k2 = 0;
+                if (kind == 1) { h1 = ho; P1 = Po; b1 = A; h2 = m.static_hull[B]; P2 = static_pose(m, B); b2 = -1; k2 = -100 - B; }
                 else if (kind == 2) { h1 = ho; P1 = Po; b1 = A; h2 = m.pool_hull[c.o[B].pool]; P2 = object_pose(c, B); b2 = B; }
                 else {
                     int Lk = m.hull_link[B];
@@ -882,13 +898,14 @@ HD void detect(SimCtx& c) {
             } else {
                 int Lk = m.hull_link[A];
                 h1 = A; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = m.static_hull[B];
-                P2 = static_pose(m, B); b2 = -1;
+                P2 = static_pose(m, B); b2 = -1; k2 = -100 - B;
             }
+            if (kind == 2 || kind == 3) k2 = b2;
 #ifdef HA_PROFILE
             unsigned long long _k0 = __builtin_amdgcn_s_memtime();
             int _nc0 = s.nc;
 #endif
-            collide_hulls(c, h1, P1, h2, P2, b1, b2);
+            collide_hulls(c, h1, P1, h2, P2, b1, b2, b1, k2);
 #ifdef HA_PROFILE
             wsync();
             PROF_COUNT(10 + kind, __builtin_amdgcn_s_memtime() - _k0);

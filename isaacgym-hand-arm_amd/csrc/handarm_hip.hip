@@ -566,7 +566,7 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     if (model->n_links > HA_MAX_LINKS || params->n_objects < 1 || params->n_objects > obj_capacity(fam) ||
         model->n_dofs + 6 * (params->n_objects < 2 ? params->n_objects : 2) > task_row_stride(params->task) ||
         model->n_dofs + 6 * params->n_objects > MAXV || model->n_bodies > MAXB ||
-        model->n_static < 0 || model->n_static > HA_MAX_STATIC ||
+        model->n_static < 0 || model->n_static > HA_MAX_STATIC || model->n_pool < 1 || model->n_pool > HA_MAX_POOL ||
         model->n_link_hulls + model->n_pool + model->n_static > HA_MAX_HULLS)
         return HA_E_MODEL;
     for (int k = 0; k < model->n_hulls; k++)

@@ -43,10 +43,13 @@ if __name__ == "__main__":
         print("    hull-hull split: " + "  ".join(f"{nm} {100.0 * buf[25 + i] / tot:5.1f}%" for i, nm in
               enumerate(["setup", "SAT A", "SAT B", "clip", "emit"])), flush=True)
 
-    if "--bench-scene" in sys.argv or "--kuka" in sys.argv or "--bin" in sys.argv:
+    if any(f in sys.argv for f in ("--bench-scene", "--kuka", "--bin", "--allegro")):
         # the bench workload: VecTask after its first (reset) steps, random actions
-        from handarm_hip.tasks import AllegroKuka, Ur5SihMultiObjectManipulation
-        if "--kuka" in sys.argv:
+        from handarm_hip.tasks import AllegroHand, AllegroKuka, Ur5SihMultiObjectManipulation
+        if "--allegro" in sys.argv:
+            n = int(args[0]) if args else 16384
+            env = AllegroHand({"env": {"numEnvs": n}, "seed": 42}, "cuda:0", "cuda:0")
+        elif "--kuka" in sys.argv:
             n = int(args[0]) if args else 4096
             env = AllegroKuka({"env": {"numEnvs": n}, "seed": 42}, "cuda:0", "cuda:0")
         elif "--bin" in sys.argv:       # bench --task binpick (config 5 shard)
