@@ -183,6 +183,9 @@ struct SimCtx {
     // narrow-phase cache: (hull, body) whose world vertices / planes are in ColScratch side A / side B. Within one
     // detect() the poses do not change, so consecutive pairs that share a side skip its setup (same values).
     int colA_h, colA_b, colB_h, colB_b;
+#ifdef HA_AB_TIMING
+    bool dry;               // A/B timing builds only: a repeated phase that must not emit contacts
+#endif
 };
 
 // friction of a contact body (link 100+L, object o, static -1) and of a contact (PhysX average combine)
@@ -520,6 +523,9 @@ HD f3 inv_scale(const SimCtx& c, int b) {
 HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int b) {
     EnvLDS& s = *c.s;
     int lane = c.lane;
+#ifdef HA_AB_TIMING
+    if (c.dry) return;
+#endif
     // the chosen lanes live in scalars, never in an indexed private array (which would go to scratch)
     float v0 = valid ? sep : 3.0e38f;
     int i0 = valid ? lane : 1 << 20;
@@ -905,7 +911,15 @@ HD void detect(SimCtx& c) {
             unsigned long long _k0 = __builtin_amdgcn_s_memtime();
             int _nc0 = s.nc;
 #endif
+#ifdef HA_AB_NARROW_TWICE
+            for (int rep = 0; rep < 2; rep++) {     // one call site: the same code size as the product
+                if (rep == 1) { c.dry = true; c.colA_h = c.colB_h = -1; }
+                collide_hulls(c, h1, P1, h2, P2, b1, b2, b1, k2);
+            }
+            c.dry = false;
+#else
             collide_hulls(c, h1, P1, h2, P2, b1, b2, b1, k2);
+#endif
 #ifdef HA_PROFILE
             wsync();
             PROF_COUNT(10 + kind, __builtin_amdgcn_s_memtime() - _k0);
@@ -957,10 +971,20 @@ HD void substep(SimCtx& c, float hdt) {
     const ha_params_t& p = *c.p;
     int lane = c.lane, D = c.D, NO = c.NO;
     int NV = D + 6 * NO;
+#ifdef HA_AB_DYN_TWICE
+    for (int rep = 0; rep < 2; rep++) {
+        fk(c);
+        dynamics(c);
+    }
+#else
     fk(c);
     PROF(0);
     dynamics(c);
+#endif
     PROF(1);
+#ifdef HA_AB_FACTOR_TWICE
+    for (int rep = 0; rep < 2; rep++)
+#endif
     factor_inverse<ND>(c);
     // free motion: velocity-product forces only (drives are constraint rows of the PGS below)
     if (lane < D) {
@@ -1012,7 +1036,19 @@ HD void substep(SimCtx& c, float hdt) {
     }
     wsync();
     PROF(2);
+#ifdef HA_AB_DETECT_TWICE
+    for (int rep = 0; rep < 2; rep++) {
+        int nc0 = s.nc;
+        wsync();
+        c.dry = rep == 1;
+        detect(c);
+        c.dry = false;
+        if (rep == 1 && lane == 0) s.nc = nc0;
+        wsync();
+    }
+#else
     detect(c);
+#endif
     PROF(3);
     PROF_COUNT(8, s.nc);
     PROF_COUNT(9, 1);
@@ -1171,6 +1207,7 @@ HD void substep(SimCtx& c, float hdt) {
         vt_lo = s_lo > 0 ? -s_lo / hdt : -p.baumgarte * s_lo / hdt;
         vt_up = s_up > 0 ? -s_up / hdt : -p.baumgarte * s_up / hdt;
     }
+    const uint64_t lo_mask = __ballot(act_lo != 0), up_mask = __ballot(act_up != 0);
     // generalized velocity: coordinate `lane` in vreg, coordinate 64 + lane in vregh (VW == 2 only)
     float vreg = lane < NV ? s.v[lane] : 0.0f;
     float vregh = (VW == 2 && lane + 64 < NV) ? s.v[lane + 64] : 0.0f;
@@ -1180,33 +1217,36 @@ HD void substep(SimCtx& c, float hdt) {
     //      contact rows r = 0..nr-1.  Same row order and arithmetic as the oracle.
     const float* J = Jb;
     const float* Y = Yb;
+#ifdef HA_AB_PGS_TWICE
+    for (int it = 0; it < 2 * p.solver_iters; it++) {
+#else
     for (int it = 0; it < p.solver_iters; it++) {
+#endif
+        // Each joint row's update is computed by the lane that owns the joint (its own v[d], lambda and row
+        // constants: the same operands the oracle uses), and only the impulse change crosses lanes (one
+        // v_readlane); the joint-limit rows run only for the joints whose limit is active (ballot masks).
         for (int d = 0; d < D; d++) {
             float mrow = lane < D ? s.Minv[d * D + lane] : 0.0f;
-            float vd = bcast(vreg, d), ld = bcast(dlam, d);
-            float nl = ld - (vd + bcast(dbias, d) + bcast(dgam, d) * ld) * bcast(dwinv, d);
-            float lim = bcast(dlim, d);
-            nl = nl < -lim ? -lim : (nl > lim ? lim : nl);
-            float dl = nl - ld;
+            float nl = dlam - (vreg + dbias + dgam * dlam) * dwinv;
+            nl = nl < -dlim ? -dlim : (nl > dlim ? dlim : nl);
+            float dl = bcast(nl - dlam, d);
             if (dl != 0.0f) {
                 if (lane == d) dlam = nl;
                 vreg += mrow * dl;
             }
-            if (bcast_i(act_lo, d)) {
-                float l0 = bcast(lam_lo, d);
-                float n0 = l0 - (bcast(vreg, d) - bcast(vt_lo, d)) * bcast(lwinv, d);
+            if ((lo_mask >> d) & 1ull) {
+                float n0 = lam_lo - (vreg - vt_lo) * lwinv;
                 n0 = n0 < 0.0f ? 0.0f : n0;
-                float d0 = n0 - l0;
+                float d0 = bcast(n0 - lam_lo, d);
                 if (d0 != 0.0f) {
                     if (lane == d) lam_lo = n0;
                     vreg += mrow * d0;
                 }
             }
-            if (bcast_i(act_up, d)) {
-                float l1 = bcast(lam_up, d);
-                float n1 = l1 - (-bcast(vreg, d) - bcast(vt_up, d)) * bcast(lwinv, d);
+            if ((up_mask >> d) & 1ull) {
+                float n1 = lam_up - (-vreg - vt_up) * lwinv;
                 n1 = n1 < 0.0f ? 0.0f : n1;
-                float d1 = n1 - l1;
+                float d1 = bcast(n1 - lam_up, d);
                 if (d1 != 0.0f) {
                     if (lane == d) lam_up = n1;
                     vreg -= mrow * d1;
@@ -1285,19 +1325,20 @@ HD void substep(SimCtx& c, float hdt) {
                     jv2 = jv2 + h2 * vregh;
                 }
                 wave_sum_rows3(jv0, jv1, jv2);
-                float l0 = bcast(lam[ch], r0), l1 = bcast(lam[ch], r0 + 1), l2 = bcast(lam[ch], r0 + 2);
-                float n0 = l0 - (jv0 - bcast(vt[ch], r0)) * bcast(winv[ch], r0);
+                // the block's three rows live in lanes r0, r0 + 1, r0 + 2: each lane evaluates its own row with
+                // its own lambda and constants (the oracle's operands) and only n0, d0, d1, d2 cross lanes
+                float lm = lam[ch];
+                float n0 = lm - (jv0 - vt[ch]) * winv[ch];
                 n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
-                float d0 = n0 - l0;
-                float hi = bcast(cmu[ch], r0) * n0;
-                jv1 = jv1 + bcast(ca0[ch], r0 + 1) * d0;
-                float n1 = l1 - (jv1 - bcast(vt[ch], r0 + 1)) * bcast(winv[ch], r0 + 1);
+                float d0 = bcast(n0 - lm, r0);
+                n0 = bcast(n0, r0);
+                float hi = cmu[ch] * n0;
+                float n1 = lm - ((jv1 + ca0[ch] * d0) - vt[ch]) * winv[ch];
                 n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
-                float d1 = n1 - l1;
-                jv2 = (jv2 + bcast(ca0[ch], r0 + 2) * d0) + bcast(ca1[ch], r0 + 2) * d1;
-                float n2 = l2 - (jv2 - bcast(vt[ch], r0 + 2)) * bcast(winv[ch], r0 + 2);
+                float d1 = bcast(n1 - lm, r0 + 1);
+                float n2 = lm - (((jv2 + ca0[ch] * d0) + ca1[ch] * d1) - vt[ch]) * winv[ch];
                 n2 = n2 < -hi ? -hi : (n2 > hi ? hi : n2);
-                float d2 = n2 - l2;
+                float d2 = bcast(n2 - lm, r0 + 2);
                 if (lane == r0) lam[ch] = n0;
                 if (lane == r0 + 1) lam[ch] = n1;
                 if (lane == r0 + 2) lam[ch] = n2;

@@ -290,6 +290,9 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     int env = blockIdx.x;
     if (env >= num_envs) return;
     SimCtx c;
+#ifdef HA_AB_TIMING
+    c.dry = false;
+#endif
     c.m = model;
     c.p = params;
     c.s = reinterpret_cast<EnvLDS*>(smem);

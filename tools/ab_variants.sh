@@ -3,7 +3,7 @@
 # (paths relative to isaacgym-hand-arm_amd/handarm_hip/; "product" = libhandarm_hip.so). Two alternating rounds,
 # one bench process per (build, round); prints value and mean step-kernel ms per run.
 R=$PWD; TASK=$1; shift
-for i in 1 2; do
+for i in $(seq 1 ${AB_ROUNDS:-2}); do
   for L in "$@"; do
     [ "$L" = product ] && L=libhandarm_hip.so
     timeout -k 10 200 python -c "
