@@ -23,6 +23,8 @@
  *                                  (vec_task.py:390-441 -> configurable_vec_task.py:347-414)
  *   ha_task_observe                post_step callbacks + compute_reward + compute_observations alone
  *   ha_task_reset                  reset_idx steady state (multi_object_manipulation.py:33-71)
+ *   ha_task_epilogue               VecTask.step's torch.clamp(obs_buf) and the AllegroKuka extras means
+ *                                  (vec_task.py:437, allegro_kuka_base.py:908-917)
  *   ha_pointclouds                 synthetic point-cloud observables' post_step refresh
  *                                  (multi_object.py:792-809, ur5sih.py:361-374)
  *   ha_gather_obs                  compute_observations' torch.cat for a custom observation list
@@ -373,11 +375,16 @@ int ha_set_dof_position_target_indexed(ha_handle h, const float* targets, const 
 int ha_set_object_collision_filter(ha_handle h, const uint8_t* enabled, void* stream);
 /* fused task entry points */
 /* per-step log counters go to slot (step_counter % n_slots) of stats[n_slots][HA_STAT_SIZE] and
- * term_sums[n_slots][4]; the slot is zeroed on the stream before the step kernel. Default 1 slot. */
+ * term_sums[n_slots][4]. Each step launch clears the NEXT step's slot, so a written slot must be read within
+ * n_slots - 1 steps. n_slots >= 2; setting the ring clears it. */
 int ha_set_stats_ring(ha_handle h, int32_t n_slots);
 int ha_task_step(ha_handle h, uint32_t flags, void* stream);
 int ha_task_observe(ha_handle h, uint32_t flags, void* stream);
 int ha_task_reset(ha_handle h, uint32_t flags, void* stream);
+/* VecTask.step's tail in one launch (vec_task.py:437, allegro_kuka_base.py:908-917): obs_out (if non-null,
+ * N x num_obs floats) = clamp(obs, -clip_obs, clip_obs); AllegroKuka only: scalars (if non-null, 4 floats) =
+ * mean prev_episode_successes, mean / min / max true_objective over the shard. */
+int ha_task_epilogue(ha_handle h, float* obs_out, float clip_obs, float* scalars, void* stream);
 /* last kernel time in ms measured with HIP events around the most recent physics/step launch (-1 if none) */
 float ha_last_kernel_ms(ha_handle h);
 /* per-launch HIP-event timing of the env kernel (bench roofline): record up to max_launches launches

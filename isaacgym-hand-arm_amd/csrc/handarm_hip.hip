@@ -313,6 +313,12 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
         S.stats = st.stats + stat_slot * HA_STAT_SIZE;
         S.term_sums = st.term_sums + stat_slot * 4;
     }
+    if (MODE == MODE_STEP && env == 0) {
+        // MODE_STEP: n_calls = the stats-ring slot of the NEXT step, cleared here (this launch only adds into
+        // stat_slot; the next step's launch runs after this one on the stream), so no memset per step
+        if (c.lane < HA_STAT_SIZE) st.stats[n_calls * HA_STAT_SIZE + c.lane] = 0;
+        if (c.lane < 4) st.term_sums[n_calls * 4 + c.lane] = 0.0f;
+    }
     if (MODE == MODE_OBSERVE) {
         if (TASK == HA_TASK_ALLEGRO_KUKA) {
             ak_in_from_tensors(c, S, env, &akp.in);
@@ -461,6 +467,48 @@ extern "C" __global__ void ha_copy_indexed_kernel(float* dst, const float* src, 
     int i = t / per, k = t % per;
     size_t base = (size_t)idx[i] * per;
     dst[base + k] = src[base + k];
+}
+
+// ----------------------------------------------------------------------------- step epilogue
+// VecTask.step's tail as ONE launch (instead of a clamp kernel plus one reduction kernel per logged scalar):
+// obs_out = clamp(obs, -clip, clip) (vec_task.py:437, a fresh buffer for obs_dict["obs"]), and for AllegroKuka the
+// extras scalars of allegro_kuka_base.py:908-917: mean prev_episode_successes, mean / min / max true_objective.
+// Block 0 reduces (fixed-order strided partial sums, then an LDS tree: deterministic); every block copies.
+extern "C" __global__ void __launch_bounds__(256) ha_epilogue_kernel(const float* __restrict__ obs,
+                                                                      float* __restrict__ obs_out, long long n_obs,
+                                                                      float clip, const float* __restrict__ ts,
+                                                                      int ts_stride, int n_env, float* __restrict__ out) {
+    long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    long long stride = (long long)gridDim.x * 256;
+    if (obs_out)
+        for (long long k = i; k < n_obs; k += stride) obs_out[k] = fminf(fmaxf(obs[k], -clip), clip);
+    if (blockIdx.x != 0 || !ts || !out) return;
+    __shared__ float red[4][256];
+    float s0 = 0.0f, s1 = 0.0f, mn = 3.0e38f, mx = -3.0e38f;
+    for (int e = threadIdx.x; e < n_env; e += 256) {
+        float ps = ts[(size_t)e * ts_stride + HA_AK_PREV_SUCC], to = ts[(size_t)e * ts_stride + HA_AK_TRUE_OBJ];
+        s0 += ps;
+        s1 += to;
+        mn = fminf(mn, to);
+        mx = fmaxf(mx, to);
+    }
+    red[0][threadIdx.x] = s0; red[1][threadIdx.x] = s1; red[2][threadIdx.x] = mn; red[3][threadIdx.x] = mx;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + w];
+            red[1][threadIdx.x] += red[1][threadIdx.x + w];
+            red[2][threadIdx.x] = fminf(red[2][threadIdx.x], red[2][threadIdx.x + w]);
+            red[3][threadIdx.x] = fmaxf(red[3][threadIdx.x], red[3][threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = red[0][0] / (float)n_env;
+        out[1] = red[1][0] / (float)n_env;
+        out[2] = red[2][0];
+        out[3] = red[3][0];
+    }
 }
 
 // ----------------------------------------------------------------------------- C ABI
@@ -715,10 +763,14 @@ int ha_set_object_collision_filter(ha_handle h, const uint8_t* enabled, void* st
     return HA_OK;
 }
 
+// n_slots >= 2: a step clears the next step's slot (so a slot folds no later than n_slots - 1 steps after it
+// was written). Clears the whole ring.
 int ha_set_stats_ring(ha_handle h, int32_t n_slots) {
-    if (!h || n_slots < 1) return HA_E_ARG;
+    if (!h || n_slots < 2) return HA_E_ARG;
     h->stat_slots = n_slots;
     h->step_counter = 0;
+    if (h->bound && h->st.stats) HIPCHK(hipMemset(h->st.stats, 0, sizeof(int32_t) * HA_STAT_SIZE * (size_t)n_slots));
+    if (h->bound && h->st.term_sums) HIPCHK(hipMemset(h->st.term_sums, 0, sizeof(float) * 4 * (size_t)n_slots));
     return HA_OK;
 }
 
@@ -734,11 +786,11 @@ static bool task_bound(ha_handle h) {
 int ha_task_step(ha_handle h, uint32_t flags, void* stream) {
     if (!h || !h->bound || !h->st.actions || !h->st.obs || !h->st.stats || !h->st.term_sums || !task_bound(h))
         return HA_E_STATE;
+    if (h->stat_slots < 2) return HA_E_STATE;
     int slot = (int)(h->step_counter % h->stat_slots);
+    int next = (int)((h->step_counter + 1) % h->stat_slots);
     h->step_counter++;
-    HIPCHK(hipMemsetAsync(h->st.stats + slot * HA_STAT_SIZE, 0, sizeof(int32_t) * HA_STAT_SIZE, (hipStream_t)stream));
-    HIPCHK(hipMemsetAsync(h->st.term_sums + slot * 4, 0, sizeof(float) * 4, (hipStream_t)stream));
-    int rc = launch(h, MODE_STEP, 0, flags, slot, stream);
+    int rc = launch(h, MODE_STEP, next, flags, slot, stream);     // clears `next` for the following step
     if (rc == HA_OK && h->task == HA_TASK_ALLEGRO_HAND && h->st.consecutive_successes) {
         // consecutive_successes EWMA over the shard's resets of this step (allegro_hand.py:714-717)
         hipLaunchKernelGGL(ah_consecutive_successes_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
@@ -747,6 +799,18 @@ int ha_task_step(ha_handle h, uint32_t flags, void* stream) {
         HIPCHK(hipGetLastError());
     }
     return rc;
+}
+
+int ha_task_epilogue(ha_handle h, float* obs_out, float clip_obs, float* scalars, void* stream) {
+    if (!h || !h->bound || !h->st.obs) return HA_E_STATE;
+    if (scalars && (h->task != HA_TASK_ALLEGRO_KUKA || !h->st.task_state)) return HA_E_ARG;
+    long long n = (long long)h->N * h->h_params.num_obs;
+    int blocks = (int)((n + 255) / 256);
+    blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+    hipLaunchKernelGGL(ha_epilogue_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, h->st.obs, obs_out, n,
+                       clip_obs, scalars ? h->st.task_state : nullptr, HA_AK_TS, h->N, scalars);
+    HIPCHK(hipGetLastError());
+    return HA_OK;
 }
 
 int ha_task_observe(ha_handle h, uint32_t flags, void* stream) {

@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from .. import model as HM
+from .. import _lib
 from .. import ref_rng as RR
 from ..sim import HandArmSim
 from .ur5sih_multi_object_manipulation import Box
@@ -91,6 +92,8 @@ class AllegroHand:
         self._rr = RR.AllegroDraws(N) if self.reference_rng else None
         self.extras = {}
         self.obs_dict = {}
+        # obs_dict["obs"] = clamp(obs_buf) by ha_task_epilogue into one of two alternating buffers
+        self._obs_out = torch.zeros((2, N, self.num_observations), device=sim_device)
         self.control_steps = 0
         self.total_successes = 0
         self.total_resets = 0
@@ -141,8 +144,11 @@ class AllegroHand:
         self.sim.task_step(self.sim_flags | self._reference_draws())
         self.control_steps += 1
         self.extras["time_outs"] = self.timeout_buf.view(torch.bool).to(self.rl_device)
-        self.extras["consecutive_successes"] = self.consecutive_successes.mean()     # allegro_hand.py:393
-        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        self.extras["consecutive_successes"] = self.consecutive_successes.view(())     # allegro_hand.py:393 (1 value)
+        out = self._obs_out[self.control_steps & 1]
+        _lib.check(self.sim.lib.ha_task_epilogue(self.sim.h, out.data_ptr(), self.clip_obs, None, self.sim._stream()),
+                   "ha_task_epilogue")
+        self.obs_dict["obs"] = out.to(self.rl_device)
         return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras
 
     def reset(self):

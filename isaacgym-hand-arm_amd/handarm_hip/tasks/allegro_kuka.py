@@ -16,6 +16,7 @@ import numpy as np
 import torch
 
 from .. import model as HM
+from .. import _lib
 from .. import ref_rng as RR
 from ..sim import HandArmSim
 from .ur5sih_multi_object_manipulation import Box
@@ -125,6 +126,11 @@ class AllegroKuka:
         self.frame_since_restart = 0
         self.extras = {}
         self.obs_dict = {}
+        # step tail (ha_task_epilogue, one launch): obs_dict["obs"] = clamp(obs_buf) in one of two alternating
+        # buffers (a fresh tensor as the reference's torch.clamp returns, valid until the step after next) and
+        # the extras means in two alternating 4-float rows
+        self._obs_out = torch.zeros((2, N, self.num_observations), device=sim_device)
+        self._scalars = torch.zeros((2, 4), device=sim_device)
         # seed-faithful draws (handarm_hip/ref_rng.py): every reset / force value from torch's global CPU
         # generator in the reference's order; random_force_prob is drawn here, as at allegro_kuka_base.py:323-327
         self.reference_rng = bool(cfg.get("sim", {}).get("reference_rng", False))
@@ -197,16 +203,20 @@ class AllegroKuka:
         self.frame_since_restart += 1
         self._curriculum()
         self.sim.task_step(self.sim_flags | self._reference_draws())
+        k = self.frame_since_restart & 1
+        out, sc = self._obs_out[k], self._scalars[k]
+        _lib.check(self.sim.lib.ha_task_epilogue(self.sim.h, out.data_ptr(), self.clip_obs, sc.data_ptr(),
+                                                 self.sim._stream()), "ha_task_epilogue")
         ex = self.extras
         ex["time_outs"] = self.timeout_buf.view(torch.bool).to(self.rl_device)
-        ex["successes"] = self.prev_episode_successes.mean()                   # :908-917
+        ex["successes"] = sc[0]                                                # :908-917
         ex["true_objective"] = self.true_objective
-        ex["true_objective_mean"] = self.true_objective.mean()
-        ex["true_objective_min"] = self.true_objective.min()
-        ex["true_objective_max"] = self.true_objective.max()
+        ex["true_objective_mean"] = sc[1]
+        ex["true_objective_min"] = sc[2]
+        ex["true_objective_max"] = sc[3]
         ex["rewards_episode"] = self.rewards_episode
         ex["scalars"] = {"success_tolerance": self.success_tolerance}
-        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        self.obs_dict["obs"] = out.to(self.rl_device)
         self.obs_dict["states"] = self.states_buf
         return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras
 

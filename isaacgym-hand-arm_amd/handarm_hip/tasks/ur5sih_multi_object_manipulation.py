@@ -473,8 +473,10 @@ class Ur5SihMultiObjectManipulation:
             actions = actions + self.sim.params.dr_act_noise * torch.randn_like(actions)
         action_tensor = torch.clamp(actions, -self.clip_actions, self.clip_actions)
         self.actions_buf.copy_(action_tensor)
-        if self._stat_pending == self.sim.stats_ring:
-            parallel.reduce_episode_stats(self)      # ring full: reduce across ranks (if any), then fold
+        if self._stat_pending >= self.sim.stats_ring - 1:
+            # ring full (this step's launch clears the slot after its own, the oldest pending one): reduce
+            # across ranks (if any), then fold
+            parallel.reduce_episode_stats(self)
         if self.pointclouds is not None:           # object_pos as of the previous refresh (see observables.py)
             self.pointclouds.snapshot_object_pose(self.sim.t["obs_cache"])
         self.sim.task_step(self.sim_flags | self._reference_draws())
