@@ -365,6 +365,8 @@ def run_config(task, envs, args, world, rank, device, log_interval_fn):
     if world > 1:
         torch.distributed.barrier()
     env.sim.enable_kernel_timing(args.steps)
+    if hasattr(env, "contact_stats"):
+        env.contact_stats(reset=True)               # contact-list diagnostics of the timed steps only
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     torch.cuda.synchronize()
     if world > 1:

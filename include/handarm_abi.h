@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 6
+#define HA_ABI_VERSION 7
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -285,6 +285,11 @@ typedef struct ha_state_t {
     float* task_state;          /* [N][HA_AK_TS] AllegroKuka per-env task state */
     float* task_scalars;        /* [4] AllegroKuka host-curriculum scalars: success_tolerance,
                                  * tolerance objective, 1 if tolerance > target, keypoint success tolerance */
+    /* v7 */
+    int32_t* contact_stats;     /* [N][4] contact-list diagnostics added up by every launch (null = off):
+                                 * substeps, substeps whose narrow phases offered more contacts than the list
+                                 * holds (the shallowest are dropped), max contacts offered in one substep,
+                                 * sum of contacts offered */
 } ha_state_t;
 
 /* stats layout (int32): [0] num_resets, [1] num_successes, then per pool object
@@ -330,7 +335,10 @@ typedef struct ha_pointcloud_t {
     int32_t flange_slot;           /* links[] slot of the UR5 flange */
 } ha_pointcloud_t;
 
-#define HA_MAX_OBS_SOURCES 4
+#define HA_MAX_OBS_SOURCES 8
+/* ha_gather_obs: a column whose source index has this bit reads its source row at an extra offset of
+ * target_object_index[env] * 13 floats (the target object's root-state row: target_object_* observables) */
+#define HA_OBS_SRC_TARGET 16
 
 /* Camera sensors (hand_arm/utils/camera.py:84-333; cameras of Ur5SihMultiObject.yaml:35-53). The camera looks along
  * its local +X axis with +Z up (Isaac Gym camera frame); images are [N][height][width] like the reference's

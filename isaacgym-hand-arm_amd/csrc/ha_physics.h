@@ -86,7 +86,8 @@ struct EnvLDS {
     float Minv[MAXD * MAXD];                    // S ~ M^-1 (factor_inverse), stride D
     float Cb[MAXD];
     float v[MAXV];
-    int nc, nr, pad0, pad1;
+    int nc, nr, noff, pad1;                     // contacts kept / rows / contacts offered this substep
+    int cst[4];                                 // contact_stats of this launch (see ha_state_t)
     union {
         PostScratch pd;
         ColScratch col;
@@ -554,6 +555,7 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
         j3 = i3;
         k = 2 + (h2 ? 1 : 0) + (h3 ? 1 : 0);
     }
+    if (lane == 0) s.noff += k;
     // gather the chosen points to every lane, lane 0 appends
     f3 P[4];
     float S[4];
@@ -823,7 +825,7 @@ HD void detect(SimCtx& c) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     int lane = c.lane;
-    if (lane == 0) s.nc = 0;
+    if (lane == 0) { s.nc = 0; s.noff = 0; }
     c.colA_h = c.colB_h = -1;       // poses changed since the last detect(): no cached hull sides
     c.colA_b = c.colB_b = -1000;
     int NO = c.NO, NLH = m.n_link_hulls, NS = m.n_static;
@@ -1050,6 +1052,13 @@ HD void substep(SimCtx& c, float hdt) {
     detect(c);
 #endif
     PROF(3);
+    if (lane == 0) {        // contact-list diagnostics (ha_state_t.contact_stats)
+        int off = s.noff;
+        s.cst[0] += 1;
+        s.cst[1] += off > c.maxc ? 1 : 0;
+        s.cst[2] = off > s.cst[2] ? off : s.cst[2];
+        s.cst[3] += off;
+    }
     PROF_COUNT(8, s.nc);
     PROF_COUNT(9, 1);
     // ---- contact rows: in chunk ch, lane r < MAXR owns global row MAXR ch + r (normal, friction 1, friction 2

@@ -175,7 +175,8 @@ extern "C" __global__ void __launch_bounds__(256) ha_pointcloud_kernel(PcLaunch 
 struct ObsGather {
     const float* src[HA_MAX_OBS_SOURCES];
     int stride[HA_MAX_OBS_SOURCES];
-    const int32_t* cols;          // [n_cols][2] (source, column)
+    const int32_t* cols;          // [n_cols][2] (source | HA_OBS_SRC_TARGET, column)
+    const int64_t* target;        // target_object_index (for HA_OBS_SRC_TARGET columns)
     float* out;
     int N, n_cols;
 };
@@ -184,7 +185,9 @@ extern "C" __global__ void __launch_bounds__(256) ha_obs_gather_kernel(ObsGather
     unsigned t = blockIdx.x * 256u + threadIdx.x;
     if (t >= (unsigned)g.N * (unsigned)g.n_cols) return;
     const int env = (int)(t / (unsigned)g.n_cols), k = (int)(t % (unsigned)g.n_cols);
-    const int s = g.cols[2 * k], c = g.cols[2 * k + 1];
+    const int sc = g.cols[2 * k], s = sc & (HA_OBS_SRC_TARGET - 1);
+    long long c = g.cols[2 * k + 1];
+    if ((sc & HA_OBS_SRC_TARGET) && g.target) c += g.target[env] * 13;
     const float* src = g.src[0];
     int stride = g.stride[0];
 #pragma unroll

@@ -93,6 +93,7 @@ __device__ void load_env(SimCtx& c, const ha_state_t& st, int env, bool take_for
         c.o[o].coll = st.collision_enabled ? st.collision_enabled[(size_t)env * NO + o] : 1;
     }
     for (int b = lane; b < MAXB; b += 64) s.u.pd.cforce[b][0] = s.u.pd.cforce[b][1] = s.u.pd.cforce[b][2] = 0.0f;
+    if (lane < 4) s.cst[lane] = 0;
     wsync();
 }
 
@@ -173,6 +174,10 @@ __device__ void store_env(SimCtx& c, const ha_state_t& st, int env) {
         bs[e] = v;
     }
     for (int e = lane; e < B * 3; e += 64) st.net_contact_force[(size_t)env * B * 3 + e] = s.u.pd.cforce[e / 3][e % 3];
+    if (st.contact_stats && lane < 4) {
+        int32_t* cs = st.contact_stats + (size_t)env * 4 + lane;
+        *cs = lane == 2 ? (s.cst[2] > *cs ? s.cst[2] : *cs) : *cs + s.cst[lane];
+    }
     wsync();
 }
 
@@ -929,6 +934,7 @@ int ha_gather_obs(ha_handle h, const float* const* sources, const int32_t* strid
         if (!g.src[q]) return HA_E_ARG;
     }
     g.cols = cols;
+    g.target = h->st.target_object_index;
     g.out = out;
     g.N = h->N;
     g.n_cols = n_cols;

@@ -132,7 +132,8 @@ STATE_FIELDS = ["root_state", "rigid_body_state", "dof_state", "net_contact_forc
                 "object_configuration_indices", "object_indices", "object_pos_initial", "object_quat_initial",
                 "ur5_target", "servo", "smoothed", "obs_cache", "reset_draws", "episode", "stats", "term_sums",
                 "flags", "collision_enabled", "dof_force", "reset_goal_buf", "successes", "goal_state",
-                "consecutive_successes", "dr_scale", "object_scale", "object_force", "task_state", "task_scalars"]
+                "consecutive_successes", "dr_scale", "object_scale", "object_force", "task_state", "task_scalars",
+                "contact_stats"]
 
 
 def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, num_actions=11, num_obs=147,
@@ -156,7 +157,7 @@ def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, nu
         "dof_force": ((N, D), f), "reset_goal_buf": ((N,), i64), "successes": ((N,), f), "goal_state": ((N, 7), f),
         "consecutive_successes": ((1,), f), "dr_scale": ((N, DR_SIZE), f),
         "object_scale": ((N, n_obj, 3), f), "object_force": ((N, n_obj, 3), f), "task_state": ((N, AK_TS), f),
-        "task_scalars": ((4,), f),
+        "task_scalars": ((4,), f), "contact_stats": ((N, 4), i32),
     }
 
 

@@ -72,23 +72,59 @@ def sees_previous_object_pose(order, name):
     return i < order.index("object_pos") or i < order.index("object_quat")
 
 
-def obs_columns(observations, n_objects):
-    """(source, column) per obs-vector column for a custom observation list: source 0 = the step kernel's obs
-    row (DEFAULT_OBSERVATIONS layout), 1 = goal_pos. Point clouds are not in the vector (their observation
-    key is their name, observables.py:199-210; observable_vec_task.py:188-191). Raises for a low-dimensional
-    observable this build does not produce."""
+# ha_gather_obs sources of a custom observation list (include/handarm_abi.h): the step kernel's obs row, goal_pos,
+# the refreshed gym tensors and the per-env object properties
+SRC_OBS, SRC_GOAL, SRC_ROOT, SRC_BODY, SRC_DOF, SRC_PROPS = range(6)
+SRC_TARGET = 16                 # HA_OBS_SRC_TARGET: + target_object_index * 13 (the target object's root row)
+TIP_LINKS = [28, 15, 21, 24, 18]  # thumb, index, middle, ring, little fingertip links (ur5sih.py:609-614)
+PROPS = 13                      # object_props row per object: mass, com (3), inertia (9)
+
+
+def default_layout(n_objects):
+    """Env layout of the Ur5SihMultiObject gym tensors without a bin (multi_object.py:562-663)."""
+    return dict(a0=3, body_robot0=1, n_dofs=17)
+
+
+def obs_columns(observations, n_objects, layout=None):
+    """(source, column) per obs-vector column for a custom observation list (sources above). Point clouds are
+    not in the vector (their observation key is their name, observables.py:199-210; observable_vec_task.py:
+    188-191). Low-dimensional observables registered by the reference (multi_object.py:121-417, ur5sih.py:233-345)
+    are copies of the refreshed state, so each is a set of fixed columns of a source:
+      ur5_joint_state: dof positions 0..5 then velocities (ur5sih.py:606-607);
+      sih_fingertip_angvel: rigid_body_state angvel of the 5 fingertips (ur5sih.py:309);
+      object_quat / object_linvel / object_angvel: the objects' root-state rows (multi_object.py:137-172);
+      object_mass / object_com / object_inertia: the pool properties of each env's objects (:907-925);
+      target_object_pos / target_object_quat / target_object_pos_initial: the target object's root row (the
+      last one re-gathers the current position every post_step, :229-240)."""
+    lay = layout or default_layout(n_objects)
+    a0, r0 = lay["a0"], lay["body_robot0"]
     sizes = default_sizes(n_objects)
     start = {n: sum(sizes[:i]) for i, n in enumerate(DEFAULT_OBSERVATIONS)}
     size = dict(zip(DEFAULT_OBSERVATIONS, sizes))
+    root = lambda o, k: (SRC_ROOT, (a0 + o) * 13 + k)                      # noqa: E731
+    extra = {
+        "goal_pos": [(SRC_GOAL, k) for k in range(3)],
+        "ur5_joint_state": [(SRC_DOF, 2 * d) for d in range(6)] + [(SRC_DOF, 2 * d + 1) for d in range(6)],
+        "sih_fingertip_angvel": [(SRC_BODY, (r0 + t) * 13 + 10 + k) for t in TIP_LINKS for k in range(3)],
+        "object_quat": [root(o, 3 + k) for o in range(n_objects) for k in range(4)],
+        "object_linvel": [root(o, 7 + k) for o in range(n_objects) for k in range(3)],
+        "object_angvel": [root(o, 10 + k) for o in range(n_objects) for k in range(3)],
+        "object_mass": [(SRC_PROPS, o * PROPS) for o in range(n_objects)],
+        "object_com": [(SRC_PROPS, o * PROPS + 1 + k) for o in range(n_objects) for k in range(3)],
+        "object_inertia": [(SRC_PROPS, o * PROPS + 4 + k) for o in range(n_objects) for k in range(9)],
+        "target_object_pos": [(SRC_ROOT | SRC_TARGET, a0 * 13 + k) for k in range(3)],
+        "target_object_quat": [(SRC_ROOT | SRC_TARGET, a0 * 13 + 3 + k) for k in range(4)],
+        "target_object_pos_initial": [(SRC_ROOT | SRC_TARGET, a0 * 13 + k) for k in range(3)],
+    }
     cols = []
     for n in observations:
         if n in POINTCLOUDS or n.endswith(("_depth", "_segmentation", "_pointcloud", "_color")):
             continue
         if n in start:
-            cols += [(0, start[n] + k) for k in range(size[n])]
-        elif n == "goal_pos":
-            cols += [(1, k) for k in range(3)]
+            cols += [(SRC_OBS, start[n] + k) for k in range(size[n])]
+        elif n in extra:
+            cols += extra[n]
         else:
-            raise NotImplementedError(f"observable {n!r}: this build produces {DEFAULT_OBSERVATIONS}, goal_pos and "
-                                      f"the synthetic point clouds {POINTCLOUDS}")
+            raise NotImplementedError(f"observable {n!r}: this build produces {DEFAULT_OBSERVATIONS}, "
+                                      f"{sorted(extra)} and the synthetic point clouds {POINTCLOUDS}")
     return cols

@@ -45,6 +45,8 @@ class HandArmSim:
         self.num_actors = self.model.n_actors
         self.num_bodies = self.model.n_bodies
         self.stats_ring = stats_ring
+        # contacts per substep the kernel family holds (ha_physics.h MAXC x chunks: 42 for the clutter family)
+        self.contact_capacity = 42 if (self.task == HM.TASK_UR5SIH and self.params.n_objects > 3) else 21
         spec = HM.state_spec(num_envs, n_links=self.num_links, n_dofs=self.num_dofs, n_obj=self.n_obj,
                              num_initial_poses=self.params.num_initial_poses, num_actions=self.params.num_actions,
                              num_obs=self.params.num_obs, n_actors=self.num_actors, n_bodies=self.num_bodies)
@@ -177,6 +179,21 @@ class HandArmSim:
 
     def task_reset(self, flags=0):
         _lib.check(self.lib.ha_task_reset(self.h, flags, self._stream()), "ha_task_reset")
+
+    def contact_stats(self, reset=False):
+        """Contact-list diagnostics since the last reset (ha_state_t.contact_stats, added up by every launch):
+        substeps, fraction of substeps whose narrow phases offered more contacts than the list holds (the
+        shallowest are then dropped), mean and max contacts offered per substep, and percentiles of the per-env
+        maximum. One device read."""
+        cs = self.t["contact_stats"].cpu().numpy().astype("int64")
+        if reset:
+            self.t["contact_stats"].zero_()
+        sub = int(cs[:, 0].sum())
+        import numpy as np
+        return {"capacity": self.contact_capacity, "substeps": sub,
+                "at_capacity_frac": float(cs[:, 1].sum() / max(sub, 1)),
+                "offered_mean": float(cs[:, 3].sum() / max(sub, 1)), "offered_max": int(cs[:, 2].max()),
+                "env_max_p50": float(np.percentile(cs[:, 2], 50)), "env_max_p99": float(np.percentile(cs[:, 2], 99))}
 
     def last_kernel_ms(self):
         return float(self.lib.ha_last_kernel_ms(self.h))

@@ -182,6 +182,7 @@ class Ur5SihMultiObjectManipulation:
         idx = [random.sample(pool, self.num_objects) for _ in range(N)]
         t["object_indices"].copy_(torch.tensor(idx, dtype=torch.int64))
         self.object_indices = t["object_indices"]
+        self._bind_gather_sources()
         # initial actor poses (create_actor start poses)
         rs = self.root_state.view(N, A, 13)
         rs[:, m.actor_robot, 0:3] = torch.tensor(m.base_pos[:], device=self.device)
@@ -253,25 +254,44 @@ class Ur5SihMultiObjectManipulation:
                 self.pointclouds.use_previous_object_pose()
         if not self.custom_obs:
             return
-        cols = OB.obs_columns(self.obs_names, self.num_objects)
+        m = self.sim.model
+        layout = dict(a0=m.actor_object0, body_robot0=m.body_robot0, n_dofs=m.n_dofs)
+        cols = OB.obs_columns(self.obs_names, self.num_objects, layout)
+        self._obs_layout = layout
         self._obs_cols = torch.tensor(cols, dtype=torch.int32, device=self.device)
         self.student_obs_buf = torch.zeros((N, len(cols)), dtype=torch.float32, device=self.device)
-        self._gather_src = (C.c_void_p * 2)(self.obs_buf.data_ptr(), self.goal_pos.data_ptr())
-        self._gather_stride = (C.c_int32 * 2)(self.obs_buf.shape[1], 3)
         self.num_observations = len(cols)
         self.obs_space = Box(np.full(self.num_observations, -np.inf), np.full(self.num_observations, np.inf))
         start, self.observations_start_end = 0, {}
         for n in self.obs_names:                  # _compute_num_observations: only key-"obs" observables
-            k = len(OB.obs_columns([n], self.num_objects))
+            k = len(OB.obs_columns([n], self.num_objects, layout))
             if k:
                 self.observations_start_end[n] = (start, start + k)
                 start += k
+
+    def _bind_gather_sources(self):
+        """ha_gather_obs sources of a custom observation list (observables.SRC_*), once the objects are chosen.
+        object_mass / object_com / object_inertia (multi_object.py:907-925) are the pool properties of each env's
+        objects, fixed at creation (the reference reads them once, at post_init)."""
+        if not self.custom_obs:
+            return
+        m, N = self.sim.model, self.num_envs
+        pm = torch.tensor(np.ctypeslib.as_array(m.pool_mass)[:m.n_pool], dtype=torch.float32)
+        pc = torch.tensor(np.ctypeslib.as_array(m.pool_com)[:m.n_pool], dtype=torch.float32)
+        pi = torch.tensor(np.ctypeslib.as_array(m.pool_inertia)[:m.n_pool], dtype=torch.float32)
+        props = torch.cat([pm[:, None], pc, pi], 1)                      # (pool, 13)
+        self.object_props = props.to(self.device)[self.sim.t["object_indices"]].reshape(N, -1).contiguous()
+        t = self.sim.t
+        srcs = [self.obs_buf, self.goal_pos, t["root_state"], t["rigid_body_state"], t["dof_state"], self.object_props]
+        self._gather_src = (C.c_void_p * len(srcs))(*[x.data_ptr() for x in srcs])
+        self._gather_stride = (C.c_int32 * len(srcs))(self.obs_buf.shape[1], 3, self.num_actors * 13,
+                                                       self.num_bodies * 13, self.num_dofs * 2, self.num_objects * 13)
 
     def _observations(self):
         """compute_observations (observable_vec_task.py:183-203) from the device buffers."""
         obs = self.obs_buf
         if self.custom_obs:
-            _lib.check(self.sim.lib.ha_gather_obs(self.sim.h, self._gather_src, self._gather_stride, 2,
+            _lib.check(self.sim.lib.ha_gather_obs(self.sim.h, self._gather_src, self._gather_stride, 6,
                                                   self._obs_cols.data_ptr(), len(self._obs_cols),
                                                   self.student_obs_buf.data_ptr(), self.sim._stream()),
                        "ha_gather_obs")
@@ -429,6 +449,10 @@ class Ur5SihMultiObjectManipulation:
             quat_init[:, p] = rs[:, :, 3:7]
             self._sync_obs_cache()
         self.objects_dropped = True
+
+    def contact_stats(self, reset=False):
+        """Contact-list diagnostics of the physics since the last reset (HandArmSim.contact_stats)."""
+        return self.sim.contact_stats(reset)
 
     def _reference_draws(self, all_envs=False):
         """reference_rng: if this step resets, draw its values on the host in the reference's order and hand them

@@ -422,6 +422,44 @@ def gen_ref_rng(path, N=16, P=4, E=4, seed=77):
     print("wrote", path, {k: v.shape for k, v in arrays.items()})
 
 
+OBS_EXTRA = ["ur5_joint_state", "sih_fingertip_angvel", "object_quat", "object_linvel", "object_angvel",
+             "object_mass", "object_com", "object_inertia", "target_object_pos", "target_object_quat",
+             "target_object_pos_initial", "goal_pos", "ur5_joint_pos"]
+
+
+def gen_obs_custom(path, N=16, steps=3, seed=21):
+    """A custom observation list of the registered low-dimensional observables (multi_object.py:121-417,
+    ur5sih.py:233-345) over random refreshed states: the reference's post_step callbacks and compute_observations
+    (observable_vec_task.py:183-203) give the obs rows."""
+    t, mom = make_task(N, seed=seed, student_obs=OBS_EXTRA)
+    g = torch.Generator().manual_seed(seed + 100)
+    n_obj = t.cfg_env.objects.num_objects
+    t.objects_dropped = True
+    t.object_pos_initial = torch.rand(N, 1, n_obj, 3, generator=g)
+    t.object_quat_initial = rand_quat(g, (N, 1, n_obj))
+    out = {k: [] for k in ["root", "body", "dof", "goal_pos", "target_idx", "obs"]}
+    for s in range(steps):
+        fill_random_state(t, g)
+        t.goal_pos[:] = torch.rand(N, 3, generator=g)
+        t.target_object_index[:] = torch.randint(n_obj, (N,), generator=g)
+        t.target_object_actor_env_index[:] = torch.tensor(t.object_actor_env_indices)[t.target_object_index]
+        t.progress_buf[:] = 5
+        t.reset_buf[:] = 0
+        for k, v in [("root", t.root_state), ("body", t.body_state), ("dof", t.dof_state), ("goal_pos", t.goal_pos),
+                     ("target_idx", t.target_object_index)]:
+            out[k].append(v.clone())
+        t.log_data = {}
+        t.post_physics_step()
+        out["obs"].append(t.obs_buf.clone())
+    arrays = {k: torch.stack(v).numpy() for k, v in out.items()}
+    arrays["object_indices"] = t.object_indices.numpy()
+    arrays["object_names"] = np.array([o.name for o in t.objects])
+    arrays["observations"] = np.array(OBS_EXTRA)
+    arrays["obs_start_end"] = np.array([t.observations_start_end[n] for n in OBS_EXTRA])
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, {k: v.shape for k, v in arrays.items()})
+
+
 def gen_quat(path, M=64, seed=4):
     tu = refload.load("isaacgym.torch_utils")
     mom = refload.load("isaacgymenvs.tasks.hand_arm.task.multi_object_manipulation")
@@ -550,6 +588,9 @@ if __name__ == "__main__":
     if "--pointclouds" in sys.argv:
         gen_pointclouds(os.path.join(HERE, "ur5sih_pointclouds_student.npz"), PC_STUDENT, seed=5)
         gen_pointclouds(os.path.join(HERE, "ur5sih_pointclouds_all.npz"), PC_ALL, seed=6)
+        sys.exit(0)
+    if "--obs" in sys.argv:     # custom list of the registered low-dimensional observables only
+        gen_obs_custom(os.path.join(HERE, "ur5sih_obs_custom.npz"))
         sys.exit(0)
     if "--rng" in sys.argv:     # seed-faithful reset / drop draws only
         gen_ref_rng(os.path.join(HERE, "ur5sih_ref_rng.npz"))

@@ -172,3 +172,30 @@ def test_full_size_cloud_properties():
     ti = cpu(env.target_object_index)
     np.testing.assert_array_equal(tgt[..., 0:3], obj[np.arange(N), ti][..., 0:3])
     np.testing.assert_array_equal(tgt[..., 3], 2 * obj[np.arange(N), ti][..., 3])
+
+
+def test_registered_low_dim_observables_through_vectask():
+    """A custom observation list of the registered low-dimensional observables (ur5_joint_state,
+    sih_fingertip_angvel, object_quat/linvel/angvel, object_mass/com/inertia, target_object_pos/quat/pos_initial,
+    goal_pos, ur5_joint_pos) through the VecTask: ha_gather_obs over the refreshed tensors reproduces the
+    reference's obs rows (tests/golden/ur5sih_obs_custom.npz) bit for bit. ur5_joint_pos comes from the step
+    kernel's obs row, so the state is put in place and one observe launch refreshes that row first."""
+    need_gpu()
+    from handarm_hip.tasks import Ur5SihMultiObjectManipulation
+    d = np.load(os.path.join(G, "ur5sih_obs_custom.npz"))
+    names = [str(n) for n in d["observations"]]
+    T, N = d["target_idx"].shape
+    env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": N, "observations": names},
+                                         "objects": {"dataset": {"ycb": [str(n) for n in d["object_names"]]}}},
+                                        "cuda:0", "cuda:0")
+    assert env.num_obs == d["obs"].shape[-1] and env.observation_keys == ["obs"]
+    put(env.sim, "object_indices", d["object_indices"])
+    env._bind_gather_sources()
+    for s in range(T):
+        put(env.sim, "root_state", d["root"][s])
+        put(env.sim, "rigid_body_state", d["body"][s])
+        put(env.sim, "dof_state", d["dof"][s])
+        put(env.sim, "goal_pos", d["goal_pos"][s])
+        put(env.sim, "target_object_index", d["target_idx"][s])
+        obs = cpu(env.reset()["obs"])            # VecTask.reset: compute_observations of the bound state
+        np.testing.assert_array_equal(obs, d["obs"][s])

@@ -95,3 +95,39 @@ def test_sample_table_area_mode():
     assert np.all(u[:, :100, 3] == 1) and np.all(u[:, 100:] == 0)
     with pytest.raises(NotImplementedError):
         OB.obs_columns(["ur5_joint_vel"], 3)
+
+
+def _gather_np(cols, srcs, target):
+    """numpy restatement of ha_gather_obs (include/handarm_abi.h): column (source | HA_OBS_SRC_TARGET, c)."""
+    N = srcs[0].shape[0]
+    out = np.zeros((N, len(cols)), np.float32)
+    for j, (s, c) in enumerate(cols):
+        src = srcs[s & (OB.SRC_TARGET - 1)]
+        off = c + (target * 13 if s & OB.SRC_TARGET else 0)
+        out[:, j] = src[np.arange(N), off]
+    return out
+
+
+def test_registered_low_dim_observables_columns_against_reference():
+    """The registered low-dimensional observables a custom list can name (ur5_joint_state, sih_fingertip_angvel,
+    object_quat/linvel/angvel, object_mass/com/inertia, target_object_pos/quat/pos_initial, goal_pos): their
+    ha_gather_obs columns over the refreshed tensors reproduce the reference's obs rows bit for bit
+    (tests/golden/ur5sih_obs_custom.npz, generated by the reference's own post_step callbacks)."""
+    from handarm_hip import model as HM
+    d = np.load(os.path.join(G, "ur5sih_obs_custom.npz"))
+    names = [str(n) for n in d["observations"]]
+    T, N = d["target_idx"].shape
+    scene = HM.load_scene()
+    m = HM.build_model(scene, [str(n) for n in d["object_names"]])
+    props = np.concatenate([np.ctypeslib.as_array(m.pool_mass)[:m.n_pool, None],
+                            np.ctypeslib.as_array(m.pool_com)[:m.n_pool],
+                            np.ctypeslib.as_array(m.pool_inertia)[:m.n_pool]], 1).astype(np.float32)
+    props = props[d["object_indices"]].reshape(N, -1)
+    cols = OB.obs_columns(names, 3, dict(a0=m.actor_object0, body_robot0=m.body_robot0, n_dofs=m.n_dofs))
+    assert len(cols) == d["obs"].shape[-1]
+    for s in range(T):
+        obs_row = np.zeros((N, 147), np.float32)          # the step kernel's row: ur5_joint_pos = dof pos 0..5
+        obs_row[:, 0:6] = d["dof"][s].reshape(N, 17, 2)[:, 0:6, 0]
+        srcs = [obs_row, d["goal_pos"][s], d["root"][s].reshape(N, -1), d["body"][s].reshape(N, -1),
+                d["dof"][s].reshape(N, -1), props]
+        np.testing.assert_array_equal(_gather_np(cols, srcs, d["target_idx"][s]), d["obs"][s])
