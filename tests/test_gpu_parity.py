@@ -223,11 +223,17 @@ def test_gpu_runs_are_bitwise_deterministic():
 
 
 # ------------------------------------------------------------------------------ full-size properties
-def test_vectask_episode_at_full_shard_size():
+@pytest.mark.parametrize("dr", [False, True])
+def test_vectask_episode_at_full_shard_size(dr):
+    """A full 8192-env shard over one episode and into the next: dr=True is the C4 shard as benched (DR on, each
+    env's 3 objects a random.sample of the 16-object pool)."""
     need_gpu()
     from handarm_hip.tasks import Ur5SihMultiObjectManipulation
     n = 8192
-    env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}}, "cuda:0", "cuda:0")
+    cfg = {"env": {"numEnvs": n}}
+    if dr:
+        cfg.update({"task": {"randomize": True}, "objects": {"dataset": {"ycb": [o["name"] for o in HM.load_scene()["objects"]]}}})
+    env = Ur5SihMultiObjectManipulation(cfg, "cuda:0", "cuda:0")
     obs = env.reset()["obs"]
     print("full-shard episode: constructed", flush=True)
     assert obs.shape == (n, 147)
@@ -252,8 +258,13 @@ def test_vectask_episode_at_full_shard_size():
             assert (reset == 1).all() and extras["time_outs"].all()
         if step == 201:                 # the reset happened inside this step
             assert (env.progress_buf == 1).all() and (reset == 0).all()
-    # observation segments are the state tensors (observable_vec_task.py:183-203)
-    o = env.obs_buf
+    # observation segments are the state tensors (observable_vec_task.py:183-203); with DR the obs carry the
+    # observation noise and the teacher obs are the clean copy
+    o = env.teacher_obs_buf if dr else env.obs_buf
+    if dr:
+        dn = (env.obs_buf - env.teacher_obs_buf)
+        assert 0.0015 < float(dn.std()) < 0.0025 and abs(float(dn.mean())) < 2e-4     # N(0, 0.002)
+        assert len(set(env.object_indices.flatten().tolist())) == 16
     torch.testing.assert_close(o[:, 0:6], env.dof_pos[:, 0:6], rtol=0, atol=0)
     torch.testing.assert_close(o[:, 80:89], env.root_pos[:, 3:6].reshape(n, 9), rtol=0, atol=0)
     torch.testing.assert_close(o[:, 63:80], env.dof_position_targets, rtol=0, atol=0)
@@ -295,3 +306,26 @@ def test_gym_api_binding_matches_direct_abi():
     gym.refresh_actor_root_state_tensor(sim_b)
     torch.cuda.synchronize()
     assert torch.equal(root, sim_a.t["root_state"]) and torch.equal(dof, sim_a.t["dof_state"])
+
+
+@pytest.mark.parametrize("task", ["ur5sih", "allegro_kuka", "allegro_hand"])
+def test_single_env_config_c1(task):
+    """BASELINE config 1 is num_envs = 1: one-workgroup launches, the stats ring at N = 1, drop init with one env,
+    episode boundaries and log folding."""
+    need_gpu()
+    from handarm_hip.tasks import AllegroHand, AllegroKuka, Ur5SihMultiObjectManipulation
+    cls = {"ur5sih": Ur5SihMultiObjectManipulation, "allegro_kuka": AllegroKuka, "allegro_hand": AllegroHand}[task]
+    env = cls({"env": {"numEnvs": 1}}, "cuda:0", "cuda:0")
+    env.reset()
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    L = env.max_episode_length
+    for step in range(1, L + 3):
+        obs_dict, rew, reset, extras = env.step(torch.rand((1, env.num_acts), device="cuda:0", generator=g) * 2 - 1)
+        assert obs_dict["obs"].shape == (1, env.num_obs)
+    torch.cuda.synchronize()
+    assert torch.isfinite(env.obs_buf).all() and torch.isfinite(env.rew_buf).all()
+    assert int(env.progress_buf[0]) >= 1
+    if task == "ur5sih":
+        assert int(env.progress_buf[0]) == 2            # the timeout reset happened at step L + 1
+        log = env.log_data                              # the ring was folded (L + 2 > ring size)
+        assert env.total_num_resets >= 1 and "reward_terms/reaching" in log
