@@ -54,7 +54,7 @@ extern "C" {
 #define HA_MAX_OBJ 8           /* objects per env: 3 in Ur5SihMultiObject.yaml:2, 8 for bin-picking (config 5) */
 #define HA_MAX_STATIC 10       /* static boxes per env (table, or table-with-hole walls + bin pieces) */
 #define HA_MAX_FIXED_BODIES 8  /* fixed rigid bodies with a model pose (table-with-hole links, bin) */
-#define HA_MAX_CONTACTS 42     /* contacts per env and substep: 21 (<= 3 objects), 42 (clutter, > 3 objects) */
+#define HA_MAX_CONTACTS 84     /* contacts per env and substep: 21 (<= 3 objects), 84 (clutter, > 3 objects) */
 #define HA_MAX_INIT_POSES 4    /* objects.drop.num_initial_poses */
 #define HA_MAX_SPLINE_PIECES 8
 #define HA_N_SPLINES 8

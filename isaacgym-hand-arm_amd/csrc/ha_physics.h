@@ -92,7 +92,9 @@ struct EnvLDS {
         PostScratch pd;
         ColScratch col;
         RowScratch rows;
-        float xfer[128];    // lane exchange outside the physics phases (controller; PGS impulses -> forces)
+        float xfer[MAXR * HA_MAX_CONTACTS / MAXC];  // lane exchange outside the physics phases (controller;
+                                                    // PGS impulses of every row -> contact forces). Must stay
+                                                    // below the rows' RK area (static_assert in PhysCfg users)
     } u;
 };
 
@@ -140,7 +142,7 @@ __host__ __device__ inline size_t obj_lds_offset_rows(size_t rows) {
 #ifndef HA_SPLIT_ABOVE_OCAP
 #define HA_SPLIT_ABOVE_OCAP 2   /* families with more object slots use split rows (Ur5Sih 3 objects, clutter) */
 #endif
-template <int ND, int OCAP, int NCH, int KL = 8>
+template <int ND, int OCAP, int NCH, int KL = 8, int LCH = NCH>
 struct PhysCfg {
     static constexpr int nd = ND, ocap = OCAP, nch = NCH;
     static constexpr int vw = ND + 6 * OCAP > 64 ? 2 : 1;
@@ -150,15 +152,30 @@ struct PhysCfg {
     static constexpr bool split = OCAP > HA_SPLIT_ABOVE_OCAP;
 #endif
     static constexpr int kl = KL;
-    static constexpr int spill_floats = split ? 2 * 3 * (MAXC * NCH - KL) * ND : 0;   // per env: J then Y
+    // split rows: the object blocks of chunks [0, lch) live in LDS, those of chunks [lch, nch) in the env's global
+    // row area after the robot-block spill rows (written by the rows phase, read back by the PGS one contact ahead)
+    static constexpr int lch = split ? LCH : NCH;
+    static constexpr int spill_robot = split ? 2 * 3 * (MAXC * NCH - KL) * ND : 0;   // per env: J then Y
+    static constexpr int spill_obj = split ? 2 * MAXR * (NCH - lch) * 12 : 0;        // per env: J then Y
+    static constexpr int spill_floats = spill_robot + spill_obj;
     static_assert(ND + 6 * OCAP <= MAXV, "generalized velocity exceeds MAXV");
     static_assert(!split || (KL >= 0 && KL <= MAXC * NCH), "LDS link slots must not exceed the contact capacity");
-    static_assert(!split || (row_slots<ND>() == 2 && MAXC * NCH <= 64), "split rows: two object slots, <= 64 contacts");
+    static_assert(!split || (row_slots<ND>() == 2 && MAXC * NCH <= 128), "split rows: two object slots, <= 128 contacts");
+    static_assert(split || MAXC * NCH <= 64, "dense rows: <= 64 contacts (one ballot)");
+    static_assert(lch >= 1 && lch <= NCH, "LDS row chunks");
+    static_assert(MAXC * NCH <= HA_MAX_CONTACTS, "contact capacity exceeds HA_MAX_CONTACTS");
 };
+// bytes of the constraint rows proper, then (several contact chunks only) the per-row PGS constants of every
+// chunk (impulse, target velocity, 1/diag, friction, two Delassus entries: 6 floats x MAXR x chunks), which the
+// PGS swaps into registers one chunk at a time
+template <class PC>
+__host__ __device__ constexpr size_t pc_rowdata_bytes() {
+    return PC::split ? 2 * sizeof(float) * ((size_t)MAXR * PC::lch * 12 + 3 * (size_t)PC::kl * PC::nd)
+                     : 2 * sizeof(float) * (size_t)MAXR * PC::nch * row_stride<PC::nd>();
+}
 template <class PC>
 __host__ __device__ constexpr size_t pc_rows_bytes() {
-    return PC::split ? 2 * sizeof(float) * ((size_t)MAXR * PC::nch * 12 + 3 * (size_t)PC::kl * PC::nd)
-                     : 2 * sizeof(float) * (size_t)MAXR * PC::nch * row_stride<PC::nd>();
+    return pc_rowdata_bytes<PC>() + (PC::nch > 1 ? 6 * sizeof(float) * (size_t)MAXR * PC::nch : 0);
 }
 template <class PC>
 __host__ __device__ inline size_t obj_lds_offset() { return obj_lds_offset_rows(pc_rows_bytes<PC>()); }
@@ -576,6 +593,10 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
         if (nc >= c.maxc) {
             float sv = lane < c.maxc ? c.k[lane].sep : -3.0e38f;
             int w = lane;
+            if (c.maxc > 64) {          // contacts 64.. in the same lanes; a tie keeps the lower index
+                float s2 = lane + 64 < c.maxc ? c.k[lane + 64].sep : -3.0e38f;
+                if (s2 > sv) { sv = s2; w = lane + 64; }
+            }
             wave_argmax(sv, w);
             if (sv <= S[t]) continue;
             slot = w;
@@ -1070,29 +1091,47 @@ HD void substep(SimCtx& c, float hdt) {
     int nr = 3 * nc;    // nc <= MAXC x NCH -> <= MAXR x NCH rows
     // split rows (PhysCfg): object blocks of every row (OW = 12 wide, J then Y), then the robot blocks of the
     // first KL link contacts (J then Y), then the env's global spill area for the link contacts after those
-    constexpr int OW = 12, KL = PC::kl, SPJ = 3 * (MAXC * NCH - KL) * ND;
+    constexpr int OW = 12, KL = PC::kl, LCH = PC::lch, SPJ = 3 * (MAXC * NCH - KL) * ND;
     float* Ob = Jb;
-    float* ObY = Ob + MAXR * NCH * OW;
-    float* Rb = ObY + MAXR * NCH * OW;
+    float* ObY = Ob + MAXR * LCH * OW;
+    float* Rb = ObY + MAXR * LCH * OW;
     float* RbY = Rb + 3 * KL * ND;
-    uint64_t lmask = 0;     // contacts that touch a robot link (split rows only)
-    if constexpr (PC::split) lmask = __ballot(lane < nc && (c.k[lane].a >= 100 || c.k[lane].b >= 100));
+    // contacts that touch a robot link (split rows only): contacts 0..63 in lmask0, 64.. in lmask1
+    uint64_t lmask0 = 0, lmask1 = 0;
+    if constexpr (PC::split) {
+        lmask0 = __ballot(lane < nc && (c.k[lane].a >= 100 || c.k[lane].b >= 100));
+        if constexpr (MAXC * NCH > 64)
+            lmask1 = __ballot(lane + 64 < nc && (c.k[lane + 64].a >= 100 || c.k[lane + 64].b >= 100));
+    }
     // robot-block slot of contact ci (-1: no link), and row k of its J or Y robot block
     auto lslot = [&](int ci) -> int {
-        return ((lmask >> ci) & 1ull) ? (int)__popcll(lmask & ((1ull << ci) - 1ull)) : -1;
+        if (MAXC * NCH <= 64 || ci < 64)
+            return ((lmask0 >> ci) & 1ull) ? (int)__popcll(lmask0 & ((1ull << ci) - 1ull)) : -1;
+        int cj = ci - 64;
+        return ((lmask1 >> cj) & 1ull) ? (int)(__popcll(lmask0) + __popcll(lmask1 & ((1ull << cj) - 1ull))) : -1;
     };
     auto rrow = [&](int ls, int k, bool y) -> float* {
         if (ls < KL) return (y ? RbY : Rb) + (3 * ls + k) * ND;
         return c.spill + (y ? SPJ : 0) + (3 * (ls - KL) + k) * ND;
     };
-    float vt[NCH], winv[NCH], lam[NCH], cmu[NCH];
-#pragma unroll
+    // object blocks (J or Y) of row r: LDS for the first LCH chunks, else the env's global row area
+    auto orow = [&](int r, bool y) -> float* {
+        if (r < MAXR * LCH) return (y ? ObY : Ob) + r * OW;
+        return c.spill + PC::spill_robot + (y ? MAXR * (NCH - LCH) * OW : 0) + (r - MAXR * LCH) * OW;
+    };
+    // PGS row constants of the lane's row in the current chunk: impulse, target velocity, 1/diagonal, friction and
+    // the block's Delassus entries. One chunk: kept in registers. Several: stored per row in RK (after the rows)
+    // and swapped into registers chunk by chunk, so registers do not grow with the contact capacity.
+    float klam = 0.f, kvt = 0.f, kwinv = 0.f, kcmu = 0.f, kca0 = 0.f, kca1 = 0.f;
+    float* RK = reinterpret_cast<float*>(reinterpret_cast<char*>(s.u.rows.J) + pc_rowdata_bytes<PC>());
+    auto rk = [&](int q, int row) -> float& { return RK[q * MAXR * NCH + row]; };
+#pragma unroll 1
     for (int ch = 0; ch < NCH; ch++) {
-        vt[ch] = 0.f; winv[ch] = 0.f; lam[ch] = 0.f; cmu[ch] = 0.f;
+        float vt_ = 0.f, winv_ = 0.f, cmu_ = 0.f;
         int r = MAXR * ch + lane;
         if (lane < MAXR && r < nr) {
             const ContactLDS& ct = c.k[r / 3];
-            cmu[ch] = ct.mu;
+            cmu_ = ct.mu;
             int k = r % 3;
             // robot block Jr / Yr (null: the contact touches no link, the block is zero) and object blocks Jo / Yo
             float *Jr, *Yr, *Jo, *Yo;
@@ -1100,8 +1139,8 @@ HD void substep(SimCtx& c, float hdt) {
                 int ls = lslot(r / 3);
                 Jr = ls >= 0 ? rrow(ls, k, false) : nullptr;
                 Yr = ls >= 0 ? rrow(ls, k, true) : nullptr;
-                Jo = Ob + r * OW;
-                Yo = ObY + r * OW;
+                Jo = orow(r, false);
+                Yo = orow(r, true);
                 for (int t = 0; t < OW; t++) Jo[t] = 0.0f;
                 if (Jr)
                     for (int t = 0; t < ND; t++) Jr[t] = 0.0f;
@@ -1124,7 +1163,7 @@ HD void substep(SimCtx& c, float hdt) {
                 float sp = ct.sep;
                 float v0 = sp > 0 ? -sp / hdt : -p.baumgarte * sp / hdt;
                 if (v0 > p.max_depen_vel) v0 = p.max_depen_vel;
-                vt[ch] = v0;
+                vt_ = v0;
             }
             // Y_r = M^-1 J_r^T (robot block through the explicit inverse, object blocks 1/m, I_w^-1)
             if (Jr) {
@@ -1152,16 +1191,20 @@ HD void substep(SimCtx& c, float hdt) {
             if (Jr)
                 for (int t = 0; t < D; t++) a += Jr[t] * Yr[t];
             for (int t = 0; t < RSN - D; t++) a += Jo[t] * Yo[t];
-            winv[ch] = 1.0f / (a + 1e-9f);
+            winv_ = 1.0f / (a + 1e-9f);
+        }
+        if (NCH == 1) {
+            kvt = vt_; kwinv = winv_; kcmu = cmu_;
+        } else if (lane < MAXR) {
+            rk(0, r) = 0.0f; rk(1, r) = vt_; rk(2, r) = winv_; rk(3, r) = cmu_;
         }
     }
     wsync();
     // coupling inside each contact's 3-row block (Delassus entries J_ri . M^-1 J_rj^T, i > j): lane of
     // friction row 1 holds a10, lane of friction row 2 holds a20 and a21
-    float ca0[NCH], ca1[NCH];
-#pragma unroll
+#pragma unroll 1
     for (int ch = 0; ch < NCH; ch++) {
-        ca0[ch] = 0.f; ca1[ch] = 0.f;
+        float ca0_ = 0.f, ca1_ = 0.f;
         int r = MAXR * ch + lane;
         if (lane < MAXR && r < nr && r % 3 != 0) {
             int k = r % 3, r0 = r - k;
@@ -1171,8 +1214,8 @@ HD void substep(SimCtx& c, float hdt) {
                 Jr = ls >= 0 ? rrow(ls, k, false) : nullptr;
                 Y0r = ls >= 0 ? rrow(ls, 0, true) : nullptr;
                 Y1r = ls >= 0 ? rrow(ls, 1, true) : nullptr;
-                Jo = Ob + r * OW;
-                Y0o = ObY + r0 * OW;
+                Jo = orow(r, false);
+                Y0o = orow(r0, true);
             } else {
                 Jr = Jb + r * RSN;
                 Y0r = Yb + r0 * RSN;
@@ -1185,14 +1228,19 @@ HD void substep(SimCtx& c, float hdt) {
             if (Jr)
                 for (int t = 0; t < D; t++) a += Jr[t] * Y0r[t];
             for (int t = 0; t < RSN - D; t++) a += Jo[t] * Y0o[t];
-            ca0[ch] = a;
+            ca0_ = a;
             if (k == 2) {
                 float b = 0.0f;
                 if (Jr)
                     for (int t = 0; t < D; t++) b += Jr[t] * Y1r[t];
                 for (int t = 0; t < RSN - D; t++) b += Jo[t] * Y1o[t];
-                ca1[ch] = b;
+                ca1_ = b;
             }
+        }
+        if (NCH == 1) {
+            kca0 = ca0_; kca1 = ca1_;
+        } else if (lane < MAXR) {
+            rk(4, r) = ca0_; rk(5, r) = ca1_;
         }
     }
     PROF(4);
@@ -1283,8 +1331,8 @@ HD void substep(SimCtx& c, float hdt) {
             if constexpr (PC::split) {
                 // object coordinates from the LDS object blocks; robot coordinates from the contact's link slot
                 // (LDS for the first KL, else the global spill rows), absent -> 0
-                const float* On = Ob + 3 * ci * OW;
-                const float* OYn = ObY + 3 * ci * OW;
+                const float* On = orow(3 * ci, false);
+                const float* OYn = orow(3 * ci, true);
                 if (ix >= D) {
                     int t = ix - D;
                     j0n = On[t]; j1n = On[OW + t]; j2n = On[2 * OW + t];
@@ -1319,9 +1367,17 @@ HD void substep(SimCtx& c, float hdt) {
             }
         };
         if (nc > 0) fetch(0);
-#pragma unroll
+#pragma unroll 1
         for (int ch = 0; ch < NCH; ch++) {
             int cend = nc < MAXC * (ch + 1) ? nc : MAXC * (ch + 1);
+            if (NCH > 1) {
+                if (MAXC * ch >= nc) break;
+                if (lane < MAXR) {          // swap this chunk's row constants in
+                    int row = MAXR * ch + lane;
+                    klam = rk(0, row); kvt = rk(1, row); kwinv = rk(2, row);
+                    kcmu = rk(3, row); kca0 = rk(4, row); kca1 = rk(5, row);
+                }
+            }
             for (int ci = MAXC * ch; ci < cend; ci++) {
                 int r0 = 3 * (ci - MAXC * ch);      // row of this contact within the chunk (= its lane)
                 float j0 = j0n, j1 = j1n, j2 = j2n, y0 = y0n, y1 = y1n, y2 = y2n;
@@ -1336,30 +1392,36 @@ HD void substep(SimCtx& c, float hdt) {
                 wave_sum_rows3(jv0, jv1, jv2);
                 // the block's three rows live in lanes r0, r0 + 1, r0 + 2: each lane evaluates its own row with
                 // its own lambda and constants (the oracle's operands) and only n0, d0, d1, d2 cross lanes
-                float lm = lam[ch];
-                float n0 = lm - (jv0 - vt[ch]) * winv[ch];
+                float lm = klam;
+                float n0 = lm - (jv0 - kvt) * kwinv;
                 n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
                 float d0 = bcast(n0 - lm, r0);
                 n0 = bcast(n0, r0);
-                float hi = cmu[ch] * n0;
-                float n1 = lm - ((jv1 + ca0[ch] * d0) - vt[ch]) * winv[ch];
+                float hi = kcmu * n0;
+                float n1 = lm - ((jv1 + kca0 * d0) - kvt) * kwinv;
                 n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
                 float d1 = bcast(n1 - lm, r0 + 1);
-                float n2 = lm - (((jv2 + ca0[ch] * d0) + ca1[ch] * d1) - vt[ch]) * winv[ch];
+                float n2 = lm - (((jv2 + kca0 * d0) + kca1 * d1) - kvt) * kwinv;
                 n2 = n2 < -hi ? -hi : (n2 > hi ? hi : n2);
                 float d2 = bcast(n2 - lm, r0 + 2);
-                if (lane == r0) lam[ch] = n0;
-                if (lane == r0 + 1) lam[ch] = n1;
-                if (lane == r0 + 2) lam[ch] = n2;
+                if (lane == r0) klam = n0;
+                if (lane == r0 + 1) klam = n1;
+                if (lane == r0 + 2) klam = n2;
                 if (d0 != 0.0f) { vreg += y0 * d0; if (VW == 2) vregh += g0 * d0; }
                 if (d1 != 0.0f) { vreg += y1 * d1; if (VW == 2) vregh += g1 * d1; }
                 if (d2 != 0.0f) { vreg += y2 * d2; if (VW == 2) vregh += g2 * d2; }
             }
+            if (NCH > 1 && lane < MAXR) rk(0, MAXR * ch + lane) = klam;     // swap the impulses out
         }
     }
+    // impulse of global row MAXR ch + lane (xfer sits before RK in the union: no overlap)
+    if (NCH == 1) {
+        if (lane < MAXR) s.u.xfer[lane] = klam;
+    } else {
 #pragma unroll
-    for (int ch = 0; ch < NCH; ch++)
-        if (lane < MAXR) s.u.xfer[MAXR * ch + lane] = lam[ch];    // impulse of global row MAXR ch + lane
+        for (int ch = 0; ch < NCH; ch++)
+            if (lane < MAXR) s.u.xfer[MAXR * ch + lane] = rk(0, MAXR * ch + lane);
+    }
     if (lane < D) s.u.pd.dforce[lane] = ((dlam + lam_lo) - lam_up) / hdt;
     wsync();
     if (lane < NV) s.v[lane] = vreg;

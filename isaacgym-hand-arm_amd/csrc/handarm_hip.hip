@@ -32,9 +32,16 @@ template <int FAM>
 __host__ __device__ constexpr int task_obj_capacity() {
     return FAM == FAM_UR5SIH_CLUTTER ? HA_MAX_OBJ : (FAM == HA_TASK_UR5SIH ? 3 : 1);
 }
-// contact chunks (MAXC contacts each)
+// contact chunks (MAXC contacts each). The clutter family holds 84 contacts per substep: a settled 8-object bin
+// offers 59 on average and at most ~90 (bench contact_stats), 42 were at capacity in 99% of substeps.
+#ifndef HB_CHUNKS
+#define HB_CHUNKS 4
+#endif
+#ifndef HB_LDS_CHUNKS       /* clutter chunks whose object-block rows stay in LDS; the rest go to the global area */
+#define HB_LDS_CHUNKS 1
+#endif
 template <int FAM>
-__host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5SIH_CLUTTER ? 2 : 1; }
+__host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5SIH_CLUTTER ? HB_CHUNKS : 1; }
 // clutter family: link contacts whose robot blocks stay in LDS (the rest use the global spill rows). 2 slots
 // keep the env block at <= 20 KB, i.e. 8 workgroups per CU (8 slots: 22.8 KB, 7 per CU)
 #ifndef HB_LINK_SLOTS
@@ -51,7 +58,8 @@ __host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5S
 #endif
 template <int FAM>
 using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>(),
-                        FAM == FAM_UR5SIH_CLUTTER ? HB_LINK_SLOTS : HA_LINK_SLOTS>;
+                        FAM == FAM_UR5SIH_CLUTTER ? HB_LINK_SLOTS : HA_LINK_SLOTS,
+                        FAM == FAM_UR5SIH_CLUTTER ? HB_LDS_CHUNKS : task_contact_chunks<FAM>()>;
 
 
 // ----------------------------------------------------------------------------- state load/store

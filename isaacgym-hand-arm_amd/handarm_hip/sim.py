@@ -45,8 +45,8 @@ class HandArmSim:
         self.num_actors = self.model.n_actors
         self.num_bodies = self.model.n_bodies
         self.stats_ring = stats_ring
-        # contacts per substep the kernel family holds (ha_physics.h MAXC x chunks: 42 for the clutter family)
-        self.contact_capacity = 42 if (self.task == HM.TASK_UR5SIH and self.params.n_objects > 3) else 21
+        # contacts per substep the kernel family holds (ha_physics.h MAXC x chunks: 84 for the clutter family)
+        self.contact_capacity = 84 if (self.task == HM.TASK_UR5SIH and self.params.n_objects > 3) else 21
         spec = HM.state_spec(num_envs, n_links=self.num_links, n_dofs=self.num_dofs, n_obj=self.n_obj,
                              num_initial_poses=self.params.num_initial_poses, num_actions=self.params.num_actions,
                              num_obs=self.params.num_obs, n_actors=self.num_actors, n_bodies=self.num_bodies)

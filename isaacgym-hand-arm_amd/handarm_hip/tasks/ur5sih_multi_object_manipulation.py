@@ -195,6 +195,7 @@ class Ur5SihMultiObjectManipulation:
         self._sync_obs_cache()      # observables' post_step in ConfigurableVecTask.__init__
         self.objects_dropped = False
         self.max_drop_rounds = int(_get(cfg, "objects.drop.max_rounds", 30))
+        self.max_drop_rounds_place = bool(_get(cfg, "objects.drop.place_remaining", True))
         self._stat_pending = 0
         self._stat_folded = 0
         self._success_rate_ewma = 0.0
@@ -407,7 +408,7 @@ class Ur5SihMultiObjectManipulation:
             in_bin = torch.zeros((N, n_obj), dtype=torch.bool, device=self.device)
             rounds = 0
             while not bool(in_bin.all()):
-                if rounds == self.max_drop_rounds:
+                if rounds == self.max_drop_rounds and self.max_drop_rounds_place:
                     # the reference loops until every object lands in the bin extent; cap it so a
                     # rolling object cannot stall initialisation (remaining objects stay where they are)
                     print(f"[handarm_hip] drop init: {int((~in_bin).sum())} objects outside the bin extent after "
@@ -419,6 +420,8 @@ class Ur5SihMultiObjectManipulation:
                     rs[bad[:, 0], bad[:, 1], 3:7] = torch.tensor([0.0, 0.0, 0.0, 1.0], device=self.device)
                     rs[bad[:, 0], bad[:, 1], 7:13] = 0.0
                     self.sim.simulate(self.task_cfg["drop_num_steps"])
+                    break
+                if rounds == self.max_drop_rounds:          # diagnostic: stop, leaving the objects where they are
                     break
                 rounds += 1
                 print(f"[handarm_hip] drop init pose {p}: round {rounds}, {int((~in_bin).sum())} objects to drop",

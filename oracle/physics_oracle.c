@@ -31,7 +31,7 @@
 #include "../include/handarm_abi.h"
 #include "../include/ha_fmath.h"
 
-#define MAXC HA_MAX_CONTACTS   /* contact list capacity; a handle uses 21 (<= 3 objects) or 42 (clutter) */
+#define MAXC HA_MAX_CONTACTS   /* contact list capacity; a handle uses 21 (<= 3 objects) or 84 (clutter) */
 #define MAXR (3 * MAXC)
 #define NOBJ HA_MAX_OBJ
 #define MAXB 48                  /* rigid bodies per env (ha_physics.h MAXB) */
@@ -874,7 +874,7 @@ hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int nu
     h->A = model->n_actors;
     h->D = model->n_dofs;
     h->B = model->n_bodies;
-    h->maxc = (params->task == HA_TASK_UR5SIH && params->n_objects > 3) ? 2 * 21 : 21;
+    h->maxc = (params->task == HA_TASK_UR5SIH && params->n_objects > 3) ? 4 * 21 : 21;   /* handarm_hip.hip HB_CHUNKS */
     return h;
 }
 void hao_destroy(hao_handle h) { free(h); }

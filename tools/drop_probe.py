@@ -1,0 +1,37 @@
+"""Drop-initialisation probe (bin-picking scene): after the drop rounds, where are the objects that are still
+outside the bin extent, and which pool objects are they? Usage (GPU box): python tools/drop_probe.py [N] [rounds]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "isaacgym-hand-arm_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from handarm_hip import model as HM  # noqa: E402
+from handarm_hip.tasks import Ur5SihMultiObjectManipulation  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+pool = [o["name"] for o in HM.load_scene()["objects"]]
+env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}, "seed": 42, "bin": {"asset": "hard_bin"},
+                                     "objects": {"num_objects": 8, "dataset": {"ycb": pool},
+                                                 "drop": {"max_rounds": rounds, "place_remaining": False}}}, "cuda:0", "cuda:0")
+env._drop_initialisation()
+torch.cuda.synchronize()
+A, a0 = env.num_actors, env.actor_object0
+rs = env.root_state.view(n, A, 13)[:, a0:a0 + 8].cpu().numpy()
+lo, hi = np.array(env.bin_extent[0]), np.array(env.bin_extent[1])
+pos = rs[..., 0:3]
+inside = ((pos >= lo) & (pos <= hi)).all(-1)
+print(f"objects outside after the drop: {int((~inside).sum())} of {inside.size}")
+idx = env.object_indices.cpu().numpy()
+bad = np.argwhere(~inside)
+for e, o in bad[:40]:
+    p = pos[e, o]
+    why = [f"{'xyz'[k]}{'<' if p[k] < lo[k] else '>'}" for k in range(3) if p[k] < lo[k] or p[k] > hi[k]]
+    print(f"env {e} obj {o} {pool[idx[e, o]]:22s} pos {np.round(p, 3)} vel {np.round(np.linalg.norm(rs[e, o, 7:10]), 3)} "
+          f"out {' '.join(why)}")
+from collections import Counter
+print("by object:", Counter(pool[idx[e, o]] for e, o in bad).most_common())
+print("by axis:", Counter(tuple(k for k in range(3) if pos[e, o, k] < lo[k] or pos[e, o, k] > hi[k]) for e, o in bad))
