@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 7
+#define HA_ABI_VERSION 8
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -152,6 +152,12 @@ typedef struct ha_model_t {
      * (multi_object.py:626-637). 0 = the table row copies the table actor's root state (earlier scenes). */
     int32_t n_fixed_bodies, body_fixed0;
     float body_fixed_pose[HA_MAX_FIXED_BODIES][7];
+    /* v8: compound pool objects (convex pieces, like the reference's V-HACD, multi_object.py:37-43): pool
+     * object i collides with hulls pool_hull[i] .. pool_hull[i] + pool_nhull[i] - 1; pool_center / pool_radius
+     * (object frame) bound all of them (= the hull's own sphere for a one-hull object). Pairs with a compound
+     * object run the narrow phase piece by piece (A's pieces outer, B's inner). */
+    int32_t pool_nhull[HA_MAX_POOL];
+    float pool_center[HA_MAX_POOL][3], pool_radius[HA_MAX_POOL];
 } ha_model_t;
 
 /* Simulation + task parameters (Ur5SihBase.yaml, Ur5SihMultiObject*.yaml). */

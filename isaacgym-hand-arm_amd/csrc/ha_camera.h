@@ -48,10 +48,16 @@ extern "C" __global__ void __launch_bounds__(256) ha_camera_kernel(CamLaunch L) 
     const ha_model_t& m = *L.m;
     const int tid = threadIdx.x;
     const int W = cam.width, H = cam.height;
-    const int NH = L.n_link_hulls + L.NO + L.n_static;
+    // this env's hull list: link hulls, then every convex piece of each object (ha_model_t v8), then static boxes
+    int n_pieces = 0;
+    for (int o = 0; o < L.NO; o++) {
+        int pool = (int)L.object_indices[(size_t)env * L.NO + o];
+        pool = (unsigned)pool < (unsigned)m.n_pool ? pool : 0;
+        n_pieces += m.pool_nhull[pool];
+    }
+    const int NH = L.n_link_hulls + n_pieces + L.n_static;
     const bool cast = !(L.flags & HA_CAM_FROM_DEPTH);
     if (cast && tid < NH) {
-        // hull k: link hulls, then objects, then static boxes
         const int k = tid;
         int hull, seg;
         float p[3], q[4];
@@ -61,17 +67,21 @@ extern "C" __global__ void __launch_bounds__(256) ha_camera_kernel(CamLaunch L) 
             const float* r = L.body + ((size_t)env * L.B + L.body_robot0 + m.hull_link[k]) * 13;
             p[0] = r[0]; p[1] = r[1]; p[2] = r[2];
             q[0] = r[3]; q[1] = r[4]; q[2] = r[5]; q[3] = r[6];
-        } else if (k < L.n_link_hulls + L.NO) {
-            const int o = k - L.n_link_hulls;
-            int pool = (int)L.object_indices[(size_t)env * L.NO + o];
-            pool = (unsigned)pool < (unsigned)m.n_pool ? pool : 0;
-            hull = m.pool_hull[pool];
+        } else if (k < L.n_link_hulls + n_pieces) {
+            int o = 0, j = k - L.n_link_hulls, pool = 0;
+            for (; o < L.NO; o++) {
+                pool = (int)L.object_indices[(size_t)env * L.NO + o];
+                pool = (unsigned)pool < (unsigned)m.n_pool ? pool : 0;
+                if (j < m.pool_nhull[pool]) break;
+                j -= m.pool_nhull[pool];
+            }
+            hull = m.pool_hull[pool] + j;
             seg = 3 + o;                                               // multi_object.py:642
             const float* r = L.root + ((size_t)env * L.A + L.a0 + o) * 13;
             p[0] = r[0]; p[1] = r[1]; p[2] = r[2];
             q[0] = r[3]; q[1] = r[4]; q[2] = r[5]; q[3] = r[6];
         } else {
-            const int s = k - L.n_link_hulls - L.NO;
+            const int s = k - L.n_link_hulls - n_pieces;
             hull = m.static_hull[s];
             seg = cam.static_seg[s];
             p[0] = m.static_pos[s][0]; p[1] = m.static_pos[s][1]; p[2] = m.static_pos[s][2];

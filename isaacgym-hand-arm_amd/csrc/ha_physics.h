@@ -44,6 +44,7 @@ struct ColScratch {
     float wpA[128][4], wpB[128][4];     // world face planes (n, d) of both hulls
     int cand[64];                       // clipping: candidate incident vertices
     int cmax[64];                       // clipping: per-candidate max plane distance (order-preserving int)
+    float gp[64][4], gn[64][4];         // compound object pair: gathered points (x, sep) and their normals
 };
 struct RowScratch {
     float J[MAXR * RS];
@@ -86,7 +87,8 @@ struct EnvLDS {
     float Minv[MAXD * MAXD];                    // S ~ M^-1 (factor_inverse), stride D
     float Cb[MAXD];
     float v[MAXV];
-    int nc, nr, noff, pad1;                     // contacts kept / rows / contacts offered this substep
+    int nc, nr, noff, ng;                       // contacts kept / rows / contacts offered this substep /
+                                                // points gathered for a compound object pair
     int cst[4];                                 // contact_stats of this launch (see ha_state_t)
     union {
         PostScratch pd;
@@ -201,6 +203,7 @@ struct SimCtx {
     // narrow-phase cache: (hull, body) whose world vertices / planes are in ColScratch side A / side B. Within one
     // detect() the poses do not change, so consecutive pairs that share a side skip its setup (same values).
     int colA_h, colA_b, colB_h, colB_b;
+    bool gather;            // a compound object pair's piece pairs: reduced points go to ColScratch gp / gn
 #ifdef HA_AB_TIMING
     bool dry;               // A/B timing builds only: a repeated phase that must not emit contacts
 #endif
@@ -537,7 +540,10 @@ HD f3 inv_scale(const SimCtx& c, int b) {
     return mk3(1.0f / sc[0], 1.0f / sc[1], 1.0f / sc[2]);
 }
 
-// append up to 4 reduced contacts (lane 0 does the list bookkeeping, same policy as the oracle)
+// append up to 4 reduced contacts (lane 0 does the list bookkeeping, same policy as the oracle). n is the
+// lane's normal: one value over the wave for a convex pair; a compound object pair's gathered points keep
+// their piece pair's normal, and the area criterion then measures about the deepest point's normal. While
+// c.gather is set (a compound pair's piece pairs) the reduced points go to the gather buffer instead.
 HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int b) {
     EnvLDS& s = *c.s;
     int lane = c.lane;
@@ -560,7 +566,8 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
         k = 2;
         f3 p1 = mk3(bcast(pt.x, i1), bcast(pt.y, i1), bcast(pt.z, i1));
         f3 e = p1 - p0;
-        float sv = dot3(cross3(e, pt - p0), n);
+        f3 n0 = mk3(bcast(n.x, i0), bcast(n.y, i0), bcast(n.z, i0));
+        float sv = dot3(cross3(e, pt - p0), n0);
         float v2 = valid ? sv : -3.0e38f;
         int i2 = lane;
         wave_argmax(v2, i2);
@@ -572,17 +579,37 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
         j3 = i3;
         k = 2 + (h2 ? 1 : 0) + (h3 ? 1 : 0);
     }
-    if (lane == 0) s.noff += k;
-    // gather the chosen points to every lane, lane 0 appends
-    f3 P[4];
+    // the chosen points to every lane
+    f3 P[4], N[4];
     float S[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         int src = t == 0 ? i0 : (t < k ? (t == 1 ? j1 : (t == 2 ? j2 : j3)) : 0);
         P[t] = mk3(bcast(pt.x, src), bcast(pt.y, src), bcast(pt.z, src));
+        N[t] = mk3(bcast(n.x, src), bcast(n.y, src), bcast(n.z, src));
         S[t] = bcast(sep, src);
     }
-    // append, or (list full) replace the shallowest contact if this one is deeper: the shallowest is the first
+    if (c.gather) {
+        // compound pair: the chosen points (in the oracle's index order) join the gather buffer
+        if (lane == 0) {
+            ColScratch& cs = s.u.col;
+            int ng = s.ng;
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                if (t < k && ng < 64) {
+                    st3(cs.gp[ng], P[t]);
+                    cs.gp[ng][3] = S[t];
+                    st3(cs.gn[ng], N[t]);
+                    ng++;
+                }
+            }
+            s.ng = ng;
+        }
+        wsync();
+        return;
+    }
+    if (lane == 0) s.noff += k;
+    // lane 0 appends, or (list full) replaces the shallowest contact if this one is deeper: the shallowest is the first
     // maximum of sep over the list (the oracle's sequential strict-compare scan), found by a wave arg-max over
     // lanes = contacts instead of a scan on lane 0 (clutter scenes run with the list full)
     float mu = contact_friction(c, a, b);
@@ -607,7 +634,7 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
             if (slot == nc) s.nc = nc + 1;
             ContactLDS& ct = c.k[slot];
             st3(ct.x, P[t]);
-            st3(ct.n, n);
+            st3(ct.n, N[t]);
             ct.sep = S[t];
             ct.mu = mu;
             ct.a = a;
@@ -842,6 +869,72 @@ HD bool pair_desc(const SimCtx& c, int p, int& kind, int& A, int& B) {
     return false;
 }
 
+// piece pairs of a candidate pair (1 unless an object is a compound of several convex pieces)
+HD int pair_pieces(const SimCtx& c, int kind, int A, int B) {
+    const ha_model_t& m = *c.m;
+    if (kind == 4) return 1;
+    int n = m.pool_nhull[c.o[A].pool];
+    if (kind == 2) n *= m.pool_nhull[c.o[B].pool];
+    return __builtin_amdgcn_readfirstlane(n);
+}
+
+// narrow phase of piece pair j of candidate pair (kind, A, B): the two sides' hulls, poses and body codes
+HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
+    const EnvLDS& s = *c.s;
+    const ha_model_t& m = *c.m;
+    if (kind == 0) {
+        collide_ground(c, m.pool_hull[c.o[A].pool] + j, object_pose(c, A), A);
+        return;
+    }
+    int h1, h2, b1, b2, k2;
+    PoseF P1, P2;
+    if (kind <= 3) {
+        int pa = c.o[A].pool;
+        int ho = m.pool_hull[pa];
+        PoseF Po = object_pose(c, A);
+        if (kind == 1) {
+            h1 = ho + j; P1 = Po; b1 = A; h2 = m.static_hull[B]; P2 = static_pose(m, B); b2 = -1; k2 = -100 - B;
+            // the piece's own sphere against the exact box (the oracle's per-piece near_box; for a one-hull object
+            // the broad phase's test again)
+            f3 cp = Po.p + qrot(Po.q, scale3(c, A, ld3(m.hull_center[h1])));
+            if (!sphere_near_box(m.static_half[B], P2, cp, scale_radius(c, A, m.hull_radius[h1]) + c.p->contact_margin))
+                return;
+        } else if (kind == 2) {
+            int pb = c.o[B].pool, n2 = m.pool_nhull[pb];
+            int j1 = j / n2;
+            h1 = ho + j1; P1 = Po; b1 = A; h2 = m.pool_hull[pb] + (j - j1 * n2); P2 = object_pose(c, B);
+            b2 = B; k2 = B;
+        } else {
+            int Lk = m.hull_link[B];
+            h1 = B; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = ho + j; P2 = Po; b2 = A; k2 = A;
+        }
+    } else {
+        int Lk = m.hull_link[A];
+        h1 = A; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = m.static_hull[B];
+        P2 = static_pose(m, B); b2 = -1; k2 = -100 - B;
+    }
+    collide_hulls(c, h1, P1, h2, P2, b1, b2, b1, k2);
+}
+
+// a compound pair's gathered points (lane = point, in gather order) -> one manifold of <= 4 contacts
+HD void gather_emit(SimCtx& c, int kind, int A, int B) {
+    EnvLDS& s = *c.s;
+    const ColScratch& cs = s.u.col;
+    wsync();
+    int lane = c.lane;
+    bool valid = lane < s.ng;
+    f3 pt = mk3(0, 0, 0), n = mk3(0, 0, 0);
+    float sep = 0;
+    if (valid) {
+        pt = ld3(cs.gp[lane]);
+        sep = cs.gp[lane][3];
+        n = ld3(cs.gn[lane]);
+    }
+    int a = kind == 3 ? 100 + c.m->hull_link[B] : A;
+    int b = kind == 2 ? B : (kind == 3 ? A : -1);
+    emit_contacts(c, valid, pt, sep, n, a, b);
+}
+
 HD void detect(SimCtx& c) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
@@ -865,22 +958,31 @@ HD void detect(SimCtx& c) {
                 cand = c.o[A].coll != 0;
                 if (kind == 2) cand = cand && c.o[B].coll != 0;
                 if (cand) {
-                    int ho = m.pool_hull[c.o[A].pool];
+                    // an object's bounding sphere covers all its convex pieces (ha_model_t v8)
+                    int pa = c.o[A].pool;
                     PoseF Po = object_pose(c, A);
-                    f3 co = Po.p + qrot(Po.q, scale3(c, A, ld3(m.hull_center[ho])));
-                    float ro = scale_radius(c, A, m.hull_radius[ho]);
+                    f3 co = Po.p + qrot(Po.q, scale3(c, A, ld3(m.pool_center[pa])));
+                    float ro = scale_radius(c, A, m.pool_radius[pa]);
                     if (kind == 0) {
                         cand = co.z - ro <= mg;
                     } else {
-                        int hb;
                         PoseF Pb;
-                        if (kind == 1) { hb = m.static_hull[B]; Pb = static_pose(m, B); }
-                        else if (kind == 2) { hb = m.pool_hull[c.o[B].pool]; Pb = object_pose(c, B); }
-                        else { hb = B; int Lk = m.hull_link[B]; Pb = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; }
+                        f3 cl;
+                        float rb;
+                        if (kind == 1) {
+                            int hb = m.static_hull[B];
+                            Pb = static_pose(m, B); cl = ld3(m.hull_center[hb]); rb = m.hull_radius[hb];
+                        } else if (kind == 2) {
+                            int pb = c.o[B].pool;
+                            Pb = object_pose(c, B); cl = ld3(m.pool_center[pb]); rb = m.pool_radius[pb];
+                        } else {
+                            int Lk = m.hull_link[B];
+                            Pb = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; cl = ld3(m.hull_center[B]); rb = m.hull_radius[B];
+                        }
                         int bb = kind == 2 ? B : -1;
-                        f3 cbb = Pb.p + qrot(Pb.q, scale3(c, bb, ld3(m.hull_center[hb])));
+                        f3 cbb = Pb.p + qrot(Pb.q, scale3(c, bb, cl));
                         f3 dc = co - cbb;
-                        float rr = ro + scale_radius(c, bb, m.hull_radius[hb]) + mg;
+                        float rr = ro + scale_radius(c, bb, rb) + mg;
                         cand = dot3(dc, dc) <= rr * rr;
                         if (kind == 1) cand = cand && sphere_near_box(m.static_half[B], Pb, co, ro + mg);
                     }
@@ -902,47 +1004,41 @@ HD void detect(SimCtx& c) {
             }
         }
         uint64_t mask = __ballot(cand);
+        // one iteration per piece pair: a compound object (several convex pieces, ha_model_t v8) runs piece
+        // pairs j = 0 .. np-1 of a candidate pair and then emits a single <= 4-point manifold for the object pair
+        // (the oracle's gather_begin / gather_end). One loop and one call site per narrow phase (a single inlined
+        // copy; a nested piece loop would keep its hoisted invariants live over the narrow phase: VGPRs)
+        int j = 0;
         while (mask) {
             int bit = __ffsll((unsigned long long)mask) - 1;
-            mask &= mask - 1;
             int q = base + bit;
             pair_desc(c, q, kind, A, B);
-            // one call site per narrow phase (keeps a single inlined copy: code size / VGPRs)
-            if (kind == 0) {
-                collide_ground(c, m.pool_hull[c.o[A].pool], object_pose(c, A), A);
-                continue;
-            }
-            int h1, h2, b1, b2, k2;
-            PoseF P1, P2;
-            if (kind <= 3) {
-                int ho = m.pool_hull[c.o[A].pool];
-                PoseF Po = object_pose(c, A);
-                k2 = 0;
-                if (kind == 1) { h1 = ho; P1 = Po; b1 = A; h2 = m.static_hull[B]; P2 = static_pose(m, B); b2 = -1; k2 = -100 - B; }
-                else if (kind == 2) { h1 = ho; P1 = Po; b1 = A; h2 = m.pool_hull[c.o[B].pool]; P2 = object_pose(c, B); b2 = B; }
-                else {
-                    int Lk = m.hull_link[B];
-                    h1 = B; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = ho; P2 = Po; b2 = A;
-                }
-            } else {
-                int Lk = m.hull_link[A];
-                h1 = A; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = m.static_hull[B];
-                P2 = static_pose(m, B); b2 = -1; k2 = -100 - B;
-            }
-            if (kind == 2 || kind == 3) k2 = b2;
+            int np = pair_pieces(c, kind, A, B);
 #ifdef HA_PROFILE
             unsigned long long _k0 = __builtin_amdgcn_s_memtime();
             int _nc0 = s.nc;
 #endif
+            if (np > 1 && j == 0) {
+                if (lane == 0) s.ng = 0;
+                c.gather = true;
+                wsync();
+            }
 #ifdef HA_AB_NARROW_TWICE
             for (int rep = 0; rep < 2; rep++) {     // one call site: the same code size as the product
                 if (rep == 1) { c.dry = true; c.colA_h = c.colB_h = -1; }
-                collide_hulls(c, h1, P1, h2, P2, b1, b2, b1, k2);
+                narrow_phase(c, kind, A, B, j);
             }
             c.dry = false;
 #else
-            collide_hulls(c, h1, P1, h2, P2, b1, b2, b1, k2);
+            narrow_phase(c, kind, A, B, j);
 #endif
+            if (++j < np) continue;
+            j = 0;
+            mask &= mask - 1;
+            if (np > 1) {
+                c.gather = false;
+                gather_emit(c, kind, A, B);
+            }
 #ifdef HA_PROFILE
             wsync();
             PROF_COUNT(10 + kind, __builtin_amdgcn_s_memtime() - _k0);

@@ -81,6 +81,7 @@ class HaModel(C.Structure):
         ("n_static", i32), ("static_hull", arr(i32, MAX_STATIC)), ("static_pos", arr(f32, MAX_STATIC, 3)),
         ("static_quat", arr(f32, MAX_STATIC, 4)), ("static_half", arr(f32, MAX_STATIC, 3)),
         ("n_fixed_bodies", i32), ("body_fixed0", i32), ("body_fixed_pose", arr(f32, MAX_FIXED_BODIES, 7)),
+        ("pool_nhull", arr(i32, MAX_POOL)), ("pool_center", arr(f32, MAX_POOL, 3)), ("pool_radius", arr(f32, MAX_POOL)),
     ]
 
 
@@ -241,7 +242,9 @@ def build_model(scene, pool_names=None):
     # static boxes: the table (static 0) and any extra pieces (table-with-hole walls, bin parts)
     statics = ([table] if table else []) + list(scene.get("statics", []))
     assert len(statics) <= MAX_STATIC
-    hulls = [(h, h["index"]) for h in scene["link_hulls"]] + [(o["hull"], -1) for o in objects] + \
+    # object pieces: the convex decomposition when the scene has one ("hulls", tools/convex_decomp.py), else the hull
+    obj_hulls = [o.get("hulls") or [o["hull"]] for o in objects]
+    hulls = [(h, h["index"]) for h in scene["link_hulls"]] + [(h, -1) for oh in obj_hulls for h in oh] + \
             [(st["hull"], -1) for st in statics]
     assert len(hulls) <= MAX_HULLS
     vs, ps = 0, 0
@@ -264,8 +267,19 @@ def build_model(scene, pool_names=None):
     m.n_link_hulls = len(scene["link_hulls"])
     m.n_pool = len(objects)
     m.n_hulls = len(hulls)
+    first = m.n_link_hulls
     for i, o in enumerate(objects):
-        m.pool_hull[i] = m.n_link_hulls + i
+        m.pool_hull[i] = first
+        m.pool_nhull[i] = len(obj_hulls[i])
+        first += len(obj_hulls[i])
+        if len(obj_hulls[i]) == 1:          # the hull's own sphere (bit-identical broad phase for one-hull objects)
+            m.pool_center[i][:] = obj_hulls[i][0]["center"]
+            m.pool_radius[i] = obj_hulls[i][0]["radius"]
+        else:
+            pts = np.concatenate([np.asarray(h["verts"], np.float64) for h in obj_hulls[i]])
+            ctr = 0.5 * (pts.min(0) + pts.max(0))
+            m.pool_center[i][:] = ctr
+            m.pool_radius[i] = float(np.linalg.norm(pts - ctr, axis=1).max()) * (1 + 1e-6)
         m.pool_mass[i] = o["mass"]
         m.pool_com[i][:] = o["com"]
         m.pool_inertia[i][:] = o["inertia"]

@@ -52,7 +52,8 @@ def hulls_of_env(m, root, body, object_indices, a0, body_robot0, static_seg):
         out.append((r[0:3], r[3:7], k, 1))
     for o, pid in enumerate(object_indices):
         r = root[a0 + o]
-        out.append((r[0:3], r[3:7], m.pool_hull[int(pid)], 3 + o))
+        for j in range(m.pool_nhull[int(pid)]):            # every convex piece of the object (ha_model_t v8)
+            out.append((r[0:3], r[3:7], m.pool_hull[int(pid)] + j, 3 + o))
     for s in range(m.n_static):
         out.append((np.array(m.static_pos[s][:], F), np.array(m.static_quat[s][:], F), m.static_hull[s],
                     static_seg[s]))

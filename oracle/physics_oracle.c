@@ -342,13 +342,15 @@ static void hull_plane(const ha_model_t* m, int hull, int k, pose_t P, const flo
     *d = dl - dot(*n, P.p);
 }
 
-/* reduce candidate list (points, sep) to <= 4 contacts; returns count appended */
-static int reduce_manifold(v3* pts, float* seps, int nc, v3 n, int* out_idx) {
+/* reduce candidate list (points, sep) to <= 4 contacts; returns count appended. The area criterion measures
+   about normal n, or (per-candidate normals nrm, compound objects) about the deepest candidate's normal. */
+static int reduce_manifold(const v3* pts, const float* seps, int nc, v3 n, const v3* nrm, int* out_idx) {
     if (nc <= 0) return 0;
     int i0 = 0;
     for (int i = 1; i < nc; i++)
         if (seps[i] < seps[i0]) i0 = i;
     out_idx[0] = i0;
+    if (nrm) n = nrm[i0];
     if (nc == 1) return 1;
     int i1 = -1;
     float best = 1e-12f;
@@ -374,23 +376,49 @@ static int reduce_manifold(v3* pts, float* seps, int nc, v3 n, int* out_idx) {
 }
 
 #define MAXCAND 128
-static int emit(contact_t* out, int* nout, int maxout, v3* pts, float* seps, int nc, v3 n, int a, int b) {
-    int idx[4];
-    int k = reduce_manifold(pts, seps, nc, n, idx);
+#define MAXGATHER 64
+/* Compound objects (several convex pieces, ha_model_t v8): between gather_begin and gather_end every piece
+   pair's reduced points collect in a per-thread buffer (at most MAXGATHER, later ones dropped) and the object
+   pair then emits ONE manifold of <= 4 points chosen from them, each keeping its piece pair's normal. */
+static __thread int g_on, g_n;
+static __thread v3 g_pt[MAXGATHER], g_nrm[MAXGATHER];
+static __thread float g_sep[MAXGATHER];
+
+static void store_points(contact_t* out, int* nout, int maxout, const v3* pts, const float* seps, const v3* nrm,
+                         v3 n, const int* idx, int k, int a, int b) {
     for (int i = 0; i < k; i++) {
+        v3 ni = nrm ? nrm[idx[i]] : n;
         if (*nout >= maxout) {
             /* replace the shallowest stored contact if this one is deeper */
             int w = 0;
             for (int j = 1; j < maxout; j++)
                 if (out[j].sep > out[w].sep) w = j;
             if (out[w].sep <= seps[idx[i]]) continue;
-            out[w].x = pts[idx[i]]; out[w].n = n; out[w].sep = seps[idx[i]]; out[w].a = a; out[w].b = b;
+            out[w].x = pts[idx[i]]; out[w].n = ni; out[w].sep = seps[idx[i]]; out[w].a = a; out[w].b = b;
             continue;
         }
         contact_t* c = &out[(*nout)++];
-        c->x = pts[idx[i]]; c->n = n; c->sep = seps[idx[i]]; c->a = a; c->b = b;
+        c->x = pts[idx[i]]; c->n = ni; c->sep = seps[idx[i]]; c->a = a; c->b = b;
     }
+}
+static int emit(contact_t* out, int* nout, int maxout, v3* pts, float* seps, int nc, v3 n, int a, int b) {
+    int idx[4];
+    int k = reduce_manifold(pts, seps, nc, n, NULL, idx);
+    if (g_on) {
+        for (int i = 0; i < k && g_n < MAXGATHER; i++, g_n++) {
+            g_pt[g_n] = pts[idx[i]]; g_sep[g_n] = seps[idx[i]]; g_nrm[g_n] = n;
+        }
+        return k;
+    }
+    store_points(out, nout, maxout, pts, seps, NULL, n, idx, k, a, b);
     return k;
+}
+static void gather_begin(void) { g_on = 1; g_n = 0; }
+static void gather_end(contact_t* out, int* nout, int maxout, int a, int b) {
+    int idx[4];
+    g_on = 0;
+    int k = reduce_manifold(g_pt, g_sep, g_n, V(0, 0, 0), g_nrm, idx);
+    store_points(out, nout, maxout, g_pt, g_sep, g_nrm, V(0, 0, 0), idx, k, a, b);
 }
 
 /* hull A (body a) vs hull B (body b); contact normal from B to A */
@@ -495,27 +523,44 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
     float mg = p->contact_margin;
     for (int o = 0; o < h->NO; o++) {
         if (!e->coll[o]) continue;
-        int ho = m->pool_hull[e->pool[o]];
+        int pa = e->pool[o];
+        int ho = m->pool_hull[pa], no = m->pool_nhull[pa];     /* the object's convex pieces (ABI v8) */
         const float* so = env_scale(e, o);
-        pose_t Po = {sub(e->oc[o], qrot(e->oq[o], scl(so, ld3(m->pool_com[e->pool[o]])))), e->oq[o]};
-        collide_ground(m, ho, Po, mg, o, so, out, &nout, h->maxc);
+        pose_t Po = {sub(e->oc[o], qrot(e->oq[o], scl(so, ld3(m->pool_com[pa])))), e->oq[o]};
+        /* a compound object (no > 1 pieces) emits one manifold per object pair (gather_begin / gather_end) */
+        if (no > 1) gather_begin();
+        for (int j = 0; j < no; j++) collide_ground(m, ho + j, Po, mg, o, so, out, &nout, h->maxc);
+        if (no > 1) gather_end(out, &nout, h->maxc, o, -1);
         for (int st = 0; st < m->n_static; st++) {
             pose_t Pst = static_pose(m, st);
-            if (near_box(m->static_half[st], Pst, add(Po.p, qrot(Po.q, scl(so, ld3(m->hull_center[ho])))),
-                         scl_r(so, m->hull_radius[ho]) + mg))
-                collide_hulls(m, ho, Po, m->static_hull[st], Pst, mg, o, -1, so, NULL, out, &nout, h->maxc);
+            if (near_box(m->static_half[st], Pst, add(Po.p, qrot(Po.q, scl(so, ld3(m->pool_center[pa])))),
+                         scl_r(so, m->pool_radius[pa]) + mg)) {
+                if (no > 1) gather_begin();
+                for (int j = 0; j < no; j++)     /* each piece's own sphere against the exact box too */
+                    if (near_box(m->static_half[st], Pst, add(Po.p, qrot(Po.q, scl(so, ld3(m->hull_center[ho + j])))),
+                                 scl_r(so, m->hull_radius[ho + j]) + mg))
+                        collide_hulls(m, ho + j, Po, m->static_hull[st], Pst, mg, o, -1, so, NULL, out, &nout, h->maxc);
+                if (no > 1) gather_end(out, &nout, h->maxc, o, -1);
+            }
         }
         for (int o2 = o + 1; o2 < h->NO; o2++) {
             if (!e->coll[o2]) continue;
-            int h2 = m->pool_hull[e->pool[o2]];
+            int pb = e->pool[o2];
+            int h2 = m->pool_hull[pb], n2 = m->pool_nhull[pb];
             const float* s2 = env_scale(e, o2);
-            pose_t P2 = {sub(e->oc[o2], qrot(e->oq[o2], scl(s2, ld3(m->pool_com[e->pool[o2]])))), e->oq[o2]};
-            collide_hulls(m, ho, Po, h2, P2, mg, o, o2, so, s2, out, &nout, h->maxc);
+            pose_t P2 = {sub(e->oc[o2], qrot(e->oq[o2], scl(s2, ld3(m->pool_com[pb])))), e->oq[o2]};
+            if (no * n2 > 1) gather_begin();
+            for (int j = 0; j < no; j++)
+                for (int j2 = 0; j2 < n2; j2++)
+                    collide_hulls(m, ho + j, Po, h2 + j2, P2, mg, o, o2, so, s2, out, &nout, h->maxc);
+            if (no * n2 > 1) gather_end(out, &nout, h->maxc, o, o2);
         }
         for (int k = 0; k < m->n_link_hulls; k++) {
             int L = m->hull_link[k];
             pose_t PL = {e->lp[L], e->lq[L]};
-            collide_hulls(m, k, PL, ho, Po, mg, 100 + L, o, NULL, so, out, &nout, h->maxc);
+            if (no > 1) gather_begin();
+            for (int j = 0; j < no; j++) collide_hulls(m, k, PL, ho + j, Po, mg, 100 + L, o, NULL, so, out, &nout, h->maxc);
+            if (no > 1) gather_end(out, &nout, h->maxc, 100 + L, o);
         }
     }
     for (int k = 0; k < m->n_link_hulls; k++) {

@@ -35,3 +35,37 @@ def test_spline_tables_equal_oracle():
     for i, name in enumerate(HM.SPLINE_ORDER):
         n = p.spline_pieces[i]
         np.testing.assert_array_equal(sp[i, :, :n], O.SPLINE_OBJS[name].table())
+
+
+def test_mug_is_a_compound_of_convex_pieces():
+    """f1: the non-convex pool object (025_mug; the reference V-HACDs every object, multi_object.py:37-43) is a set
+    of convex pieces (tools/convex_decomp.py): the cavity and the handle gap are open, the pieces stay inside the
+    pool bounding sphere, and every other pool object keeps one hull."""
+    import numpy as np
+    from handarm_hip import model as HM
+    for asset in (HM.ASSET, HM.BIN_ASSET):
+        m = HM.build_model(HM.load_scene(asset))
+        names = [o["name"] for o in HM.load_scene(asset)["objects"]]
+        mug = names.index("025_mug")
+        assert m.pool_nhull[mug] >= 8
+        assert all(m.pool_nhull[i] == 1 for i in range(m.n_pool) if i != mug)
+        assert m.n_hulls <= 64 and m.pool_hull[mug] + m.pool_nhull[mug] <= m.n_hulls
+        pieces = range(m.pool_hull[mug], m.pool_hull[mug] + m.pool_nhull[mug])
+        planes = np.ctypeslib.as_array(m.planes)
+
+        def inside(x):
+            for k in pieces:
+                p = planes[m.hull_plane_start[k]:m.hull_plane_start[k] + m.hull_nplanes[k]]
+                if np.all(p[:, :3] @ x + p[:, 3] <= 0):
+                    return True
+            return False
+        verts = np.concatenate([np.ctypeslib.as_array(m.verts)[m.hull_vert_start[k]:m.hull_vert_start[k] + m.hull_nverts[k], :3]
+                                for k in pieces])
+        c = np.array(m.pool_center[mug][:])
+        assert np.linalg.norm(verts - c, axis=1).max() <= m.pool_radius[mug]
+        # the mug's axis is z; its cavity (centre column, above the base) is empty space, the wall is not
+        lo, hi = verts.min(0), verts.max(0)
+        axis = np.array([verts[:, 0].min() + 0.046, 0.5 * (lo[1] + hi[1])])
+        assert not inside(np.array([axis[0], axis[1], 0.5 * (lo[2] + hi[2])]))
+        assert not inside(np.array([axis[0], axis[1], hi[2] - 0.01]))
+        assert inside(np.array([axis[0], axis[1], lo[2] + 0.002]))        # the base slab

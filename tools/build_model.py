@@ -333,20 +333,36 @@ def build_robot():
             "base_quat": [0.0, 0.0, 0.0, 1.0]}, hulls
 
 
+# Pool objects whose collision shape is a set of convex pieces, like the reference's V-HACD
+# (multi_object.py:37-43): the mug is the one clearly non-convex pool object (mesh volume 138 cm3 against 525 cm3
+# for its convex hull; every other pool object is within 20 %), so it alone is decomposed (tools/convex_decomp.py
+# decompose_vessel: base slab, 6 wall sectors, 2 handle pieces; the cavity and the handle gap stay open).
+DECOMPOSE = {"025_mug": "vessel"}
+
+
 def build_object(name):
     urdf = os.path.join(ASSETS, "object_sets", "urdf", "ycb", name + ".urdf")
     root = ET.parse(urdf).getroot()
     link = root.find("link")
     mass = float(link.find("inertial/mass").get("value"))
     mesh = link.find("collision/geometry/mesh").get("filename")
-    v, _ = load_mesh(os.path.normpath(os.path.join(os.path.dirname(urdf), mesh)), [1, 1, 1])
+    v, f = load_mesh(os.path.normpath(os.path.join(os.path.dirname(urdf), mesh)), [1, 1, 1])
     hull = hull_record(v, MAX_OBJ_VERTS)
     vol, com, I_unit = polyhedron_mass_props(v)
     R, ctr, ext = min_volume_obb(reduce_points(v, 256))
-    return {"name": name, "mass": mass, "com": com.tolist(),
-            "inertia": (I_unit * mass / vol).reshape(-1).tolist(), "hull": hull,
-            "bbox_from_origin_pos": ctr.tolist(), "bbox_from_origin_quat": scipy_quat(R).tolist(),
-            "bbox_extents": ext.tolist()}
+    rec = {"name": name, "mass": mass, "com": com.tolist(),
+           "inertia": (I_unit * mass / vol).reshape(-1).tolist(), "hull": hull,
+           "bbox_from_origin_pos": ctr.tolist(), "bbox_from_origin_quat": scipy_quat(R).tolist(),
+           "bbox_extents": ext.tolist()}
+    if name in DECOMPOSE:
+        import convex_decomp as CD
+        pieces, _ = CD.decompose_vessel(v, f)
+        rec["hulls"] = [hull_record(p, MAX_OBJ_VERTS) for p in pieces]
+        # mass properties of the actual (non-convex) shape: the closed mesh itself
+        vol, com, I_unit = CD.mesh_volume_props(v, f)
+        rec["com"] = com.tolist()
+        rec["inertia"] = (I_unit * mass / vol).reshape(-1).tolist()
+    return rec
 
 
 def box_hull(half):

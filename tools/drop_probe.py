@@ -11,16 +11,21 @@ import torch  # noqa: E402
 from handarm_hip import model as HM  # noqa: E402
 from handarm_hip.tasks import Ur5SihMultiObjectManipulation  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
-rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+n = int(args[0]) if args else 2048
+rounds = int(args[1]) if len(args) > 1 else 30
+nobin = "--nobin" in sys.argv          # the C4 scene: no bin, 3 objects of the 16-object pool on the table
+no = 3 if nobin else 8
 pool = [o["name"] for o in HM.load_scene()["objects"]]
-env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}, "seed": 42, "bin": {"asset": "hard_bin"},
-                                     "objects": {"num_objects": 8, "dataset": {"ycb": pool},
-                                                 "drop": {"max_rounds": rounds, "place_remaining": False}}}, "cuda:0", "cuda:0")
+cfg = {"env": {"numEnvs": n}, "seed": 42, "objects": {"num_objects": no, "dataset": {"ycb": pool},
+                                                        "drop": {"max_rounds": rounds, "place_remaining": False}}}
+if not nobin:
+    cfg["bin"] = {"asset": "hard_bin"}
+env = Ur5SihMultiObjectManipulation(cfg, "cuda:0", "cuda:0")
 env._drop_initialisation()
 torch.cuda.synchronize()
 A, a0 = env.num_actors, env.actor_object0
-rs = env.root_state.view(n, A, 13)[:, a0:a0 + 8].cpu().numpy()
+rs = env.root_state.view(n, A, 13)[:, a0:a0 + no].cpu().numpy()
 lo, hi = np.array(env.bin_extent[0]), np.array(env.bin_extent[1])
 pos = rs[..., 0:3]
 inside = ((pos >= lo) & (pos <= hi)).all(-1)

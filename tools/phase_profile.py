@@ -43,7 +43,7 @@ if __name__ == "__main__":
         print("    hull-hull split: " + "  ".join(f"{nm} {100.0 * buf[25 + i] / tot:5.1f}%" for i, nm in
               enumerate(["setup", "SAT A", "SAT B", "clip", "emit"])), flush=True)
 
-    if any(f in sys.argv for f in ("--bench-scene", "--kuka", "--bin", "--allegro")):
+    if any(f in sys.argv for f in ("--bench-scene", "--kuka", "--bin", "--allegro", "--c4")):
         # the bench workload: VecTask after its first (reset) steps, random actions
         from handarm_hip.tasks import AllegroHand, AllegroKuka, Ur5SihMultiObjectManipulation
         if "--allegro" in sys.argv:
@@ -58,6 +58,13 @@ if __name__ == "__main__":
             env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}, "seed": 42, "bin": {"asset": "hard_bin"},
                                                  "objects": {"num_objects": 8, "dataset": {"ycb": pool}}},
                                                 "cuda:0", "cuda:0")
+        elif "--c4" in sys.argv:        # bench config 4: 16-object YCB pool, DR on (--nomug: the pool without the mug)
+            from handarm_hip import model as HM
+            pool = [o["name"] for o in HM.load_scene()["objects"]]
+            if "--nomug" in sys.argv:
+                pool = [p for p in pool if "mug" not in p]
+            env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}, "seed": 42, "task": {"randomize": True},
+                                                 "objects": {"dataset": {"ycb": pool}}}, "cuda:0", "cuda:0")
         else:
             env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}, "seed": 42}, "cuda:0", "cuda:0")
         env.reset()
