@@ -12,6 +12,8 @@
  *   ha_create / ha_bind_state      gym.create_sim + prepare_sim + acquire_*_tensor + wrap_tensor
  *                                  (tasks/base/vec_task.py:58-64,288; hand_arm/base/observable_vec_task.py:123-155)
  *   ha_simulate                    gym.simulate (vec_task.py:412; multi_object_manipulation.py:67,124,139,172)
+ *   ha_simulate_envs               gym.simulate of _drop_objects (multi_object_manipulation.py:124), stepping only
+ *                                  the envs that still have an object to drop
  *   ha_refresh                     gym.refresh_{dof_state,actor_root_state,rigid_body_state,net_contact_force}_tensor
  *                                  (observable_vec_task.py:173-177)
  *   ha_set_dof_position_target     gym.set_dof_position_target_tensor (hand_arm/base/actionable_vec_task.py:39-40)
@@ -42,7 +44,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 8
+#define HA_ABI_VERSION 9
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -240,6 +242,12 @@ typedef struct ha_params_t {
     float ak_fingertip_offsets[4][3];
     int32_t ak_palm_link, ak_fingertip_links[4];
     int32_t ak_num_arm_dofs;           /* 7 */
+    /* v9: resting-contact stability. Penetration up to contact_slop gets no Baumgarte push-out (the push-out
+     * velocity is kept by the body, and re-adding it every substep rocks resting objects); a manifold's points
+     * 2-4 are chosen only among candidates within manifold_window of its deepest point (speculative points
+     * higher up a rounded side would otherwise displace the true support corners). */
+    float contact_slop;                /* 0.001 m */
+    float manifold_window;             /* 0.002 m */
 } ha_params_t;
 
 /* Device buffers (caller-allocated). Layouts match the Isaac Gym tensors exactly. */
@@ -378,6 +386,10 @@ int ha_destroy(ha_handle h);
 int ha_bind_state(ha_handle h, const ha_state_t* state);
 /* gym-style tensor API */
 int ha_simulate(ha_handle h, int32_t n_calls, uint32_t flags, void* stream);
+/* v9: ha_simulate for a subset of envs (device array of n_envs distinct env indices; the other envs do not move).
+ * The drop initialisation's later rounds step only the envs that still have an object to drop. */
+int ha_simulate_envs(ha_handle h, int32_t n_calls, uint32_t flags, const int32_t* env_ids, int32_t n_envs,
+                     void* stream);
 int ha_refresh(ha_handle h, void* stream);
 int ha_set_dof_position_target(ha_handle h, const float* targets, void* stream);
 int ha_set_actor_root_state_indexed(ha_handle h, const float* root_state, const int32_t* actor_indices,

@@ -557,8 +557,10 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
     if (i0 >= (1 << 20)) return;
     int k = 1, j1 = 0, j2 = 0, j3 = 0;        // chosen lanes of points 1..3 (valid below k)
     f3 p0 = mk3(bcast(pt.x, i0), bcast(pt.y, i0), bcast(pt.z, i0));
+    // points 2-4 only among the candidates within manifold_window of the deepest one (ha_params_t v9)
+    bool near = valid && sep <= v0 + c.p->manifold_window;
     f3 dd = pt - p0;
-    float v1 = valid ? dot3(dd, dd) : -1.0f;
+    float v1 = near ? dot3(dd, dd) : -1.0f;
     int i1 = lane;
     wave_argmax(v1, i1);
     if (v1 > 1e-12f) {
@@ -568,10 +570,10 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
         f3 e = p1 - p0;
         f3 n0 = mk3(bcast(n.x, i0), bcast(n.y, i0), bcast(n.z, i0));
         float sv = dot3(cross3(e, pt - p0), n0);
-        float v2 = valid ? sv : -3.0e38f;
+        float v2 = near ? sv : -3.0e38f;
         int i2 = lane;
         wave_argmax(v2, i2);
-        float v3 = valid ? sv : 3.0e38f;
+        float v3 = near ? sv : 3.0e38f;
         int i3 = lane;
         wave_argmin(v3, i3);
         bool h2 = v2 > 1e-12f, h3 = v3 < -1e-12f;
@@ -1257,7 +1259,8 @@ HD void substep(SimCtx& c, float hdt) {
             jac_body(c, ct.b, x, dir, -1.0f, Jr, Jo, so0);
             if (k == 0) {
                 float sp = ct.sep;
-                float v0 = sp > 0 ? -sp / hdt : -p.baumgarte * sp / hdt;
+                float sb = sp + p.contact_slop < 0.0f ? sp + p.contact_slop : 0.0f;   // penetration beyond the slop
+                float v0 = sp > 0 ? -sp / hdt : -p.baumgarte * sb / hdt;
                 if (v0 > p.max_depen_vel) v0 = p.max_depen_vel;
                 vt_ = v0;
             }

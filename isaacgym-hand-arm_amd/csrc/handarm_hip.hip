@@ -296,14 +296,16 @@ static_assert(HA_ND + 6 * HA_MAX_OBJ <= MAXV, "bin-picking (8 objects) must fit 
 template <int FAM, int MODE>
 __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params,
                                          const ha_state_t& st, int num_envs, int n_calls, uint32_t flags,
-                                         int stat_slot, float* __restrict__ spill) {
+                                         int stat_slot, float* __restrict__ spill,
+                                         const int32_t* __restrict__ env_ids) {
     constexpr int TASK = fam_task<FAM>();
     constexpr int ND = task_nd<FAM>();
     constexpr int NCH = task_contact_chunks<FAM>();
     using PC = FamPhys<FAM>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    int env = blockIdx.x;
-    if (env >= num_envs) return;
+    // one workgroup per env; ha_simulate_envs launches one per listed env
+    int env = env_ids ? env_ids[blockIdx.x] : (int)blockIdx.x;
+    if (env < 0 || env >= num_envs) return;
     SimCtx c;
     c.gather = false;
 #ifdef HA_AB_TIMING
@@ -420,8 +422,8 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     extern "C" __global__ void __launch_bounds__(64)                                                          \
         __attribute__((amdgpu_waves_per_eu(FAM == HA_TASK_UR5SIH ? HA_WAVES_PER_EU : 1)))                       \
         name(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params, ha_state_t st,       \
-             int num_envs, int n_calls, uint32_t flags, int stat_slot, float* spill) {                          \
-        env_body<FAM, MODE>(model, params, st, num_envs, n_calls, flags, stat_slot, spill);                    \
+             int num_envs, int n_calls, uint32_t flags, int stat_slot, float* spill, const int32_t* env_ids) {  \
+        env_body<FAM, MODE>(model, params, st, num_envs, n_calls, flags, stat_slot, spill, env_ids);           \
     }
 HA_KERNEL(ha_step_kernel, HA_TASK_UR5SIH, MODE_STEP)
 HA_KERNEL(ha_simulate_kernel, HA_TASK_UR5SIH, MODE_SIMULATE)
@@ -440,7 +442,8 @@ HA_KERNEL(ak_simulate_kernel, HA_TASK_ALLEGRO_KUKA, MODE_SIMULATE)
 HA_KERNEL(ak_observe_kernel, HA_TASK_ALLEGRO_KUKA, MODE_OBSERVE)
 HA_KERNEL(ak_reset_kernel, HA_TASK_ALLEGRO_KUKA, MODE_RESET)
 
-typedef void (*env_kernel_t)(const ha_model_t*, const ha_params_t*, ha_state_t, int, int, uint32_t, int, float*);
+typedef void (*env_kernel_t)(const ha_model_t*, const ha_params_t*, ha_state_t, int, int, uint32_t, int, float*,
+                             const int32_t*);
 static env_kernel_t kernel_for(int fam, int mode) {
     if (fam == FAM_UR5SIH_CLUTTER) {
         switch (mode) {
@@ -691,13 +694,14 @@ int ha_bind_state(ha_handle h, const ha_state_t* state) {
     return HA_OK;
 }
 
-static int launch(ha_handle h, int mode, int n_calls, uint32_t flags, int slot, void* stream) {
+static int launch(ha_handle h, int mode, int n_calls, uint32_t flags, int slot, void* stream,
+                  const int32_t* env_ids = nullptr, int n_ids = 0) {
     if (!h || !h->bound) return HA_E_STATE;
     hipStream_t s = (hipStream_t)stream;
     bool rec = h->t_ev && h->t_count < h->t_max;
     (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count] : h->ev0, s);
-    hipLaunchKernelGGL(kernel_for(h->fam, mode), dim3(h->N), dim3(64), lds_bytes(h->fam), s, h->d_model, h->d_params, h->st,
-                       h->N, n_calls, flags, slot, h->d_spill);
+    hipLaunchKernelGGL(kernel_for(h->fam, mode), dim3(env_ids ? n_ids : h->N), dim3(64), lds_bytes(h->fam), s, h->d_model,
+                       h->d_params, h->st, h->N, n_calls, flags, slot, h->d_spill, env_ids);
     HIPCHK(hipGetLastError());
     (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count + 1] : h->ev1, s);
     if (rec) {
@@ -712,6 +716,12 @@ int ha_simulate(ha_handle h, int32_t n_calls, uint32_t flags, void* stream) {
     if (n_calls < 0) return HA_E_ARG;
     if (n_calls == 0 || (flags & HA_FLAG_NO_PHYSICS)) return HA_OK;
     return launch(h, MODE_SIMULATE, n_calls, flags, 0, stream);
+}
+
+int ha_simulate_envs(ha_handle h, int32_t n_calls, uint32_t flags, const int32_t* env_ids, int32_t n_envs, void* stream) {
+    if (!h || n_calls < 0 || n_envs < 0 || (n_envs > 0 && !env_ids) || n_envs > h->N) return HA_E_ARG;
+    if (n_calls == 0 || n_envs == 0 || (flags & HA_FLAG_NO_PHYSICS)) return HA_OK;
+    return launch(h, MODE_SIMULATE, n_calls, flags, 0, stream, env_ids, n_envs);
 }
 
 // The bound tensors ARE the simulation state (zero-copy), so refresh has nothing to copy.

@@ -25,6 +25,7 @@ SIGNATURES = {
     "ha_destroy": ([H], C.c_int),
     "ha_bind_state": ([H, C.POINTER(HM.HaState)], C.c_int),
     "ha_simulate": ([H, C.c_int32, C.c_uint32, S], C.c_int),
+    "ha_simulate_envs": ([H, C.c_int32, C.c_uint32, C.c_void_p, C.c_int32, S], C.c_int),
     "ha_refresh": ([H, S], C.c_int),
     "ha_set_dof_position_target": ([H, fp, S], C.c_int),
     "ha_set_actor_root_state_indexed": ([H, fp, fp, C.c_int32, S], C.c_int),

@@ -121,6 +121,7 @@ class HaParams(C.Structure):
         ("ak_target_lo", arr(f32, 3)), ("ak_target_size", arr(f32, 3)), ("ak_palm_offset", arr(f32, 3)),
         ("ak_fingertip_offsets", arr(f32, 4, 3)), ("ak_palm_link", i32), ("ak_fingertip_links", arr(i32, 4)),
         ("ak_num_arm_dofs", i32),
+        ("contact_slop", f32), ("manifold_window", f32),                       # v9
     ]
 
 
@@ -395,6 +396,7 @@ def natural_cubic_spline_table(knots, values):
 DEFAULT_TASK = dict(
     dt=0.016666667, substeps=2, control_freq_inv=3, solver_iters=8, gravity=(0.0, 0.0, -9.81),
     friction=1.0, contact_margin=0.01, baumgarte=0.2, max_depen_vel=1.0, object_ang_damping=0.5,
+    contact_slop=0.001, manifold_window=0.002,
     joint_limit_margin=0.02, n_objects=3, num_initial_poses=1, max_episode_length=200,
     sih_alpha=0.8, reward_reaching=1.0, reward_lifting=5.0, reward_goal=50.0, reward_success=50.0,
     lifting_threshold=0.05, goal_threshold=0.05, goal_pos=(0.28, 0.58, 0.8), goal_noise=(0.15, 0.15, 0.1),
@@ -500,6 +502,7 @@ def build_params(cfg=None, task=None):
         c.update(cfg)
     p = HaParams()
     for k in ["dt", "substeps", "control_freq_inv", "solver_iters", "friction", "contact_margin", "baumgarte",
+              "contact_slop", "manifold_window",
               "max_depen_vel", "object_ang_damping", "joint_limit_margin", "n_objects", "num_initial_poses",
               "max_episode_length", "sih_alpha", "reward_reaching", "reward_lifting", "reward_goal",
               "reward_success", "lifting_threshold", "goal_threshold", "seed"]:

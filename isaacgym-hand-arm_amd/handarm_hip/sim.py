@@ -139,8 +139,14 @@ class HandArmSim:
     refresh_dof_state_tensor = refresh_actor_root_state_tensor
     refresh_net_contact_force_tensor = refresh_actor_root_state_tensor
 
-    def simulate(self, n_calls=1, flags=0):
-        _lib.check(self.lib.ha_simulate(self.h, n_calls, flags, self._stream()), "ha_simulate")
+    def simulate(self, n_calls=1, flags=0, env_ids=None):
+        """gym.simulate n_calls times; env_ids (device tensor of distinct env indices): those envs only."""
+        if env_ids is None:
+            _lib.check(self.lib.ha_simulate(self.h, n_calls, flags, self._stream()), "ha_simulate")
+            return
+        ids = env_ids.to(device=self.device, dtype=torch.int32).contiguous()
+        _lib.check(self.lib.ha_simulate_envs(self.h, n_calls, flags, C.c_void_p(ids.data_ptr()), ids.numel(),
+                                             self._stream()), "ha_simulate_envs")
 
     def fetch_results(self, wait=True):
         if wait:

@@ -194,8 +194,12 @@ class Ur5SihMultiObjectManipulation:
         t["sim_targets"].copy_(self.dof_pos)
         self._sync_obs_cache()      # observables' post_step in ConfigurableVecTask.__init__
         self.objects_dropped = False
-        self.max_drop_rounds = int(_get(cfg, "objects.drop.max_rounds", 30))
-        self.max_drop_rounds_place = bool(_get(cfg, "objects.drop.place_remaining", True))
+        # the reference drops until every object lands in the extent (multi_object_manipulation.py:97-136); a
+        # round cap is a diagnostic option only (objects.drop.max_rounds: stop there, or with
+        # objects.drop.place_remaining place the rest upright above the extent centre)
+        mr = _get(cfg, "objects.drop.max_rounds", None)
+        self.max_drop_rounds = None if mr is None else int(mr)
+        self.max_drop_rounds_place = bool(_get(cfg, "objects.drop.place_remaining", False))
         self._stat_pending = 0
         self._stat_folded = 0
         self._success_rate_ewma = 0.0
@@ -409,8 +413,7 @@ class Ur5SihMultiObjectManipulation:
             rounds = 0
             while not bool(in_bin.all()):
                 if rounds == self.max_drop_rounds and self.max_drop_rounds_place:
-                    # the reference loops until every object lands in the bin extent; cap it so a
-                    # rolling object cannot stall initialisation (remaining objects stay where they are)
+                    # diagnostic option (not the reference's behaviour): place the remaining objects
                     print(f"[handarm_hip] drop init: {int((~in_bin).sum())} objects outside the bin extent after "
                           f"{rounds} rounds; placing them upright above the bin centre", file=sys.stderr, flush=True)
                     bad = (~in_bin).nonzero(as_tuple=False)
@@ -441,7 +444,11 @@ class Ur5SihMultiObjectManipulation:
                             rf = torch_rand_float(-1.0, 1.0, (len(env_ids), 2), device=self.device)
                             rs[env_ids, i, 3:7] = randomize_rotation(rf[:, 0], rf[:, 1])
                         rs[env_ids, i, 7:13] = 0.0
-                        self.sim.simulate(self.task_cfg["drop_num_steps"])
+                        # the reference steps every env here; only the envs dropping object i are stepped (the
+                        # others have nothing in flight, and all envs settle together below): later rounds,
+                        # which re-drop a handful of objects, cost a handful of envs instead of the shard
+                        self.sim.simulate(self.task_cfg["drop_num_steps"],
+                                          env_ids=env_ids if len(env_ids) < N else None)
                 obj_pos = rs[:, :, 0:3]
                 in_bin = ((obj_pos >= bin_lo) & (obj_pos <= bin_hi)).all(-1)
             for _ in range(600):                                                    # settle

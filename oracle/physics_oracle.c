@@ -344,7 +344,7 @@ static void hull_plane(const ha_model_t* m, int hull, int k, pose_t P, const flo
 
 /* reduce candidate list (points, sep) to <= 4 contacts; returns count appended. The area criterion measures
    about normal n, or (per-candidate normals nrm, compound objects) about the deepest candidate's normal. */
-static int reduce_manifold(const v3* pts, const float* seps, int nc, v3 n, const v3* nrm, int* out_idx) {
+static int reduce_manifold(const v3* pts, const float* seps, int nc, v3 n, const v3* nrm, float window, int* out_idx) {
     if (nc <= 0) return 0;
     int i0 = 0;
     for (int i = 1; i < nc; i++)
@@ -352,9 +352,11 @@ static int reduce_manifold(const v3* pts, const float* seps, int nc, v3 n, const
     out_idx[0] = i0;
     if (nrm) n = nrm[i0];
     if (nc == 1) return 1;
+    float lim = seps[i0] + window;      /* points 2-4: within the window of the deepest point */
     int i1 = -1;
     float best = 1e-12f;
     for (int i = 0; i < nc; i++) {
+        if (seps[i] > lim) continue;
         v3 d = sub(pts[i], pts[i0]);
         float dd = dot(d, d);
         if (dd > best) { best = dd; i1 = i; }
@@ -365,6 +367,7 @@ static int reduce_manifold(const v3* pts, const float* seps, int nc, v3 n, const
     int i2 = -1, i3 = -1;
     float bmax = 1e-12f, bmin = -1e-12f;
     for (int i = 0; i < nc; i++) {
+        if (seps[i] > lim) continue;
         float s = dot(crs(e, sub(pts[i], pts[i0])), n);
         if (s > bmax) { bmax = s; i2 = i; }
         if (s < bmin) { bmin = s; i3 = i; }
@@ -381,6 +384,7 @@ static int reduce_manifold(const v3* pts, const float* seps, int nc, v3 n, const
    pair's reduced points collect in a per-thread buffer (at most MAXGATHER, later ones dropped) and the object
    pair then emits ONE manifold of <= 4 points chosen from them, each keeping its piece pair's normal. */
 static __thread int g_on, g_n;
+static __thread float g_window;     /* ha_params_t.manifold_window of the running detect() */
 static __thread v3 g_pt[MAXGATHER], g_nrm[MAXGATHER];
 static __thread float g_sep[MAXGATHER];
 
@@ -403,7 +407,7 @@ static void store_points(contact_t* out, int* nout, int maxout, const v3* pts, c
 }
 static int emit(contact_t* out, int* nout, int maxout, v3* pts, float* seps, int nc, v3 n, int a, int b) {
     int idx[4];
-    int k = reduce_manifold(pts, seps, nc, n, NULL, idx);
+    int k = reduce_manifold(pts, seps, nc, n, NULL, g_window, idx);
     if (g_on) {
         for (int i = 0; i < k && g_n < MAXGATHER; i++, g_n++) {
             g_pt[g_n] = pts[idx[i]]; g_sep[g_n] = seps[idx[i]]; g_nrm[g_n] = n;
@@ -417,7 +421,7 @@ static void gather_begin(void) { g_on = 1; g_n = 0; }
 static void gather_end(contact_t* out, int* nout, int maxout, int a, int b) {
     int idx[4];
     g_on = 0;
-    int k = reduce_manifold(g_pt, g_sep, g_n, V(0, 0, 0), g_nrm, idx);
+    int k = reduce_manifold(g_pt, g_sep, g_n, V(0, 0, 0), g_nrm, g_window, idx);
     store_points(out, nout, maxout, g_pt, g_sep, g_nrm, V(0, 0, 0), idx, k, a, b);
 }
 
@@ -521,6 +525,7 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
     const ha_params_t* p = &h->p;
     int nout = 0;
     float mg = p->contact_margin;
+    g_window = p->manifold_window;
     for (int o = 0; o < h->NO; o++) {
         if (!e->coll[o]) continue;
         int pa = e->pool[o];
@@ -697,7 +702,8 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
         R.contact[r] = c;
         if (k == 0) {
             float s = cs[c].sep;
-            float vt = s > 0 ? -s / hdt : -p->baumgarte * s / hdt;
+            float sb = s + p->contact_slop < 0.0f ? s + p->contact_slop : 0.0f;   /* penetration beyond the slop */
+            float vt = s > 0 ? -s / hdt : -p->baumgarte * sb / hdt;
             if (vt > p->max_depen_vel) vt = p->max_depen_vel;
             R.vt[r] = vt; R.lo[r] = 0; R.hi[r] = 3.0e38f; R.fric_of[r] = -1;
         } else {

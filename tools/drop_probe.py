@@ -40,3 +40,20 @@ for e, o in bad[:40]:
 from collections import Counter
 print("by object:", Counter(pool[idx[e, o]] for e, o in bad).most_common())
 print("by axis:", Counter(tuple(k for k in range(3) if pos[e, o, k] < lo[k] or pos[e, o, k] > hi[k]) for e, o in bad))
+
+# --settle K: step K more physics calls and follow the objects that were outside (do they come to rest?)
+if "--settle" in sys.argv:
+    K = int(sys.argv[sys.argv.index("--settle") + 1])
+    track = [(int(e), int(o)) for e, o in bad]
+    for k in range(K // 100):
+        env.sim.simulate(100)
+        torch.cuda.synchronize()
+        rs2 = env.root_state.view(n, A, 13)[:, a0:a0 + no].cpu().numpy()
+        sp = np.array([np.linalg.norm(rs2[e, o, 7:10]) for e, o in track])
+        allsp = np.linalg.norm(rs2[..., 7:10], axis=-1)
+        print(f"settle +{100 * (k + 1)}: tracked speed median {np.median(sp):.4f} max {sp.max():.4f}; all objects "
+              f"speed p99 {np.percentile(allsp, 99):.4f} max {allsp.max():.4f}, >0.01: {int((allsp > 0.01).sum())}",
+              flush=True)
+    for e, o in track[:12]:
+        print(f"  env {e} obj {o} {pool[idx[e, o]]:22s} pos {np.round(rs2[e, o, 0:3], 3)} "
+              f"quat {np.round(rs2[e, o, 3:7], 3)} vel {np.round(rs2[e, o, 7:13], 3)}")
