@@ -398,9 +398,9 @@ def run_config(task, envs, args, world, rank, device, log_interval_fn):
     else:
         parallel.reduce_episode_stats(env)
         extra["success_rate_ewma"] = env.log_data.get("success_rate_ewma/overall")
-        cs = env.contact_stats() if hasattr(env, "contact_stats") else None
-        if cs is not None:
-            extra["contacts"] = cs
+    cs = env.contact_stats() if hasattr(env, "contact_stats") else None
+    if cs is not None:
+        extra["contacts"] = cs
     kernel = STEP_KERNEL[task]
     kavg = statistics.mean(kern_ms) if kern_ms else float("nan")
     bytes_env = bytes_per_env_step(task, env, args)

@@ -411,6 +411,8 @@ int ha_task_reset(ha_handle h, uint32_t flags, void* stream);
  * N x num_obs floats) = clamp(obs, -clip_obs, clip_obs); AllegroKuka only: scalars (if non-null, 4 floats) =
  * mean prev_episode_successes, mean / min / max true_objective over the shard. */
 int ha_task_epilogue(ha_handle h, float* obs_out, float clip_obs, float* scalars, void* stream);
+/* v9: contacts per substep the handle's kernel family holds (over it, the shallowest give way) */
+int ha_contact_capacity(ha_handle h);
 /* last kernel time in ms measured with HIP events around the most recent physics/step launch (-1 if none) */
 float ha_last_kernel_ms(ha_handle h);
 /* per-launch HIP-event timing of the env kernel (bench roofline): record up to max_launches launches

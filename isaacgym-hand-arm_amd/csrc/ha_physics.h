@@ -22,7 +22,9 @@
 #define NOBJ HA_MAX_OBJ
 #define MAXD 24
 #define HA_ND 17         /* DOF count the kernels are compiled for (UR5 + SIH); checked by ha_create */
-#define MAXB 48          /* rigid bodies per env (contact-force rows): robot links + objects + statics */
+// compound object pair: reduced points gathered over its piece pairs (later ones dropped; the oracle's MAXGATHER)
+#define HA_MAX_GATHER 32
+#define MAXB 44          /* rigid bodies per env (contact-force rows): robot links + objects + statics (bin scene: 44) */
 #define MAXV 72          /* generalized velocity coordinates D + 6 x objects (17 + 6 x 8 = 65 for bin-picking) */
 
 // What the task observables read after refresh_simulation_tensors(): flange pose, fingertip states,
@@ -44,7 +46,7 @@ struct ColScratch {
     float wpA[128][4], wpB[128][4];     // world face planes (n, d) of both hulls
     int cand[64];                       // clipping: candidate incident vertices
     int cmax[64];                       // clipping: per-candidate max plane distance (order-preserving int)
-    float gp[64][4], gn[64][4];         // compound object pair: gathered points (x, sep) and their normals
+    float gp[HA_MAX_GATHER][4], gn[HA_MAX_GATHER][4];   // compound object pair: gathered points (x, sep), normals
 };
 struct RowScratch {
     float J[MAXR * RS];
@@ -144,9 +146,11 @@ __host__ __device__ inline size_t obj_lds_offset_rows(size_t rows) {
 #ifndef HA_SPLIT_ABOVE_OCAP
 #define HA_SPLIT_ABOVE_OCAP 2   /* families with more object slots use split rows (Ur5Sih 3 objects, clutter) */
 #endif
-template <int ND, int OCAP, int NCH, int KL = 8, int LCH = NCH>
+template <int ND, int OCAP, int NCH, int KL = 8, int LCH = NCH, int CAP = MAXC>
 struct PhysCfg {
     static constexpr int nd = ND, ocap = OCAP, nch = NCH;
+    // contacts per chunk: MAXC, or fewer for a one-chunk family on dense rows (its rows and list shrink with it)
+    static constexpr int cap = CAP;
     static constexpr int vw = ND + 6 * OCAP > 64 ? 2 : 1;
 #ifdef HA_DENSE_ROWS    /* diagnostic build (tools/split_rows_check.py): every family on dense rows */
     static constexpr bool split = false;
@@ -166,6 +170,7 @@ struct PhysCfg {
     static_assert(split || MAXC * NCH <= 64, "dense rows: <= 64 contacts (one ballot)");
     static_assert(lch >= 1 && lch <= NCH, "LDS row chunks");
     static_assert(MAXC * NCH <= HA_MAX_CONTACTS, "contact capacity exceeds HA_MAX_CONTACTS");
+    static_assert(CAP == MAXC || (NCH == 1 && !split && CAP >= 1 && CAP < MAXC), "reduced capacity: one dense chunk");
 };
 // bytes of the constraint rows proper, then (several contact chunks only) the per-row PGS constants of every
 // chunk (impulse, target velocity, 1/diag, friction, two Delassus entries: 6 floats x MAXR x chunks), which the
@@ -173,7 +178,7 @@ struct PhysCfg {
 template <class PC>
 __host__ __device__ constexpr size_t pc_rowdata_bytes() {
     return PC::split ? 2 * sizeof(float) * ((size_t)MAXR * PC::lch * 12 + 3 * (size_t)PC::kl * PC::nd)
-                     : 2 * sizeof(float) * (size_t)MAXR * PC::nch * row_stride<PC::nd>();
+                     : 2 * sizeof(float) * (size_t)3 * PC::cap * PC::nch * row_stride<PC::nd>();
 }
 template <class PC>
 __host__ __device__ constexpr size_t pc_rows_bytes() {
@@ -187,7 +192,7 @@ __host__ __device__ inline size_t contact_lds_offset() {
 }
 template <class PC>
 __host__ __device__ inline size_t task_lds_bytes() {
-    return contact_lds_offset<PC>() + (size_t)MAXC * PC::nch * sizeof(ContactLDS);
+    return contact_lds_offset<PC>() + (size_t)PC::cap * PC::nch * sizeof(ContactLDS);
 }
 
 struct SimCtx {
@@ -598,7 +603,7 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
             int ng = s.ng;
 #pragma unroll
             for (int t = 0; t < 4; t++) {
-                if (t < k && ng < 64) {
+                if (t < k && ng < HA_MAX_GATHER) {
                     st3(cs.gp[ng], P[t]);
                     cs.gp[ng][3] = S[t];
                     st3(cs.gn[ng], N[t]);
@@ -1184,7 +1189,7 @@ HD void substep(SimCtx& c, float hdt) {
     //      of contact MAXC ch + r / 3). Rows are packed with the task's stride (J then Y), so a one-object task
     //      needs less LDS (row_stride, task_lds_bytes)
     float* Jb = s.u.rows.J;
-    float* Yb = Jb + MAXR * NCH * RSN;
+    float* Yb = Jb + 3 * PC::cap * NCH * RSN;
     int nc = s.nc;
     int nr = 3 * nc;    // nc <= MAXC x NCH -> <= MAXR x NCH rows
     // split rows (PhysCfg): object blocks of every row (OW = 12 wide, J then Y), then the robot blocks of the

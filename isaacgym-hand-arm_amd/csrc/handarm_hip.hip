@@ -56,10 +56,37 @@ __host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5S
 #ifndef HA_WAVES_PER_EU
 #define HA_WAVES_PER_EU 3
 #endif
+// AllegroKuka / AllegroHand (one dense chunk): contacts per substep, and waves per SIMD asked of their
+// register allocation. 12 contacts put the env block at 13.6 KB of LDS and 3 waves per SIMD cap the kernels at
+// 168 VGPRs (84 / 72 B/lane scratch), so 12 workgroups run per CU instead of 8 (LDS 20.1 / 16.6 KB, 193
+// VGPRs): C2 0.705 -> 0.652 ms, C3 3.23 -> 2.70 ms (tools/ab_variants.sh). The list is then over capacity in
+// 1.3% (C2) / 2.0% (C3) of substeps, where the shallowest contacts give way (bench contact_stats).
+#ifndef HA_AK_CONTACTS
+#define HA_AK_CONTACTS 12
+#endif
+#ifndef HA_AH_CONTACTS
+#define HA_AH_CONTACTS 12
+#endif
+#ifndef HA_AK_WAVES_PER_EU
+#define HA_AK_WAVES_PER_EU 3
+#endif
+#ifndef HA_AH_WAVES_PER_EU
+#define HA_AH_WAVES_PER_EU 3
+#endif
+template <int FAM>
+__host__ __device__ constexpr int task_chunk_capacity() {
+    return FAM == HA_TASK_ALLEGRO_KUKA ? HA_AK_CONTACTS : (FAM == HA_TASK_ALLEGRO_HAND ? HA_AH_CONTACTS : MAXC);
+}
+template <int FAM>
+__host__ __device__ constexpr int task_waves_per_eu() {
+    return FAM == HA_TASK_UR5SIH ? HA_WAVES_PER_EU
+           : (FAM == HA_TASK_ALLEGRO_KUKA ? HA_AK_WAVES_PER_EU : (FAM == HA_TASK_ALLEGRO_HAND ? HA_AH_WAVES_PER_EU : 1));
+}
 template <int FAM>
 using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>(),
                         FAM == FAM_UR5SIH_CLUTTER ? HB_LINK_SLOTS : HA_LINK_SLOTS,
-                        FAM == FAM_UR5SIH_CLUTTER ? HB_LDS_CHUNKS : task_contact_chunks<FAM>()>;
+                        FAM == FAM_UR5SIH_CLUTTER ? HB_LDS_CHUNKS : task_contact_chunks<FAM>(),
+                        task_chunk_capacity<FAM>()>;
 
 
 // ----------------------------------------------------------------------------- state load/store
@@ -317,7 +344,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.o = reinterpret_cast<ObjLDS*>(smem + obj_lds_offset<PC>());
     c.k = reinterpret_cast<ContactLDS*>(smem + contact_lds_offset<PC>());
     c.spill = PC::split ? spill + (size_t)env * PC::spill_floats : nullptr;
-    c.maxc = MAXC * NCH;
+    c.maxc = PC::cap * NCH;
     c.lane = threadIdx.x;
     c.D = ND;                     // == model->n_dofs (ha_create); a constant, so loops over D unroll
     c.NO = params->n_objects;
@@ -420,7 +447,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
 
 #define HA_KERNEL(name, FAM, MODE)                                                                              \
     extern "C" __global__ void __launch_bounds__(64)                                                          \
-        __attribute__((amdgpu_waves_per_eu(FAM == HA_TASK_UR5SIH ? HA_WAVES_PER_EU : 1)))                       \
+        __attribute__((amdgpu_waves_per_eu(task_waves_per_eu<FAM>())))                                        \
         name(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params, ha_state_t st,       \
              int num_envs, int n_calls, uint32_t flags, int stat_slot, float* spill, const int32_t* env_ids) {  \
         env_body<FAM, MODE>(model, params, st, num_envs, n_calls, flags, stat_slot, spill, env_ids);           \
@@ -584,6 +611,16 @@ static size_t lds_bytes(int fam) {
         case HA_TASK_ALLEGRO_HAND: return fam_lds_bytes<HA_TASK_ALLEGRO_HAND>();
         case HA_TASK_ALLEGRO_KUKA: return fam_lds_bytes<HA_TASK_ALLEGRO_KUKA>();
         default: return fam_lds_bytes<HA_TASK_UR5SIH>();
+    }
+}
+template <int FAM>
+static int fam_contacts() { return FamPhys<FAM>::cap * FamPhys<FAM>::nch; }
+static int contact_capacity(int fam) {
+    switch (fam) {
+        case FAM_UR5SIH_CLUTTER: return fam_contacts<FAM_UR5SIH_CLUTTER>();
+        case HA_TASK_ALLEGRO_HAND: return fam_contacts<HA_TASK_ALLEGRO_HAND>();
+        case HA_TASK_ALLEGRO_KUKA: return fam_contacts<HA_TASK_ALLEGRO_KUKA>();
+        default: return fam_contacts<HA_TASK_UR5SIH>();
     }
 }
 static int task_row_stride(int task) {
@@ -1046,6 +1083,8 @@ int ha_render_camera(ha_handle h, const ha_camera_t* cam, const float* view_inv,
     }
     return HA_OK;
 }
+
+int ha_contact_capacity(ha_handle h) { return h ? contact_capacity(h->fam) : HA_E_ARG; }
 
 float ha_last_kernel_ms(ha_handle h) {
     if (!h || !h->timed) return -1.0f;

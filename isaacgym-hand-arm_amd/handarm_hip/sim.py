@@ -45,8 +45,6 @@ class HandArmSim:
         self.num_actors = self.model.n_actors
         self.num_bodies = self.model.n_bodies
         self.stats_ring = stats_ring
-        # contacts per substep the kernel family holds (ha_physics.h MAXC x chunks: 84 for the clutter family)
-        self.contact_capacity = 84 if (self.task == HM.TASK_UR5SIH and self.params.n_objects > 3) else 21
         spec = HM.state_spec(num_envs, n_links=self.num_links, n_dofs=self.num_dofs, n_obj=self.n_obj,
                              num_initial_poses=self.params.num_initial_poses, num_actions=self.params.num_actions,
                              num_obs=self.params.num_obs, n_actors=self.num_actors, n_bodies=self.num_bodies)
@@ -70,6 +68,8 @@ class HandArmSim:
         h = C.c_void_p()
         _lib.check(self.lib.ha_create(C.byref(self.model), C.byref(self.params), num_envs, C.byref(h)), "ha_create")
         self.h = h
+        # contacts per substep the kernel family holds (clutter 84, Ur5Sih 21, AllegroKuka / AllegroHand 12)
+        self.contact_capacity = int(self.lib.ha_contact_capacity(self.h))
         self.state = HM.HaState()
         null = HM.null_fields(task)
         for k in HM.STATE_FIELDS:

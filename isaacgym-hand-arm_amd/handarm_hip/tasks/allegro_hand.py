@@ -98,6 +98,10 @@ class AllegroHand:
         self.total_successes = 0
         self.total_resets = 0
 
+    def contact_stats(self, reset=False):
+        """Contact-list diagnostics of the physics since the last reset (HandArmSim.contact_stats)."""
+        return self.sim.contact_stats(reset)
+
     # ---------------------------------------------------------------- VecTask surface
     @property
     def num_envs(self):

@@ -139,6 +139,10 @@ class AllegroKuka:
             self._rr = RR.KukaDraws(N, sub, tuple(self.tcfg["force_prob_range"]), float(self.tcfg["force_scale"]))
             self.random_force_prob.copy_(self._rr.prob.to(sim_device))
 
+    def contact_stats(self, reset=False):
+        """Contact-list diagnostics of the physics since the last reset (HandArmSim.contact_stats)."""
+        return self.sim.contact_stats(reset)
+
     # ---------------------------------------------------------------- VecTask surface
     @property
     def num_envs(self):

@@ -379,7 +379,7 @@ static int reduce_manifold(const v3* pts, const float* seps, int nc, v3 n, const
 }
 
 #define MAXCAND 128
-#define MAXGATHER 64
+#define MAXGATHER 32     /* ha_physics.h HA_MAX_GATHER */
 /* Compound objects (several convex pieces, ha_model_t v8): between gather_begin and gather_end every piece
    pair's reduced points collect in a per-thread buffer (at most MAXGATHER, later ones dropped) and the object
    pair then emits ONE manifold of <= 4 points chosen from them, each keeping its piece pair's normal. */
@@ -925,7 +925,9 @@ hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int nu
     h->A = model->n_actors;
     h->D = model->n_dofs;
     h->B = model->n_bodies;
-    h->maxc = (params->task == HA_TASK_UR5SIH && params->n_objects > 3) ? 4 * 21 : 21;   /* handarm_hip.hip HB_CHUNKS */
+    /* the device family's capacity (ha_contact_capacity): clutter 4 chunks of 21 (handarm_hip.hip HB_CHUNKS),
+       Ur5Sih 21, AllegroKuka / AllegroHand 12 (HA_AK_CONTACTS / HA_AH_CONTACTS) */
+    h->maxc = params->task == HA_TASK_UR5SIH ? (params->n_objects > 3 ? 4 * 21 : 21) : 12;
     return h;
 }
 void hao_destroy(hao_handle h) { free(h); }
