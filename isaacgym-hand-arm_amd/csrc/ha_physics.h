@@ -1091,6 +1091,9 @@ template <class PC>
 HD void substep(SimCtx& c, float hdt) {
     constexpr int ND = PC::nd, NCH = PC::nch, VW = PC::vw;
     constexpr int RSN = row_stride<ND>();
+    // the lane id goes through an opaque move each substep: the per-lane 64-bit model addresses are then
+    // recomputed here (one or two VALU ops) instead of being hoisted out of the substep loop and spilled
+    asm volatile("" : "+v"(c.lane));
     PROF_BEGIN();
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;

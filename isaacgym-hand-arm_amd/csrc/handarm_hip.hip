@@ -320,6 +320,14 @@ static_assert(HA_ND + 6 * HA_MAX_OBJ <= MAXV, "bin-picking (8 objects) must fit 
 // One kernel per (task, mode) (one workgroup = one wavefront = one env): each is compiled with only its
 // own path, which keeps every kernel's code small, gives the DOF count to the compiler as a constant, and
 // gives the profiler a distinct name per kernel.
+// After the physics the env index and lane id are re-derived through an opaque move, so the per-lane 64-bit
+// tensor addresses load_env computed are recomputed by store_env / the task epilogue instead of being kept
+// live (spilled to scratch: 8 B per lane each) across the whole physics
+__device__ __forceinline__ void after_physics(SimCtx& c, int& env) {
+    asm volatile("" : "+s"(env));
+    asm volatile("" : "+v"(c.lane));
+}
+
 template <int FAM, int MODE>
 __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params,
                                          const ha_state_t& st, int num_envs, int n_calls, uint32_t flags,
@@ -380,6 +388,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     load_env(c, S, env, MODE == MODE_SIMULATE);
     if (MODE == MODE_SIMULATE) {
         run_physics<PC>(c, n_calls);
+        after_physics(c, env);
         store_env(c, S, env);
         return;
     }
@@ -399,6 +408,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
         ak_forces(c, S, env, flags, tsv);
         if (c.lane < AK_TS_KP) tsg[c.lane] = tsv;
         if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<PC>(c, c.p->control_freq_inv);   // vec_task.py:409-412
+        after_physics(c, env);
         store_env(c, S, env);
         if (c.lane == 0) S.progress_buf[env] = S.progress_buf[env] + 1;                // allegro_kuka_base.py:1429
         ak_in_from_lds(c, &akp.in);
@@ -415,6 +425,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
         }
         ah_controller(c, S, env);
         if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<PC>(c, c.p->control_freq_inv);   // vec_task.py:409-412
+        after_physics(c, env);
         store_env(c, S, env);
         if (c.lane == 0) S.progress_buf[env] = S.progress_buf[env] + 1;                // allegro_hand.py:629
         ah_in_from_lds(c, &ain);
@@ -424,6 +435,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     if (MODE == MODE_RESET) {
         task_reset(c, S, env, flags);
         if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<PC>(c, 1);
+        after_physics(c, env);
         task_reset_finish(c, S, env);
         store_env(c, S, env);
         return;
@@ -438,6 +450,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     // a single copy of the physics code.
     for (int ph = do_reset ? 0 : 1; ph < 2; ph++) {
         if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<PC>(c, ph == 0 ? 1 : c.p->control_freq_inv);
+        after_physics(c, env);
         if (ph == 0) task_reset_finish(c, S, env);
     }
     store_env(c, S, env);
