@@ -39,7 +39,7 @@ struct ObsIn {
 
 struct DynScratch {
     float Ic[HA_MAX_LINKS][13];                 // composite spatial inertia (m, h, J) at world origin
-    float Vl[HA_MAX_LINKS][6], Al[HA_MAX_LINKS][6], Fl[HA_MAX_LINKS][6];
+    float Al[HA_MAX_LINKS][6], Fl[HA_MAX_LINKS][6];
 };
 struct ColScratch {
     float wvA[64][4], wvB[64][4];       // world vertices of both hulls
@@ -52,15 +52,25 @@ struct RowScratch {
     float J[MAXR * RS];
     float Y[MAXR * RS];
 };
-// dynamics (M + spatial scratch) and, after the last substep, the refresh/observation staging. cforce is
-// written after each substep's PGS (nothing overlaps it until the next substep's rows phase).
+// Dynamics (M + spatial scratch) and, after the physics, the refresh / observation staging, which overlap:
+// the staging and the last substep's joint / contact forces (written after each substep's PGS) are only read
+// after the last substep, and the next substep's dynamics may overwrite them. The link twists Vl are written
+// by the dynamics and again by the refresh (link_twists), and read by the observation staging, so they stay
+// outside the overlap.
 struct PostScratch {
-    float M[MAXD * MAXD];                       // M, then its Cholesky factor L (stride D)
-    DynScratch dyn;
-    ObsIn in;
-    float obs[216];                             // Ur5Sih: 108 + 13 x objects (212 at 8 objects)
-    float cforce[MAXB][3];
-    float dforce[MAXD];                         // joint force of the last substep (drive + limits) / h
+    float Vl[HA_MAX_LINKS][6];                  // link twists (w, v at the world origin)
+    union {
+        struct {
+            float M[MAXD * MAXD];               // M, then its Cholesky factor L (stride D)
+            DynScratch dyn;
+        };
+        struct {
+            ObsIn in;
+            float obs[216];                     // Ur5Sih: 108 + 13 x objects (212 at 8 objects)
+            float cforce[MAXB][3];
+            float dforce[MAXD];                 // joint force of the last substep (drive + limits) / h
+        };
+    };
 };
 
 // One free object's state (LDS). These live after the EnvLDS block, one per object slot of the task
@@ -168,7 +178,7 @@ struct PhysCfg {
     static_assert(!split || (KL >= 0 && KL <= MAXC * NCH), "LDS link slots must not exceed the contact capacity");
     static_assert(!split || (row_slots<ND>() == 2 && MAXC * NCH <= 128), "split rows: two object slots, <= 128 contacts");
     static_assert(split || MAXC * NCH <= 64, "dense rows: <= 64 contacts (one ballot)");
-    static_assert(lch >= 1 && lch <= NCH, "LDS row chunks");
+    static_assert(lch >= 0 && lch <= NCH, "LDS row chunks");
     static_assert(MAXC * NCH <= HA_MAX_CONTACTS, "contact capacity exceeds HA_MAX_CONTACTS");
     static_assert(CAP == MAXC || (NCH == 1 && !split && CAP >= 1 && CAP < MAXC), "reduced capacity: one dense chunk");
 };
@@ -353,7 +363,7 @@ HD void dynamics(SimCtx& c) {
         for (int k = 0; k < 9; k++) ic[4 + k] = I.J[k];
         if (i == 0) {
 #pragma unroll
-            for (int k = 0; k < 6; k++) { s.u.pd.dyn.Vl[0][k] = 0.f; s.u.pd.dyn.Al[0][k] = 0.f; }
+            for (int k = 0; k < 6; k++) { s.u.pd.Vl[0][k] = 0.f; s.u.pd.dyn.Al[0][k] = 0.f; }
         }
     }
     // zero M
@@ -373,7 +383,7 @@ HD void dynamics(SimCtx& c) {
     for (int lev = 1; lev <= m.max_level; lev++) {
         if (my_lev == lev) {
             int i = lane, par = my_par, d = my_d;
-            f3 vw = ld3(&s.u.pd.dyn.Vl[par][0]), vv = ld3(&s.u.pd.dyn.Vl[par][3]);
+            f3 vw = ld3(&s.u.pd.Vl[par][0]), vv = ld3(&s.u.pd.Vl[par][3]);
             f3 aw = ld3(&s.u.pd.dyn.Al[par][0]), av = ld3(&s.u.pd.dyn.Al[par][3]);
             if (d >= 0) {
                 f3 sw = my_sw, sv = my_sv;
@@ -382,14 +392,14 @@ HD void dynamics(SimCtx& c) {
                 aw = aw + cross3(vw, sw);
                 av = av + (cross3(vw, sv) + cross3(vv, sw));
             }
-            st3(&s.u.pd.dyn.Vl[i][0], vw); st3(&s.u.pd.dyn.Vl[i][3], vv);
+            st3(&s.u.pd.Vl[i][0], vw); st3(&s.u.pd.Vl[i][3], vv);
             st3(&s.u.pd.dyn.Al[i][0], aw); st3(&s.u.pd.dyn.Al[i][3], av);
         }
         wsync();
     }
     if (own) {
         int i = lane;
-        f3 vw = ld3(&s.u.pd.dyn.Vl[i][0]), vv = ld3(&s.u.pd.dyn.Vl[i][3]);
+        f3 vw = ld3(&s.u.pd.Vl[i][0]), vv = ld3(&s.u.pd.Vl[i][3]);
         f3 aw = ld3(&s.u.pd.dyn.Al[i][0]), av = ld3(&s.u.pd.dyn.Al[i][3]);
         f3 n1, f1, n2, f2;
         inert_apply(I, aw, av, n1, f1);

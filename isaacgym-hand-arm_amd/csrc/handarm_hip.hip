@@ -37,8 +37,11 @@ __host__ __device__ constexpr int task_obj_capacity() {
 #ifndef HB_CHUNKS
 #define HB_CHUNKS 4
 #endif
-#ifndef HB_LDS_CHUNKS       /* clutter chunks whose object-block rows stay in LDS; the rest go to the global area */
-#define HB_LDS_CHUNKS 1
+// clutter chunks whose object-block rows stay in LDS (0..4); the rest go to the env's global row area, which the
+// PGS reads one contact ahead. 0: env block 16.8 KB, 9 workgroups per CU (1: 22.0 KB, 7 per CU): C5 shard
+// 23.0 -> 19.5 ms (tools/ab_variants.sh binpick)
+#ifndef HB_LDS_CHUNKS
+#define HB_LDS_CHUNKS 0
 #endif
 template <int FAM>
 __host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5SIH_CLUTTER ? HB_CHUNKS : 1; }
@@ -47,12 +50,14 @@ __host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5S
 #ifndef HB_LINK_SLOTS
 #define HB_LINK_SLOTS 2
 #endif
-#ifndef HA_LINK_SLOTS   /* the Ur5Sih 3-object family's LDS link slots (split rows, HA_SPLIT_ABOVE_OCAP) */
-#define HA_LINK_SLOTS 8
+// the Ur5Sih 3-object family's LDS link slots (split rows, HA_SPLIT_ABOVE_OCAP): 4 put the env block at 13.5 KB,
+// 12 workgroups per CU (8 slots: 15.1 KB, 10 per CU): C4 shard 5.24 -> 5.01 ms; more link contacts use the
+// global spill rows (tests/test_gpu_parity.py::test_link_contacts_spill_rows_match_oracle)
+#ifndef HA_LINK_SLOTS
+#define HA_LINK_SLOTS 4
 #endif
-// minimum waves per SIMD asked of the Ur5Sih (3-object) kernels' register allocation: 3 (168 VGPRs, 72 B/lane
-// scratch) with split rows (15.1 KB LDS) runs 10 workgroups per CU instead of 8: C4 shard 5.01 -> 4.88 ms
-// (tools/ab_variants.sh ur5sih; 1 = the compiler's choice, 191 VGPRs)
+// minimum waves per SIMD asked of the Ur5Sih (3-object) kernels' register allocation: 3 (<= 168 VGPRs; 149
+// without spills now) so the VGPRs allow the 12 workgroups per CU the LDS does
 #ifndef HA_WAVES_PER_EU
 #define HA_WAVES_PER_EU 3
 #endif
@@ -132,24 +137,24 @@ __device__ void load_env(SimCtx& c, const ha_state_t& st, int env, bool take_for
     wsync();
 }
 
-// link twists into s.u.pd.dyn.Vl (level-synchronous); needs fk()
+// link twists into s.u.pd.Vl (level-synchronous); needs fk()
 __device__ void link_twists(SimCtx& c) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     int lane = c.lane, L = c.L;
-    if (lane == 0) for (int k = 0; k < 6; k++) s.u.pd.dyn.Vl[0][k] = 0.f;
+    if (lane == 0) for (int k = 0; k < 6; k++) s.u.pd.Vl[0][k] = 0.f;
     wsync();
     for (int lev = 1; lev <= m.max_level; lev++) {
         if (lane < L && m.link_level[lane] == lev) {
             int i = lane, par = m.link_parent[i], d = m.link_dof[i];
-            f3 vw = ld3(&s.u.pd.dyn.Vl[par][0]), vv = ld3(&s.u.pd.dyn.Vl[par][3]);
+            f3 vw = ld3(&s.u.pd.Vl[par][0]), vv = ld3(&s.u.pd.Vl[par][3]);
             if (d >= 0) {
                 f3 axd = ld3(s.ax[d]);
                 vw = vw + axd * s.qd[d];
                 vv = vv + cross3(ld3(s.an[d]), axd) * s.qd[d];
             }
-            st3(&s.u.pd.dyn.Vl[i][0], vw);
-            st3(&s.u.pd.dyn.Vl[i][3], vv);
+            st3(&s.u.pd.Vl[i][0], vw);
+            st3(&s.u.pd.Vl[i][3], vv);
         }
         wsync();
     }
@@ -162,10 +167,10 @@ __device__ float link_state(const SimCtx& c, int i, int k) {
     if (k < 7) return s.lq[i][k - 3];
     if (k < 10) {
         f3 cc = ld3(s.lp[i]) + qrot(ldq(s.lq[i]), ld3(c.m->link_com[i]));
-        f3 lin = ld3(&s.u.pd.dyn.Vl[i][3]) + cross3(ld3(&s.u.pd.dyn.Vl[i][0]), cc);
+        f3 lin = ld3(&s.u.pd.Vl[i][3]) + cross3(ld3(&s.u.pd.Vl[i][0]), cc);
         return k == 7 ? lin.x : (k == 8 ? lin.y : lin.z);
     }
-    return s.u.pd.dyn.Vl[i][k - 10];        // angular velocity: Vl = (w, v at the world origin)
+    return s.u.pd.Vl[i][k - 10];        // angular velocity: Vl = (w, v at the world origin)
 }
 // root-state row k of object o (origin pose, not COM) from LDS
 __device__ float object_state(const SimCtx& c, int o, int k) {
@@ -180,7 +185,7 @@ __device__ float object_state(const SimCtx& c, int o, int k) {
 }
 
 // writes dof_state, dof_force, sim targets, object root states, rigid_body_state and net_contact_force
-// (the refresh_* tensors). Leaves the link twists in s.u.pd.dyn.Vl for the task's observation snapshot.
+// (the refresh_* tensors). Leaves the link twists in s.u.pd.Vl for the task's observation snapshot.
 __device__ void store_env(SimCtx& c, const ha_state_t& st, int env) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;

@@ -115,9 +115,9 @@ def test_bin_simulate_matches_oracle_bit_for_bit(seed, calls):
 
 def test_bin_link_contacts_spill_rows_match_oracle():
     """Three objects placed on hand link hulls: more robot-link contacts per env than the clutter kernel's 2 LDS
-    link slots (HB_LINK_SLOTS), so the split rows' global spill area (PhysCfg::split) carries part of the robot blocks, while
-    the contact list stays below capacity. Bit-identical to the C oracle on every env, like the single-call test. (tools/split_rows_check.py checks this scene bit for bit against a
-    dense-row build.)"""
+    link slots (HB_LINK_SLOTS), so the split rows' global spill area (PhysCfg::split) carries part of the robot
+    blocks, while the contact list stays below capacity. Bit-identical to the C oracle on every env, like the
+    single-call test. (tools/split_rows_check.py checks this scene bit for bit against a dense-row build.)"""
     n = 64
     sim, orc, st = _bin_oracle_and_sim(n, 3)
     sim.simulate(1)                  # link poses of this scene (rigid_body_state rows of the robot)

@@ -174,6 +174,31 @@ def test_simulate_env_subset_matches_oracle():
     scenes.assert_physics_bit_identical(sim, st, n, tag="env subset")
 
 
+def test_link_contacts_spill_rows_match_oracle():
+    """Ur5Sih family (split rows, HA_LINK_SLOTS LDS slots for robot blocks): the three objects placed on hand link
+    hulls give more robot-link contact rows per env than the LDS slots hold, so the env's global spill rows carry
+    the rest. Bit-identical to the C oracle on every env."""
+    n = 64
+    sim, orc, st = _oracle_and_sim(n, 7, near_hand=0.0)
+    sim.simulate(1)                  # link poses of this scene
+    body = get(sim, "rigid_body_state").reshape(n, 34, 13)
+    hull_links = sorted({int(sim.model.hull_link[k]) for k in range(sim.model.n_link_hulls)})
+    links = [hull_links[-1], hull_links[-4], hull_links[-7]]
+    rs = st["root_state"].reshape(n, 6, 13)
+    rs[:, 3:6, 0:3] = body[:, sim.model.body_robot0 + np.array(links), 0:3]
+    rs[:, 3:6, 7:13] = 0.0
+    put(sim, "root_state", st["root_state"])
+    for k in ("dof_state", "sim_targets"):
+        put(sim, k, st[k])
+    sim.simulate(1)
+    orc.simulate(st, 1)
+    f = get(sim, "net_contact_force").reshape(n, 34, 3)[:, sim.model.body_robot0:sim.model.body_robot0 + sim.model.n_links]
+    touched = (np.abs(f).sum(-1) > 0).sum(1)
+    print("ur5sih link-contact scene: robot links in contact per env: median %d, max %d" % (np.median(touched), touched.max()))
+    assert np.median(touched) >= 3
+    scenes.assert_physics_bit_identical(sim, st, n, tag="ur5sih link contacts")
+
+
 def test_simulate_many_calls_stays_physical():
     n = 256
     sim, orc, st = _oracle_and_sim(n, 7, near_hand=0.0)
