@@ -96,7 +96,6 @@ struct EnvLDS {
     float q[MAXD], qd[MAXD], tgt[MAXD];
     float lp[HA_MAX_LINKS][3], lq[HA_MAX_LINKS][4];
     float ax[MAXD][3], an[MAXD][3];
-    float Minv[MAXD * MAXD];                    // S ~ M^-1 (factor_inverse), stride D
     float Cb[MAXD];
     float v[MAXV];
     int nc, nr, noff, ng;                       // contacts kept / rows / contacts offered this substep /
@@ -195,7 +194,12 @@ __host__ __device__ constexpr size_t pc_rows_bytes() {
     return pc_rowdata_bytes<PC>() + (PC::nch > 1 ? 6 * sizeof(float) * (size_t)MAXR * PC::nch : 0);
 }
 template <class PC>
-__host__ __device__ inline size_t obj_lds_offset() { return obj_lds_offset_rows(pc_rows_bytes<PC>()); }
+__host__ __device__ inline size_t minv_lds_offset() { return obj_lds_offset_rows(pc_rows_bytes<PC>()); }
+// S ~ M^-1 (factor_inverse), D x D at stride D: after the union, sized for the family's DOF count
+template <class PC>
+__host__ __device__ inline size_t obj_lds_offset() {
+    return (minv_lds_offset<PC>() + (size_t)PC::nd * PC::nd * sizeof(float) + 15) & ~(size_t)15;
+}
 template <class PC>
 __host__ __device__ inline size_t contact_lds_offset() {
     return obj_lds_offset<PC>() + (size_t)PC::ocap * sizeof(ObjLDS);
@@ -211,6 +215,7 @@ struct SimCtx {
     EnvLDS* s;
     ObjLDS* o;              // the env's object slots (after the EnvLDS block, see task_lds_bytes)
     ContactLDS* k;          // the env's contact list (after the object slots)
+    float* Minv;            // S ~ M^-1, D x D (after the phase union, see obj_lds_offset)
     int lane, D, NO, L;
     int maxc;               // contact capacity (MAXC x chunks of the kernel family)
     const float* dr;        // this env's domain-randomization row (HA_DR_*), or null when DR is off
@@ -506,7 +511,7 @@ HD void factor_inverse(SimCtx& c) {
     }
     if (lane < ND) {
 #pragma unroll
-        for (int i = 0; i < ND; i++) s.Minv[lane * ND + i] = x[i];
+        for (int i = 0; i < ND; i++) c.Minv[lane * ND + i] = x[i];
     }
     wsync();
 }
@@ -1128,7 +1133,7 @@ HD void substep(SimCtx& c, float hdt) {
     // free motion: velocity-product forces only (drives are constraint rows of the PGS below)
     if (lane < D) {
         float acc = 0.0f;
-        for (int j = 0; j < D; j++) acc += s.Minv[lane * D + j] * (-hdt * s.Cb[j]);
+        for (int j = 0; j < D; j++) acc += c.Minv[lane * D + j] * (-hdt * s.Cb[j]);
         s.v[lane] = s.qd[lane] + acc;
     }
     if (lane < NO) {
@@ -1286,7 +1291,7 @@ HD void substep(SimCtx& c, float hdt) {
             if (Jr) {
                 for (int i = 0; i < D; i++) {
                     float acc = 0.0f;
-                    for (int j = 0; j < D; j++) acc += s.Minv[i * D + j] * Jr[j];
+                    for (int j = 0; j < D; j++) acc += c.Minv[i * D + j] * Jr[j];
                     Yr[i] = acc;
                 }
             }
@@ -1369,7 +1374,7 @@ HD void substep(SimCtx& c, float hdt) {
     if (lane < D) {
         float kp = m.dof_kp[lane], kd = m.dof_kd[lane];
         float den = kd + hdt * kp;
-        float mii = s.Minv[lane * D + lane];
+        float mii = c.Minv[lane * D + lane];
         dgam = 1.0f / (hdt * den);
         dbias = kp / den * (s.q[lane] - s.tgt[lane]);
         dwinv = 1.0f / (mii + dgam);
@@ -1400,7 +1405,7 @@ HD void substep(SimCtx& c, float hdt) {
         // constants: the same operands the oracle uses), and only the impulse change crosses lanes (one
         // v_readlane); the joint-limit rows run only for the joints whose limit is active (ballot masks).
         for (int d = 0; d < D; d++) {
-            float mrow = lane < D ? s.Minv[d * D + lane] : 0.0f;
+            float mrow = lane < D ? c.Minv[d * D + lane] : 0.0f;
             float nl = dlam - (vreg + dbias + dgam * dlam) * dwinv;
             nl = nl < -dlim ? -dlim : (nl > dlim ? dlim : nl);
             float dl = bcast(nl - dlam, d);

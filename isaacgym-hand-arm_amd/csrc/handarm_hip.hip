@@ -354,6 +354,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.m = model;
     c.p = params;
     c.s = reinterpret_cast<EnvLDS*>(smem);
+    c.Minv = reinterpret_cast<float*>(smem + minv_lds_offset<PC>());
     c.o = reinterpret_cast<ObjLDS*>(smem + obj_lds_offset<PC>());
     c.k = reinterpret_cast<ContactLDS*>(smem + contact_lds_offset<PC>());
     c.spill = PC::split ? spill + (size_t)env * PC::spill_floats : nullptr;
