@@ -41,12 +41,21 @@ struct DynScratch {
     float Ic[HA_MAX_LINKS][13];                 // composite spatial inertia (m, h, J) at world origin
     float Al[HA_MAX_LINKS][6], Fl[HA_MAX_LINKS][6];
 };
-struct ColScratch {
-    float wvA[64][4], wvB[64][4];       // world vertices of both hulls
-    float wpA[128][4], wpB[128][4];     // world face planes (n, d) of both hulls
-    int cand[64];                       // clipping: candidate incident vertices
-    int cmax[64];                       // clipping: per-candidate max plane distance (order-preserving int)
-    float gp[HA_MAX_GATHER][4], gn[HA_MAX_GATHER][4];   // compound object pair: gathered points (x, sep), normals
+// Narrow-phase scratch in the phase union, laid out per kernel family for its largest hull (NV vertices, NP face
+// planes; ha_create checks the model against it): world vertices and planes of both hull sides, the clipping
+// candidates and their max side-plane distances, and a compound pair's gathered points and normals
+template <int NV, int NP>
+struct ColLayout {
+    static constexpr size_t wvA = 0, wvB = wvA + 16 * NV, wpA = wvB + 16 * NV, wpB = wpA + 16 * NP;
+    static constexpr size_t cand = wpB + 16 * NP, cmax = cand + 4 * NV, gp = cmax + 4 * NV;
+    static constexpr size_t gn = gp + 16 * HA_MAX_GATHER, bytes = gn + 16 * HA_MAX_GATHER;
+};
+struct ColView {
+    float (*wvA)[4], (*wvB)[4];         // world vertices of both hulls
+    float (*wpA)[4], (*wpB)[4];         // world face planes (n, d) of both hulls
+    int* cand;                          // clipping: candidate incident vertices
+    int* cmax;                          // clipping: per-candidate max plane distance (order-preserving int)
+    float (*gp)[4], (*gn)[4];           // compound object pair: gathered points (x, sep) and normals
 };
 struct RowScratch {
     float J[MAXR * RS];
@@ -102,8 +111,7 @@ struct EnvLDS {
                                                 // points gathered for a compound object pair
     int cst[4];                                 // contact_stats of this launch (see ha_state_t)
     union {
-        PostScratch pd;
-        ColScratch col;
+        PostScratch pd;                         // (the narrow-phase scratch, ColLayout, is sized per family)
         RowScratch rows;
         float xfer[MAXR * HA_MAX_CONTACTS / MAXC];  // lane exchange outside the physics phases (controller;
                                                     // PGS impulses of every row -> contact forces). Must stay
@@ -138,7 +146,7 @@ HD int compact_index(int lane, int D, int so0, int so1) {
 // chunks (J and Y of MAXR x chunks rows), then the object slots (ObjLDS x capacity), then the contact list
 // (ContactLDS x MAXC x chunks), 16-byte aligned
 __host__ __device__ inline size_t obj_lds_offset_rows(size_t rows) {
-    size_t u = sizeof(PostScratch) > sizeof(ColScratch) ? sizeof(PostScratch) : sizeof(ColScratch);
+    size_t u = sizeof(PostScratch);
     if (rows > u) u = rows;
     return (offsetof(EnvLDS, u) + u + 15) & ~(size_t)15;
 }
@@ -155,9 +163,11 @@ __host__ __device__ inline size_t obj_lds_offset_rows(size_t rows) {
 #ifndef HA_SPLIT_ABOVE_OCAP
 #define HA_SPLIT_ABOVE_OCAP 2   /* families with more object slots use split rows (Ur5Sih 3 objects, clutter) */
 #endif
-template <int ND, int OCAP, int NCH, int KL = 8, int LCH = NCH, int CAP = MAXC>
+template <int ND, int OCAP, int NCH, int KL = 8, int LCH = NCH, int CAP = MAXC, int CV = 64, int CP = 128>
 struct PhysCfg {
     static constexpr int nd = ND, ocap = OCAP, nch = NCH;
+    static constexpr int colv = CV, colp = CP;      // largest hull: vertices, face planes (ColLayout)
+    static constexpr size_t col_bytes = ColLayout<CV, CP>::bytes;
     // contacts per chunk: MAXC, or fewer for a one-chunk family on dense rows (its rows and list shrink with it)
     static constexpr int cap = CAP;
     static constexpr int vw = ND + 6 * OCAP > 64 ? 2 : 1;
@@ -194,7 +204,21 @@ __host__ __device__ constexpr size_t pc_rows_bytes() {
     return pc_rowdata_bytes<PC>() + (PC::nch > 1 ? 6 * sizeof(float) * (size_t)MAXR * PC::nch : 0);
 }
 template <class PC>
-__host__ __device__ inline size_t minv_lds_offset() { return obj_lds_offset_rows(pc_rows_bytes<PC>()); }
+__host__ __device__ inline size_t minv_lds_offset() {
+    return obj_lds_offset_rows(pc_rows_bytes<PC>() > PC::col_bytes ? pc_rows_bytes<PC>() : PC::col_bytes);
+}
+// the family's narrow-phase scratch view into the phase union
+template <class PC>
+__device__ inline ColView col_view(void* u) {
+    using L = ColLayout<PC::colv, PC::colp>;
+    char* b = reinterpret_cast<char*>(u);
+    ColView v;
+    v.wvA = reinterpret_cast<float(*)[4]>(b + L::wvA); v.wvB = reinterpret_cast<float(*)[4]>(b + L::wvB);
+    v.wpA = reinterpret_cast<float(*)[4]>(b + L::wpA); v.wpB = reinterpret_cast<float(*)[4]>(b + L::wpB);
+    v.cand = reinterpret_cast<int*>(b + L::cand); v.cmax = reinterpret_cast<int*>(b + L::cmax);
+    v.gp = reinterpret_cast<float(*)[4]>(b + L::gp); v.gn = reinterpret_cast<float(*)[4]>(b + L::gn);
+    return v;
+}
 // S ~ M^-1 (factor_inverse), D x D at stride D: after the union, sized for the family's DOF count
 template <class PC>
 __host__ __device__ inline size_t obj_lds_offset() {
@@ -216,6 +240,7 @@ struct SimCtx {
     ObjLDS* o;              // the env's object slots (after the EnvLDS block, see task_lds_bytes)
     ContactLDS* k;          // the env's contact list (after the object slots)
     float* Minv;            // S ~ M^-1, D x D (after the phase union, see obj_lds_offset)
+    ColView col;            // narrow-phase scratch of the family (col_view)
     int lane, D, NO, L;
     int maxc;               // contact capacity (MAXC x chunks of the kernel family)
     const float* dr;        // this env's domain-randomization row (HA_DR_*), or null when DR is off
@@ -614,7 +639,7 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
     if (c.gather) {
         // compound pair: the chosen points (in the oracle's index order) join the gather buffer
         if (lane == 0) {
-            ColScratch& cs = s.u.col;
+            const ColView& cs = c.col;
             int ng = s.ng;
 #pragma unroll
             for (int t = 0; t < 4; t++) {
@@ -756,7 +781,7 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     if (dot3(dc, dc) > rr * rr) return;
     int nva = m.hull_nverts[ha], nvb = m.hull_nverts[hb];
     int npa = m.hull_nplanes[ha], npb = m.hull_nplanes[hb];
-    ColScratch& cs = s.u.col;
+    const ColView& cs = c.col;
 #ifdef HA_PROFILE
     unsigned long long _h0 = __builtin_amdgcn_s_memtime();
 #define HPROF(i) do { wsync(); unsigned long long _h1 = __builtin_amdgcn_s_memtime(); PROF_COUNT(i, _h1 - _h0); _h0 = _h1; } while (0)
@@ -941,7 +966,7 @@ HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
 // a compound pair's gathered points (lane = point, in gather order) -> one manifold of <= 4 contacts
 HD void gather_emit(SimCtx& c, int kind, int A, int B) {
     EnvLDS& s = *c.s;
-    const ColScratch& cs = s.u.col;
+    const ColView& cs = c.col;
     wsync();
     int lane = c.lane;
     bool valid = lane < s.ng;

@@ -76,7 +76,7 @@ __host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5S
 #define HA_AK_WAVES_PER_EU 3
 #endif
 #ifndef HA_AH_WAVES_PER_EU
-#define HA_AH_WAVES_PER_EU 3
+#define HA_AH_WAVES_PER_EU 4
 #endif
 template <int FAM>
 __host__ __device__ constexpr int task_chunk_capacity() {
@@ -87,11 +87,18 @@ __host__ __device__ constexpr int task_waves_per_eu() {
     return FAM == HA_TASK_UR5SIH ? HA_WAVES_PER_EU
            : (FAM == HA_TASK_ALLEGRO_KUKA ? HA_AK_WAVES_PER_EU : (FAM == HA_TASK_ALLEGRO_HAND ? HA_AH_WAVES_PER_EU : 1));
 }
+// largest hull a family's narrow-phase scratch holds: the YCB pool hulls have up to 64 vertices and 124 face
+// planes; the Allegro scenes' hulls (cooked to <= 32 vertices, <= 60 planes) take half, which puts the
+// AllegroHand env block at 10.2 KB: 16 workgroups per CU with 4 waves per SIMD
+template <int FAM>
+__host__ __device__ constexpr int task_col_verts() { return (FAM == HA_TASK_ALLEGRO_KUKA || FAM == HA_TASK_ALLEGRO_HAND) ? 32 : 64; }
+template <int FAM>
+__host__ __device__ constexpr int task_col_planes() { return (FAM == HA_TASK_ALLEGRO_KUKA || FAM == HA_TASK_ALLEGRO_HAND) ? 64 : 128; }
 template <int FAM>
 using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>(),
                         FAM == FAM_UR5SIH_CLUTTER ? HB_LINK_SLOTS : HA_LINK_SLOTS,
                         FAM == FAM_UR5SIH_CLUTTER ? HB_LDS_CHUNKS : task_contact_chunks<FAM>(),
-                        task_chunk_capacity<FAM>()>;
+                        task_chunk_capacity<FAM>(), task_col_verts<FAM>(), task_col_planes<FAM>()>;
 
 
 // ----------------------------------------------------------------------------- state load/store
@@ -355,6 +362,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.p = params;
     c.s = reinterpret_cast<EnvLDS*>(smem);
     c.Minv = reinterpret_cast<float*>(smem + minv_lds_offset<PC>());
+    c.col = col_view<PC>(&c.s->u);
     c.o = reinterpret_cast<ObjLDS*>(smem + obj_lds_offset<PC>());
     c.k = reinterpret_cast<ContactLDS*>(smem + contact_lds_offset<PC>());
     c.spill = PC::split ? spill + (size_t)env * PC::spill_floats : nullptr;
@@ -695,8 +703,18 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
         model->n_static < 0 || model->n_static > HA_MAX_STATIC || model->n_pool < 1 || model->n_pool > HA_MAX_POOL ||
         model->n_hulls > HA_MAX_HULLS)
         return HA_E_MODEL;
+    // every hull must fit the family's narrow-phase scratch (ColLayout)
+    int col_v = (fam == HA_TASK_ALLEGRO_KUKA || fam == HA_TASK_ALLEGRO_HAND) ? FamPhys<HA_TASK_ALLEGRO_HAND>::colv
+                                                                           : FamPhys<HA_TASK_UR5SIH>::colv;
+    int col_p = (fam == HA_TASK_ALLEGRO_KUKA || fam == HA_TASK_ALLEGRO_HAND) ? FamPhys<HA_TASK_ALLEGRO_HAND>::colp
+                                                                           : FamPhys<HA_TASK_UR5SIH>::colp;
+    static_assert(FamPhys<HA_TASK_ALLEGRO_HAND>::colv == FamPhys<HA_TASK_ALLEGRO_KUKA>::colv &&
+                      FamPhys<HA_TASK_ALLEGRO_HAND>::colp == FamPhys<HA_TASK_ALLEGRO_KUKA>::colp &&
+                      FamPhys<HA_TASK_UR5SIH>::colv == FamPhys<FAM_UR5SIH_CLUTTER>::colv &&
+                      FamPhys<HA_TASK_UR5SIH>::colp == FamPhys<FAM_UR5SIH_CLUTTER>::colp,
+                  "narrow-phase scratch limits per family pair");
     for (int k = 0; k < model->n_hulls; k++)
-        if (model->hull_nverts[k] > 64 || model->hull_nplanes[k] > 128) return HA_E_MODEL;
+        if (model->hull_nverts[k] > col_v || model->hull_nplanes[k] > col_p) return HA_E_MODEL;
     for (int i = 0; i < model->n_pool; i++)
         if (model->pool_nhull[i] < 1 || model->pool_hull[i] < 0 ||
             model->pool_hull[i] + model->pool_nhull[i] > model->n_hulls)
