@@ -563,6 +563,12 @@ HD PoseF object_pose(const SimCtx& c, int o) {
     qf q = ldq(c.o[o].oq);
     return PoseF{ld3(c.o[o].oc) - qrot(q, scale3(c, o, ld3(c.m->pool_com[c.o[o].pool]))), q};
 }
+// object o's pool id when o is wave-uniform (narrow phase): in an SGPR, so the model reads it indexes are scalar
+HD int upool(const SimCtx& c, int o) { return __builtin_amdgcn_readfirstlane(c.o[o].pool); }
+HD PoseF object_pose_u(const SimCtx& c, int o) {
+    qf q = ldq(c.o[o].oq);
+    return PoseF{ld3(c.o[o].oc) - qrot(q, scale3(c, o, ld3(c.m->pool_com[upool(c, o)]))), q};
+}
 
 // face plane k of a hull in world space; for a scaled body (inv_sc = 1 / scale, read once per hull pair by
 // the caller) n' = S^-1 n / |S^-1 n|, d' = d / |S^-1 n|
@@ -920,9 +926,9 @@ HD bool pair_desc(const SimCtx& c, int p, int& kind, int& A, int& B) {
 HD int pair_pieces(const SimCtx& c, int kind, int A, int B) {
     const ha_model_t& m = *c.m;
     if (kind == 4) return 1;
-    int n = m.pool_nhull[c.o[A].pool];
-    if (kind == 2) n *= m.pool_nhull[c.o[B].pool];
-    return __builtin_amdgcn_readfirstlane(n);
+    int n = m.pool_nhull[upool(c, A)];
+    if (kind == 2) n *= m.pool_nhull[upool(c, B)];
+    return n;
 }
 
 // narrow phase of piece pair j of candidate pair (kind, A, B): the two sides' hulls, poses and body codes
@@ -930,15 +936,15 @@ HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
     const EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     if (kind == 0) {
-        collide_ground(c, m.pool_hull[c.o[A].pool] + j, object_pose(c, A), A);
+        collide_ground(c, m.pool_hull[upool(c, A)] + j, object_pose_u(c, A), A);
         return;
     }
     int h1, h2, b1, b2, k2;
     PoseF P1, P2;
     if (kind <= 3) {
-        int pa = c.o[A].pool;
+        int pa = upool(c, A);
         int ho = m.pool_hull[pa];
-        PoseF Po = object_pose(c, A);
+        PoseF Po = object_pose_u(c, A);
         if (kind == 1) {
             h1 = ho + j; P1 = Po; b1 = A; h2 = m.static_hull[B]; P2 = static_pose(m, B); b2 = -1; k2 = -100 - B;
             // the piece's own sphere against the exact box (the oracle's per-piece near_box; for a one-hull object
@@ -947,9 +953,9 @@ HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
             if (!sphere_near_box(m.static_half[B], P2, cp, scale_radius(c, A, m.hull_radius[h1]) + c.p->contact_margin))
                 return;
         } else if (kind == 2) {
-            int pb = c.o[B].pool, n2 = m.pool_nhull[pb];
+            int pb = upool(c, B), n2 = m.pool_nhull[pb];
             int j1 = j / n2;
-            h1 = ho + j1; P1 = Po; b1 = A; h2 = m.pool_hull[pb] + (j - j1 * n2); P2 = object_pose(c, B);
+            h1 = ho + j1; P1 = Po; b1 = A; h2 = m.pool_hull[pb] + (j - j1 * n2); P2 = object_pose_u(c, B);
             b2 = B; k2 = B;
         } else {
             int Lk = m.hull_link[B];
