@@ -33,8 +33,15 @@ def init_distributed(backend=None):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rk = int(os.environ.get("RANK", "0"))
     lr = int(os.environ.get("LOCAL_RANK", "0"))
-    backend = backend or "nccl"
-    device = f"cuda:{lr}" if backend == "nccl" else "cpu"
+    # rehearsal on a box with fewer GPUs than ranks: HA_DIST_BACKEND=gloo HA_DIST_SHARE_GPU=1 puts rank r on
+    # cuda:(r % device_count) and reduces over gloo (RCCL needs one GPU per rank)
+    backend = os.environ.get("HA_DIST_BACKEND", backend or "nccl")
+    if backend == "nccl":
+        device = f"cuda:{lr}"
+    elif os.environ.get("HA_DIST_SHARE_GPU") == "1" and torch.cuda.is_available():
+        device = f"cuda:{lr % torch.cuda.device_count()}"
+    else:
+        device = "cpu"
     if device != "cpu":
         torch.cuda.set_device(device)
     if ws > 1:

@@ -188,3 +188,21 @@ def test_apply_rigid_body_force_tensors_local_space():
     exp = f_world / mass[:, None] * dt + np.array([0.0, 0.0, -9.81]) * dt
     np.testing.assert_allclose(v, exp, rtol=1e-3, atol=1e-5)
     assert np.all(get(sim, "object_force") == 0)
+
+
+def test_create_rejects_hulls_beyond_the_family_scratch():
+    """The Allegro families' narrow-phase scratch holds hulls of <= 32 vertices / 64 planes (ColLayout): ha_create
+    refuses a model with a larger hull instead of overrunning LDS."""
+    need_gpu()
+    import ctypes as C
+    from handarm_hip import _lib
+    scene = HM.load_scene(HM.KUKA_ASSET)
+    model = HM.build_model(scene)
+    params, _ = HM.build_params(task=HM.TASK_ALLEGRO_KUKA)
+    lib = _lib.load()
+    h = C.c_void_p()
+    assert lib.ha_create(C.byref(model), C.byref(params), 4, C.byref(h)) == 0
+    lib.ha_destroy(h)
+    model.hull_nverts[0] = 40
+    h2 = C.c_void_p()
+    assert lib.ha_create(C.byref(model), C.byref(params), 4, C.byref(h2)) != 0
