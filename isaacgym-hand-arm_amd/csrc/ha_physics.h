@@ -44,11 +44,12 @@ struct DynScratch {
 // Narrow-phase scratch in the phase union, laid out per kernel family for its largest hull (NV vertices, NP face
 // planes; ha_create checks the model against it): world vertices and planes of both hull sides, the clipping
 // candidates and their max side-plane distances, and a compound pair's gathered points and normals
-template <int NV, int NP>
+// (NG gathered points: HA_MAX_GATHER, or 0 for a family without compound objects, which ha_create enforces)
+template <int NV, int NP, int NG = HA_MAX_GATHER>
 struct ColLayout {
     static constexpr size_t wvA = 0, wvB = wvA + 16 * NV, wpA = wvB + 16 * NV, wpB = wpA + 16 * NP;
     static constexpr size_t cand = wpB + 16 * NP, cmax = cand + 4 * NV, gp = cmax + 4 * NV;
-    static constexpr size_t gn = gp + 16 * HA_MAX_GATHER, bytes = gn + 16 * HA_MAX_GATHER;
+    static constexpr size_t gn = gp + 16 * NG, bytes = gn + 16 * NG;
 };
 struct ColView {
     float (*wvA)[4], (*wvB)[4];         // world vertices of both hulls
@@ -154,63 +155,91 @@ __host__ __device__ inline size_t obj_lds_offset_rows(size_t rows) {
 // Compile-time shape of a kernel family's physics: DOF count, object slots, contact chunks (MAXC contacts
 // each) and velocity words per lane (coordinates lane and lane + 64 when D + 6 x objects > 64).
 //
-// Split rows (the clutter family, split = true): most clutter contacts touch no robot link (object-bin,
-// object-object), and such a row's robot block is zero in J and in Y = M^-1 J^T. The rows then keep only
-// their two 6-wide object blocks in LDS (12 floats each of J and Y), and the robot blocks of the contacts that
-// do touch a link get a slot of their own: the first KL link contacts in LDS, the rest in a per-env global
-// spill area (ha_create allocates it; L2-resident, rare). Every dot product visits the nonzero terms in the
-// dense order and a skipped zero block adds exact zeros, so results are bit-identical to the dense rows.
+// Split rows (split = true): most clutter contacts touch no robot link (object-bin, object-object), and such a
+// row's robot block is zero in J and in Y = M^-1 J^T. The rows then keep only their object blocks in LDS (OW =
+// 6 x object slots floats each of J and Y), and the robot blocks of the contacts that do touch a link get a slot
+// of their own: the first KL link contacts in LDS, the rest in a per-env global spill area (ha_create allocates
+// it; L2-resident, rare). Every dot product visits the nonzero terms in the dense order and a skipped zero block
+// adds exact zeros, so results are bit-identical to the dense rows. The Ur5Sih families (3 and 8 object slots)
+// split by default (HA_SPLIT_ABOVE_OCAP); AllegroKuka (one object slot, SPLIT = 1) splits too: its cube-table
+// contacts, most of the list, touch no link.
+//
+// Minv in the union (MU = true, AllegroKuka): S ~ M^-1 sits at the END of the phase union, over the dynamics
+// scratch (dead once dynamics() has produced M and Cb) and clear of M (which factor_inverse reads while writing
+// S), of the narrow-phase scratch (detect runs while S is live) and of the constraint rows (the rows phase and
+// the PGS read S): the static_asserts below check the three. Otherwise S follows the union.
 #ifndef HA_SPLIT_ABOVE_OCAP
 #define HA_SPLIT_ABOVE_OCAP 2   /* families with more object slots use split rows (Ur5Sih 3 objects, clutter) */
 #endif
-template <int ND, int OCAP, int NCH, int KL = 8, int LCH = NCH, int CAP = MAXC, int CV = 64, int CP = 128>
+template <int ND, int OCAP, int NCH, int KL = 8, int LCH = NCH, int CAP = MAXC, int CV = 64, int CP = 128,
+          int SPLIT = -1, int NG = HA_MAX_GATHER, bool MU = false>
 struct PhysCfg {
     static constexpr int nd = ND, ocap = OCAP, nch = NCH;
-    static constexpr int colv = CV, colp = CP;      // largest hull: vertices, face planes (ColLayout)
-    static constexpr size_t col_bytes = ColLayout<CV, CP>::bytes;
-    // contacts per chunk: MAXC, or fewer for a one-chunk family on dense rows (its rows and list shrink with it)
+    static constexpr int colv = CV, colp = CP, colg = NG;   // largest hull: vertices, face planes; gather points
+    static constexpr size_t col_bytes = ColLayout<CV, CP, NG>::bytes;
+    // contacts per chunk: MAXC, or fewer for a one-chunk family (its rows and list shrink with it)
     static constexpr int cap = CAP;
+    static constexpr int rpc = 3 * CAP;             // constraint rows per chunk
     static constexpr int vw = ND + 6 * OCAP > 64 ? 2 : 1;
 #ifdef HA_DENSE_ROWS    /* diagnostic build (tools/split_rows_check.py): every family on dense rows */
     static constexpr bool split = false;
 #else
-    static constexpr bool split = OCAP > HA_SPLIT_ABOVE_OCAP;
+    static constexpr bool split = SPLIT >= 0 ? SPLIT != 0 : OCAP > HA_SPLIT_ABOVE_OCAP;
 #endif
+    static constexpr int ow = 6 * row_slots<ND>();  // split rows: object-block width
     static constexpr int kl = KL;
+    static constexpr bool minv_in_union = MU;
     // split rows: the object blocks of chunks [0, lch) live in LDS, those of chunks [lch, nch) in the env's global
     // row area after the robot-block spill rows (written by the rows phase, read back by the PGS one contact ahead)
     static constexpr int lch = split ? LCH : NCH;
-    static constexpr int spill_robot = split ? 2 * 3 * (MAXC * NCH - KL) * ND : 0;   // per env: J then Y
-    static constexpr int spill_obj = split ? 2 * MAXR * (NCH - lch) * 12 : 0;        // per env: J then Y
+    static constexpr int spill_robot = split ? 2 * 3 * (CAP * NCH - KL) * ND : 0;   // per env: J then Y
+    static constexpr int spill_obj = split ? 2 * rpc * (NCH - lch) * ow : 0;        // per env: J then Y
     static constexpr int spill_floats = spill_robot + spill_obj;
     static_assert(ND + 6 * OCAP <= MAXV, "generalized velocity exceeds MAXV");
-    static_assert(!split || (KL >= 0 && KL <= MAXC * NCH), "LDS link slots must not exceed the contact capacity");
-    static_assert(!split || (row_slots<ND>() == 2 && MAXC * NCH <= 128), "split rows: two object slots, <= 128 contacts");
-    static_assert(split || MAXC * NCH <= 64, "dense rows: <= 64 contacts (one ballot)");
+    static_assert(!split || (KL >= 0 && KL <= CAP * NCH), "LDS link slots must not exceed the contact capacity");
+    static_assert(!split || CAP * NCH <= 128, "split rows: <= 128 contacts");
+    static_assert(split || CAP * NCH <= 64, "dense rows: <= 64 contacts (one ballot)");
     static_assert(lch >= 0 && lch <= NCH, "LDS row chunks");
-    static_assert(MAXC * NCH <= HA_MAX_CONTACTS, "contact capacity exceeds HA_MAX_CONTACTS");
-    static_assert(CAP == MAXC || (NCH == 1 && !split && CAP >= 1 && CAP < MAXC), "reduced capacity: one dense chunk");
+    static_assert(CAP * NCH <= HA_MAX_CONTACTS, "contact capacity exceeds HA_MAX_CONTACTS");
+    static_assert(CAP == MAXC || (NCH == 1 && CAP >= 1 && CAP < MAXC), "reduced capacity: one chunk");
+    static_assert(NG == 0 || NG == HA_MAX_GATHER, "gather buffer: HA_MAX_GATHER points or none");
+    static_assert(CP >= 8, "sat_planes reads plane slots 0..7 of the narrow-phase scratch");
 };
 // bytes of the constraint rows proper, then (several contact chunks only) the per-row PGS constants of every
 // chunk (impulse, target velocity, 1/diag, friction, two Delassus entries: 6 floats x MAXR x chunks), which the
 // PGS swaps into registers one chunk at a time
 template <class PC>
 __host__ __device__ constexpr size_t pc_rowdata_bytes() {
-    return PC::split ? 2 * sizeof(float) * ((size_t)MAXR * PC::lch * 12 + 3 * (size_t)PC::kl * PC::nd)
-                     : 2 * sizeof(float) * (size_t)3 * PC::cap * PC::nch * row_stride<PC::nd>();
+    return PC::split ? 2 * sizeof(float) * ((size_t)PC::rpc * PC::lch * PC::ow + 3 * (size_t)PC::kl * PC::nd)
+                     : 2 * sizeof(float) * (size_t)PC::rpc * PC::nch * row_stride<PC::nd>();
 }
 template <class PC>
 __host__ __device__ constexpr size_t pc_rows_bytes() {
     return pc_rowdata_bytes<PC>() + (PC::nch > 1 ? 6 * sizeof(float) * (size_t)MAXR * PC::nch : 0);
 }
+// S ~ M^-1 (factor_inverse), D x D at stride D, sized for the family's DOF count: at the end of the union
+// (minv_in_union) or after it
+template <class PC>
+__host__ __device__ constexpr size_t minv_union_offset() {
+    return (sizeof(PostScratch) - (size_t)PC::nd * PC::nd * sizeof(float)) & ~(size_t)15;
+}
 template <class PC>
 __host__ __device__ inline size_t minv_lds_offset() {
-    return obj_lds_offset_rows(pc_rows_bytes<PC>() > PC::col_bytes ? pc_rows_bytes<PC>() : PC::col_bytes);
+    if constexpr (PC::minv_in_union) {
+        static_assert(offsetof(PostScratch, M) + (size_t)PC::nd * PC::nd * sizeof(float) <= minv_union_offset<PC>(),
+                      "S must not overlap M (factor_inverse reads M while writing S)");
+        static_assert(offsetof(PostScratch, dyn) <= minv_union_offset<PC>(), "S may overlap only the dynamics scratch");
+        static_assert(PC::col_bytes <= minv_union_offset<PC>(), "S must not overlap the narrow-phase scratch");
+        static_assert(pc_rows_bytes<PC>() <= minv_union_offset<PC>(), "S must not overlap the constraint rows");
+        return offsetof(EnvLDS, u) + minv_union_offset<PC>();
+    } else {
+        return obj_lds_offset_rows(pc_rows_bytes<PC>() > PC::col_bytes ? pc_rows_bytes<PC>() : PC::col_bytes);
+    }
 }
 // the family's narrow-phase scratch view into the phase union
 template <class PC>
 __device__ inline ColView col_view(void* u) {
-    using L = ColLayout<PC::colv, PC::colp>;
+    using L = ColLayout<PC::colv, PC::colp, PC::colg>;
     char* b = reinterpret_cast<char*>(u);
     ColView v;
     v.wvA = reinterpret_cast<float(*)[4]>(b + L::wvA); v.wvB = reinterpret_cast<float(*)[4]>(b + L::wvB);
@@ -219,10 +248,12 @@ __device__ inline ColView col_view(void* u) {
     v.gp = reinterpret_cast<float(*)[4]>(b + L::gp); v.gn = reinterpret_cast<float(*)[4]>(b + L::gn);
     return v;
 }
-// S ~ M^-1 (factor_inverse), D x D at stride D: after the union, sized for the family's DOF count
 template <class PC>
 __host__ __device__ inline size_t obj_lds_offset() {
-    return (minv_lds_offset<PC>() + (size_t)PC::nd * PC::nd * sizeof(float) + 15) & ~(size_t)15;
+    if constexpr (PC::minv_in_union)
+        return obj_lds_offset_rows(pc_rows_bytes<PC>() > PC::col_bytes ? pc_rows_bytes<PC>() : PC::col_bytes);
+    else
+        return (minv_lds_offset<PC>() + (size_t)PC::nd * PC::nd * sizeof(float) + 15) & ~(size_t)15;
 }
 template <class PC>
 __host__ __device__ inline size_t contact_lds_offset() {
@@ -731,17 +762,23 @@ HD float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
 HD void sat_planes(const SimCtx& c, const float (*wp)[4], int np, const float (*wv)[4], int nv, float& sep, int& kbest) {
     int lane = c.lane;
     if (np <= 8) {
-        // few planes (boxes): lane = vertex, one wave min per plane
+        // few planes (boxes): lane = vertex, one wave min per plane. The eight plane slots are unrolled so their
+        // independent DPP reduction chains interleave (slots k >= np read in-bounds scratch and are masked), then
+        // the strict-compare scan over k keeps the oracle's first maximum
         f3 v = mk3(0, 0, 0);
         if (lane < nv) v = ld3(wv[lane]);
-        float best = -3.0e38f;
-        int bk = 1 << 20;
-        for (int k = 0; k < np; k++) {
+        float mn[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
             f3 n = ld3(wp[k]);
             float d = wp[k][3];
-            float mn = wave_min(lane < nv ? dot3(n, v) + d : 3.0e38f);
-            if (mn > best) { best = mn; bk = k; }
+            mn[k] = wave_min(lane < nv && k < np ? dot3(n, v) + d : 3.0e38f);
         }
+        float best = -3.0e38f;
+        int bk = 1 << 20;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (k < np && mn[k] > best) { best = mn[k]; bk = k; }
         sep = best;
         kbest = bk;
         return;
@@ -1241,12 +1278,12 @@ HD void substep(SimCtx& c, float hdt) {
     float* Yb = Jb + 3 * PC::cap * NCH * RSN;
     int nc = s.nc;
     int nr = 3 * nc;    // nc <= MAXC x NCH -> <= MAXR x NCH rows
-    // split rows (PhysCfg): object blocks of every row (OW = 12 wide, J then Y), then the robot blocks of the
+    // split rows (PhysCfg): object blocks of every row (OW wide, J then Y), then the robot blocks of the
     // first KL link contacts (J then Y), then the env's global spill area for the link contacts after those
-    constexpr int OW = 12, KL = PC::kl, LCH = PC::lch, SPJ = 3 * (MAXC * NCH - KL) * ND;
+    constexpr int OW = PC::ow, KL = PC::kl, LCH = PC::lch, RPC = PC::rpc, SPJ = 3 * (PC::cap * NCH - KL) * ND;
     float* Ob = Jb;
-    float* ObY = Ob + MAXR * LCH * OW;
-    float* Rb = ObY + MAXR * LCH * OW;
+    float* ObY = Ob + RPC * LCH * OW;
+    float* Rb = ObY + RPC * LCH * OW;
     float* RbY = Rb + 3 * KL * ND;
     // contacts that touch a robot link (split rows only): contacts 0..63 in lmask0, 64.. in lmask1
     uint64_t lmask0 = 0, lmask1 = 0;
@@ -1268,8 +1305,8 @@ HD void substep(SimCtx& c, float hdt) {
     };
     // object blocks (J or Y) of row r: LDS for the first LCH chunks, else the env's global row area
     auto orow = [&](int r, bool y) -> float* {
-        if (r < MAXR * LCH) return (y ? ObY : Ob) + r * OW;
-        return c.spill + PC::spill_robot + (y ? MAXR * (NCH - LCH) * OW : 0) + (r - MAXR * LCH) * OW;
+        if (LCH == NCH || r < RPC * LCH) return (y ? ObY : Ob) + r * OW;   // every chunk in LDS: no global path
+        return c.spill + PC::spill_robot + (y ? RPC * (NCH - LCH) * OW : 0) + (r - RPC * LCH) * OW;
     };
     // PGS row constants of the lane's row in the current chunk: impulse, target velocity, 1/diagonal, friction and
     // the block's Delassus entries. One chunk: kept in registers. Several: stored per row in RK (after the rows)
@@ -1320,9 +1357,15 @@ HD void substep(SimCtx& c, float hdt) {
             }
             // Y_r = M^-1 J_r^T (robot block through the explicit inverse, object blocks 1/m, I_w^-1)
             if (Jr) {
+                // J_r to registers first: Jr may be a global spill row (a generic pointer), read once here
+                // instead of D times in the product loop (same sums, same order)
+                float jr[ND];
+#pragma unroll
+                for (int j = 0; j < ND; j++) jr[j] = Jr[j];
                 for (int i = 0; i < D; i++) {
                     float acc = 0.0f;
-                    for (int j = 0; j < D; j++) acc += c.Minv[i * D + j] * Jr[j];
+#pragma unroll
+                    for (int j = 0; j < ND; j++) acc += c.Minv[i * D + j] * jr[j];
                     Yr[i] = acc;
                 }
             }
@@ -1361,31 +1404,32 @@ HD void substep(SimCtx& c, float hdt) {
         int r = MAXR * ch + lane;
         if (lane < MAXR && r < nr && r % 3 != 0) {
             int k = r % 3, r0 = r - k;
-            const float *Jr, *Y0r, *Y1r, *Jo, *Y0o;
+            const float *Jo, *Y0o;
+            float a = 0.0f, b = 0.0f;           // robot-block partial sums (J_rk . Y_r0, J_rk . Y_r1), t = 0 .. D-1
+            auto rdot = [&](const float* Jr, const float* Y0r, const float* Y1r) {
+                for (int t = 0; t < D; t++) a += Jr[t] * Y0r[t];
+                if (k == 2)
+                    for (int t = 0; t < D; t++) b += Jr[t] * Y1r[t];
+            };
             if constexpr (PC::split) {
+                // LDS slot or global spill row on separate paths, so each keeps its own address space
                 int ls = lslot(r / 3);
-                Jr = ls >= 0 ? rrow(ls, k, false) : nullptr;
-                Y0r = ls >= 0 ? rrow(ls, 0, true) : nullptr;
-                Y1r = ls >= 0 ? rrow(ls, 1, true) : nullptr;
+                if (ls >= 0 && ls < KL) rdot(Rb + (3 * ls + k) * ND, RbY + 3 * ls * ND, RbY + (3 * ls + 1) * ND);
+                else if (ls >= KL) {
+                    const float* sr = c.spill + 3 * (ls - KL) * ND;
+                    rdot(sr + k * ND, sr + SPJ, sr + SPJ + ND);
+                }
                 Jo = orow(r, false);
                 Y0o = orow(r0, true);
             } else {
-                Jr = Jb + r * RSN;
-                Y0r = Yb + r0 * RSN;
-                Y1r = Y0r + RSN;
-                Jo = Jr + D;
-                Y0o = Y0r + D;
+                rdot(Jb + r * RSN, Yb + r0 * RSN, Yb + (r0 + 1) * RSN);
+                Jo = Jb + r * RSN + D;
+                Y0o = Yb + r0 * RSN + D;
             }
             const float* Y1o = Y0o + (PC::split ? OW : RSN);
-            float a = 0.0f;
-            if (Jr)
-                for (int t = 0; t < D; t++) a += Jr[t] * Y0r[t];
             for (int t = 0; t < RSN - D; t++) a += Jo[t] * Y0o[t];
             ca0_ = a;
             if (k == 2) {
-                float b = 0.0f;
-                if (Jr)
-                    for (int t = 0; t < D; t++) b += Jr[t] * Y1r[t];
                 for (int t = 0; t < RSN - D; t++) b += Jo[t] * Y1o[t];
                 ca1_ = b;
             }
@@ -1486,18 +1530,30 @@ HD void substep(SimCtx& c, float hdt) {
                 // (LDS for the first KL, else the global spill rows), absent -> 0
                 const float* On = orow(3 * ci, false);
                 const float* OYn = orow(3 * ci, true);
-                if (ix >= D) {
+                int lsc = lslot(ci);            // wave-uniform
+                if (LCH == NCH && lsc < KL) {
+                    // every entry of this contact is in LDS: one set of loads, each lane's block (object block at
+                    // stride OW, or the link slot's robot block at stride ND) chosen per lane
+                    bool ob = ix >= D, rb = ix >= 0 && ix < D && lsc >= 0;
+                    const float* P = ob ? On + (ix - D) : Rb + 3 * lsc * ND + ix;
+                    const float* PY = ob ? OYn + (ix - D) : RbY + 3 * lsc * ND + ix;
+                    int st = ob ? OW : ND;
+                    if (ob || rb) {
+                        j0n = P[0]; j1n = P[st]; j2n = P[2 * st];
+                        y0n = PY[0]; y1n = PY[st]; y2n = PY[2 * st];
+                    }
+                } else if (ix >= D) {
                     int t = ix - D;
                     j0n = On[t]; j1n = On[OW + t]; j2n = On[2 * OW + t];
                     y0n = OYn[t]; y1n = OYn[OW + t]; y2n = OYn[2 * OW + t];
                 } else if (ix >= 0) {
-                    int ls = lslot(ci);
-                    if (ls >= 0) {
-                        const float* Rn = rrow(ls, 0, false);
-                        const float* RYn = rrow(ls, 0, true);
+                    int ls = lslot(ci);         // wave-uniform: one path per contact, LDS or global
+                    auto ld6 = [&](const float* Rn, const float* RYn) {
                         j0n = Rn[ix]; j1n = Rn[ND + ix]; j2n = Rn[2 * ND + ix];
                         y0n = RYn[ix]; y1n = RYn[ND + ix]; y2n = RYn[2 * ND + ix];
-                    }
+                    };
+                    if (ls >= 0 && ls < KL) ld6(Rb + 3 * ls * ND, RbY + 3 * ls * ND);
+                    else if (ls >= KL) ld6(c.spill + 3 * (ls - KL) * ND, c.spill + SPJ + 3 * (ls - KL) * ND);
                 }
                 if (VW == 2 && ixh >= D) {
                     int t = ixh - D;

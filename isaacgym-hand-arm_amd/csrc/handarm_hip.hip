@@ -73,7 +73,7 @@ __host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5S
 #define HA_AH_CONTACTS 12
 #endif
 #ifndef HA_AK_WAVES_PER_EU
-#define HA_AK_WAVES_PER_EU 3
+#define HA_AK_WAVES_PER_EU 4
 #endif
 #ifndef HA_AH_WAVES_PER_EU
 #define HA_AH_WAVES_PER_EU 4
@@ -94,11 +94,24 @@ template <int FAM>
 __host__ __device__ constexpr int task_col_verts() { return (FAM == HA_TASK_ALLEGRO_KUKA || FAM == HA_TASK_ALLEGRO_HAND) ? 32 : 64; }
 template <int FAM>
 __host__ __device__ constexpr int task_col_planes() { return (FAM == HA_TASK_ALLEGRO_KUKA || FAM == HA_TASK_ALLEGRO_HAND) ? 64 : 128; }
+// AllegroKuka env block (PhysCfg SPLIT / NG / MU): split rows with HA_AK_LINK_SLOTS link contacts in LDS, no
+// compound-object gather buffer (its one object is a cuboid; ha_create enforces one hull per pool object) and
+// S ~ M^-1 inside the phase union: 13.3 -> 9.1 KB, so 16 workgroups per CU hold the 4096 envs of config C2 in
+// one round (12 per CU ran them in 1.33 rounds). HA_AK_COMPACT=0 restores the round-2 layout (A/B timing).
+#ifndef HA_AK_COMPACT
+#define HA_AK_COMPACT 1
+#endif
+#ifndef HA_AK_LINK_SLOTS
+#define HA_AK_LINK_SLOTS 4
+#endif
+template <int FAM>
+__host__ __device__ constexpr bool task_compact() { return FAM == HA_TASK_ALLEGRO_KUKA && HA_AK_COMPACT; }
 template <int FAM>
 using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>(),
-                        FAM == FAM_UR5SIH_CLUTTER ? HB_LINK_SLOTS : HA_LINK_SLOTS,
+                        FAM == FAM_UR5SIH_CLUTTER ? HB_LINK_SLOTS : (task_compact<FAM>() ? HA_AK_LINK_SLOTS : HA_LINK_SLOTS),
                         FAM == FAM_UR5SIH_CLUTTER ? HB_LDS_CHUNKS : task_contact_chunks<FAM>(),
-                        task_chunk_capacity<FAM>(), task_col_verts<FAM>(), task_col_planes<FAM>()>;
+                        task_chunk_capacity<FAM>(), task_col_verts<FAM>(), task_col_planes<FAM>(),
+                        task_compact<FAM>() ? 1 : -1, task_compact<FAM>() ? 0 : HA_MAX_GATHER, task_compact<FAM>()>;
 
 
 // ----------------------------------------------------------------------------- state load/store
@@ -715,9 +728,11 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
                   "narrow-phase scratch limits per family pair");
     for (int k = 0; k < model->n_hulls; k++)
         if (model->hull_nverts[k] > col_v || model->hull_nplanes[k] > col_p) return HA_E_MODEL;
+    // a family without a gather buffer (ColLayout NG = 0) takes single-hull pool objects only
+    bool one_hull = fam == HA_TASK_ALLEGRO_KUKA && FamPhys<HA_TASK_ALLEGRO_KUKA>::colg == 0;
     for (int i = 0; i < model->n_pool; i++)
         if (model->pool_nhull[i] < 1 || model->pool_hull[i] < 0 ||
-            model->pool_hull[i] + model->pool_nhull[i] > model->n_hulls)
+            model->pool_hull[i] + model->pool_nhull[i] > model->n_hulls || (one_hull && model->pool_nhull[i] != 1))
             return HA_E_MODEL;
     if (params->num_initial_poses < 1 || params->num_initial_poses > HA_MAX_INIT_POSES) return HA_E_ARG;
     ha_handle h = (ha_handle)calloc(1, sizeof(ha_handle_s));
