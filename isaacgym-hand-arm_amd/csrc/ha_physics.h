@@ -663,6 +663,30 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
         j3 = i3;
         k = 2 + (h2 ? 1 : 0) + (h3 ? 1 : 0);
     }
+#ifndef HA_EMIT_PARALLEL
+#define HA_EMIT_PARALLEL 1
+#endif
+    if (HA_EMIT_PARALLEL && !c.gather) {
+        int nc0 = s.nc;
+        if (nc0 + k <= c.maxc) {
+            // room for all k points (the common case): each chosen lane writes its own point into slot nc + t,
+            // the values lane 0 would write after broadcasting them (the chosen lanes are distinct)
+            if (lane == 0) { s.noff += k; s.nc = nc0 + k; }
+            float mu = contact_friction(c, a, b);
+            int t = lane == i0 ? 0 : (k > 1 && lane == j1 ? 1 : (k > 2 && lane == j2 ? 2 : (k > 3 && lane == j3 ? 3 : -1)));
+            if (t >= 0) {
+                ContactLDS& ct = c.k[nc0 + t];
+                st3(ct.x, pt);
+                st3(ct.n, n);
+                ct.sep = sep;
+                ct.mu = mu;
+                ct.a = a;
+                ct.b = b;
+            }
+            wsync();
+            return;
+        }
+    }
     // the chosen points to every lane
     f3 P[4], N[4];
     float S[4];

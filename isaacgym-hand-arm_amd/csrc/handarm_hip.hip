@@ -117,7 +117,7 @@ using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_c
 // ----------------------------------------------------------------------------- state load/store
 // Generic over the env layout in ha_model_t (actor / rigid-body creation order of the task).
 // take_force: consume st.object_force (ha_simulate = gym.simulate after apply_rigid_body_force_tensors)
-__device__ void load_env(SimCtx& c, const ha_state_t& st, int env, bool take_force = false) {
+__device__ __forceinline__ void load_env(SimCtx& c, const ha_state_t& st, int env, bool take_force = false) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     int lane = c.lane, D = c.D, NO = c.NO, A = m.n_actors;
@@ -158,7 +158,7 @@ __device__ void load_env(SimCtx& c, const ha_state_t& st, int env, bool take_for
 }
 
 // link twists into s.u.pd.Vl (level-synchronous); needs fk()
-__device__ void link_twists(SimCtx& c) {
+__device__ __forceinline__ void link_twists(SimCtx& c) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     int lane = c.lane, L = c.L;
@@ -206,7 +206,7 @@ __device__ float object_state(const SimCtx& c, int o, int k) {
 
 // writes dof_state, dof_force, sim targets, object root states, rigid_body_state and net_contact_force
 // (the refresh_* tensors). Leaves the link twists in s.u.pd.Vl for the task's observation snapshot.
-__device__ void store_env(SimCtx& c, const ha_state_t& st, int env) {
+__device__ __forceinline__ void store_env(SimCtx& c, const ha_state_t& st, int env) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     int lane = c.lane, D = c.D, NO = c.NO, A = m.n_actors, L = c.L, B = m.n_bodies;
@@ -243,7 +243,7 @@ __device__ void store_env(SimCtx& c, const ha_state_t& st, int env) {
 
 // Ur5Sih observation snapshot (what the observables read after refresh_*): from the LDS state after
 // store_env (same final kinematics)
-__device__ void ur5sih_obs_in(SimCtx& c, ObsIn* in) {
+__device__ __forceinline__ void ur5sih_obs_in(SimCtx& c, ObsIn* in) {
     EnvLDS& s = *c.s;
     int lane = c.lane, D = c.D, NO = c.NO;
     if (lane < 7) in->flange[lane] = lane < 3 ? s.lp[LINK_FLANGE][lane] : s.lq[LINK_FLANGE][lane - 3];
@@ -283,7 +283,7 @@ __device__ __forceinline__ void run_physics(SimCtx& c, int n_calls) {
 }
 
 // AllegroHand observation staging
-__device__ void ah_in_from_lds(SimCtx& c, AhIn* in) {
+__device__ __forceinline__ void ah_in_from_lds(SimCtx& c, AhIn* in) {
     EnvLDS& s = *c.s;
     int lane = c.lane, D = c.D;
     if (lane < D) {
@@ -307,7 +307,7 @@ __device__ void ah_in_from_tensors(SimCtx& c, const ha_state_t& st, int env, AhI
 }
 
 // AllegroKuka observation staging (palm = iiwa7_link_7, fingertips = *_link_3)
-__device__ void ak_in_from_lds(SimCtx& c, AkIn* in) {
+__device__ __forceinline__ void ak_in_from_lds(SimCtx& c, AkIn* in) {
     EnvLDS& s = *c.s;
     const ha_params_t& p = *c.p;
     int lane = c.lane, D = c.D;
