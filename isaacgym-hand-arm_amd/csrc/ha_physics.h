@@ -279,6 +279,7 @@ struct SimCtx {
     // narrow-phase cache: (hull, body) whose world vertices / planes are in ColScratch side A / side B. Within one
     // detect() the poses do not change, so consecutive pairs that share a side skip its setup (same values).
     int colA_h, colA_b, colB_h, colB_b;
+    bool colA_p;            // side A's world planes are in ColScratch too (SAT B runs first and may exit before them)
     bool gather;            // a compound object pair's piece pairs: reduced points go to ColScratch gp / gn
 #ifdef HA_AB_TIMING
     bool dry;               // A/B timing builds only: a repeated phase that must not emit contacts
@@ -859,15 +860,7 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     bool needA = ha != c.colA_h || keyA != c.colA_b, needB = hb != c.colB_h || keyB != c.colB_b;
     if (needA) {
         if (lane < nva) st3(cs.wvA[lane], PA.p + qrot(PA.q, scale3(c, a, ld3(m.verts[m.hull_vert_start[ha] + lane]))));
-        bool scA = body_scaled(c, a);
-        f3 isA = inv_scale(c, a);
-        for (int k = lane; k < npa; k += 64) {
-            f3 n; float d;
-            world_plane(m, ha, k, PA, scA, isA, n, d);
-            st3(cs.wpA[k], n);
-            cs.wpA[k][3] = d;
-        }
-        c.colA_h = ha; c.colA_b = keyA;
+        c.colA_h = ha; c.colA_b = keyA; c.colA_p = false;
     }
     if (needB) {
         if (lane < nvb) st3(cs.wvB[lane], PB.p + qrot(PB.q, scale3(c, b, ld3(m.verts[m.hull_vert_start[hb] + lane]))));
@@ -883,14 +876,30 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     }
     if (needA || needB) wsync();
     HPROF(25);
+    // B's face planes against A's vertices first: side A's planes (a link hull's up to 60) are only built when
+    // that test does not separate the pair. Either test alone separating means no contact, so the order changes
+    // no result
     float sepA, sepB;
     int kA, kB;
-    sat_planes(c, cs.wpA, npa, cs.wvB, nvb, sepA, kA);
-    HPROF(26);
-    if (sepA > mg) return;
     sat_planes(c, cs.wpB, npb, cs.wvA, nva, sepB, kB);
     HPROF(27);
     if (sepB > mg) return;
+    if (!c.colA_p) {
+        bool scA = body_scaled(c, a);
+        f3 isA = inv_scale(c, a);
+        for (int k = lane; k < npa; k += 64) {
+            f3 n; float d;
+            world_plane(m, ha, k, PA, scA, isA, n, d);
+            st3(cs.wpA[k], n);
+            cs.wpA[k][3] = d;
+        }
+        c.colA_p = true;
+        wsync();
+    }
+    HPROF(25);
+    sat_planes(c, cs.wpA, npa, cs.wvB, nvb, sepA, kA);
+    HPROF(26);
+    if (sepA > mg) return;
     for (int pass = 0; pass < 2; pass++) {
         bool refB = (sepB >= sepA) ? (pass == 0) : (pass == 1);
         int kr = refB ? kB : kA;
@@ -1055,6 +1064,7 @@ HD void detect(SimCtx& c) {
     int lane = c.lane;
     if (lane == 0) { s.nc = 0; s.noff = 0; }
     c.colA_h = c.colB_h = -1;       // poses changed since the last detect(): no cached hull sides
+    c.colA_p = false;
     c.colA_b = c.colB_b = -1000;
     int NO = c.NO, NLH = m.n_link_hulls, NS = m.n_static;
     int npairs = 0;
