@@ -20,7 +20,7 @@ from handarm_hip import model as HM
 
 pytestmark = pytest.mark.gpu
 
-N, E, P = 4096, 8, 10
+N, E, P = 4096, 8, 4       # P: HA_MAX_INIT_POSES
 
 
 def need_gpu():

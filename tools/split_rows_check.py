@@ -7,7 +7,7 @@ against a build that keeps every family on dense rows (-DHA_DENSE_ROWS).
     python tools/split_rows_check.py --compare gpurun_out/rows_dense.npz gpurun_out/rows_split.npz
 
 Scenes (bin-picking, 8 objects, 256 envs, 3 gym.simulate calls each): the settled-clutter test scene; three
-objects on hand link hulls (more link contacts than the family's LDS link slots (HA_LINK_SLOTS 8 for Ur5Sih, HB_LINK_SLOTS 2 for the clutter family) -> global spill rows); eight objects
+objects on hand link hulls (more link contacts than the family's LDS link slots (HA_LINK_SLOTS 4 for Ur5Sih, HB_LINK_SLOTS 2 for the clutter family, HA_AK_LINK_SLOTS 4 for AllegroKuka) -> global spill rows); eight objects
 on link hulls (contact list at capacity). Ur5Sih (3 objects, 256 envs, 3 calls): the test scene, and
 the three objects placed on hand link hulls (link contacts into the LDS link slots and beyond)."""
 import os
