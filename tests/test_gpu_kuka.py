@@ -128,6 +128,32 @@ def test_kuka_simulate_matches_oracle_bit_for_bit(seed, force, calls):
     assert np.all(get(sim, "object_force") == 0)                 # consumed by the call, like the oracle
 
 
+def test_kuka_link_contacts_spill_rows_match_oracle():
+    """AllegroKuka on split rows (HA_AK_LINK_SLOTS robot blocks in LDS, the rest in the env's global spill rows):
+    the cuboid placed inside the hand, on the palm, touches several links at once, so link contacts go past the
+    LDS slots. Bit-identical to the C oracle on every env."""
+    n = 128
+    sim, orc, st = _oracle_and_sim(n, 2, 0.0)
+    sim.simulate(1)                  # link poses of this scene
+    m = sim.model
+    B, A = m.n_bodies, m.n_actors
+    body = get(sim, "rigid_body_state").reshape(n, B, 13)
+    palm = int(sim.params.ak_palm_link)
+    rs = st["root_state"].reshape(n, A, 13)
+    rs[:, m.actor_object0, 0:3] = body[:, m.body_robot0 + palm, 0:3]
+    rs[:, m.actor_object0, 7:13] = 0.0
+    put(sim, "root_state", st["root_state"])
+    for k in ("dof_state", "sim_targets"):
+        put(sim, k, st[k])
+    sim.simulate(1)
+    orc.simulate(st, 1)
+    f = get(sim, "net_contact_force").reshape(n, B, 3)[:, m.body_robot0:m.body_robot0 + m.n_links]
+    touched = (np.abs(f).sum(-1) > 0).sum(1)
+    print("kuka link-contact scene: robot links in contact per env: median %d, max %d" % (np.median(touched), touched.max()))
+    assert touched.max() > 4, "no env has more link contacts than the LDS link slots"
+    scenes.assert_physics_bit_identical(sim, st, n, tag="kuka link contacts")
+
+
 @pytest.mark.parametrize("sub", ["regrasping", "reorientation"])
 def test_kuka_vectask_episode_at_full_size(sub):
     """C2 size (4096 envs): first step resets every env, then 150 random-action steps through the fused kernel;
