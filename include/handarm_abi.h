@@ -381,6 +381,8 @@ typedef struct ha_handle_s* ha_handle;
 int ha_abi_version(void);
 /* sizeof the three structs as compiled into the library (host-side mirror check) */
 int ha_struct_sizes(int32_t* model_size, int32_t* params_size, int32_t* state_size);
+/* HA_E_MODEL when the model exceeds what the task's kernel family is compiled for: DOF count, links, bodies, hulls
+ * larger than the family's narrow-phase scratch, pool size, and (AllegroKuka) pool objects of more than one hull */
 int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_envs, ha_handle* out);
 int ha_destroy(ha_handle h);
 int ha_bind_state(ha_handle h, const ha_state_t* state);

@@ -232,3 +232,19 @@ def test_create_rejects_hulls_beyond_the_family_scratch():
     model.hull_nverts[0] = 40
     h2 = C.c_void_p()
     assert lib.ha_create(C.byref(model), C.byref(params), 4, C.byref(h2)) != 0
+
+
+def test_create_rejects_compound_pool_objects():
+    """The AllegroKuka env block has no compound-object gather buffer (PhysCfg NG = 0): ha_create refuses a pool
+    object made of several hulls (HA_E_MODEL) instead of writing past the family's narrow-phase scratch."""
+    need_gpu()
+    import ctypes as C
+    from handarm_hip import _lib
+    scene = HM.load_scene(HM.KUKA_ASSET)
+    model = HM.build_model(scene)
+    params, _ = HM.build_params(task=HM.TASK_ALLEGRO_KUKA)
+    lib = _lib.load()
+    assert model.pool_hull[0] + 2 <= model.n_hulls
+    model.pool_nhull[0] = 2
+    h = C.c_void_p()
+    assert lib.ha_create(C.byref(model), C.byref(params), 4, C.byref(h)) == -4      # HA_E_MODEL
