@@ -92,15 +92,18 @@ struct ObjLDS {
     float osc[4];                       // per-env dimension scale of the pool hull; [3] = 1 when scaled
     float ofx[4];                       // world force on the COM for this physics call (apply_rigid_body_force)
     float om;                           // mass
-    int pool, coll, pad;                // pool id, collision enabled
+    int pool, coll;                     // pool id, collision enabled
 };
 
 // One contact point (LDS, after the object slots): up to MAXC x chunks per env (task_lds_bytes).
+// 32 bytes: the combined friction is not stored (contact_friction(a, b) again in the rows phase, the same
+// value), and the body codes fit 16 bits
 struct ContactLDS {
     float x[3], n[3];                   // world point, normal from body b to body a
-    float sep, mu;                      // separation (< 0: penetration), combined friction
-    int a, b;                           // body codes: -1 static, 0..NOBJ-1 object, 100 + link
+    float sep;                          // separation (< 0: penetration)
+    short a, b;                         // body codes: -1 static, 0..NOBJ-1 object, 100 + link
 };
+static_assert(sizeof(ContactLDS) == 32, "ContactLDS layout");
 
 struct EnvLDS {
     float q[MAXD], qd[MAXD], tgt[MAXD];
@@ -673,16 +676,14 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
             // room for all k points (the common case): each chosen lane writes its own point into slot nc + t,
             // the values lane 0 would write after broadcasting them (the chosen lanes are distinct)
             if (lane == 0) { s.noff += k; s.nc = nc0 + k; }
-            float mu = contact_friction(c, a, b);
             int t = lane == i0 ? 0 : (k > 1 && lane == j1 ? 1 : (k > 2 && lane == j2 ? 2 : (k > 3 && lane == j3 ? 3 : -1)));
             if (t >= 0) {
                 ContactLDS& ct = c.k[nc0 + t];
                 st3(ct.x, pt);
                 st3(ct.n, n);
                 ct.sep = sep;
-                ct.mu = mu;
-                ct.a = a;
-                ct.b = b;
+                ct.a = (short)a;
+                ct.b = (short)b;
             }
             wsync();
             return;
@@ -721,7 +722,6 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
     // lane 0 appends, or (list full) replaces the shallowest contact if this one is deeper: the shallowest is the first
     // maximum of sep over the list (the oracle's sequential strict-compare scan), found by a wave arg-max over
     // lanes = contacts instead of a scan on lane 0 (clutter scenes run with the list full)
-    float mu = contact_friction(c, a, b);
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         if (t >= k) break;
@@ -745,9 +745,8 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
             st3(ct.x, P[t]);
             st3(ct.n, N[t]);
             ct.sep = S[t];
-            ct.mu = mu;
-            ct.a = a;
-            ct.b = b;
+            ct.a = (short)a;
+            ct.b = (short)b;
         }
         wsync();
     }
@@ -1354,7 +1353,7 @@ HD void substep(SimCtx& c, float hdt) {
         int r = MAXR * ch + lane;
         if (lane < MAXR && r < nr) {
             const ContactLDS& ct = c.k[r / 3];
-            cmu_ = ct.mu;
+            cmu_ = contact_friction(c, ct.a, ct.b);
             int k = r % 3;
             // robot block Jr / Yr (null: the contact touches no link, the block is zero) and object blocks Jo / Yo
             float *Jr, *Yr, *Jo, *Yo;

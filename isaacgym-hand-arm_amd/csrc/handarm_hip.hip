@@ -93,7 +93,7 @@ __host__ __device__ constexpr int task_waves_per_eu() {
 template <int FAM>
 __host__ __device__ constexpr int task_col_verts() { return (FAM == HA_TASK_ALLEGRO_KUKA || FAM == HA_TASK_ALLEGRO_HAND) ? 32 : 64; }
 template <int FAM>
-__host__ __device__ constexpr int task_col_planes() { return (FAM == HA_TASK_ALLEGRO_KUKA || FAM == HA_TASK_ALLEGRO_HAND) ? 64 : 128; }
+__host__ __device__ constexpr int task_col_planes() { return (FAM == HA_TASK_ALLEGRO_KUKA || FAM == HA_TASK_ALLEGRO_HAND) ? 64 : 124; }
 // AllegroKuka env block (PhysCfg SPLIT / NG / MU): split rows with HA_AK_LINK_SLOTS link contacts in LDS, no
 // compound-object gather buffer (its one object is a cuboid; ha_create enforces one hull per pool object) and
 // S ~ M^-1 inside the phase union: 13.3 -> 9.1 KB, so 16 workgroups per CU hold the 4096 envs of config C2 in
