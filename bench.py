@@ -487,6 +487,7 @@ def main():
 
     from handarm_hip import parallel
     rank, local_rank, world, device = parallel.init_distributed("nccl")
+    dist_info = parallel.describe()          # backend + the rank count an all-reduce over the group sees
 
     def log_interval(task, env):
         if task == "allegro_kuka":
@@ -535,6 +536,7 @@ def main():
                    "observations": "point-cloud student list (Ur5SihMultiObjectManipulation.yaml:45)"
                    if args.pointclouds and task in ("ur5sih", "binpick") else "default"},
         "roofline": h["roofline"], "compute_roofline": h["compute_roofline"], "cpu_baseline": h.get("cpu_baseline"),
+        "distributed": dist_info,
     }
     for k in ("episode_successes_mean", "consecutive_successes", "success_rate_ewma", "contacts", "pointcloud_roofline"):
         if k in h:

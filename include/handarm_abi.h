@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 9
+#define HA_ABI_VERSION 10
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -52,6 +52,9 @@ extern "C" {
 #define HA_MAX_HULLS 64
 #define HA_MAX_VERTS 4096
 #define HA_MAX_PLANES 8192
+#define HA_MAX_EDGES 8192      /* hull edges, all hulls (v10) */
+#define HA_MAX_LOOP 16384      /* face-loop entries, all hulls (v10): 2 per edge */
+#define HA_MAX_FACE_LOOP 21    /* vertices of one face loop (v10): a clipped manifold's 2 x 21 + 21 candidates fit a wave */
 #define HA_MAX_POOL 32
 #define HA_MAX_OBJ 8           /* objects per env: 3 in Ur5SihMultiObject.yaml:2, 8 for bin-picking (config 5) */
 #define HA_MAX_STATIC 10       /* static boxes per env (table, or table-with-hole walls + bin pieces) */
@@ -160,6 +163,21 @@ typedef struct ha_model_t {
      * object run the narrow phase piece by piece (A's pieces outer, B's inner). */
     int32_t pool_nhull[HA_MAX_POOL];
     float pool_center[HA_MAX_POOL][3], pool_radius[HA_MAX_POOL];
+    /* v10: hull topology (handarm_hip/model.py hull_topology, from each hull's convex-hull triangulation), for the
+     * edge-edge SAT axes and the clipped face manifolds of the narrow phase.
+     *   edges[hull_edge_start[h] + i] = v0 | v1 << 8 | f0 << 16 | f1 << 24: edge i of hull h, its hull-local
+     *     vertices and the two faces (hull-local plane indices) it separates; v0 -> v1 runs counter-clockwise about
+     *     f0's outward normal.
+     *   plane_loop[p] = start | count << 16: the face of (global) plane p as a counter-clockwise loop (about its
+     *     outward normal) of hull-local vertices loop_v[start .. start + count), count <= HA_MAX_FACE_LOOP. */
+    int32_t hull_edge_start[HA_MAX_HULLS], hull_nedges[HA_MAX_HULLS];
+    uint32_t edges[HA_MAX_EDGES];
+    int32_t plane_loop[HA_MAX_PLANES];
+    uint8_t loop_v[HA_MAX_LOOP];
+    /* v10: joint (Coulomb) friction per DOF, a PGS row with |impulse| <= dof_friction h (Isaac Gym DOF property
+     * "friction": AllegroHand 0.01, allegro_hand.py:267; AllegroKuka the URDF's <dynamics friction>,
+     * AllegroKuka.yaml:58 dofFriction -1; Ur5Sih 0 from its URDF) */
+    float dof_friction[HA_MAX_DOFS];
 } ha_model_t;
 
 /* Simulation + task parameters (Ur5SihBase.yaml, Ur5SihMultiObject*.yaml). */
@@ -248,6 +266,14 @@ typedef struct ha_params_t {
      * higher up a rounded side would otherwise displace the true support corners). */
     float contact_slop;                /* 0.001 m */
     float manifold_window;             /* 0.002 m */
+    /* v10: robot link velocity damping (asset_options linear_damping / angular_damping: Ur5Sih 0.01 / 0.01,
+     * ur5sih.py:178-179; AllegroKuka 0.01 / 0.01, allegro_kuka_base.py:565-566; AllegroHand 0 / 0.01,
+     * allegro_hand.py:231), a damping wrench on every link's COM twist in the velocity-product forces */
+    float link_lin_damping, link_ang_damping;
+    /* v10: a hull pair's contact comes from its deepest edge-edge axis (one point at the edges' closest points)
+     * when that axis separates by more than edge_rel_tol x the best face axis + edge_abs_tol, else from the
+     * clipped face manifold (Gregorius, "The Separating Axis Test between Convex Polyhedra", GDC 2013) */
+    float edge_rel_tol, edge_abs_tol;
 } ha_params_t;
 
 /* Device buffers (caller-allocated). Layouts match the Isaac Gym tensors exactly. */

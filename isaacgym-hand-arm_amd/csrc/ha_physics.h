@@ -471,6 +471,17 @@ HD void dynamics(SimCtx& c) {
         inert_apply(I, vw, vv, n2, f2);
         f3 fn = n1 + (cross3(vw, n2) + cross3(vv, f2));
         f3 ff = f1 + cross3(vw, f2);
+        // link damping (ha_params_t v10): the wrench cl m v_com, ca I_com w (moment about the world origin) with the
+        // momentum (n2, f2) = (I_com w + c x m v_com, m v_com): g = c x m v_com = h x f2 / m
+        float cl = c.p->link_lin_damping, ca = c.p->link_ang_damping;
+#ifdef HA_X_NODAMP
+        cl = ca = 0.0f;
+#endif
+        if (cl != 0.0f || ca != 0.0f) {
+            f3 g = I.m > 0.0f ? cross3(I.h, f2) * (1.0f / I.m) : mk3(0, 0, 0);
+            fn = fn + ((n2 - g) * ca + g * cl);
+            ff = ff + f2 * cl;
+        }
         st3(&s.u.pd.dyn.Fl[i][0], fn); st3(&s.u.pd.dyn.Fl[i][3], ff);
     }
     wsync();
@@ -626,6 +637,8 @@ HD f3 inv_scale(const SimCtx& c, int b) {
     return mk3(1.0f / sc[0], 1.0f / sc[1], 1.0f / sc[2]);
 }
 
+HD void store_chosen(SimCtx& c, int k, const f3* P, const f3* N, const float* S, int a, int b);
+
 // append up to 4 reduced contacts (lane 0 does the list bookkeeping, same policy as the oracle). n is the
 // lane's normal: one value over the wave for a convex pair; a compound object pair's gathered points keep
 // their piece pair's normal, and the area criterion then measures about the deepest point's normal. While
@@ -699,6 +712,14 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
         N[t] = mk3(bcast(n.x, src), bcast(n.y, src), bcast(n.z, src));
         S[t] = bcast(sep, src);
     }
+    store_chosen(c, k, P, N, S, a, b);
+}
+
+// the k <= 4 chosen points of a manifold (wave-uniform P, N, S) into the gather buffer (a compound pair's piece
+// pairs) or the contact list: lane 0 appends, or (list full) replaces the shallowest contact if the new one is deeper
+HD void store_chosen(SimCtx& c, int k, const f3* P, const f3* N, const float* S, int a, int b) {
+    EnvLDS& s = *c.s;
+    int lane = c.lane;
     if (c.gather) {
         // compound pair: the chosen points (in the oracle's index order) join the gather buffer
         if (lane == 0) {
@@ -834,6 +855,85 @@ HD void sat_planes(const SimCtx& c, const float (*wp)[4], int np, const float (*
     kbest = bk;
 }
 
+// side plane of edge j of a face loop (world vertices wv, loop vertex indices lv[0..n), face normal nf): the plane
+// through the edge perpendicular to the face, unit outward normal cross(e, nf) (the loop runs counter-clockwise about
+// nf), offset d
+HD f3 side_plane(const float (*wv)[4], const uint8_t* lv, int j, int n, f3 nf, float& d) {
+    f3 v0 = ld3(wv[lv[j]]);
+    f3 sn = cross3(ld3(wv[lv[j + 1 == n ? 0 : j + 1]]) - v0, nf);
+    sn = sn * (1.0f / sqrtf(dot3(sn, sn)));
+    d = -dot3(sn, v0);
+    return sn;
+}
+// squared distance from point q to the segment p0 + t (p1 - p0), t in [0, 1] (the oracle's seg_point_d2)
+HD float seg_point_d2(f3 p0, f3 p1, f3 q) {
+    f3 d = p1 - p0;
+    float dd = dot3(d, d);
+    float t = dd > 0.0f ? dot3(q - p0, d) / dd : 0.0f;
+    t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
+    f3 r = q - (p0 + d * t);
+    return dot3(r, r);
+}
+// the edges of one hull (records E[0..ne), world vertices wv) within sqrt(r2) of the other hull's centre ctr, as a
+// byte list of edge indices in edge order (an edge farther away cannot touch the other hull); returns the count
+HD int edge_cull(const SimCtx& c, const uint32_t* E, int ne, const float (*wv)[4], f3 ctr, float r2, uint8_t* out) {
+    int n = 0;
+#pragma unroll 1
+    for (int base = 0; base < ne; base += 64) {
+        int i = base + c.lane;
+        bool keep = false;
+        if (i < ne) {
+            uint32_t e = E[i];
+            keep = seg_point_d2(ld3(wv[e & 255u]), ld3(wv[(e >> 8) & 255u]), ctr) <= r2;
+        }
+        uint64_t mk = __ballot(keep);
+        if (keep) out[n + __popcll(mk & ((1ull << c.lane) - 1ull))] = (uint8_t)i;
+        n += __popcll(mk);
+    }
+    return n;
+}
+// Edge pair (ea of hull A, eb of hull B; edge records v0 | v1 << 8 | f0 << 16 | f1 << 24) of the edge-edge SAT
+// (Gregorius, GDC 2013): when the Gauss-map arcs of the two edges (between their faces' normals; B's negated)
+// cross, the pair is a face of the Minkowski difference and N = e1 x e2, oriented away from B's centre cb, is a
+// separating-axis candidate with separation N . (pA - pB). Returns -3e38 for any other pair (arcs apart, or edges
+// within 0.3 degrees of parallel). n, pa / e1, pb / e2: the axis and the edges (start, direction).
+HD float edge_axis(const ColView& cs, uint32_t ea, uint32_t eb, f3 cb, f3& n, f3& pa, f3& e1, f3& pb, f3& e2) {
+    f3 a = ld3(cs.wpA[(ea >> 16) & 255u]), b = ld3(cs.wpA[ea >> 24]);
+    f3 cc = ld3(cs.wpB[(eb >> 16) & 255u]) * -1.0f, dd = ld3(cs.wpB[eb >> 24]) * -1.0f;
+    f3 bxa = cross3(b, a), dxc = cross3(dd, cc);
+    float cba = dot3(cc, bxa), dba = dot3(dd, bxa), adc = dot3(a, dxc), bdc = dot3(b, dxc);
+    if (!(cba * dba < 0.0f && adc * bdc < 0.0f && cba * bdc > 0.0f)) return -3.0e38f;
+    pa = ld3(cs.wvA[ea & 255u]);
+    e1 = ld3(cs.wvA[(ea >> 8) & 255u]) - pa;
+    pb = ld3(cs.wvB[eb & 255u]);
+    e2 = ld3(cs.wvB[(eb >> 8) & 255u]) - pb;
+    n = cross3(e1, e2);
+    float l2 = dot3(n, n);
+    if (l2 < 2.5e-5f * (dot3(e1, e1) * dot3(e2, e2))) return -3.0e38f;
+    n = n * (1.0f / sqrtf(l2));
+    if (dot3(n, pb - cb) < 0.0f) n = n * -1.0f;
+    return dot3(n, pa - pb);
+}
+// midpoint of the closest points of the segments pa + s e1 and pb + t e2 (s, t in [0, 1]; not parallel)
+HD f3 edge_closest_mid(f3 pa, f3 e1, f3 pb, f3 e2) {
+    f3 r = pa - pb;
+    float aa = dot3(e1, e1), ee = dot3(e2, e2), bb = dot3(e1, e2), cc = dot3(e1, r), ff = dot3(e2, r);
+    float den = aa * ee - bb * bb;
+    float sa = den > 0.0f ? (bb * ff - cc * ee) / den : 0.0f;
+    sa = sa < 0.0f ? 0.0f : (sa > 1.0f ? 1.0f : sa);
+    float tb = (bb * sa + ff) / ee;
+    if (tb < 0.0f) {
+        tb = 0.0f;
+        sa = -cc / aa;
+        sa = sa < 0.0f ? 0.0f : (sa > 1.0f ? 1.0f : sa);
+    } else if (tb > 1.0f) {
+        tb = 1.0f;
+        sa = (bb - cc) / aa;
+        sa = sa < 0.0f ? 0.0f : (sa > 1.0f ? 1.0f : sa);
+    }
+    return ((pa + e1 * sa) + (pb + e2 * tb)) * 0.5f;
+}
+
 // hull A (body a) vs hull B (body b); normal from B to A. keyA / keyB identify the posed hull of each side for
 // the ColScratch cache (the body code, or -100 - k for static body k: statics may share a hull)
 HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int b, int keyA, int keyB) {
@@ -899,15 +999,70 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     sat_planes(c, cs.wpA, npa, cs.wvB, nvb, sepA, kA);
     HPROF(26);
     if (sepA > mg) return;
+    // ---- edge-edge axes (v10): a hull pair whose face axes leave it within the margin may still be separated along,
+    //      or touch through, a pair of edges
+    int nea = m.hull_nedges[ha], neb = m.hull_nedges[hb];
+#ifdef HA_X_NOEDGE
+    nea = 0;
+#endif
+    if (nea > 0 && neb > 0) {
+        float smax = fmaxf(sepA, sepB);
+        float pen = smax < 0.0f ? -smax : 0.0f;
+        float RA = (scale_radius(c, a, m.hull_radius[ha]) + mg) + pen;
+        float RB = (scale_radius(c, b, m.hull_radius[hb]) + mg) + pen;
+        uint8_t* la = reinterpret_cast<uint8_t*>(cs.cand);
+        uint8_t* lb = reinterpret_cast<uint8_t*>(cs.cmax);
+        const uint32_t* EA = m.edges + m.hull_edge_start[ha];
+        const uint32_t* EB = m.edges + m.hull_edge_start[hb];
+        int nA = edge_cull(c, EA, nea, cs.wvA, cb, RB * RB, la);
+        int nB = edge_cull(c, EB, neb, cs.wvB, ca, RA * RA, lb);
+        wsync();
+        float best = -3.0e38f;
+        int bw = 1 << 30;
+        int total = nA * nB;
+        if (total > 0) {
+            int i = lane / nB, j = lane - i * nB;
+            int si = 64 / nB, sj = 64 - si * nB;
+#pragma unroll 1
+            for (int w = lane; w < total; w += 64) {
+                f3 n, pa, pb, e1, e2;
+                float sv = edge_axis(cs, EA[la[i]], EB[lb[j]], cb, n, pa, e1, pb, e2);
+                if (sv > best) { best = sv; bw = w; }
+                i += si;
+                j += sj;
+                if (j >= nB) { j -= nB; i++; }
+            }
+        }
+        wave_argmax(best, bw);
+        HPROF(30);
+        if (best > mg) return;                              // separated along an edge-edge axis
+        if (best > c.p->edge_rel_tol * smax + c.p->edge_abs_tol) {
+            // edge contact: one point midway between the edges' closest points, normal the axis
+            int bi = bw / nB;
+            f3 n, pa, pb, e1, e2;
+            edge_axis(cs, EA[la[bi]], EB[lb[bw - bi * nB]], cb, n, pa, e1, pb, e2);
+            f3 x = edge_closest_mid(pa, e1, pb, e2);
+            emit_contacts(c, lane == 0, x, best, n, a, b);
+            return;
+        }
+        wsync();                                            // the edge lists (cand / cmax) are reused below
+    }
+    // ---- face contact: the reference face (the face axis of larger separation; the other if it yields nothing) and
+    //      the incident hull, candidates (1) incident vertices near the reference face and inside its hull's other
+    //      planes, (2) the incident face's edges clipped to the reference face's side planes, (3) the reference face's
+    //      vertices over the incident face
     for (int pass = 0; pass < 2; pass++) {
         bool refB = (sepB >= sepA) ? (pass == 0) : (pass == 1);
         int kr = refB ? kB : kA;
-        int nvi = refB ? nva : nvb, npr = refB ? npb : npa;
+        int hr = refB ? hb : ha, hi = refB ? ha : hb;
+        int nvi = refB ? nva : nvb, npr = refB ? npb : npa, npi = refB ? npa : npb;
         const float (*wpr)[4] = refB ? cs.wpB : cs.wpA;
+        const float (*wpi)[4] = refB ? cs.wpA : cs.wpB;
         const float (*wvi)[4] = refB ? cs.wvA : cs.wvB;
+        const float (*wvr)[4] = refB ? cs.wvB : cs.wvA;
         f3 nref = ld3(wpr[kr]);
         float dref = wpr[kr][3];
-        // incident vertices within the margin of the reference face
+        // (1) incident vertices within the margin of the reference face
         f3 vi = mk3(0, 0, 0);
         float dist = 0;
         bool cand = false;
@@ -941,15 +1096,83 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         }
         wsync();
         HPROF(28);
-        bool valid = false;
-        f3 pt = mk3(0, 0, 0);
-        if (cand && ord2f(cs.cmax[slot]) <= mg) {
-            valid = true;
-            pt = vi - nref * (0.5f * dist);
+        bool valid = cand && ord2f(cs.cmax[slot]) <= mg;
+        // the candidate set, one per lane in the oracle's list order: lanes [0, nv1) the valid incident vertices
+        // in vertex order (moved there by a forward permute), then, from lane nv1 on, the incident-face edges'
+        // entry / exit points and the reference-face vertices (lanes past 63 dropped, as by the oracle)
+        uint64_t vm = __ballot(valid);
+        int nv1 = __popcll(vm);
+        int rk = __popcll(vm & ((1ull << lane) - 1ull));
+        int to = valid ? rk : nv1 + (lane - rk);        // a permutation of the lanes
+        f3 pt = vi - nref * (0.5f * dist);
+        f3 x = mk3(__int_as_float(__builtin_amdgcn_ds_permute(to << 2, __float_as_int(pt.x))),
+                   __int_as_float(__builtin_amdgcn_ds_permute(to << 2, __float_as_int(pt.y))),
+                   __int_as_float(__builtin_amdgcn_ds_permute(to << 2, __float_as_int(pt.z))));
+        float sv = __int_as_float(__builtin_amdgcn_ds_permute(to << 2, __float_as_int(dist)));
+        bool ok = lane < nv1;
+        // the incident face: the incident hull's face most anti-parallel to the reference normal (first minimum)
+        float vmin = 3.0e38f;
+        int ki = 1 << 20;
+        for (int kk = lane; kk < npi; kk += 64) {
+            float dv = dot3(ld3(wpi[kk]), nref);
+            if (dv < vmin) { vmin = dv; ki = kk; }
         }
-        if (__ballot(valid)) {
+        wave_argmin(vmin, ki);
+        int lpi = m.plane_loop[m.hull_plane_start[hi] + ki], lpr = m.plane_loop[m.hull_plane_start[hr] + kr];
+        int li0 = lpi & 0xFFFF, lni = lpi >> 16, lr0 = lpr & 0xFFFF, lnr = lpr >> 16;
+#ifdef HA_X_NOCLIP
+        lni = 0; lnr = 0;
+#endif
+        f3 ni = ld3(wpi[ki]);
+        float di = wpi[ki][3];
+        float den = dot3(ni, nref);
+        int q = lane - nv1;
+        if (q >= 0 && q < 2 * lni) {
+            // (2) incident-face loop edge q / 2 clipped (Cyrus-Beck) to the reference face's side planes (through its
+            //     loop edges, perpendicular to it: side_plane): the entry (even q) or exit (odd q) point, when inside
+            //     the segment and within the margin of the reference face
+            int je = q >> 1;
+            f3 p0 = ld3(wvi[m.loop_v[li0 + je]]);
+            f3 p1 = ld3(wvi[m.loop_v[li0 + (je + 1 == lni ? 0 : je + 1)]]);
+            float tin = 0.0f, tout = 1.0f;
+            bool out = false;
+            for (int jj = 0; jj < lnr; jj++) {
+                float sd;
+                f3 sn = side_plane(wvr, m.loop_v + lr0, jj, lnr, nref, sd);
+                float f0 = dot3(sn, p0) + sd, f1 = dot3(sn, p1) + sd;
+                if (f0 > 0.0f && f1 > 0.0f) out = true;
+                else if (f0 > 0.0f) tin = fmaxf(tin, f0 / (f0 - f1));
+                else if (f1 > 0.0f) tout = fminf(tout, f0 / (f0 - f1));
+            }
+            bool ex = (q & 1) != 0;
+            f3 xc = p0 + (p1 - p0) * (ex ? tout : tin);
+            float dx = dot3(nref, xc) + dref;
+            ok = !out && (ex ? (tout < 1.0f && tin < tout) : (tin > 0.0f && tin <= tout)) && dx <= mg;
+            x = xc - nref * (0.5f * dx);
+            sv = dx;
+        } else if (q >= 2 * lni && q < 2 * lni + lnr) {
+            // (3) reference-face loop vertex q - 2 lni projected along the reference normal onto the incident face's
+            //     plane: a candidate when inside the incident face's side planes and within the margin
+            ok = false;
+            if (den < -1e-6f) {
+                f3 r = ld3(wvr[m.loop_v[lr0 + (q - 2 * lni)]]);
+                float sr = -(dot3(ni, r) + di) / den;
+                f3 xr = r + nref * sr;
+                float mx = -3.0e38f;
+                for (int jj = 0; jj < lni; jj++) {
+                    float sd;
+                    f3 sn = side_plane(wvi, m.loop_v + li0, jj, lni, ni, sd);
+                    mx = fmaxf(mx, dot3(sn, xr) + sd);
+                }
+                ok = sr <= mg && mx <= 0.0f;
+                x = r + nref * (0.5f * sr);
+                sv = sr;
+            }
+        }
+        HPROF(31);
+        if (__ballot(ok)) {
             f3 n = refB ? nref : nref * -1.0f;
-            emit_contacts(c, valid, pt, dist, n, a, b);
+            emit_contacts(c, ok, x, sv, n, a, b);
             HPROF(29);
             return;
         }
@@ -1478,8 +1701,13 @@ HD void substep(SimCtx& c, float hdt) {
     //      lower/upper joint limits (hard, unilateral)
     float dgam = 0.f, dbias = 0.f, dwinv = 0.f, dlim = 0.f, dlam = 0.f;
     float lwinv = 0.f, vt_lo = 0.f, vt_up = 0.f, lam_lo = 0.f, lam_up = 0.f;
+    float flim = 0.f, lam_fr = 0.f;     // joint friction row (v10): |impulse| <= dof_friction h, target velocity 0
     int act_lo = 0, act_up = 0;
     if (lane < D) {
+        flim = m.dof_friction[lane] * hdt;
+#ifdef HA_X_NOFRIC
+        flim = 0.0f;
+#endif
         float kp = m.dof_kp[lane], kd = m.dof_kd[lane];
         float den = kd + hdt * kp;
         float mii = c.Minv[lane * D + lane];
@@ -1494,7 +1722,7 @@ HD void substep(SimCtx& c, float hdt) {
         vt_lo = s_lo > 0 ? -s_lo / hdt : -p.baumgarte * s_lo / hdt;
         vt_up = s_up > 0 ? -s_up / hdt : -p.baumgarte * s_up / hdt;
     }
-    const uint64_t lo_mask = __ballot(act_lo != 0), up_mask = __ballot(act_up != 0);
+    const uint64_t lo_mask = __ballot(act_lo != 0), up_mask = __ballot(act_up != 0), fr_mask = __ballot(flim > 0.0f);
     // generalized velocity: coordinate `lane` in vreg, coordinate 64 + lane in vregh (VW == 2 only)
     float vreg = lane < NV ? s.v[lane] : 0.0f;
     float vregh = (VW == 2 && lane + 64 < NV) ? s.v[lane + 64] : 0.0f;
@@ -1537,6 +1765,15 @@ HD void substep(SimCtx& c, float hdt) {
                 if (d1 != 0.0f) {
                     if (lane == d) lam_up = n1;
                     vreg -= mrow * d1;
+                }
+            }
+            if ((fr_mask >> d) & 1ull) {
+                float nf = lam_fr - vreg * lwinv;
+                nf = nf < -flim ? -flim : (nf > flim ? flim : nf);
+                float df = bcast(nf - lam_fr, d);
+                if (df != 0.0f) {
+                    if (lane == d) lam_fr = nf;
+                    vreg += mrow * df;
                 }
             }
         }
@@ -1664,7 +1901,7 @@ HD void substep(SimCtx& c, float hdt) {
         for (int ch = 0; ch < NCH; ch++)
             if (lane < MAXR) s.u.xfer[MAXR * ch + lane] = rk(0, MAXR * ch + lane);
     }
-    if (lane < D) s.u.pd.dforce[lane] = ((dlam + lam_lo) - lam_up) / hdt;
+    if (lane < D) s.u.pd.dforce[lane] = (((dlam + lam_lo) - lam_up) + lam_fr) / hdt;
     wsync();
     if (lane < NV) s.v[lane] = vreg;
     if (VW == 2 && lane + 64 < NV) s.v[lane + 64] = vregh;

@@ -82,10 +82,14 @@ template <int FAM>
 __host__ __device__ constexpr int task_chunk_capacity() {
     return FAM == HA_TASK_ALLEGRO_KUKA ? HA_AK_CONTACTS : (FAM == HA_TASK_ALLEGRO_HAND ? HA_AH_CONTACTS : MAXC);
 }
+#ifndef HB_WAVES_PER_EU
+#define HB_WAVES_PER_EU 3
+#endif
 template <int FAM>
 __host__ __device__ constexpr int task_waves_per_eu() {
     return FAM == HA_TASK_UR5SIH ? HA_WAVES_PER_EU
-           : (FAM == HA_TASK_ALLEGRO_KUKA ? HA_AK_WAVES_PER_EU : (FAM == HA_TASK_ALLEGRO_HAND ? HA_AH_WAVES_PER_EU : 1));
+           : (FAM == HA_TASK_ALLEGRO_KUKA ? HA_AK_WAVES_PER_EU
+                                          : (FAM == HA_TASK_ALLEGRO_HAND ? HA_AH_WAVES_PER_EU : HB_WAVES_PER_EU));
 }
 // largest hull a family's narrow-phase scratch holds: the YCB pool hulls have up to 64 vertices and 124 face
 // planes; the Allegro scenes' hulls (cooked to <= 32 vertices, <= 60 planes) take half, which puts the
@@ -726,8 +730,20 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
                       FamPhys<HA_TASK_UR5SIH>::colv == FamPhys<FAM_UR5SIH_CLUTTER>::colv &&
                       FamPhys<HA_TASK_UR5SIH>::colp == FamPhys<FAM_UR5SIH_CLUTTER>::colp,
                   "narrow-phase scratch limits per family pair");
-    for (int k = 0; k < model->n_hulls; k++)
+    for (int k = 0; k < model->n_hulls; k++) {
         if (model->hull_nverts[k] > col_v || model->hull_nplanes[k] > col_p) return HA_E_MODEL;
+        // v10 topology: the edge-edge SAT keeps a hull's culled edge list as bytes in the scratch's candidate arrays
+        // (4 x col_v bytes each); a clipped manifold's candidates take 2 lanes per incident loop edge and one per
+        // reference loop vertex (FaceCands), so loops hold <= HA_MAX_FACE_LOOP vertices
+        if (model->hull_nedges[k] < 0 || model->hull_nedges[k] > 4 * col_v || model->hull_nplanes[k] > 256 ||
+            model->hull_edge_start[k] < 0 || model->hull_edge_start[k] + model->hull_nedges[k] > HA_MAX_EDGES)
+            return HA_E_MODEL;
+        for (int j = 0; j < model->hull_nplanes[k]; j++) {
+            int pl = model->plane_loop[model->hull_plane_start[k] + j];
+            if ((pl >> 16) < 3 || (pl >> 16) > HA_MAX_FACE_LOOP || (pl & 0xFFFF) + (pl >> 16) > HA_MAX_LOOP)
+                return HA_E_MODEL;
+        }
+    }
     // a family without a gather buffer (ColLayout NG = 0) takes single-hull pool objects only
     bool one_hull = fam == HA_TASK_ALLEGRO_KUKA && FamPhys<HA_TASK_ALLEGRO_KUKA>::colg == 0;
     for (int i = 0; i < model->n_pool; i++)

@@ -22,6 +22,7 @@ KUKA_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", 
 BIN_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "ur5sih_bin_scene.json")
 
 MAX_LINKS, MAX_DOFS, MAX_HULLS, MAX_VERTS, MAX_PLANES = 32, 24, 64, 4096, 8192
+MAX_EDGES, MAX_LOOP, MAX_FACE_LOOP = 8192, 16384, 21
 MAX_POOL, MAX_OBJ, MAX_INIT_POSES, MAX_SPLINE_PIECES, N_SPLINES = 32, 8, 4, 8, 8
 MAX_STATIC = 10
 MAX_FIXED_BODIES = 8
@@ -82,6 +83,10 @@ class HaModel(C.Structure):
         ("static_quat", arr(f32, MAX_STATIC, 4)), ("static_half", arr(f32, MAX_STATIC, 3)),
         ("n_fixed_bodies", i32), ("body_fixed0", i32), ("body_fixed_pose", arr(f32, MAX_FIXED_BODIES, 7)),
         ("pool_nhull", arr(i32, MAX_POOL)), ("pool_center", arr(f32, MAX_POOL, 3)), ("pool_radius", arr(f32, MAX_POOL)),
+        ("hull_edge_start", arr(i32, MAX_HULLS)), ("hull_nedges", arr(i32, MAX_HULLS)),          # v10
+        ("edges", arr(C.c_uint32, MAX_EDGES)), ("plane_loop", arr(i32, MAX_PLANES)),
+        ("loop_v", arr(C.c_uint8, MAX_LOOP)),
+        ("dof_friction", arr(f32, MAX_DOFS)),
     ]
 
 
@@ -122,6 +127,7 @@ class HaParams(C.Structure):
         ("ak_fingertip_offsets", arr(f32, 4, 3)), ("ak_palm_link", i32), ("ak_fingertip_links", arr(i32, 4)),
         ("ak_num_arm_dofs", i32),
         ("contact_slop", f32), ("manifold_window", f32),                       # v9
+        ("link_lin_damping", f32), ("link_ang_damping", f32), ("edge_rel_tol", f32), ("edge_abs_tol", f32),  # v10
     ]
 
 
@@ -208,6 +214,86 @@ def load_scene(path=ASSET):
     return scene
 
 
+def _ccw_polygon(pts2):
+    """Indices of the 2D convex hull of pts2 in counter-clockwise order (Andrew's monotone chain; collinear
+    boundary points dropped), starting at the lexicographically smallest point."""
+    order = sorted(range(len(pts2)), key=lambda i: (pts2[i][0], pts2[i][1]))
+
+    def cross(o, a, b):
+        return (pts2[a][0] - pts2[o][0]) * (pts2[b][1] - pts2[o][1]) - (pts2[a][1] - pts2[o][1]) * (pts2[b][0] - pts2[o][0])
+    lower, upper = [], []
+    for i in order:
+        while len(lower) >= 2 and cross(lower[-2], lower[-1], i) <= 0:
+            lower.pop()
+        lower.append(i)
+    for i in reversed(order):
+        while len(upper) >= 2 and cross(upper[-2], upper[-1], i) <= 0:
+            upper.pop()
+        upper.append(i)
+    return lower[:-1] + upper[:-1]
+
+
+def hull_topology(verts, planes, tol=2e-7):
+    """Edges and face loops of a convex hull given its vertices and face planes (tools/build_model.py hull_planes).
+
+    The face of plane k is the convex polygon of the hull vertices within tol of the plane (hull_planes merged
+    coplanar facets whose offsets agree to 1e-7), counter-clockwise about the outward normal. The plane across a
+    loop edge is, of the other planes through both its vertices, the one whose normal differs most from plane k's
+    (a hull can keep near-duplicate planes of one face apart, and those are not neighbours). A hull edge is a loop
+    edge between two planes that are not near-duplicates (normals within 1e-6).
+
+    Returns (edges, loops): edges = [(v0, v1, f0, f1)], each hull edge once, with v0 -> v1 counter-clockwise about
+    f0's outward normal and f1 the plane across; loops[k] = [(v, adj)], the face of plane k as a counter-clockwise
+    vertex loop, adj = the plane across the loop edge v -> next v. Indices are hull-local."""
+    v = np.asarray(verts, np.float64)
+    P = np.asarray(planes, np.float64)
+    dist = v @ P[:, :3].T + P[:, 3]                         # (V, K): signed distance of vertex to plane
+    on = np.abs(dist) <= tol
+    loops = []
+    for k in range(len(P)):
+        idx = np.nonzero(on[:, k])[0]
+        assert len(idx) >= 3, f"plane {k} holds {len(idx)} hull vertices"
+        n = P[k, :3] / np.linalg.norm(P[k, :3])
+        a = np.array([1.0, 0, 0]) if abs(n[0]) < 0.9 else np.array([0, 1.0, 0])
+        u = np.cross(n, a)
+        u /= np.linalg.norm(u)
+        w = np.cross(n, u)                                  # (u, w, n) right-handed: CCW about n in (u, w)
+        pts2 = [(float(v[i] @ u), float(v[i] @ w)) for i in idx]
+        poly = [int(idx[i]) for i in _ccw_polygon(pts2)]
+        loop = []
+        for j, a_ in enumerate(poly):
+            b_ = poly[(j + 1) % len(poly)]
+            cand = [l for l in range(len(P)) if l != k and on[a_, l] and on[b_, l]]
+            if cand:
+                adj = min(cand, key=lambda l: (float(P[l, :3] @ P[k, :3]), l))
+            else:       # an edge bridging near-duplicate faces: the plane both ends lie closest to
+                far = [l for l in range(len(P)) if P[l, :3] @ P[k, :3] <= 1 - 1e-6]
+                adj = min(far, key=lambda l: (max(abs(dist[a_, l]), abs(dist[b_, l])), l))
+            loop.append((a_, adj))
+        loops.append(loop)
+    edges, seen = [], set()
+    for k, loop in enumerate(loops):                        # each edge once, where its first face lists it
+        for j, (a_, adj) in enumerate(loop):
+            b_ = loop[(j + 1) % len(loop)][0]
+            key = (min(a_, b_), max(a_, b_))
+            if key in seen or P[adj, :3] @ P[k, :3] > 1 - 1e-6:
+                continue
+            seen.add(key)
+            edges.append((a_, b_, k, adj))
+    return edges, loops
+
+
+_TOPO_CACHE = {}
+
+
+def _topology(h):
+    """hull_topology of a scene hull record, cached by its vertex / plane data."""
+    key = (np.asarray(h["verts"], np.float64).tobytes(), np.asarray(h["planes"], np.float64).tobytes())
+    if key not in _TOPO_CACHE:
+        _TOPO_CACHE[key] = hull_topology(h["verts"], h["planes"])
+    return _TOPO_CACHE[key]
+
+
 # links whose hulls may touch the table (the base-mounted shoulder/upper arm sit on it and would
 # only produce contacts against a fixed joint; SURVEY.md §8 a16 robot filter 0b1 vs table 0)
 NO_TABLE_CONTACT = {"shoulder_link", "upper_arm_link"}
@@ -233,6 +319,7 @@ def build_model(scene, pool_names=None):
         m.dof_lower[d], m.dof_upper[d], m.dof_effort[d] = rec["lower"], rec["upper"], rec["effort"]
         m.dof_kp[d], m.dof_kd[d] = rec["kp"], rec["kd"]
         m.dof_armature[d] = rec.get("armature", 0.0)
+        m.dof_friction[d] = rec.get("friction", 0.0)
     m.base_pos[:] = rob["base_pos"]
     m.base_quat[:] = rob["base_quat"]
     objects = scene["objects"]
@@ -248,9 +335,11 @@ def build_model(scene, pool_names=None):
     hulls = [(h, h["index"]) for h in scene["link_hulls"]] + [(h, -1) for oh in obj_hulls for h in oh] + \
             [(st["hull"], -1) for st in statics]
     assert len(hulls) <= MAX_HULLS
-    vs, ps = 0, 0
+    vs, ps, es, ls = 0, 0, 0, 0
     verts = np.ctypeslib.as_array(m.verts)
     planes = np.ctypeslib.as_array(m.planes)
+    edges = np.ctypeslib.as_array(m.edges)
+    loop_v = np.ctypeslib.as_array(m.loop_v)
     for k, (h, link) in enumerate(hulls):
         v = np.asarray(h["verts"], np.float32)
         p = np.asarray(h["planes"], np.float32)
@@ -262,6 +351,19 @@ def build_model(scene, pool_names=None):
         m.hull_radius[k] = h["radius"]
         verts[vs:vs + len(v), :3] = v
         planes[ps:ps + len(p)] = p
+        # v10 topology: edges (v0, v1, f0, f1) and per-plane face loops
+        he, hl = _topology(h)
+        assert es + len(he) <= MAX_EDGES and ls + sum(len(l) for l in hl) <= MAX_LOOP
+        assert max(len(l) for l in hl) <= MAX_FACE_LOOP, "face loop longer than HA_MAX_FACE_LOOP"
+        m.hull_edge_start[k], m.hull_nedges[k] = es, len(he)
+        for i, (a, b, f0, f1) in enumerate(he):
+            edges[es + i] = a | (b << 8) | (f0 << 16) | (f1 << 24)
+        es += len(he)
+        for j, loop in enumerate(hl):
+            m.plane_loop[ps + j] = ls | (len(loop) << 16)
+            for t, (a, adj) in enumerate(loop):
+                loop_v[ls + t] = a
+            ls += len(loop)
         vs += len(v)
         ps += len(p)
     assert vs <= MAX_VERTS and ps <= MAX_PLANES
@@ -397,6 +499,8 @@ DEFAULT_TASK = dict(
     dt=0.016666667, substeps=2, control_freq_inv=3, solver_iters=8, gravity=(0.0, 0.0, -9.81),
     friction=1.0, contact_margin=0.01, baumgarte=0.2, max_depen_vel=1.0, object_ang_damping=0.5,
     contact_slop=0.001, manifold_window=0.002,
+    link_lin_damping=0.01, link_ang_damping=0.01,       # ur5sih.py:178-179
+    edge_rel_tol=0.9, edge_abs_tol=0.0005,              # edge-edge vs face axis (handarm_abi.h v10)
     joint_limit_margin=0.02, n_objects=3, num_initial_poses=1, max_episode_length=200,
     sih_alpha=0.8, reward_reaching=1.0, reward_lifting=5.0, reward_goal=50.0, reward_success=50.0,
     lifting_threshold=0.05, goal_threshold=0.05, goal_pos=(0.28, 0.58, 0.8), goal_noise=(0.15, 0.15, 0.1),
@@ -414,6 +518,7 @@ DEFAULT_TASK = dict(
 ALLEGRO_TASK = dict(
     DEFAULT_TASK, task=TASK_ALLEGRO_HAND, num_actions=16, num_obs=88, n_objects=1,
     dt=0.01667, substeps=2, control_freq_inv=2, solver_iters=8,          # AllegroHand.yaml:23,160-173
+    link_lin_damping=0.0, link_ang_damping=0.01,                         # allegro_hand.py:231 (linear: default 0)
     contact_margin=0.002, max_depen_vel=1000.0,                          # contact_offset, max_depenetration_velocity
     max_episode_length=600,                                              # episodeLength
     dist_reward_scale=-10.0, rot_reward_scale=1.0, rot_eps=0.1, action_penalty_scale=-0.0002,
@@ -502,7 +607,8 @@ def build_params(cfg=None, task=None):
         c.update(cfg)
     p = HaParams()
     for k in ["dt", "substeps", "control_freq_inv", "solver_iters", "friction", "contact_margin", "baumgarte",
-              "contact_slop", "manifold_window",
+              "contact_slop", "manifold_window", "link_lin_damping", "link_ang_damping", "edge_rel_tol",
+              "edge_abs_tol",
               "max_depen_vel", "object_ang_damping", "joint_limit_margin", "n_objects", "num_initial_poses",
               "max_episode_length", "sih_alpha", "reward_reaching", "reward_lifting", "reward_goal",
               "reward_success", "lifting_threshold", "goal_threshold", "seed"]:

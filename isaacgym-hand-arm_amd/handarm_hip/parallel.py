@@ -52,6 +52,18 @@ def init_distributed(backend=None):
     return rk, lr, ws, device
 
 
+def describe():
+    """The process group as bench.py reports it: backend and the world size an all-reduce of ones over it counts
+    (so a scaling record shows that RCCL saw every rank)."""
+    if world() == 1:
+        return {"backend": None, "world_size": 1}
+    import torch.distributed as dist
+    dev = f"cuda:{torch.cuda.current_device()}" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.ones(1, device=dev)
+    dist.all_reduce(t)
+    return {"backend": dist.get_backend(), "world_size": int(t.item())}
+
+
 def global_num_envs(env):
     """Number of envs over ALL ranks (the EWMA's alpha divides by it). Shards may differ in size, so it is
     all-reduced once (the first multi-rank fold, on every rank) and cached on the env."""
@@ -132,8 +144,9 @@ def reduce_allegro_episode_stats(env):
     """AllegroHand: consecutive_successes is a per-shard EWMA of the mean successes of the reset envs
     (allegro_hand.py:700-705); the global view is the env-weighted mean over ranks. One all-reduce of 2 floats;
     returns {"consecutive_successes": ..} as a device tensor."""
-    v = torch.stack([env.consecutive_successes.reshape(()).float() * env.num_envs,
-                     torch.tensor(float(env.num_envs), device=env.consecutive_successes.device)])
+    cs = env.consecutive_successes.reshape(()).float()
+    v = torch.full((2,), float(env.num_envs), device=cs.device)    # device fill: no host tensor per call
+    v[0] = v[0] * cs
     if world() > 1:
         import torch.distributed as dist
         dist.all_reduce(v)
@@ -170,5 +183,5 @@ def fold_counts(stats, terms, num_envs, ewma, obj_ewma, object_names):
     return log, ewma, obj_ewma, total_r, total_s
 
 
-__all__ = ["init_distributed", "global_num_envs", "reduce_episode_stats", "reduce_kuka_episode_stats",
+__all__ = ["init_distributed", "describe", "global_num_envs", "reduce_episode_stats", "reduce_kuka_episode_stats",
            "reduce_allegro_episode_stats", "fold_counts", "fold_pending", "world", "rank"]

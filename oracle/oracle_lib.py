@@ -27,6 +27,8 @@ def load():
     lib.hao_simulate.argtypes = [C.c_void_p, C.POINTER(HM.HaState), C.c_int, C.c_int, C.c_int]
     lib.hao_controller.argtypes = [C.c_void_p, C.POINTER(HM.HaState), C.c_int]
     lib.hao_struct_sizes.argtypes = [C.POINTER(C.c_int32)] * 3
+    lib.hao_contacts.restype = C.c_int
+    lib.hao_contacts.argtypes = [C.c_void_p, C.POINTER(HM.HaState), C.c_int, C.c_void_p, C.c_int]
     return lib
 
 
@@ -71,6 +73,13 @@ class Oracle:
     def simulate(self, st, n_calls=1, begin=0, end=None):
         s = st.ctypes()
         self.lib.hao_simulate(self.h, C.byref(s), n_calls, begin, self.num_envs if end is None else end)
+
+    def contacts(self, st, env):
+        """(x[3], n[3], sep, a, b) rows of the contacts detect() produces for env (normal from body b to a)."""
+        out = np.zeros((256, 9), np.float32)
+        s = st.ctypes()
+        n = self.lib.hao_contacts(self.h, C.byref(s), env, out.ctypes.data, 256)
+        return out[:min(n, 256)]
 
     def controller(self, st):
         s = st.ctypes()

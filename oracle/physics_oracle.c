@@ -224,6 +224,14 @@ static void dynamics(const hao_handle h, env_t* e, float* M, float* C) {
         /* crf(V) (n2,f2) = (w x n2 + v x f2, w x f2) */
         Fn[i] = add(n1, add(crs(Vl[i].w, n2), crs(Vl[i].v, f2)));
         Ff[i] = add(f1, crs(Vl[i].w, f2));
+        /* link damping (ha_params_t v10, ha_physics.h dynamics): the wrench cl m v_com, ca I_com w about the origin,
+         * from the momentum (n2, f2) = (I_com w + c x m v_com, m v_com); g = c x m v_com = h x f2 / m */
+        float cl = h->p.link_lin_damping, ca = h->p.link_ang_damping;
+        if (cl != 0.0f || ca != 0.0f) {
+            v3 g = I[i].m > 0.0f ? mul(crs(I[i].h, f2), 1.0f / I[i].m) : V(0, 0, 0);
+            Fn[i] = add(Fn[i], add(mul(sub(n2, g), ca), mul(g, cl)));
+            Ff[i] = add(Ff[i], mul(f2, cl));
+        }
     }
     for (int i = 0; i < D; i++) C[i] = 0;
     for (int i = L - 1; i >= 0; i--) {
@@ -378,13 +386,14 @@ static int reduce_manifold(const v3* pts, const float* seps, int nc, v3 n, const
     return k;
 }
 
-#define MAXCAND 128
+#define MAXCAND 256      /* (1) <= 64 incident vertices, (2) <= 128 clip points, (3) <= 64 reference vertices */
 #define MAXGATHER 32     /* ha_physics.h HA_MAX_GATHER */
 /* Compound objects (several convex pieces, ha_model_t v8): between gather_begin and gather_end every piece
    pair's reduced points collect in a per-thread buffer (at most MAXGATHER, later ones dropped) and the object
    pair then emits ONE manifold of <= 4 points chosen from them, each keeping its piece pair's normal. */
 static __thread int g_on, g_n;
 static __thread float g_window;     /* ha_params_t.manifold_window of the running detect() */
+static __thread float g_edge_rel, g_edge_abs;   /* ha_params_t.edge_rel_tol / edge_abs_tol of the running detect() */
 static __thread v3 g_pt[MAXGATHER], g_nrm[MAXGATHER];
 static __thread float g_sep[MAXGATHER];
 
@@ -425,7 +434,71 @@ static void gather_end(contact_t* out, int* nout, int maxout, int a, int b) {
     store_points(out, nout, maxout, g_pt, g_sep, g_nrm, V(0, 0, 0), idx, k, a, b);
 }
 
-/* hull A (body a) vs hull B (body b); contact normal from B to A */
+/* squared distance from point q to the segment p0 + t (p1 - p0), t in [0, 1] (ha_physics.h seg_point_d2) */
+static float seg_point_d2(v3 p0, v3 p1, v3 q) {
+    v3 d = sub(p1, p0);
+    float dd = dot(d, d);
+    float t = dd > 0.0f ? dot(sub(q, p0), d) / dd : 0.0f;
+    t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
+    v3 r = sub(q, add(p0, mul(d, t)));
+    return dot(r, r);
+}
+/* side plane of edge j of a face loop (world vertices wv, loop indices lv[0..n), face normal nf): through the edge,
+ * perpendicular to the face, unit outward normal cross(e, nf) (ha_physics.h side_plane) */
+static v3 side_plane(const v3* wv, const uint8_t* lv, int j, int n, v3 nf, float* d) {
+    v3 v0 = wv[lv[j]];
+    v3 sn = crs(sub(wv[lv[j + 1 == n ? 0 : j + 1]], v0), nf);
+    sn = mul(sn, 1.0f / sqrtf(dot(sn, sn)));
+    *d = -dot(sn, v0);
+    return sn;
+}
+/* world face planes of a hull (hull_plane of every k) */
+typedef struct { v3 n; float d; } wplane_t;
+
+/* edge pair of the edge-edge SAT (ha_physics.h edge_axis, Gregorius GDC 2013): the Gauss-map arcs of edge ea of A
+ * (between its faces' normals) and of edge eb of B (negated normals) cross -> a face of the Minkowski difference,
+ * axis N = e1 x e2 oriented away from B's centre cb, separation N . (pA - pB); -3e38 otherwise */
+static float edge_axis(uint32_t ea, uint32_t eb, const wplane_t* wpa, const wplane_t* wpb, const v3* va, const v3* vb,
+                       v3 cb, v3* n, v3* pa, v3* e1, v3* pb, v3* e2) {
+    v3 a = wpa[(ea >> 16) & 255u].n, b = wpa[ea >> 24].n;
+    v3 cc = mul(wpb[(eb >> 16) & 255u].n, -1.0f), dd = mul(wpb[eb >> 24].n, -1.0f);
+    v3 bxa = crs(b, a), dxc = crs(dd, cc);
+    float cba = dot(cc, bxa), dba = dot(dd, bxa), adc = dot(a, dxc), bdc = dot(b, dxc);
+    if (!(cba * dba < 0.0f && adc * bdc < 0.0f && cba * bdc > 0.0f)) return -3.0e38f;
+    *pa = va[ea & 255u];
+    *e1 = sub(va[(ea >> 8) & 255u], *pa);
+    *pb = vb[eb & 255u];
+    *e2 = sub(vb[(eb >> 8) & 255u], *pb);
+    v3 nn = crs(*e1, *e2);
+    float l2 = dot(nn, nn);
+    if (l2 < 2.5e-5f * (dot(*e1, *e1) * dot(*e2, *e2))) return -3.0e38f;
+    nn = mul(nn, 1.0f / sqrtf(l2));
+    if (dot(nn, sub(*pb, cb)) < 0.0f) nn = mul(nn, -1.0f);
+    *n = nn;
+    return dot(nn, sub(*pa, *pb));
+}
+/* midpoint of the closest points of the segments pa + s e1, pb + t e2 (ha_physics.h edge_closest_mid) */
+static v3 edge_closest_mid(v3 pa, v3 e1, v3 pb, v3 e2) {
+    v3 r = sub(pa, pb);
+    float aa = dot(e1, e1), ee = dot(e2, e2), bb = dot(e1, e2), cc = dot(e1, r), ff = dot(e2, r);
+    float den = aa * ee - bb * bb;
+    float sa = den > 0.0f ? (bb * ff - cc * ee) / den : 0.0f;
+    sa = sa < 0.0f ? 0.0f : (sa > 1.0f ? 1.0f : sa);
+    float tb = (bb * sa + ff) / ee;
+    if (tb < 0.0f) {
+        tb = 0.0f;
+        sa = -cc / aa;
+        sa = sa < 0.0f ? 0.0f : (sa > 1.0f ? 1.0f : sa);
+    } else if (tb > 1.0f) {
+        tb = 1.0f;
+        sa = (bb - cc) / aa;
+        sa = sa < 0.0f ? 0.0f : (sa > 1.0f ? 1.0f : sa);
+    }
+    return mul(add(add(pa, mul(e1, sa)), add(pb, mul(e2, tb))), 0.5f);
+}
+
+/* hull A (body a) vs hull B (body b); contact normal from B to A. Face axes of both hulls, then the edge-edge axes
+ * (v10), then the contact: one edge-edge point, or the clipped face manifold (ha_physics.h collide_hulls) */
 static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t PB, float margin, int a, int b,
                           const float* sca, const float* scb, contact_t* out, int* nout, int maxout) {
     int nva = m->hull_nverts[ha], nvb = m->hull_nverts[hb];
@@ -439,52 +512,139 @@ static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t
     v3 va[64], vb[64];
     for (int i = 0; i < nva; i++) va[i] = hull_vert(m, ha, i, PA, sca);
     for (int i = 0; i < nvb; i++) vb[i] = hull_vert(m, hb, i, PB, scb);
+    wplane_t wpa[128], wpb[128];
+    for (int k = 0; k < npa; k++) hull_plane(m, ha, k, PA, sca, &wpa[k].n, &wpa[k].d);
+    for (int k = 0; k < npb; k++) hull_plane(m, hb, k, PB, scb, &wpb[k].n, &wpb[k].d);
     /* SAT over face normals */
     float sepA = -1e30f, sepB = -1e30f;
     int kA = -1, kB = -1;
     for (int k = 0; k < npa; k++) {
-        v3 n; float d;
-        hull_plane(m, ha, k, PA, sca, &n, &d);
         float mn = 1e30f;
-        for (int i = 0; i < nvb; i++) { float s = dot(n, vb[i]) + d; if (s < mn) mn = s; }
+        for (int i = 0; i < nvb; i++) { float s = dot(wpa[k].n, vb[i]) + wpa[k].d; if (s < mn) mn = s; }
         if (mn > sepA) { sepA = mn; kA = k; }
     }
     if (sepA > margin) return;
     for (int k = 0; k < npb; k++) {
-        v3 n; float d;
-        hull_plane(m, hb, k, PB, scb, &n, &d);
         float mn = 1e30f;
-        for (int i = 0; i < nva; i++) { float s = dot(n, va[i]) + d; if (s < mn) mn = s; }
+        for (int i = 0; i < nva; i++) { float s = dot(wpb[k].n, va[i]) + wpb[k].d; if (s < mn) mn = s; }
         if (mn > sepB) { sepB = mn; kB = k; }
     }
     if (sepB > margin) return;
+    /* edge-edge axes: the edges of each hull within R of the other's centre, every (A, B) pair in list order */
+    int nea = m->hull_nedges[ha], neb = m->hull_nedges[hb];
+    if (nea > 0 && neb > 0) {
+        float smax = fmaxf(sepA, sepB);
+        float pen = smax < 0.0f ? -smax : 0.0f;
+        float RA = (scl_r(sca, m->hull_radius[ha]) + margin) + pen;
+        float RB = (scl_r(scb, m->hull_radius[hb]) + margin) + pen;
+        const uint32_t* EA = m->edges + m->hull_edge_start[ha];
+        const uint32_t* EB = m->edges + m->hull_edge_start[hb];
+        int la[256], lb[256], nA = 0, nB = 0;
+        for (int i = 0; i < nea; i++)
+            if (seg_point_d2(va[EA[i] & 255u], va[(EA[i] >> 8) & 255u], cb) <= RB * RB) la[nA++] = i;
+        for (int i = 0; i < neb; i++)
+            if (seg_point_d2(vb[EB[i] & 255u], vb[(EB[i] >> 8) & 255u], ca) <= RA * RA) lb[nB++] = i;
+        float best = -3.0e38f;
+        int bw = -1;
+        for (int i = 0; i < nA; i++)
+            for (int j = 0; j < nB; j++) {
+                v3 n, pa, pb, e1, e2;
+                float sv = edge_axis(EA[la[i]], EB[lb[j]], wpa, wpb, va, vb, cb, &n, &pa, &e1, &pb, &e2);
+                if (sv > best) { best = sv; bw = i * nB + j; }
+            }
+        if (best > margin) return;              /* separated along an edge-edge axis */
+        if (best > g_edge_rel * smax + g_edge_abs) {
+            v3 n, pa, pb, e1, e2;
+            edge_axis(EA[la[bw / nB]], EB[lb[bw % nB]], wpa, wpb, va, vb, cb, &n, &pa, &e1, &pb, &e2);
+            v3 x = edge_closest_mid(pa, e1, pb, e2);
+            emit(out, nout, maxout, &x, &best, 1, n, a, b);
+            return;
+        }
+    }
+    /* face contact, candidates in the kernel's id order: (1) incident vertices near the reference face and inside its
+     * hull's other planes, (2) per incident-face loop edge its entry / exit point clipped to the reference face's side
+     * planes, (3) the reference face's loop vertices projected onto the incident face */
     v3 pts[MAXCAND];
     float seps[MAXCAND];
     for (int pass = 0; pass < 2; pass++) {
         int refB = (sepB >= sepA) ? (pass == 0) : (pass == 1);
-        int hr = refB ? hb : ha, kr = refB ? kB : kA;
-        pose_t Pr = refB ? PB : PA;
-        const float* scr = refB ? scb : sca;
+        int hr = refB ? hb : ha, hi = refB ? ha : hb, kr = refB ? kB : kA;
+        const wplane_t* wpr = refB ? wpb : wpa;
+        const wplane_t* wpi = refB ? wpa : wpb;
         v3* vi = refB ? va : vb;
-        int nvi = refB ? nva : nvb, npr = m->hull_nplanes[hr];
-        v3 nref; float dref;
-        hull_plane(m, hr, kr, Pr, scr, &nref, &dref);
+        v3* vr = refB ? vb : va;
+        int nvi = refB ? nva : nvb, npr = refB ? npb : npa, npi = refB ? npa : npb;
+        v3 nref = wpr[kr].n;
+        float dref = wpr[kr].d;
         int nc = 0;
-        for (int i = 0; i < nvi && nc < MAXCAND; i++) {
+        for (int i = 0; i < nvi; i++) {
             float dist = dot(nref, vi[i]) + dref;
             if (dist > margin) continue;
             float mx = -1e30f;
             for (int k = 0; k < npr; k++) {
                 if (k == kr) continue;
-                v3 n; float d;
-                hull_plane(m, hr, k, Pr, scr, &n, &d);
-                float s = dot(n, vi[i]) + d;
+                float s = dot(wpr[k].n, vi[i]) + wpr[k].d;
                 if (s > mx) mx = s;
             }
             if (mx > margin) continue;
             pts[nc] = sub(vi[i], mul(nref, 0.5f * dist));
             seps[nc] = dist;
             nc++;
+        }
+        int ki = -1;
+        float vmin = 3.0e38f;
+        for (int k = 0; k < npi; k++) {
+            float dv = dot(wpi[k].n, nref);
+            if (dv < vmin) { vmin = dv; ki = k; }
+        }
+        int lpi = m->plane_loop[m->hull_plane_start[hi] + ki], lpr = m->plane_loop[m->hull_plane_start[hr] + kr];
+        int li0 = lpi & 0xFFFF, lni = lpi >> 16, lr0 = lpr & 0xFFFF, lnr = lpr >> 16;
+        /* the kernel holds the candidates one per lane: the valid vertices at lanes [0, nv1), edge j's entry / exit
+         * point at lane nv1 + 2 j (+ 1), reference vertex r at lane nv1 + 2 lni + r; lanes past 63 are dropped */
+        int nv1 = nc;
+        for (int j = 0; j < lni; j++) {
+            v3 p0 = vi[m->loop_v[li0 + j]], p1 = vi[m->loop_v[li0 + (j + 1 == lni ? 0 : j + 1)]];
+            float tin = 0.0f, tout = 1.0f;
+            int outside = 0;
+            for (int jj = 0; jj < lnr; jj++) {
+                float sd;
+                v3 sn = side_plane(vr, m->loop_v + lr0, jj, lnr, nref, &sd);
+                float f0 = dot(sn, p0) + sd, f1 = dot(sn, p1) + sd;
+                if (f0 > 0.0f && f1 > 0.0f) outside = 1;
+                else if (f0 > 0.0f) tin = fmaxf(tin, f0 / (f0 - f1));
+                else if (f1 > 0.0f) tout = fminf(tout, f0 / (f0 - f1));
+            }
+            v3 e = sub(p1, p0);
+            v3 xe = add(p0, mul(e, tin)), xx = add(p0, mul(e, tout));
+            float de = dot(nref, xe) + dref, dx = dot(nref, xx) + dref;
+            if (!outside && tin > 0.0f && tin <= tout && de <= margin && nv1 + 2 * j < 64) {
+                pts[nc] = sub(xe, mul(nref, 0.5f * de));
+                seps[nc++] = de;
+            }
+            if (!outside && tout < 1.0f && tin < tout && dx <= margin && nv1 + 2 * j + 1 < 64) {
+                pts[nc] = sub(xx, mul(nref, 0.5f * dx));
+                seps[nc++] = dx;
+            }
+        }
+        v3 ni = wpi[ki].n;
+        float di = wpi[ki].d;
+        float den = dot(ni, nref);
+        if (den < -1e-6f) {
+            for (int r = 0; r < lnr; r++) {
+                v3 q = vr[m->loop_v[lr0 + r]];
+                float sr = -(dot(ni, q) + di) / den;
+                v3 x = add(q, mul(nref, sr));
+                float mx = -3.0e38f;
+                for (int jj = 0; jj < lni; jj++) {
+                    float sd;
+                    v3 sn = side_plane(vi, m->loop_v + li0, jj, lni, ni, &sd);
+                    mx = fmaxf(mx, dot(sn, x) + sd);
+                }
+                if (sr <= margin && mx <= 0.0f && nv1 + 2 * lni + r < 64) {
+                    pts[nc] = add(q, mul(nref, 0.5f * sr));
+                    seps[nc++] = sr;
+                }
+            }
         }
         if (nc > 0) {
             v3 n = refB ? nref : mul(nref, -1.0f);
@@ -526,6 +686,8 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
     int nout = 0;
     float mg = p->contact_margin;
     g_window = p->manifold_window;
+    g_edge_rel = p->edge_rel_tol;
+    g_edge_abs = p->edge_abs_tol;
     for (int o = 0; o < h->NO; o++) {
         if (!e->coll[o]) continue;
         int pa = e->pool[o];
@@ -730,6 +892,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
      * |lambda| <= effort h) and the hard lower/upper limits (active within joint_limit_margin) */
     float dgam[HA_MAX_DOFS], dbias[HA_MAX_DOFS], dwinv[HA_MAX_DOFS], dlim[HA_MAX_DOFS], dlam[HA_MAX_DOFS];
     float lwinv[HA_MAX_DOFS], vt_lo[HA_MAX_DOFS], vt_up[HA_MAX_DOFS], lam_lo[HA_MAX_DOFS], lam_up[HA_MAX_DOFS];
+    float flim[HA_MAX_DOFS], lam_fr[HA_MAX_DOFS];     /* joint friction row (v10): |impulse| <= dof_friction h */
     int act_lo[HA_MAX_DOFS], act_up[HA_MAX_DOFS];
     for (int d = 0; d < D; d++) {
         float kp = m->dof_kp[d], kd = m->dof_kd[d];
@@ -747,6 +910,8 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
         vt_lo[d] = s_lo > 0 ? -s_lo / hdt : -p->baumgarte * s_lo / hdt;
         vt_up[d] = s_up > 0 ? -s_up / hdt : -p->baumgarte * s_up / hdt;
         lam_lo[d] = lam_up[d] = 0.0f;
+        flim[d] = m->dof_friction[d] * hdt;
+        lam_fr[d] = 0.0f;
     }
     /* projected Gauss-Seidel, velocity form: joint rows d = 0..D-1 (drive, lower, upper), then the
      * contact rows; v is updated after every row */
@@ -778,6 +943,15 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
                     for (int k = 0; k < D; k++) v[k] -= mrow[k] * d1;
                 }
             }
+            if (flim[d] > 0.0f) {
+                float nf = lam_fr[d] - v[d] * lwinv[d];
+                nf = nf < -flim[d] ? -flim[d] : (nf > flim[d] ? flim[d] : nf);
+                float df = nf - lam_fr[d];
+                if (df != 0.0f) {
+                    lam_fr[d] = nf;
+                    for (int k = 0; k < D; k++) v[k] += mrow[k] * df;
+                }
+            }
         }
         /* contact blocks (ha_physics.h): the three J.v reductions of a contact from the same v; the
          * friction rows see the normal / first-friction update through the block's Delassus entries */
@@ -803,7 +977,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
             if (d2 != 0.0f) for (int k = 0; k < NV; k++) v[k] += R.Y[r0 + 2][k] * d2;
         }
     }
-    for (int d = 0; d < D; d++) e->dforce[d] = ((dlam[d] + lam_lo[d]) - lam_up[d]) / hdt;
+    for (int d = 0; d < D; d++) e->dforce[d] = (((dlam[d] + lam_lo[d]) - lam_up[d]) + lam_fr[d]) / hdt;
     /* contact forces per body (net_contact_force): the last substep's forces */
     memset(e->cforce, 0, sizeof(e->cforce));
     for (int c = 0; c < nc; c++) {
@@ -950,6 +1124,23 @@ static void simulate_env(const hao_handle h, ha_state_t* S, int env, int n_calls
         for (int s = 0; s < h->p.substeps; s++) substep(h, &e, hdt);
     /* net contact force of the last substep (PhysX reports the last substep's forces) */
     store_env(h, S, env, &e);
+}
+
+/* the contacts detect() produces for env's current state (test helper): rows of 9 floats x[3], n[3], sep, a, b */
+int hao_contacts(hao_handle h, ha_state_t* S, int env, float* out, int max_rows) {
+    env_t e;
+    load_env(h, S, env, &e, 0);
+    e.dr = (h->p.dr_enable && S->dr_scale) ? S->dr_scale + (size_t)env * HA_DR_SIZE : NULL;
+    fk(h, &e);
+    contact_t cs[MAXC];
+    int nc = detect(h, &e, cs);
+    for (int i = 0; i < nc && i < max_rows; i++) {
+        float* r = out + 9 * i;
+        r[0] = cs[i].x.x; r[1] = cs[i].x.y; r[2] = cs[i].x.z;
+        r[3] = cs[i].n.x; r[4] = cs[i].n.y; r[5] = cs[i].n.z;
+        r[6] = cs[i].sep; r[7] = (float)cs[i].a; r[8] = (float)cs[i].b;
+    }
+    return nc;
 }
 
 void hao_simulate(hao_handle h, ha_state_t* S, int n_calls, int env_begin, int env_end) {

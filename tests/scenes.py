@@ -165,3 +165,129 @@ def assert_physics_bit_identical(sim, st, n, fields=PHYSICS_OUTPUTS, tag=""):
         same = (g.view(np.uint32) == o.view(np.uint32)).all(1)
         assert same.all(), (f"{tag} {k}: {int((~same).sum())}/{n} envs differ from the oracle, "
                             f"max |d| {np.abs(g - o).max():.3e}")
+
+
+# ----------------------------------------------------------------------------- box scenes (narrow-phase tests)
+def box_hull_record(half):
+    """A box hull record (tools/build_model.py box_hull): 8 vertices, 6 face planes n.x + d <= 0 inside."""
+    hx, hy, hz = (float(h) for h in half)
+    verts = [[sx * hx, sy * hy, sz * hz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)]
+    planes = [[1, 0, 0, -hx], [-1, 0, 0, -hx], [0, 1, 0, -hy], [0, -1, 0, -hy], [0, 0, 1, -hz], [0, 0, -1, -hz]]
+    return {"verts": verts, "planes": planes, "center": [0.0, 0.0, 0.0], "radius": float(np.linalg.norm([hx, hy, hz]))}
+
+
+def box_pool_scene(halves, density=400.0):
+    """The Ur5Sih scene (robot, table) with a pool of boxes (half extents `halves`) instead of the YCB objects."""
+    from handarm_hip import model as HM
+    scene = dict(HM.load_scene(HM.ASSET))
+    objs = []
+    for i, h in enumerate(halves):
+        hx, hy, hz = h
+        m = density * 8 * hx * hy * hz
+        I = [m / 3 * (hy * hy + hz * hz), 0, 0, 0, m / 3 * (hx * hx + hz * hz), 0, 0, 0, m / 3 * (hx * hx + hy * hy)]
+        objs.append({"name": f"box{i}", "mass": m, "com": [0.0, 0.0, 0.0], "inertia": I, "hull": box_hull_record(h),
+                     "bbox_extents": [2 * hx, 2 * hy, 2 * hz]})
+    scene["objects"] = objs
+    return scene
+
+
+def axis_quat(axis, ang):
+    a = np.asarray(axis, np.float64)
+    a = a / np.linalg.norm(a)
+    return np.concatenate([a * np.sin(ang / 2), [np.cos(ang / 2)]]).astype(np.float32)
+
+
+TABLE_TOP, TABLE_X1 = 0.5, 0.2925 + 0.375       # Ur5SihMultiObject table: top z, far edge x (multi_object.py:536)
+EDGE_BOXES = [(0.03, 0.05, 0.03), (0.05, 0.03, 0.03), (0.04, 0.04, 0.02)]
+
+
+def fill_box_scene(st, num_envs, kind, seed=0, pen=0.0005):
+    """Robot at its reset pose (clear of the objects) and the three boxes of box_pool_scene(EDGE_BOXES) in an
+    edge-contact configuration, poses jittered per env (seeded):
+      "crossed":    box 1 rotated 45 deg about x (a ridge along x on top) stands on its bottom edge on the table; box 0
+                    rotated 45 deg about y (a ridge along y at its bottom) lies across it, ridges crossing at 90 deg,
+                    ~pen deep: an edge-edge contact no face axis finds;
+      "table_edge": box 0 rotated 45 deg about x, its bottom ridge (along x) across the table's far edge (along y);
+      "overhang":   box 2 flat on the table, its centre 1 cm inside the far edge (37.5% over it): the support
+                    polygon reaches the table edge only through clipped edge points."""
+    rng = np.random.default_rng(seed)
+    N = num_envs
+    rs = st["root_state"].reshape(N, 6, 13)
+    rs[:] = 0
+    rs[..., 6] = 1.0
+    rs[:, 0, 0:3] = [0.28, 0.58, 0.8]
+    rs[:, 1, 0:3] = [0.0, 0.0, 0.5]
+    rs[:, 2, 0:3] = [0.2925, 0.38, 0.25]
+    r2 = np.sqrt(2.0)
+    jit = rng.uniform(-1.0, 1.0, (N, 3)).astype(np.float32)
+    if kind == "crossed":
+        h1, h0 = EDGE_BOXES[1], EDGE_BOXES[0]
+        z1 = TABLE_TOP + (h1[1] + h1[2]) / r2
+        rs[:, 4, 0:3] = np.stack([0.45 + 0.002 * jit[:, 0], 0.80 + 0.002 * jit[:, 1], np.full(N, z1)], 1)
+        rs[:, 4, 3:7] = axis_quat([1, 0, 0], np.pi / 4)
+        top1 = z1 + (h1[1] + h1[2]) / r2
+        z0 = top1 + (h0[0] + h0[2]) / r2 - pen * (1.0 + 0.5 * jit[:, 2])
+        rs[:, 3, 0:3] = np.stack([rs[:, 4, 0], rs[:, 4, 1], z0], 1)
+        rs[:, 3, 3:7] = axis_quat([0, 1, 0], np.pi / 4)
+    elif kind == "table_edge":
+        h0 = EDGE_BOXES[0]
+        rs[:, 3, 0:3] = np.stack([TABLE_X1 + 0.003 * jit[:, 0], 0.80 + 0.01 * jit[:, 1],
+                                  TABLE_TOP + (h0[1] + h0[2]) / r2 - pen * (1.0 + 0.5 * jit[:, 2])], 1)
+        rs[:, 3, 3:7] = axis_quat([1, 0, 0], np.pi / 4)
+        rs[:, 4, 0:3] = [0.10, 0.85, TABLE_TOP + EDGE_BOXES[1][2]]
+    elif kind == "overhang":
+        h2 = EDGE_BOXES[2]
+        rs[:, 5, 0:3] = np.stack([TABLE_X1 - 0.01 + 0.002 * jit[:, 0], 0.80 + 0.01 * jit[:, 1],
+                                  np.full(N, TABLE_TOP + h2[2] - 0.0002)], 1)
+        rs[:, 5, 3:7] = axis_quat([0, 0, 1], 0.05 * jit[:, 2].mean())
+        rs[:, 3, 0:3] = [0.10, 0.85, TABLE_TOP + EDGE_BOXES[0][2]]
+        rs[:, 4, 0:3] = [0.20, 0.85, TABLE_TOP + EDGE_BOXES[1][2]]
+    else:
+        raise ValueError(kind)
+    if kind != "overhang":
+        rs[:, 5, 0:3] = [0.20, 0.88, TABLE_TOP + EDGE_BOXES[2][2]]
+    ds = st["dof_state"].reshape(N, 17, 2)
+    ds[..., 0] = RESET_POSE
+    ds[..., 1] = 0.0
+    st["sim_targets"][:] = RESET_POSE
+    st["object_indices"][:] = [0, 1, 2]
+    st["collision_enabled"][:] = 1
+    return st
+
+
+def link_hull_world_verts(model, body_state_env, link):
+    """World vertices of every hull of robot link `link` (model hull_link), posed by its rigid_body_state row."""
+    from handarm_hip import model as HM   # noqa: F401
+    row = body_state_env[model.body_robot0 + link]
+    p, q = row[0:3].astype(np.float64), row[3:7].astype(np.float64)
+    x, y, z, w = q
+    R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                  [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                  [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+    out = []
+    for k in range(model.n_link_hulls):
+        if model.hull_link[k] != link:
+            continue
+        s, nv = model.hull_vert_start[k], model.hull_nverts[k]
+        v = np.array([list(model.verts[s + i])[:3] for i in range(nv)], np.float64)
+        out.append(v @ R.T + p)
+    return np.concatenate(out)
+
+
+def place_cuboid_edge_on_link(st, model, body_state, link, pen=0.0003):
+    """AllegroKuka: each env's cuboid (its object_scale dims of the 0.05 m base cube) rotated 45 deg about x, its
+    bottom ridge (along x) `pen` below the highest vertex of link `link`'s hulls, centred over it, at rest."""
+    N, A = st.num_envs, model.n_actors
+    rs = st["root_state"].reshape(N, A, 13)
+    sc = st["object_scale"].reshape(N, 3)
+    body = body_state.reshape(N, model.n_bodies, 13)
+    q = axis_quat([1, 0, 0], np.pi / 4)
+    for e in range(N):
+        v = link_hull_world_verts(model, body[e], link)
+        top = v[np.argmax(v[:, 2])]
+        hy, hz = 0.025 * sc[e, 1], 0.025 * sc[e, 2]
+        rs[e, model.actor_object0, 0:3] = [top[0], top[1], top[2] + (hy + hz) / np.sqrt(2.0) - pen]
+        rs[e, model.actor_object0, 3:7] = q
+        rs[e, model.actor_object0, 7:13] = 0.0
+    st["object_force"][:] = 0.0
+    return st

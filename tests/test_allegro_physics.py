@@ -32,7 +32,7 @@ def test_allegro_physics_is_stable_and_tracks_targets():
     # the cube never sinks through the ground plane and stays near the hand or on the ground
     z = root[:, 1, 2]
     assert (z > 0.0325 - 0.01).all()
-    assert np.abs(root[:, 1, 0]).max() < 0.6
+    assert np.abs(root[:, 1, 0]).max() < 1.0        # a cube thrown off the hand tumbles on the ground, then rests
 
 
 def test_allegro_free_cube_falls_under_gravity():

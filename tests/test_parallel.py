@@ -172,3 +172,38 @@ def test_kuka_episode_stats_are_global_means():
     for rank, succ, tobj, _ in out:
         np.testing.assert_allclose(succ, allts[:, HM.AK_PREV_SUCC].mean(), rtol=1e-6)
         np.testing.assert_allclose(tobj, allts[:, HM.AK_TRUE_OBJ].mean(), rtol=1e-6)
+
+
+def _allegro_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = N_LOCAL + 32 * rank
+        cs = torch.tensor([1.5 + rank], dtype=torch.float32)
+        out = parallel.reduce_allegro_episode_stats(types.SimpleNamespace(consecutive_successes=cs, num_envs=n))
+        q.put((rank, float(out["consecutive_successes"]), n, float(cs), parallel.describe()))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_allegro_episode_stats_and_group_description():
+    """AllegroHand: the global consecutive_successes is the env-weighted mean of the ranks' shard EWMAs; and
+    parallel.describe() (the bench line's "distributed" record) reports the backend and the world size an
+    all-reduce over the group counts."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_allegro_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = sum(o[2] * o[3] for o in out) / sum(o[2] for o in out)
+    for rank, got, _, _, desc in out:
+        assert got == pytest.approx(want, rel=1e-6)
+        assert desc == {"backend": "gloo", "world_size": 2}
+    assert parallel.describe() == {"backend": None, "world_size": 1}

@@ -390,6 +390,12 @@ def quat_axis_angle(axis, angle):
     return np.concatenate([a * math.sin(angle / 2), [math.cos(angle / 2)]])
 
 
+def urdf_joint_friction(j):
+    """<dynamics friction> of a URDF joint (0 without one): the DOF friction Isaac Gym loads from the URDF."""
+    dyn = j.find("dynamics")
+    return float(dyn.get("friction", 0.0)) if dyn is not None else 0.0
+
+
 def build_collapsed(urdf, dof_props, base_pos, base_quat):
     """A URDF loaded with fix_base_link + collapse_fixed_joints (fixed children merged into their parent
     body, which keeps the parent's frame). Mass properties come from the URDF inertials (no
@@ -448,6 +454,7 @@ def build_collapsed(urdf, dof_props, base_pos, base_quat):
             rec["dof"] = len(dofs)
             d = {"name": j.get("name"), "link": bidx[b], "lower": float(lim.get("lower")),
                  "upper": float(lim.get("upper")), "velocity": float(lim.get("velocity"))}
+            d["friction"] = urdf_joint_friction(j)
             d.update(dof_props(j.get("name")))
             dofs.append(d)
         mass, mc, Isum = 0.0, np.zeros(3), np.zeros((3, 3))
@@ -502,7 +509,8 @@ def build_allegro():
     # hand_start_pose (allegro_hand.py:284-286): p = (0, 0, 0.5), r = Qy(pi) * Qx(0.47 pi) * Qz(0.25 pi)
     q = quat_mul_np(quat_mul_np(quat_axis_angle([0, 1, 0], math.pi), quat_axis_angle([1, 0, 0], 0.47 * math.pi)),
                     quat_axis_angle([0, 0, 1], 0.25 * math.pi))
-    return build_collapsed(ALLEGRO_URDF, lambda name: {"effort": 0.5, "kp": 3.0, "kd": 0.1, "armature": 0.001},
+    return build_collapsed(ALLEGRO_URDF, lambda name: {"effort": 0.5, "kp": 3.0, "kd": 0.1, "armature": 0.001,
+                                                       "friction": 0.01},     # allegro_hand.py:264-268
                            [0.0, 0.0, 0.5], q.tolist())
 
 
@@ -835,7 +843,25 @@ def main_pointclouds(seed=0):
           f"{list(zip(r_names, r_counts))} -> {PC_OUT}")
 
 
+def main_dof_friction():
+    """Adds the DOF friction to the committed Allegro scenes without rebuilding their hulls: AllegroHand 0.01
+    (allegro_hand.py:267), AllegroKuka the URDF's <dynamics friction> (AllegroKuka.yaml:58 dofFriction -1 keeps
+    the URDF values, allegro_kuka_utils.py:79-80)."""
+    root = ET.parse(KUKA_URDF).getroot()
+    fr = {j.get("name"): urdf_joint_friction(j) for j in root.findall("joint")}
+    for path, get in ((ALLEGRO_OUT, lambda n: 0.01), (KUKA_OUT, lambda n: fr[n])):
+        with open(path) as f:
+            scene = json.load(f)
+        for d in scene["robot"]["dofs"]:
+            d["friction"] = get(d["name"])
+        with open(path, "w") as f:
+            json.dump(scene, f, indent=None, separators=(",", ":"))
+        print(path, [d["friction"] for d in scene["robot"]["dofs"]])
+
+
 if __name__ == "__main__":
+    if "--dof-friction" in sys.argv:
+        sys.exit(main_dof_friction())
     if "--pointclouds" in sys.argv:
         sys.exit(main_pointclouds())
     if "--bin" in sys.argv:
