@@ -100,6 +100,10 @@ extern "C" {
 #define HA_E_STATE -3
 #define HA_E_MODEL -4
 
+/* ha_params_t.narrow_phase_flags */
+#define HA_NP_NO_EDGE_AXES 1
+#define HA_NP_NO_CLIP 2
+
 /* flags for ha_task_step / ha_simulate */
 #define HA_FLAG_NO_PHYSICS 1u      /* skip physics substeps (task-math parity tests) */
 #define HA_FLAG_REPLAY_DRAWS 2u    /* reset draws come from ha_state_t.reset_draws (host RNG replay) */
@@ -274,6 +278,9 @@ typedef struct ha_params_t {
      * when that axis separates by more than edge_rel_tol x the best face axis + edge_abs_tol, else from the
      * clipped face manifold (Gregorius, "The Separating Axis Test between Convex Polyhedra", GDC 2013) */
     float edge_rel_tol, edge_abs_tol;
+    /* v10: narrow-phase switches (A/B timing, diagnostics; 0 = the full narrow phase): HA_NP_NO_EDGE_AXES skips
+     * the edge-edge axes, HA_NP_NO_CLIP keeps a face manifold to its incident vertices (the v9 narrow phase) */
+    int32_t narrow_phase_flags;
 } ha_params_t;
 
 /* Device buffers (caller-allocated). Layouts match the Isaac Gym tensors exactly. */

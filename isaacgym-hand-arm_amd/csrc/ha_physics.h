@@ -474,9 +474,6 @@ HD void dynamics(SimCtx& c) {
         // link damping (ha_params_t v10): the wrench cl m v_com, ca I_com w (moment about the world origin) with the
         // momentum (n2, f2) = (I_com w + c x m v_com, m v_com): g = c x m v_com = h x f2 / m
         float cl = c.p->link_lin_damping, ca = c.p->link_ang_damping;
-#ifdef HA_X_NODAMP
-        cl = ca = 0.0f;
-#endif
         if (cl != 0.0f || ca != 0.0f) {
             f3 g = I.m > 0.0f ? cross3(I.h, f2) * (1.0f / I.m) : mk3(0, 0, 0);
             fn = fn + ((n2 - g) * ca + g * cl);
@@ -898,16 +895,17 @@ HD int edge_cull(const SimCtx& c, const uint32_t* E, int ne, const float (*wv)[4
 // separating-axis candidate with separation N . (pA - pB). Returns -3e38 for any other pair (arcs apart, or edges
 // within 0.3 degrees of parallel). n, pa / e1, pb / e2: the axis and the edges (start, direction).
 HD float edge_axis(const ColView& cs, uint32_t ea, uint32_t eb, f3 cb, f3& n, f3& pa, f3& e1, f3& pb, f3& e2) {
-    f3 a = ld3(cs.wpA[(ea >> 16) & 255u]), b = ld3(cs.wpA[ea >> 24]);
-    f3 cc = ld3(cs.wpB[(eb >> 16) & 255u]) * -1.0f, dd = ld3(cs.wpB[eb >> 24]) * -1.0f;
-    f3 bxa = cross3(b, a), dxc = cross3(dd, cc);
-    float cba = dot3(cc, bxa), dba = dot3(dd, bxa), adc = dot3(a, dxc), bdc = dot3(b, dxc);
-    if (!(cba * dba < 0.0f && adc * bdc < 0.0f && cba * bdc > 0.0f)) return -3.0e38f;
+    // the outputs are set on every path (the caller reads them after the winning pair's call)
     pa = ld3(cs.wvA[ea & 255u]);
     e1 = ld3(cs.wvA[(ea >> 8) & 255u]) - pa;
     pb = ld3(cs.wvB[eb & 255u]);
     e2 = ld3(cs.wvB[(eb >> 8) & 255u]) - pb;
     n = cross3(e1, e2);
+    f3 a = ld3(cs.wpA[(ea >> 16) & 255u]), b = ld3(cs.wpA[ea >> 24]);
+    f3 cc = ld3(cs.wpB[(eb >> 16) & 255u]) * -1.0f, dd = ld3(cs.wpB[eb >> 24]) * -1.0f;
+    f3 bxa = cross3(b, a), dxc = cross3(dd, cc);
+    float cba = dot3(cc, bxa), dba = dot3(dd, bxa), adc = dot3(a, dxc), bdc = dot3(b, dxc);
+    if (!(cba * dba < 0.0f && adc * bdc < 0.0f && cba * bdc > 0.0f)) return -3.0e38f;
     float l2 = dot3(n, n);
     if (l2 < 2.5e-5f * (dot3(e1, e1) * dot3(e2, e2))) return -3.0e38f;
     n = n * (1.0f / sqrtf(l2));
@@ -1002,9 +1000,7 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     // ---- edge-edge axes (v10): a hull pair whose face axes leave it within the margin may still be separated along,
     //      or touch through, a pair of edges
     int nea = m.hull_nedges[ha], neb = m.hull_nedges[hb];
-#ifdef HA_X_NOEDGE
-    nea = 0;
-#endif
+    if (c.p->narrow_phase_flags & HA_NP_NO_EDGE_AXES) nea = 0;
     if (nea > 0 && neb > 0) {
         float smax = fmaxf(sepA, sepB);
         float pen = smax < 0.0f ? -smax : 0.0f;
@@ -1120,9 +1116,7 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         wave_argmin(vmin, ki);
         int lpi = m.plane_loop[m.hull_plane_start[hi] + ki], lpr = m.plane_loop[m.hull_plane_start[hr] + kr];
         int li0 = lpi & 0xFFFF, lni = lpi >> 16, lr0 = lpr & 0xFFFF, lnr = lpr >> 16;
-#ifdef HA_X_NOCLIP
-        lni = 0; lnr = 0;
-#endif
+        if (c.p->narrow_phase_flags & HA_NP_NO_CLIP) lni = lnr = 0;
         f3 ni = ld3(wpi[ki]);
         float di = wpi[ki][3];
         float den = dot3(ni, nref);
@@ -1234,9 +1228,13 @@ HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
     int h1, h2, b1, b2, k2;
     PoseF P1, P2;
     if (kind <= 3) {
-        int pa = upool(c, A);
-        int ho = m.pool_hull[pa];
+        // the objects of the pair: A on side A (kinds 1, 2), and the object on side B (kind 2: B, kind 3: A), posed by
+        // one call each, so that the branches below only pick values (the branches share no look-alike calls)
+        int pa = upool(c, A), ho = m.pool_hull[pa];
+        int ob = kind == 2 ? B : A;
+        int pb = upool(c, ob), n2 = m.pool_nhull[pb];
         PoseF Po = object_pose_u(c, A);
+        PoseF Pb = object_pose_u(c, ob);
         if (kind == 1) {
             h1 = ho + j; P1 = Po; b1 = A; h2 = m.static_hull[B]; P2 = static_pose(m, B); b2 = -1; k2 = -100 - B;
             // the piece's own sphere against the exact box (the oracle's per-piece near_box; for a one-hull object
@@ -1245,13 +1243,11 @@ HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
             if (!sphere_near_box(m.static_half[B], P2, cp, scale_radius(c, A, m.hull_radius[h1]) + c.p->contact_margin))
                 return;
         } else if (kind == 2) {
-            int pb = upool(c, B), n2 = m.pool_nhull[pb];
             int j1 = j / n2;
-            h1 = ho + j1; P1 = Po; b1 = A; h2 = m.pool_hull[pb] + (j - j1 * n2); P2 = object_pose_u(c, B);
-            b2 = B; k2 = B;
+            h1 = ho + j1; P1 = Po; b1 = A; h2 = m.pool_hull[pb] + (j - j1 * n2); P2 = Pb; b2 = B; k2 = B;
         } else {
             int Lk = m.hull_link[B];
-            h1 = B; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = ho + j; P2 = Po; b2 = A; k2 = A;
+            h1 = B; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = ho + j; P2 = Pb; b2 = A; k2 = A;
         }
     } else {
         int Lk = m.hull_link[A];
@@ -1359,6 +1355,10 @@ HD void detect(SimCtx& c) {
             int bit = __ffsll((unsigned long long)mask) - 1;
             int q = base + bit;
             pair_desc(c, q, kind, A, B);
+            // the pair is wave-uniform: say so, so that the narrow phase branches on scalars (no exec-masked regions)
+            kind = __builtin_amdgcn_readfirstlane(kind);
+            A = __builtin_amdgcn_readfirstlane(A);
+            B = __builtin_amdgcn_readfirstlane(B);
             int np = pair_pieces(c, kind, A, B);
 #ifdef HA_PROFILE
             unsigned long long _k0 = __builtin_amdgcn_s_memtime();
@@ -1705,9 +1705,6 @@ HD void substep(SimCtx& c, float hdt) {
     int act_lo = 0, act_up = 0;
     if (lane < D) {
         flim = m.dof_friction[lane] * hdt;
-#ifdef HA_X_NOFRIC
-        flim = 0.0f;
-#endif
         float kp = m.dof_kp[lane], kd = m.dof_kd[lane];
         float den = kd + hdt * kp;
         float mii = c.Minv[lane * D + lane];

@@ -44,6 +44,7 @@ AK_REWARD_KEYS = ["raw_fingertip_delta_rew", "raw_hand_delta_penalty", "raw_lift
 FLAG_NO_PHYSICS = 1
 FLAG_REPLAY_DRAWS = 2
 FLAG_OBS_ONLY = 4
+NP_NO_EDGE_AXES, NP_NO_CLIP = 1, 2      # ha_params_t.narrow_phase_flags
 
 f32, i32 = C.c_float, C.c_int32
 
@@ -128,6 +129,7 @@ class HaParams(C.Structure):
         ("ak_num_arm_dofs", i32),
         ("contact_slop", f32), ("manifold_window", f32),                       # v9
         ("link_lin_damping", f32), ("link_ang_damping", f32), ("edge_rel_tol", f32), ("edge_abs_tol", f32),  # v10
+        ("narrow_phase_flags", i32),
     ]
 
 
@@ -501,6 +503,7 @@ DEFAULT_TASK = dict(
     contact_slop=0.001, manifold_window=0.002,
     link_lin_damping=0.01, link_ang_damping=0.01,       # ur5sih.py:178-179
     edge_rel_tol=0.9, edge_abs_tol=0.0005,              # edge-edge vs face axis (handarm_abi.h v10)
+    narrow_phase_flags=0,                               # HA_NP_* (A/B and diagnostics only)
     joint_limit_margin=0.02, n_objects=3, num_initial_poses=1, max_episode_length=200,
     sih_alpha=0.8, reward_reaching=1.0, reward_lifting=5.0, reward_goal=50.0, reward_success=50.0,
     lifting_threshold=0.05, goal_threshold=0.05, goal_pos=(0.28, 0.58, 0.8), goal_noise=(0.15, 0.15, 0.1),
@@ -608,7 +611,7 @@ def build_params(cfg=None, task=None):
     p = HaParams()
     for k in ["dt", "substeps", "control_freq_inv", "solver_iters", "friction", "contact_margin", "baumgarte",
               "contact_slop", "manifold_window", "link_lin_damping", "link_ang_damping", "edge_rel_tol",
-              "edge_abs_tol",
+              "edge_abs_tol", "narrow_phase_flags",
               "max_depen_vel", "object_ang_damping", "joint_limit_margin", "n_objects", "num_initial_poses",
               "max_episode_length", "sih_alpha", "reward_reaching", "reward_lifting", "reward_goal",
               "reward_success", "lifting_threshold", "goal_threshold", "seed"]:

@@ -49,6 +49,10 @@ def obs_sizes(n_objects):
 NO_BIN_EXTENT = [[0.03, 0.28, 0.5], [0.53, 0.78, 0.7]]
 
 
+# drop rounds after which the initialisation gives up with an error (objects.drop.max_rounds unset); the
+# reference has no limit (multi_object_manipulation.py:97), a full 8192-env shard needs a handful of rounds
+DROP_ROUNDS_LIMIT = 1000
+
 class Box:
     """Minimal gym.spaces.Box (openai-gym is not a dependency here)."""
 
@@ -193,6 +197,10 @@ class Ur5SihMultiObjectManipulation:
         self.dof_pos[:] = torch.tensor(self.sim.params.reset_pose[:D], device=self.device)
         t["sim_targets"].copy_(self.dof_pos)
         self._sync_obs_cache()      # observables' post_step in ConfigurableVecTask.__init__
+        if self.pointclouds is not None:
+            # the clouds' post_step there too (configurable_vec_task.py:43-44): with sim.reference_rng its
+            # torch.randperm is a draw from the global CPU generator before the first reset's (multi_object.py:806)
+            self.pointclouds.refresh()
         self.objects_dropped = False
         # the reference drops until every object lands in the extent (multi_object_manipulation.py:97-136); a
         # round cap is a diagnostic option only (objects.drop.max_rounds: stop there, or with
@@ -426,9 +434,19 @@ class Ur5SihMultiObjectManipulation:
                     break
                 if rounds == self.max_drop_rounds:          # diagnostic: stop, leaving the objects where they are
                     break
+                if self.max_drop_rounds is None and rounds >= DROP_ROUNDS_LIMIT:
+                    # the reference loops forever on an object that never lands in the extent; fail loudly instead
+                    bad = (~in_bin).nonzero(as_tuple=False)[:10].tolist()
+                    raise RuntimeError(f"drop initialisation: {int((~in_bin).sum())} objects still outside the bin "
+                                       f"extent after {rounds} rounds (env, object): {bad}")
                 rounds += 1
                 print(f"[handarm_hip] drop init pose {p}: round {rounds}, {int((~in_bin).sum())} objects to drop",
                       file=sys.stderr, flush=True)
+                # envs stepped while object i drops: the reference steps every env (multi_object_manipulation.py:
+                # 123-125); with sim.reference_rng so does this loop. Otherwise the envs that dropped any object in
+                # this round so far (an env that re-dropped object j < i keeps stepping while object i drops, as in
+                # the reference); envs with nothing in flight this round wait (they settle with all envs below)
+                dropping = torch.zeros(N, dtype=torch.bool, device=self.device)
                 for i in range(n_obj):
                     enabled[:, i] = 1
                     self.sim.set_object_collisions(enabled)
@@ -444,11 +462,10 @@ class Ur5SihMultiObjectManipulation:
                             rf = torch_rand_float(-1.0, 1.0, (len(env_ids), 2), device=self.device)
                             rs[env_ids, i, 3:7] = randomize_rotation(rf[:, 0], rf[:, 1])
                         rs[env_ids, i, 7:13] = 0.0
-                        # the reference steps every env here; only the envs dropping object i are stepped (the
-                        # others have nothing in flight, and all envs settle together below): later rounds,
-                        # which re-drop a handful of objects, cost a handful of envs instead of the shard
+                        dropping |= ~in_bin[:, i]
+                        step_ids = None if self.reference_rng else dropping.nonzero(as_tuple=False).squeeze(-1)
                         self.sim.simulate(self.task_cfg["drop_num_steps"],
-                                          env_ids=env_ids if len(env_ids) < N else None)
+                                          env_ids=step_ids if step_ids is not None and len(step_ids) < N else None)
                 obj_pos = rs[:, :, 0:3]
                 in_bin = ((obj_pos >= bin_lo) & (obj_pos <= bin_hi)).all(-1)
             for _ in range(600):                                                    # settle
@@ -458,6 +475,10 @@ class Ur5SihMultiObjectManipulation:
             pos_init[:, p] = rs[:, :, 0:3]
             quat_init[:, p] = rs[:, :, 3:7]
             self._sync_obs_cache()
+            if self.pointclouds is not None:
+                # every observable's post_step after the settle (multi_object_manipulation.py:149-150): the object
+                # cloud's randperm draw, in the reference's order with sim.reference_rng
+                self.pointclouds.refresh()
         self.objects_dropped = True
 
     def contact_stats(self, reset=False):

@@ -394,6 +394,7 @@ static int reduce_manifold(const v3* pts, const float* seps, int nc, v3 n, const
 static __thread int g_on, g_n;
 static __thread float g_window;     /* ha_params_t.manifold_window of the running detect() */
 static __thread float g_edge_rel, g_edge_abs;   /* ha_params_t.edge_rel_tol / edge_abs_tol of the running detect() */
+static __thread int g_np_flags;                 /* ha_params_t.narrow_phase_flags */
 static __thread v3 g_pt[MAXGATHER], g_nrm[MAXGATHER];
 static __thread float g_sep[MAXGATHER];
 
@@ -532,6 +533,7 @@ static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t
     if (sepB > margin) return;
     /* edge-edge axes: the edges of each hull within R of the other's centre, every (A, B) pair in list order */
     int nea = m->hull_nedges[ha], neb = m->hull_nedges[hb];
+    if (g_np_flags & HA_NP_NO_EDGE_AXES) nea = 0;
     if (nea > 0 && neb > 0) {
         float smax = fmaxf(sepA, sepB);
         float pen = smax < 0.0f ? -smax : 0.0f;
@@ -599,6 +601,7 @@ static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t
         }
         int lpi = m->plane_loop[m->hull_plane_start[hi] + ki], lpr = m->plane_loop[m->hull_plane_start[hr] + kr];
         int li0 = lpi & 0xFFFF, lni = lpi >> 16, lr0 = lpr & 0xFFFF, lnr = lpr >> 16;
+        if (g_np_flags & HA_NP_NO_CLIP) lni = lnr = 0;
         /* the kernel holds the candidates one per lane: the valid vertices at lanes [0, nv1), edge j's entry / exit
          * point at lane nv1 + 2 j (+ 1), reference vertex r at lane nv1 + 2 lni + r; lanes past 63 are dropped */
         int nv1 = nc;
@@ -688,6 +691,7 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
     g_window = p->manifold_window;
     g_edge_rel = p->edge_rel_tol;
     g_edge_abs = p->edge_abs_tol;
+    g_np_flags = p->narrow_phase_flags;
     for (int o = 0; o < h->NO; o++) {
         if (!e->coll[o]) continue;
         int pa = e->pool[o];

@@ -509,6 +509,7 @@ def gen_pointclouds(path, student, N=8, steps=4, seed=5):
            + clouds}
     orig = torch.randperm
     perms = []
+    torch.manual_seed(seed + 200)    # the reference draws the cloud randperm from torch's global generator
 
     def randperm(*a, **k):
         r = orig(*a, **k)

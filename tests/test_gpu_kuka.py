@@ -97,8 +97,9 @@ def test_kuka_step_with_resets_replayed_against_reference_goldens(sub):
         np.testing.assert_allclose(get(sim, "goal_state"), d["goal_after"][t], rtol=1e-6, atol=1e-6)
         # fingertip / palm rows come from the device FK here and from the C oracle's FK in the goldens
         close(get(sim, "obs"), d["obs"][t], 1e-5, 2e-5, f"obs step {t}")
-        np.testing.assert_allclose(get(sim, "rew"), d["rew"][t], rtol=1e-4, atol=2e-3)
-        np.testing.assert_allclose(get(sim, "task_state")[:, :32], d["task_state"][t][:, :32], rtol=1e-5, atol=2e-3)
+        # measured max |d| 1.24e-5 over both subtasks (tools/kuka_tol_probe.py)
+        np.testing.assert_allclose(get(sim, "rew"), d["rew"][t], rtol=1e-5, atol=1e-4)
+        np.testing.assert_allclose(get(sim, "task_state")[:, :32], d["task_state"][t][:, :32], rtol=1e-5, atol=1e-4)
 
 
 def _oracle_and_sim(n, seed, force):
