@@ -852,16 +852,6 @@ HD void sat_planes(const SimCtx& c, const float (*wp)[4], int np, const float (*
     kbest = bk;
 }
 
-// side plane of edge j of a face loop (world vertices wv, loop vertex indices lv[0..n), face normal nf): the plane
-// through the edge perpendicular to the face, unit outward normal cross(e, nf) (the loop runs counter-clockwise about
-// nf), offset d
-HD f3 side_plane(const float (*wv)[4], const uint8_t* lv, int j, int n, f3 nf, float& d) {
-    f3 v0 = ld3(wv[lv[j]]);
-    f3 sn = cross3(ld3(wv[lv[j + 1 == n ? 0 : j + 1]]) - v0, nf);
-    sn = sn * (1.0f / sqrtf(dot3(sn, sn)));
-    d = -dot3(sn, v0);
-    return sn;
-}
 // squared distance from point q to the segment p0 + t (p1 - p0), t in [0, 1] (the oracle's seg_point_d2)
 HD float seg_point_d2(f3 p0, f3 p1, f3 q) {
     f3 d = p1 - p0;
@@ -1015,18 +1005,61 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         wsync();
         float best = -3.0e38f;
         int bw = 1 << 30;
-        int total = nA * nB;
-        if (total > 0) {
-            int i = lane / nB, j = lane - i * nB;
-            int si = 64 / nB, sj = 64 - si * nB;
+        // pairs (i, j) of the two lists, w = i nB + j: the lanes take the elements of the longer list (64 at a time)
+        // and loop over the shorter one, whose element is wave-uniform per iteration. Per-edge terms (start,
+        // direction, face normals, the Gauss-arc normal, the B edge's offset from cb) are formed once per element,
+        // by the same expressions edge_axis evaluates per pair; the winner (max, then lowest w) is the oracle's
+        // i-major scan
+        if (nA > 0 && nB > 0) {
+            bool aLong = nA >= nB;
+            int nL = aLong ? nA : nB, nS = aLong ? nB : nA;
+            const uint8_t* lL = aLong ? la : lb;
+            const uint8_t* lS = aLong ? lb : la;
+            const uint32_t* EL = aLong ? EA : EB;
+            const uint32_t* ES = aLong ? EB : EA;
+            const float (*wvL)[4] = aLong ? cs.wvA : cs.wvB;
+            const float (*wvS)[4] = aLong ? cs.wvB : cs.wvA;
+            const float (*wpL)[4] = aLong ? cs.wpA : cs.wpB;
+            const float (*wpS)[4] = aLong ? cs.wpB : cs.wpA;
+            // the short list's records, element t in lane t (t < 64)
+            uint32_t recS = lane < nS ? ES[lS[lane]] : 0u;
 #pragma unroll 1
-            for (int w = lane; w < total; w += 64) {
-                f3 n, pa, pb, e1, e2;
-                float sv = edge_axis(cs, EA[la[i]], EB[lb[j]], cb, n, pa, e1, pb, e2);
-                if (sv > best) { best = sv; bw = w; }
-                i += si;
-                j += sj;
-                if (j >= nB) { j -= nB; i++; }
+            for (int base = 0; base < nL; base += 64) {
+                int li = base + lane;
+                bool act = li < nL;
+                uint32_t rl = act ? EL[lL[li]] : EL[lL[0]];
+                // this lane's edge: A side (pa, e1, a, b, bxa) or B side (pb, e2, -f0, -f1, dxc, pb - cb)
+                f3 lp = ld3(wvL[rl & 255u]);
+                f3 le = ld3(wvL[(rl >> 8) & 255u]) - lp;
+                f3 lf0 = ld3(wpL[(rl >> 16) & 255u]), lf1 = ld3(wpL[rl >> 24]);
+                if (!aLong) { lf0 = lf0 * -1.0f; lf1 = lf1 * -1.0f; }
+                f3 lx = cross3(lf1, lf0);
+                f3 lo = lp - cb;
+#pragma unroll 1
+                for (int si = 0; si < nS; si++) {
+                    uint32_t rs = si < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)recS, si)
+                                          : ES[__builtin_amdgcn_readfirstlane(lS[si])];
+                    f3 sp = ld3(wvS[rs & 255u]);
+                    f3 se = ld3(wvS[(rs >> 8) & 255u]) - sp;
+                    f3 sf0 = ld3(wpS[(rs >> 16) & 255u]), sf1 = ld3(wpS[rs >> 24]);
+                    if (aLong) { sf0 = sf0 * -1.0f; sf1 = sf1 * -1.0f; }
+                    f3 sx = cross3(sf1, sf0);
+                    // A: (a, b, bxa) = (f0, f1, f1 x f0); B: (c, d, dxc) = (-f0, -f1, (-f1) x (-f0))
+                    f3 a = aLong ? lf0 : sf0, b = aLong ? lf1 : sf1, bxa = aLong ? lx : sx;
+                    f3 cc = aLong ? sf0 : lf0, dd = aLong ? sf1 : lf1, dxc = aLong ? sx : lx;
+                    float cba = dot3(cc, bxa), dba = dot3(dd, bxa), adc = dot3(a, dxc), bdc = dot3(b, dxc);
+                    if (!(cba * dba < 0.0f && adc * bdc < 0.0f && cba * bdc > 0.0f)) continue;
+                    f3 pa = aLong ? lp : sp, e1 = aLong ? le : se, pb = aLong ? sp : lp, e2 = aLong ? se : le;
+                    f3 n = cross3(e1, e2);
+                    float l2 = dot3(n, n);
+                    if (l2 < 2.5e-5f * (dot3(e1, e1) * dot3(e2, e2))) continue;
+                    n = n * (1.0f / sqrtf(l2));
+                    f3 pbo = aLong ? sp - cb : lo;
+                    if (dot3(n, pbo) < 0.0f) n = n * -1.0f;
+                    float sv = dot3(n, pa - pb);
+                    int w = aLong ? li * nB + si : si * nB + li;
+                    if (act && sv > best) { best = sv; bw = w; }
+                }
             }
         }
         wave_argmax(best, bw);
@@ -1120,48 +1153,71 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         f3 ni = ld3(wpi[ki]);
         float di = wpi[ki][3];
         float den = dot3(ni, nref);
+        // the two face loops staged in lanes: lane j holds loop vertex j of each face and the side plane through
+        // loop edge j (side_plane, the same expression for every (candidate, plane) pair), so the clipping loops
+        // below read them with v_readlane instead of re-deriving them per candidate from the model's loop lists
+        int rv = lane < lnr ? m.loop_v[lr0 + lane] : 0, iv = lane < lni ? m.loop_v[li0 + lane] : 0;
+        f3 rsn = mk3(0, 0, 0), isn = mk3(0, 0, 0);
+        float rsd = 0.0f, isd = 0.0f;
+        if (lane < lnr) {
+            int rv1 = m.loop_v[lr0 + (lane + 1 == lnr ? 0 : lane + 1)];
+            f3 v0 = ld3(wvr[rv]);
+            rsn = cross3(ld3(wvr[rv1]) - v0, nref);
+            rsn = rsn * (1.0f / sqrtf(dot3(rsn, rsn)));
+            rsd = -dot3(rsn, v0);
+        }
+        if (lane < lni) {
+            int iv1 = m.loop_v[li0 + (lane + 1 == lni ? 0 : lane + 1)];
+            f3 v0 = ld3(wvi[iv]);
+            isn = cross3(ld3(wvi[iv1]) - v0, ni);
+            isn = isn * (1.0f / sqrtf(dot3(isn, isn)));
+            isd = -dot3(isn, v0);
+        }
         int q = lane - nv1;
-        if (q >= 0 && q < 2 * lni) {
-            // (2) incident-face loop edge q / 2 clipped (Cyrus-Beck) to the reference face's side planes (through its
-            //     loop edges, perpendicular to it: side_plane): the entry (even q) or exit (odd q) point, when inside
-            //     the segment and within the margin of the reference face
-            int je = q >> 1;
-            f3 p0 = ld3(wvi[m.loop_v[li0 + je]]);
-            f3 p1 = ld3(wvi[m.loop_v[li0 + (je + 1 == lni ? 0 : je + 1)]]);
-            float tin = 0.0f, tout = 1.0f;
-            bool out = false;
-            for (int jj = 0; jj < lnr; jj++) {
-                float sd;
-                f3 sn = side_plane(wvr, m.loop_v + lr0, jj, lnr, nref, sd);
-                float f0 = dot3(sn, p0) + sd, f1 = dot3(sn, p1) + sd;
-                if (f0 > 0.0f && f1 > 0.0f) out = true;
-                else if (f0 > 0.0f) tin = fmaxf(tin, f0 / (f0 - f1));
-                else if (f1 > 0.0f) tout = fminf(tout, f0 / (f0 - f1));
-            }
+        int qe = q >> 1, qr = q - 2 * lni;
+        int ivq0 = __shfl(iv, qe < 0 ? 0 : qe), ivq1 = __shfl(iv, qe + 1 >= lni ? 0 : qe + 1);
+        int rvq = __shfl(rv, qr < 0 ? 0 : qr);
+        // (2) lanes q < 2 lni: incident-face loop edge q / 2 clipped (Cyrus-Beck) to the reference face's side planes
+        //     (through its loop edges, perpendicular to it): the entry (even q) or exit (odd q) point, when inside the
+        //     segment and within the margin of the reference face
+        // (3) lanes 2 lni <= q < 2 lni + lnr: reference-face loop vertex q - 2 lni projected along the reference normal
+        //     onto the incident face's plane: a candidate when inside the incident face's side planes and within the
+        //     margin
+        // The plane loops run in wave-uniform control flow: a v_readlane of a lane's side plane inside a divergent
+        // branch would read a register the allocator may reuse in that lane on the other branch
+        bool isclip = q >= 0 && q < 2 * lni;
+        bool isref = q >= 2 * lni && q < 2 * lni + lnr;
+        f3 p0 = ld3(wvi[ivq0]), p1 = ld3(wvi[ivq1]);
+        f3 r = ld3(wvr[rvq]);
+        float sr = den < -1e-6f ? -(dot3(ni, r) + di) / den : 0.0f;
+        f3 xr = r + nref * sr;
+        float tin = 0.0f, tout = 1.0f, mx = -3.0e38f;
+        bool out = false;
+#pragma unroll 1
+        for (int jj = 0; jj < lnr; jj++) {
+            f3 sn = mk3(bcast(rsn.x, jj), bcast(rsn.y, jj), bcast(rsn.z, jj));
+            float sd = bcast(rsd, jj);
+            float f0 = dot3(sn, p0) + sd, f1 = dot3(sn, p1) + sd;
+            if (f0 > 0.0f && f1 > 0.0f) out = true;
+            else if (f0 > 0.0f) tin = fmaxf(tin, f0 / (f0 - f1));
+            else if (f1 > 0.0f) tout = fminf(tout, f0 / (f0 - f1));
+        }
+#pragma unroll 1
+        for (int jj = 0; jj < lni; jj++) {
+            f3 sn = mk3(bcast(isn.x, jj), bcast(isn.y, jj), bcast(isn.z, jj));
+            mx = fmaxf(mx, dot3(sn, xr) + bcast(isd, jj));
+        }
+        if (isclip) {
             bool ex = (q & 1) != 0;
             f3 xc = p0 + (p1 - p0) * (ex ? tout : tin);
             float dx = dot3(nref, xc) + dref;
             ok = !out && (ex ? (tout < 1.0f && tin < tout) : (tin > 0.0f && tin <= tout)) && dx <= mg;
             x = xc - nref * (0.5f * dx);
             sv = dx;
-        } else if (q >= 2 * lni && q < 2 * lni + lnr) {
-            // (3) reference-face loop vertex q - 2 lni projected along the reference normal onto the incident face's
-            //     plane: a candidate when inside the incident face's side planes and within the margin
-            ok = false;
-            if (den < -1e-6f) {
-                f3 r = ld3(wvr[m.loop_v[lr0 + (q - 2 * lni)]]);
-                float sr = -(dot3(ni, r) + di) / den;
-                f3 xr = r + nref * sr;
-                float mx = -3.0e38f;
-                for (int jj = 0; jj < lni; jj++) {
-                    float sd;
-                    f3 sn = side_plane(wvi, m.loop_v + li0, jj, lni, ni, sd);
-                    mx = fmaxf(mx, dot3(sn, xr) + sd);
-                }
-                ok = sr <= mg && mx <= 0.0f;
-                x = r + nref * (0.5f * sr);
-                sv = sr;
-            }
+        } else if (isref) {
+            ok = den < -1e-6f && sr <= mg && mx <= 0.0f;
+            x = r + nref * (0.5f * sr);
+            sv = sr;
         }
         HPROF(31);
         if (__ballot(ok)) {

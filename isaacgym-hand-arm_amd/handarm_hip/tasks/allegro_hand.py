@@ -92,7 +92,11 @@ class AllegroHand:
         self._rr = RR.AllegroDraws(N) if self.reference_rng else None
         self.extras = {}
         self.obs_dict = {}
-        # obs_dict["obs"] = clamp(obs_buf) by ha_task_epilogue into one of two alternating buffers
+        # obs_dict["obs"] = clamp(obs_buf) by ha_task_epilogue into one of two alternating buffers: step t's obs
+        # (and extras["consecutive_successes"], a view of the task's counter) stay valid through step t+1 and are
+        # overwritten by step t+2. env.freshOutputs=True returns new tensors every step, as the reference's
+        # torch.clamp / .mean() do (allegro_hand.py:393,707)
+        self.fresh_outputs = bool(env.get("freshOutputs", False))
         self._obs_out = torch.zeros((2, N, self.num_observations), device=sim_device)
         self.control_steps = 0
         self.total_successes = 0
@@ -143,13 +147,15 @@ class AllegroHand:
         return torch.zeros((self.num_envs, self.num_actions), dtype=torch.float32, device=self.rl_device)
 
     def step(self, actions):
-        """VecTask.step (vec_task.py:390-441) -> pre_physics_step / simulate x2 / post_physics_step, fused."""
+        """VecTask.step (vec_task.py:390-441) -> pre_physics_step / simulate x2 / post_physics_step, fused.
+        obs_dict["obs"] is valid until the step after next unless env.freshOutputs is set (see __init__)."""
         torch.clamp(actions, -self.clip_actions, self.clip_actions, out=self.actions_buf)
         self.sim.task_step(self.sim_flags | self._reference_draws())
         self.control_steps += 1
         self.extras["time_outs"] = self.timeout_buf.view(torch.bool).to(self.rl_device)
-        self.extras["consecutive_successes"] = self.consecutive_successes.view(())     # allegro_hand.py:393 (1 value)
-        out = self._obs_out[self.control_steps & 1]
+        cs = self.consecutive_successes.view(())                                     # allegro_hand.py:393 (1 value)
+        self.extras["consecutive_successes"] = cs.clone() if self.fresh_outputs else cs
+        out = torch.empty_like(self._obs_out[0]) if self.fresh_outputs else self._obs_out[self.control_steps & 1]
         _lib.check(self.sim.lib.ha_task_epilogue(self.sim.h, out.data_ptr(), self.clip_obs, None, self.sim._stream()),
                    "ha_task_epilogue")
         self.obs_dict["obs"] = out.to(self.rl_device)

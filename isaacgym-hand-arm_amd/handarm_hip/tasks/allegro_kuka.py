@@ -126,9 +126,12 @@ class AllegroKuka:
         self.frame_since_restart = 0
         self.extras = {}
         self.obs_dict = {}
-        # step tail (ha_task_epilogue, one launch): obs_dict["obs"] = clamp(obs_buf) in one of two alternating
-        # buffers (a fresh tensor as the reference's torch.clamp returns, valid until the step after next) and
-        # the extras means in two alternating 4-float rows
+        # step tail (ha_task_epilogue, one launch): obs_dict["obs"] = clamp(obs_buf) and the extras means
+        # (successes, true_objective mean/min/max). Lifetime: by default they land in one of two alternating
+        # buffers, so the tensors step t returns stay valid through step t+1 and are overwritten by step t+2 (no
+        # allocation per step). env.freshOutputs=True gives every step new tensors, as the reference's
+        # torch.clamp / .mean() do (allegro_kuka_base.py:908-917,1445), for a consumer that keeps them longer
+        self.fresh_outputs = bool(env.get("freshOutputs", False))
         self._obs_out = torch.zeros((2, N, self.num_observations), device=sim_device)
         self._scalars = torch.zeros((2, 4), device=sim_device)
         # seed-faithful draws (handarm_hip/ref_rng.py): every reset / force value from torch's global CPU
@@ -202,13 +205,19 @@ class AllegroKuka:
             self._set_tolerance(tol)
 
     def step(self, actions):
-        """VecTask.step (vec_task.py:390-441) -> pre_physics_step / simulate / post_physics_step, fused."""
+        """VecTask.step (vec_task.py:390-441) -> pre_physics_step / simulate / post_physics_step, fused.
+        obs_dict["obs"] and the extras means are valid until the step after next unless env.freshOutputs is set
+        (see __init__); rew / reset / time_outs are the task's buffers, as in the reference."""
         torch.clamp(actions, -self.clip_actions, self.clip_actions, out=self.actions_buf)
         self.frame_since_restart += 1
         self._curriculum()
         self.sim.task_step(self.sim_flags | self._reference_draws())
-        k = self.frame_since_restart & 1
-        out, sc = self._obs_out[k], self._scalars[k]
+        if self.fresh_outputs:
+            out = torch.empty_like(self._obs_out[0])
+            sc = torch.empty_like(self._scalars[0])
+        else:
+            k = self.frame_since_restart & 1
+            out, sc = self._obs_out[k], self._scalars[k]
         _lib.check(self.sim.lib.ha_task_epilogue(self.sim.h, out.data_ptr(), self.clip_obs, sc.data_ptr(),
                                                  self.sim._stream()), "ha_task_epilogue")
         ex = self.extras

@@ -276,7 +276,7 @@ def link_hull_world_verts(model, body_state_env, link):
 
 def place_cuboid_edge_on_link(st, model, body_state, link, pen=0.0003):
     """AllegroKuka: each env's cuboid (its object_scale dims of the 0.05 m base cube) rotated 45 deg about x, its
-    bottom ridge (along x) `pen` below the highest vertex of link `link`'s hulls, centred over it, at rest."""
+    bottom ridge (along x) `pen` below the highest vertex of link `link`'s hulls and over it, at rest."""
     N, A = st.num_envs, model.n_actors
     rs = st["root_state"].reshape(N, A, 13)
     sc = st["object_scale"].reshape(N, 3)
@@ -286,7 +286,9 @@ def place_cuboid_edge_on_link(st, model, body_state, link, pen=0.0003):
         v = link_hull_world_verts(model, body[e], link)
         top = v[np.argmax(v[:, 2])]
         hy, hz = 0.025 * sc[e, 1], 0.025 * sc[e, 2]
-        rs[e, model.actor_object0, 0:3] = [top[0], top[1], top[2] + (hy + hz) / np.sqrt(2.0) - pen]
+        # the lowest ridge is the (-y, -z) edge, offset (hz - hy)/sqrt(2) in y from the centre
+        rs[e, model.actor_object0, 0:3] = [top[0], top[1] - (hz - hy) / np.sqrt(2.0),
+                                           top[2] + (hy + hz) / np.sqrt(2.0) - pen]
         rs[e, model.actor_object0, 3:7] = q
         rs[e, model.actor_object0, 7:13] = 0.0
     st["object_force"][:] = 0.0

@@ -41,7 +41,7 @@ if __name__ == "__main__":
             print(f"    narrow {name:10s}: {buf[15 + k] / sub:6.2f} pairs/substep, {buf[20 + k] / sub:6.2f} with contacts, "
                   f"{100.0 * buf[10 + k] / tot:5.1f}% of substep cycles", flush=True)
         print("    hull-hull split: " + "  ".join(f"{nm} {100.0 * buf[25 + i] / tot:5.1f}%" for i, nm in
-              enumerate(["setup", "SAT A", "SAT B", "clip", "emit"])), flush=True)
+              enumerate(["setup", "SAT A", "SAT B", "incident", "emit", "edge-edge", "clip"])), flush=True)
 
     if any(f in sys.argv for f in ("--bench-scene", "--kuka", "--bin", "--allegro", "--c4")):
         # the bench workload: VecTask after its first (reset) steps, random actions
