@@ -284,6 +284,9 @@ struct SimCtx {
     int colA_h, colA_b, colB_h, colB_b;
     bool colA_p;            // side A's world planes are in ColScratch too (SAT B runs first and may exit before them)
     bool gather;            // a compound object pair's piece pairs: reduced points go to ColScratch gp / gn
+#ifdef HA_PROFILE
+    int pk;                 // profiled build: kind of the running pair
+#endif
 #ifdef HA_AB_TIMING
     bool dry;               // A/B timing builds only: a repeated phase that must not emit contacts
 #endif
@@ -309,7 +312,7 @@ HD float wave_sum_rows(float x) {
 // Diagnostic phase timers (built only into libhandarm_hip_prof.so, -DHA_PROFILE): lane 0 of every
 // wave adds the s_memtime delta of each phase; read back with ha_profile_read().
 #ifdef HA_PROFILE
-__device__ unsigned long long g_prof[32];
+__device__ unsigned long long g_prof[96];   // [32 + 8 kind + phase]: the hull-hull split per pair kind
 #define PROF_BEGIN() unsigned long long _pt = __builtin_amdgcn_s_memtime();
 #define PROF_COUNT(i, v)                                               \
     do {                                                               \
@@ -939,7 +942,8 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     const ColView& cs = c.col;
 #ifdef HA_PROFILE
     unsigned long long _h0 = __builtin_amdgcn_s_memtime();
-#define HPROF(i) do { wsync(); unsigned long long _h1 = __builtin_amdgcn_s_memtime(); PROF_COUNT(i, _h1 - _h0); _h0 = _h1; } while (0)
+#define HPROF(i) do { wsync(); unsigned long long _h1 = __builtin_amdgcn_s_memtime(); PROF_COUNT(i, _h1 - _h0); \
+                          PROF_COUNT(32 + 8 * c.pk + (i) - 25, _h1 - _h0); _h0 = _h1; } while (0)
 #else
 #define HPROF(i)
 #endif
@@ -955,6 +959,9 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         f3 isB = inv_scale(c, b);
         for (int k = lane; k < npb; k += 64) {
             f3 n; float d;
+#ifdef HA_X_PLANE_INLOOP    /* diagnostic: the inverse scale read inside the plane loop */
+            isB = inv_scale(c, b);
+#endif
             world_plane(m, hb, k, PB, scB, isB, n, d);
             st3(cs.wpB[k], n);
             cs.wpB[k][3] = d;
@@ -976,6 +983,9 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         f3 isA = inv_scale(c, a);
         for (int k = lane; k < npa; k += 64) {
             f3 n; float d;
+#ifdef HA_X_PLANE_INLOOP
+            isA = inv_scale(c, a);
+#endif
             world_plane(m, ha, k, PA, scA, isA, n, d);
             st3(cs.wpA[k], n);
             cs.wpA[k][3] = d;
@@ -1415,6 +1425,9 @@ HD void detect(SimCtx& c) {
             kind = __builtin_amdgcn_readfirstlane(kind);
             A = __builtin_amdgcn_readfirstlane(A);
             B = __builtin_amdgcn_readfirstlane(B);
+#ifdef HA_PROFILE
+            c.pk = kind;
+#endif
             int np = pair_pieces(c, kind, A, B);
 #ifdef HA_PROFILE
             unsigned long long _k0 = __builtin_amdgcn_s_memtime();

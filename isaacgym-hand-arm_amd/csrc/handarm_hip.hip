@@ -1165,11 +1165,11 @@ float ha_last_kernel_ms(ha_handle h) {
 }  // extern "C"
 
 #ifdef HA_PROFILE
-// diagnostic build only: per-phase s_memtime totals summed over waves (see PROF in ha_physics.h)
+// diagnostic build only: per-phase s_memtime totals summed over waves (see PROF in ha_physics.h), 96 counters
 extern "C" int ha_profile_read(unsigned long long* out32, int reset) {
-    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 32) != hipSuccess) return HA_E_HIP;
+    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 96) != hipSuccess) return HA_E_HIP;
     if (reset) {
-        unsigned long long z[32] = {0};
+        unsigned long long z[96] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return HA_E_HIP;
     }
     return HA_OK;

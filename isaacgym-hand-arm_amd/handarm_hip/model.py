@@ -616,6 +616,8 @@ def build_params(cfg=None, task=None):
               "max_episode_length", "sih_alpha", "reward_reaching", "reward_lifting", "reward_goal",
               "reward_success", "lifting_threshold", "goal_threshold", "seed"]:
         setattr(p, k, c[k])
+    if os.environ.get("HA_NP_FLAGS"):          # A/B timing of the narrow-phase stages (HA_NP_*), diagnostics only
+        p.narrow_phase_flags = int(os.environ["HA_NP_FLAGS"])
     p.gravity[:] = c["gravity"]
     p.action_dt = c["dt"]                      # VecTask.dt = sim_params.dt (vec_task.py:267)
     p.sih_beta = 1.0 - c["sih_alpha"]          # (1 - alpha) * s: python double, cast once (ur5sih.py:496)

@@ -11,6 +11,10 @@ for p in (ROOT, PKG_PARENT):
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+if os.environ.get("HA_LIB"):        # diagnostics: run the suite against a variant build of the library
+    from handarm_hip import _lib
+    _lib.LIB_PATH = os.environ["HA_LIB"]
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")

@@ -26,7 +26,7 @@ if __name__ == "__main__":
     from tools.perf_probe import run
     lib = _lib.load()
     lib.ha_profile_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    buf = (C.c_ulonglong * 32)()
+    buf = (C.c_ulonglong * 96)()
     args = [x for x in sys.argv[1:] if not x.startswith("--")]
     n = int(args[0]) if args else 8192
 
@@ -42,6 +42,11 @@ if __name__ == "__main__":
                   f"{100.0 * buf[10 + k] / tot:5.1f}% of substep cycles", flush=True)
         print("    hull-hull split: " + "  ".join(f"{nm} {100.0 * buf[25 + i] / tot:5.1f}%" for i, nm in
               enumerate(["setup", "SAT A", "SAT B", "incident", "emit", "edge-edge", "clip"])), flush=True)
+        for k, name in enumerate(["obj-ground", "obj-static", "obj-obj", "link-obj", "link-static"]):
+            row = [buf[32 + 8 * k + i] for i in range(7)]
+            if sum(row):
+                print(f"      {name:11s}: " + "  ".join(f"{nm} {100.0 * v / tot:5.1f}%" for nm, v in
+                      zip(["setup", "SAT A", "SAT B", "incident", "emit", "edge-edge", "clip"], row)), flush=True)
 
     if any(f in sys.argv for f in ("--bench-scene", "--kuka", "--bin", "--allegro", "--c4")):
         # the bench workload: VecTask after its first (reset) steps, random actions
