@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 10
+#define HA_ABI_VERSION 11
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -448,6 +448,11 @@ int ha_task_reset(ha_handle h, uint32_t flags, void* stream);
 int ha_task_epilogue(ha_handle h, float* obs_out, float clip_obs, float* scalars, void* stream);
 /* v9: contacts per substep the handle's kernel family holds (over it, the shallowest give way) */
 int ha_contact_capacity(ha_handle h);
+/* v11: dispatch order of the full-shard launches (no gym counterpart: a scheduling hint; results do not depend on
+ * it). order: device array of the N env indices, a permutation, that workgroup i of every later full-shard launch
+ * simulates (kept by pointer: the caller keeps it alive), or NULL for the identity. Envs expected to take longest
+ * first shortens a multi-round launch's tail (longest-processing-time order; handarm_hip/sim.py rebalance). */
+int ha_set_env_order(ha_handle h, const int32_t* order, int32_t n);
 /* last kernel time in ms measured with HIP events around the most recent physics/step launch (-1 if none) */
 float ha_last_kernel_ms(ha_handle h);
 /* per-launch HIP-event timing of the env kernel (bench roofline): record up to max_launches launches

@@ -554,7 +554,7 @@ HD void factor_inverse(SimCtx& c) {
     for (int j = 0; j < ND; j++) {
         float t = a[j];
 #pragma unroll
-        for (int k = 0; k < j; k++) t -= a[k] * bcast(a[k], j);
+        for (int k = 0; k < j; k++) t = fmaf(-a[k], bcast(a[k], j), t);
         float ljj = sqrtf(fmaxf(bcast(t, j), 1e-30f));
         a[j] = lane == j ? ljj : (lane > j ? t / ljj : a[j]);
     }
@@ -568,7 +568,7 @@ HD void factor_inverse(SimCtx& c) {
 #pragma unroll
         for (int k = 0; k < i; k++) {
             float lik = bcast(a[k], i);
-            t = k >= lane ? t + lik * y[k] : t;
+            t = k >= lane ? fmaf(lik, y[k], t) : t;
         }
         y[i] = i == lane ? rl[i] : (i > lane ? -t * rl[i] : 0.0f);
     }
@@ -577,7 +577,7 @@ HD void factor_inverse(SimCtx& c) {
     for (int i = ND - 1; i >= 0; i--) {
         float t = y[i];
 #pragma unroll
-        for (int k = i + 1; k < ND; k++) t -= bcast(a[i], k) * x[k];
+        for (int k = i + 1; k < ND; k++) t = fmaf(-bcast(a[i], k), x[k], t);
         x[i] = t * rl[i];
     }
     if (lane < ND) {
@@ -1010,8 +1010,10 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         uint8_t* lb = reinterpret_cast<uint8_t*>(cs.cmax);
         const uint32_t* EA = m.edges + m.hull_edge_start[ha];
         const uint32_t* EB = m.edges + m.hull_edge_start[hb];
-        int nA = edge_cull(c, EA, nea, cs.wvA, cb, RB * RB, la);
+        // side B first (the static box, or the object of a link pair): its list is empty for most pairs (a table's
+        // edges are far from an object resting on its face), and then no pair exists and side A's cull is skipped
         int nB = edge_cull(c, EB, neb, cs.wvB, ca, RA * RA, lb);
+        int nA = nB > 0 ? edge_cull(c, EA, nea, cs.wvA, cb, RB * RB, la) : 0;
         wsync();
         float best = -3.0e38f;
         int bw = 1 << 30;
@@ -1526,7 +1528,7 @@ HD void substep(SimCtx& c, float hdt) {
     // free motion: velocity-product forces only (drives are constraint rows of the PGS below)
     if (lane < D) {
         float acc = 0.0f;
-        for (int j = 0; j < D; j++) acc += c.Minv[lane * D + j] * (-hdt * s.Cb[j]);
+        for (int j = 0; j < D; j++) acc = fmaf(c.Minv[lane * D + j], -hdt * s.Cb[j], acc);
         s.v[lane] = s.qd[lane] + acc;
     }
     if (lane < NO) {
@@ -1690,7 +1692,7 @@ HD void substep(SimCtx& c, float hdt) {
                 for (int i = 0; i < D; i++) {
                     float acc = 0.0f;
 #pragma unroll
-                    for (int j = 0; j < ND; j++) acc += c.Minv[i * D + j] * jr[j];
+                    for (int j = 0; j < ND; j++) acc = fmaf(c.Minv[i * D + j], jr[j], acc);
                     Yr[i] = acc;
                 }
             }
@@ -1710,8 +1712,8 @@ HD void substep(SimCtx& c, float hdt) {
             // same term order as the dense row: robot block, then the object blocks
             float a = 0.0f;
             if (Jr)
-                for (int t = 0; t < D; t++) a += Jr[t] * Yr[t];
-            for (int t = 0; t < RSN - D; t++) a += Jo[t] * Yo[t];
+                for (int t = 0; t < D; t++) a = fmaf(Jr[t], Yr[t], a);
+            for (int t = 0; t < RSN - D; t++) a = fmaf(Jo[t], Yo[t], a);
             winv_ = 1.0f / (a + 1e-9f);
         }
         if (NCH == 1) {
@@ -1732,9 +1734,9 @@ HD void substep(SimCtx& c, float hdt) {
             const float *Jo, *Y0o;
             float a = 0.0f, b = 0.0f;           // robot-block partial sums (J_rk . Y_r0, J_rk . Y_r1), t = 0 .. D-1
             auto rdot = [&](const float* Jr, const float* Y0r, const float* Y1r) {
-                for (int t = 0; t < D; t++) a += Jr[t] * Y0r[t];
+                for (int t = 0; t < D; t++) a = fmaf(Jr[t], Y0r[t], a);
                 if (k == 2)
-                    for (int t = 0; t < D; t++) b += Jr[t] * Y1r[t];
+                    for (int t = 0; t < D; t++) b = fmaf(Jr[t], Y1r[t], b);
             };
             if constexpr (PC::split) {
                 // LDS slot or global spill row on separate paths, so each keeps its own address space
@@ -1752,10 +1754,10 @@ HD void substep(SimCtx& c, float hdt) {
                 Y0o = Yb + r0 * RSN + D;
             }
             const float* Y1o = Y0o + (PC::split ? OW : RSN);
-            for (int t = 0; t < RSN - D; t++) a += Jo[t] * Y0o[t];
+            for (int t = 0; t < RSN - D; t++) a = fmaf(Jo[t], Y0o[t], a);
             ca0_ = a;
             if (k == 2) {
-                for (int t = 0; t < RSN - D; t++) b += Jo[t] * Y1o[t];
+                for (int t = 0; t < RSN - D; t++) b = fmaf(Jo[t], Y1o[t], b);
                 ca1_ = b;
             }
         }
@@ -1813,7 +1815,7 @@ HD void substep(SimCtx& c, float hdt) {
             float dl = bcast(nl - dlam, d);
             if (dl != 0.0f) {
                 if (lane == d) dlam = nl;
-                vreg += mrow * dl;
+                vreg = fmaf(mrow, dl, vreg);
             }
             if ((lo_mask >> d) & 1ull) {
                 float n0 = lam_lo - (vreg - vt_lo) * lwinv;
@@ -1821,7 +1823,7 @@ HD void substep(SimCtx& c, float hdt) {
                 float d0 = bcast(n0 - lam_lo, d);
                 if (d0 != 0.0f) {
                     if (lane == d) lam_lo = n0;
-                    vreg += mrow * d0;
+                    vreg = fmaf(mrow, d0, vreg);
                 }
             }
             if ((up_mask >> d) & 1ull) {
@@ -1830,7 +1832,7 @@ HD void substep(SimCtx& c, float hdt) {
                 float d1 = bcast(n1 - lam_up, d);
                 if (d1 != 0.0f) {
                     if (lane == d) lam_up = n1;
-                    vreg -= mrow * d1;
+                    vreg = fmaf(-mrow, d1, vreg);
                 }
             }
             if ((fr_mask >> d) & 1ull) {
@@ -1839,7 +1841,7 @@ HD void substep(SimCtx& c, float hdt) {
                 float df = bcast(nf - lam_fr, d);
                 if (df != 0.0f) {
                     if (lane == d) lam_fr = nf;
-                    vreg += mrow * df;
+                    vreg = fmaf(mrow, df, vreg);
                 }
             }
         }
@@ -1943,18 +1945,18 @@ HD void substep(SimCtx& c, float hdt) {
                 float d0 = bcast(n0 - lm, r0);
                 n0 = bcast(n0, r0);
                 float hi = kcmu * n0;
-                float n1 = lm - ((jv1 + kca0 * d0) - kvt) * kwinv;
+                float n1 = lm - (fmaf(kca0, d0, jv1) - kvt) * kwinv;
                 n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
                 float d1 = bcast(n1 - lm, r0 + 1);
-                float n2 = lm - (((jv2 + kca0 * d0) + kca1 * d1) - kvt) * kwinv;
+                float n2 = lm - (fmaf(kca1, d1, fmaf(kca0, d0, jv2)) - kvt) * kwinv;
                 n2 = n2 < -hi ? -hi : (n2 > hi ? hi : n2);
                 float d2 = bcast(n2 - lm, r0 + 2);
                 if (lane == r0) klam = n0;
                 if (lane == r0 + 1) klam = n1;
                 if (lane == r0 + 2) klam = n2;
-                if (d0 != 0.0f) { vreg += y0 * d0; if (VW == 2) vregh += g0 * d0; }
-                if (d1 != 0.0f) { vreg += y1 * d1; if (VW == 2) vregh += g1 * d1; }
-                if (d2 != 0.0f) { vreg += y2 * d2; if (VW == 2) vregh += g2 * d2; }
+                if (d0 != 0.0f) { vreg = fmaf(y0, d0, vreg); if (VW == 2) vregh = fmaf(g0, d0, vregh); }
+                if (d1 != 0.0f) { vreg = fmaf(y1, d1, vreg); if (VW == 2) vregh = fmaf(g1, d1, vregh); }
+                if (d2 != 0.0f) { vreg = fmaf(y2, d2, vreg); if (VW == 2) vregh = fmaf(g2, d2, vregh); }
             }
             if (NCH > 1 && lane < MAXR) rk(0, MAXR * ch + lane) = klam;     // swap the impulses out
         }

@@ -108,11 +108,26 @@ __host__ __device__ constexpr int task_col_planes() { return (FAM == HA_TASK_ALL
 #ifndef HA_AK_LINK_SLOTS
 #define HA_AK_LINK_SLOTS 4
 #endif
+// AllegroHand in the same compact layout (split rows, no gather buffer, S in the union): every AllegroHand contact
+// touches a finger link, so its rows are robot blocks in HA_AH_LINK_SLOTS LDS slots and the global spill rows
+#ifndef HA_AH_COMPACT
+#define HA_AH_COMPACT 0
+#endif
+#ifndef HA_AH_LINK_SLOTS
+#define HA_AH_LINK_SLOTS 5
+#endif
 template <int FAM>
-__host__ __device__ constexpr bool task_compact() { return FAM == HA_TASK_ALLEGRO_KUKA && HA_AK_COMPACT; }
+__host__ __device__ constexpr bool task_compact() {
+    return (FAM == HA_TASK_ALLEGRO_KUKA && HA_AK_COMPACT) || (FAM == HA_TASK_ALLEGRO_HAND && HA_AH_COMPACT);
+}
 template <int FAM>
-using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>(),
-                        FAM == FAM_UR5SIH_CLUTTER ? HB_LINK_SLOTS : (task_compact<FAM>() ? HA_AK_LINK_SLOTS : HA_LINK_SLOTS),
+__host__ __device__ constexpr int task_link_slots() {
+    return FAM == FAM_UR5SIH_CLUTTER ? HB_LINK_SLOTS
+                                     : (!task_compact<FAM>() ? HA_LINK_SLOTS
+                                                              : (FAM == HA_TASK_ALLEGRO_KUKA ? HA_AK_LINK_SLOTS : HA_AH_LINK_SLOTS));
+}
+template <int FAM>
+using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>(), task_link_slots<FAM>(),
                         FAM == FAM_UR5SIH_CLUTTER ? HB_LDS_CHUNKS : task_contact_chunks<FAM>(),
                         task_chunk_capacity<FAM>(), task_col_verts<FAM>(), task_col_planes<FAM>(),
                         task_compact<FAM>() ? 1 : -1, task_compact<FAM>() ? 0 : HA_MAX_GATHER, task_compact<FAM>()>;
@@ -489,12 +504,30 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     post_step(c, S, env, in, false);                           // configurable_vec_task.py:359-390
 }
 
+#if defined(HA_PROFILE) || defined(HA_ENVT)
+// diagnostic builds: each workgroup's start / end on the constant 100 MHz clock (s_memrealtime), by launch slot
+__device__ unsigned long long g_envt[2 * 65536];
+#define HA_ENV_T0() unsigned long long _e0 = __builtin_amdgcn_s_memrealtime();
+#define HA_ENV_T1()                                                                               \
+    do {                                                                                          \
+        __syncthreads();                                                                          \
+        if (threadIdx.x == 0 && blockIdx.x < 65536) {                                             \
+            g_envt[2 * blockIdx.x] = _e0;                                                         \
+            g_envt[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();                        \
+        }                                                                                         \
+    } while (0)
+#else
+#define HA_ENV_T0()
+#define HA_ENV_T1()
+#endif
 #define HA_KERNEL(name, FAM, MODE)                                                                              \
     extern "C" __global__ void __launch_bounds__(64)                                                          \
         __attribute__((amdgpu_waves_per_eu(task_waves_per_eu<FAM>())))                                        \
         name(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params, ha_state_t st,       \
              int num_envs, int n_calls, uint32_t flags, int stat_slot, float* spill, const int32_t* env_ids) {  \
+        HA_ENV_T0();                                                                                            \
         env_body<FAM, MODE>(model, params, st, num_envs, n_calls, flags, stat_slot, spill, env_ids);           \
+        HA_ENV_T1();                                                                                            \
     }
 HA_KERNEL(ha_step_kernel, HA_TASK_UR5SIH, MODE_STEP)
 HA_KERNEL(ha_simulate_kernel, HA_TASK_UR5SIH, MODE_SIMULATE)
@@ -619,6 +652,7 @@ struct ha_handle_s {
     int pc_count;
     hipEvent_t* pc_ev;    // 2 * t_max events (ha_pointclouds launches)
     float* d_spill;       // split-row families: robot-block rows beyond the LDS slots, N x spill_floats
+    const int32_t* order; // ha_set_env_order: env of workgroup i in full-shard launches (null: identity)
 };
 
 #define HIPCHK(x)                                                                     \
@@ -745,7 +779,8 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
         }
     }
     // a family without a gather buffer (ColLayout NG = 0) takes single-hull pool objects only
-    bool one_hull = fam == HA_TASK_ALLEGRO_KUKA && FamPhys<HA_TASK_ALLEGRO_KUKA>::colg == 0;
+    bool one_hull = (fam == HA_TASK_ALLEGRO_KUKA && FamPhys<HA_TASK_ALLEGRO_KUKA>::colg == 0) ||
+                    (fam == HA_TASK_ALLEGRO_HAND && FamPhys<HA_TASK_ALLEGRO_HAND>::colg == 0);
     for (int i = 0; i < model->n_pool; i++)
         if (model->pool_nhull[i] < 1 || model->pool_hull[i] < 0 ||
             model->pool_hull[i] + model->pool_nhull[i] > model->n_hulls || (one_hull && model->pool_nhull[i] != 1))
@@ -805,6 +840,10 @@ static int launch(ha_handle h, int mode, int n_calls, uint32_t flags, int slot, 
     hipStream_t s = (hipStream_t)stream;
     bool rec = h->t_ev && h->t_count < h->t_max;
     (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count] : h->ev0, s);
+    if (!env_ids && h->order) {            // full shard in the caller's dispatch order (ha_set_env_order)
+        env_ids = h->order;
+        n_ids = h->N;
+    }
     hipLaunchKernelGGL(kernel_for(h->fam, mode), dim3(env_ids ? n_ids : h->N), dim3(64), lds_bytes(h->fam), s, h->d_model,
                        h->d_params, h->st, h->N, n_calls, flags, slot, h->d_spill, env_ids);
     HIPCHK(hipGetLastError());
@@ -821,6 +860,12 @@ int ha_simulate(ha_handle h, int32_t n_calls, uint32_t flags, void* stream) {
     if (n_calls < 0) return HA_E_ARG;
     if (n_calls == 0 || (flags & HA_FLAG_NO_PHYSICS)) return HA_OK;
     return launch(h, MODE_SIMULATE, n_calls, flags, 0, stream);
+}
+
+int ha_set_env_order(ha_handle h, const int32_t* order, int32_t n) {
+    if (!h || (order && n != h->N)) return HA_E_ARG;
+    h->order = order;
+    return HA_OK;
 }
 
 int ha_simulate_envs(ha_handle h, int32_t n_calls, uint32_t flags, const int32_t* env_ids, int32_t n_envs, void* stream) {
@@ -1172,6 +1217,14 @@ extern "C" int ha_profile_read(unsigned long long* out32, int reset) {
         unsigned long long z[96] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return HA_E_HIP;
     }
+    return HA_OK;
+}
+#endif
+#if defined(HA_PROFILE) || defined(HA_ENVT)
+// per-workgroup (start, end) stamps of the last launch of a kernel family (n workgroups)
+extern "C" int ha_profile_env_times(unsigned long long* out, int n) {
+    if (n < 0 || n > 65536) return HA_E_ARG;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_envt), sizeof(unsigned long long) * 2 * n) != hipSuccess) return HA_E_HIP;
     return HA_OK;
 }
 #endif

@@ -14,6 +14,7 @@ Difference to Isaac Gym worth knowing: because the acquired tensors are the simu
 writes into them take effect even without a set_*_indexed call (the reference always calls it).
 """
 import ctypes as C
+import os
 
 import torch
 
@@ -26,7 +27,7 @@ TORCH_DTYPE = {"float32": torch.float32, "int64": torch.int64, "uint8": torch.ui
 
 class HandArmSim:
     def __init__(self, num_envs, device="cuda:0", task_cfg=None, scene=None, pool_names=None, stats_ring=64,
-                 task=None):
+                 task=None, rebalance_every=8):
         if not str(device).startswith("cuda"):
             raise _lib.HandArmError("libhandarm_hip runs on a HIP device only (device must be 'cuda:N')")
         self.lib = _lib.load()
@@ -76,6 +77,24 @@ class HandArmSim:
             setattr(self.state, k, None if k in null else self.t[k].data_ptr())
         _lib.check(self.lib.ha_bind_state(self.h, C.byref(self.state)), "ha_bind_state")
         _lib.check(self.lib.ha_set_stats_ring(self.h, stats_ring), "ha_set_stats_ring")
+        # longest-first dispatch order of the fused step (ha_set_env_order), refreshed every `rebalance_every` steps
+        self.rebalance_every = int(os.environ.get("HA_REBALANCE", rebalance_every))
+        self._rb_count = 0
+        if self.rebalance_every > 0:
+            self._env_order = torch.arange(num_envs, dtype=torch.int32, device=self.device)
+            self._cost_prev = torch.zeros(num_envs, dtype=torch.int32, device=self.device)
+            _lib.check(self.lib.ha_set_env_order(self.h, C.c_void_p(self._env_order.data_ptr()), num_envs),
+                       "ha_set_env_order")
+
+    def rebalance(self):
+        """Dispatch the envs that offered the most contacts since the last call first (device argsort, stable, no
+        host sync). In a launch with more envs than resident workgroup slots, the slots that free up take the
+        cheaper envs last, so the launch's tail shrinks (longest-processing-time order); a one-round launch spreads
+        its heavy envs over the CUs. Results do not depend on the order (one workgroup per env)."""
+        cs = self.t["contact_stats"][:, 3]
+        cost = cs - self._cost_prev
+        self._cost_prev.copy_(cs)
+        self._env_order.copy_(torch.argsort(cost, descending=True, stable=True))
 
     def _init_kuka(self):
         """AllegroKuka buffers at env creation: per-env object dims and keypoint offsets, goal_states
@@ -178,6 +197,11 @@ class HandArmSim:
 
     # -------------------------------------------------------------- fused task entry points
     def task_step(self, flags=0):
+        if self.rebalance_every > 0:
+            self._rb_count += 1
+            if self._rb_count >= self.rebalance_every:
+                self._rb_count = 0
+                self.rebalance()
         _lib.check(self.lib.ha_task_step(self.h, flags, self._stream()), "ha_task_step")
 
     def task_observe(self, flags=0):

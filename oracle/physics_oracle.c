@@ -268,11 +268,11 @@ static void dynamics(const hao_handle h, env_t* e, float* M, float* C) {
 static void cholesky(float* A, int n) {
     for (int j = 0; j < n; j++) {
         float s = A[j * n + j];
-        for (int k = 0; k < j; k++) s -= A[j * n + k] * A[j * n + k];
+        for (int k = 0; k < j; k++) s = fmaf(-A[j * n + k], A[j * n + k], s);
         A[j * n + j] = sqrtf(fmaxf(s, 1e-30f));
         for (int i = j + 1; i < n; i++) {
             float t = A[i * n + j];
-            for (int k = 0; k < j; k++) t -= A[i * n + k] * A[j * n + k];
+            for (int k = 0; k < j; k++) t = fmaf(-A[i * n + k], A[j * n + k], t);
             A[i * n + j] = t / A[j * n + j];
         }
     }
@@ -288,7 +288,7 @@ static void inverse_from_cholesky(const float* Lm, int n, float* Li, float* S) {
         Li[j * n + j] = rl[j];
         for (int i = j + 1; i < n; i++) {
             float t = 0.0f;
-            for (int k = j; k < i; k++) t += Lm[i * n + k] * Li[k * n + j];
+            for (int k = j; k < i; k++) t = fmaf(Lm[i * n + k], Li[k * n + j], t);
             Li[i * n + j] = -t * rl[i];
         }
     }
@@ -296,7 +296,7 @@ static void inverse_from_cholesky(const float* Lm, int n, float* Li, float* S) {
         float x[HA_MAX_DOFS];
         for (int i = n - 1; i >= 0; i--) {
             float t = Li[i * n + j];
-            for (int k = i + 1; k < n; k++) t -= Lm[k * n + i] * x[k];
+            for (int k = i + 1; k < n; k++) t = fmaf(-Lm[k * n + i], x[k], t);
             x[i] = t * rl[i];
         }
         for (int i = 0; i < n; i++) S[j * n + i] = x[i];
@@ -773,7 +773,7 @@ static void apply_minv(const hao_handle h, const env_t* e, const float* Minv, co
     int D = dofn(h);
     for (int i = 0; i < D; i++) {
         float acc = 0.0f;
-        for (int j = 0; j < D; j++) acc += Minv[i * D + j] * J[j];
+        for (int j = 0; j < D; j++) acc = fmaf(Minv[i * D + j], J[j], acc);
         Y[i] = acc;
     }
     for (int o = 0; o < h->NO; o++) {
@@ -816,7 +816,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
     float v[MAXV];
     for (int i = 0; i < D; i++) {
         float acc = 0.0f;
-        for (int j = 0; j < D; j++) acc += Minv[i * D + j] * (-hdt * C[j]);
+        for (int j = 0; j < D; j++) acc = fmaf(Minv[i * D + j], -hdt * C[j], acc);
         v[i] = e->qd[i] + acc;
     }
     for (int o = 0; o < NO; o++) {
@@ -877,7 +877,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
         }
         apply_minv(h, e, Minv, R.J[r], R.Y[r]);
         float a = 0.0f;
-        for (int t = 0; t < NV; t++) a += R.J[r][t] * R.Y[r][t];
+        for (int t = 0; t < NV; t++) a = fmaf(R.J[r][t], R.Y[r][t], a);
         winv[r] = 1.0f / (a + 1e-9f);
         lam[r] = 0.0f;
     }
@@ -886,9 +886,9 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
     for (int c = 0; c < nc; c++) {
         const float *J1 = R.J[3 * c + 1], *J2 = R.J[3 * c + 2], *Y0 = R.Y[3 * c], *Y1 = R.Y[3 * c + 1];
         float x = 0.0f, y = 0.0f, z = 0.0f;
-        for (int t = 0; t < NV; t++) x += J1[t] * Y0[t];
-        for (int t = 0; t < NV; t++) y += J2[t] * Y0[t];
-        for (int t = 0; t < NV; t++) z += J2[t] * Y1[t];
+        for (int t = 0; t < NV; t++) x = fmaf(J1[t], Y0[t], x);
+        for (int t = 0; t < NV; t++) y = fmaf(J2[t], Y0[t], y);
+        for (int t = 0; t < NV; t++) z = fmaf(J2[t], Y1[t], z);
         a10[c] = x; a20[c] = y; a21[c] = z;
     }
     /* joint rows of dof d: PD drive as a soft, impulse-bounded constraint (PhysX articulation drive
@@ -927,7 +927,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
             float dl = nl - dlam[d];
             if (dl != 0.0f) {
                 dlam[d] = nl;
-                for (int k = 0; k < D; k++) v[k] += mrow[k] * dl;
+                for (int k = 0; k < D; k++) v[k] = fmaf(mrow[k], dl, v[k]);
             }
             if (act_lo[d]) {
                 float n0 = lam_lo[d] - (v[d] - vt_lo[d]) * lwinv[d];
@@ -935,7 +935,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
                 float d0 = n0 - lam_lo[d];
                 if (d0 != 0.0f) {
                     lam_lo[d] = n0;
-                    for (int k = 0; k < D; k++) v[k] += mrow[k] * d0;
+                    for (int k = 0; k < D; k++) v[k] = fmaf(mrow[k], d0, v[k]);
                 }
             }
             if (act_up[d]) {
@@ -944,7 +944,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
                 float d1 = n1 - lam_up[d];
                 if (d1 != 0.0f) {
                     lam_up[d] = n1;
-                    for (int k = 0; k < D; k++) v[k] -= mrow[k] * d1;
+                    for (int k = 0; k < D; k++) v[k] = fmaf(-mrow[k], d1, v[k]);
                 }
             }
             if (flim[d] > 0.0f) {
@@ -953,7 +953,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
                 float df = nf - lam_fr[d];
                 if (df != 0.0f) {
                     lam_fr[d] = nf;
-                    for (int k = 0; k < D; k++) v[k] += mrow[k] * df;
+                    for (int k = 0; k < D; k++) v[k] = fmaf(mrow[k], df, v[k]);
                 }
             }
         }
@@ -967,18 +967,18 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
             n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
             float d0 = n0 - l0;
             float hi = (0.5f * (body_friction(h, e, cs[c].a) + body_friction(h, e, cs[c].b))) * n0;
-            jv1 = jv1 + a10[c] * d0;
+            jv1 = fmaf(a10[c], d0, jv1);
             float n1 = l1 - (jv1 - R.vt[r0 + 1]) * winv[r0 + 1];
             n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
             float d1 = n1 - l1;
-            jv2 = (jv2 + a20[c] * d0) + a21[c] * d1;
+            jv2 = fmaf(a21[c], d1, fmaf(a20[c], d0, jv2));
             float n2 = l2 - (jv2 - R.vt[r0 + 2]) * winv[r0 + 2];
             n2 = n2 < -hi ? -hi : (n2 > hi ? hi : n2);
             float d2 = n2 - l2;
             lam[r0] = n0; lam[r0 + 1] = n1; lam[r0 + 2] = n2;
-            if (d0 != 0.0f) for (int k = 0; k < NV; k++) v[k] += R.Y[r0][k] * d0;
-            if (d1 != 0.0f) for (int k = 0; k < NV; k++) v[k] += R.Y[r0 + 1][k] * d1;
-            if (d2 != 0.0f) for (int k = 0; k < NV; k++) v[k] += R.Y[r0 + 2][k] * d2;
+            if (d0 != 0.0f) for (int k = 0; k < NV; k++) v[k] = fmaf(R.Y[r0][k], d0, v[k]);
+            if (d1 != 0.0f) for (int k = 0; k < NV; k++) v[k] = fmaf(R.Y[r0 + 1][k], d1, v[k]);
+            if (d2 != 0.0f) for (int k = 0; k < NV; k++) v[k] = fmaf(R.Y[r0 + 2][k], d2, v[k]);
         }
     }
     for (int d = 0; d < D; d++) e->dforce[d] = (((dlam[d] + lam_lo[d]) - lam_up[d]) + lam_fr[d]) / hdt;

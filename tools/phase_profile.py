@@ -12,6 +12,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "isaacgym-hand-arm_amd")]
 from handarm_hip import _lib, build  # noqa: E402
 
 PROF_LIB = os.path.join(build.PKG, "libhandarm_hip_prof.so")
+ENVT_LIB = os.path.join(build.PKG, "libhandarm_hip_envt.so")     # -DHA_ENVT: workgroup spans only (no phase atomics)
 PHASES = ["fk", "dynamics(CRBA+RNEA)", "chol+Minv+free+objects", "detect", "contact rows J,Y", "joint rows", "PGS",
           "forces+integrate"]
 
@@ -20,12 +21,15 @@ if __name__ == "__main__":
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", *build.FLAGS, "-DHA_PROFILE", "-I", build.INCLUDE,
                "-o", PROF_LIB, os.path.join(build.CSRC, "handarm_hip.hip")]
         subprocess.check_call(cmd)
+        subprocess.check_call([x if x != "-DHA_PROFILE" else "-DHA_ENVT" for x in cmd[:-3]] + ["-o", ENVT_LIB, cmd[-1]])
         sys.exit(0)
-    _lib.LIB_PATH = PROF_LIB
+    envt_only = "--envt-only" in sys.argv
+    _lib.LIB_PATH = ENVT_LIB if envt_only else PROF_LIB
     import torch
     from tools.perf_probe import run
     lib = _lib.load()
-    lib.ha_profile_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    if not envt_only:
+        lib.ha_profile_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     buf = (C.c_ulonglong * 96)()
     args = [x for x in sys.argv[1:] if not x.startswith("--")]
     n = int(args[0]) if args else 8192
@@ -78,15 +82,49 @@ if __name__ == "__main__":
         for _ in range(20):
             env.step(torch.rand((n, na), device="cuda:0", generator=g) * 2 - 1)
         torch.cuda.synchronize()
-        lib.ha_profile_read(buf, 1)
+        if not envt_only:
+            lib.ha_profile_read(buf, 1)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(10):
             env.step(torch.rand((n, na), device="cuda:0", generator=g) * 2 - 1)
         e1.record()
         torch.cuda.synchronize()
-        print(f"bench scene n={n}: {e0.elapsed_time(e1) / 10:.3f} ms/step (profiled build)", flush=True)
-        report("bench scene")
+        print(f"bench scene n={n}: {e0.elapsed_time(e1) / 10:.3f} ms/step "
+              f"({'workgroup-span build' if envt_only else 'profiled build'})", flush=True)
+        if not envt_only:
+            report("bench scene")
+        if "--envt" in sys.argv or envt_only:
+            # per-workgroup spans of one more step (s_memrealtime, 100 MHz): the spread of env durations, and what
+            # the slow envs have in common (contacts offered, resets)
+            import numpy as np
+            sim = env.sim
+            rb = sim.t["reset_buf"].cpu().numpy().astype(bool)
+            cs0 = sim.t["contact_stats"].cpu().numpy().astype(np.int64).copy()
+            env.step(torch.rand((n, na), device="cuda:0", generator=g) * 2 - 1)
+            torch.cuda.synchronize()
+            cs = sim.t["contact_stats"].cpu().numpy().astype(np.int64) - cs0
+            lib.ha_profile_env_times.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+            tb = (C.c_ulonglong * (2 * n))()
+            lib.ha_profile_env_times(tb, n)
+            t = np.frombuffer(tb, dtype=np.uint64).reshape(n, 2).astype(np.int64)
+            t0 = t[:, 0].min()
+            dur = (t[:, 1] - t[:, 0]) * 0.01          # us
+            st = (t[:, 0] - t0) * 0.01
+            end = (t[:, 1] - t0) * 0.01
+            print(f"env spans (us): kernel {end.max():.1f}; start p50 {np.percentile(st, 50):.1f} p99 {np.percentile(st, 99):.1f} "
+                  f"max {st.max():.1f}; duration min {dur.min():.1f} p10 {np.percentile(dur, 10):.1f} "
+                  f"p50 {np.percentile(dur, 50):.1f} p90 {np.percentile(dur, 90):.1f} p99 {np.percentile(dur, 99):.1f} "
+                  f"max {dur.max():.1f}; mean/max {dur.mean() / dur.max():.2f}", flush=True)
+            off = cs[:, 3] / np.maximum(cs[:, 0], 1)
+            for lo, hi in ((0, 50), (50, 90), (90, 99), (99, 100)):
+                a, b = np.percentile(dur, lo), np.percentile(dur, hi)
+                sel = (dur >= a) & (dur <= b)
+                print(f"  duration p{lo}-p{hi} ({a:.0f}-{b:.0f} us): {sel.sum()} envs, resets {rb[sel].mean():.3f}, "
+                      f"contacts offered/substep {off[sel].mean():.2f}, max offered {cs[sel, 2].mean():.1f}, "
+                      f"over capacity {cs[sel, 1].sum() / max(cs[sel, 0].sum(), 1):.4f}", flush=True)
+            hist, edges = np.histogram(dur, bins=12)
+            print("  histogram: " + "  ".join(f"{edges[i]:.0f}:{hist[i]}" for i in range(12)), flush=True)
         sys.exit(0)
     for objects in (False, True):
         lib.ha_profile_read(buf, 1)
