@@ -342,7 +342,8 @@ def compute_roofline(kernel, envs, kavg_ms):
     return {"bound": "valu", "achieved": rate, "peak": VALU_PEAK_WAVE_INSTS, "unit": "wave-instructions/s",
             "frac": rate / VALU_PEAK_WAVE_INSTS, "valu_insts_per_launch": sq["valu_insts_per_launch"],
             "waves_per_simd": 4 * sq["wave_cycles_per_launch"] / (t * NOMINAL_CLOCK_HZ) / 1024,
-            "valu_active_frac": sq.get("valu_active_frac"), "source": f"profiles/sq_{kernel}.json"}
+            "valu_active_frac": sq.get("valu_active_frac"),
+            "valu_lane_utilization": sq.get("valu_lane_utilization"), "source": f"profiles/sq_{kernel}.json"}
 
 
 def run_config(task, envs, args, world, rank, device, log_interval_fn):

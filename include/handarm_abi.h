@@ -103,6 +103,7 @@ extern "C" {
 /* ha_params_t.narrow_phase_flags */
 #define HA_NP_NO_EDGE_AXES 1
 #define HA_NP_NO_CLIP 2
+#define HA_NP_NO_SPHERE_CULL 4
 
 /* flags for ha_task_step / ha_simulate */
 #define HA_FLAG_NO_PHYSICS 1u      /* skip physics substeps (task-math parity tests) */

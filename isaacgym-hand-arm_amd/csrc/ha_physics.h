@@ -949,10 +949,9 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
 #endif
     // world vertices and planes of both hulls, unless this side's (hull, body) is already in ColScratch
     bool needA = ha != c.colA_h || keyA != c.colA_b, needB = hb != c.colB_h || keyB != c.colB_b;
-    if (needA) {
-        if (lane < nva) st3(cs.wvA[lane], PA.p + qrot(PA.q, scale3(c, a, ld3(m.verts[m.hull_vert_start[ha] + lane]))));
-        c.colA_h = ha; c.colA_b = keyA; c.colA_p = false;
-    }
+    // side A's body-frame vertex of this lane, loaded before B's setup so that its latency overlaps it
+    f3 vA = mk3(0, 0, 0);
+    if (needA && lane < nva) vA = ld3(m.verts[m.hull_vert_start[ha] + lane]);
     if (needB) {
         if (lane < nvb) st3(cs.wvB[lane], PB.p + qrot(PB.q, scale3(c, b, ld3(m.verts[m.hull_vert_start[hb] + lane]))));
         bool scB = body_scaled(c, b);
@@ -967,8 +966,23 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
             cs.wpB[k][3] = d;
         }
         c.colB_h = hb; c.colB_b = keyB;
+        wsync();
     }
-    if (needA || needB) wsync();
+    // side A's bounding sphere against B's face planes before A's setup: a plane the sphere clears by more than
+    // the margin (with a 1 mm allowance for rounding) clears every vertex of A too, so SAT over B's planes would
+    // separate the pair; such a pair (most link hulls near an object) skips A's setup and the SAT. No result
+    // changes: the oracle runs the full test and finds the same separation
+    if (c.p->narrow_phase_flags & HA_NP_NO_SPHERE_CULL) {
+    } else {
+        float sc = -3.0e38f;
+        for (int k = lane; k < npb; k += 64) sc = fmaxf(sc, dot3(ld3(cs.wpB[k]), ca) + cs.wpB[k][3]);
+        if (wave_max(sc) - scale_radius(c, a, m.hull_radius[ha]) > mg + 1e-3f) return;
+    }
+    if (needA) {
+        if (lane < nva) st3(cs.wvA[lane], PA.p + qrot(PA.q, scale3(c, a, vA)));
+        c.colA_h = ha; c.colA_b = keyA; c.colA_p = false;
+        wsync();
+    }
     HPROF(25);
     // B's face planes against A's vertices first: side A's planes (a link hull's up to 60) are only built when
     // that test does not separate the pair. Either test alone separating means no contact, so the order changes
@@ -1424,9 +1438,11 @@ HD void detect(SimCtx& c) {
             int q = base + bit;
             pair_desc(c, q, kind, A, B);
             // the pair is wave-uniform: say so, so that the narrow phase branches on scalars (no exec-masked regions)
+#ifndef HA_X_DIVERGENT_PAIR   /* diagnostic: the pair indices left as the compiler sees them */
             kind = __builtin_amdgcn_readfirstlane(kind);
             A = __builtin_amdgcn_readfirstlane(A);
             B = __builtin_amdgcn_readfirstlane(B);
+#endif
 #ifdef HA_PROFILE
             c.pk = kind;
 #endif
@@ -1808,41 +1824,53 @@ HD void substep(SimCtx& c, float hdt) {
         // Each joint row's update is computed by the lane that owns the joint (its own v[d], lambda and row
         // constants: the same operands the oracle uses), and only the impulse change crosses lanes (one
         // v_readlane); the joint-limit rows run only for the joints whose limit is active (ballot masks).
+        // Lane d runs its DOF's rows (drive, active limits, friction) in order on its own copy of v[d], applying
+        // each impulse change with the same fmaf(M^-1[d][d], delta, v) the all-lane update gives lane d; then the
+        // changes cross lanes together (independent v_readlanes) and every lane applies them in the row order.
+        // Same values and order as one row at a time (the oracle), one lane exchange per DOF instead of per row.
         for (int d = 0; d < D; d++) {
             float mrow = lane < D ? c.Minv[d * D + lane] : 0.0f;
-            float nl = dlam - (vreg + dbias + dgam * dlam) * dwinv;
+            const bool lo = (lo_mask >> d) & 1ull, up = (up_mask >> d) & 1ull, fr = (fr_mask >> d) & 1ull;
+            float vd = vreg;
+            float nl = dlam - (vd + dbias + dgam * dlam) * dwinv;
             nl = nl < -dlim ? -dlim : (nl > dlim ? dlim : nl);
-            float dl = bcast(nl - dlam, d);
+            float el = nl - dlam;
+            if (el != 0.0f) vd = fmaf(mrow, el, vd);
+            float n0 = 0.f, n1 = 0.f, nf = 0.f, e0 = 0.f, e1 = 0.f, ef = 0.f;
+            if (lo) {
+                n0 = lam_lo - (vd - vt_lo) * lwinv;
+                n0 = n0 < 0.0f ? 0.0f : n0;
+                e0 = n0 - lam_lo;
+                if (e0 != 0.0f) vd = fmaf(mrow, e0, vd);
+            }
+            if (up) {
+                n1 = lam_up - (-vd - vt_up) * lwinv;
+                n1 = n1 < 0.0f ? 0.0f : n1;
+                e1 = n1 - lam_up;
+                if (e1 != 0.0f) vd = fmaf(-mrow, e1, vd);
+            }
+            if (fr) {
+                nf = lam_fr - vd * lwinv;
+                nf = nf < -flim ? -flim : (nf > flim ? flim : nf);
+                ef = nf - lam_fr;
+            }
+            float dl = bcast(el, d);
+            float d0 = lo ? bcast(e0, d) : 0.0f, d1 = up ? bcast(e1, d) : 0.0f, df = fr ? bcast(ef, d) : 0.0f;
             if (dl != 0.0f) {
                 if (lane == d) dlam = nl;
                 vreg = fmaf(mrow, dl, vreg);
             }
-            if ((lo_mask >> d) & 1ull) {
-                float n0 = lam_lo - (vreg - vt_lo) * lwinv;
-                n0 = n0 < 0.0f ? 0.0f : n0;
-                float d0 = bcast(n0 - lam_lo, d);
-                if (d0 != 0.0f) {
-                    if (lane == d) lam_lo = n0;
-                    vreg = fmaf(mrow, d0, vreg);
-                }
+            if (d0 != 0.0f) {
+                if (lane == d) lam_lo = n0;
+                vreg = fmaf(mrow, d0, vreg);
             }
-            if ((up_mask >> d) & 1ull) {
-                float n1 = lam_up - (-vreg - vt_up) * lwinv;
-                n1 = n1 < 0.0f ? 0.0f : n1;
-                float d1 = bcast(n1 - lam_up, d);
-                if (d1 != 0.0f) {
-                    if (lane == d) lam_up = n1;
-                    vreg = fmaf(-mrow, d1, vreg);
-                }
+            if (d1 != 0.0f) {
+                if (lane == d) lam_up = n1;
+                vreg = fmaf(-mrow, d1, vreg);
             }
-            if ((fr_mask >> d) & 1ull) {
-                float nf = lam_fr - vreg * lwinv;
-                nf = nf < -flim ? -flim : (nf > flim ? flim : nf);
-                float df = bcast(nf - lam_fr, d);
-                if (df != 0.0f) {
-                    if (lane == d) lam_fr = nf;
-                    vreg = fmaf(mrow, df, vreg);
-                }
+            if (df != 0.0f) {
+                if (lane == d) lam_fr = nf;
+                vreg = fmaf(mrow, df, vreg);
             }
         }
         // contact blocks: the three J.v reductions of a contact run together; the friction rows see the

@@ -24,4 +24,6 @@ bash "$R/tools/gpu_round.sh" \
   "sq1x|60|python $R/tools/pmc_extract.py $O/sq1 --kernel $K --out $O/${TAG}_sq1${SFX}.csv --delete > $O/${TAG}_sq1${SFX}_summary.txt" \
   "sq2|400|$P --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA --output-format csv -d $O/sq2 -- $B" \
   "sq2x|60|python $R/tools/pmc_extract.py $O/sq2 --kernel $K --out $O/${TAG}_sq2${SFX}.csv --delete > $O/${TAG}_sq2${SFX}_summary.txt" \
-  "sqsum|60|python $R/tools/sq_summary.py $O/${TAG}_sq1${SFX}.csv $O/${TAG}_sq2${SFX}.csv --kernel $K --envs $ENVS --out $O/sq_$K.json"
+  "sq3|400|$P --pmc SQ_THREAD_CYCLES_VALU --output-format csv -d $O/sq3 -- $B" \
+  "sq3x|60|python $R/tools/pmc_extract.py $O/sq3 --kernel $K --out $O/${TAG}_sq3${SFX}.csv --delete > $O/${TAG}_sq3${SFX}_summary.txt" \
+  "sqsum|60|python $R/tools/sq_summary.py $O/${TAG}_sq1${SFX}.csv $O/${TAG}_sq2${SFX}.csv $O/${TAG}_sq3${SFX}.csv --kernel $K --envs $ENVS --out $O/sq_$K.json"

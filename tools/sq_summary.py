@@ -40,6 +40,10 @@ def main():
            else None,
            "lds_bank_conflict_per_lds_inst": (m["SQ_LDS_BANK_CONFLICT"] / m["SQ_INSTS_LDS"])
            if m.get("SQ_INSTS_LDS") and "SQ_LDS_BANK_CONFLICT" in m else None,
+           # rocprofiler-sdk counter_defs.yaml VALUUtilization: active lanes per VALU instruction-cycle / 64 (the
+           # third SQ pass holds SQ_THREAD_CYCLES_VALU alone: a counter in two passes would add up per dispatch id here)
+           "valu_lane_utilization": (m["SQ_THREAD_CYCLES_VALU"] / (m["SQ_ACTIVE_INST_VALU"] * 64.0))
+           if m.get("SQ_THREAD_CYCLES_VALU") and m.get("SQ_ACTIVE_INST_VALU") else None,
            "source": a.csv}
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
