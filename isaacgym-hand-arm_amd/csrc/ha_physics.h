@@ -949,9 +949,6 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
 #endif
     // world vertices and planes of both hulls, unless this side's (hull, body) is already in ColScratch
     bool needA = ha != c.colA_h || keyA != c.colA_b, needB = hb != c.colB_h || keyB != c.colB_b;
-    // side A's body-frame vertex of this lane, loaded before B's setup so that its latency overlaps it
-    f3 vA = mk3(0, 0, 0);
-    if (needA && lane < nva) vA = ld3(m.verts[m.hull_vert_start[ha] + lane]);
     if (needB) {
         if (lane < nvb) st3(cs.wvB[lane], PB.p + qrot(PB.q, scale3(c, b, ld3(m.verts[m.hull_vert_start[hb] + lane]))));
         bool scB = body_scaled(c, b);
@@ -979,7 +976,7 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         if (wave_max(sc) - scale_radius(c, a, m.hull_radius[ha]) > mg + 1e-3f) return;
     }
     if (needA) {
-        if (lane < nva) st3(cs.wvA[lane], PA.p + qrot(PA.q, scale3(c, a, vA)));
+        if (lane < nva) st3(cs.wvA[lane], PA.p + qrot(PA.q, scale3(c, a, ld3(m.verts[m.hull_vert_start[ha] + lane]))));
         c.colA_h = ha; c.colA_b = keyA; c.colA_p = false;
         wsync();
     }

@@ -66,8 +66,11 @@ __host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5S
 // 168 VGPRs (84 / 72 B/lane scratch), so 12 workgroups run per CU instead of 8 (LDS 20.1 / 16.6 KB, 193
 // VGPRs): C2 0.705 -> 0.652 ms, C3 3.23 -> 2.70 ms (tools/ab_variants.sh). The list is then over capacity in
 // 1.3% (C2) / 2.0% (C3) of substeps, where the shallowest contacts give way (bench contact_stats).
+// AllegroKuka holds a full chunk (21) since round 3: with 2 LDS link slots its rows still fit in front of S in the
+// phase union (9.3 KB env block, 16 workgroups per CU); C2 over capacity 1.3% -> 0.09% of substeps for +2.7%
+// step time. AllegroHand stays at 12: 21 in the compact layout cost +9% (0.12%), the dense rows do not fit.
 #ifndef HA_AK_CONTACTS
-#define HA_AK_CONTACTS 12
+#define HA_AK_CONTACTS 21
 #endif
 #ifndef HA_AH_CONTACTS
 #define HA_AH_CONTACTS 12
@@ -106,7 +109,7 @@ __host__ __device__ constexpr int task_col_planes() { return (FAM == HA_TASK_ALL
 #define HA_AK_COMPACT 1
 #endif
 #ifndef HA_AK_LINK_SLOTS
-#define HA_AK_LINK_SLOTS 4
+#define HA_AK_LINK_SLOTS 2
 #endif
 // AllegroHand in the same compact layout (split rows, no gather buffer, S in the union): every AllegroHand contact
 // touches a finger link, so its rows are robot blocks in HA_AH_LINK_SLOTS LDS slots and the global spill rows

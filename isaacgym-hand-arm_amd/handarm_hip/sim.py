@@ -69,7 +69,7 @@ class HandArmSim:
         h = C.c_void_p()
         _lib.check(self.lib.ha_create(C.byref(self.model), C.byref(self.params), num_envs, C.byref(h)), "ha_create")
         self.h = h
-        # contacts per substep the kernel family holds (clutter 84, Ur5Sih 21, AllegroKuka / AllegroHand 12)
+        # contacts per substep the kernel family holds (clutter 84, Ur5Sih 21, AllegroKuka 21, AllegroHand 12)
         self.contact_capacity = int(self.lib.ha_contact_capacity(self.h))
         self.state = HM.HaState()
         null = HM.null_fields(task)

@@ -1104,8 +1104,9 @@ hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int nu
     h->D = model->n_dofs;
     h->B = model->n_bodies;
     /* the device family's capacity (ha_contact_capacity): clutter 4 chunks of 21 (handarm_hip.hip HB_CHUNKS),
-       Ur5Sih 21, AllegroKuka / AllegroHand 12 (HA_AK_CONTACTS / HA_AH_CONTACTS) */
-    h->maxc = params->task == HA_TASK_UR5SIH ? (params->n_objects > 3 ? 4 * 21 : 21) : 12;
+       Ur5Sih 21, AllegroKuka 21, AllegroHand 12 (HA_AK_CONTACTS / HA_AH_CONTACTS) */
+    h->maxc = params->task == HA_TASK_UR5SIH ? (params->n_objects > 3 ? 4 * 21 : 21)
+                                             : (params->task == HA_TASK_ALLEGRO_KUKA ? 21 : 12);
     return h;
 }
 void hao_destroy(hao_handle h) { free(h); }
