@@ -75,8 +75,20 @@ HD void inv3(const float A[9], float out[9]) {
 
 // ---------------------------------------------------------------- wavefront primitives (wave64)
 HD int lane_id() { return threadIdx.x & 63; }
-// Block == one wavefront: s_barrier is a no-op wait for lockstep lanes but orders the LDS traffic.
+// Block == one wavefront (every env kernel is __launch_bounds__(64)): lanes exchange data through LDS (and the
+// env's global rows) inside one wave, whose memory operations the hardware performs in program order. A
+// wavefront-scope release / acquire pair is then all the ordering needed: it stops the compiler from moving
+// memory operations across the point, and unlike __syncthreads() (workgroup scope: s_waitcnt lgkmcnt(0) at every
+// call even with the s_barrier elided for one wave) it does not stall on in-flight LDS and scalar loads.
+#ifdef HA_X_WSYNC_BLOCK     /* A/B: the workgroup-scope barrier */
 HD void wsync() { __syncthreads(); }
+#else
+HD void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+#endif
 
 // value of lane `src` in every lane; src must be wave-uniform (v_readlane_b32 -> SGPR)
 HD float bcast(float x, int src) {

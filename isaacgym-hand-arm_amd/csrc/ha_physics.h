@@ -1821,53 +1821,41 @@ HD void substep(SimCtx& c, float hdt) {
         // Each joint row's update is computed by the lane that owns the joint (its own v[d], lambda and row
         // constants: the same operands the oracle uses), and only the impulse change crosses lanes (one
         // v_readlane); the joint-limit rows run only for the joints whose limit is active (ballot masks).
-        // Lane d runs its DOF's rows (drive, active limits, friction) in order on its own copy of v[d], applying
-        // each impulse change with the same fmaf(M^-1[d][d], delta, v) the all-lane update gives lane d; then the
-        // changes cross lanes together (independent v_readlanes) and every lane applies them in the row order.
-        // Same values and order as one row at a time (the oracle), one lane exchange per DOF instead of per row.
         for (int d = 0; d < D; d++) {
             float mrow = lane < D ? c.Minv[d * D + lane] : 0.0f;
-            const bool lo = (lo_mask >> d) & 1ull, up = (up_mask >> d) & 1ull, fr = (fr_mask >> d) & 1ull;
-            float vd = vreg;
-            float nl = dlam - (vd + dbias + dgam * dlam) * dwinv;
+            float nl = dlam - (vreg + dbias + dgam * dlam) * dwinv;
             nl = nl < -dlim ? -dlim : (nl > dlim ? dlim : nl);
-            float el = nl - dlam;
-            if (el != 0.0f) vd = fmaf(mrow, el, vd);
-            float n0 = 0.f, n1 = 0.f, nf = 0.f, e0 = 0.f, e1 = 0.f, ef = 0.f;
-            if (lo) {
-                n0 = lam_lo - (vd - vt_lo) * lwinv;
-                n0 = n0 < 0.0f ? 0.0f : n0;
-                e0 = n0 - lam_lo;
-                if (e0 != 0.0f) vd = fmaf(mrow, e0, vd);
-            }
-            if (up) {
-                n1 = lam_up - (-vd - vt_up) * lwinv;
-                n1 = n1 < 0.0f ? 0.0f : n1;
-                e1 = n1 - lam_up;
-                if (e1 != 0.0f) vd = fmaf(-mrow, e1, vd);
-            }
-            if (fr) {
-                nf = lam_fr - vd * lwinv;
-                nf = nf < -flim ? -flim : (nf > flim ? flim : nf);
-                ef = nf - lam_fr;
-            }
-            float dl = bcast(el, d);
-            float d0 = lo ? bcast(e0, d) : 0.0f, d1 = up ? bcast(e1, d) : 0.0f, df = fr ? bcast(ef, d) : 0.0f;
+            float dl = bcast(nl - dlam, d);
             if (dl != 0.0f) {
                 if (lane == d) dlam = nl;
                 vreg = fmaf(mrow, dl, vreg);
             }
-            if (d0 != 0.0f) {
-                if (lane == d) lam_lo = n0;
-                vreg = fmaf(mrow, d0, vreg);
+            if ((lo_mask >> d) & 1ull) {
+                float n0 = lam_lo - (vreg - vt_lo) * lwinv;
+                n0 = n0 < 0.0f ? 0.0f : n0;
+                float d0 = bcast(n0 - lam_lo, d);
+                if (d0 != 0.0f) {
+                    if (lane == d) lam_lo = n0;
+                    vreg = fmaf(mrow, d0, vreg);
+                }
             }
-            if (d1 != 0.0f) {
-                if (lane == d) lam_up = n1;
-                vreg = fmaf(-mrow, d1, vreg);
+            if ((up_mask >> d) & 1ull) {
+                float n1 = lam_up - (-vreg - vt_up) * lwinv;
+                n1 = n1 < 0.0f ? 0.0f : n1;
+                float d1 = bcast(n1 - lam_up, d);
+                if (d1 != 0.0f) {
+                    if (lane == d) lam_up = n1;
+                    vreg = fmaf(-mrow, d1, vreg);
+                }
             }
-            if (df != 0.0f) {
-                if (lane == d) lam_fr = nf;
-                vreg = fmaf(mrow, df, vreg);
+            if ((fr_mask >> d) & 1ull) {
+                float nf = lam_fr - vreg * lwinv;
+                nf = nf < -flim ? -flim : (nf > flim ? flim : nf);
+                float df = bcast(nf - lam_fr, d);
+                if (df != 0.0f) {
+                    if (lane == d) lam_fr = nf;
+                    vreg = fmaf(mrow, df, vreg);
+                }
             }
         }
         // contact blocks: the three J.v reductions of a contact run together; the friction rows see the
