@@ -175,7 +175,7 @@ __host__ __device__ inline size_t obj_lds_offset_rows(size_t rows) {
 #define HA_SPLIT_ABOVE_OCAP 2   /* families with more object slots use split rows (Ur5Sih 3 objects, clutter) */
 #endif
 template <int ND, int OCAP, int NCH, int KL = 8, int LCH = NCH, int CAP = MAXC, int CV = 64, int CP = 128,
-          int SPLIT = -1, int NG = HA_MAX_GATHER, bool MU = false>
+          int SPLIT = -1, int NG = HA_MAX_GATHER, bool MU = false, bool RC = false>
 struct PhysCfg {
     static constexpr int nd = ND, ocap = OCAP, nch = NCH;
     static constexpr int colv = CV, colp = CP, colg = NG;   // largest hull: vertices, face planes; gather points
@@ -192,11 +192,14 @@ struct PhysCfg {
     static constexpr int ow = 6 * row_slots<ND>();  // split rows: object-block width
     static constexpr int kl = KL;
     static constexpr bool minv_in_union = MU;
+    // split rows with recomputed object blocks (RC, the clutter family): no object-block rows are stored at all; the
+    // rows phase and the PGS evaluate a contact row's object blocks in registers from the contact entry (obj_blocks)
+    static constexpr bool rc = RC && split;
     // split rows: the object blocks of chunks [0, lch) live in LDS, those of chunks [lch, nch) in the env's global
     // row area after the robot-block spill rows (written by the rows phase, read back by the PGS one contact ahead)
     static constexpr int lch = split ? LCH : NCH;
     static constexpr int spill_robot = split ? 2 * 3 * (CAP * NCH - KL) * ND : 0;   // per env: J then Y
-    static constexpr int spill_obj = split ? 2 * rpc * (NCH - lch) * ow : 0;        // per env: J then Y
+    static constexpr int spill_obj = split && !rc ? 2 * rpc * (NCH - lch) * ow : 0;  // per env: J then Y
     static constexpr int spill_floats = spill_robot + spill_obj;
     static_assert(ND + 6 * OCAP <= MAXV, "generalized velocity exceeds MAXV");
     static_assert(!split || (KL >= 0 && KL <= CAP * NCH), "LDS link slots must not exceed the contact capacity");
@@ -1509,6 +1512,38 @@ HD void tangents(f3 n, f3& t1, f3& t2) {
     t2 = cross3(n, t1);
 }
 
+// Object blocks of one contact row (slot 0: object so0, slot 1: so1; row direction dir), in registers, by the
+// expressions of jac_body and the stored rows: J = (0 + sgn dir, 0 + sgn (x - c_o) x dir) with sgn +1 for body a
+// and -1 for body b, Y = (J_lin (1 / m), I_w^-1 J_ang); an absent slot is zero. Used by the families that recompute
+// instead of storing them (PhysCfg RC), so every value equals the stored-row value bit for bit.
+HD void obj_block(const SimCtx& c, int o, int a, f3 x, f3 dir, float* j6, float* y6) {
+    if (o < 0) {
+#pragma unroll
+        for (int t = 0; t < 6; t++) { j6[t] = 0.0f; y6[t] = 0.0f; }
+        return;
+    }
+    float sgn = o == a ? 1.0f : -1.0f;
+    f3 ang = cross3(x - ld3(c.o[o].oc), dir);
+    j6[0] = 0.0f + sgn * dir.x; j6[1] = 0.0f + sgn * dir.y; j6[2] = 0.0f + sgn * dir.z;
+    j6[3] = 0.0f + sgn * ang.x; j6[4] = 0.0f + sgn * ang.y; j6[5] = 0.0f + sgn * ang.z;
+    float im = c.o[o].oc[3];
+    y6[0] = j6[0] * im; y6[1] = j6[1] * im; y6[2] = j6[2] * im;
+    f3 ya = mv3(c.o[o].oIinv, mk3(j6[3], j6[4], j6[5]));
+    y6[3] = ya.x; y6[4] = ya.y; y6[5] = ya.z;
+}
+// entry t (0..5) of slot object o's block of row direction dir: (J, Y), the values obj_block gives
+HD void obj_entry(const SimCtx& c, int o, int a, f3 x, f3 dir, int t, float& j, float& y) {
+    float sgn = o == a ? 1.0f : -1.0f;
+    f3 ang = cross3(x - ld3(c.o[o].oc), dir);
+    f3 jl = mk3(0.0f + sgn * dir.x, 0.0f + sgn * dir.y, 0.0f + sgn * dir.z);
+    f3 ja = mk3(0.0f + sgn * ang.x, 0.0f + sgn * ang.y, 0.0f + sgn * ang.z);
+    f3 ya = mv3(c.o[o].oIinv, ja);
+    float im = c.o[o].oc[3];
+    float jv = t == 0 ? jl.x : (t == 1 ? jl.y : (t == 2 ? jl.z : (t == 3 ? ja.x : (t == 4 ? ja.y : ja.z))));
+    j = jv;
+    y = t < 3 ? jv * im : (t == 3 ? ya.x : (t == 4 ? ya.y : ya.z));
+}
+
 
 template <class PC>
 HD void substep(SimCtx& c, float hdt) {
@@ -1580,6 +1615,7 @@ HD void substep(SimCtx& c, float hdt) {
         for (int k = 0; k < 9; k++) c.o[o].oIinv[k] = Ii[k];
         mass = mass * sc;
         c.o[o].om = mass;
+        c.o[o].oc[3] = 1.0f / mass;     // the rows' 1 / m (obj_blocks reads it instead of dividing per PGS fetch)
         // external force (zero unless a task applied one): constant over the call's substeps
         f3 lv = (ld3(c.o[o].ov) + ld3(p.gravity) * hdt) + ld3(c.o[o].ofx) * (hdt / mass);
         f3 av = ld3(c.o[o].ow) * damp;
@@ -1664,13 +1700,19 @@ HD void substep(SimCtx& c, float hdt) {
             int k = r % 3;
             // robot block Jr / Yr (null: the contact touches no link, the block is zero) and object blocks Jo / Yo
             float *Jr, *Yr, *Jo, *Yo;
+            float jo_rc[PC::rc ? OW : 1], yo_rc[PC::rc ? OW : 1];     // RC: this row's object blocks, in registers
             if constexpr (PC::split) {
                 int ls = lslot(r / 3);
                 Jr = ls >= 0 ? rrow(ls, k, false) : nullptr;
                 Yr = ls >= 0 ? rrow(ls, k, true) : nullptr;
-                Jo = orow(r, false);
-                Yo = orow(r, true);
-                for (int t = 0; t < OW; t++) Jo[t] = 0.0f;
+                if constexpr (PC::rc) {
+                    Jo = jo_rc;
+                    Yo = yo_rc;
+                } else {
+                    Jo = orow(r, false);
+                    Yo = orow(r, true);
+                    for (int t = 0; t < OW; t++) Jo[t] = 0.0f;
+                }
                 if (Jr)
                     for (int t = 0; t < ND; t++) Jr[t] = 0.0f;
             } else {
@@ -1686,8 +1728,16 @@ HD void substep(SimCtx& c, float hdt) {
             f3 x = ld3(ct.x);
             int so0, so1;
             contact_slots(ct.a, ct.b, so0, so1);
-            jac_body(c, ct.a, x, dir, 1.0f, Jr, Jo, so0);
-            jac_body(c, ct.b, x, dir, -1.0f, Jr, Jo, so0);
+            if constexpr (PC::rc) {
+                // robot block from the link bodies; both object blocks (and their Y) straight into registers
+                if (ct.a >= 100) jac_body(c, ct.a, x, dir, 1.0f, Jr, nullptr, so0);
+                if (ct.b >= 100) jac_body(c, ct.b, x, dir, -1.0f, Jr, nullptr, so0);
+                obj_block(c, so0, ct.a, x, dir, jo_rc, yo_rc);
+                obj_block(c, so1, ct.a, x, dir, jo_rc + 6, yo_rc + 6);
+            } else {
+                jac_body(c, ct.a, x, dir, 1.0f, Jr, Jo, so0);
+                jac_body(c, ct.b, x, dir, -1.0f, Jr, Jo, so0);
+            }
             if (k == 0) {
                 float sp = ct.sep;
                 float sb = sp + p.contact_slop < 0.0f ? sp + p.contact_slop : 0.0f;   // penetration beyond the slop
@@ -1709,7 +1759,7 @@ HD void substep(SimCtx& c, float hdt) {
                     Yr[i] = acc;
                 }
             }
-            for (int sl = 0; sl < row_slots<ND>(); sl++) {
+            for (int sl = 0; sl < (PC::rc ? 0 : row_slots<ND>()); sl++) {    // RC: Y already from obj_block
                 int o = sl == 0 ? so0 : so1;
                 const float* Jos = Jo + 6 * sl;
                 float* Yos = Yo + 6 * sl;
@@ -1751,6 +1801,7 @@ HD void substep(SimCtx& c, float hdt) {
                 if (k == 2)
                     for (int t = 0; t < D; t++) b = fmaf(Jr[t], Y1r[t], b);
             };
+            float jo_rc[PC::rc ? OW : 1], y0_rc[PC::rc ? 2 * OW : 1];     // RC: J of this row, Y of rows r0, r0 + 1
             if constexpr (PC::split) {
                 // LDS slot or global spill row on separate paths, so each keeps its own address space
                 int ls = lslot(r / 3);
@@ -1759,8 +1810,27 @@ HD void substep(SimCtx& c, float hdt) {
                     const float* sr = c.spill + 3 * (ls - KL) * ND;
                     rdot(sr + k * ND, sr + SPJ, sr + SPJ + ND);
                 }
-                Jo = orow(r, false);
-                Y0o = orow(r0, true);
+                if constexpr (PC::rc) {
+                    const ContactLDS& ct = c.k[r / 3];
+                    f3 n = ld3(ct.n), t1, t2;
+                    tangents(n, t1, t2);
+                    f3 x = ld3(ct.x);
+                    int so0, so1;
+                    contact_slots(ct.a, ct.b, so0, so1);
+                    float scratch[OW];
+                    f3 dk = k == 1 ? t1 : t2;
+                    obj_block(c, so0, ct.a, x, dk, jo_rc, scratch);
+                    obj_block(c, so1, ct.a, x, dk, jo_rc + 6, scratch + 6);
+                    obj_block(c, so0, ct.a, x, n, scratch, y0_rc);
+                    obj_block(c, so1, ct.a, x, n, scratch + 6, y0_rc + 6);
+                    obj_block(c, so0, ct.a, x, t1, scratch, y0_rc + OW);
+                    obj_block(c, so1, ct.a, x, t1, scratch + 6, y0_rc + OW + 6);
+                    Jo = jo_rc;
+                    Y0o = y0_rc;
+                } else {
+                    Jo = orow(r, false);
+                    Y0o = orow(r0, true);
+                }
             } else {
                 rdot(Jb + r * RSN, Yb + r0 * RSN, Yb + (r0 + 1) * RSN);
                 Jo = Jb + r * RSN + D;
@@ -1876,6 +1946,46 @@ HD void substep(SimCtx& c, float hdt) {
             }
             j0n = 0.f; j1n = 0.f; j2n = 0.f; y0n = 0.f; y1n = 0.f; y2n = 0.f;
             h0n = 0.f; h1n = 0.f; h2n = 0.f; g0n = 0.f; g1n = 0.f; g2n = 0.f;
+            if constexpr (PC::rc) {
+                // object coordinates recomputed from the contact entry (obj_entry: the rows phase's values);
+                // robot coordinates from the contact's link slot (LDS for the first KL, else the spill rows)
+                const ContactLDS& ct = c.k[ci];
+                int so0, so1;
+                contact_slots(ct.a, ct.b, so0, so1);
+                bool o1 = ix >= D, o2 = VW == 2 && ixh >= D;
+                if (o1 || o2) {
+                    f3 n = ld3(ct.n), t1, t2;
+                    tangents(n, t1, t2);
+                    f3 x = ld3(ct.x);
+                    if (o1) {
+                        int t = ix - D, o = t < 6 ? so0 : so1, e = t < 6 ? t : t - 6;
+                        obj_entry(c, o, ct.a, x, n, e, j0n, y0n);
+                        obj_entry(c, o, ct.a, x, t1, e, j1n, y1n);
+                        obj_entry(c, o, ct.a, x, t2, e, j2n, y2n);
+                    }
+                    if (o2) {
+                        int t = ixh - D, o = t < 6 ? so0 : so1, e = t < 6 ? t : t - 6;
+                        obj_entry(c, o, ct.a, x, n, e, h0n, g0n);
+                        obj_entry(c, o, ct.a, x, t1, e, h1n, g1n);
+                        obj_entry(c, o, ct.a, x, t2, e, h2n, g2n);
+                    }
+                }
+                if (ix >= 0 && ix < D) {
+                    int ls = lslot(ci);         // wave-uniform: one path per contact, LDS or global
+                    if (ls >= 0 && ls < KL) {
+                        const float* Rn = Rb + 3 * ls * ND;
+                        const float* RYn = RbY + 3 * ls * ND;
+                        j0n = Rn[ix]; j1n = Rn[ND + ix]; j2n = Rn[2 * ND + ix];
+                        y0n = RYn[ix]; y1n = RYn[ND + ix]; y2n = RYn[2 * ND + ix];
+                    } else if (ls >= KL) {
+                        const float* Rn = c.spill + 3 * (ls - KL) * ND;
+                        const float* RYn = c.spill + SPJ + 3 * (ls - KL) * ND;
+                        j0n = Rn[ix]; j1n = Rn[ND + ix]; j2n = Rn[2 * ND + ix];
+                        y0n = RYn[ix]; y1n = RYn[ND + ix]; y2n = RYn[2 * ND + ix];
+                    }
+                }
+                return;
+            }
             if constexpr (PC::split) {
                 // object coordinates from the LDS object blocks; robot coordinates from the contact's link slot
                 // (LDS for the first KL, else the global spill rows), absent -> 0

@@ -45,6 +45,12 @@ __host__ __device__ constexpr int task_obj_capacity() {
 #endif
 template <int FAM>
 __host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5SIH_CLUTTER ? HB_CHUNKS : 1; }
+// clutter family: the object blocks of the contact rows are recomputed in registers from the contact entries in the
+// rows phase and at every PGS fetch (PhysCfg RC) instead of stored in the env's global row area (24 KB per env and
+// substep that L2 could not hold: the PGS waited on HBM at every contact). 0 restores the stored rows (A/B)
+#ifndef HB_RECOMPUTE
+#define HB_RECOMPUTE 1
+#endif
 // clutter family: link contacts whose robot blocks stay in LDS (the rest use the global spill rows). 2 slots
 // keep the env block at <= 20 KB, i.e. 8 workgroups per CU (8 slots: 22.8 KB, 7 per CU)
 #ifndef HB_LINK_SLOTS
@@ -133,7 +139,8 @@ template <int FAM>
 using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_chunks<FAM>(), task_link_slots<FAM>(),
                         FAM == FAM_UR5SIH_CLUTTER ? HB_LDS_CHUNKS : task_contact_chunks<FAM>(),
                         task_chunk_capacity<FAM>(), task_col_verts<FAM>(), task_col_planes<FAM>(),
-                        task_compact<FAM>() ? 1 : -1, task_compact<FAM>() ? 0 : HA_MAX_GATHER, task_compact<FAM>()>;
+                        task_compact<FAM>() ? 1 : -1, task_compact<FAM>() ? 0 : HA_MAX_GATHER, task_compact<FAM>(),
+                        FAM == FAM_UR5SIH_CLUTTER && HB_RECOMPUTE>;
 
 
 // ----------------------------------------------------------------------------- state load/store
