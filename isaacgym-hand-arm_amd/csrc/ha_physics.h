@@ -809,6 +809,7 @@ HD float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
 // same expression as in the oracle; only the parallel order of the (exact) min/max differs.
 HD void sat_planes(const SimCtx& c, const float (*wp)[4], int np, const float (*wv)[4], int nv, float& sep, int& kbest) {
     int lane = c.lane;
+#ifdef HA_X_SAT_LANE_VERTEX   /* A/B: lane = vertex, one wave min per plane */
     if (np <= 8) {
         // few planes (boxes): lane = vertex, one wave min per plane. The eight plane slots are unrolled so their
         // independent DPP reduction chains interleave (slots k >= np read in-bounds scratch and are masked), then
@@ -831,6 +832,32 @@ HD void sat_planes(const SimCtx& c, const float (*wp)[4], int np, const float (*
         kbest = bk;
         return;
     }
+#else
+    if (np <= 8) {
+        // few planes (boxes): lane = (plane k = lane / 8, vertex group g = lane % 8). A lane takes the min over its
+        // group's vertices g, g + 8, ..., then the plane's eight lanes combine (quad_perm xor1, xor2,
+        // row_half_mirror: a min inside each 8-lane group), then one wave max over the planes; its first k is the
+        // lowest lane holding it (the oracle's strict-compare scan keeps the first maximum). Every (k, i) value is
+        // the oracle's expression and min / max are exact, so the order does not matter
+        int k = lane >> 3, g = lane & 7;
+        float m = 3.0e38f;
+        if (k < np) {
+            f3 n = ld3(wp[k]);
+            float d = wp[k][3];
+#pragma unroll 1
+            for (int i = g; i < nv; i += 8) m = fminf(m, dot3(n, ld3(wv[i])) + d);
+        }
+        m = fminf(m, dpp_f<0xB1>(m));
+        m = fminf(m, dpp_f<0x4E>(m));
+        m = fminf(m, dpp_f<0x141>(m));
+        float v = k < np ? m : -3.0e38f;
+        float best = wave_max(v);
+        uint64_t hit = __ballot(k < np && v == best);
+        sep = best;
+        kbest = (int)((__ffsll((unsigned long long)hit) - 1) >> 3);
+        return;
+    }
+#endif
     // lane = plane (k = lane, lane + 64), loop over the vertices with batched LDS loads
     float best = -3.0e38f;
     int bk = 1 << 20;

@@ -45,11 +45,12 @@ __host__ __device__ constexpr int task_obj_capacity() {
 #endif
 template <int FAM>
 __host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5SIH_CLUTTER ? HB_CHUNKS : 1; }
-// clutter family: the object blocks of the contact rows are recomputed in registers from the contact entries in the
-// rows phase and at every PGS fetch (PhysCfg RC) instead of stored in the env's global row area (24 KB per env and
-// substep that L2 could not hold: the PGS waited on HBM at every contact). 0 restores the stored rows (A/B)
+// clutter family: 1 recomputes the object blocks of the contact rows in registers from the contact entries in the
+// rows phase and at every PGS fetch (PhysCfg RC) instead of storing them in the env's global row area. Measured on
+// C5 (round 3): 22.1 -> 30.8 ms per step, the ~140 VALU per fetch cost more than the stored rows' traffic, which the
+// one-contact-ahead prefetch hides; the product keeps the stored rows
 #ifndef HB_RECOMPUTE
-#define HB_RECOMPUTE 1
+#define HB_RECOMPUTE 0
 #endif
 // clutter family: link contacts whose robot blocks stay in LDS (the rest use the global spill rows). 2 slots
 // keep the env block at <= 20 KB, i.e. 8 workgroups per CU (8 slots: 22.8 KB, 7 per CU)
