@@ -225,9 +225,13 @@ __host__ __device__ constexpr size_t pc_rows_bytes() {
 }
 // S ~ M^-1 (factor_inverse), D x D at stride D, sized for the family's DOF count: at the end of the union
 // (minv_in_union) or after it
+// (after the constraint rows when those reach past it: the union then grows by the difference, which the
+// AllegroKuka layout spends on a third LDS link slot)
 template <class PC>
 __host__ __device__ constexpr size_t minv_union_offset() {
-    return (sizeof(PostScratch) - (size_t)PC::nd * PC::nd * sizeof(float)) & ~(size_t)15;
+    size_t a = (sizeof(PostScratch) - (size_t)PC::nd * PC::nd * sizeof(float)) & ~(size_t)15;
+    size_t r = (pc_rows_bytes<PC>() + 15) & ~(size_t)15;
+    return a > r ? a : r;
 }
 template <class PC>
 __host__ __device__ inline size_t minv_lds_offset() {
@@ -256,8 +260,11 @@ __device__ inline ColView col_view(void* u) {
 }
 template <class PC>
 __host__ __device__ inline size_t obj_lds_offset() {
-    if constexpr (PC::minv_in_union)
-        return obj_lds_offset_rows(pc_rows_bytes<PC>() > PC::col_bytes ? pc_rows_bytes<PC>() : PC::col_bytes);
+    if constexpr (PC::minv_in_union) {
+        size_t u = pc_rows_bytes<PC>() > PC::col_bytes ? pc_rows_bytes<PC>() : PC::col_bytes;
+        size_t se = minv_union_offset<PC>() + (size_t)PC::nd * PC::nd * sizeof(float);
+        return obj_lds_offset_rows(u > se ? u : se);
+    }
     else
         return (minv_lds_offset<PC>() + (size_t)PC::nd * PC::nd * sizeof(float) + 15) & ~(size_t)15;
 }
