@@ -27,7 +27,7 @@ TORCH_DTYPE = {"float32": torch.float32, "int64": torch.int64, "uint8": torch.ui
 
 class HandArmSim:
     def __init__(self, num_envs, device="cuda:0", task_cfg=None, scene=None, pool_names=None, stats_ring=64,
-                 task=None, rebalance_every=8):
+                 task=None, rebalance_every=4):
         if not str(device).startswith("cuda"):
             raise _lib.HandArmError("libhandarm_hip runs on a HIP device only (device must be 'cuda:N')")
         self.lib = _lib.load()
