@@ -225,9 +225,11 @@ class Ur5SihMultiObjectManipulation:
         sees (handarm_hip/observables.py)."""
         self.obs_names = list(env.get("observations") or OB.DEFAULT_OBSERVATIONS)
         teacher = list(env.get("teacher_observations") or OB.DEFAULT_OBSERVATIONS)
-        if teacher != OB.DEFAULT_OBSERVATIONS:
-            raise NotImplementedError("teacher_observations: this build writes the default teacher list "
-                                      f"{OB.DEFAULT_OBSERVATIONS}")
+        # a custom teacher list (cfg teacher_observations, observable_vec_task.py:17-18,194-203) is gathered like a
+        # custom student list: its "obs"-key observables concatenated into obs_dict["teacher"]["obs"], its clouds
+        # in obs_dict["teacher"][name]
+        self.teacher_names = teacher
+        self.custom_teacher = teacher != OB.DEFAULT_OBSERVATIONS
         # camera observables `{camera}_{depth,segmentation,pointcloud}` (observable_vec_task.py:36-82): one sensor
         # per camera of cfg["cameras"] that the list names; refreshed after every other observable
         # (configurable_vec_task.py:91-114), so they do not enter the post-step order
@@ -251,13 +253,17 @@ class Ur5SihMultiObjectManipulation:
                     and n not in self.camera_obs:
                 raise NotImplementedError(f"observable {n!r}: this build produces the synthetic clouds "
                                           f"{OB.POINTCLOUDS} and camera images {IMAGE_TYPES} of cfg['cameras']")
+        for n in teacher:
+            if n.endswith(("_pointcloud", "_depth", "_segmentation", "_color")) and n not in OB.POINTCLOUDS:
+                raise NotImplementedError(f"teacher observable {n!r}: a teacher list takes the low-dimensional "
+                                          f"observables and the synthetic clouds {OB.POINTCLOUDS}")
         order = OB.post_step_order([n for n in self.obs_names if n not in self.camera_obs], teacher)
         if not OB.sees_previous_object_pose(order, "object_bounding_box"):
             raise NotImplementedError("observation list refreshes object_bounding_box after object_pos; the step "
                                       "kernel implements the default order (bbox sees the previous pose)")
         self.custom_obs = self.obs_names != OB.DEFAULT_OBSERVATIONS
         self.pointclouds = None
-        pc_names = [n for n in self.obs_names if n in OB.POINTCLOUDS]
+        pc_names = [n for n in dict.fromkeys(self.obs_names + teacher) if n in OB.POINTCLOUDS]
         if pc_names:
             g = torch.Generator(device=self.device).manual_seed(int(cfg.get("seed", 42)))
             self.pointclouds = SyntheticPointclouds(self.sim, pc_names, objects, _get(cfg, "pointclouds", {}), g)
@@ -265,12 +271,26 @@ class Ur5SihMultiObjectManipulation:
             if any(OB.sees_previous_object_pose(order, n) for n in
                    ("object_synthetic_pointcloud", "target_object_synthetic_pointcloud") if n in order):
                 self.pointclouds.use_previous_object_pose()
-        if not self.custom_obs:
+        if not (self.custom_obs or self.custom_teacher):
             return
         m = self.sim.model
         layout = dict(a0=m.actor_object0, body_robot0=m.body_robot0, n_dofs=m.n_dofs)
-        cols = OB.obs_columns(self.obs_names, self.num_objects, layout)
         self._obs_layout = layout
+        if self.custom_teacher:
+            tcols = OB.obs_columns(teacher, self.num_objects, layout)
+            self._teacher_cols = torch.tensor(tcols, dtype=torch.int32, device=self.device)
+            self.teacher_custom_buf = torch.zeros((N, len(tcols)), dtype=torch.float32, device=self.device)
+            self.num_teacher_observations = len(tcols)
+            self.teacher_obs_space = Box(np.full(len(tcols), -np.inf), np.full(len(tcols), np.inf))
+            start, self.teacher_observations_start_end = 0, {}
+            for n in teacher:
+                k = len(OB.obs_columns([n], self.num_objects, layout))
+                if k:
+                    self.teacher_observations_start_end[n] = (start, start + k)
+                    start += k
+        if not self.custom_obs:
+            return
+        cols = OB.obs_columns(self.obs_names, self.num_objects, layout)
         self._obs_cols = torch.tensor(cols, dtype=torch.int32, device=self.device)
         self.student_obs_buf = torch.zeros((N, len(cols)), dtype=torch.float32, device=self.device)
         self.num_observations = len(cols)
@@ -286,7 +306,7 @@ class Ur5SihMultiObjectManipulation:
         """ha_gather_obs sources of a custom observation list (observables.SRC_*), once the objects are chosen.
         object_mass / object_com / object_inertia (multi_object.py:907-925) are the pool properties of each env's
         objects, fixed at creation (the reference reads them once, at post_init)."""
-        if not self.custom_obs:
+        if not (self.custom_obs or self.custom_teacher):
             return
         m, N = self.sim.model, self.num_envs
         pm = torch.tensor(np.ctypeslib.as_array(m.pool_mass)[:m.n_pool], dtype=torch.float32)
@@ -312,12 +332,24 @@ class Ur5SihMultiObjectManipulation:
         self.obs_dict["obs"] = torch.clamp(obs, -self.clip_obs, self.clip_obs).to(self.rl_device)
         if self.pointclouds is not None:
             for n, t in self.pointclouds.outputs.items():
-                self.obs_dict[n] = t.to(self.rl_device)
+                if n in self.obs_names:
+                    self.obs_dict[n] = t.to(self.rl_device)
         for n, (cam, kind) in self.camera_obs.items():
             img = self.cameras[cam].images[kind]
             # PointcloudObservable's FlattenPointcloud transform (transforms.py:17-20): (N, H * W, 4)
             self.obs_dict[n] = (img.flatten(1, 2) if kind == "pointcloud" else img).to(self.rl_device)
-        self.obs_dict["teacher"] = {"obs": torch.clamp(self.teacher_obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)}
+        teacher = self.teacher_obs_buf
+        if self.custom_teacher:
+            _lib.check(self.sim.lib.ha_gather_obs(self.sim.h, self._gather_src, self._gather_stride, 6,
+                                                  self._teacher_cols.data_ptr(), len(self._teacher_cols),
+                                                  self.teacher_custom_buf.data_ptr(), self.sim._stream()),
+                       "ha_gather_obs")
+            teacher = self.teacher_custom_buf
+        self.obs_dict["teacher"] = {"obs": torch.clamp(teacher, -self.clip_obs, self.clip_obs).to(self.rl_device)}
+        if self.pointclouds is not None:
+            for n in self.teacher_names:
+                if n in self.pointclouds.outputs:
+                    self.obs_dict["teacher"][n] = self.pointclouds.outputs[n].to(self.rl_device)
         return self.obs_dict
 
     # ------------------------------------------------------------------ VecTask properties

@@ -199,3 +199,32 @@ def test_registered_low_dim_observables_through_vectask():
         put(env.sim, "target_object_index", d["target_idx"][s])
         obs = cpu(env.reset()["obs"])            # VecTask.reset: compute_observations of the bound state
         np.testing.assert_array_equal(obs, d["obs"][s])
+
+
+def test_custom_teacher_list_through_vectask():
+    """A custom teacher list (cfg teacher_observations, observable_vec_task.py:17-18,194-203) next to the default
+    student list: obs_dict["teacher"]["obs"] is the concatenation of the listed observables, the same rows the
+    reference computes for that list as a student list (tests/golden/ur5sih_obs_custom.npz), bit for bit; the
+    student obs stay the default list."""
+    need_gpu()
+    from handarm_hip.tasks import Ur5SihMultiObjectManipulation
+    d = np.load(os.path.join(G, "ur5sih_obs_custom.npz"))
+    names = [str(n) for n in d["observations"]]
+    T, N = d["target_idx"].shape
+    env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": N, "teacher_observations": names},
+                                         "objects": {"dataset": {"ycb": [str(n) for n in d["object_names"]]}}},
+                                        "cuda:0", "cuda:0")
+    assert env.num_teacher_obs == d["obs"].shape[-1] and env.num_obs == 147
+    se = env.teacher_observations_start_end                # the attribute (the property keeps the reference's None)
+    assert list(se) == [n for n in names if n in se] and max(e for _, e in se.values()) == env.num_teacher_obs
+    put(env.sim, "object_indices", d["object_indices"])
+    env._bind_gather_sources()
+    for s in range(T):
+        put(env.sim, "root_state", d["root"][s])
+        put(env.sim, "rigid_body_state", d["body"][s])
+        put(env.sim, "dof_state", d["dof"][s])
+        put(env.sim, "goal_pos", d["goal_pos"][s])
+        put(env.sim, "target_object_index", d["target_idx"][s])
+        od = env.reset()
+        np.testing.assert_array_equal(cpu(od["teacher"]["obs"]), d["obs"][s])
+        assert od["obs"].shape == (N, 147)
