@@ -86,6 +86,18 @@ class HandArmSim:
             _lib.check(self.lib.ha_set_env_order(self.h, C.c_void_p(self._env_order.data_ptr()), num_envs),
                        "ha_set_env_order")
 
+    def snapshot(self):
+        """Device copy of the env-state SoA (every tensor the kernels read or write: gym state tensors, targets,
+        controller and task state, counters, DR rows, draws). restore() puts the shard back exactly, so the next
+        steps reproduce bit for bit (SURVEY.md §5 checkpoint row; the task classes' get_env_state / set_env_state
+        keep the host-side curriculum values, as in the reference). One device-to-device copy per tensor."""
+        return {k: v.clone() for k, v in self.t.items()}
+
+    def restore(self, snap):
+        """Copy a snapshot() back into the bound tensors (same shapes; the kernels keep their pointers)."""
+        for k, v in snap.items():
+            self.t[k].copy_(v)
+
     def rebalance(self):
         """Dispatch the envs that offered the most contacts since the last call first (device argsort, stable, no
         host sync). In a launch with more envs than resident workgroup slots, the slots that free up take the
