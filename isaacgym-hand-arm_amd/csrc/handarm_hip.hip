@@ -612,19 +612,35 @@ extern "C" __global__ void __launch_bounds__(256) ha_epilogue_kernel(const float
                                                                       float* __restrict__ obs_out, long long n_obs,
                                                                       float clip, const float* __restrict__ ts,
                                                                       int ts_stride, int n_env, float* __restrict__ out) {
-    long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-    long long stride = (long long)gridDim.x * 256;
-    if (obs_out)
-        for (long long k = i; k < n_obs; k += stride) obs_out[k] = fminf(fmaxf(obs[k], -clip), clip);
-    if (blockIdx.x != 0 || !ts || !out) return;
+    // block 0 reduces the task scalars (when asked); the obs clamp runs on the other blocks
+    bool red_block = ts && out && blockIdx.x == 0;
+    if (obs_out && !(red_block && gridDim.x > 1)) {
+        long long b = red_block ? 0 : (ts && out ? blockIdx.x - 1 : blockIdx.x);
+        long long nb = ts && out && gridDim.x > 1 ? gridDim.x - 1 : gridDim.x;
+        for (long long k = b * 256 + threadIdx.x; k < n_obs; k += nb * 256) obs_out[k] = fminf(fmaxf(obs[k], -clip), clip);
+    }
+    if (!red_block) return;
     __shared__ float red[4][256];
     float s0 = 0.0f, s1 = 0.0f, mn = 3.0e38f, mx = -3.0e38f;
-    for (int e = threadIdx.x; e < n_env; e += 256) {
-        float ps = ts[(size_t)e * ts_stride + HA_AK_PREV_SUCC], to = ts[(size_t)e * ts_stride + HA_AK_TRUE_OBJ];
-        s0 += ps;
-        s1 += to;
-        mn = fminf(mn, to);
-        mx = fmaxf(mx, to);
+    // the thread's envs e = tid, tid + 256, ... in order; eight rows' loads are issued before they are added, so the
+    // strided reads overlap instead of costing one round trip each (same sums in the same order)
+    for (int e0 = threadIdx.x; e0 < n_env; e0 += 256 * 8) {
+        float ps[8], to[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            int e = e0 + 256 * u;
+            ps[u] = e < n_env ? ts[(size_t)e * ts_stride + HA_AK_PREV_SUCC] : 0.0f;
+            to[u] = e < n_env ? ts[(size_t)e * ts_stride + HA_AK_TRUE_OBJ] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            if (e0 + 256 * u < n_env) {
+                s0 += ps[u];
+                s1 += to[u];
+                mn = fminf(mn, to[u]);
+                mx = fmaxf(mx, to[u]);
+            }
+        }
     }
     red[0][threadIdx.x] = s0; red[1][threadIdx.x] = s1; red[2][threadIdx.x] = mn; red[3][threadIdx.x] = mx;
     __syncthreads();
