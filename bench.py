@@ -368,15 +368,17 @@ def run_config(task, envs, args, world, rank, device, log_interval_fn):
     env.sim.enable_kernel_timing(args.steps)
     if hasattr(env, "contact_stats"):
         env.contact_stats(reset=True)               # contact-list diagnostics of the timed steps only
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # one event per step boundary (K + 1), not a pair per step: every event record costs a few microseconds of GPU
+    # idle in the stream, which the measurement should not add to the workload
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
+    ev[0].record()
     for k in range(args.steps):
-        ev[k][0].record()
         env.step(pool[k % len(pool)])
-        ev[k][1].record()
+        ev[k + 1].record()
         if (k + 1) % LOG_INTERVAL == 0:
             log_interval_fn(task, env)
     torch.cuda.synchronize()
@@ -387,7 +389,7 @@ def run_config(task, envs, args, world, rank, device, log_interval_fn):
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-    step_ms = [a.elapsed_time(b) for a, b in ev]
+    step_ms = [ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)]
     kern_ms = env.sim.kernel_times_ms(args.steps)
     pcs = getattr(env, "pointclouds", None)
     pc_ms = pcs.kernel_times_ms(args.steps) if pcs is not None else []

@@ -454,7 +454,8 @@ int ha_contact_capacity(ha_handle h);
  * simulates (kept by pointer: the caller keeps it alive), or NULL for the identity. Envs expected to take longest
  * first shortens a multi-round launch's tail (longest-processing-time order; handarm_hip/sim.py rebalance). */
 int ha_set_env_order(ha_handle h, const int32_t* order, int32_t n);
-/* last kernel time in ms measured with HIP events around the most recent physics/step launch (-1 if none) */
+/* last kernel time in ms measured with HIP events around the most recent timed physics/step launch (-1 if none;
+ * launches record events only while ha_enable_kernel_timing is on) */
 float ha_last_kernel_ms(ha_handle h);
 /* per-launch HIP-event timing of the env kernel (bench roofline): record up to max_launches launches
  * (0 disables); ha_kernel_times synchronises and returns the recorded durations in ms */

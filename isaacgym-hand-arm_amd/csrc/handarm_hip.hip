@@ -865,8 +865,10 @@ static int launch(ha_handle h, int mode, int n_calls, uint32_t flags, int slot, 
                   const int32_t* env_ids = nullptr, int n_ids = 0) {
     if (!h || !h->bound) return HA_E_STATE;
     hipStream_t s = (hipStream_t)stream;
+    // HIP events only while timing is enabled (ha_enable_kernel_timing): an event record in the stream costs a few
+    // microseconds of GPU idle between the kernels, which a training loop should not pay
     bool rec = h->t_ev && h->t_count < h->t_max;
-    (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count] : h->ev0, s);
+    if (rec) (void)hipEventRecord(h->t_ev[2 * h->t_count], s);
     if (!env_ids && h->order) {            // full shard in the caller's dispatch order (ha_set_env_order)
         env_ids = h->order;
         n_ids = h->N;
@@ -874,12 +876,11 @@ static int launch(ha_handle h, int mode, int n_calls, uint32_t flags, int slot, 
     hipLaunchKernelGGL(kernel_for(h->fam, mode), dim3(env_ids ? n_ids : h->N), dim3(64), lds_bytes(h->fam), s, h->d_model,
                        h->d_params, h->st, h->N, n_calls, flags, slot, h->d_spill, env_ids);
     HIPCHK(hipGetLastError());
-    (void)hipEventRecord(rec ? h->t_ev[2 * h->t_count + 1] : h->ev1, s);
     if (rec) {
-        (void)hipEventRecord(h->ev1, s);
+        (void)hipEventRecord(h->t_ev[2 * h->t_count + 1], s);
         h->t_count++;
+        h->timed = 1;
     }
-    h->timed = 1;
     return HA_OK;
 }
 
@@ -1227,10 +1228,11 @@ int ha_render_camera(ha_handle h, const ha_camera_t* cam, const float* view_inv,
 int ha_contact_capacity(ha_handle h) { return h ? contact_capacity(h->fam) : HA_E_ARG; }
 
 float ha_last_kernel_ms(ha_handle h) {
-    if (!h || !h->timed) return -1.0f;
+    if (!h || !h->timed || !h->t_ev || h->t_count < 1) return -1.0f;
     float ms = -1.0f;
-    if (hipEventSynchronize(h->ev1) != hipSuccess) return -1.0f;
-    if (hipEventElapsedTime(&ms, h->ev0, h->ev1) != hipSuccess) return -1.0f;
+    int k = h->t_count - 1;
+    if (hipEventSynchronize(h->t_ev[2 * k + 1]) != hipSuccess) return -1.0f;
+    if (hipEventElapsedTime(&ms, h->t_ev[2 * k], h->t_ev[2 * k + 1]) != hipSuccess) return -1.0f;
     return ms;
 }
 
