@@ -114,3 +114,47 @@ def test_allegro_reference_rng_steps():
         np.testing.assert_allclose(get(sim, "dof_state"), d["dof_after"][t], rtol=1e-6, atol=1e-6)
         np.testing.assert_allclose(get(sim, "root_state"), d["root_after"][t], rtol=1e-5, atol=2e-6)
         np.testing.assert_allclose(get(sim, "obs"), d["obs"][t], rtol=1e-5, atol=2e-6)
+
+
+def test_ur5sih_reference_rng_draw_order_with_point_clouds(monkeypatch):
+    """With sim.reference_rng and a point-cloud observation list, the CPU generator sees the reference's draw order
+    (ADVICE round 2): the clouds' torch.randperm of ConfigurableVecTask.__init__'s post_step
+    (configurable_vec_task.py:43-44, multi_object.py:806) before any drop draw, every drop's position / rotation
+    draws (multi_object_manipulation.py:107-110), one randperm after each initial pose's settle (:149-150), and
+    only then the first reset_idx draws (:62-91). The draws go through the recorded wrappers unchanged."""
+    need_gpu()
+    from handarm_hip import ref_rng as RR
+    from handarm_hip.tasks import Ur5SihMultiObjectManipulation
+    seq = []
+    real_perm, real_drop, real_reset = torch.randperm, RR.ur5sih_drop_pose, RR.ur5sih_reset_draws
+
+    def perm(*a, **k):
+        if "device" not in k and "generator" not in k:
+            seq.append("perm")
+        return real_perm(*a, **k)
+
+    def drop(n, *a, **k):
+        seq.append("drop")
+        return real_drop(n, *a, **k)
+
+    def reset(*a, **k):
+        seq.append("reset")
+        return real_reset(*a, **k)
+
+    monkeypatch.setattr(torch, "randperm", perm)
+    monkeypatch.setattr(RR, "ur5sih_drop_pose", drop)
+    monkeypatch.setattr(RR, "ur5sih_reset_draws", reset)
+    P, N = 2, 16
+    obs = ["goal_pos", "ur5_flange_pose", "dof_position_targets", "object_synthetic_pointcloud",
+           "ur5sih_synthetic_pointcloud", "goal_synthetic_pointcloud"]
+    torch.manual_seed(5)
+    env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": N, "observations": obs}, "sim": {"reference_rng": True},
+                                         "objects": {"drop": {"num_initial_poses": P}}}, "cuda:0", "cuda:0")
+    env.reset()
+    env.step(torch.zeros((N, env.num_acts), device="cuda:0"))
+    first_reset = seq.index("reset")
+    head = seq[:first_reset]
+    assert head[0] == "perm" and head[-1] == "perm" and head.count("perm") == P + 1, head
+    # each pose's drop draws form one run between two randperms
+    runs = "".join("p" if x == "perm" else "d" for x in head).split("p")[1:-1]
+    assert len(runs) == P and all(len(r) >= env.num_objects for r in runs), head
