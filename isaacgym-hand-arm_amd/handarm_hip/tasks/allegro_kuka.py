@@ -18,6 +18,7 @@ import torch
 from .. import model as HM
 from .. import _lib
 from .. import ref_rng as RR
+from .. import state_files as SF
 from ..sim import HandArmSim
 from .ur5sih_multi_object_manipulation import Box
 
@@ -66,9 +67,9 @@ class AllegroKuka:
             raise NotImplementedError("observationType 'full_state' and objectType 'block' (the AllegroKuka.yaml "
                                       "values) are implemented")
         if env.get("useRelativeControl", False) or env.get("privilegedActions", False) or \
-                env.get("randomizeObjectDimensions", True) is False or env.get("loadInitialStates", False):
-            raise NotImplementedError("only the AllegroKuka.yaml defaults for relative control, privileged actions, "
-                                      "object dimensions and initial-state loading are implemented")
+                env.get("randomizeObjectDimensions", True) is False:
+            raise NotImplementedError("only the AllegroKuka.yaml defaults for relative control, privileged actions "
+                                      "and object dimensions are implemented")
         self.num_environments = int(env.get("numEnvs", 8192))
         self.num_agents = 1
         task_cfg = dict(task=HM.TASK_ALLEGRO_KUKA, subtask=sub, seed=int(cfg.get("seed", 42)))
@@ -141,6 +142,20 @@ class AllegroKuka:
         if self.reference_rng:
             self._rr = RR.KukaDraws(N, sub, tuple(self.tcfg["force_prob_range"]), float(self.tcfg["force_scale"]))
             self.random_force_prob.copy_(self._rr.prob.to(sim_device))
+        # state dump / replay (allegro_kuka_base.py:95-101,545-546): off in AllegroKuka.yaml. Either one moves the
+        # resets of a step into their own launch (ha_task_reset, then ha_task_step finds no reset flags), so the
+        # loaded states can be written in between, as reset_idx does before its set_*_tensor_indexed calls
+        self.save_states = bool(env.get("saveStates", False))
+        self.save_states_filename = env.get("saveStatesFile", "rootTensorsDofStates.bin")
+        self.should_load_initial_states = bool(env.get("loadInitialStates", False))
+        self.load_states_filename = env.get("loadStatesFile", "rootTensorsDofStates.bin")
+        self.initial_root_state_tensors = self.initial_dof_state_tensors = None
+        self.initial_state_idx = self.num_initial_states = 0
+        self._recorder = SF.EpisodeStateRecorder(N) if self.save_states else None
+        if self.should_load_initial_states:
+            self.initial_root_state_tensors, self.initial_dof_state_tensors = SF.read_state_file(
+                self.load_states_filename, device=sim_device)
+            self.num_initial_states = len(self.initial_root_state_tensors)
 
     def contact_stats(self, reset=False):
         """Contact-list diagnostics of the physics since the last reset (HandArmSim.contact_stats)."""
@@ -211,7 +226,16 @@ class AllegroKuka:
         torch.clamp(actions, -self.clip_actions, self.clip_actions, out=self.actions_buf)
         self.frame_since_restart += 1
         self._curriculum()
-        self.sim.task_step(self.sim_flags | self._reference_draws())
+        flags = self.sim_flags | self._reference_draws()
+        if self.save_states or self.should_load_initial_states:
+            env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()     # host read, only with state files on
+            if len(env_ids) > 0:
+                self.sim.task_reset(flags)
+                self._after_reset(env_ids)
+        self.sim.task_step(flags)
+        if self._recorder is not None:                                      # post_physics_step, :1445-1446
+            N = self.num_environments
+            self._recorder.accumulate(self.root_state_tensor.view(N, -1, 13), self.dof_state.view(N, -1, 2))
         if self.fresh_outputs:
             out = torch.empty_like(self._obs_out[0])
             sc = torch.empty_like(self._scalars[0])
@@ -243,7 +267,31 @@ class AllegroKuka:
     def reset_idx(self, env_ids):
         """reset_idx (allegro_kuka_base.py:1246-1353) for the listed envs."""
         self.reset_buf[env_ids] = 1
+        if self.save_states or self.should_load_initial_states:
+            env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()
         self.sim.task_reset(self.sim_flags | self._reference_draws(forces=False))
+        if self.save_states or self.should_load_initial_states:
+            self._after_reset(env_ids)
+
+    def _after_reset(self, env_ids):
+        """The end of reset_idx (allegro_kuka_base.py:1292-1312,1349-1350) for envs the reset launch just reset:
+        DOF states and the cube's root state from the loaded file, cycling through it (the targets keep the
+        randomised reset pose, as in the reference), then the dump of the envs' recorded episodes."""
+        N = self.num_environments
+        if self.should_load_initial_states:
+            n = len(env_ids)
+            if n > self.num_initial_states:
+                print(f"Not enough initial states to load {n}/{self.num_initial_states}...")
+            else:
+                if self.initial_state_idx + n > self.num_initial_states:
+                    self.initial_state_idx = 0
+                sl = slice(self.initial_state_idx, self.initial_state_idx + n)
+                a0 = self.sim.model.actor_object0
+                self.dof_state.view(N, -1, 2)[env_ids] = self.initial_dof_state_tensors[sl].clone()
+                self.root_state_tensor.view(N, -1, 13)[env_ids, a0] = self.initial_root_state_tensors[sl, a0].clone()
+                self.initial_state_idx += n
+        if self._recorder is not None:
+            SF.append_chunks(self.save_states_filename, self._recorder.dump(env_ids.tolist()))
 
     def _reference_draws(self, forces=True):
         """reference_rng: this step's draws on the host (one read of the reset flags), uploaded for
