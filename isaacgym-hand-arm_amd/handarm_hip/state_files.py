@@ -5,8 +5,8 @@ episode was sampled,
     u32 big-endian  number of states in the chunk
     u32 big-endian  length L1, then L1 bytes: torch.save of the root states  (k, num_actors, 13)
     u32 big-endian  length L2, then L2 bytes: torch.save of the DOF states   (k, num_dofs, 2)
-Chunks are appended (file mode "ab") on every reset_idx. Actor rows follow this build's actor layout
-(model.actor_object0 is the cube), as the reference's follow its own.
+Chunks are appended (file mode "ab") on every reset_idx. Actor rows follow the reference's per-env order
+(arm+hand, cube, table, goal; model.actor_object0 is the cube).
 
 Loading uses torch.load(weights_only=True): the payloads are plain tensors, so nothing in the file is executed.
 """
