@@ -249,3 +249,37 @@ def test_create_rejects_compound_pool_objects():
     model.pool_nhull[0] = 2
     h = C.c_void_p()
     assert lib.ha_create(C.byref(model), C.byref(params), 4, C.byref(h)) == -4      # HA_E_MODEL
+
+
+def test_kuka_friction_cone_on_the_gpu():
+    """The Coulomb-friction schedule of test_kuka_physics.py on the kernel: static friction holds a push at half
+    the limit, a push at 1.25 times it slides the cuboid with (1.25 - 1) mu g, upright; and the whole 68-call
+    trajectory stays bit-identical to the C oracle."""
+    from tests.test_kuka_physics import check_friction, friction_schedule
+    n = 24
+    sim, orc, st = _oracle_and_sim(n, 0, 0.0)
+    scales = get(sim, "object_scale").reshape(n, 1, 3)
+    root = st["root_state"].reshape(n, 4, 13)
+    root[:, 1, 7:13] = 0
+    root[:, 1, 3:7] = [0, 0, 0, 1]
+    root[:, 1, 0:2] = [0.13, -0.09]
+    root[:, 1, 2] = 0.53 + 0.025 * scales[:, 0, 2] + 0.002
+    for k in HM.STATE_FIELDS:
+        if k not in ("stats", "term_sums", "task_state", "task_scalars"):
+            put(sim, k, st[k])
+    mu, dt = sim.params.friction, sim.params.dt
+
+    def gpu_force(f):
+        sim.t["object_force"].view(n, -1, 3)[:, 0] = torch.from_numpy(f).cuda()
+
+    flat, rec = friction_schedule(n, scales, mu, dt, lambda: sim.simulate(1),
+                                  lambda: get(sim, "root_state").reshape(n, 4, 13),
+                                  lambda: sim.t["dof_state"].view(n, 23, 2), gpu_force)
+    check_friction(flat, rec, mu, dt)
+
+    def cpu_force(f):
+        st["object_force"].reshape(n, -1, 3)[:, 0] = f
+
+    friction_schedule(n, scales, mu, dt, lambda: orc.simulate(st, 1), lambda: st["root_state"].reshape(n, 4, 13),
+                      lambda: st["dof_state"].reshape(n, 23, 2), cpu_force)
+    scenes.assert_physics_bit_identical(sim, st, n, tag="kuka friction schedule")

@@ -73,3 +73,65 @@ def test_arm_and_hand_stay_stable_under_random_targets_and_forces():
     # PD drives (kp 40, kd 5) track the targets unless a contact or an effort limit holds a joint back
     assert np.median(np.abs(dof[..., 0] - st["sim_targets"])) < 0.05
     assert (root[:, 1, 2] > 0.0).all() and (root[:, 1, 2] < 1.5).all()
+
+
+def friction_schedule(n, scales, mu, dt, simulate, root, dof, force):
+    """Coulomb friction on the table (pyramid rows along x / y for a z contact normal, mu = combined friction):
+    cuboids rest upright, then flat ones (x extent >= 1.5 x height, so the friction torque cannot tip them) get a
+    horizontal push along -x at the centre of mass: half the friction limit for 30 calls, then 1.25 times it for
+    12 calls. simulate() runs one gym.simulate; root(), dof() are writable (n, 4, 13) / (n, 23, 2) views or
+    copies, force(f) sets this call's (n, 3) object force. Returns the flat-env mask and the recorded states."""
+    flat = scales[:, 0, 0] >= 1.5 * scales[:, 0, 2]
+    mass = 400.0 * 0.05 ** 3 * scales[:, 0].prod(-1)
+    limit = mu * mass * 9.81
+    rec = {}
+
+    def run(calls, push):
+        for _ in range(calls):
+            f = np.zeros((n, 3), np.float32)
+            f[flat, 0] = -push * limit[flat]
+            force(f)
+            dof()[..., 1] = 0                                      # the hand holds still, away from the table
+            simulate()
+
+    run(30, 0.0)
+    rec["settled"] = root().copy()
+    run(30, 0.5)
+    rec["held"] = root().copy()
+    run(8, 1.25)
+    rec["pushed"] = root().copy()
+    return flat, rec
+
+
+def check_friction(flat, rec, mu, dt):
+    s, h, p = rec["settled"][:, 1], rec["held"][:, 1], rec["pushed"][:, 1]
+    assert flat.sum() >= 5
+    # below the limit: static friction holds (no creep beyond 1 mm, at rest)
+    assert np.abs(h[:, 0:3] - s[:, 0:3]).max() < 1e-3
+    assert np.abs(h[:, 7:10]).max() < 5e-3
+    # above it: kinetic friction mu N opposes the push, so the cuboid gains (1.25 - 1) mu g per second
+    v_exp = -0.25 * mu * 9.81 * 8 * dt
+    np.testing.assert_allclose(p[flat, 7], v_exp, rtol=0.02)
+    assert np.abs(p[flat, 8]).max() < 0.05 * abs(v_exp)           # no sideways drift
+    assert np.abs(p[flat, 3:5]).max() < 0.05                      # slides upright, does not tip
+    assert np.abs(p[~flat, 7:10]).max() < 5e-3                    # unpushed cuboids stay at rest
+
+
+def test_friction_holds_below_and_slides_above_the_coulomb_limit():
+    n = 24
+    scene, model, params, st, scales, lo, up = setup(n)
+    root = st["root_state"].reshape(n, 4, 13)
+    root[:, 1, 7:13] = 0
+    root[:, 1, 3:7] = [0, 0, 0, 1]
+    root[:, 1, 0:2] = [0.13, -0.09]
+    root[:, 1, 2] = 0.53 + 0.025 * scales[:, 0, 2] + 0.002
+    orc = Oracle(model, params, n)
+
+    def force(f):
+        st["object_force"].reshape(n, -1, 3)[:, 0] = f
+
+    flat, rec = friction_schedule(n, scales, params.friction, params.dt, lambda: orc.simulate(st, 1),
+                                  lambda: st["root_state"].reshape(n, 4, 13),
+                                  lambda: st["dof_state"].reshape(n, 23, 2), force)
+    print("friction: pushed flat cuboids vx", rec["pushed"][flat, 1, 7].round(3).tolist())
+    check_friction(flat, rec, params.friction, params.dt)
