@@ -283,3 +283,26 @@ def test_kuka_friction_cone_on_the_gpu():
     friction_schedule(n, scales, mu, dt, lambda: orc.simulate(st, 1), lambda: st["root_state"].reshape(n, 4, 13),
                       lambda: st["dof_state"].reshape(n, 23, 2), cpu_force)
     scenes.assert_physics_bit_identical(sim, st, n, tag="kuka friction schedule")
+
+
+def test_kuka_dropped_cuboids_on_the_gpu():
+    """The drop schedule of test_kuka_physics.py on the kernel: bounded penetration at impact, no bounce, rest at
+    the contact slop, upright; bit-identical to the C oracle after the 60 calls."""
+    from tests.test_kuka_physics import check_drop, drop_schedule
+    n = 24
+    sim, orc, st = _oracle_and_sim(n, 0, 0.0)
+    scales = get(sim, "object_scale").reshape(n, 1, 3)
+    root = st["root_state"].reshape(n, 4, 13)
+    root[:, 1, 7:13] = 0
+    root[:, 1, 3:7] = [0, 0, 0, 1]
+    root[:, 1, 0:2] = [0.13, -0.09]
+    root[:, 1, 2] = 0.53 + 0.025 * scales[:, 0, 2] + 0.10
+    for k in HM.STATE_FIELDS:
+        if k not in ("stats", "term_sums", "task_state", "task_scalars"):
+            put(sim, k, st[k])
+    flat, zs = drop_schedule(n, scales, lambda: sim.simulate(1), lambda: get(sim, "root_state").reshape(n, 4, 13),
+                             lambda: sim.t["dof_state"].view(n, 23, 2))
+    check_drop(flat, zs, get(sim, "root_state").reshape(n, 4, 13), sim.params.contact_slop)
+    drop_schedule(n, scales, lambda: orc.simulate(st, 1), lambda: st["root_state"].reshape(n, 4, 13),
+                  lambda: st["dof_state"].reshape(n, 23, 2))
+    scenes.assert_physics_bit_identical(sim, st, n, tag="kuka drop schedule")

@@ -135,3 +135,46 @@ def test_friction_holds_below_and_slides_above_the_coulomb_limit():
                                   lambda: st["dof_state"].reshape(n, 23, 2), force)
     print("friction: pushed flat cuboids vx", rec["pushed"][flat, 1, 7].round(3).tolist())
     check_friction(flat, rec, params.friction, params.dt)
+
+
+def drop_schedule(n, scales, simulate, root, dof, calls=60, height=0.10):
+    """Flat cuboids (as in friction_schedule) dropped from `height` above their resting height onto the table;
+    returns the flat mask and z - z_rest of every env after every call."""
+    flat = scales[:, 0, 0] >= 1.5 * scales[:, 0, 2]
+    zs = []
+    for _ in range(calls):
+        dof()[..., 1] = 0
+        simulate()
+        zs.append(root()[:, 1, 2] - (0.53 + 0.025 * scales[:, 0, 2]))
+    return flat, np.array(zs)
+
+
+def check_drop(flat, zs, root_final, slop):
+    z = zs[:, flat]
+    impact = np.argmax(z < slop, axis=0)
+    assert (impact > 0).all() and (impact < 20).all()
+    # penetration peaks at the impact call (1.4 m/s): measured 3.6 mm on this build; it is worked off to the
+    # contact slop (the depth the position correction leaves alone) and the cuboid does not bounce back up
+    assert -z.min() < 5e-3
+    for e in range(z.shape[1]):
+        assert z[impact[e] + 1:, e].max() < 0.5 * slop
+    np.testing.assert_allclose(z[-10:], -slop, atol=0.2 * slop)
+    assert np.abs(root_final[flat, 1, 7:10]).max() < 5e-3             # at rest
+    assert np.abs(root_final[flat, 1, 10:13]).max() < 5e-2            # residual rocking (measured 0.023 rad/s)
+    # upright to within the slop across the base (measured tilt <= 0.85 deg: quat x, y <= 0.0074)
+    assert np.abs(root_final[flat, 1, 3:5]).max() < 1e-2
+
+
+def test_dropped_cuboids_penetrate_boundedly_and_come_to_rest_at_the_slop():
+    n = 24
+    scene, model, params, st, scales, lo, up = setup(n)
+    root = st["root_state"].reshape(n, 4, 13)
+    root[:, 1, 7:13] = 0
+    root[:, 1, 3:7] = [0, 0, 0, 1]
+    root[:, 1, 0:2] = [0.13, -0.09]
+    root[:, 1, 2] = 0.53 + 0.025 * scales[:, 0, 2] + 0.10
+    orc = Oracle(model, params, n)
+    flat, zs = drop_schedule(n, scales, lambda: orc.simulate(st, 1), lambda: st["root_state"].reshape(n, 4, 13),
+                             lambda: st["dof_state"].reshape(n, 23, 2))
+    print("drop: peak penetration %.2f mm, final %.3f mm" % (-zs[:, flat].min() * 1e3, zs[-1, flat].mean() * 1e3))
+    check_drop(flat, zs, root, params.contact_slop)
