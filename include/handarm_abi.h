@@ -179,9 +179,10 @@ typedef struct ha_model_t {
     uint32_t edges[HA_MAX_EDGES];
     int32_t plane_loop[HA_MAX_PLANES];
     uint8_t loop_v[HA_MAX_LOOP];
-    /* v10: joint (Coulomb) friction per DOF, a PGS row with |impulse| <= dof_friction h (Isaac Gym DOF property
-     * "friction": AllegroHand 0.01, allegro_hand.py:267; AllegroKuka the URDF's <dynamics friction>,
-     * AllegroKuka.yaml:58 dofFriction -1; Ur5Sih 0 from its URDF) */
+    /* v10: joint friction coefficient per DOF (Isaac Gym DOF property "friction", a coefficient: the friction force is
+     * the DOF force times it, docs/domain_randomization.md:197): a PGS row with target velocity 0 and
+     * |impulse| <= dof_friction |drive + limit impulse of the DOF| (AllegroHand 0.01, allegro_hand.py:267; AllegroKuka
+     * the URDF's <dynamics friction>, AllegroKuka.yaml:58 dofFriction -1; Ur5Sih 0 from its URDF) */
     float dof_friction[HA_MAX_DOFS];
 } ha_model_t;
 
@@ -454,8 +455,8 @@ int ha_contact_capacity(ha_handle h);
  * simulates (kept by pointer: the caller keeps it alive), or NULL for the identity. Envs expected to take longest
  * first shortens a multi-round launch's tail (longest-processing-time order; handarm_hip/sim.py rebalance). */
 int ha_set_env_order(ha_handle h, const int32_t* order, int32_t n);
-/* last kernel time in ms measured with HIP events around the most recent timed physics/step launch (-1 if none;
- * launches record events only while ha_enable_kernel_timing is on) */
+/* time in ms of the most recent physics/step launch, from its HIP events; -1 when that launch was not timed (timing
+ * off, or the ha_enable_kernel_timing record buffer full) or none ran */
 float ha_last_kernel_ms(ha_handle h);
 /* per-launch HIP-event timing of the env kernel (bench roofline): record up to max_launches launches
  * (0 disables); ha_kernel_times synchronises and returns the recorded durations in ms */

@@ -34,11 +34,12 @@ HD float ah_draw(const SimCtx& c, const ha_state_t& st, int env, uint32_t flags,
 // torch_jit_utils.py:118-123 quat_from_angle_axis with a unit axis, then quat_unit
 HD void ah_quat_from_angle_axis(float angle, int axis, float* q) {
     float th = angle / 2.0f;
-    float sn = sinf(th);
+    float sn, cs;
+    ha_sincosf(th, &sn, &cs);           // the shared sine / cosine (include/ha_fmath.h, oracle/f32.py sincos)
     q[0] = axis == 0 ? sn : 0.0f * sn;
     q[1] = axis == 1 ? sn : 0.0f * sn;
     q[2] = axis == 2 ? sn : 0.0f * sn;
-    q[3] = cosf(th);
+    q[3] = cs;
     float n = sqrtf(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]);
     n = fmaxf(n, 1e-9f);
 #pragma unroll

@@ -75,10 +75,15 @@ HD float ak_norm3(const float* v) { return sqrtf((v[0] * v[0] + v[1] * v[1]) + v
 HD void ak_random_quat(float u0, float u1, float u2, float* q) {
     const float TWO_PI = 6.283185307179586f;      // 2 * np.pi, rounded by the tensor multiply
     float a = sqrtf(1.0f - u0), b = sqrtf(u0);
-    q[3] = a * sinf(TWO_PI * u1);
-    q[0] = a * cosf(TWO_PI * u1);
-    q[1] = b * sinf(TWO_PI * u2);
-    q[2] = b * cosf(TWO_PI * u2);
+    // the shared sine / cosine (include/ha_fmath.h), so the oracle chain of the fused step reproduces the reset
+    // pose bit for bit (oracle/f32.py sincos)
+    float s1, c1, s2, c2;
+    ha_sincosf(TWO_PI * u1, &s1, &c1);
+    ha_sincosf(TWO_PI * u2, &s2, &c2);
+    q[3] = a * s1;
+    q[0] = a * c1;
+    q[1] = b * s2;
+    q[2] = b * c2;
 }
 
 // reset_object_pose for this env (draw base k0: position noise [k0, k0+3), quat uvw [k0+3, k0+6)).

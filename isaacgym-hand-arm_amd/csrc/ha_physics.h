@@ -1889,10 +1889,14 @@ HD void substep(SimCtx& c, float hdt) {
     //      lower/upper joint limits (hard, unilateral)
     float dgam = 0.f, dbias = 0.f, dwinv = 0.f, dlim = 0.f, dlam = 0.f;
     float lwinv = 0.f, vt_lo = 0.f, vt_up = 0.f, lam_lo = 0.f, lam_up = 0.f;
-    float flim = 0.f, lam_fr = 0.f;     // joint friction row (v10): |impulse| <= dof_friction h, target velocity 0
+    // joint friction row (Isaac Gym DOF property "friction", a coefficient: "a generalized friction force is calculated
+    // as DOF force multiplied by friction", docs/domain_randomization.md:197): target velocity 0 and
+    // |impulse| <= dof_friction |drive + lower - upper impulse| of the DOF, re-bounded each sweep like a contact's
+    // friction rows by its normal impulse
+    float fcoef = 0.f, lam_fr = 0.f;
     int act_lo = 0, act_up = 0;
     if (lane < D) {
-        flim = m.dof_friction[lane] * hdt;
+        fcoef = m.dof_friction[lane];
         float kp = m.dof_kp[lane], kd = m.dof_kd[lane];
         float den = kd + hdt * kp;
         float mii = c.Minv[lane * D + lane];
@@ -1907,7 +1911,7 @@ HD void substep(SimCtx& c, float hdt) {
         vt_lo = s_lo > 0 ? -s_lo / hdt : -p.baumgarte * s_lo / hdt;
         vt_up = s_up > 0 ? -s_up / hdt : -p.baumgarte * s_up / hdt;
     }
-    const uint64_t lo_mask = __ballot(act_lo != 0), up_mask = __ballot(act_up != 0), fr_mask = __ballot(flim > 0.0f);
+    const uint64_t lo_mask = __ballot(act_lo != 0), up_mask = __ballot(act_up != 0), fr_mask = __ballot(fcoef > 0.0f);
     // generalized velocity: coordinate `lane` in vreg, coordinate 64 + lane in vregh (VW == 2 only)
     float vreg = lane < NV ? s.v[lane] : 0.0f;
     float vregh = (VW == 2 && lane + 64 < NV) ? s.v[lane + 64] : 0.0f;
@@ -1953,6 +1957,7 @@ HD void substep(SimCtx& c, float hdt) {
                 }
             }
             if ((fr_mask >> d) & 1ull) {
+                float flim = fcoef * fabsf((dlam + lam_lo) - lam_up);
                 float nf = lam_fr - vreg * lwinv;
                 nf = nf < -flim ? -flim : (nf > flim ? flim : nf);
                 float df = bcast(nf - lam_fr, d);

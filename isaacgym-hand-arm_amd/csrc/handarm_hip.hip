@@ -799,9 +799,22 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
         if (model->hull_nedges[k] < 0 || model->hull_nedges[k] > 4 * col_v || model->hull_nplanes[k] > 256 ||
             model->hull_edge_start[k] < 0 || model->hull_edge_start[k] + model->hull_nedges[k] > HA_MAX_EDGES)
             return HA_E_MODEL;
-        for (int j = 0; j < model->hull_nplanes[k]; j++) {
+        // the topology records index the hull's LDS vertex / plane scratch directly: every index must be in range
+        int nv = model->hull_nverts[k], np_ = model->hull_nplanes[k];
+        if (model->hull_vert_start[k] < 0 || model->hull_vert_start[k] + nv > HA_MAX_VERTS ||
+            model->hull_plane_start[k] < 0 || model->hull_plane_start[k] + np_ > HA_MAX_PLANES)
+            return HA_E_MODEL;
+        for (int j = 0; j < np_; j++) {
             int pl = model->plane_loop[model->hull_plane_start[k] + j];
             if ((pl >> 16) < 3 || (pl >> 16) > HA_MAX_FACE_LOOP || (pl & 0xFFFF) + (pl >> 16) > HA_MAX_LOOP)
+                return HA_E_MODEL;
+            for (int t = 0; t < (pl >> 16); t++)
+                if (model->loop_v[(pl & 0xFFFF) + t] >= nv) return HA_E_MODEL;
+        }
+        for (int j = 0; j < model->hull_nedges[k]; j++) {
+            uint32_t e = model->edges[model->hull_edge_start[k] + j];
+            if ((int)(e & 255u) >= nv || (int)((e >> 8) & 255u) >= nv || (int)((e >> 16) & 255u) >= np_ ||
+                (int)(e >> 24) >= np_)
                 return HA_E_MODEL;
         }
     }
@@ -879,8 +892,8 @@ static int launch(ha_handle h, int mode, int n_calls, uint32_t flags, int slot, 
     if (rec) {
         (void)hipEventRecord(h->t_ev[2 * h->t_count + 1], s);
         h->t_count++;
-        h->timed = 1;
     }
+    h->timed = rec ? 1 : 0;         // ha_last_kernel_ms: -1 for an untimed launch instead of an older launch's time
     return HA_OK;
 }
 

@@ -27,7 +27,7 @@ TORCH_DTYPE = {"float32": torch.float32, "int64": torch.int64, "uint8": torch.ui
 
 class HandArmSim:
     def __init__(self, num_envs, device="cuda:0", task_cfg=None, scene=None, pool_names=None, stats_ring=64,
-                 task=None, rebalance_every=4):
+                 task=None, rebalance_every=None):
         if not str(device).startswith("cuda"):
             raise _lib.HandArmError("libhandarm_hip runs on a HIP device only (device must be 'cuda:N')")
         self.lib = _lib.load()
@@ -78,7 +78,10 @@ class HandArmSim:
         _lib.check(self.lib.ha_bind_state(self.h, C.byref(self.state)), "ha_bind_state")
         _lib.check(self.lib.ha_set_stats_ring(self.h, stats_ring), "ha_set_stats_ring")
         # longest-first dispatch order of the fused step (ha_set_env_order), refreshed every `rebalance_every` steps
-        self.rebalance_every = int(os.environ.get("HA_REBALANCE", rebalance_every))
+        # (0: identity order). An explicit argument wins; HA_REBALANCE (A/B scripts) only replaces the default 4
+        if rebalance_every is None:
+            rebalance_every = int(os.environ.get("HA_REBALANCE", 4))
+        self.rebalance_every = int(rebalance_every)
         self._rb_count = 0
         if self.rebalance_every > 0:
             self._env_order = torch.arange(num_envs, dtype=torch.int32, device=self.device)

@@ -7,7 +7,8 @@ operation order.
 """
 import numpy as np
 
-from oracle.task_oracle import F, quat_conjugate, quat_mul, randomize_rotation, scale, unscale
+from oracle import f32
+from oracle.task_oracle import F, quat_conjugate, quat_mul, scale, unscale
 
 NUM_OBS, NUM_ACT, D = 88, 16, 16
 DRAW_GOAL, DRAW_RESET, DRAW_RESET_GOAL = 0, 4, 41       # ah_task.h AH_DRAW_*
@@ -19,6 +20,25 @@ CFG = dict(dist_reward_scale=-10.0, rot_reward_scale=1.0, rot_eps=0.1, action_pe
            reset_dof_vel_noise=0.0, act_moving_average=1.0,
            object_init=(0.0, -0.2, 0.56, 0.0, 0.0, 0.0, 1.0), goal_init=(0.0, -0.2, 0.52),
            goal_displacement=(-0.2, -0.06, 0.12))
+
+
+def _quat_from_angle_axis(angle, axis):
+    """torch_jit_utils.py:118-123 for a unit axis (0: x, 1: y), as ah_task.h ah_quat_from_angle_axis evaluates it:
+    the shared float32 sine / cosine (oracle/f32.py, include/ha_fmath.h), then quat_unit."""
+    th = np.asarray(angle, F) / F(2.0)
+    sn, cs = f32.sincos(th)
+    z = F(0.0) * sn
+    q = [sn if axis == 0 else z, sn if axis == 1 else z, z, cs]
+    n = np.sqrt(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]).astype(F)
+    n = np.maximum(n, F(1e-9))
+    return np.stack([c / n for c in q], -1).astype(F)
+
+
+def randomize_rotation(rand0, rand1):
+    """allegro_hand.py:722-725 (x, then y unit axis; quat_mul of torch_jit_utils.py:41-62)."""
+    pi = F(np.pi)
+    return quat_mul(_quat_from_angle_axis(np.asarray(rand0, F) * pi, 0),
+                    _quat_from_angle_axis(np.asarray(rand1, F) * pi, 1))
 
 
 def observations(dof_pos, dof_vel, dof_force, obj, goal_state, actions, lo, up, c=CFG):

@@ -9,6 +9,7 @@ task tensors travel in the device's ``task_state`` row layout (handarm_hip.model
 import numpy as np
 
 from handarm_hip import model as HM
+from oracle import f32
 
 F = np.float32
 D, NARM = 23, 7
@@ -38,8 +39,9 @@ def random_quat(u):
     """get_random_quat (allegro_kuka_base.py:1178-1189) from uvw draws (n, 3)."""
     two_pi = F(2 * np.pi)
     a, b = np.sqrt(F(1.0) - u[:, 0]), np.sqrt(u[:, 0])
-    return np.stack([a * np.cos(two_pi * u[:, 1]), b * np.sin(two_pi * u[:, 2]), b * np.cos(two_pi * u[:, 2]),
-                     a * np.sin(two_pi * u[:, 1])], 1).astype(F)
+    s1, c1 = f32.sincos(two_pi * u[:, 1])       # the kernels' shared sine / cosine (include/ha_fmath.h)
+    s2, c2 = f32.sincos(two_pi * u[:, 2])
+    return np.stack([a * c1, b * s2, b * c2, a * s1], 1).astype(F)
 
 
 def post(p, ts, dof_pos, dof_vel, rb, obj, goal, progress, successes, reset_buf, scale, scalars, lo, up, obs_only=False):

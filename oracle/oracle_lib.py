@@ -29,7 +29,16 @@ def load():
     lib.hao_struct_sizes.argtypes = [C.POINTER(C.c_int32)] * 3
     lib.hao_contacts.restype = C.c_int
     lib.hao_contacts.argtypes = [C.c_void_p, C.POINTER(HM.HaState), C.c_int, C.c_void_p, C.c_int]
+    lib.hao_sincos.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
     return lib
+
+
+def sincos(x):
+    """include/ha_fmath.h ha_sincosf over a float32 array, as compiled into the C oracle."""
+    x = np.ascontiguousarray(x, np.float32)
+    s, c = np.empty_like(x), np.empty_like(x)
+    load().hao_sincos(x.ctypes.data, x.size, s.ctypes.data, c.ctypes.data)
+    return s, c
 
 
 class HostState:

@@ -896,7 +896,9 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
      * |lambda| <= effort h) and the hard lower/upper limits (active within joint_limit_margin) */
     float dgam[HA_MAX_DOFS], dbias[HA_MAX_DOFS], dwinv[HA_MAX_DOFS], dlim[HA_MAX_DOFS], dlam[HA_MAX_DOFS];
     float lwinv[HA_MAX_DOFS], vt_lo[HA_MAX_DOFS], vt_up[HA_MAX_DOFS], lam_lo[HA_MAX_DOFS], lam_up[HA_MAX_DOFS];
-    float flim[HA_MAX_DOFS], lam_fr[HA_MAX_DOFS];     /* joint friction row (v10): |impulse| <= dof_friction h */
+    /* joint friction row: |impulse| <= dof_friction |drive + lower - upper impulse| (a coefficient, Isaac Gym's DOF
+     * "friction", docs/domain_randomization.md:197), re-bounded each sweep (ha_physics.h) */
+    float fcoef[HA_MAX_DOFS], lam_fr[HA_MAX_DOFS];
     int act_lo[HA_MAX_DOFS], act_up[HA_MAX_DOFS];
     for (int d = 0; d < D; d++) {
         float kp = m->dof_kp[d], kd = m->dof_kd[d];
@@ -914,7 +916,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
         vt_lo[d] = s_lo > 0 ? -s_lo / hdt : -p->baumgarte * s_lo / hdt;
         vt_up[d] = s_up > 0 ? -s_up / hdt : -p->baumgarte * s_up / hdt;
         lam_lo[d] = lam_up[d] = 0.0f;
-        flim[d] = m->dof_friction[d] * hdt;
+        fcoef[d] = m->dof_friction[d];
         lam_fr[d] = 0.0f;
     }
     /* projected Gauss-Seidel, velocity form: joint rows d = 0..D-1 (drive, lower, upper), then the
@@ -947,9 +949,10 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
                     for (int k = 0; k < D; k++) v[k] = fmaf(-mrow[k], d1, v[k]);
                 }
             }
-            if (flim[d] > 0.0f) {
+            if (fcoef[d] > 0.0f) {
+                float flim = fcoef[d] * fabsf((dlam[d] + lam_lo[d]) - lam_up[d]);
                 float nf = lam_fr[d] - v[d] * lwinv[d];
-                nf = nf < -flim[d] ? -flim[d] : (nf > flim[d] ? flim[d] : nf);
+                nf = nf < -flim ? -flim : (nf > flim ? flim : nf);
                 float df = nf - lam_fr[d];
                 if (df != 0.0f) {
                     lam_fr[d] = nf;
@@ -1199,4 +1202,10 @@ void hao_controller(hao_handle h, ha_state_t* S, int env) {
     tgt[D_LF] = tgt[D_RING];
     tgt[D_LF_DISTAL] = tgt[D_RF_DISTAL];
     for (int d = 0; d < h->D; d++) S->sim_targets[env * h->D + d] = tgt[d];
+}
+
+/* test helper: the shared float32 sine / cosine (include/ha_fmath.h) over an array, for the numpy port in
+   oracle/f32.py */
+void hao_sincos(const float* x, int n, float* s, float* c) {
+    for (int i = 0; i < n; i++) ha_sincosf(x[i], &s[i], &c[i]);
 }

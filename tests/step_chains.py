@@ -1,0 +1,189 @@
+"""Oracle chains of the fused step kernels (test infrastructure).
+
+One ``VecTask.step()`` of each task family, restated on the host from the oracles, in the order the fused step
+kernel runs it (``csrc/handarm_hip.hip`` env_body, MODE_STEP):
+
+* AllegroKuka (``ak_step_kernel``, allegro_kuka_base.py:1355-1447): numpy ``pre_physics_step``
+  (oracle/kuka_oracle.pre: goal / env resets from replayed draws, targets, random forces), the local-space
+  force rotated to world by the object's pose, ``control_freq_inv`` gym.simulate calls of the C oracle,
+  progress + 1, numpy ``compute_observations`` + ``compute_kuka_reward`` (kuka_oracle.post).
+* AllegroHand (``ah_step_kernel``, allegro_hand.py:586-629,663-719): goal / env resets, absolute targets,
+  C-oracle physics, progress + 1, ``compute_full_state`` (with the physics' joint forces) and the reward.
+* Ur5Sih, 3 objects with DR rows (``ha_step_kernel``, configurable_vec_task.py:347-414) and the 8-object clutter
+  family (``hb_step_kernel``): the C oracle's controller, reset_idx for reset envs (replayed draws, DR rows from
+  the device-mode hash), reset_idx's extra gym.simulate, the ``control_freq_inv`` calls, the observables, the
+  DR observation noise, reward and done.
+
+Each chain mutates an ``oracle.oracle_lib.HostState`` in place. Only tests import this module.
+"""
+import numpy as np
+
+from handarm_hip import model as HM
+from oracle import f32
+from oracle import allegro_oracle as AO
+from oracle import kuka_oracle as KO
+from oracle import task_oracle as TO
+
+F = np.float32
+
+
+# ----------------------------------------------------------------------------- AllegroKuka
+def kuka_step(orc, hs, p, lo, up, scalars, draws):
+    """ak_step_kernel on hs (HostState of the Kuka layout). Returns (obs, rew, timeout)."""
+    N, D = hs.num_envs, 23
+    A = orc.model.n_actors
+    st = dict(dof=hs["dof_state"].reshape(N, D, 2), root=hs["root_state"].reshape(N, A, 13), goal=hs["goal_state"],
+              targets=hs["dof_position_targets"], reset=hs["reset_buf"], reset_goal=hs["reset_goal_buf"],
+              progress=hs["progress_buf"], successes=hs["successes"], ts=hs["task_state"])
+    KO.pre(p, st, hs["actions"], draws, lo, up)
+    hs["sim_targets"][:] = hs["dof_position_targets"]
+    # apply_rigid_body_force_tensors(LOCAL_SPACE) at the object COM: world force = R(q_object) F_local (ak_forces)
+    a0 = orc.model.actor_object0
+    fl = hs["task_state"][:, HM.AK_RB_FORCE:HM.AK_RB_FORCE + 3]
+    fw = f32.qrot(st["root"][:, a0, 3:7], fl) if p.ak_force_scale > 0 else np.zeros((N, 3), F)
+    hs["object_force"].reshape(N, 3)[:] = fw
+    orc.simulate(hs, p.control_freq_inv)
+    hs["progress_buf"][:] = hs["progress_buf"] + 1
+    rb = hs["rigid_body_state"].reshape(N, orc.model.n_bodies, 13)[:, orc.model.body_robot0:]
+    obs, rew, rs, rg, pr, sc = KO.post(p, hs["task_state"], st["dof"][..., 0], st["dof"][..., 1], rb, st["root"][:, a0],
+                                       hs["goal_state"], hs["progress_buf"], hs["successes"], hs["reset_buf"],
+                                       hs["object_scale"].reshape(N, 3), scalars, lo, up)
+    hs["reset_buf"][:], hs["reset_goal_buf"][:], hs["progress_buf"][:], hs["successes"][:] = rs, rg, pr, sc
+    hs["rew"][:] = rew
+    hs["obs"][:] = obs
+    return obs, rew, KO.timeout(p, pr, rs)
+
+
+# ----------------------------------------------------------------------------- AllegroHand
+def allegro_step(orc, hs, p, lo, up, draws):
+    """ah_step_kernel on hs (HostState of the AllegroHand layout). Returns (obs, rew, timeout, cons)."""
+    N, D = hs.num_envs, 16
+    c = dict(AO.CFG)
+    c["act_moving_average"] = float(p.ah_act_moving_average)
+    root = hs["root_state"].reshape(N, 3, 13)
+    dof = hs["dof_state"].reshape(N, D, 2)
+    for e in range(N):
+        goal, full = hs["reset_goal_buf"][e] != 0, hs["reset_buf"][e] != 0
+        if goal or full:
+            base = AO.DRAW_RESET_GOAL if full else AO.DRAW_GOAL
+            AO.goal_reset(hs["goal_state"], root, e, draws[e, base], draws[e, base + 1], c)
+            hs["reset_goal_buf"][e] = 0
+        if full:
+            AO.env_reset(root, dof[..., 0], dof[..., 1], hs["dof_position_targets"], e,
+                         draws[e, AO.DRAW_RESET:AO.DRAW_RESET + 37], lo, up, c)
+            hs["progress_buf"][e], hs["reset_buf"][e], hs["successes"][e] = 0, 0, 0
+    hs["dof_position_targets"][:] = AO.targets_from_actions(hs["actions"], hs["dof_position_targets"], lo, up, c)
+    hs["sim_targets"][:] = hs["dof_position_targets"]
+    orc.simulate(hs, p.control_freq_inv)
+    hs["progress_buf"][:] = hs["progress_buf"] + 1
+    obs = AO.observations(dof[..., 0], dof[..., 1], hs["dof_force"], root[:, 1], hs["goal_state"], hs["actions"], lo, up, c)
+    rew, rs, rg, pr, sc, cons = AO.reward(root[:, 1], hs["goal_state"], hs["actions"], hs["reset_buf"],
+                                          hs["reset_goal_buf"], hs["progress_buf"], hs["successes"],
+                                          hs["consecutive_successes"][0], c)
+    hs["reset_buf"][:], hs["reset_goal_buf"][:], hs["progress_buf"][:], hs["successes"][:] = rs, rg, pr, sc
+    hs["consecutive_successes"][0] = cons
+    hs["rew"][:] = rew
+    hs["obs"][:] = obs
+    timeout = (pr >= c["max_episode_length"] - 1) & (rs != 0)
+    return obs, rew, timeout, cons
+
+
+# ----------------------------------------------------------------------------- Ur5Sih (3 objects / clutter)
+def dr_sample_rows(p, env, episode):
+    """ha_task.h dr_sample for the listed envs: per-link / per-object mass scale U[lo, hi] and friction
+    friction x U[lo, hi] bucketed into dr_fric_buckets values (dr_utils.py:71-147 semantics), from the device-mode
+    counter hash (uniform01(seed, env, episode, 1000 + k)). float32, operation for operation."""
+    env = np.asarray(env, np.uint32)
+    episode = np.asarray(episode, np.uint32)
+    n = len(env)
+    rows = np.zeros((n, HM.DR_SIZE), F)
+    mlo, mhi, flo, fhi = F(p.dr_mass_lo), F(p.dr_mass_hi), F(p.dr_fric_lo), F(p.dr_fric_hi)
+    nb = int(p.dr_fric_buckets)
+
+    def u(k, lo, hi):
+        return (lo + (hi - lo) * f32.uniform01(p.seed, env, episode, 1000 + k)).astype(F)
+
+    def bucket(v):
+        w = fhi - flo
+        i = np.floor((v - flo) / w * F(nb)).astype(np.int64)
+        i = np.clip(i, 0, nb - 1)
+        return (w * i.astype(F) / F(nb) + flo).astype(F)
+
+    fr = F(p.friction)
+    for L in range(HM.MAX_LINKS):
+        rows[:, HM.DR_LINK_MASS + L] = u(L, mlo, mhi)
+        rows[:, HM.DR_LINK_FRIC + L] = bucket(fr * u(100 + L, flo, fhi))
+    for o in range(HM.MAX_OBJ):
+        rows[:, HM.DR_OBJ_MASS + o] = u(50 + o, mlo, mhi)
+        rows[:, HM.DR_OBJ_FRIC + o] = bucket(fr * u(150 + o, flo, fhi))
+    return rows
+
+
+def ur5sih_step(orc, hs, p, model, draws):
+    """ha_step_kernel / hb_step_kernel on hs (replayed reset draws: [0] configuration, [1] target object,
+    [2:5] goal noise). Returns (teacher_obs, obs, rew, timeout)."""
+    N, D, NO = hs.num_envs, 17, int(p.n_objects)
+    A, B = model.n_actors, model.n_bodies
+    a0 = model.actor_object0
+    actors = np.arange(a0, a0 + NO)
+    orc.controller(hs)
+    root = hs["root_state"].reshape(N, A, 13)
+    dof = hs["dof_state"].reshape(N, D, 2)
+    resets = np.nonzero(hs["reset_buf"])[0]
+    if len(resets):
+        cfgs = np.clip(draws[resets, 0].astype(np.int64), 0, int(p.num_initial_poses) - 1)
+        tgts = np.clip(draws[resets, 1].astype(np.int64), 0, NO - 1)
+        if p.dr_enable:
+            hs["dr_scale"][resets] = dr_sample_rows(p, resets, hs["episode"][resets])
+        for i, e in enumerate(resets):
+            cfg = cfgs[i]
+            pos0 = hs["object_pos_initial"][e, cfg]
+            quat0 = hs["object_quat_initial"][e, cfg]
+            root[e, actors, 0:3] = pos0
+            root[e, actors, 3:7] = quat0
+            root[e, actors, 7:13] = 0
+            g = np.array(p.goal_pos, F) + (F(2.0) * (draws[e, 2:5].astype(F) - F(0.5))) * np.array(p.goal_noise, F)
+            hs["goal_pos"][e] = g
+            root[e, model.actor_goal, 0:3] = g
+            hs["target_object_index"][e] = tgts[i]
+            hs["object_configuration_indices"][e] = cfg
+            hs["servo"][e] = np.array(p.servo_upper, F)
+            hs["smoothed"][e] = 0
+            rp = np.array(list(p.reset_pose)[:D], F)
+            dof[e, :, 0] = rp
+            dof[e, :, 1] = 0
+            hs["sim_targets"][e] = rp
+            tt = rp.copy()
+            tt[6:] = 0
+            hs["dof_position_targets"][e] = tt
+            orc.simulate(hs, 1, begin=int(e), end=int(e) + 1)       # reset_idx's gym.simulate
+            hs["ur5_target"][e] = dof[e, 0:6, 0]
+            hs["reset_buf"][e] = 0
+            hs["progress_buf"][e] = 0
+            hs["goal_reached_before"][e] = 0
+            hs["episode"][e] = hs["episode"][e] + 1
+    orc.simulate(hs, p.control_freq_inv)
+    body = hs["rigid_body_state"].reshape(N, B, 13)
+    pid = hs["object_indices"]
+    bb = lambda arr: np.array([[list(arr[i]) for i in row] for row in pid], F)       # noqa: E731
+    teacher, _ = TO.observations(root, body, dof, hs["dof_position_targets"], hs["goal_pos"], hs["target_object_index"],
+                                 bb(model.pool_bbox_pos), bb(model.pool_bbox_quat), bb(model.pool_bbox_ext),
+                                 hs["obs_cache"], object_actors=actors)
+    obs = teacher.copy()
+    if p.dr_enable:
+        nctr = (hs["episode"].astype(np.uint32) << np.uint32(12)) ^ hs["progress_buf"].astype(np.uint32)
+        cols = np.arange(teacher.shape[1])
+        noise = f32.gauss01(p.seed, np.arange(N, dtype=np.uint32)[:, None], nctr[:, None], cols[None, :])
+        obs = (teacher + F(p.dr_obs_noise) * noise).astype(F)
+    hs["obs_cache"][:] = root[:, actors, 0:7]
+    prog = hs["progress_buf"] + 1
+    hs["progress_buf"][:] = prog
+    rs = np.where(prog >= p.max_episode_length, 1, hs["reset_buf"]).astype(np.int64)
+    timeout = (prog >= p.max_episode_length - 1) & (rs != 0)
+    hs["reset_buf"][:] = rs
+    rew, reached, _ = TO.reward(root, body, hs["goal_pos"], hs["target_object_index"],
+                                hs["object_configuration_indices"], hs["object_pos_initial"], object_actors=actors)
+    hs["goal_reached_before"][:] = (hs["goal_reached_before"] != 0) | reached
+    hs["rew"][:] = rew
+    return teacher, obs, rew, timeout
+

@@ -29,10 +29,54 @@ def test_allegro_physics_is_stable_and_tracks_targets():
     err = np.abs(dof[..., 0] - st["sim_targets"])
     assert np.median(err) < 0.05, np.median(err)
     assert (dof[..., 0] >= lo - 0.05).all() and (dof[..., 0] <= up + 0.05).all()
-    # the cube never sinks through the ground plane and stays near the hand or on the ground
+    # the cube never sinks through the ground plane
     z = root[:, 1, 2]
     assert (z > 0.0325 - 0.01).all()
-    assert np.abs(root[:, 1, 0]).max() < 1.0        # a cube thrown off the hand tumbles on the ground, then rests
+
+
+def _cube_energy(model, root):
+    """mechanical energy of the cube: translational + rotational kinetic energy + potential energy (ground z = 0)."""
+    m = model.pool_mass[0]
+    I0 = np.array(list(model.pool_inertia[0]), np.float64).reshape(3, 3)
+    q = root[:, 1, 3:7].astype(np.float64)
+    x, y, zq, w = q.T
+    R = np.stack([np.stack([1 - 2 * (y * y + zq * zq), 2 * (x * y - zq * w), 2 * (x * zq + y * w)], -1),
+                  np.stack([2 * (x * y + zq * w), 1 - 2 * (x * x + zq * zq), 2 * (y * zq - x * w)], -1),
+                  np.stack([2 * (x * zq - y * w), 2 * (y * zq + x * w), 1 - 2 * (x * x + y * y)], -1)], 1)
+    om = root[:, 1, 10:13].astype(np.float64)
+    Iw = R @ I0 @ np.transpose(R, (0, 2, 1))
+    v = root[:, 1, 7:10].astype(np.float64)
+    return 0.5 * m * (v * v).sum(-1) + 0.5 * np.einsum("ni,nij,nj->n", om, Iw, om) + m * 9.81 * root[:, 1, 2]
+
+
+def test_allegro_cube_released_by_the_hand_gains_no_energy():
+    """The random scene starts with fingers interpenetrating the cube by up to 3.4 cm, and AllegroHand's
+    max_depenetration_velocity (1000, AllegroHand.yaml) lets the push-out throw it (up to ~1.6 m/s: env 7 flies 1.4 m).
+    That throw is the only energy source once the hand lets go: from the call on which no finger touches the cube,
+    its mechanical energy (kinetic + rotational + potential) never grows from one call to the next, through the fall,
+    the ground impacts (edge-edge and clipped-face contacts) and the tumbling, within 1% + 1e-4 J."""
+    n = 16
+    model, params, st, lo, up = setup(n)
+    orc = Oracle(model, params, n)
+    root = st["root_state"].reshape(n, 3, 13)
+    seps = np.array([orc.contacts(st, e)[:, 6].min(initial=0.0) for e in range(n)])
+    assert seps.min() < -0.02, "the scene starts with deep finger-cube interpenetration"
+    released = np.zeros(n, bool)
+    e_prev = _cube_energy(model, root)
+    checked = 0
+    for c in range(60):
+        touch = np.array([any(int(a) >= 100 or int(b) >= 100 for a, b in orc.contacts(st, e)[:, 7:9]) for e in range(n)])
+        released |= ~touch
+        orc.simulate(st, 1)
+        e_now = _cube_energy(model, root)
+        chk = released & ~touch
+        grow = e_now - e_prev
+        assert (grow[chk] <= 0.01 * e_prev[chk] + 1e-4).all(), (c, np.nonzero(chk & (grow > 0.01 * e_prev + 1e-4)))
+        checked += int(chk.sum())
+        e_prev = e_now
+    assert checked > 100 and released.sum() >= 4
+    z = root[:, 1, 2]
+    assert (z > 0.0325 - 0.01).all()
 
 
 def test_allegro_free_cube_falls_under_gravity():
