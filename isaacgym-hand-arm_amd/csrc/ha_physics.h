@@ -13,6 +13,8 @@
 // Everything loops at run time (small code: the kernel must stay resident in the instruction cache),
 // and the phase-local scratch (dynamics, collision, rows) shares one LDS union.
 #pragma once
+#include <type_traits>
+
 #include "ha_device.h"
 #include "../../include/handarm_abi.h"
 
@@ -174,14 +176,20 @@ __host__ __device__ inline size_t obj_lds_offset_rows(size_t rows) {
 #ifndef HA_SPLIT_ABOVE_OCAP
 #define HA_SPLIT_ABOVE_OCAP 2   /* families with more object slots use split rows (Ur5Sih 3 objects, clutter) */
 #endif
+//
+// Overflow chunks (OVF = true, the Ur5Sih and AllegroHand families): chunk 0 keeps the family's LDS layout (contact
+// entries, rows, the PGS row constants in registers), and chunks 1..NCH-1 keep their contact entries, constraint rows
+// and row constants in the env's global area (L2-resident), so the contact capacity grows without LDS. A substep
+// with <= CAP contacts never touches that area; a substep over CAP swaps every chunk's row constants through it.
 template <int ND, int OCAP, int NCH, int KL = 8, int LCH = NCH, int CAP = MAXC, int CV = 64, int CP = 128,
-          int SPLIT = -1, int NG = HA_MAX_GATHER, bool MU = false, bool RC = false>
+          int SPLIT = -1, int NG = HA_MAX_GATHER, bool MU = false, bool RC = false, bool OVF = false>
 struct PhysCfg {
     static constexpr int nd = ND, ocap = OCAP, nch = NCH;
     static constexpr int colv = CV, colp = CP, colg = NG;   // largest hull: vertices, face planes; gather points
     static constexpr size_t col_bytes = ColLayout<CV, CP, NG>::bytes;
-    // contacts per chunk: MAXC, or fewer for a one-chunk family (its rows and list shrink with it)
+    // contacts per chunk (MAXC, or fewer: the rows and the LDS list shrink with it)
     static constexpr int cap = CAP;
+    static constexpr bool ovf = OVF && NCH > 1;
     static constexpr int rpc = 3 * CAP;             // constraint rows per chunk
     static constexpr int vw = ND + 6 * OCAP > 64 ? 2 : 1;
 #ifdef HA_DENSE_ROWS    /* diagnostic build (tools/split_rows_check.py): every family on dense rows */
@@ -197,17 +205,26 @@ struct PhysCfg {
     static constexpr bool rc = RC && split;
     // split rows: the object blocks of chunks [0, lch) live in LDS, those of chunks [lch, nch) in the env's global
     // row area after the robot-block spill rows (written by the rows phase, read back by the PGS one contact ahead)
-    static constexpr int lch = split ? LCH : NCH;
+    // (OVF: chunk 0's rows in LDS, split or dense, the others in the global area)
+    static constexpr int lch = ovf ? 1 : (split ? LCH : NCH);
     static constexpr int spill_robot = split ? 2 * 3 * (CAP * NCH - KL) * ND : 0;   // per env: J then Y
     static constexpr int spill_obj = split && !rc ? 2 * rpc * (NCH - lch) * ow : 0;  // per env: J then Y
-    static constexpr int spill_floats = spill_robot + spill_obj;
+    // OVF global area after those: dense rows of chunks 1.. (J then Y), the row constants of every chunk (6 x rpc x
+    // NCH, the LDS RK layout), the contact entries of chunks 1.. (8 floats each)
+    static constexpr int spill_dense = ovf && !split ? 2 * rpc * (NCH - 1) * row_stride<ND>() : 0;
+    static constexpr int spill_rk = ovf ? 6 * rpc * NCH : 0;
+    static constexpr int spill_ct = ovf ? 8 * CAP * (NCH - 1) : 0;
+    static constexpr int off_dense = spill_robot + spill_obj, off_rk = off_dense + spill_dense,
+                         off_ct = off_rk + spill_rk;
+    static constexpr int spill_floats = off_ct + spill_ct;
     static_assert(ND + 6 * OCAP <= MAXV, "generalized velocity exceeds MAXV");
     static_assert(!split || (KL >= 0 && KL <= CAP * NCH), "LDS link slots must not exceed the contact capacity");
     static_assert(!split || CAP * NCH <= 128, "split rows: <= 128 contacts");
     static_assert(split || CAP * NCH <= 64, "dense rows: <= 64 contacts (one ballot)");
     static_assert(lch >= 0 && lch <= NCH, "LDS row chunks");
     static_assert(CAP * NCH <= HA_MAX_CONTACTS, "contact capacity exceeds HA_MAX_CONTACTS");
-    static_assert(CAP == MAXC || (NCH == 1 && CAP >= 1 && CAP < MAXC), "reduced capacity: one chunk");
+    static_assert(CAP >= 1 && CAP <= MAXC, "contacts per chunk");
+    static_assert(!ovf || !rc, "overflow chunks with recomputed object blocks");
     static_assert(NG == 0 || NG == HA_MAX_GATHER, "gather buffer: HA_MAX_GATHER points or none");
     static_assert(CP >= 8, "sat_planes reads plane slots 0..7 of the narrow-phase scratch");
 };
@@ -217,11 +234,11 @@ struct PhysCfg {
 template <class PC>
 __host__ __device__ constexpr size_t pc_rowdata_bytes() {
     return PC::split ? 2 * sizeof(float) * ((size_t)PC::rpc * PC::lch * PC::ow + 3 * (size_t)PC::kl * PC::nd)
-                     : 2 * sizeof(float) * (size_t)PC::rpc * PC::nch * row_stride<PC::nd>();
+                     : 2 * sizeof(float) * (size_t)PC::rpc * PC::lch * row_stride<PC::nd>();
 }
 template <class PC>
 __host__ __device__ constexpr size_t pc_rows_bytes() {
-    return pc_rowdata_bytes<PC>() + (PC::nch > 1 ? 6 * sizeof(float) * (size_t)MAXR * PC::nch : 0);
+    return pc_rowdata_bytes<PC>() + (PC::nch > 1 && !PC::ovf ? 6 * sizeof(float) * (size_t)PC::rpc * PC::nch : 0);
 }
 // S ~ M^-1 (factor_inverse), D x D at stride D, sized for the family's DOF count: at the end of the union
 // (minv_in_union) or after it
@@ -274,7 +291,7 @@ __host__ __device__ inline size_t contact_lds_offset() {
 }
 template <class PC>
 __host__ __device__ inline size_t task_lds_bytes() {
-    return contact_lds_offset<PC>() + (size_t)PC::cap * PC::nch * sizeof(ContactLDS);
+    return contact_lds_offset<PC>() + (size_t)PC::cap * (PC::ovf ? 1 : PC::nch) * sizeof(ContactLDS);
 }
 
 struct SimCtx {
@@ -282,7 +299,10 @@ struct SimCtx {
     const ha_params_t* __restrict__ p;
     EnvLDS* s;
     ObjLDS* o;              // the env's object slots (after the EnvLDS block, see task_lds_bytes)
-    ContactLDS* k;          // the env's contact list (after the object slots)
+    ContactLDS* k;          // the env's contact list (after the object slots): entries [0, kc0)
+    ContactLDS* kg;         // overflow chunks (PhysCfg OVF): entries [kc0, maxc) in the env's global area; null
+                            // otherwise (a constant the compiler folds: ct_global is then false)
+    int kc0;                // entries in LDS
     float* Minv;            // S ~ M^-1, D x D (after the phase union, see obj_lds_offset)
     ColView col;            // narrow-phase scratch of the family (col_view)
     int lane, D, NO, L;
@@ -301,6 +321,39 @@ struct SimCtx {
     bool dry;               // A/B timing builds only: a repeated phase that must not emit contacts
 #endif
 };
+
+// Contact entry ci of the list: LDS for [0, kc0), the env's global overflow entries after that (PhysCfg OVF). Read and
+// written by value: a pointer that may address either LDS or global memory would be a flat pointer, so each access
+// keeps its two address spaces on separate paths.
+HD bool ct_global(const SimCtx& c, int ci) { return c.kg != nullptr && ci >= c.kc0; }
+HD ContactLDS ct_get(const SimCtx& c, int ci) {
+    if (ct_global(c, ci)) return c.kg[ci - c.kc0];
+    return c.k[ci];
+}
+HD float ct_sep(const SimCtx& c, int ci) {
+    if (ct_global(c, ci)) return c.kg[ci - c.kc0].sep;
+    return c.k[ci].sep;
+}
+HD void ct_ab(const SimCtx& c, int ci, int& a, int& b) {
+    if (ct_global(c, ci)) {
+        a = c.kg[ci - c.kc0].a;
+        b = c.kg[ci - c.kc0].b;
+    } else {
+        a = c.k[ci].a;
+        b = c.k[ci].b;
+    }
+}
+HD void ct_fill(ContactLDS& ct, f3 x, f3 n, float sep, int a, int b) {
+    st3(ct.x, x);
+    st3(ct.n, n);
+    ct.sep = sep;
+    ct.a = (short)a;
+    ct.b = (short)b;
+}
+HD void ct_put(const SimCtx& c, int ci, f3 x, f3 n, float sep, int a, int b) {
+    if (ct_global(c, ci)) ct_fill(c.kg[ci - c.kc0], x, n, sep, a, b);
+    else ct_fill(c.k[ci], x, n, sep, a, b);
+}
 
 // friction of a contact body (link 100+L, object o, static -1) and of a contact (PhysX average combine)
 HD float body_friction(const SimCtx& c, int b) {
@@ -700,14 +753,7 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
             // the values lane 0 would write after broadcasting them (the chosen lanes are distinct)
             if (lane == 0) { s.noff += k; s.nc = nc0 + k; }
             int t = lane == i0 ? 0 : (k > 1 && lane == j1 ? 1 : (k > 2 && lane == j2 ? 2 : (k > 3 && lane == j3 ? 3 : -1)));
-            if (t >= 0) {
-                ContactLDS& ct = c.k[nc0 + t];
-                st3(ct.x, pt);
-                st3(ct.n, n);
-                ct.sep = sep;
-                ct.a = (short)a;
-                ct.b = (short)b;
-            }
+            if (t >= 0) ct_put(c, nc0 + t, pt, n, sep, a, b);
             wsync();
             return;
         }
@@ -758,10 +804,10 @@ HD void store_chosen(SimCtx& c, int k, const f3* P, const f3* N, const float* S,
         if (t >= k) break;
         int nc = s.nc, slot;
         if (nc >= c.maxc) {
-            float sv = lane < c.maxc ? c.k[lane].sep : -3.0e38f;
+            float sv = lane < c.maxc ? ct_sep(c, lane) : -3.0e38f;
             int w = lane;
             if (c.maxc > 64) {          // contacts 64.. in the same lanes; a tie keeps the lower index
-                float s2 = lane + 64 < c.maxc ? c.k[lane + 64].sep : -3.0e38f;
+                float s2 = lane + 64 < c.maxc ? ct_sep(c, lane + 64) : -3.0e38f;
                 if (s2 > sv) { sv = s2; w = lane + 64; }
             }
             wave_argmax(sv, w);
@@ -772,12 +818,7 @@ HD void store_chosen(SimCtx& c, int k, const f3* P, const f3* N, const float* S,
         }
         if (lane == 0) {
             if (slot == nc) s.nc = nc + 1;
-            ContactLDS& ct = c.k[slot];
-            st3(ct.x, P[t]);
-            st3(ct.n, N[t]);
-            ct.sep = S[t];
-            ct.a = (short)a;
-            ct.b = (short)b;
+            ct_put(c, slot, P[t], N[t], S[t], a, b);
         }
         wsync();
     }
@@ -1681,30 +1722,38 @@ HD void substep(SimCtx& c, float hdt) {
     }
     PROF_COUNT(8, s.nc);
     PROF_COUNT(9, 1);
-    // ---- contact rows: in chunk ch, lane r < MAXR owns global row MAXR ch + r (normal, friction 1, friction 2
-    //      of contact MAXC ch + r / 3). Rows are packed with the task's stride (J then Y), so a one-object task
-    //      needs less LDS (row_stride, task_lds_bytes)
+    // ---- contact rows: in chunk ch, lane r < RPC owns global row RPC ch + r (normal, friction 1, friction 2 of
+    //      contact CAP ch + r / 3). Rows are packed with the task's stride (J then Y), so a one-object task needs less
+    //      LDS (row_stride, task_lds_bytes)
+    constexpr int CAP = PC::cap, RPC = PC::rpc;
     float* Jb = s.u.rows.J;
-    float* Yb = Jb + 3 * PC::cap * NCH * RSN;
+    float* Yb = Jb + RPC * PC::lch * RSN;
     int nc = s.nc;
-    int nr = 3 * nc;    // nc <= MAXC x NCH -> <= MAXR x NCH rows
+    int nr = 3 * nc;    // nc <= CAP x NCH -> <= RPC x NCH rows
     // split rows (PhysCfg): object blocks of every row (OW wide, J then Y), then the robot blocks of the
     // first KL link contacts (J then Y), then the env's global spill area for the link contacts after those
-    constexpr int OW = PC::ow, KL = PC::kl, LCH = PC::lch, RPC = PC::rpc, SPJ = 3 * (PC::cap * NCH - KL) * ND;
+    constexpr int OW = PC::ow, KL = PC::kl, LCH = PC::lch, SPJ = 3 * (CAP * NCH - KL) * ND;
     float* Ob = Jb;
     float* ObY = Ob + RPC * LCH * OW;
     float* Rb = ObY + RPC * LCH * OW;
     float* RbY = Rb + 3 * KL * ND;
+    // overflow chunks (PhysCfg OVF): dense rows of chunks 1.. in the env's global area (J, then Y)
+    float* gJ = PC::ovf ? c.spill + PC::off_dense : nullptr;
+    float* gY = PC::ovf ? gJ + RPC * (NCH - 1) * RSN : nullptr;
     // contacts that touch a robot link (split rows only): contacts 0..63 in lmask0, 64.. in lmask1
     uint64_t lmask0 = 0, lmask1 = 0;
     if constexpr (PC::split) {
-        lmask0 = __ballot(lane < nc && (c.k[lane].a >= 100 || c.k[lane].b >= 100));
-        if constexpr (MAXC * NCH > 64)
-            lmask1 = __ballot(lane + 64 < nc && (c.k[lane + 64].a >= 100 || c.k[lane + 64].b >= 100));
+        int a0 = 0, b0 = 0, a1 = 0, b1 = 0;
+        if (lane < nc) ct_ab(c, lane, a0, b0);
+        lmask0 = __ballot(lane < nc && (a0 >= 100 || b0 >= 100));
+        if constexpr (CAP * NCH > 64) {
+            if (lane + 64 < nc) ct_ab(c, lane + 64, a1, b1);
+            lmask1 = __ballot(lane + 64 < nc && (a1 >= 100 || b1 >= 100));
+        }
     }
     // robot-block slot of contact ci (-1: no link), and row k of its J or Y robot block
     auto lslot = [&](int ci) -> int {
-        if (MAXC * NCH <= 64 || ci < 64)
+        if (CAP * NCH <= 64 || ci < 64)
             return ((lmask0 >> ci) & 1ull) ? (int)__popcll(lmask0 & ((1ull << ci) - 1ull)) : -1;
         int cj = ci - 64;
         return ((lmask1 >> cj) & 1ull) ? (int)(__popcll(lmask0) + __popcll(lmask1 & ((1ull << cj) - 1ull))) : -1;
@@ -1713,23 +1762,29 @@ HD void substep(SimCtx& c, float hdt) {
         if (ls < KL) return (y ? RbY : Rb) + (3 * ls + k) * ND;
         return c.spill + (y ? SPJ : 0) + (3 * (ls - KL) + k) * ND;
     };
-    // object blocks (J or Y) of row r: LDS for the first LCH chunks, else the env's global row area
-    auto orow = [&](int r, bool y) -> float* {
-        if (LCH == NCH || r < RPC * LCH) return (y ? ObY : Ob) + r * OW;   // every chunk in LDS: no global path
+    // object blocks (J or Y) of row r in the env's global row area (chunks LCH..)
+    auto orow_g = [&](int r, bool y) -> float* {
         return c.spill + PC::spill_robot + (y ? RPC * (NCH - LCH) * OW : 0) + (r - RPC * LCH) * OW;
     };
     // PGS row constants of the lane's row in the current chunk: impulse, target velocity, 1/diagonal, friction and
-    // the block's Delassus entries. One chunk: kept in registers. Several: stored per row in RK (after the rows)
-    // and swapped into registers chunk by chunk, so registers do not grow with the contact capacity.
+    // the block's Delassus entries. One chunk: kept in registers. Several: stored per row in RK (after the rows, or
+    // for overflow chunks in the env's global area) and swapped into registers chunk by chunk, so registers do not
+    // grow with the contact capacity. Overflow chunks: while a substep has <= CAP contacts (chunk 0 only) the
+    // constants stay in registers and RK is not touched
     float klam = 0.f, kvt = 0.f, kwinv = 0.f, kcmu = 0.f, kca0 = 0.f, kca1 = 0.f;
-    float* RK = reinterpret_cast<float*>(reinterpret_cast<char*>(s.u.rows.J) + pc_rowdata_bytes<PC>());
-    auto rk = [&](int q, int row) -> float& { return RK[q * MAXR * NCH + row]; };
-#pragma unroll 1
-    for (int ch = 0; ch < NCH; ch++) {
+    float* RK;
+    if constexpr (PC::ovf) RK = c.spill + PC::off_rk;
+    else RK = reinterpret_cast<float*>(reinterpret_cast<char*>(s.u.rows.J) + pc_rowdata_bytes<PC>());
+    auto rk = [&](int q, int row) -> float& { return RK[q * RPC * NCH + row]; };
+    const bool multi = NCH > 1 && (!PC::ovf || nc > CAP);       // wave-uniform
+    // chunk ch's rows. LDS (true) / global (false) dense rows are separate instantiations, so that no pointer may
+    // address both (a flat pointer would make chunk 0's LDS rows flat accesses too)
+    auto rows_chunk = [&](int ch, auto lds_tag) {
+        constexpr bool LDSROWS = decltype(lds_tag)::value;
         float vt_ = 0.f, winv_ = 0.f, cmu_ = 0.f;
-        int r = MAXR * ch + lane;
-        if (lane < MAXR && r < nr) {
-            const ContactLDS& ct = c.k[r / 3];
+        int r = RPC * ch + lane;
+        if (lane < RPC && r < nr) {
+            const ContactLDS ct = ct_get(c, r / 3);
             cmu_ = contact_friction(c, ct.a, ct.b);
             int k = r % 3;
             // robot block Jr / Yr (null: the contact touches no link, the block is zero) and object blocks Jo / Yo
@@ -1743,15 +1798,25 @@ HD void substep(SimCtx& c, float hdt) {
                     Jo = jo_rc;
                     Yo = yo_rc;
                 } else {
-                    Jo = orow(r, false);
-                    Yo = orow(r, true);
+                    if constexpr (LDSROWS) {
+                        Jo = Ob + r * OW;
+                        Yo = ObY + r * OW;
+                    } else {
+                        Jo = orow_g(r, false);
+                        Yo = orow_g(r, true);
+                    }
                     for (int t = 0; t < OW; t++) Jo[t] = 0.0f;
                 }
                 if (Jr)
                     for (int t = 0; t < ND; t++) Jr[t] = 0.0f;
             } else {
-                Jr = Jb + r * RSN;
-                Yr = Yb + r * RSN;
+                if constexpr (LDSROWS) {
+                    Jr = Jb + r * RSN;
+                    Yr = Yb + r * RSN;
+                } else {
+                    Jr = gJ + (r - RPC) * RSN;
+                    Yr = gY + (r - RPC) * RSN;
+                }
                 Jo = Jr + D;
                 Yo = Yr + D;
                 for (int t = 0; t < RSN; t++) Jr[t] = 0.0f;
@@ -1813,20 +1878,27 @@ HD void substep(SimCtx& c, float hdt) {
             for (int t = 0; t < RSN - D; t++) a = fmaf(Jo[t], Yo[t], a);
             winv_ = 1.0f / (a + 1e-9f);
         }
-        if (NCH == 1) {
+        if (NCH == 1 || (PC::ovf && ch == 0)) {
             kvt = vt_; kwinv = winv_; kcmu = cmu_;
-        } else if (lane < MAXR) {
+        }
+        if (multi && lane < RPC) {
             rk(0, r) = 0.0f; rk(1, r) = vt_; rk(2, r) = winv_; rk(3, r) = cmu_;
         }
+    };
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ch++) {
+        if (NCH > 1 && RPC * ch >= nr && (PC::ovf || ch > 0)) break;      // wave-uniform: no rows left
+        if (ch < LCH) rows_chunk(ch, std::true_type{});       // LDS rows (every chunk of a dense one-layout family)
+        else rows_chunk(ch, std::false_type{});
     }
     wsync();
     // coupling inside each contact's 3-row block (Delassus entries J_ri . M^-1 J_rj^T, i > j): lane of
     // friction row 1 holds a10, lane of friction row 2 holds a20 and a21
-#pragma unroll 1
-    for (int ch = 0; ch < NCH; ch++) {
+    auto delassus_chunk = [&](int ch, auto lds_tag) {
+        constexpr bool LDSROWS = decltype(lds_tag)::value;
         float ca0_ = 0.f, ca1_ = 0.f;
-        int r = MAXR * ch + lane;
-        if (lane < MAXR && r < nr && r % 3 != 0) {
+        int r = RPC * ch + lane;
+        if (lane < RPC && r < nr && r % 3 != 0) {
             int k = r % 3, r0 = r - k;
             const float *Jo, *Y0o;
             float a = 0.0f, b = 0.0f;           // robot-block partial sums (J_rk . Y_r0, J_rk . Y_r1), t = 0 .. D-1
@@ -1845,7 +1917,7 @@ HD void substep(SimCtx& c, float hdt) {
                     rdot(sr + k * ND, sr + SPJ, sr + SPJ + ND);
                 }
                 if constexpr (PC::rc) {
-                    const ContactLDS& ct = c.k[r / 3];
+                    const ContactLDS ct = ct_get(c, r / 3);
                     f3 n = ld3(ct.n), t1, t2;
                     tangents(n, t1, t2);
                     f3 x = ld3(ct.x);
@@ -1861,14 +1933,21 @@ HD void substep(SimCtx& c, float hdt) {
                     obj_block(c, so1, ct.a, x, t1, scratch + 6, y0_rc + OW + 6);
                     Jo = jo_rc;
                     Y0o = y0_rc;
+                } else if constexpr (LDSROWS) {
+                    Jo = Ob + r * OW;
+                    Y0o = ObY + r0 * OW;
                 } else {
-                    Jo = orow(r, false);
-                    Y0o = orow(r0, true);
+                    Jo = orow_g(r, false);
+                    Y0o = orow_g(r0, true);
                 }
-            } else {
+            } else if constexpr (LDSROWS) {
                 rdot(Jb + r * RSN, Yb + r0 * RSN, Yb + (r0 + 1) * RSN);
                 Jo = Jb + r * RSN + D;
                 Y0o = Yb + r0 * RSN + D;
+            } else {
+                rdot(gJ + (r - RPC) * RSN, gY + (r0 - RPC) * RSN, gY + (r0 + 1 - RPC) * RSN);
+                Jo = gJ + (r - RPC) * RSN + D;
+                Y0o = gY + (r0 - RPC) * RSN + D;
             }
             const float* Y1o = Y0o + (PC::split ? OW : RSN);
             for (int t = 0; t < RSN - D; t++) a = fmaf(Jo[t], Y0o[t], a);
@@ -1878,11 +1957,18 @@ HD void substep(SimCtx& c, float hdt) {
                 ca1_ = b;
             }
         }
-        if (NCH == 1) {
+        if (NCH == 1 || (PC::ovf && ch == 0)) {
             kca0 = ca0_; kca1 = ca1_;
-        } else if (lane < MAXR) {
+        }
+        if (multi && lane < RPC) {
             rk(4, r) = ca0_; rk(5, r) = ca1_;
         }
+    };
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ch++) {
+        if (NCH > 1 && RPC * ch >= nr && (PC::ovf || ch > 0)) break;
+        if (ch < LCH) delassus_chunk(ch, std::true_type{});
+        else delassus_chunk(ch, std::false_type{});
     }
     PROF(4);
     // ---- joint rows, lane d: PD drive (soft implicit spring-damper, |impulse| <= effort h) and the
@@ -1978,8 +2064,9 @@ HD void substep(SimCtx& c, float hdt) {
             int ix = lane < RSN ? lane : -1;       // one slot: the compact row is the dense row
             int ixh = -1;
             if constexpr (row_slots<ND>() == 2) {
-                int so0, so1;
-                contact_slots(c.k[ci].a, c.k[ci].b, so0, so1);
+                int ca, cb, so0, so1;
+                ct_ab(c, ci, ca, cb);
+                contact_slots(ca, cb, so0, so1);
                 ix = compact_index(lane, D, so0, so1);
                 if (VW == 2) ixh = compact_index(lane + 64, D, so0, so1);
             }
@@ -1988,7 +2075,7 @@ HD void substep(SimCtx& c, float hdt) {
             if constexpr (PC::rc) {
                 // object coordinates recomputed from the contact entry (obj_entry: the rows phase's values);
                 // robot coordinates from the contact's link slot (LDS for the first KL, else the spill rows)
-                const ContactLDS& ct = c.k[ci];
+                const ContactLDS ct = ct_get(c, ci);
                 int so0, so1;
                 contact_slots(ct.a, ct.b, so0, so1);
                 bool o1 = ix >= D, o2 = VW == 2 && ixh >= D;
@@ -2026,14 +2113,16 @@ HD void substep(SimCtx& c, float hdt) {
                 return;
             }
             if constexpr (PC::split) {
-                // object coordinates from the LDS object blocks; robot coordinates from the contact's link slot
-                // (LDS for the first KL, else the global spill rows), absent -> 0
-                const float* On = orow(3 * ci, false);
-                const float* OYn = orow(3 * ci, true);
-                int lsc = lslot(ci);            // wave-uniform
-                if (LCH == NCH && lsc < KL) {
+                // object coordinates from the object blocks (LDS for chunks < LCH, else the env's global row area);
+                // robot coordinates from the contact's link slot (LDS for the first KL, else the global spill rows),
+                // absent -> 0. LDS and global sources stay on separate paths (both conditions are wave-uniform)
+                int lsc = lslot(ci);
+                bool lds_obj = LCH == NCH || ci < CAP * LCH;
+                if (lds_obj && lsc < KL) {
                     // every entry of this contact is in LDS: one set of loads, each lane's block (object block at
                     // stride OW, or the link slot's robot block at stride ND) chosen per lane
+                    const float* On = Ob + 3 * ci * OW;
+                    const float* OYn = ObY + 3 * ci * OW;
                     bool ob = ix >= D, rb = ix >= 0 && ix < D && lsc >= 0;
                     const float* P = ob ? On + (ix - D) : Rb + 3 * lsc * ND + ix;
                     const float* PY = ob ? OYn + (ix - D) : RbY + 3 * lsc * ND + ix;
@@ -2044,10 +2133,14 @@ HD void substep(SimCtx& c, float hdt) {
                     }
                 } else if (ix >= D) {
                     int t = ix - D;
-                    j0n = On[t]; j1n = On[OW + t]; j2n = On[2 * OW + t];
-                    y0n = OYn[t]; y1n = OYn[OW + t]; y2n = OYn[2 * OW + t];
+                    auto ldo = [&](const float* On, const float* OYn) {
+                        j0n = On[t]; j1n = On[OW + t]; j2n = On[2 * OW + t];
+                        y0n = OYn[t]; y1n = OYn[OW + t]; y2n = OYn[2 * OW + t];
+                    };
+                    if (lds_obj) ldo(Ob + 3 * ci * OW, ObY + 3 * ci * OW);
+                    else ldo(orow_g(3 * ci, false), orow_g(3 * ci, true));
                 } else if (ix >= 0) {
-                    int ls = lslot(ci);         // wave-uniform: one path per contact, LDS or global
+                    int ls = lsc;
                     auto ld6 = [&](const float* Rn, const float* RYn) {
                         j0n = Rn[ix]; j1n = Rn[ND + ix]; j2n = Rn[2 * ND + ix];
                         y0n = RYn[ix]; y1n = RYn[ND + ix]; y2n = RYn[2 * ND + ix];
@@ -2057,38 +2150,44 @@ HD void substep(SimCtx& c, float hdt) {
                 }
                 if (VW == 2 && ixh >= D) {
                     int t = ixh - D;
-                    h0n = On[t]; h1n = On[OW + t]; h2n = On[2 * OW + t];
-                    g0n = OYn[t]; g1n = OYn[OW + t]; g2n = OYn[2 * OW + t];
+                    auto ldh = [&](const float* On, const float* OYn) {
+                        h0n = On[t]; h1n = On[OW + t]; h2n = On[2 * OW + t];
+                        g0n = OYn[t]; g1n = OYn[OW + t]; g2n = OYn[2 * OW + t];
+                    };
+                    if (lds_obj) ldh(Ob + 3 * ci * OW, ObY + 3 * ci * OW);
+                    else ldh(orow_g(3 * ci, false), orow_g(3 * ci, true));
                 }
                 return;
             }
-            const float* Jn = J + 3 * ci * RSN;
-            const float* Yn = Y + 3 * ci * RSN;
-            if (ix >= 0) {
-                j0n = Jn[ix]; j1n = Jn[RSN + ix]; j2n = Jn[2 * RSN + ix];
-                y0n = Yn[ix]; y1n = Yn[RSN + ix]; y2n = Yn[2 * RSN + ix];
-            }
-            if (VW == 2) {
-                if (ixh >= 0) {
-                    h0n = Jn[ixh]; h1n = Jn[RSN + ixh]; h2n = Jn[2 * RSN + ixh];
-                    g0n = Yn[ixh]; g1n = Yn[RSN + ixh]; g2n = Yn[2 * RSN + ixh];
+            auto ldd = [&](const float* Jn, const float* Yn) {
+                if (ix >= 0) {
+                    j0n = Jn[ix]; j1n = Jn[RSN + ix]; j2n = Jn[2 * RSN + ix];
+                    y0n = Yn[ix]; y1n = Yn[RSN + ix]; y2n = Yn[2 * RSN + ix];
                 }
-            }
+                if (VW == 2) {
+                    if (ixh >= 0) {
+                        h0n = Jn[ixh]; h1n = Jn[RSN + ixh]; h2n = Jn[2 * RSN + ixh];
+                        g0n = Yn[ixh]; g1n = Yn[RSN + ixh]; g2n = Yn[2 * RSN + ixh];
+                    }
+                }
+            };
+            if (PC::ovf && ci >= CAP) ldd(gJ + 3 * (ci - CAP) * RSN, gY + 3 * (ci - CAP) * RSN);   // wave-uniform
+            else ldd(J + 3 * ci * RSN, Y + 3 * ci * RSN);
         };
         if (nc > 0) fetch(0);
 #pragma unroll 1
         for (int ch = 0; ch < NCH; ch++) {
-            int cend = nc < MAXC * (ch + 1) ? nc : MAXC * (ch + 1);
+            int cend = nc < CAP * (ch + 1) ? nc : CAP * (ch + 1);
             if (NCH > 1) {
-                if (MAXC * ch >= nc) break;
-                if (lane < MAXR) {          // swap this chunk's row constants in
-                    int row = MAXR * ch + lane;
+                if (CAP * ch >= nc) break;
+                if (multi && lane < RPC) {          // swap this chunk's row constants in
+                    int row = RPC * ch + lane;
                     klam = rk(0, row); kvt = rk(1, row); kwinv = rk(2, row);
                     kcmu = rk(3, row); kca0 = rk(4, row); kca1 = rk(5, row);
                 }
             }
-            for (int ci = MAXC * ch; ci < cend; ci++) {
-                int r0 = 3 * (ci - MAXC * ch);      // row of this contact within the chunk (= its lane)
+            for (int ci = CAP * ch; ci < cend; ci++) {
+                int r0 = 3 * (ci - CAP * ch);       // row of this contact within the chunk (= its lane)
                 float j0 = j0n, j1 = j1n, j2 = j2n, y0 = y0n, y1 = y1n, y2 = y2n;
                 float h0 = h0n, h1 = h1n, h2 = h2n, g0 = g0n, g1 = g1n, g2 = g2n;
                 if (ci + 1 < nc) fetch(ci + 1);
@@ -2120,16 +2219,16 @@ HD void substep(SimCtx& c, float hdt) {
                 if (d1 != 0.0f) { vreg = fmaf(y1, d1, vreg); if (VW == 2) vregh = fmaf(g1, d1, vregh); }
                 if (d2 != 0.0f) { vreg = fmaf(y2, d2, vreg); if (VW == 2) vregh = fmaf(g2, d2, vregh); }
             }
-            if (NCH > 1 && lane < MAXR) rk(0, MAXR * ch + lane) = klam;     // swap the impulses out
+            if (multi && lane < RPC) rk(0, RPC * ch + lane) = klam;     // swap the impulses out
         }
     }
-    // impulse of global row MAXR ch + lane (xfer sits before RK in the union: no overlap)
-    if (NCH == 1) {
-        if (lane < MAXR) s.u.xfer[lane] = klam;
+    // impulse of global row RPC ch + lane (xfer sits before RK in the union: no overlap)
+    if (!multi) {
+        if (lane < RPC) s.u.xfer[lane] = klam;
     } else {
-#pragma unroll
+#pragma unroll 1
         for (int ch = 0; ch < NCH; ch++)
-            if (lane < MAXR) s.u.xfer[MAXR * ch + lane] = rk(0, MAXR * ch + lane);
+            if (lane < RPC && CAP * ch < nc) s.u.xfer[RPC * ch + lane] = rk(0, RPC * ch + lane);
     }
     if (lane < D) s.u.pd.dforce[lane] = (((dlam + lam_lo) - lam_up) + lam_fr) / hdt;
     wsync();
@@ -2141,7 +2240,7 @@ HD void substep(SimCtx& c, float hdt) {
         for (int b = 0; b < MAXB; b++) s.u.pd.cforce[b][0] = s.u.pd.cforce[b][1] = s.u.pd.cforce[b][2] = 0.f;
         for (int ci = 0; ci < nc; ci++) {
             int r0 = 3 * ci;
-            const ContactLDS& ct = c.k[ci];
+            const ContactLDS ct = ct_get(c, ci);
             f3 n = ld3(ct.n), t1, t2;
             tangents(n, t1, t2);
             f3 f = (n * s.u.xfer[r0] + t1 * s.u.xfer[r0 + 1]) + t2 * s.u.xfer[r0 + 2];

@@ -43,8 +43,23 @@ __host__ __device__ constexpr int task_obj_capacity() {
 #ifndef HB_LDS_CHUNKS
 #define HB_LDS_CHUNKS 0
 #endif
+// Ur5Sih (3 objects) and AllegroHand: overflow chunks (PhysCfg OVF). Chunk 0 keeps the one-chunk LDS layout (21 /
+// 12 contacts); the further chunks' contact entries, rows and row constants live in the env's global area, touched
+// only by substeps with more contacts than chunk 0 holds. Round 3 measured C4 over 21 contacts in 5.4% of the
+// substeps of a whole episode (per-env maximum 57 at p99) and C3 over 12 in 3.2% (maximum 41)
+#ifndef HA_CHUNKS
+#define HA_CHUNKS 4
+#endif
+#ifndef HA_AH_CHUNKS
+#define HA_AH_CHUNKS 4
+#endif
 template <int FAM>
-__host__ __device__ constexpr int task_contact_chunks() { return FAM == FAM_UR5SIH_CLUTTER ? HB_CHUNKS : 1; }
+__host__ __device__ constexpr int task_contact_chunks() {
+    return FAM == FAM_UR5SIH_CLUTTER ? HB_CHUNKS
+                                     : (FAM == HA_TASK_UR5SIH ? HA_CHUNKS : (FAM == HA_TASK_ALLEGRO_HAND ? HA_AH_CHUNKS : 1));
+}
+template <int FAM>
+__host__ __device__ constexpr bool task_overflow() { return FAM == HA_TASK_UR5SIH || FAM == HA_TASK_ALLEGRO_HAND; }
 // clutter family: 1 recomputes the object blocks of the contact rows in registers from the contact entries in the
 // rows phase and at every PGS fetch (PhysCfg RC) instead of storing them in the env's global row area. Measured on
 // C5 (round 3): 22.1 -> 30.8 ms per step, the ~140 VALU per fetch cost more than the stored rows' traffic, which the
@@ -141,7 +156,7 @@ using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_c
                         FAM == FAM_UR5SIH_CLUTTER ? HB_LDS_CHUNKS : task_contact_chunks<FAM>(),
                         task_chunk_capacity<FAM>(), task_col_verts<FAM>(), task_col_planes<FAM>(),
                         task_compact<FAM>() ? 1 : -1, task_compact<FAM>() ? 0 : HA_MAX_GATHER, task_compact<FAM>(),
-                        FAM == FAM_UR5SIH_CLUTTER && HB_RECOMPUTE>;
+                        FAM == FAM_UR5SIH_CLUTTER && HB_RECOMPUTE, task_overflow<FAM>()>;
 
 
 // ----------------------------------------------------------------------------- state load/store
@@ -408,8 +423,11 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.col = col_view<PC>(&c.s->u);
     c.o = reinterpret_cast<ObjLDS*>(smem + obj_lds_offset<PC>());
     c.k = reinterpret_cast<ContactLDS*>(smem + contact_lds_offset<PC>());
-    c.spill = PC::split ? spill + (size_t)env * PC::spill_floats : nullptr;
+    c.spill = (PC::split || PC::ovf) ? spill + (size_t)env * PC::spill_floats : nullptr;
     c.maxc = PC::cap * NCH;
+    // overflow chunks: contact entries past chunk 0 in the env's global area (null otherwise: ct_global folds away)
+    c.kg = PC::ovf ? reinterpret_cast<ContactLDS*>(c.spill + PC::off_ct) : nullptr;
+    c.kc0 = PC::ovf ? PC::cap : PC::cap * NCH;
     c.lane = threadIdx.x;
     c.D = ND;                     // == model->n_dofs (ha_create); a constant, so loops over D unroll
     c.NO = params->n_objects;

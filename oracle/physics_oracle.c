@@ -1107,12 +1107,14 @@ hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int nu
     h->D = model->n_dofs;
     h->B = model->n_bodies;
     /* the device family's capacity (ha_contact_capacity): clutter 4 chunks of 21 (handarm_hip.hip HB_CHUNKS),
-       Ur5Sih 21, AllegroKuka 21, AllegroHand 12 (HA_AK_CONTACTS / HA_AH_CONTACTS) */
-    h->maxc = params->task == HA_TASK_UR5SIH ? (params->n_objects > 3 ? 4 * 21 : 21)
-                                             : (params->task == HA_TASK_ALLEGRO_KUKA ? 21 : 12);
+       Ur5Sih 4 chunks of 21 (HA_CHUNKS), AllegroKuka 21 (HA_AK_CONTACTS), AllegroHand 4 chunks of 12
+       (HA_AH_CONTACTS x HA_AH_CHUNKS); hao_set_capacity overrides it for A/B builds */
+    h->maxc = params->task == HA_TASK_UR5SIH ? 4 * 21 : (params->task == HA_TASK_ALLEGRO_KUKA ? 21 : 4 * 12);
     return h;
 }
 void hao_destroy(hao_handle h) { free(h); }
+/* contact capacity of the device build under test (ha_contact_capacity): a build with other chunk macros */
+void hao_set_capacity(hao_handle h, int maxc) { if (maxc > 0 && maxc <= MAXC) h->maxc = maxc; }
 /* OpenMP threads of hao_simulate (bench.py's cpu_baseline reports an all-cores and a 1-thread sample) */
 void hao_set_threads(int n) { if (n > 0) omp_set_num_threads(n); }
 int hao_get_threads(void) { return omp_get_max_threads(); }

@@ -156,13 +156,20 @@ def ur5sih_step(orc, hs, p, model, draws):
             tt = rp.copy()
             tt[6:] = 0
             hs["dof_position_targets"][e] = tt
-            orc.simulate(hs, 1, begin=int(e), end=int(e) + 1)       # reset_idx's gym.simulate
-            hs["ur5_target"][e] = dof[e, 0:6, 0]
+            # reset_idx's gym.simulate, then the step's control_freq_inv calls: the kernel keeps the env's state in
+            # LDS across them (no round trip through the root-state tensor, as PhysX keeps its bodies between
+            # calls), so the oracle runs them as one 1 + control_freq_inv call sequence; the joint positions after
+            # the first call set ur5_target (ur5sih.py:388-389)
+            probe = hs.copy()
+            orc.simulate(probe, 1, begin=int(e), end=int(e) + 1)
+            hs["ur5_target"][e] = probe["dof_state"].reshape(N, D, 2)[e, 0:6, 0]
+            orc.simulate(hs, 1 + p.control_freq_inv, begin=int(e), end=int(e) + 1)
             hs["reset_buf"][e] = 0
             hs["progress_buf"][e] = 0
             hs["goal_reached_before"][e] = 0
             hs["episode"][e] = hs["episode"][e] + 1
-    orc.simulate(hs, p.control_freq_inv)
+    for e in np.nonzero(~np.isin(np.arange(N), resets))[0]:
+        orc.simulate(hs, p.control_freq_inv, begin=int(e), end=int(e) + 1)
     body = hs["rigid_body_state"].reshape(N, B, 13)
     pid = hs["object_indices"]
     bb = lambda arr: np.array([[list(arr[i]) for i in row] for row in pid], F)       # noqa: E731

@@ -51,28 +51,39 @@ def _cube_energy(model, root):
 
 def test_allegro_cube_released_by_the_hand_gains_no_energy():
     """The random scene starts with fingers interpenetrating the cube by up to 3.4 cm, and AllegroHand's
-    max_depenetration_velocity (1000, AllegroHand.yaml) lets the push-out throw it (up to ~1.6 m/s: env 7 flies 1.4 m).
-    That throw is the only energy source once the hand lets go: from the call on which no finger touches the cube,
-    its mechanical energy (kinetic + rotational + potential) never grows from one call to the next, through the fall,
-    the ground impacts (edge-edge and clipped-face contacts) and the tumbling, within 1% + 1e-4 J."""
+    max_depenetration_velocity (1000, AllegroHand.yaml) lets the push-out throw it (up to ~1.6 m/s: it can fly over a
+    metre). That throw is the only energy source once the hand lets go. From the call on which no finger touches the
+    cube: (1) its mechanical energy (kinetic + rotational + potential) never exceeds its value at release (+1%); (2) from
+    one call to the next it grows only by the Baumgarte push-out of a ground penetration present at the start of the
+    call (a cube landing at 3 m/s moves 2.6 cm per substep, against a 2 mm speculative margin), by at most the
+    potential energy of that depth, m g depth, plus 1% + 1e-4 J."""
     n = 16
     model, params, st, lo, up = setup(n)
     orc = Oracle(model, params, n)
     root = st["root_state"].reshape(n, 3, 13)
     seps = np.array([orc.contacts(st, e)[:, 6].min(initial=0.0) for e in range(n)])
     assert seps.min() < -0.02, "the scene starts with deep finger-cube interpenetration"
+    mg = model.pool_mass[0] * 9.81
     released = np.zeros(n, bool)
+    e_rel = np.zeros(n)
     e_prev = _cube_energy(model, root)
-    checked = 0
+    checked = pushed = 0
     for c in range(60):
-        touch = np.array([any(int(a) >= 100 or int(b) >= 100 for a, b in orc.contacts(st, e)[:, 7:9]) for e in range(n)])
+        cts = [orc.contacts(st, e) for e in range(n)]
+        touch = np.array([any(int(a) >= 100 or int(b) >= 100 for a, b in ct[:, 7:9]) for ct in cts])
+        pen = np.array([max(0.0, -min([float(r[6]) for r in ct if int(r[8]) == -1], default=0.0)) for ct in cts])
+        new = ~released & ~touch
+        e_rel[new] = e_prev[new]
         released |= ~touch
         orc.simulate(st, 1)
         e_now = _cube_energy(model, root)
         chk = released & ~touch
         grow = e_now - e_prev
-        assert (grow[chk] <= 0.01 * e_prev[chk] + 1e-4).all(), (c, np.nonzero(chk & (grow > 0.01 * e_prev + 1e-4)))
+        allow = 0.01 * e_prev + 1e-4 + mg * pen
+        assert (grow[chk] <= allow[chk]).all(), (c, np.nonzero(chk & (grow > allow)))
+        assert (e_now[chk] <= 1.01 * e_rel[chk] + 1e-4).all(), (c, np.nonzero(chk & (e_now > 1.01 * e_rel + 1e-4)))
         checked += int(chk.sum())
+        pushed += int((chk & (grow > 0.01 * e_prev + 1e-4)).sum())
         e_prev = e_now
     assert checked > 100 and released.sum() >= 4
     z = root[:, 1, 2]
