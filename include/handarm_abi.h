@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 11
+#define HA_ABI_VERSION 12
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -64,6 +64,7 @@ extern "C" {
 #define HA_MAX_SPLINE_PIECES 8
 #define HA_N_SPLINES 8
 #define HA_MAX_MPAIRS 192
+#define HA_MAX_SELF_PAIRS 512  /* robot link-hull pairs tested for self-collision (v12) */
 #define HA_DRAW_STRIDE 80     /* floats of reset_draws per env (replayed host RNG draws) */
 /* per-env domain-randomization samples (ha_state_t.dr_scale rows) */
 #define HA_DR_LINK_MASS 0      /* [HA_MAX_LINKS] robot link mass (and inertia) scale */
@@ -184,6 +185,15 @@ typedef struct ha_model_t {
      * |impulse| <= dof_friction |drive + limit impulse of the DOF| (AllegroHand 0.01, allegro_hand.py:267; AllegroKuka
      * the URDF's <dynamics friction>, AllegroKuka.yaml:58 dofFriction -1; Ur5Sih 0 from its URDF) */
     float dof_friction[HA_MAX_DOFS];
+    /* v12: self-collision of the robot's links. The Allegro families create the hand actor with collision filter -1
+     * (allegro_hand.py:334-335, allegro_kuka_base.py:664: the asset's filters, which a URDF does not set), so PhysX
+     * collides every link pair of the articulation except parent and child. self_pair[k] = hull a | hull b << 8
+     * (link hulls of two such links, a < b), tested after the link-static pairs; hull_obb[h] = the link hull's
+     * oriented box in the link frame (centre[3], half extents[3], quat[4] xyzw, pad[2]) for the mid-phase cull
+     * (include/ha_obb.h). n_self_pairs = 0: no self-collision (Ur5Sih: filter 0b1, ur5sih.py:123-125). */
+    int32_t n_self_pairs;
+    uint16_t self_pair[HA_MAX_SELF_PAIRS];
+    float hull_obb[HA_MAX_HULLS][12];
 } ha_model_t;
 
 /* Simulation + task parameters (Ur5SihBase.yaml, Ur5SihMultiObject*.yaml). */

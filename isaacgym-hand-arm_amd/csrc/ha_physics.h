@@ -17,6 +17,7 @@
 
 #include "ha_device.h"
 #include "../../include/handarm_abi.h"
+#include "../../include/ha_obb.h"
 
 #define MAXC 21          /* contacts per chunk: 3 rows each -> 63 rows, one per lane (lane 63 idle) */
 #define MAXR (3 * MAXC)
@@ -1346,7 +1347,7 @@ HD PoseF static_pose(const ha_model_t& m, int k) { return PoseF{ld3(m.static_pos
 
 // pair enumeration in the oracle's order (see detect() in physics_oracle.c)
 // pair p -> (kind, A, B): kinds 0 object-ground, 1 object-static B, 2 object-object, 3 link hull B - object,
-// 4 link hull A - static B
+// 4 link hull A - static B, 5 self-collision pair A of the model (ha_model_t v12 self_pair)
 HD bool pair_desc(const SimCtx& c, int p, int& kind, int& A, int& B) {
     int NO = c.NO, NLH = c.m->n_link_hulls, NS = c.m->n_static;
     for (int o = 0; o < NO; o++) {
@@ -1362,13 +1363,21 @@ HD bool pair_desc(const SimCtx& c, int p, int& kind, int& A, int& B) {
         p -= n;
     }
     if (p < NLH * NS) { kind = 4; A = p / NS; B = p - A * NS; return true; }
+    p -= NLH * NS;
+    if (p < c.m->n_self_pairs) { kind = 5; A = p; B = -1; return true; }
     return false;
+}
+// the two link hulls of self-collision pair k
+HD void self_pair_hulls(const ha_model_t& m, int k, int& ha, int& hb) {
+    uint32_t sp = m.self_pair[k];
+    ha = (int)(sp & 255u);
+    hb = (int)(sp >> 8);
 }
 
 // piece pairs of a candidate pair (1 unless an object is a compound of several convex pieces)
 HD int pair_pieces(const SimCtx& c, int kind, int A, int B) {
     const ha_model_t& m = *c.m;
-    if (kind == 4) return 1;
+    if (kind >= 4) return 1;
     int n = m.pool_nhull[upool(c, A)];
     if (kind == 2) n *= m.pool_nhull[upool(c, B)];
     return n;
@@ -1406,10 +1415,16 @@ HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
             int Lk = m.hull_link[B];
             h1 = B; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = ho + j; P2 = Pb; b2 = A; k2 = A;
         }
-    } else {
+    } else if (kind == 4) {
         int Lk = m.hull_link[A];
         h1 = A; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = m.static_hull[B];
         P2 = static_pose(m, B); b2 = -1; k2 = -100 - B;
+    } else {
+        // self-collision: link hull a (side A) against link hull b (side B), normal from b to a
+        self_pair_hulls(m, A, h1, h2);
+        int La = m.hull_link[h1], Lb = m.hull_link[h2];
+        P1 = PoseF{ld3(s.lp[La]), ldq(s.lq[La])}; b1 = 100 + La;
+        P2 = PoseF{ld3(s.lp[Lb]), ldq(s.lq[Lb])}; b2 = 100 + Lb; k2 = b2;
     }
     collide_hulls(c, h1, P1, h2, P2, b1, b2, b1, k2);
 }
@@ -1444,7 +1459,7 @@ HD void detect(SimCtx& c) {
     int NO = c.NO, NLH = m.n_link_hulls, NS = m.n_static;
     int npairs = 0;
     for (int o = 0; o < NO; o++) npairs += 1 + NS + (NO - 1 - o) + NLH;
-    npairs += NLH * NS;
+    npairs += NLH * NS + m.n_self_pairs;
     wsync();
     for (int base = 0; base < npairs; base += 64) {
         // parallel broad phase: one pair per lane
@@ -1486,6 +1501,15 @@ HD void detect(SimCtx& c) {
                         if (kind == 1) cand = cand && sphere_near_box(m.static_half[B], Pb, co, ro + mg);
                     }
                 }
+            } else if (kind == 5) {
+                // self-collision pair: the two link hulls' oriented boxes, grown by the margin (include/ha_obb.h)
+                int h1, h2;
+                self_pair_hulls(m, A, h1, h2);
+                int La = m.hull_link[h1], Lb = m.hull_link[h2];
+                float ca[3], Ra[9], cb[3], Rb[9];
+                ha_obb_world(s.lp[La], s.lq[La], m.hull_obb[h1], ca, Ra);
+                ha_obb_world(s.lp[Lb], s.lq[Lb], m.hull_obb[h2], cb, Rb);
+                cand = ha_obb_near(ca, Ra, m.hull_obb[h1] + 3, cb, Rb, m.hull_obb[h2] + 3, mg) != 0;
             } else {
                 int Lk = m.hull_link[A];
                 cand = m.link_table_collide[Lk] != 0;
@@ -1549,9 +1573,10 @@ HD void detect(SimCtx& c) {
             }
 #ifdef HA_PROFILE
             wsync();
-            PROF_COUNT(10 + kind, __builtin_amdgcn_s_memtime() - _k0);
-            PROF_COUNT(15 + kind, 1);
-            PROF_COUNT(20 + kind, s.nc != _nc0);
+            // kinds 0..4: time / pairs / pairs with contacts at 10 / 15 / 20 + kind; self pairs (kind 5) at 80..82
+            PROF_COUNT(kind < 5 ? 10 + kind : 80, __builtin_amdgcn_s_memtime() - _k0);
+            PROF_COUNT(kind < 5 ? 15 + kind : 81, 1);
+            PROF_COUNT(kind < 5 ? 20 + kind : 82, s.nc != _nc0);
 #endif
         }
     }

@@ -836,6 +836,12 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
                 return HA_E_MODEL;
         }
     }
+    // self-collision pairs (v12): two link hulls of the model each
+    if (model->n_self_pairs < 0 || model->n_self_pairs > HA_MAX_SELF_PAIRS) return HA_E_MODEL;
+    for (int k = 0; k < model->n_self_pairs; k++) {
+        int a = model->self_pair[k] & 255, b = model->self_pair[k] >> 8;
+        if (a >= model->n_link_hulls || b >= model->n_link_hulls || a == b) return HA_E_MODEL;
+    }
     // a family without a gather buffer (ColLayout NG = 0) takes single-hull pool objects only
     bool one_hull = (fam == HA_TASK_ALLEGRO_KUKA && FamPhys<HA_TASK_ALLEGRO_KUKA>::colg == 0) ||
                     (fam == HA_TASK_ALLEGRO_HAND && FamPhys<HA_TASK_ALLEGRO_HAND>::colg == 0);

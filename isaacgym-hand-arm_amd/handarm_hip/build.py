@@ -17,7 +17,7 @@ def needs_build():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(INCLUDE, h) for h in ("handarm_abi.h", "ha_fmath.h")]
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(INCLUDE, h) for h in ("handarm_abi.h", "ha_fmath.h", "ha_obb.h")]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 

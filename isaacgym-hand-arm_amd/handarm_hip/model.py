@@ -27,6 +27,7 @@ MAX_POOL, MAX_OBJ, MAX_INIT_POSES, MAX_SPLINE_PIECES, N_SPLINES = 32, 8, 4, 8, 8
 MAX_STATIC = 10
 MAX_FIXED_BODIES = 8
 MAX_MPAIRS = 192
+MAX_SELF_PAIRS = 512
 STAT_SIZE = 2 + 2 * MAX_POOL
 DRAW_STRIDE = 80
 DR_SIZE = 80
@@ -88,6 +89,7 @@ class HaModel(C.Structure):
         ("edges", arr(C.c_uint32, MAX_EDGES)), ("plane_loop", arr(i32, MAX_PLANES)),
         ("loop_v", arr(C.c_uint8, MAX_LOOP)),
         ("dof_friction", arr(f32, MAX_DOFS)),
+        ("n_self_pairs", i32), ("self_pair", arr(C.c_uint16, MAX_SELF_PAIRS)), ("hull_obb", arr(f32, MAX_HULLS, 12)),  # v12
     ]
 
 
@@ -442,7 +444,65 @@ def build_model(scene, pool_names=None):
     m.n_mpairs = len(pairs)
     for k, (d, e) in enumerate(pairs):
         m.mpair[k][0], m.mpair[k][1] = d, e
+    _self_collision(m, scene, links)
     return m
+
+
+def hull_obb(verts):
+    """Oriented box of a hull's vertices (principal axes of the vertex cloud, extents from the projections, a
+    right-handed frame): centre[3], half extents[3], quat[4] (xyzw), pad[2] -- the ha_model_t.hull_obb record."""
+    v = np.asarray(verts, np.float64)
+    c0 = v.mean(0)
+    _, _, vt = np.linalg.svd(v - c0)
+    R = vt.T.copy()
+    if np.linalg.det(R) < 0:
+        R[:, 2] = -R[:, 2]
+    loc = (v - c0) @ R
+    lo, hi = loc.min(0), loc.max(0)
+    c = c0 + R @ ((lo + hi) / 2)
+    half = (hi - lo) / 2 * (1 + 1e-5) + 1e-6          # float32 rounding of the pose must not cut a vertex off
+    # rotation matrix -> quaternion (xyzw), largest-component branch
+    tr = np.trace(R)
+    if tr > 0:
+        S = np.sqrt(tr + 1.0) * 2
+        q = [(R[2, 1] - R[1, 2]) / S, (R[0, 2] - R[2, 0]) / S, (R[1, 0] - R[0, 1]) / S, 0.25 * S]
+    else:
+        i = int(np.argmax(np.diag(R)))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        S = np.sqrt(1.0 + R[i, i] - R[j, j] - R[k, k]) * 2
+        q = [0.0] * 4
+        q[i] = 0.25 * S
+        q[j] = (R[j, i] + R[i, j]) / S
+        q[k] = (R[k, i] + R[i, k]) / S
+        q[3] = (R[k, j] - R[j, k]) / S
+    q = np.asarray(q) / np.linalg.norm(q)
+    return list(c) + list(half) + list(q) + [0.0, 0.0]
+
+
+def _self_collision(m, scene, links):
+    """ha_model_t v12 self-collision pairs: with scene["self_collision"] (the Allegro scenes: their hand actors use
+    collision filter -1, allegro_hand.py:334-335, allegro_kuka_base.py:664), every pair of link hulls on two links
+    that are not parent and child (PhysX's articulation filter), minus scene["self_collision"]["exclude"] link pairs.
+    Every link hull gets its oriented box (hull_obb) either way."""
+    for k, h in enumerate(scene["link_hulls"]):
+        m.hull_obb[k][:] = hull_obb(h["verts"])
+    sc = scene.get("self_collision")
+    m.n_self_pairs = 0
+    if not sc:
+        return
+    excl = {tuple(sorted(p)) for p in sc.get("exclude", [])}
+    hl = [h["index"] for h in scene["link_hulls"]]
+    pairs = []
+    for a in range(len(hl)):
+        for b in range(a + 1, len(hl)):
+            la, lb = hl[a], hl[b]
+            if la == lb or links[la]["parent"] == lb or links[lb]["parent"] == la or tuple(sorted((la, lb))) in excl:
+                continue
+            pairs.append(a | (b << 8))
+    assert len(pairs) <= MAX_SELF_PAIRS
+    m.n_self_pairs = len(pairs)
+    for k, v in enumerate(pairs):
+        m.self_pair[k] = v
 
 
 # ----------------------------------------------------------------------------- splines (host)

@@ -30,6 +30,7 @@
 
 #include "../include/handarm_abi.h"
 #include "../include/ha_fmath.h"
+#include "../include/ha_obb.h"
 
 #define MAXC HA_MAX_CONTACTS   /* contact list capacity; a handle uses 21 (<= 3 objects) or 84 (clutter) */
 #define MAXR (3 * MAXC)
@@ -743,6 +744,20 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
             if (near_box(m->static_half[st], Pst, add(PL.p, qrot(PL.q, ld3(m->hull_center[k]))), m->hull_radius[k] + mg))
                 collide_hulls(m, k, PL, m->static_hull[st], Pst, mg, 100 + L, -1, NULL, NULL, out, &nout, h->maxc);
         }
+    }
+    /* self-collision (v12): link hull pairs of non-adjacent links whose oriented boxes come within the margin
+       (include/ha_obb.h, the kernel's mid-phase), normal from hull b to hull a */
+    for (int k = 0; k < m->n_self_pairs; k++) {
+        int ha = m->self_pair[k] & 255, hb = m->self_pair[k] >> 8;
+        int la = m->hull_link[ha], lb = m->hull_link[hb];
+        float pa[3] = {e->lp[la].x, e->lp[la].y, e->lp[la].z}, qa[4] = {e->lq[la].x, e->lq[la].y, e->lq[la].z, e->lq[la].w};
+        float pb[3] = {e->lp[lb].x, e->lp[lb].y, e->lp[lb].z}, qb[4] = {e->lq[lb].x, e->lq[lb].y, e->lq[lb].z, e->lq[lb].w};
+        float ca[3], Ra[9], cb[3], Rb[9];
+        ha_obb_world(pa, qa, m->hull_obb[ha], ca, Ra);
+        ha_obb_world(pb, qb, m->hull_obb[hb], cb, Rb);
+        if (!ha_obb_near(ca, Ra, m->hull_obb[ha] + 3, cb, Rb, m->hull_obb[hb] + 3, mg)) continue;
+        pose_t PA = {e->lp[la], e->lq[la]}, PB = {e->lp[lb], e->lq[lb]};
+        collide_hulls(m, ha, PA, hb, PB, mg, 100 + la, 100 + lb, NULL, NULL, out, &nout, h->maxc);
     }
     return nout;
 }

@@ -70,7 +70,9 @@ def test_allegro_cube_released_by_the_hand_gains_no_energy():
     checked = pushed = 0
     for c in range(60):
         cts = [orc.contacts(st, e) for e in range(n)]
-        touch = np.array([any(int(a) >= 100 or int(b) >= 100 for a, b in ct[:, 7:9]) for ct in cts])
+        # a finger on the cube (object 0): link-link (self-collision) contacts do not count
+        touch = np.array([any((int(a) >= 100 and int(b) == 0) or (int(a) == 0 and int(b) >= 100) for a, b in ct[:, 7:9])
+                          for ct in cts])
         pen = np.array([max(0.0, -min([float(r[6]) for r in ct if int(r[8]) == -1], default=0.0)) for ct in cts])
         new = ~released & ~touch
         e_rel[new] = e_prev[new]

@@ -523,6 +523,12 @@ def build_cube(size=0.065, density=400.0):
             "inertia": [I, 0, 0, 0, I, 0, 0, 0, I], "hull": box_hull(half)}
 
 
+# self-collision of the Allegro actors (ha_model_t v12): every non-adjacent link pair, minus the link pairs whose
+# convex hulls already touch at the default pose (the cooked hulls are larger than the meshes near the joints)
+ALLEGRO_SELF_COLLISION = {"exclude": []}
+KUKA_SELF_COLLISION = {"exclude": []}
+
+
 def main_allegro():
     robot, link_hulls = build_allegro()
     L = len(robot["links"])
@@ -532,6 +538,8 @@ def main_allegro():
              "layout": {"n_actors": 3, "actor_robot": 0, "actor_object0": 1, "actor_goal": 2, "actor_table": -1,
                         "n_bodies": L + 2, "body_robot0": 0, "body_object0": L, "body_goal": L + 1,
                         "body_table": -1},
+             # hand actor with collision filter -1 (allegro_hand.py:334-335): its links collide with each other
+             "self_collision": ALLEGRO_SELF_COLLISION,
              "generator": "tools/build_model.py --allegro (reference assets @ /root/reference/assets/urdf)"}
     with open(ALLEGRO_OUT, "w") as f:
         json.dump(scene, f, indent=None, separators=(",", ":"))
@@ -617,6 +625,8 @@ def main_kuka():
              "layout": {"n_actors": 4, "actor_robot": 0, "actor_object0": 1, "actor_goal": 3, "actor_table": 2,
                         "n_bodies": L + 3, "body_robot0": 0, "body_object0": L, "body_goal": L + 2,
                         "body_table": L + 1},
+             # arm + hand actor with collision filter -1 (allegro_kuka_base.py:664): its links collide with each other
+             "self_collision": KUKA_SELF_COLLISION,
              "generator": "tools/build_model.py --kuka (reference assets @ /root/reference/assets/urdf)"}
     with open(KUKA_OUT, "w") as f:
         json.dump(scene, f, indent=None, separators=(",", ":"))
