@@ -426,6 +426,30 @@ def run_config(task, envs, args, world, rank, device, log_interval_fn):
                                       "kernel_avg_ms": statistics.mean(pc_ms), "algorithmic_bytes_per_env": pb,
                                       "achieved": pach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": pach / HBM_PEAK_GBS}
+    if task in ("ur5sih", "binpick") and args.episode_steps > 0:
+        # the whole-episode window: the K-step window above starts right after the first reset, where
+        # the arm has not reached the objects yet; the next episode_steps steps (one full 200-step episode, so one
+        # synchronous reset step) give the steady-state rate and contact statistics north_star's figure is about
+        env.contact_stats(reset=True)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        t1 = time.perf_counter()
+        for k in range(args.episode_steps):
+            env.step(pool[k % len(pool)])
+            if (k + 1) % LOG_INTERVAL == 0:
+                log_interval_fn(task, env)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([el], device=device, dtype=torch.float64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        rec["episode_window"] = {"steps": args.episode_steps, "value": world * envs * args.episode_steps / el,
+                                 "unit": "env-steps/s", "ms_per_step": el / args.episode_steps * 1e3,
+                                 "includes_reset_step": args.episode_steps >= 200, "contacts": env.contact_stats()}
     del env, pool
     import gc
     gc.collect()
@@ -483,6 +507,9 @@ def main():
     ap.add_argument("--no-dr", action="store_true", help="ur5sih: domain randomization off")
     ap.add_argument("--pointclouds", action="store_true",
                     help="ur5sih / binpick: the point-cloud student observation list (synthetic clouds every step)")
+    ap.add_argument("--episode-steps", type=int, default=200,
+                    help="ur5sih / binpick: also time this many steps after the K-step window (one whole 200-step "
+                         "episode incl. its synchronous reset step; 0: off)")
     ap.add_argument("--cpu-envs", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU sample of the headline config")
     ap.add_argument("--cpu-seconds-sub", type=float, default=4.0, help="CPU sample of each sub-record")

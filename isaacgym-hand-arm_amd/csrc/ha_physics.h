@@ -183,9 +183,12 @@ __host__ __device__ inline size_t obj_lds_offset_rows(size_t rows) {
 // and row constants in the env's global area (L2-resident), so the contact capacity grows without LDS. A substep
 // with <= CAP contacts never touches that area; a substep over CAP swaps every chunk's row constants through it.
 template <int ND, int OCAP, int NCH, int KL = 8, int LCH = NCH, int CAP = MAXC, int CV = 64, int CP = 128,
-          int SPLIT = -1, int NG = HA_MAX_GATHER, bool MU = false, bool RC = false, bool OVF = false>
+          int SPLIT = -1, int NG = HA_MAX_GATHER, bool MU = false, bool RC = false, bool OVF = false, bool SELF = false>
 struct PhysCfg {
     static constexpr int nd = ND, ocap = OCAP, nch = NCH;
+    // the family's robot collides with itself (ha_model_t v12 self pairs; the Allegro families). Without it the
+    // self-pair pass is not compiled (its registers would count against every family)
+    static constexpr bool selfc = SELF;
     static constexpr int colv = CV, colp = CP, colg = NG;   // largest hull: vertices, face planes; gather points
     static constexpr size_t col_bytes = ColLayout<CV, CP, NG>::bytes;
     // contacts per chunk (MAXC, or fewer: the rows and the LDS list shrink with it)
@@ -345,11 +348,10 @@ HD void ct_ab(const SimCtx& c, int ci, int& a, int& b) {
     }
 }
 HD void ct_fill(ContactLDS& ct, f3 x, f3 n, float sep, int a, int b) {
-    st3(ct.x, x);
-    st3(ct.n, n);
-    ct.sep = sep;
-    ct.a = (short)a;
-    ct.b = (short)b;
+    // eight dword stores: the two 16-bit body codes go as one packed word
+    float* q = reinterpret_cast<float*>(&ct);
+    q[0] = x.x; q[1] = x.y; q[2] = x.z; q[3] = n.x; q[4] = n.y; q[5] = n.z; q[6] = sep;
+    q[7] = __int_as_float((a & 0xFFFF) | (b << 16));
 }
 HD void ct_put(const SimCtx& c, int ci, f3 x, f3 n, float sep, int a, int b) {
     if (ct_global(c, ci)) ct_fill(c.kg[ci - c.kc0], x, n, sep, a, b);
@@ -1164,7 +1166,7 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
                 }
             }
         }
-        wave_argmax(best, bw);
+        if (nA > 0 && nB > 0) wave_argmax(best, bw);      // (no pair: best stays -3e38, no reduction needed)
         HPROF(30);
         if (best > mg) return;                              // separated along an edge-edge axis
         if (best > c.p->edge_rel_tol * smax + c.p->edge_abs_tol) {
@@ -1347,7 +1349,7 @@ HD PoseF static_pose(const ha_model_t& m, int k) { return PoseF{ld3(m.static_pos
 
 // pair enumeration in the oracle's order (see detect() in physics_oracle.c)
 // pair p -> (kind, A, B): kinds 0 object-ground, 1 object-static B, 2 object-object, 3 link hull B - object,
-// 4 link hull A - static B, 5 self-collision pair A of the model (ha_model_t v12 self_pair)
+// 4 link hull A - static B; then (detect's self-pair pass) 5: self-collision pair A of the model (v12 self_pair)
 HD bool pair_desc(const SimCtx& c, int p, int& kind, int& A, int& B) {
     int NO = c.NO, NLH = c.m->n_link_hulls, NS = c.m->n_static;
     for (int o = 0; o < NO; o++) {
@@ -1363,8 +1365,6 @@ HD bool pair_desc(const SimCtx& c, int p, int& kind, int& A, int& B) {
         p -= n;
     }
     if (p < NLH * NS) { kind = 4; A = p / NS; B = p - A * NS; return true; }
-    p -= NLH * NS;
-    if (p < c.m->n_self_pairs) { kind = 5; A = p; B = -1; return true; }
     return false;
 }
 // the two link hulls of self-collision pair k
@@ -1448,6 +1448,58 @@ HD void gather_emit(SimCtx& c, int kind, int A, int B) {
     emit_contacts(c, valid, pt, sep, n, a, b);
 }
 
+// self-collision pass (ha_model_t v12; after every other pair, the oracle's order): per batch of 64 pairs, the link
+// hulls' world boxes (lane = hull, include/ha_obb.h ha_obb_world) go to the narrow-phase scratch, each lane tests one
+// pair's boxes against each other (ha_obb_near), and the candidates run the hull narrow phase in pair order. The box
+// table is rebuilt per batch because the narrow phases overwrite the scratch (26 hulls: one lane pass)
+HD void detect_self(SimCtx& c) {
+    EnvLDS& s = *c.s;
+    const ha_model_t& m = *c.m;
+    int lane = c.lane, NLH = m.n_link_hulls, nsp = m.n_self_pairs;
+    float mg = c.p->contact_margin;
+    float (*ob)[16] = reinterpret_cast<float(*)[16]>(c.col.wvA);     // per hull: centre 3, R 9, half 3
+#pragma unroll 1
+    for (int base = 0; base < nsp; base += 64) {
+        if (lane < NLH) {
+            int L = m.hull_link[lane];
+            float* w = ob[lane];
+            ha_obb_world(s.lp[L], s.lq[L], m.hull_obb[lane], w, w + 3);
+            w[12] = m.hull_obb[lane][3]; w[13] = m.hull_obb[lane][4]; w[14] = m.hull_obb[lane][5];
+        }
+        c.colA_h = c.colB_h = -1;       // the box table overwrote the cached hull sides
+        c.colA_p = false;
+        wsync();
+        int p = base + lane;
+        bool cand = false;
+        if (p < nsp) {
+            int h1, h2;
+            self_pair_hulls(m, p, h1, h2);
+            cand = ha_obb_near(ob[h1], ob[h1] + 3, ob[h1] + 12, ob[h2], ob[h2] + 3, ob[h2] + 12, mg) != 0;
+        }
+        uint64_t mask = __ballot(cand);
+        wsync();
+        while (mask) {
+            int bit = __ffsll((unsigned long long)mask) - 1;
+            mask &= mask - 1;
+            int k = __builtin_amdgcn_readfirstlane(base + bit);
+#ifdef HA_PROFILE
+            c.pk = 5;
+            unsigned long long _k0 = __builtin_amdgcn_s_memtime();
+            int _nc0 = s.nc;
+#endif
+            narrow_phase(c, 5, k, -1, 0);
+#ifdef HA_PROFILE
+            wsync();
+            PROF_COUNT(80, __builtin_amdgcn_s_memtime() - _k0);          // self pairs: time / pairs / with contacts
+            PROF_COUNT(81, 1);
+            PROF_COUNT(82, s.nc != _nc0);
+#endif
+        }
+    }
+    wsync();
+}
+
+template <bool SELF>
 HD void detect(SimCtx& c) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
@@ -1459,7 +1511,7 @@ HD void detect(SimCtx& c) {
     int NO = c.NO, NLH = m.n_link_hulls, NS = m.n_static;
     int npairs = 0;
     for (int o = 0; o < NO; o++) npairs += 1 + NS + (NO - 1 - o) + NLH;
-    npairs += NLH * NS + m.n_self_pairs;
+    npairs += NLH * NS;
     wsync();
     for (int base = 0; base < npairs; base += 64) {
         // parallel broad phase: one pair per lane
@@ -1501,15 +1553,6 @@ HD void detect(SimCtx& c) {
                         if (kind == 1) cand = cand && sphere_near_box(m.static_half[B], Pb, co, ro + mg);
                     }
                 }
-            } else if (kind == 5) {
-                // self-collision pair: the two link hulls' oriented boxes, grown by the margin (include/ha_obb.h)
-                int h1, h2;
-                self_pair_hulls(m, A, h1, h2);
-                int La = m.hull_link[h1], Lb = m.hull_link[h2];
-                float ca[3], Ra[9], cb[3], Rb[9];
-                ha_obb_world(s.lp[La], s.lq[La], m.hull_obb[h1], ca, Ra);
-                ha_obb_world(s.lp[Lb], s.lq[Lb], m.hull_obb[h2], cb, Rb);
-                cand = ha_obb_near(ca, Ra, m.hull_obb[h1] + 3, cb, Rb, m.hull_obb[h2] + 3, mg) != 0;
             } else {
                 int Lk = m.hull_link[A];
                 cand = m.link_table_collide[Lk] != 0;
@@ -1573,14 +1616,14 @@ HD void detect(SimCtx& c) {
             }
 #ifdef HA_PROFILE
             wsync();
-            // kinds 0..4: time / pairs / pairs with contacts at 10 / 15 / 20 + kind; self pairs (kind 5) at 80..82
-            PROF_COUNT(kind < 5 ? 10 + kind : 80, __builtin_amdgcn_s_memtime() - _k0);
-            PROF_COUNT(kind < 5 ? 15 + kind : 81, 1);
-            PROF_COUNT(kind < 5 ? 20 + kind : 82, s.nc != _nc0);
+            PROF_COUNT(10 + kind, __builtin_amdgcn_s_memtime() - _k0);     // time / pairs / pairs with contacts
+            PROF_COUNT(15 + kind, 1);
+            PROF_COUNT(20 + kind, s.nc != _nc0);
 #endif
         }
     }
     wsync();
+    if constexpr (SELF) detect_self(c);
 }
 
 // ----------------------------------------------------------------------------- constraint rows
@@ -1729,13 +1772,13 @@ HD void substep(SimCtx& c, float hdt) {
         int nc0 = s.nc;
         wsync();
         c.dry = rep == 1;
-        detect(c);
+        detect<PC::selfc>(c);
         c.dry = false;
         if (rep == 1 && lane == 0) s.nc = nc0;
         wsync();
     }
 #else
-    detect(c);
+    detect<PC::selfc>(c);
 #endif
     PROF(3);
     if (lane == 0) {        // contact-list diagnostics (ha_state_t.contact_stats)
@@ -1753,7 +1796,7 @@ HD void substep(SimCtx& c, float hdt) {
     constexpr int CAP = PC::cap, RPC = PC::rpc;
     float* Jb = s.u.rows.J;
     float* Yb = Jb + RPC * PC::lch * RSN;
-    int nc = s.nc;
+    int nc = __builtin_amdgcn_readfirstlane(s.nc);      // wave-uniform (an SGPR: the chunk loops branch on it)
     int nr = 3 * nc;    // nc <= CAP x NCH -> <= RPC x NCH rows
     // split rows (PhysCfg): object blocks of every row (OW wide, J then Y), then the robot blocks of the
     // first KL link contacts (J then Y), then the env's global spill area for the link contacts after those

@@ -156,7 +156,8 @@ using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_c
                         FAM == FAM_UR5SIH_CLUTTER ? HB_LDS_CHUNKS : task_contact_chunks<FAM>(),
                         task_chunk_capacity<FAM>(), task_col_verts<FAM>(), task_col_planes<FAM>(),
                         task_compact<FAM>() ? 1 : -1, task_compact<FAM>() ? 0 : HA_MAX_GATHER, task_compact<FAM>(),
-                        FAM == FAM_UR5SIH_CLUTTER && HB_RECOMPUTE, task_overflow<FAM>()>;
+                        FAM == FAM_UR5SIH_CLUTTER && HB_RECOMPUTE, task_overflow<FAM>(),
+                        FAM == HA_TASK_ALLEGRO_HAND || FAM == HA_TASK_ALLEGRO_KUKA>;
 
 
 // ----------------------------------------------------------------------------- state load/store
@@ -536,14 +537,17 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
 #if defined(HA_PROFILE) || defined(HA_ENVT)
 // diagnostic builds: each workgroup's start / end on the constant 100 MHz clock (s_memrealtime), by launch slot
 __device__ unsigned long long g_envt[2 * 65536];
-#define HA_ENV_T0() unsigned long long _e0 = __builtin_amdgcn_s_memrealtime();
+// (the start stamp is stored right away: an s_memrealtime value kept live across the whole kernel made the backend
+// stop with "illegal VGPR to SGPR copy" in the overflow-chunk families)
+#define HA_ENV_T0()                                                                               \
+    do {                                                                                          \
+        unsigned long long _e0 = __builtin_amdgcn_s_memrealtime();                                \
+        if (threadIdx.x == 0 && blockIdx.x < 65536) g_envt[2 * blockIdx.x] = _e0;                 \
+    } while (0)
 #define HA_ENV_T1()                                                                               \
     do {                                                                                          \
         __syncthreads();                                                                          \
-        if (threadIdx.x == 0 && blockIdx.x < 65536) {                                             \
-            g_envt[2 * blockIdx.x] = _e0;                                                         \
-            g_envt[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();                        \
-        }                                                                                         \
+        if (threadIdx.x == 0 && blockIdx.x < 65536) g_envt[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define HA_ENV_T0()
@@ -836,8 +840,14 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
                 return HA_E_MODEL;
         }
     }
-    // self-collision pairs (v12): two link hulls of the model each
+    // self-collision pairs (v12): two link hulls of the model each; only the Allegro families' kernels run them
     if (model->n_self_pairs < 0 || model->n_self_pairs > HA_MAX_SELF_PAIRS) return HA_E_MODEL;
+    if (model->n_self_pairs > 0 && params->task == HA_TASK_UR5SIH) return HA_E_MODEL;
+    // the self-pair pass keeps a 64-byte world box per link hull in the narrow-phase scratch (detect_self)
+    if (model->n_self_pairs > 0 &&
+        (size_t)model->n_link_hulls * 64 > (fam == HA_TASK_ALLEGRO_HAND ? FamPhys<HA_TASK_ALLEGRO_HAND>::col_bytes
+                                                                        : FamPhys<HA_TASK_ALLEGRO_KUKA>::col_bytes))
+        return HA_E_MODEL;
     for (int k = 0; k < model->n_self_pairs; k++) {
         int a = model->self_pair[k] & 255, b = model->self_pair[k] >> 8;
         if (a >= model->n_link_hulls || b >= model->n_link_hulls || a == b) return HA_E_MODEL;

@@ -41,12 +41,13 @@ if __name__ == "__main__":
         print(f"{label}: contacts/substep {buf[8] / max(buf[9], 1):.2f}", flush=True)
         print("  " + "  ".join(f"{PHASES[i]} {100.0 * buf[i] / tot:5.1f}%" for i in range(8)), flush=True)
         sub = max(buf[9], 1)
-        for k, name in enumerate(["obj-ground", "obj-static", "obj-obj", "link-obj", "link-static"]):
-            print(f"    narrow {name:10s}: {buf[15 + k] / sub:6.2f} pairs/substep, {buf[20 + k] / sub:6.2f} with contacts, "
-                  f"{100.0 * buf[10 + k] / tot:5.1f}% of substep cycles", flush=True)
+        for k, name in enumerate(["obj-ground", "obj-static", "obj-obj", "link-obj", "link-static", "link-link"]):
+            t_, n_, h_ = (10 + k, 15 + k, 20 + k) if k < 5 else (80, 81, 82)       # self pairs (kind 5) at 80..82
+            print(f"    narrow {name:10s}: {buf[n_] / sub:6.2f} pairs/substep, {buf[h_] / sub:6.2f} with contacts, "
+                  f"{100.0 * buf[t_] / tot:5.1f}% of substep cycles", flush=True)
         print("    hull-hull split: " + "  ".join(f"{nm} {100.0 * buf[25 + i] / tot:5.1f}%" for i, nm in
               enumerate(["setup", "SAT A", "SAT B", "incident", "emit", "edge-edge", "clip"])), flush=True)
-        for k, name in enumerate(["obj-ground", "obj-static", "obj-obj", "link-obj", "link-static"]):
+        for k, name in enumerate(["obj-ground", "obj-static", "obj-obj", "link-obj", "link-static", "link-link"]):
             row = [buf[32 + 8 * k + i] for i in range(7)]
             if sum(row):
                 print(f"      {name:11s}: " + "  ".join(f"{nm} {100.0 * v / tot:5.1f}%" for nm, v in
