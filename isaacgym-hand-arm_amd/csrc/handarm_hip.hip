@@ -53,13 +53,18 @@ __host__ __device__ constexpr int task_obj_capacity() {
 #ifndef HA_AH_CHUNKS
 #define HA_AH_CHUNKS 4
 #endif
+// AllegroKuka: with the hand's self-collision (v12) a substep offers 12 contacts on average and up to ~50 under random
+// actions; chunk 0 holds 21 in LDS, a second chunk in the env's global area takes the rest
+#ifndef HA_AK_CHUNKS
+#define HA_AK_CHUNKS 2
+#endif
 template <int FAM>
 __host__ __device__ constexpr int task_contact_chunks() {
     return FAM == FAM_UR5SIH_CLUTTER ? HB_CHUNKS
-                                     : (FAM == HA_TASK_UR5SIH ? HA_CHUNKS : (FAM == HA_TASK_ALLEGRO_HAND ? HA_AH_CHUNKS : 1));
+           : (FAM == HA_TASK_UR5SIH ? HA_CHUNKS : (FAM == HA_TASK_ALLEGRO_HAND ? HA_AH_CHUNKS : HA_AK_CHUNKS));
 }
 template <int FAM>
-__host__ __device__ constexpr bool task_overflow() { return FAM == HA_TASK_UR5SIH || FAM == HA_TASK_ALLEGRO_HAND; }
+__host__ __device__ constexpr bool task_overflow() { return FAM != FAM_UR5SIH_CLUTTER; }
 // clutter family: 1 recomputes the object blocks of the contact rows in registers from the contact entries in the
 // rows phase and at every PGS fetch (PhysCfg RC) instead of storing them in the env's global row area. Measured on
 // C5 (round 3): 22.1 -> 30.8 ms per step, the ~140 VALU per fetch cost more than the stored rows' traffic, which the

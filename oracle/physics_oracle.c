@@ -1122,9 +1122,9 @@ hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int nu
     h->D = model->n_dofs;
     h->B = model->n_bodies;
     /* the device family's capacity (ha_contact_capacity): clutter 4 chunks of 21 (handarm_hip.hip HB_CHUNKS),
-       Ur5Sih 4 chunks of 21 (HA_CHUNKS), AllegroKuka 21 (HA_AK_CONTACTS), AllegroHand 4 chunks of 12
-       (HA_AH_CONTACTS x HA_AH_CHUNKS); hao_set_capacity overrides it for A/B builds */
-    h->maxc = params->task == HA_TASK_UR5SIH ? 4 * 21 : (params->task == HA_TASK_ALLEGRO_KUKA ? 21 : 4 * 12);
+       Ur5Sih 4 chunks of 21 (HA_CHUNKS), AllegroKuka 2 chunks of 21 (HA_AK_CONTACTS x HA_AK_CHUNKS), AllegroHand
+       4 chunks of 12 (HA_AH_CONTACTS x HA_AH_CHUNKS); hao_set_capacity overrides it for A/B builds */
+    h->maxc = params->task == HA_TASK_UR5SIH ? 4 * 21 : (params->task == HA_TASK_ALLEGRO_KUKA ? 2 * 21 : 4 * 12);
     return h;
 }
 void hao_destroy(hao_handle h) { free(h); }

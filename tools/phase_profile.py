@@ -18,7 +18,10 @@ PHASES = ["fk", "dynamics(CRBA+RNEA)", "chol+Minv+free+objects", "detect", "cont
 
 if __name__ == "__main__":
     if "--build" in sys.argv:
-        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", *build.FLAGS, "-DHA_PROFILE", "-I", build.INCLUDE,
+        # -DHA_AK_CHUNKS=1: with the phase stamps, hipcc 7.2's backend stops on the AllegroKuka overflow chunk
+        # ("illegal VGPR to SGPR copy"); the diagnostic builds profile AllegroKuka with its LDS chunk only (the product
+        # overflows in ~2% of C2 substeps)
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", *build.FLAGS, "-DHA_AK_CHUNKS=1", "-DHA_PROFILE", "-I", build.INCLUDE,
                "-o", PROF_LIB, os.path.join(build.CSRC, "handarm_hip.hip")]
         subprocess.check_call(cmd)
         subprocess.check_call([x if x != "-DHA_PROFILE" else "-DHA_ENVT" for x in cmd[:-3]] + ["-o", ENVT_LIB, cmd[-1]])
