@@ -41,10 +41,14 @@ HA_OB_FN void ha_obb_world(const float* lp, const float* lq, const float* ob, fl
     c[2] = lp[2] + ((vz + w * tz) + (x * ty - y * tx));
 }
 
-/* boxes (ca, Ra, half extents ha) and (cb, Rb, hb) within the margin mg of each other on all 15 SAT axes? */
+/* boxes (ca, Ra, half extents ha) and (cb, Rb, hb) within the margin mg of each other: their circumscribed spheres
+ * first (one distance), then all 15 SAT axes */
 HA_OB_FN int ha_obb_near(const float* ca, const float* Ra, const float* ha, const float* cb, const float* Rb,
                          const float* hb, float mg) {
     float T0 = cb[0] - ca[0], T1 = cb[1] - ca[1], T2 = cb[2] - ca[2];
+    float rs = (sqrtf((ha[0] * ha[0] + ha[1] * ha[1]) + ha[2] * ha[2]) + sqrtf((hb[0] * hb[0] + hb[1] * hb[1]) + hb[2] * hb[2]))
+               + mg;
+    if ((T0 * T0 + T1 * T1) + T2 * T2 > rs * rs) return 0;
     float R[3][3], AR[3][3], t[3];
     for (int i = 0; i < 3; i++) {
         t[i] = (Ra[i] * T0 + Ra[3 + i] * T1) + Ra[6 + i] * T2;

@@ -117,6 +117,7 @@ struct EnvLDS {
     int nc, nr, noff, ng;                       // contacts kept / rows / contacts offered this substep /
                                                 // points gathered for a compound object pair
     int cst[4];                                 // contact_stats of this launch (see ha_state_t)
+    uint32_t selfm[HA_MAX_SELF_PAIRS / 32];     // self-collision candidates of this substep (detect_self), a bit a pair
     union {
         PostScratch pd;                         // (the narrow-phase scratch, ColLayout, is sized per family)
         RowScratch rows;
@@ -220,7 +221,10 @@ struct PhysCfg {
     static constexpr int spill_ct = ovf ? 8 * CAP * (NCH - 1) : 0;
     static constexpr int off_dense = spill_robot + spill_obj, off_rk = off_dense + spill_dense,
                          off_ct = off_rk + spill_rk;
-    static constexpr int spill_floats = off_ct + spill_ct;
+    // self-collision families: one byte per self pair, the separating face of the pair's last narrow phase
+    static constexpr int spill_selfc = SELF ? HA_MAX_SELF_PAIRS / 4 : 0;
+    static constexpr int off_selfc = off_ct + spill_ct;
+    static constexpr int spill_floats = off_selfc + spill_selfc;
     static_assert(ND + 6 * OCAP <= MAXV, "generalized velocity exceeds MAXV");
     static_assert(!split || (KL >= 0 && KL <= CAP * NCH), "LDS link slots must not exceed the contact capacity");
     static_assert(!split || CAP * NCH <= 128, "split rows: <= 128 contacts");
@@ -318,6 +322,10 @@ struct SimCtx {
     int colA_h, colA_b, colB_h, colB_b;
     bool colA_p;            // side A's world planes are in ColScratch too (SAT B runs first and may exit before them)
     bool gather;            // a compound object pair's piece pairs: reduced points go to ColScratch gp / gn
+    // self-collision pairs (PhysCfg SELF): the separating face the last narrow phase found (0x80 | k: face k of side B,
+    // k: face k of side A, 0xFF: none), and the env's per-pair record of it in its global area (null otherwise)
+    int sepf;
+    uint8_t* selfc;
 #ifdef HA_PROFILE
     int pk;                 // profiled build: kind of the running pair
 #endif
@@ -1017,6 +1025,7 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     f3 cb = PB.p + qrot(PB.q, scale3(c, b, ld3(m.hull_center[hb])));
     f3 dc = ca - cb;
     float rr = scale_radius(c, a, m.hull_radius[ha]) + scale_radius(c, b, m.hull_radius[hb]) + mg;
+    c.sepf = 0xFF;
     if (dot3(dc, dc) > rr * rr) return;
     int nva = m.hull_nverts[ha], nvb = m.hull_nverts[hb];
     int npa = m.hull_nplanes[ha], npb = m.hull_nplanes[hb];
@@ -1053,8 +1062,19 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     if (c.p->narrow_phase_flags & HA_NP_NO_SPHERE_CULL) {
     } else {
         float sc = -3.0e38f;
-        for (int k = lane; k < npb; k += 64) sc = fmaxf(sc, dot3(ld3(cs.wpB[k]), ca) + cs.wpB[k][3]);
-        if (wave_max(sc) - scale_radius(c, a, m.hull_radius[ha]) > mg + 1e-3f) return;
+        int kc = 1 << 20;
+        for (int k = lane; k < npb; k += 64) {
+            float v = dot3(ld3(cs.wpB[k]), ca) + cs.wpB[k][3];
+            if (v > sc) { sc = v; kc = k; }
+        }
+        float scm = wave_max(sc);
+        if (scm - scale_radius(c, a, m.hull_radius[ha]) > mg + 1e-3f) {
+            if (c.selfc) {                  // self pair: B's face k separates A, the hint detect_self checks next time
+                wave_argmax(sc, kc);
+                c.sepf = 0x80 | kc;
+            }
+            return;
+        }
     }
     if (needA) {
         if (lane < nva) st3(cs.wvA[lane], PA.p + qrot(PA.q, scale3(c, a, ld3(m.verts[m.hull_vert_start[ha] + lane]))));
@@ -1069,7 +1089,10 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     int kA, kB;
     sat_planes(c, cs.wpB, npb, cs.wvA, nva, sepB, kB);
     HPROF(27);
-    if (sepB > mg) return;
+    if (sepB > mg) {
+        c.sepf = 0x80 | kB;
+        return;
+    }
     if (!c.colA_p) {
         bool scA = body_scaled(c, a);
         f3 isA = inv_scale(c, a);
@@ -1088,7 +1111,10 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
     HPROF(25);
     sat_planes(c, cs.wpA, npa, cs.wvB, nvb, sepA, kA);
     HPROF(26);
-    if (sepA > mg) return;
+    if (sepA > mg) {
+        c.sepf = kA;
+        return;
+    }
     // ---- edge-edge axes (v10): a hull pair whose face axes leave it within the margin may still be separated along,
     //      or touch through, a pair of edges
     int nea = m.hull_nedges[ha], neb = m.hull_nedges[hb];
@@ -1448,27 +1474,33 @@ HD void gather_emit(SimCtx& c, int kind, int A, int B) {
     emit_contacts(c, valid, pt, sep, n, a, b);
 }
 
-// self-collision pass (ha_model_t v12; after every other pair, the oracle's order): per batch of 64 pairs, the link
-// hulls' world boxes (lane = hull, include/ha_obb.h ha_obb_world) go to the narrow-phase scratch, each lane tests one
-// pair's boxes against each other (ha_obb_near), and the candidates run the hull narrow phase in pair order. The box
-// table is rebuilt per batch because the narrow phases overwrite the scratch (26 hulls: one lane pass)
+// self-collision pass (ha_model_t v12; after every other pair, the oracle's order):
+//  1. the link hulls' world boxes (lane = hull, include/ha_obb.h ha_obb_world) into the narrow-phase scratch;
+//  2. one lane per pair tests the two boxes (ha_obb_near: circumscribed spheres, then 15 SAT axes); the candidate
+//     bits go to EnvLDS.selfm (the narrow phases below overwrite the scratch);
+//  3. per candidate, in pair order: if the pair's last narrow phase ended on a separating face (the env's per-pair
+//     byte in its global area), that one face is tested first, with the narrow phase's own expressions (world plane,
+//     the other hull's world vertices, min): still separating by more than the margin means the full narrow phase
+//     would stop on a face too (its SAT maximises over every face), so the pair is skipped with the same result.
+//     The record is a hint only: results never depend on it (the oracle has none);
+//  4. otherwise the hull narrow phase, which records the separating face for the next substep.
 HD void detect_self(SimCtx& c) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     int lane = c.lane, NLH = m.n_link_hulls, nsp = m.n_self_pairs;
     float mg = c.p->contact_margin;
     float (*ob)[16] = reinterpret_cast<float(*)[16]>(c.col.wvA);     // per hull: centre 3, R 9, half 3
+    if (lane < NLH) {
+        int L = m.hull_link[lane];
+        float* w = ob[lane];
+        ha_obb_world(s.lp[L], s.lq[L], m.hull_obb[lane], w, w + 3);
+        w[12] = m.hull_obb[lane][3]; w[13] = m.hull_obb[lane][4]; w[14] = m.hull_obb[lane][5];
+    }
+    c.colA_h = c.colB_h = -1;           // the box table overwrote the cached hull sides
+    c.colA_p = false;
+    wsync();
 #pragma unroll 1
     for (int base = 0; base < nsp; base += 64) {
-        if (lane < NLH) {
-            int L = m.hull_link[lane];
-            float* w = ob[lane];
-            ha_obb_world(s.lp[L], s.lq[L], m.hull_obb[lane], w, w + 3);
-            w[12] = m.hull_obb[lane][3]; w[13] = m.hull_obb[lane][4]; w[14] = m.hull_obb[lane][5];
-        }
-        c.colA_h = c.colB_h = -1;       // the box table overwrote the cached hull sides
-        c.colA_p = false;
-        wsync();
         int p = base + lane;
         bool cand = false;
         if (p < nsp) {
@@ -1476,18 +1508,48 @@ HD void detect_self(SimCtx& c) {
             self_pair_hulls(m, p, h1, h2);
             cand = ha_obb_near(ob[h1], ob[h1] + 3, ob[h1] + 12, ob[h2], ob[h2] + 3, ob[h2] + 12, mg) != 0;
         }
-        uint64_t mask = __ballot(cand);
-        wsync();
+        uint64_t mk = __ballot(cand);
+        if (lane == 0) {
+            s.selfm[base >> 5] = (uint32_t)mk;
+            s.selfm[(base >> 5) + 1] = (uint32_t)(mk >> 32);
+        }
+    }
+    wsync();
+#pragma unroll 1
+    for (int w32 = 0; w32 < (nsp + 31) >> 5; w32++) {
+        uint32_t mask = s.selfm[w32];
+#pragma unroll 1
         while (mask) {
-            int bit = __ffsll((unsigned long long)mask) - 1;
+            int bit = __ffs(mask) - 1;
             mask &= mask - 1;
-            int k = __builtin_amdgcn_readfirstlane(base + bit);
+            int k = __builtin_amdgcn_readfirstlane(32 * w32 + bit);
+            int h1, h2;
+            self_pair_hulls(m, k, h1, h2);
+            int La = m.hull_link[h1], Lb = m.hull_link[h2];
+            int rec = c.selfc ? (int)c.selfc[k] : 0xFF;
+            rec = __builtin_amdgcn_readfirstlane(rec);
+            if (rec != 0xFF) {
+                // the recorded face (side B: hull h2, else hull h1) against the other hull's vertices
+                bool fb = (rec & 0x80) != 0;
+                int hf = fb ? h2 : h1, hv = fb ? h1 : h2, kf = rec & 0x7F;
+                int Lf = fb ? Lb : La, Lv = fb ? La : Lb;
+                if (kf < m.hull_nplanes[hf]) {
+                    PoseF PF = PoseF{ld3(s.lp[Lf]), ldq(s.lq[Lf])}, PV = PoseF{ld3(s.lp[Lv]), ldq(s.lq[Lv])};
+                    f3 n;
+                    float d;
+                    world_plane(m, hf, kf, PF, false, mk3(1, 1, 1), n, d);
+                    float v = 3.0e38f;
+                    if (lane < m.hull_nverts[hv]) v = dot3(n, PV.p + qrot(PV.q, ld3(m.verts[m.hull_vert_start[hv] + lane]))) + d;
+                    if (wave_min(v) > mg) continue;         // separated on that face, as the narrow phase would find
+                }
+            }
 #ifdef HA_PROFILE
             c.pk = 5;
             unsigned long long _k0 = __builtin_amdgcn_s_memtime();
             int _nc0 = s.nc;
 #endif
             narrow_phase(c, 5, k, -1, 0);
+            if (c.selfc && lane == 0 && c.sepf != rec) c.selfc[k] = (uint8_t)c.sepf;
 #ifdef HA_PROFILE
             wsync();
             PROF_COUNT(80, __builtin_amdgcn_s_memtime() - _k0);          // self pairs: time / pairs / with contacts

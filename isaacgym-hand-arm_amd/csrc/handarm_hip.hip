@@ -429,7 +429,9 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.col = col_view<PC>(&c.s->u);
     c.o = reinterpret_cast<ObjLDS*>(smem + obj_lds_offset<PC>());
     c.k = reinterpret_cast<ContactLDS*>(smem + contact_lds_offset<PC>());
-    c.spill = (PC::split || PC::ovf) ? spill + (size_t)env * PC::spill_floats : nullptr;
+    c.spill = (PC::split || PC::ovf || PC::selfc) ? spill + (size_t)env * PC::spill_floats : nullptr;
+    c.selfc = PC::selfc ? reinterpret_cast<uint8_t*>(c.spill + PC::off_selfc) : nullptr;
+    c.sepf = 0xFF;
     c.maxc = PC::cap * NCH;
     // overflow chunks: contact entries past chunk 0 in the env's global area (null otherwise: ct_global folds away)
     c.kg = PC::ovf ? reinterpret_cast<ContactLDS*>(c.spill + PC::off_ct) : nullptr;
@@ -881,7 +883,12 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     HIPCHK(hipMalloc(&h->d_params, sizeof(ha_params_t)));
     HIPCHK(hipMemcpy(h->d_model, model, sizeof(ha_model_t), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->d_params, params, sizeof(ha_params_t), hipMemcpyHostToDevice));
-    if (spill_floats(fam)) HIPCHK(hipMalloc(&h->d_spill, sizeof(float) * spill_floats(fam) * (size_t)num_envs));
+    if (spill_floats(fam)) {
+        HIPCHK(hipMalloc(&h->d_spill, sizeof(float) * spill_floats(fam) * (size_t)num_envs));
+        // every byte 0xFF: the self-collision records start as "no separating face" (the other areas are written
+        // before they are read)
+        HIPCHK(hipMemset(h->d_spill, 0xFF, sizeof(float) * spill_floats(fam) * (size_t)num_envs));
+    }
     for (int mode : {MODE_STEP, MODE_SIMULATE, MODE_OBSERVE, MODE_RESET})
         HIPCHK(hipFuncSetAttribute((const void*)kernel_for(h->fam, mode), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds_bytes(h->fam)));
