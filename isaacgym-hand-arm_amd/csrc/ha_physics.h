@@ -1446,11 +1446,14 @@ HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
         h1 = A; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = m.static_hull[B];
         P2 = static_pose(m, B); b2 = -1; k2 = -100 - B;
     } else {
-        // self-collision: link hull a (side A) against link hull b (side B), normal from b to a
-        self_pair_hulls(m, A, h1, h2);
-        int La = m.hull_link[h1], Lb = m.hull_link[h2];
-        P1 = PoseF{ld3(s.lp[La]), ldq(s.lq[La])}; b1 = 100 + La;
-        P2 = PoseF{ld3(s.lp[Lb]), ldq(s.lq[Lb])}; b2 = 100 + Lb; k2 = b2;
+        // self-collision pair (a, b), a < b: hull b on side A, hull a on side B (normal from a to b). Consecutive pairs
+        // share hull a, so side B's world vertices / planes stay in the scratch and a pair whose side-A sphere clears one
+        // of a's planes never sets up side A
+        int ha_, hb_;
+        self_pair_hulls(m, A, ha_, hb_);
+        int La = m.hull_link[ha_], Lb = m.hull_link[hb_];
+        h1 = hb_; P1 = PoseF{ld3(s.lp[Lb]), ldq(s.lq[Lb])}; b1 = 100 + Lb;
+        h2 = ha_; P2 = PoseF{ld3(s.lp[La]), ldq(s.lq[La])}; b2 = 100 + La; k2 = b2;
     }
     collide_hulls(c, h1, P1, h2, P2, b1, b2, b1, k2);
 }
@@ -1529,10 +1532,10 @@ HD void detect_self(SimCtx& c) {
             int rec = c.selfc ? (int)c.selfc[k] : 0xFF;
             rec = __builtin_amdgcn_readfirstlane(rec);
             if (rec != 0xFF) {
-                // the recorded face (side B: hull h2, else hull h1) against the other hull's vertices
+                // the recorded face (side B: hull a = h1, side A: hull b = h2) against the other hull's vertices
                 bool fb = (rec & 0x80) != 0;
-                int hf = fb ? h2 : h1, hv = fb ? h1 : h2, kf = rec & 0x7F;
-                int Lf = fb ? Lb : La, Lv = fb ? La : Lb;
+                int hf = fb ? h1 : h2, hv = fb ? h2 : h1, kf = rec & 0x7F;
+                int Lf = fb ? La : Lb, Lv = fb ? Lb : La;
                 if (kf < m.hull_nplanes[hf]) {
                     PoseF PF = PoseF{ld3(s.lp[Lf]), ldq(s.lq[Lf])}, PV = PoseF{ld3(s.lp[Lv]), ldq(s.lq[Lv])};
                     f3 n;
@@ -1543,12 +1546,21 @@ HD void detect_self(SimCtx& c) {
                     if (wave_min(v) > mg) continue;         // separated on that face, as the narrow phase would find
                 }
             }
+#ifdef HA_X_SELF_NO_NARROW    /* A/B timing builds only: the self pass without its narrow phases */
+            continue;
+#endif
 #ifdef HA_PROFILE
             c.pk = 5;
             unsigned long long _k0 = __builtin_amdgcn_s_memtime();
             int _nc0 = s.nc;
 #endif
+#ifdef HA_X_SELF_DRY      /* A/B timing builds only: self narrow phases that emit no contacts */
+            c.dry = true;
+#endif
             narrow_phase(c, 5, k, -1, 0);
+#ifdef HA_X_SELF_DRY
+            c.dry = false;
+#endif
             if (c.selfc && lane == 0 && c.sepf != rec) c.selfc[k] = (uint8_t)c.sepf;
 #ifdef HA_PROFILE
             wsync();

@@ -162,7 +162,11 @@ using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_c
                         task_chunk_capacity<FAM>(), task_col_verts<FAM>(), task_col_planes<FAM>(),
                         task_compact<FAM>() ? 1 : -1, task_compact<FAM>() ? 0 : HA_MAX_GATHER, task_compact<FAM>(),
                         FAM == FAM_UR5SIH_CLUTTER && HB_RECOMPUTE, task_overflow<FAM>(),
+#ifdef HA_X_NO_SELF     /* A/B timing builds only: the Allegro families without their self-collision pass */
+                        false>;
+#else
                         FAM == HA_TASK_ALLEGRO_HAND || FAM == HA_TASK_ALLEGRO_KUKA>;
+#endif
 
 
 // ----------------------------------------------------------------------------- state load/store

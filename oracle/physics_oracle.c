@@ -746,7 +746,7 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
         }
     }
     /* self-collision (v12): link hull pairs of non-adjacent links whose oriented boxes come within the margin
-       (include/ha_obb.h, the kernel's mid-phase), normal from hull b to hull a */
+       (include/ha_obb.h, the kernel's mid-phase) */
     for (int k = 0; k < m->n_self_pairs; k++) {
         int ha = m->self_pair[k] & 255, hb = m->self_pair[k] >> 8;
         int la = m->hull_link[ha], lb = m->hull_link[hb];
@@ -756,8 +756,9 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
         ha_obb_world(pa, qa, m->hull_obb[ha], ca, Ra);
         ha_obb_world(pb, qb, m->hull_obb[hb], cb, Rb);
         if (!ha_obb_near(ca, Ra, m->hull_obb[ha] + 3, cb, Rb, m->hull_obb[hb] + 3, mg)) continue;
+        /* hull b on side A, hull a on side B (ha_physics.h narrow_phase kind 5): normal from a to b */
         pose_t PA = {e->lp[la], e->lq[la]}, PB = {e->lp[lb], e->lq[lb]};
-        collide_hulls(m, ha, PA, hb, PB, mg, 100 + la, 100 + lb, NULL, NULL, out, &nout, h->maxc);
+        collide_hulls(m, hb, PB, ha, PA, mg, 100 + lb, 100 + la, NULL, NULL, out, &nout, h->maxc);
     }
     return nout;
 }
