@@ -1493,6 +1493,9 @@ HD void detect_self(SimCtx& c) {
     int lane = c.lane, NLH = m.n_link_hulls, nsp = m.n_self_pairs;
     float mg = c.p->contact_margin;
     float (*ob)[16] = reinterpret_cast<float(*)[16]>(c.col.wvA);     // per hull: centre 3, R 9, half 3
+#ifdef HA_PROFILE
+    unsigned long long _s0 = __builtin_amdgcn_s_memtime();
+#endif
     if (lane < NLH) {
         int L = m.hull_link[lane];
         float* w = ob[lane];
@@ -1518,6 +1521,9 @@ HD void detect_self(SimCtx& c) {
         }
     }
     wsync();
+#ifdef HA_PROFILE
+    PROF_COUNT(83, __builtin_amdgcn_s_memtime() - _s0);              // box table + box tests
+#endif
 #pragma unroll 1
     for (int w32 = 0; w32 < (nsp + 31) >> 5; w32++) {
         uint32_t mask = s.selfm[w32];
@@ -1529,8 +1535,15 @@ HD void detect_self(SimCtx& c) {
             int h1, h2;
             self_pair_hulls(m, k, h1, h2);
             int La = m.hull_link[h1], Lb = m.hull_link[h2];
+#ifdef HA_PROFILE
+            unsigned long long _r0 = __builtin_amdgcn_s_memtime();
+            PROF_COUNT(85, 1);                                              // candidates
+#endif
             int rec = c.selfc ? (int)c.selfc[k] : 0xFF;
             rec = __builtin_amdgcn_readfirstlane(rec);
+#ifdef HA_PROFILE
+            PROF_COUNT(86, rec != 0xFF);                                    // candidates with a record
+#endif
             if (rec != 0xFF) {
                 // the recorded face (side B: hull a = h1, side A: hull b = h2) against the other hull's vertices
                 bool fb = (rec & 0x80) != 0;
@@ -1543,7 +1556,13 @@ HD void detect_self(SimCtx& c) {
                     world_plane(m, hf, kf, PF, false, mk3(1, 1, 1), n, d);
                     float v = 3.0e38f;
                     if (lane < m.hull_nverts[hv]) v = dot3(n, PV.p + qrot(PV.q, ld3(m.verts[m.hull_vert_start[hv] + lane]))) + d;
-                    if (wave_min(v) > mg) continue;         // separated on that face, as the narrow phase would find
+                    bool skip = wave_min(v) > mg;
+#ifdef HA_PROFILE
+                    wsync();
+                    PROF_COUNT(84, __builtin_amdgcn_s_memtime() - _r0);    // record checks
+                    PROF_COUNT(87, skip);                                   // skipped by their record
+#endif
+                    if (skip) continue;                     // separated on that face, as the narrow phase would find
                 }
             }
 #ifdef HA_X_SELF_NO_NARROW    /* A/B timing builds only: the self pass without its narrow phases */

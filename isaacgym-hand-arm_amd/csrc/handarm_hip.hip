@@ -548,6 +548,8 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
 #if defined(HA_PROFILE) || defined(HA_ENVT)
 // diagnostic builds: each workgroup's start / end on the constant 100 MHz clock (s_memrealtime), by launch slot
 __device__ unsigned long long g_envt[2 * 65536];
+// and where it ran: HW_ID (wave, SIMD, CU, SH, SE bits) and XCC_ID of its wave
+__device__ unsigned int g_envhw[2 * 65536];
 // (the start stamp is stored right away: an s_memrealtime value kept live across the whole kernel made the backend
 // stop with "illegal VGPR to SGPR copy" in the overflow-chunk families)
 #define HA_ENV_T0()                                                                               \
@@ -558,7 +560,11 @@ __device__ unsigned long long g_envt[2 * 65536];
 #define HA_ENV_T1()                                                                               \
     do {                                                                                          \
         __syncthreads();                                                                          \
-        if (threadIdx.x == 0 && blockIdx.x < 65536) g_envt[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime(); \
+        if (threadIdx.x == 0 && blockIdx.x < 65536) {                                            \
+            g_envt[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();                          \
+            g_envhw[2 * blockIdx.x] = __builtin_amdgcn_s_getreg((31 << 11) | 4);                    \
+            g_envhw[2 * blockIdx.x + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);               \
+        }                                                                                           \
     } while (0)
 #else
 #define HA_ENV_T0()
@@ -1317,6 +1323,12 @@ extern "C" int ha_profile_read(unsigned long long* out32, int reset) {
 extern "C" int ha_profile_env_times(unsigned long long* out, int n) {
     if (n < 0 || n > 65536) return HA_E_ARG;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_envt), sizeof(unsigned long long) * 2 * n) != hipSuccess) return HA_E_HIP;
+    return HA_OK;
+}
+// (HW_ID, XCC_ID) of each workgroup of that launch
+extern "C" int ha_profile_env_hw(unsigned int* out, int n) {
+    if (n < 0 || n > 65536) return HA_E_ARG;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_envhw), sizeof(unsigned int) * 2 * n) != hipSuccess) return HA_E_HIP;
     return HA_OK;
 }
 #endif

@@ -11,17 +11,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "isaacgym-hand-arm_amd")]
 from handarm_hip import _lib, build  # noqa: E402
 
-PROF_LIB = os.path.join(build.PKG, "libhandarm_hip_prof.so")
-ENVT_LIB = os.path.join(build.PKG, "libhandarm_hip_envt.so")     # -DHA_ENVT: workgroup spans only (no phase atomics)
+PROF_LIB = os.path.join(build.PKG, os.environ.get("HA_PROF_LIB", "libhandarm_hip_prof.so"))   # A/B: another name
+ENVT_LIB = os.path.join(build.PKG, os.environ.get("HA_ENVT_LIB", "libhandarm_hip_envt.so"))     # -DHA_ENVT: workgroup spans only (no phase atomics)
 PHASES = ["fk", "dynamics(CRBA+RNEA)", "chol+Minv+free+objects", "detect", "contact rows J,Y", "joint rows", "PGS",
           "forces+integrate"]
 
 if __name__ == "__main__":
     if "--build" in sys.argv:
-        # -DHA_AK_CHUNKS=1: with the phase stamps, hipcc 7.2's backend stops on the AllegroKuka overflow chunk
-        # ("illegal VGPR to SGPR copy"); the diagnostic builds profile AllegroKuka with its LDS chunk only (the product
-        # overflows in ~2% of C2 substeps)
-        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", *build.FLAGS, "-DHA_AK_CHUNKS=1", "-DHA_PROFILE", "-I", build.INCLUDE,
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", *build.FLAGS, *sys.argv[sys.argv.index("--build") + 1:], "-DHA_PROFILE", "-I", build.INCLUDE,
                "-o", PROF_LIB, os.path.join(build.CSRC, "handarm_hip.hip")]
         subprocess.check_call(cmd)
         subprocess.check_call([x if x != "-DHA_PROFILE" else "-DHA_ENVT" for x in cmd[:-3]] + ["-o", ENVT_LIB, cmd[-1]])
@@ -48,6 +45,10 @@ if __name__ == "__main__":
             t_, n_, h_ = (10 + k, 15 + k, 20 + k) if k < 5 else (80, 81, 82)       # self pairs (kind 5) at 80..82
             print(f"    narrow {name:10s}: {buf[n_] / sub:6.2f} pairs/substep, {buf[h_] / sub:6.2f} with contacts, "
                   f"{100.0 * buf[t_] / tot:5.1f}% of substep cycles", flush=True)
+        if buf[85]:
+            print(f"    self pass: box table + box tests {100.0 * buf[83] / tot:5.1f}%, {buf[85] / sub:6.2f} candidates/substep, "
+                  f"{buf[86] / sub:6.2f} with a record, {buf[87] / sub:6.2f} skipped by it; record checks "
+                  f"{100.0 * buf[84] / tot:5.1f}%", flush=True)
         print("    hull-hull split: " + "  ".join(f"{nm} {100.0 * buf[25 + i] / tot:5.1f}%" for i, nm in
               enumerate(["setup", "SAT A", "SAT B", "incident", "emit", "edge-edge", "clip"])), flush=True)
         for k, name in enumerate(["obj-ground", "obj-static", "obj-obj", "link-obj", "link-static", "link-link"]):
@@ -114,6 +115,20 @@ if __name__ == "__main__":
             tb = (C.c_ulonglong * (2 * n))()
             lib.ha_profile_env_times(tb, n)
             t = np.frombuffer(tb, dtype=np.uint64).reshape(n, 2).astype(np.int64)
+            # the stamps are per launch slot; slot i ran env order[i] (ha_set_env_order): per env from here on
+            order = sim._env_order.cpu().numpy() if getattr(sim, "rebalance_every", 0) > 0 else np.arange(n)
+            t_env = np.empty_like(t)
+            t_env[order] = t
+            t = t_env
+            hw = None
+            if hasattr(lib, "ha_profile_env_hw"):
+                hb = (C.c_uint * (2 * n))()
+                lib.ha_profile_env_hw.argtypes = [C.POINTER(C.c_uint), C.c_int]
+                lib.ha_profile_env_hw(hb, n)
+                hw = np.frombuffer(hb, dtype=np.uint32).reshape(n, 2).copy()
+                hw_env = np.empty_like(hw)
+                hw_env[order] = hw
+                hw = hw_env
             t0 = t[:, 0].min()
             dur = (t[:, 1] - t[:, 0]) * 0.01          # us
             st = (t[:, 0] - t0) * 0.01
@@ -129,6 +144,27 @@ if __name__ == "__main__":
                 print(f"  duration p{lo}-p{hi} ({a:.0f}-{b:.0f} us): {sel.sum()} envs, resets {rb[sel].mean():.3f}, "
                       f"contacts offered/substep {off[sel].mean():.2f}, mean of the env max offered (run) {cs[sel, 2].mean():.1f}, "
                       f"over capacity {cs[sel, 1].sum() / max(cs[sel, 0].sum(), 1):.4f}", flush=True)
+            print(f"  corr(duration, contacts offered/substep) {np.corrcoef(dur, off)[0, 1]:.3f}, "
+                  f"corr(duration, env max offered) {np.corrcoef(dur, cs[:, 2])[0, 1]:.3f}", flush=True)
+            if hw is not None:
+                # HW_ID: SIMD [5:4], CU [11:8], SH [12], SE [15:13]; XCC_ID [3:0]
+                h0, xcc = hw[:, 0], hw[:, 1] & 15
+                simd, cu, sh, se = (h0 >> 4) & 3, (h0 >> 8) & 15, (h0 >> 12) & 1, (h0 >> 13) & 7
+                cu_key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+                simd_key = cu_key * 4 + simd
+                for name, key in (("CU", cu_key), ("SIMD", simd_key)):
+                    u, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+                    tot = np.bincount(inv, weights=dur)
+                    mx = np.zeros(len(u)); np.maximum.at(mx, inv, dur)
+                    print(f"  per {name}: {len(u)} used, envs each min {cnt.min()} max {cnt.max()}; summed env time "
+                          f"min {tot.min():.0f} p50 {np.median(tot):.0f} max {tot.max():.0f} us; slowest env per {name} "
+                          f"min {mx.min():.0f} p50 {np.median(mx):.0f} max {mx.max():.0f} us", flush=True)
+                    top = np.argsort(dur)[-max(n // 100, 1):]
+                    print(f"    the 1% slowest envs: their {name}'s summed env time p50 {np.median(tot[inv[top]]):.0f} us "
+                          f"(all: {np.median(tot[inv]):.0f})", flush=True)
+                xs = np.unique(xcc)
+                print("  per XCC: " + "  ".join(f"{x}: p50 {np.median(dur[xcc == x]):.0f} max {dur[xcc == x].max():.0f}"
+                                                for x in xs), flush=True)
             hist, edges = np.histogram(dur, bins=12)
             print("  histogram: " + "  ".join(f"{edges[i]:.0f}:{hist[i]}" for i in range(12)), flush=True)
         sys.exit(0)
