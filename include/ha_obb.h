@@ -41,14 +41,20 @@ HA_OB_FN void ha_obb_world(const float* lp, const float* lq, const float* ob, fl
     c[2] = lp[2] + ((vz + w * tz) + (x * ty - y * tx));
 }
 
-/* boxes (ca, Ra, half extents ha) and (cb, Rb, hb) within the margin mg of each other: their circumscribed spheres
- * first (one distance), then all 15 SAT axes */
-HA_OB_FN int ha_obb_near(const float* ca, const float* Ra, const float* ha, const float* cb, const float* Rb,
-                         const float* hb, float mg) {
+/* radius of a box's circumscribed sphere (half extents h) */
+HA_OB_FN float ha_obb_radius(const float* h) { return sqrtf((h[0] * h[0] + h[1] * h[1]) + h[2] * h[2]); }
+
+/* the circumscribed spheres (centres ca, cb, radii ra, rb from ha_obb_radius) within the margin mg */
+HA_OB_FN int ha_obb_spheres_near(const float* ca, float ra, const float* cb, float rb, float mg) {
     float T0 = cb[0] - ca[0], T1 = cb[1] - ca[1], T2 = cb[2] - ca[2];
-    float rs = (sqrtf((ha[0] * ha[0] + ha[1] * ha[1]) + ha[2] * ha[2]) + sqrtf((hb[0] * hb[0] + hb[1] * hb[1]) + hb[2] * hb[2]))
-               + mg;
-    if ((T0 * T0 + T1 * T1) + T2 * T2 > rs * rs) return 0;
+    float rs = (ra + rb) + mg;
+    return !((T0 * T0 + T1 * T1) + T2 * T2 > rs * rs);
+}
+
+/* boxes (ca, Ra, half extents ha) and (cb, Rb, hb) not separated by more than mg on any of the 15 SAT axes */
+HA_OB_FN int ha_obb_sat(const float* ca, const float* Ra, const float* ha, const float* cb, const float* Rb,
+                        const float* hb, float mg) {
+    float T0 = cb[0] - ca[0], T1 = cb[1] - ca[1], T2 = cb[2] - ca[2];
     float R[3][3], AR[3][3], t[3];
     for (int i = 0; i < 3; i++) {
         t[i] = (Ra[i] * T0 + Ra[3 + i] * T1) + Ra[6 + i] * T2;
@@ -80,6 +86,14 @@ HA_OB_FN int ha_obb_near(const float* ca, const float* Ra, const float* ha, cons
         }
     }
     return 1;
+}
+
+/* boxes (ca, Ra, half extents ha) and (cb, Rb, hb) within the margin mg of each other: their circumscribed spheres
+ * first (one distance), then all 15 SAT axes */
+HA_OB_FN int ha_obb_near(const float* ca, const float* Ra, const float* ha, const float* cb, const float* Rb,
+                         const float* hb, float mg) {
+    if (!ha_obb_spheres_near(ca, ha_obb_radius(ha), cb, ha_obb_radius(hb), mg)) return 0;
+    return ha_obb_sat(ca, Ra, ha, cb, Rb, hb, mg);
 }
 
 #undef HA_OB_FN

@@ -1478,9 +1478,12 @@ HD void gather_emit(SimCtx& c, int kind, int A, int B) {
 }
 
 // self-collision pass (ha_model_t v12; after every other pair, the oracle's order):
-//  1. the link hulls' world boxes (lane = hull, include/ha_obb.h ha_obb_world) into the narrow-phase scratch;
-//  2. one lane per pair tests the two boxes (ha_obb_near: circumscribed spheres, then 15 SAT axes); the candidate
-//     bits go to EnvLDS.selfm (the narrow phases below overwrite the scratch);
+//  1. the link hulls' world boxes (lane = hull, include/ha_obb.h ha_obb_world) and their circumscribed radii into the
+//     narrow-phase scratch, component-major (lanes reading different hulls read consecutive words);
+//  2. one lane per pair tests the two spheres (ha_obb_spheres_near); the pairs that pass are compacted, in pair order,
+//     and one lane per such pair runs the 15 SAT axes (ha_obb_sat) - the oracle's ha_obb_near, split so that the
+//     axis tests run on full waves. The candidate bits go to EnvLDS.selfm (the narrow phases below overwrite the
+//     scratch), and the first 64 candidates' records are loaded into a register at once;
 //  3. per candidate, in pair order: if the pair's last narrow phase ended on a separating face (the env's per-pair
 //     byte in its global area), that one face is tested first, with the narrow phase's own expressions (world plane,
 //     the other hull's world vertices, min): still separating by more than the margin means the full narrow phase
@@ -1492,38 +1495,71 @@ HD void detect_self(SimCtx& c) {
     const ha_model_t& m = *c.m;
     int lane = c.lane, NLH = m.n_link_hulls, nsp = m.n_self_pairs;
     float mg = c.p->contact_margin;
-    float (*ob)[16] = reinterpret_cast<float(*)[16]>(c.col.wvA);     // per hull: centre 3, R 9, half 3
+    float* tab = reinterpret_cast<float*>(c.col.wvA);        // tab[comp NLH + hull]: centre 3, R 9, half 3, radius
+    uint16_t* spl = reinterpret_cast<uint16_t*>(tab + 16 * NLH);     // pairs whose spheres are near
+    uint16_t* cdl = spl + nsp;                                       // the first 64 candidates
 #ifdef HA_PROFILE
     unsigned long long _s0 = __builtin_amdgcn_s_memtime();
 #endif
     if (lane < NLH) {
         int L = m.hull_link[lane];
-        float* w = ob[lane];
+        float w[15];
         ha_obb_world(s.lp[L], s.lq[L], m.hull_obb[lane], w, w + 3);
         w[12] = m.hull_obb[lane][3]; w[13] = m.hull_obb[lane][4]; w[14] = m.hull_obb[lane][5];
+        for (int i = 0; i < 15; i++) tab[i * NLH + lane] = w[i];
+        tab[15 * NLH + lane] = ha_obb_radius(w + 12);
     }
+    if (lane < HA_MAX_SELF_PAIRS / 32) s.selfm[lane] = 0u;
     c.colA_h = c.colB_h = -1;           // the box table overwrote the cached hull sides
     c.colA_p = false;
     wsync();
+    const uint64_t below = (1ull << lane) - 1ull;
+    int nsl = 0;
 #pragma unroll 1
     for (int base = 0; base < nsp; base += 64) {
         int p = base + lane;
-        bool cand = false;
+        bool near = false;
         if (p < nsp) {
             int h1, h2;
             self_pair_hulls(m, p, h1, h2);
-            cand = ha_obb_near(ob[h1], ob[h1] + 3, ob[h1] + 12, ob[h2], ob[h2] + 3, ob[h2] + 12, mg) != 0;
+            float ca[3] = {tab[h1], tab[NLH + h1], tab[2 * NLH + h1]};
+            float cb[3] = {tab[h2], tab[NLH + h2], tab[2 * NLH + h2]};
+            near = ha_obb_spheres_near(ca, tab[15 * NLH + h1], cb, tab[15 * NLH + h2], mg) != 0;
         }
-        uint64_t mk = __ballot(cand);
-        if (lane == 0) {
-            s.selfm[base >> 5] = (uint32_t)mk;
-            s.selfm[(base >> 5) + 1] = (uint32_t)(mk >> 32);
-        }
+        uint64_t mk = __ballot(near);
+        if (near) spl[nsl + __popcll(mk & below)] = (uint16_t)p;
+        nsl += __popcll(mk);
     }
     wsync();
+    int ncd = 0;
+#pragma unroll 1
+    for (int base = 0; base < nsl; base += 64) {
+        int i = base + lane, p = 0;
+        bool cand = false;
+        if (i < nsl) {
+            p = spl[i];
+            int h1, h2;
+            self_pair_hulls(m, p, h1, h2);
+            float A[15], B[15];
+            for (int q = 0; q < 15; q++) { A[q] = tab[q * NLH + h1]; B[q] = tab[q * NLH + h2]; }
+            cand = ha_obb_sat(A, A + 3, A + 12, B, B + 3, B + 12, mg) != 0;
+        }
+        uint64_t mk = __ballot(cand);
+        if (cand) {
+            atomicOr(&s.selfm[p >> 5], 1u << (p & 31));
+            int r = ncd + __popcll(mk & below);
+            if (r < 64) cdl[r] = (uint16_t)p;
+        }
+        ncd += __popcll(mk);
+    }
+    wsync();
+    // the records of the first 64 candidates (in pair order, the order of the loop below), one load for all
+    int crec = 0xFF;
+    if (c.selfc && lane < ncd) crec = c.selfc[cdl[lane]];
 #ifdef HA_PROFILE
     PROF_COUNT(83, __builtin_amdgcn_s_memtime() - _s0);              // box table + box tests
 #endif
+    int rank = 0;
 #pragma unroll 1
     for (int w32 = 0; w32 < (nsp + 31) >> 5; w32++) {
         uint32_t mask = s.selfm[w32];
@@ -1539,8 +1575,10 @@ HD void detect_self(SimCtx& c) {
             unsigned long long _r0 = __builtin_amdgcn_s_memtime();
             PROF_COUNT(85, 1);                                              // candidates
 #endif
-            int rec = c.selfc ? (int)c.selfc[k] : 0xFF;
-            rec = __builtin_amdgcn_readfirstlane(rec);
+            int rec;
+            if (rank < 64) rec = __builtin_amdgcn_readlane(crec, rank);
+            else rec = __builtin_amdgcn_readfirstlane(c.selfc ? (int)c.selfc[k] : 0xFF);
+            rank++;
 #ifdef HA_PROFILE
             PROF_COUNT(86, rec != 0xFF);                                    // candidates with a record
 #endif

@@ -860,9 +860,10 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     // self-collision pairs (v12): two link hulls of the model each; only the Allegro families' kernels run them
     if (model->n_self_pairs < 0 || model->n_self_pairs > HA_MAX_SELF_PAIRS) return HA_E_MODEL;
     if (model->n_self_pairs > 0 && params->task == HA_TASK_UR5SIH) return HA_E_MODEL;
-    // the self-pair pass keeps a 64-byte world box per link hull in the narrow-phase scratch (detect_self)
+    // the self-pair pass keeps a 64-byte world box per link hull, a 2-byte entry per pair and 64 candidate entries in
+    // the narrow-phase scratch (detect_self)
     if (model->n_self_pairs > 0 &&
-        (size_t)model->n_link_hulls * 64 > (fam == HA_TASK_ALLEGRO_HAND ? FamPhys<HA_TASK_ALLEGRO_HAND>::col_bytes
+        (size_t)model->n_link_hulls * 64 + 2 * (size_t)model->n_self_pairs + 128 > (fam == HA_TASK_ALLEGRO_HAND ? FamPhys<HA_TASK_ALLEGRO_HAND>::col_bytes
                                                                         : FamPhys<HA_TASK_ALLEGRO_KUKA>::col_bytes))
         return HA_E_MODEL;
     for (int k = 0; k < model->n_self_pairs; k++) {
