@@ -27,6 +27,8 @@
  *   ha_task_reset                  reset_idx steady state (multi_object_manipulation.py:33-71)
  *   ha_task_epilogue               VecTask.step's torch.clamp(obs_buf) and the AllegroKuka extras means
  *                                  (vec_task.py:437, allegro_kuka_base.py:908-917)
+ *   ha_task_step_io                VecTask.step whole for the Allegro tasks: the action clamp (vec_task.py:400-404),
+ *                                  the fused step and the epilogue's outputs, in ONE launch
  *   ha_pointclouds                 synthetic point-cloud observables' post_step refresh
  *                                  (multi_object.py:792-809, ur5sih.py:361-374)
  *   ha_gather_obs                  compute_observations' torch.cat for a custom observation list
@@ -304,7 +306,7 @@ typedef struct ha_state_t {
     float* sim_targets;         /* [N][D] position targets the physics sees */
     float* dof_position_targets;/* [N][D] task-side tensor (observed) */
     /* task */
-    const float* actions;       /* [N][11] */
+    const float* actions;       /* [N][11] (ha_task_step_io stores the clamped caller actions here) */
     float* obs;                 /* [N][147] */
     float* teacher_obs;         /* [N][147] */
     float* rew;                 /* [N] */
@@ -458,6 +460,13 @@ int ha_task_reset(ha_handle h, uint32_t flags, void* stream);
  * N x num_obs floats) = clamp(obs, -clip_obs, clip_obs); AllegroKuka only: scalars (if non-null, 4 floats) =
  * mean prev_episode_successes, mean / min / max true_objective over the shard. */
 int ha_task_epilogue(ha_handle h, float* obs_out, float clip_obs, float* scalars, void* stream);
+/* ha_task_step with VecTask.step's head and tail inside the same launch (AllegroHand / AllegroKuka handles; HA_E_ARG
+ * otherwise): actions (if non-null, N x num_actions floats, the caller's raw actions) are clamped to
+ * +-clip_actions where the task reads them and stored clamped into the bound actions tensor (vec_task.py:400-404);
+ * obs_out and scalars as ha_task_epilogue (scalars: AllegroKuka only; reduced in a fixed order by the launch's last
+ * workgroups, so the values are deterministic but may differ from ha_task_epilogue's in the last bits). */
+int ha_task_step_io(ha_handle h, uint32_t flags, const float* actions, float clip_actions, float* obs_out,
+                    float clip_obs, float* scalars, void* stream);
 /* v9: contacts per substep the handle's kernel family holds (over it, the shallowest give way) */
 int ha_contact_capacity(ha_handle h);
 /* v11: dispatch order of the full-shard launches (no gym counterpart: a scheduling hint; results do not depend on

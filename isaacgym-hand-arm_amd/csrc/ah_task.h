@@ -129,7 +129,8 @@ HD void ah_controller(SimCtx& c, const ha_state_t& st, int env) {
     int lane = c.lane, D = c.D;
     if (lane < D) {
         float lo = m.dof_lower[lane], up = m.dof_upper[lane];
-        float a = st.actions[(size_t)env * AH_NUM_ACT + lane];
+        float a = act_at(c, st, (size_t)env * AH_NUM_ACT + lane);
+        if (c.act_in) const_cast<float*>(st.actions)[(size_t)env * AH_NUM_ACT + lane] = a;          // the task's stored actions
         float* prev = st.dof_position_targets + (size_t)env * D;
         float cur = 0.5f * (a + 1.0f) * (up - lo) + lo;                           // scale()
         cur = p.ah_act_moving_average * cur + p.sih_beta * prev[lane];           // sih_beta := 1 - ama (python double)
@@ -146,7 +147,6 @@ HD void ah_post(SimCtx& c, const ha_state_t& st, int env, const AhIn& in, bool o
     const ha_params_t& p = *c.p;
     int lane = c.lane, D = c.D;
     const float* gs = st.goal_state + (size_t)env * 7;
-    const float* act = st.actions + (size_t)env * AH_NUM_ACT;
     float qdiff[4];
     {
         float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
@@ -164,8 +164,9 @@ HD void ah_post(SimCtx& c, const ha_state_t& st, int env, const AhIn& in, bool o
         else if (k < 61) v = p.ah_vel_obs_scale * in.obj[k - 48];                // angvel
         else if (k < 68) v = gs[k - 61];
         else if (k < 72) v = qdiff[k - 68];
-        else v = act[k - 72];
+        else v = act_at(c, st, (size_t)env * AH_NUM_ACT + (k - 72));
         ob[k] = v;
+        obs_out_put(c, (size_t)env * AH_NUM_OBS + k, v);
     }
     if (obs_only) return;
     if (lane == 0) {
@@ -176,7 +177,10 @@ HD void ah_post(SimCtx& c, const ha_state_t& st, int env, const AhIn& in, bool o
         float dist_rew = goal_dist * p.ah_dist_reward_scale;
         float rot_rew = 1.0f / (fabsf(rot_dist) + p.ah_rot_eps) * p.ah_rot_reward_scale;
         float ap = 0.0f;
-        for (int k = 0; k < AH_NUM_ACT; k++) ap += act[k] * act[k];
+        for (int k = 0; k < AH_NUM_ACT; k++) {
+            float ak = act_at(c, st, (size_t)env * AH_NUM_ACT + k);
+            ap += ak * ak;
+        }
         float reward = dist_rew + rot_rew + ap * p.ah_action_penalty_scale;
         int64_t goal_resets = fabsf(rot_dist) <= p.ah_success_tolerance ? 1 : st.reset_goal_buf[env];
         float succ = st.successes[env] + (float)goal_resets;

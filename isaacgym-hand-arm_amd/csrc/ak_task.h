@@ -198,7 +198,8 @@ HD void ak_controller(SimCtx& c, const ha_state_t& st, int env) {
     int lane = c.lane, D = c.D;
     if (lane < D) {
         float lo = m.dof_lower[lane], up = m.dof_upper[lane];
-        float a = st.actions[(size_t)env * AK_NUM_ACT + lane];
+        float a = act_at(c, st, (size_t)env * AK_NUM_ACT + lane);
+        if (c.act_in) const_cast<float*>(st.actions)[(size_t)env * AK_NUM_ACT + lane] = a;          // the task's stored actions
         float* prev = st.dof_position_targets + (size_t)env * D;
         float cur;
         if (lane >= p.ak_num_arm_dofs) {
@@ -398,6 +399,7 @@ HD void ak_post(SimCtx& c, const ha_state_t& st, int env, AkPost& ak, bool obs_o
         float v = ak.obs[k];
         if (clampv > 0.0f && !obs_only) v = fminf(fmaxf(v, -clampv), clampv);   // clamp_obs (post_physics_step)
         og[k] = v;
+        obs_out_put(c, (size_t)env * nobs + k, v);
     }
     if (lane < AK_TS_KP) tsg[lane] = ak.ts[lane];
 }

@@ -326,13 +326,30 @@ struct SimCtx {
     // k: face k of side A, 0xFF: none), and the env's per-pair record of it in its global area (null otherwise)
     int sepf;
     uint8_t* selfc;
+    // VecTask.step's head and tail folded into the step launch (ha_task_step_io; null / unused otherwise): the caller's
+    // raw actions, clamped to +-clip_act where the task reads them (act_at), and a second, clamped copy of obs
+    const float* act_in;
+    float* obs_out;
+    float clip_act, clip_obs;
 #ifdef HA_PROFILE
     int pk;                 // profiled build: kind of the running pair
+    int pcls;               // profiled build: this substep is heavy (g_prof's second set)
 #endif
 #ifdef HA_AB_TIMING
     bool dry;               // A/B timing builds only: a repeated phase that must not emit contacts
 #endif
 };
+
+// action i of the step (env-major index): the caller's raw action clamped (vec_task.py:400-404, torch.clamp) when the
+// launch got them (ha_task_step_io), else the bound actions tensor
+HD float act_at(const SimCtx& c, const ha_state_t& st, size_t i) {
+    if (c.act_in) return fminf(fmaxf(c.act_in[i], -c.clip_act), c.clip_act);
+    return st.actions[i];
+}
+// obs_dict["obs"] = clamp(obs_buf, -clip, clip) (vec_task.py:437) next to obs_buf, when the launch asks for it
+HD void obs_out_put(const SimCtx& c, size_t i, float v) {
+    if (c.obs_out) c.obs_out[i] = fminf(fmaxf(v, -c.clip_obs), c.clip_obs);
+}
 
 // Contact entry ci of the list: LDS for [0, kc0), the env's global overflow entries after that (PhysCfg OVF). Read and
 // written by value: a pointer that may address either LDS or global memory would be a flat pointer, so each access
@@ -386,17 +403,22 @@ HD float wave_sum_rows(float x) {
 // Diagnostic phase timers (built only into libhandarm_hip_prof.so, -DHA_PROFILE): lane 0 of every
 // wave adds the s_memtime delta of each phase; read back with ha_profile_read().
 #ifdef HA_PROFILE
-__device__ unsigned long long g_prof[96];   // [32 + 8 kind + phase]: the hull-hull split per pair kind
+// [32 + 8 kind + phase]: the hull-hull split per pair kind; a second set of 96 for the substeps whose narrow phases
+// offered more than HA_PROFILE_HEAVY contacts (the previous substep's class for the phases before detect)
+__device__ unsigned long long g_prof[2 * 96];
+#ifndef HA_PROFILE_HEAVY
+#define HA_PROFILE_HEAVY 24
+#endif
 #define PROF_BEGIN() unsigned long long _pt = __builtin_amdgcn_s_memtime();
 #define PROF_COUNT(i, v)                                               \
     do {                                                               \
-        if (c.lane == 0) atomicAdd(&g_prof[i], (unsigned long long)(v)); \
+        if (c.lane == 0) atomicAdd(&g_prof[(i) + 96 * c.pcls], (unsigned long long)(v)); \
     } while (0)
 #define PROF(i)                                                        \
     do {                                                               \
         wsync();                                                       \
         unsigned long long _n = __builtin_amdgcn_s_memtime();          \
-        if (c.lane == 0) atomicAdd(&g_prof[i], _n - _pt);              \
+        if (c.lane == 0) atomicAdd(&g_prof[(i) + 96 * c.pcls], _n - _pt); \
         _pt = _n;                                                      \
     } while (0)
 #else
@@ -1912,6 +1934,9 @@ HD void substep(SimCtx& c, float hdt) {
     detect<PC::selfc>(c);
 #endif
     PROF(3);
+#ifdef HA_PROFILE
+    c.pcls = s.noff > HA_PROFILE_HEAVY ? 1 : 0;
+#endif
     if (lane == 0) {        // contact-list diagnostics (ha_state_t.contact_stats)
         int off = s.noff;
         s.cst[0] += 1;
@@ -2206,6 +2231,15 @@ HD void substep(SimCtx& c, float hdt) {
     //      contact rows r = 0..nr-1.  Same row order and arithmetic as the oracle.
     const float* J = Jb;
     const float* Y = Yb;
+    // several chunks: the row constants of the chunk after the current one, loaded while the current one is solved
+    float sl = 0.f, svt = 0.f, swinv = 0.f, scmu = 0.f, sca0 = 0.f, sca1 = 0.f;
+    auto stage = [&](int ch) {
+        int row = RPC * ch + lane;
+        sl = rk(0, row); svt = rk(1, row); swinv = rk(2, row);
+        scmu = rk(3, row); sca0 = rk(4, row); sca1 = rk(5, row);
+    };
+    if (multi && lane < RPC) stage(0);
+    const int nca = (nc + CAP - 1) / CAP;                   // chunks in use (wave-uniform)
 #ifdef HA_AB_PGS_TWICE
     for (int it = 0; it < 2 * p.solver_iters; it++) {
 #else
@@ -2257,9 +2291,16 @@ HD void substep(SimCtx& c, float hdt) {
         // re-reducing J.v after each row (row-by-row Gauss-Seidel) up to rounding
         // lane = generalized coordinate; its entry of a compact row is at compact_index (or absent -> 0).
         // The next contact's row entries are prefetched while the current one reduces.
+        // (two contacts ahead: the m set is filled by fetch, the n set is the next contact's; an overflow chunk's rows
+        // and most link contacts' robot blocks come from the env's global area, whose latency one contact of
+        // reductions does not cover)
         float j0n = 0.f, j1n = 0.f, j2n = 0.f, y0n = 0.f, y1n = 0.f, y2n = 0.f;
         float h0n = 0.f, h1n = 0.f, h2n = 0.f, g0n = 0.f, g1n = 0.f, g2n = 0.f;   // coordinate 64 + lane
+        float j0m = 0.f, j1m = 0.f, j2m = 0.f, y0m = 0.f, y1m = 0.f, y2m = 0.f;
+        float h0m = 0.f, h1m = 0.f, h2m = 0.f, g0m = 0.f, g1m = 0.f, g2m = 0.f;
         auto fetch = [&](int ci) {
+            float &j0n = j0m, &j1n = j1m, &j2n = j2m, &y0n = y0m, &y1n = y1m, &y2n = y2m;
+            float &h0n = h0m, &h1n = h1m, &h2n = h2m, &g0n = g0m, &g1n = g1m, &g2n = g2m;
             int ix = lane < RSN ? lane : -1;       // one slot: the compact row is the dense row
             int ixh = -1;
             if constexpr (row_slots<ND>() == 2) {
@@ -2373,23 +2414,32 @@ HD void substep(SimCtx& c, float hdt) {
             if (PC::ovf && ci >= CAP) ldd(gJ + 3 * (ci - CAP) * RSN, gY + 3 * (ci - CAP) * RSN);   // wave-uniform
             else ldd(J + 3 * ci * RSN, Y + 3 * ci * RSN);
         };
-        if (nc > 0) fetch(0);
+        auto advance = [&]() {
+            j0n = j0m; j1n = j1m; j2n = j2m; y0n = y0m; y1n = y1m; y2n = y2m;
+            h0n = h0m; h1n = h1m; h2n = h2m; g0n = g0m; g1n = g1m; g2n = g2m;
+        };
+        if (nc > 0) { fetch(0); advance(); }
+        if (nc > 1) fetch(1);
 #pragma unroll 1
         for (int ch = 0; ch < NCH; ch++) {
             int cend = nc < CAP * (ch + 1) ? nc : CAP * (ch + 1);
             if (NCH > 1) {
                 if (CAP * ch >= nc) break;
-                if (multi && lane < RPC) {          // swap this chunk's row constants in
-                    int row = RPC * ch + lane;
-                    klam = rk(0, row); kvt = rk(1, row); kwinv = rk(2, row);
-                    kcmu = rk(3, row); kca0 = rk(4, row); kca1 = rk(5, row);
+                if (multi && (nca > 1 || it == 0)) {
+                    // this chunk's row constants from the staging registers; the next chunk's (or the next
+                    // iteration's chunk 0, whose impulses were stored at its end) are loaded now, under this chunk.
+                    // One chunk in use (nca == 1): its constants stay in registers after the first iteration
+                    klam = sl; kvt = svt; kwinv = swinv; kcmu = scmu; kca0 = sca0; kca1 = sca1;
+                    int nx = (ch + 1 < NCH && CAP * (ch + 1) < nc) ? ch + 1 : 0;
+                    if (nca > 1 && lane < RPC) stage(nx);
                 }
             }
             for (int ci = CAP * ch; ci < cend; ci++) {
                 int r0 = 3 * (ci - CAP * ch);       // row of this contact within the chunk (= its lane)
                 float j0 = j0n, j1 = j1n, j2 = j2n, y0 = y0n, y1 = y1n, y2 = y2n;
                 float h0 = h0n, h1 = h1n, h2 = h2n, g0 = g0n, g1 = g1n, g2 = g2n;
-                if (ci + 1 < nc) fetch(ci + 1);
+                advance();
+                if (ci + 2 < nc) fetch(ci + 2);
                 float jv0 = j0 * vreg, jv1 = j1 * vreg, jv2 = j2 * vreg;
                 if (VW == 2) {
                     jv0 = jv0 + h0 * vregh;

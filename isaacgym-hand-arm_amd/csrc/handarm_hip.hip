@@ -408,11 +408,71 @@ __device__ __forceinline__ void after_physics(SimCtx& c, int& env) {
     asm volatile("" : "+v"(c.lane));
 }
 
+// VecTask.step's head and tail inside the step launch (ha_task_step_io, the Allegro families); all null: the plain step.
+// act_in: the caller's raw actions, clamped to +-clip_act where the task reads them and stored clamped into the
+// actions tensor (vec_task.py:400-404); obs_out: clamp(obs, +-clip_obs), the fresh obs_dict["obs"] (vec_task.py:437);
+// scalars: AllegroKuka's extras means (allegro_kuka_base.py:908-917) by the last workgroups (ak_extras)
+struct StepIO {
+    const float* act_in;
+    float* obs_out;
+    float* scalars;
+    float* partials;        // 4 floats per group of 64 envs
+    int32_t* counters;      // per group, then one for the groups; zero between launches
+    float clip_act, clip_obs;
+};
+
+// AllegroKuka extras: mean prev_episode_successes, mean / min / max true_objective over the shard, in the step launch.
+// Each env's workgroup publishes its task_state (ak_post) and counts itself into its group of 64 envs; the group's
+// last workgroup reduces the group (lane = env, fixed DPP tree) into a partial and counts the group in; the last group
+// reduces the partials (lane l: groups l, l + 64, ... in order, then the same tree). Fixed order: deterministic.
+__device__ __forceinline__ void ak_extras(const SimCtx& c, const ha_state_t& S, int env, const StepIO& io, int N) {
+    int lane = c.lane;
+    int g = env >> 6, G = (N + 63) >> 6;
+    int gsize = N - 64 * g < 64 ? N - 64 * g : 64;
+    __threadfence();
+    int last = 0;
+    if (lane == 0) last = atomicAdd(&io.counters[g], 1) == gsize - 1 ? 1 : 0;
+    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    __threadfence();
+    float ps = 0.0f, to = 0.0f, mn = 3.0e38f, mx = -3.0e38f;
+    if (lane < gsize) {
+        const float* t = S.task_state + (size_t)(64 * g + lane) * HA_AK_TS;
+        ps = t[HA_AK_PREV_SUCC];
+        to = t[HA_AK_TRUE_OBJ];
+        mn = to;
+        mx = to;
+    }
+    ps = wave_sum_rows(ps); to = wave_sum_rows(to); mn = wave_min(mn); mx = wave_max(mx);
+    if (lane == 0) {
+        float* q = io.partials + 4 * g;
+        q[0] = ps; q[1] = to; q[2] = mn; q[3] = mx;
+        io.counters[g] = 0;
+    }
+    __threadfence();
+    last = 0;
+    if (lane == 0) last = atomicAdd(&io.counters[G], 1) == G - 1 ? 1 : 0;
+    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    __threadfence();
+    float a0 = 0.0f, a1 = 0.0f, a2 = 3.0e38f, a3 = -3.0e38f;
+    for (int q = lane; q < G; q += 64) {
+        const float* r = io.partials + 4 * q;
+        a0 += r[0]; a1 += r[1]; a2 = fminf(a2, r[2]); a3 = fmaxf(a3, r[3]);
+    }
+    a0 = wave_sum_rows(a0); a1 = wave_sum_rows(a1); a2 = wave_min(a2); a3 = wave_max(a3);
+    if (lane == 0) {
+        io.scalars[0] = a0 / (float)N;
+        io.scalars[1] = a1 / (float)N;
+        io.scalars[2] = a2;
+        io.scalars[3] = a3;
+        io.counters[G] = 0;
+    }
+}
+
 template <int FAM, int MODE>
 __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params,
                                          const ha_state_t& st, int num_envs, int n_calls, uint32_t flags,
                                          int stat_slot, float* __restrict__ spill,
-                                         const int32_t* __restrict__ env_ids) {
+                                         const int32_t* __restrict__ env_ids, const StepIO& io) {
     constexpr int TASK = fam_task<FAM>();
     constexpr int ND = task_nd<FAM>();
     constexpr int NCH = task_contact_chunks<FAM>();
@@ -436,6 +496,13 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.spill = (PC::split || PC::ovf || PC::selfc) ? spill + (size_t)env * PC::spill_floats : nullptr;
     c.selfc = PC::selfc ? reinterpret_cast<uint8_t*>(c.spill + PC::off_selfc) : nullptr;
     c.sepf = 0xFF;
+#ifdef HA_PROFILE
+    c.pcls = 0;
+#endif
+    c.act_in = MODE == MODE_STEP ? io.act_in : nullptr;
+    c.obs_out = MODE == MODE_STEP ? io.obs_out : nullptr;
+    c.clip_act = io.clip_act;
+    c.clip_obs = io.clip_obs;
     c.maxc = PC::cap * NCH;
     // overflow chunks: contact entries past chunk 0 in the env's global area (null otherwise: ct_global folds away)
     c.kg = PC::ovf ? reinterpret_cast<ContactLDS*>(c.spill + PC::off_ct) : nullptr;
@@ -500,6 +567,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
         if (c.lane == 0) S.progress_buf[env] = S.progress_buf[env] + 1;                // allegro_kuka_base.py:1429
         ak_in_from_lds(c, &akp.in);
         ak_post(c, S, env, akp, false);
+        if (MODE == MODE_STEP && io.scalars) ak_extras(c, S, env, io, num_envs);
         return;
     }
     if (TASK == HA_TASK_ALLEGRO_HAND) {
@@ -574,9 +642,10 @@ __device__ unsigned int g_envhw[2 * 65536];
     extern "C" __global__ void __launch_bounds__(64)                                                          \
         __attribute__((amdgpu_waves_per_eu(task_waves_per_eu<FAM>())))                                        \
         name(const ha_model_t* __restrict__ model, const ha_params_t* __restrict__ params, ha_state_t st,       \
-             int num_envs, int n_calls, uint32_t flags, int stat_slot, float* spill, const int32_t* env_ids) {  \
+             int num_envs, int n_calls, uint32_t flags, int stat_slot, float* spill, const int32_t* env_ids,     \
+             StepIO io) {                                                                                       \
         HA_ENV_T0();                                                                                            \
-        env_body<FAM, MODE>(model, params, st, num_envs, n_calls, flags, stat_slot, spill, env_ids);           \
+        env_body<FAM, MODE>(model, params, st, num_envs, n_calls, flags, stat_slot, spill, env_ids, io);       \
         HA_ENV_T1();                                                                                            \
     }
 HA_KERNEL(ha_step_kernel, HA_TASK_UR5SIH, MODE_STEP)
@@ -597,7 +666,7 @@ HA_KERNEL(ak_observe_kernel, HA_TASK_ALLEGRO_KUKA, MODE_OBSERVE)
 HA_KERNEL(ak_reset_kernel, HA_TASK_ALLEGRO_KUKA, MODE_RESET)
 
 typedef void (*env_kernel_t)(const ha_model_t*, const ha_params_t*, ha_state_t, int, int, uint32_t, int, float*,
-                             const int32_t*);
+                             const int32_t*, StepIO);
 static env_kernel_t kernel_for(int fam, int mode) {
     if (fam == FAM_UR5SIH_CLUTTER) {
         switch (mode) {
@@ -719,6 +788,9 @@ struct ha_handle_s {
     hipEvent_t* pc_ev;    // 2 * t_max events (ha_pointclouds launches)
     float* d_spill;       // split-row families: robot-block rows beyond the LDS slots, N x spill_floats
     const int32_t* order; // ha_set_env_order: env of workgroup i in full-shard launches (null: identity)
+    StepIO io;            // ha_task_step_io: the step launch's folded head / tail (zero otherwise)
+    float* d_io_partials; // AllegroKuka extras: 4 floats per group of 64 envs
+    int32_t* d_io_counters;   // and ceil(N / 64) + 1 counters, zero between launches
 };
 
 #define HIPCHK(x)                                                                     \
@@ -900,6 +972,12 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
         // before they are read)
         HIPCHK(hipMemset(h->d_spill, 0xFF, sizeof(float) * spill_floats(fam) * (size_t)num_envs));
     }
+    if (fam == HA_TASK_ALLEGRO_KUKA) {
+        size_t G = ((size_t)num_envs + 63) / 64;
+        HIPCHK(hipMalloc(&h->d_io_partials, sizeof(float) * 4 * G));
+        HIPCHK(hipMalloc(&h->d_io_counters, sizeof(int32_t) * (G + 1)));
+        HIPCHK(hipMemset(h->d_io_counters, 0, sizeof(int32_t) * (G + 1)));
+    }
     for (int mode : {MODE_STEP, MODE_SIMULATE, MODE_OBSERVE, MODE_RESET})
         HIPCHK(hipFuncSetAttribute((const void*)kernel_for(h->fam, mode), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds_bytes(h->fam)));
@@ -914,6 +992,8 @@ int ha_destroy(ha_handle h) {
     (void)hipFree(h->d_model);
     (void)hipFree(h->d_params);
     if (h->d_spill) (void)hipFree(h->d_spill);
+    if (h->d_io_partials) (void)hipFree(h->d_io_partials);
+    if (h->d_io_counters) (void)hipFree(h->d_io_counters);
     (void)hipEventDestroy(h->ev0);
     (void)hipEventDestroy(h->ev1);
     free(h);
@@ -944,7 +1024,8 @@ static int launch(ha_handle h, int mode, int n_calls, uint32_t flags, int slot, 
         n_ids = h->N;
     }
     hipLaunchKernelGGL(kernel_for(h->fam, mode), dim3(env_ids ? n_ids : h->N), dim3(64), lds_bytes(h->fam), s, h->d_model,
-                       h->d_params, h->st, h->N, n_calls, flags, slot, h->d_spill, env_ids);
+                       h->d_params, h->st, h->N, n_calls, flags, slot, h->d_spill, env_ids,
+                       mode == MODE_STEP ? h->io : StepIO{});
     HIPCHK(hipGetLastError());
     if (rec) {
         (void)hipEventRecord(h->t_ev[2 * h->t_count + 1], s);
@@ -1076,6 +1157,18 @@ int ha_task_step(ha_handle h, uint32_t flags, void* stream) {
                            h->h_params.ah_av_factor);
         HIPCHK(hipGetLastError());
     }
+    return rc;
+}
+
+int ha_task_step_io(ha_handle h, uint32_t flags, const float* actions, float clip_actions, float* obs_out,
+                    float clip_obs, float* scalars, void* stream) {
+    if (!h) return HA_E_ARG;
+    if (h->fam != HA_TASK_ALLEGRO_KUKA && h->fam != HA_TASK_ALLEGRO_HAND) return HA_E_ARG;
+    if (scalars && (h->fam != HA_TASK_ALLEGRO_KUKA || !h->d_io_counters)) return HA_E_ARG;
+    if ((actions && !(clip_actions >= 0.0f)) || (obs_out && !(clip_obs >= 0.0f))) return HA_E_ARG;
+    h->io = StepIO{actions, obs_out, scalars, h->d_io_partials, h->d_io_counters, clip_actions, clip_obs};
+    int rc = ha_task_step(h, flags, stream);
+    h->io = StepIO{};
     return rc;
 }
 
@@ -1311,9 +1404,9 @@ float ha_last_kernel_ms(ha_handle h) {
 #ifdef HA_PROFILE
 // diagnostic build only: per-phase s_memtime totals summed over waves (see PROF in ha_physics.h), 96 counters
 extern "C" int ha_profile_read(unsigned long long* out32, int reset) {
-    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 96) != hipSuccess) return HA_E_HIP;
+    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 192) != hipSuccess) return HA_E_HIP;
     if (reset) {
-        unsigned long long z[96] = {0};
+        unsigned long long z[192] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return HA_E_HIP;
     }
     return HA_OK;

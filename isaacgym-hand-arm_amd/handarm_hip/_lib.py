@@ -36,6 +36,7 @@ SIGNATURES = {
     "ha_task_step": ([H, C.c_uint32, S], C.c_int),
     "ha_task_observe": ([H, C.c_uint32, S], C.c_int),
     "ha_task_epilogue": ([H, C.c_void_p, C.c_float, C.c_void_p, S], C.c_int),
+    "ha_task_step_io": ([H, C.c_uint32, C.c_void_p, C.c_float, C.c_void_p, C.c_float, C.c_void_p, S], C.c_int),
     "ha_task_reset": ([H, C.c_uint32, S], C.c_int),
     "ha_last_kernel_ms": ([H], C.c_float),
     "ha_contact_capacity": ([H], C.c_int),

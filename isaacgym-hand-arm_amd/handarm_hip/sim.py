@@ -219,6 +219,24 @@ class HandArmSim:
                 self.rebalance()
         _lib.check(self.lib.ha_task_step(self.h, flags, self._stream()), "ha_task_step")
 
+    def task_step_io(self, flags, actions, clip_actions, obs_out, clip_obs, scalars=None):
+        """task_step with VecTask.step's action clamp and the epilogue's outputs in the same launch (Allegro tasks):
+        actions (raw, N x num_actions float32 on the device) clamped into the actions tensor, obs_out = clamp(obs),
+        scalars (AllegroKuka, 4 floats) = the extras means."""
+        if self.rebalance_every > 0:
+            self._rb_count += 1
+            if self._rb_count >= self.rebalance_every:
+                self._rb_count = 0
+                self.rebalance()
+        a = actions
+        if a.dtype != torch.float32 or a.device != self.device or not a.is_contiguous():
+            a = a.to(self.device, torch.float32).contiguous()
+        _lib.check(self.lib.ha_task_step_io(self.h, flags, C.c_void_p(a.data_ptr()), float(clip_actions),
+                                            C.c_void_p(obs_out.data_ptr()), float(clip_obs),
+                                            C.c_void_p(scalars.data_ptr()) if scalars is not None else None,
+                                            self._stream()), "ha_task_step_io")
+        return a            # keep the converted copy alive until the launch has read it (the caller holds it)
+
     def task_observe(self, flags=0):
         _lib.check(self.lib.ha_task_observe(self.h, flags, self._stream()), "ha_task_observe")
 

@@ -14,7 +14,6 @@ import numpy as np
 import torch
 
 from .. import model as HM
-from .. import _lib
 from .. import ref_rng as RR
 from ..sim import HandArmSim
 from .ur5sih_multi_object_manipulation import Box
@@ -92,7 +91,7 @@ class AllegroHand:
         self._rr = RR.AllegroDraws(N) if self.reference_rng else None
         self.extras = {}
         self.obs_dict = {}
-        # obs_dict["obs"] = clamp(obs_buf) by ha_task_epilogue into one of two alternating buffers: step t's obs
+        # obs_dict["obs"] = clamp(obs_buf) by the step launch (ha_task_step_io) into one of two alternating buffers: step t's obs
         # (and extras["consecutive_successes"], a view of the task's counter) stay valid through step t+1 and are
         # overwritten by step t+2. env.freshOutputs=True returns new tensors every step, as the reference's
         # torch.clamp / .mean() do (allegro_hand.py:393,707)
@@ -149,15 +148,14 @@ class AllegroHand:
     def step(self, actions):
         """VecTask.step (vec_task.py:390-441) -> pre_physics_step / simulate x2 / post_physics_step, fused.
         obs_dict["obs"] is valid until the step after next unless env.freshOutputs is set (see __init__)."""
-        torch.clamp(actions, -self.clip_actions, self.clip_actions, out=self.actions_buf)
-        self.sim.task_step(self.sim_flags | self._reference_draws())
+        out = torch.empty_like(self._obs_out[0]) if self.fresh_outputs else self._obs_out[(self.control_steps + 1) & 1]
+        # one launch: the action clamp into actions_buf (vec_task.py:400-404), the fused step and obs_dict["obs"] =
+        # clamp(obs_buf) into `out` (ha_task_step_io)
+        self.sim.task_step_io(self.sim_flags | self._reference_draws(), actions, self.clip_actions, out, self.clip_obs)
         self.control_steps += 1
         self.extras["time_outs"] = self.timeout_buf.view(torch.bool).to(self.rl_device)
         cs = self.consecutive_successes.view(())                                     # allegro_hand.py:393 (1 value)
         self.extras["consecutive_successes"] = cs.clone() if self.fresh_outputs else cs
-        out = torch.empty_like(self._obs_out[0]) if self.fresh_outputs else self._obs_out[self.control_steps & 1]
-        _lib.check(self.sim.lib.ha_task_epilogue(self.sim.h, out.data_ptr(), self.clip_obs, None, self.sim._stream()),
-                   "ha_task_epilogue")
         self.obs_dict["obs"] = out.to(self.rl_device)
         return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras
 

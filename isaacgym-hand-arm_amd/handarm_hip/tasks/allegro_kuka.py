@@ -16,7 +16,6 @@ import numpy as np
 import torch
 
 from .. import model as HM
-from .. import _lib
 from .. import ref_rng as RR
 from .. import state_files as SF
 from ..sim import HandArmSim
@@ -127,7 +126,7 @@ class AllegroKuka:
         self.frame_since_restart = 0
         self.extras = {}
         self.obs_dict = {}
-        # step tail (ha_task_epilogue, one launch): obs_dict["obs"] = clamp(obs_buf) and the extras means
+        # step tail (in the step launch, ha_task_step_io): obs_dict["obs"] = clamp(obs_buf) and the extras means
         # (successes, true_objective mean/min/max). Lifetime: by default they land in one of two alternating
         # buffers, so the tensors step t returns stay valid through step t+1 and are overwritten by step t+2 (no
         # allocation per step). env.freshOutputs=True gives every step new tensors, as the reference's
@@ -223,7 +222,6 @@ class AllegroKuka:
         """VecTask.step (vec_task.py:390-441) -> pre_physics_step / simulate / post_physics_step, fused.
         obs_dict["obs"] and the extras means are valid until the step after next unless env.freshOutputs is set
         (see __init__); rew / reset / time_outs are the task's buffers, as in the reference."""
-        torch.clamp(actions, -self.clip_actions, self.clip_actions, out=self.actions_buf)
         self.frame_since_restart += 1
         self._curriculum()
         flags = self.sim_flags | self._reference_draws()
@@ -232,18 +230,18 @@ class AllegroKuka:
             if len(env_ids) > 0:
                 self.sim.task_reset(flags)
                 self._after_reset(env_ids)
-        self.sim.task_step(flags)
-        if self._recorder is not None:                                      # post_physics_step, :1445-1446
-            N = self.num_environments
-            self._recorder.accumulate(self.root_state_tensor.view(N, -1, 13), self.dof_state.view(N, -1, 2))
         if self.fresh_outputs:
             out = torch.empty_like(self._obs_out[0])
             sc = torch.empty_like(self._scalars[0])
         else:
             k = self.frame_since_restart & 1
             out, sc = self._obs_out[k], self._scalars[k]
-        _lib.check(self.sim.lib.ha_task_epilogue(self.sim.h, out.data_ptr(), self.clip_obs, sc.data_ptr(),
-                                                 self.sim._stream()), "ha_task_epilogue")
+        # one launch: the action clamp into actions_buf (vec_task.py:400-404), the fused step, obs_dict["obs"] =
+        # clamp(obs_buf) into `out` and the extras means into `sc` (ha_task_step_io)
+        self.sim.task_step_io(flags, actions, self.clip_actions, out, self.clip_obs, sc)
+        if self._recorder is not None:                                      # post_physics_step, :1445-1446
+            N = self.num_environments
+            self._recorder.accumulate(self.root_state_tensor.view(N, -1, 13), self.dof_state.view(N, -1, 2))
         ex = self.extras
         ex["time_outs"] = self.timeout_buf.view(torch.bool).to(self.rl_device)
         ex["successes"] = sc[0]                                                # :908-917

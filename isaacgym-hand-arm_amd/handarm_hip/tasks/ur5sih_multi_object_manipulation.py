@@ -558,8 +558,7 @@ class Ur5SihMultiObjectManipulation:
             self._drop_initialisation()
         if self.randomize:      # action noise before the clamp (vec_task.py:400-404)
             actions = actions + self.sim.params.dr_act_noise * torch.randn_like(actions)
-        action_tensor = torch.clamp(actions, -self.clip_actions, self.clip_actions)
-        self.actions_buf.copy_(action_tensor)
+        torch.clamp(actions, -self.clip_actions, self.clip_actions, out=self.actions_buf)
         if self._stat_pending >= self.sim.stats_ring - 1:
             # ring full (this step's launch clears the slot after its own, the oldest pending one): reduce
             # across ranks (if any), then fold

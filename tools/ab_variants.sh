@@ -10,6 +10,6 @@ for i in $(seq 1 ${AB_ROUNDS:-2}); do
 import sys, runpy; sys.path[:0]=['isaacgym-hand-arm_amd']
 from handarm_hip import _lib; _lib.LIB_PATH='$R/isaacgym-hand-arm_amd/handarm_hip/$L'
 sys.argv=['bench.py','--task','$TASK','--no-cpu-baseline']; runpy.run_path('bench.py', run_name='__main__')" > gpurun_out/ab_${L%.so}_$i.json || exit 1
-    python -c "import json; d=json.loads([l for l in open('gpurun_out/ab_${L%.so}_$i.json') if l.startswith('{')][-1]); print('$L round $i', round(d['value']), round(d['roofline']['kernel_avg_ms'], 3))"
+    python -c "import json; d=json.loads([l for l in open('gpurun_out/ab_${L%.so}_$i.json') if l.startswith('{')][-1]); e=d.get('episode_window'); print('$L round $i', round(d['value']), round(d['roofline']['kernel_avg_ms'], 3), ('episode %d %.3f ms' % (e['value'], e['ms_per_step'])) if e else '')"
   done
 done

@@ -30,13 +30,22 @@ if __name__ == "__main__":
     lib = _lib.load()
     if not envt_only:
         lib.ha_profile_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    buf = (C.c_ulonglong * 96)()
+    raw = (C.c_ulonglong * 192)()     # two sets of 96: light substeps, then heavy ones (HA_PROFILE_HEAVY)
     args = [x for x in sys.argv[1:] if not x.startswith("--")]
     n = int(args[0]) if args else 8192
 
     def report(label):
         torch.cuda.synchronize()
-        lib.ha_profile_read(buf, 1)
+        lib.ha_profile_read(raw, 1)
+        both = [raw[i] + raw[96 + i] for i in range(96)]
+        report_set(label, both)
+        heavy = [raw[96 + i] for i in range(96)]
+        if heavy[9]:
+            print(f"  heavy substeps only (> 24 contacts offered): {100.0 * heavy[9] / max(both[9], 1):.2f}% of substeps, "
+                  f"{100.0 * sum(heavy[:8]) / max(sum(both[:8]), 1):.1f}% of cycles", flush=True)
+            report_set(label + " [heavy]", heavy)
+
+    def report_set(label, buf):
         tot = sum(buf[:8])
         print(f"{label}: contacts/substep {buf[8] / max(buf[9], 1):.2f}", flush=True)
         print("  " + "  ".join(f"{PHASES[i]} {100.0 * buf[i] / tot:5.1f}%" for i in range(8)), flush=True)
@@ -84,15 +93,24 @@ if __name__ == "__main__":
         env.reset()
         na = env.num_acts
         g = torch.Generator(device="cuda:0").manual_seed(42)
-        for _ in range(20):
-            env.step(torch.rand((n, na), device="cuda:0", generator=g) * 2 - 1)
+        warm = int(os.environ.get("HA_PROFILE_WARM", 20))     # steps before the profiled window (episode: 200)
+        # HA_PROFILE_POOL=1: bench.py's actions, a pool of 16 random action batches cycled (their mean drifts the arm)
+        apool = ([torch.rand((n, na), device="cuda:0", generator=g) * 2 - 1 for _ in range(16)]
+                 if os.environ.get("HA_PROFILE_POOL") == "1" else None)
+        _k = [0]
+
+        def next_actions():
+            _k[0] += 1
+            return apool[_k[0] % 16] if apool else torch.rand((n, na), device="cuda:0", generator=g) * 2 - 1
+        for _ in range(warm):
+            env.step(next_actions())
         torch.cuda.synchronize()
         if not envt_only:
-            lib.ha_profile_read(buf, 1)
+            lib.ha_profile_read(raw, 1)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(10):
-            env.step(torch.rand((n, na), device="cuda:0", generator=g) * 2 - 1)
+            env.step(next_actions())
         e1.record()
         torch.cuda.synchronize()
         print(f"bench scene n={n}: {e0.elapsed_time(e1) / 10:.3f} ms/step "
@@ -106,7 +124,7 @@ if __name__ == "__main__":
             sim = env.sim
             rb = sim.t["reset_buf"].cpu().numpy().astype(bool)
             cs0 = sim.t["contact_stats"].cpu().numpy().astype(np.int64).copy()
-            env.step(torch.rand((n, na), device="cuda:0", generator=g) * 2 - 1)
+            env.step(next_actions())
             torch.cuda.synchronize()
             cs1 = sim.t["contact_stats"].cpu().numpy().astype(np.int64)
             cs = cs1 - cs0
@@ -169,6 +187,6 @@ if __name__ == "__main__":
             print("  histogram: " + "  ".join(f"{edges[i]:.0f}:{hist[i]}" for i in range(12)), flush=True)
         sys.exit(0)
     for objects in (False, True):
-        lib.ha_profile_read(buf, 1)
+        lib.ha_profile_read(raw, 1)
         run(n, "objects on" if objects else "objects off", objects=objects)
         report("objects on" if objects else "objects off")
