@@ -568,7 +568,8 @@ def main():
         "roofline": h["roofline"], "compute_roofline": h["compute_roofline"], "cpu_baseline": h.get("cpu_baseline"),
         "distributed": dist_info,
     }
-    for k in ("episode_successes_mean", "consecutive_successes", "success_rate_ewma", "contacts", "pointcloud_roofline"):
+    for k in ("episode_successes_mean", "consecutive_successes", "success_rate_ewma", "contacts", "pointcloud_roofline",
+              "episode_window"):
         if k in h:
             out[k] = h[k]
     if subs:

@@ -117,7 +117,6 @@ struct EnvLDS {
     int nc, nr, noff, ng;                       // contacts kept / rows / contacts offered this substep /
                                                 // points gathered for a compound object pair
     int cst[4];                                 // contact_stats of this launch (see ha_state_t)
-    uint32_t selfm[HA_MAX_SELF_PAIRS / 32];     // self-collision candidates of this substep (detect_self), a bit a pair
     union {
         PostScratch pd;                         // (the narrow-phase scratch, ColLayout, is sized per family)
         RowScratch rows;
@@ -298,8 +297,14 @@ __host__ __device__ inline size_t contact_lds_offset() {
     return obj_lds_offset<PC>() + (size_t)PC::ocap * sizeof(ObjLDS);
 }
 template <class PC>
-__host__ __device__ inline size_t task_lds_bytes() {
+__host__ __device__ inline size_t selfm_lds_offset() {
     return contact_lds_offset<PC>() + (size_t)PC::cap * (PC::ovf ? 1 : PC::nch) * sizeof(ContactLDS);
+}
+// the self-collision candidate bits (detect_self), a bit a pair, after the contact list: only in the families that
+// collide the robot with itself, so the others' env blocks do not grow
+template <typename PC>
+__host__ __device__ inline size_t task_lds_bytes() {
+    return selfm_lds_offset<PC>() + (PC::selfc ? HA_MAX_SELF_PAIRS / 8 : 0);
 }
 
 struct SimCtx {
@@ -326,6 +331,7 @@ struct SimCtx {
     // k: face k of side A, 0xFF: none), and the env's per-pair record of it in its global area (null otherwise)
     int sepf;
     uint8_t* selfc;
+    uint32_t* selfm;        // LDS: this substep's self-pair candidates, a bit a pair (selfm_lds_offset; null otherwise)
     // VecTask.step's head and tail folded into the step launch (ha_task_step_io; null / unused otherwise): the caller's
     // raw actions, clamped to +-clip_act where the task reads them (act_at), and a second, clamped copy of obs
     const float* act_in;
@@ -1187,30 +1193,54 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
                 if (!aLong) { lf0 = lf0 * -1.0f; lf1 = lf1 * -1.0f; }
                 f3 lx = cross3(lf1, lf0);
                 f3 lo = lp - cb;
+                // two passes per 64 short-list edges: (1) the Gauss-map test of this lane's edge against each of them
+                // (wave-uniform short edge, its face normals broadcast from LDS) into a bit mask; (2) each lane walks
+                // its own passing pairs in increasing order and evaluates their axes. The same pairs, values and
+                // first-max-wins order as one loop evaluating every pair, but the axis arithmetic runs only on the
+                // lanes whose pair passed instead of on the whole wave whenever any lane's did
 #pragma unroll 1
-                for (int si = 0; si < nS; si++) {
-                    uint32_t rs = si < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)recS, si)
-                                          : ES[__builtin_amdgcn_readfirstlane(lS[si])];
-                    f3 sp = ld3(wvS[rs & 255u]);
-                    f3 se = ld3(wvS[(rs >> 8) & 255u]) - sp;
-                    f3 sf0 = ld3(wpS[(rs >> 16) & 255u]), sf1 = ld3(wpS[rs >> 24]);
-                    if (aLong) { sf0 = sf0 * -1.0f; sf1 = sf1 * -1.0f; }
-                    f3 sx = cross3(sf1, sf0);
-                    // A: (a, b, bxa) = (f0, f1, f1 x f0); B: (c, d, dxc) = (-f0, -f1, (-f1) x (-f0))
-                    f3 a = aLong ? lf0 : sf0, b = aLong ? lf1 : sf1, bxa = aLong ? lx : sx;
-                    f3 cc = aLong ? sf0 : lf0, dd = aLong ? sf1 : lf1, dxc = aLong ? sx : lx;
-                    float cba = dot3(cc, bxa), dba = dot3(dd, bxa), adc = dot3(a, dxc), bdc = dot3(b, dxc);
-                    if (!(cba * dba < 0.0f && adc * bdc < 0.0f && cba * bdc > 0.0f)) continue;
-                    f3 pa = aLong ? lp : sp, e1 = aLong ? le : se, pb = aLong ? sp : lp, e2 = aLong ? se : le;
-                    f3 n = cross3(e1, e2);
-                    float l2 = dot3(n, n);
-                    if (l2 < 2.5e-5f * (dot3(e1, e1) * dot3(e2, e2))) continue;
-                    n = n * (1.0f / sqrtf(l2));
-                    f3 pbo = aLong ? sp - cb : lo;
-                    if (dot3(n, pbo) < 0.0f) n = n * -1.0f;
-                    float sv = dot3(n, pa - pb);
-                    int w = aLong ? li * nB + si : si * nB + li;
-                    if (act && sv > best) { best = sv; bw = w; }
+                for (int sb = 0; sb < nS; sb += 64) {
+                    int ns = nS - sb < 64 ? nS - sb : 64;
+                    uint64_t pm = 0;
+#pragma unroll 1
+                    for (int t = 0; t < ns; t++) {
+                        int si = sb + t;
+                        uint32_t rs = si < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)recS, si)
+                                              : ES[__builtin_amdgcn_readfirstlane(lS[si])];
+                        f3 sf0 = ld3(wpS[(rs >> 16) & 255u]), sf1 = ld3(wpS[rs >> 24]);
+                        if (aLong) { sf0 = sf0 * -1.0f; sf1 = sf1 * -1.0f; }
+                        f3 sx = cross3(sf1, sf0);
+                        // A: (a, b, bxa) = (f0, f1, f1 x f0); B: (c, d, dxc) = (-f0, -f1, (-f1) x (-f0))
+                        f3 a = aLong ? lf0 : sf0, b = aLong ? lf1 : sf1, bxa = aLong ? lx : sx;
+                        f3 cc = aLong ? sf0 : lf0, dd = aLong ? sf1 : lf1, dxc = aLong ? sx : lx;
+                        float cba = dot3(cc, bxa), dba = dot3(dd, bxa), adc = dot3(a, dxc), bdc = dot3(b, dxc);
+                        bool pass = cba * dba < 0.0f && adc * bdc < 0.0f && cba * bdc > 0.0f;
+                        pm |= (uint64_t)(pass ? 1u : 0u) << t;
+                    }
+                    if (!act) pm = 0;
+#pragma unroll 1
+                    while (__ballot(pm != 0) != 0ull) {
+                        // (the short edge's record comes from its lane with every lane active: a lane permute whose
+                        // source lane is inactive would not read its value)
+                        int t = pm != 0 ? __ffsll((unsigned long long)pm) - 1 : 0;
+                        int si = sb + t;
+                        uint32_t rs = (uint32_t)__shfl((int)recS, t);
+                        if (pm == 0) continue;
+                        pm &= pm - 1;
+                        if (sb > 0) rs = ES[lS[si]];
+                        f3 sp = ld3(wvS[rs & 255u]);
+                        f3 se = ld3(wvS[(rs >> 8) & 255u]) - sp;
+                        f3 pa = aLong ? lp : sp, e1 = aLong ? le : se, pb = aLong ? sp : lp, e2 = aLong ? se : le;
+                        f3 n = cross3(e1, e2);
+                        float l2 = dot3(n, n);
+                        if (l2 < 2.5e-5f * (dot3(e1, e1) * dot3(e2, e2))) continue;
+                        n = n * (1.0f / sqrtf(l2));
+                        f3 pbo = aLong ? sp - cb : lo;
+                        if (dot3(n, pbo) < 0.0f) n = n * -1.0f;
+                        float sv = dot3(n, pa - pb);
+                        int w = aLong ? li * nB + si : si * nB + li;
+                        if (sv > best) { best = sv; bw = w; }
+                    }
                 }
             }
         }
@@ -1504,7 +1534,7 @@ HD void gather_emit(SimCtx& c, int kind, int A, int B) {
 //     narrow-phase scratch, component-major (lanes reading different hulls read consecutive words);
 //  2. one lane per pair tests the two spheres (ha_obb_spheres_near); the pairs that pass are compacted, in pair order,
 //     and one lane per such pair runs the 15 SAT axes (ha_obb_sat) - the oracle's ha_obb_near, split so that the
-//     axis tests run on full waves. The candidate bits go to EnvLDS.selfm (the narrow phases below overwrite the
+//     axis tests run on full waves. The candidate bits go to the env's LDS bit set (the narrow phases below overwrite the
 //     scratch), and the first 64 candidates' records are loaded into a register at once;
 //  3. per candidate, in pair order: if the pair's last narrow phase ended on a separating face (the env's per-pair
 //     byte in its global area), that one face is tested first, with the narrow phase's own expressions (world plane,
@@ -1531,7 +1561,7 @@ HD void detect_self(SimCtx& c) {
         for (int i = 0; i < 15; i++) tab[i * NLH + lane] = w[i];
         tab[15 * NLH + lane] = ha_obb_radius(w + 12);
     }
-    if (lane < HA_MAX_SELF_PAIRS / 32) s.selfm[lane] = 0u;
+    if (lane < HA_MAX_SELF_PAIRS / 32) c.selfm[lane] = 0u;
     c.colA_h = c.colB_h = -1;           // the box table overwrote the cached hull sides
     c.colA_p = false;
     wsync();
@@ -1568,7 +1598,7 @@ HD void detect_self(SimCtx& c) {
         }
         uint64_t mk = __ballot(cand);
         if (cand) {
-            atomicOr(&s.selfm[p >> 5], 1u << (p & 31));
+            atomicOr(&c.selfm[p >> 5], 1u << (p & 31));
             int r = ncd + __popcll(mk & below);
             if (r < 64) cdl[r] = (uint16_t)p;
         }
@@ -1584,7 +1614,7 @@ HD void detect_self(SimCtx& c) {
     int rank = 0;
 #pragma unroll 1
     for (int w32 = 0; w32 < (nsp + 31) >> 5; w32++) {
-        uint32_t mask = s.selfm[w32];
+        uint32_t mask = c.selfm[w32];
 #pragma unroll 1
         while (mask) {
             int bit = __ffs(mask) - 1;

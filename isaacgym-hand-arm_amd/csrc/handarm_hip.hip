@@ -495,6 +495,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.k = reinterpret_cast<ContactLDS*>(smem + contact_lds_offset<PC>());
     c.spill = (PC::split || PC::ovf || PC::selfc) ? spill + (size_t)env * PC::spill_floats : nullptr;
     c.selfc = PC::selfc ? reinterpret_cast<uint8_t*>(c.spill + PC::off_selfc) : nullptr;
+    c.selfm = PC::selfc ? reinterpret_cast<uint32_t*>(smem + selfm_lds_offset<PC>()) : nullptr;
     c.sepf = 0xFF;
 #ifdef HA_PROFILE
     c.pcls = 0;
