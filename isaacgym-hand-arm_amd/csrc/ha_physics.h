@@ -361,32 +361,52 @@ HD void obs_out_put(const SimCtx& c, size_t i, float v) {
 // written by value: a pointer that may address either LDS or global memory would be a flat pointer, so each access
 // keeps its two address spaces on separate paths.
 HD bool ct_global(const SimCtx& c, int ci) { return c.kg != nullptr && ci >= c.kc0; }
+// The two branches address different memories on purpose; the address-space casts keep the compiler from merging
+// them into one generic (flat) access through a selected pointer: a flat load waits on the vector-memory counter
+// too, so one in the PGS loop (ct_ab) would also wait for the global rows prefetched for the next contact
+#define HA_AS_LDS __attribute__((address_space(3)))
+#define HA_AS_GLB __attribute__((address_space(1)))
+HD const HA_AS_LDS ContactLDS* ct_lds(const SimCtx& c, int ci) { return (const HA_AS_LDS ContactLDS*)(c.k + ci); }
+HD const HA_AS_GLB ContactLDS* ct_glb(const SimCtx& c, int ci) {
+    return (const HA_AS_GLB ContactLDS*)(c.kg + (ci - c.kc0));
+}
 HD ContactLDS ct_get(const SimCtx& c, int ci) {
-    if (ct_global(c, ci)) return c.kg[ci - c.kc0];
-    return c.k[ci];
+    ContactLDS r;
+    if (ct_global(c, ci)) {
+        const HA_AS_GLB ContactLDS* g = ct_glb(c, ci);
+        r.x[0] = g->x[0]; r.x[1] = g->x[1]; r.x[2] = g->x[2];
+        r.n[0] = g->n[0]; r.n[1] = g->n[1]; r.n[2] = g->n[2];
+        r.sep = g->sep; r.a = g->a; r.b = g->b;
+    } else {
+        const HA_AS_LDS ContactLDS* l = ct_lds(c, ci);
+        r.x[0] = l->x[0]; r.x[1] = l->x[1]; r.x[2] = l->x[2];
+        r.n[0] = l->n[0]; r.n[1] = l->n[1]; r.n[2] = l->n[2];
+        r.sep = l->sep; r.a = l->a; r.b = l->b;
+    }
+    return r;
 }
 HD float ct_sep(const SimCtx& c, int ci) {
-    if (ct_global(c, ci)) return c.kg[ci - c.kc0].sep;
-    return c.k[ci].sep;
+    if (ct_global(c, ci)) return ct_glb(c, ci)->sep;
+    return ct_lds(c, ci)->sep;
 }
 HD void ct_ab(const SimCtx& c, int ci, int& a, int& b) {
     if (ct_global(c, ci)) {
-        a = c.kg[ci - c.kc0].a;
-        b = c.kg[ci - c.kc0].b;
+        a = ct_glb(c, ci)->a;
+        b = ct_glb(c, ci)->b;
     } else {
-        a = c.k[ci].a;
-        b = c.k[ci].b;
+        a = ct_lds(c, ci)->a;
+        b = ct_lds(c, ci)->b;
     }
 }
-HD void ct_fill(ContactLDS& ct, f3 x, f3 n, float sep, int a, int b) {
+template <typename Q>
+HD void ct_fill(Q* q, f3 x, f3 n, float sep, int a, int b) {
     // eight dword stores: the two 16-bit body codes go as one packed word
-    float* q = reinterpret_cast<float*>(&ct);
     q[0] = x.x; q[1] = x.y; q[2] = x.z; q[3] = n.x; q[4] = n.y; q[5] = n.z; q[6] = sep;
     q[7] = __int_as_float((a & 0xFFFF) | (b << 16));
 }
 HD void ct_put(const SimCtx& c, int ci, f3 x, f3 n, float sep, int a, int b) {
-    if (ct_global(c, ci)) ct_fill(c.kg[ci - c.kc0], x, n, sep, a, b);
-    else ct_fill(c.k[ci], x, n, sep, a, b);
+    if (ct_global(c, ci)) ct_fill((HA_AS_GLB float*)(c.kg + (ci - c.kc0)), x, n, sep, a, b);
+    else ct_fill((HA_AS_LDS float*)(c.k + ci), x, n, sep, a, b);
 }
 
 // friction of a contact body (link 100+L, object o, static -1) and of a contact (PhysX average combine)
@@ -2098,10 +2118,12 @@ HD void substep(SimCtx& c, float hdt) {
                 if (v0 > p.max_depen_vel) v0 = p.max_depen_vel;
                 vt_ = v0;
             }
-            // Y_r = M^-1 J_r^T (robot block through the explicit inverse, object blocks 1/m, I_w^-1)
+            // Y_r = M^-1 J_r^T (robot block through the explicit inverse, object blocks 1/m, I_w^-1). The robot terms of
+            // J_r . Y_r (the dense row's first terms, in its order) accumulate here from registers, so the block is
+            // not read back: Jr / Yr may be a global spill row (a generic pointer, flat accesses)
+            float a = 0.0f;
             if (Jr) {
-                // J_r to registers first: Jr may be a global spill row (a generic pointer), read once here
-                // instead of D times in the product loop (same sums, same order)
+                // J_r to registers first: read once here instead of D times in the product loop (same sums, same order)
                 float jr[ND];
 #pragma unroll
                 for (int j = 0; j < ND; j++) jr[j] = Jr[j];
@@ -2110,6 +2132,7 @@ HD void substep(SimCtx& c, float hdt) {
 #pragma unroll
                     for (int j = 0; j < ND; j++) acc = fmaf(c.Minv[i * D + j], jr[j], acc);
                     Yr[i] = acc;
+                    a = fmaf(jr[i], acc, a);
                 }
             }
             for (int sl = 0; sl < (PC::rc ? 0 : row_slots<ND>()); sl++) {    // RC: Y already from obj_block
@@ -2125,10 +2148,7 @@ HD void substep(SimCtx& c, float hdt) {
                 f3 a = mv3(c.o[o].oIinv, mk3(Jos[3], Jos[4], Jos[5]));
                 Yos[3] = a.x; Yos[4] = a.y; Yos[5] = a.z;
             }
-            // same term order as the dense row: robot block, then the object blocks
-            float a = 0.0f;
-            if (Jr)
-                for (int t = 0; t < D; t++) a = fmaf(Jr[t], Yr[t], a);
+            // same term order as the dense row: robot block (above), then the object blocks
             for (int t = 0; t < RSN - D; t++) a = fmaf(Jo[t], Yo[t], a);
             winv_ = 1.0f / (a + 1e-9f);
         }
