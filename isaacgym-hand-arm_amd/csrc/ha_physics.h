@@ -398,6 +398,9 @@ HD void ct_ab(const SimCtx& c, int ci, int& a, int& b) {
         b = ct_lds(c, ci)->b;
     }
 }
+// typed views of a row pointer the caller knows to be LDS / global (the PGS fetch's two load paths stay apart)
+HD const HA_AS_LDS float* lds_f(const float* p) { return (const HA_AS_LDS float*)p; }
+HD const HA_AS_GLB float* glb_f(const float* p) { return (const HA_AS_GLB float*)p; }
 template <typename Q>
 HD void ct_fill(Q* q, f3 x, f3 n, float sep, int a, int b) {
     // eight dword stores: the two 16-bit body codes go as one packed word
@@ -2423,33 +2426,33 @@ HD void substep(SimCtx& c, float hdt) {
                     }
                 } else if (ix >= D) {
                     int t = ix - D;
-                    auto ldo = [&](const float* On, const float* OYn) {
+                    auto ldo = [&](auto On, auto OYn) {
                         j0n = On[t]; j1n = On[OW + t]; j2n = On[2 * OW + t];
                         y0n = OYn[t]; y1n = OYn[OW + t]; y2n = OYn[2 * OW + t];
                     };
-                    if (lds_obj) ldo(Ob + 3 * ci * OW, ObY + 3 * ci * OW);
-                    else ldo(orow_g(3 * ci, false), orow_g(3 * ci, true));
+                    if (lds_obj) ldo(lds_f(Ob + 3 * ci * OW), lds_f(ObY + 3 * ci * OW));
+                    else ldo(glb_f(orow_g(3 * ci, false)), glb_f(orow_g(3 * ci, true)));
                 } else if (ix >= 0) {
                     int ls = lsc;
-                    auto ld6 = [&](const float* Rn, const float* RYn) {
+                    auto ld6 = [&](auto Rn, auto RYn) {
                         j0n = Rn[ix]; j1n = Rn[ND + ix]; j2n = Rn[2 * ND + ix];
                         y0n = RYn[ix]; y1n = RYn[ND + ix]; y2n = RYn[2 * ND + ix];
                     };
-                    if (ls >= 0 && ls < KL) ld6(Rb + 3 * ls * ND, RbY + 3 * ls * ND);
-                    else if (ls >= KL) ld6(c.spill + 3 * (ls - KL) * ND, c.spill + SPJ + 3 * (ls - KL) * ND);
+                    if (ls >= 0 && ls < KL) ld6(lds_f(Rb + 3 * ls * ND), lds_f(RbY + 3 * ls * ND));
+                    else if (ls >= KL) ld6(glb_f(c.spill + 3 * (ls - KL) * ND), glb_f(c.spill + SPJ + 3 * (ls - KL) * ND));
                 }
                 if (VW == 2 && ixh >= D) {
                     int t = ixh - D;
-                    auto ldh = [&](const float* On, const float* OYn) {
+                    auto ldh = [&](auto On, auto OYn) {
                         h0n = On[t]; h1n = On[OW + t]; h2n = On[2 * OW + t];
                         g0n = OYn[t]; g1n = OYn[OW + t]; g2n = OYn[2 * OW + t];
                     };
-                    if (lds_obj) ldh(Ob + 3 * ci * OW, ObY + 3 * ci * OW);
-                    else ldh(orow_g(3 * ci, false), orow_g(3 * ci, true));
+                    if (lds_obj) ldh(lds_f(Ob + 3 * ci * OW), lds_f(ObY + 3 * ci * OW));
+                    else ldh(glb_f(orow_g(3 * ci, false)), glb_f(orow_g(3 * ci, true)));
                 }
                 return;
             }
-            auto ldd = [&](const float* Jn, const float* Yn) {
+            auto ldd = [&](auto Jn, auto Yn) {
                 if (ix >= 0) {
                     j0n = Jn[ix]; j1n = Jn[RSN + ix]; j2n = Jn[2 * RSN + ix];
                     y0n = Yn[ix]; y1n = Yn[RSN + ix]; y2n = Yn[2 * RSN + ix];
@@ -2461,8 +2464,8 @@ HD void substep(SimCtx& c, float hdt) {
                     }
                 }
             };
-            if (PC::ovf && ci >= CAP) ldd(gJ + 3 * (ci - CAP) * RSN, gY + 3 * (ci - CAP) * RSN);   // wave-uniform
-            else ldd(J + 3 * ci * RSN, Y + 3 * ci * RSN);
+            if (PC::ovf && ci >= CAP) ldd(glb_f(gJ + 3 * (ci - CAP) * RSN), glb_f(gY + 3 * (ci - CAP) * RSN));   // wave-uniform
+            else ldd(lds_f(J + 3 * ci * RSN), lds_f(Y + 3 * ci * RSN));
         };
         auto advance = [&]() {
             j0n = j0m; j1n = j1m; j2n = j2m; y0n = y0m; y1n = y1m; y2n = y2m;
