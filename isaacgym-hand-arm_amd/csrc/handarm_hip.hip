@@ -135,8 +135,10 @@ __host__ __device__ constexpr int task_col_planes() { return (FAM == HA_TASK_ALL
 #ifndef HA_AK_COMPACT
 #define HA_AK_COMPACT 1
 #endif
+// (3 since round 4: with the hand's self contacts most contacts touch links; the third slot fits in front of S,
+// 9.9 KB per env, still 16 workgroups per CU: C2 -0.4% and fewer spill-row writes)
 #ifndef HA_AK_LINK_SLOTS
-#define HA_AK_LINK_SLOTS 2
+#define HA_AK_LINK_SLOTS 3
 #endif
 // AllegroHand in the same compact layout (split rows, no gather buffer, S in the union): every AllegroHand contact
 // touches a finger link, so its rows are robot blocks in HA_AH_LINK_SLOTS LDS slots and the global spill rows
