@@ -1044,6 +1044,47 @@ int ha_simulate(ha_handle h, int32_t n_calls, uint32_t flags, void* stream) {
     return launch(h, MODE_SIMULATE, n_calls, flags, 0, stream);
 }
 
+// Longest-first dispatch order from the contacts each env offered since the last call (contact_stats column 3 minus
+// cost_prev, which is then updated): one workgroup, a counting sort on the cost clamped to 1023 (descending; envs of
+// equal cost in arbitrary order: the order is a scheduling hint, results do not depend on it). One launch instead of
+// the ~10 small torch kernels of a device argsort
+extern "C" __global__ void __launch_bounds__(1024) ha_env_order_kernel(const int32_t* __restrict__ stats,
+                                                                        int32_t* __restrict__ cost_prev,
+                                                                        int32_t* __restrict__ order, int n) {
+    __shared__ int cnt[1024], pos[1024];
+    int t = threadIdx.x;
+    auto bucket = [&](int e) {
+        int cost = stats[4 * (size_t)e + 3] - cost_prev[e];
+        return 1023 - (cost < 0 ? 0 : (cost > 1023 ? 1023 : cost));      // bucket 0: the most expensive envs
+    };
+    cnt[t] = 0;
+    __syncthreads();
+    for (int e = t; e < n; e += 1024) atomicAdd(&cnt[bucket(e)], 1);
+    __syncthreads();
+    pos[t] = cnt[t];
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {           // inclusive scan of the bucket counts (Hillis-Steele)
+        int v = t >= off ? pos[t - off] : 0;
+        __syncthreads();
+        pos[t] += v;
+        __syncthreads();
+    }
+    pos[t] -= cnt[t];                                    // exclusive: each bucket's first slot
+    __syncthreads();
+    for (int e = t; e < n; e += 1024) {
+        order[atomicAdd(&pos[bucket(e)], 1)] = e;
+        cost_prev[e] = stats[4 * (size_t)e + 3];
+    }
+}
+
+int ha_update_env_order(ha_handle h, int32_t* order, int32_t* cost_prev, void* stream) {
+    if (!h || !h->bound || !order || !cost_prev || !h->st.contact_stats) return HA_E_ARG;
+    hipLaunchKernelGGL(ha_env_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, h->st.contact_stats,
+                       cost_prev, order, h->N);
+    HIPCHK(hipGetLastError());
+    return HA_OK;
+}
+
 int ha_set_env_order(ha_handle h, const int32_t* order, int32_t n) {
     if (!h || (order && n != h->N)) return HA_E_ARG;
     h->order = order;

@@ -78,9 +78,10 @@ class HandArmSim:
         _lib.check(self.lib.ha_bind_state(self.h, C.byref(self.state)), "ha_bind_state")
         _lib.check(self.lib.ha_set_stats_ring(self.h, stats_ring), "ha_set_stats_ring")
         # longest-first dispatch order of the fused step (ha_set_env_order), refreshed every `rebalance_every` steps
-        # (0: identity order). An explicit argument wins; HA_REBALANCE (A/B scripts) only replaces the default 4
+        # (0: identity order; one ha_update_env_order launch per refresh). An explicit argument wins; HA_REBALANCE (A/B
+        # scripts) only replaces the default 1
         if rebalance_every is None:
-            rebalance_every = int(os.environ.get("HA_REBALANCE", 4))
+            rebalance_every = int(os.environ.get("HA_REBALANCE", 1))
         self.rebalance_every = int(rebalance_every)
         self._rb_count = 0
         if self.rebalance_every > 0:
@@ -106,10 +107,9 @@ class HandArmSim:
         host sync). In a launch with more envs than resident workgroup slots, the slots that free up take the
         cheaper envs last, so the launch's tail shrinks (longest-processing-time order); a one-round launch spreads
         its heavy envs over the CUs. Results do not depend on the order (one workgroup per env)."""
-        cs = self.t["contact_stats"][:, 3]
-        cost = cs - self._cost_prev
-        self._cost_prev.copy_(cs)
-        self._env_order.copy_(torch.argsort(cost, descending=True, stable=True))
+        _lib.check(self.lib.ha_update_env_order(self.h, C.c_void_p(self._env_order.data_ptr()),
+                                                C.c_void_p(self._cost_prev.data_ptr()), self._stream()),
+                   "ha_update_env_order")
 
     def _init_kuka(self):
         """AllegroKuka buffers at env creation: per-env object dims and keypoint offsets, goal_states
