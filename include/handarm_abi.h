@@ -476,8 +476,8 @@ int ha_contact_capacity(ha_handle h);
 int ha_set_env_order(ha_handle h, const int32_t* order, int32_t n);
 /* v12: refresh a dispatch order in place on the device (one launch, no host sync): the envs that offered the most
  * contacts since the last refresh (contact_stats column 3 minus cost_prev[N], which is then updated) first; order[N]
- * is typically the array handed to ha_set_env_order */
-int ha_update_env_order(ha_handle h, int32_t* order, int32_t* cost_prev, void* stream);
+ * is typically the array handed to ha_set_env_order. snake > 0 reverses every other block of `snake` positions */
+int ha_update_env_order(ha_handle h, int32_t* order, int32_t* cost_prev, int32_t snake, void* stream);
 /* time in ms of the most recent physics/step launch, from its HIP events; -1 when that launch was not timed (timing
  * off, or the ha_enable_kernel_timing record buffer full) or none ran */
 float ha_last_kernel_ms(ha_handle h);

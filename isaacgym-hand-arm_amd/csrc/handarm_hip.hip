@@ -1050,7 +1050,8 @@ int ha_simulate(ha_handle h, int32_t n_calls, uint32_t flags, void* stream) {
 // the ~10 small torch kernels of a device argsort
 extern "C" __global__ void __launch_bounds__(1024) ha_env_order_kernel(const int32_t* __restrict__ stats,
                                                                         int32_t* __restrict__ cost_prev,
-                                                                        int32_t* __restrict__ order, int n) {
+                                                                        int32_t* __restrict__ order, int n,
+                                                                        int snake) {
     __shared__ int cnt[1024], pos[1024];
     int t = threadIdx.x;
     auto bucket = [&](int e) {
@@ -1072,15 +1073,24 @@ extern "C" __global__ void __launch_bounds__(1024) ha_env_order_kernel(const int
     pos[t] -= cnt[t];                                    // exclusive: each bucket's first slot
     __syncthreads();
     for (int e = t; e < n; e += 1024) {
-        order[atomicAdd(&pos[bucket(e)], 1)] = e;
+        int q = atomicAdd(&pos[bucket(e)], 1);
+        if (snake > 0) {
+            // rank q -> position: every other block of `snake` positions reversed, so that the workgroups dispatched
+            // to the same CU in successive blocks alternate heavy and light (block = the CU count: one wave per CU
+            // per block)
+            int blk = q / snake, j = q - blk * snake;
+            int last = blk * snake + snake <= n ? snake : n - blk * snake;
+            if (blk & 1) q = blk * snake + (last - 1 - j);
+        }
+        order[q] = e;
         cost_prev[e] = stats[4 * (size_t)e + 3];
     }
 }
 
-int ha_update_env_order(ha_handle h, int32_t* order, int32_t* cost_prev, void* stream) {
-    if (!h || !h->bound || !order || !cost_prev || !h->st.contact_stats) return HA_E_ARG;
+int ha_update_env_order(ha_handle h, int32_t* order, int32_t* cost_prev, int32_t snake, void* stream) {
+    if (!h || !h->bound || !order || !cost_prev || !h->st.contact_stats || snake < 0) return HA_E_ARG;
     hipLaunchKernelGGL(ha_env_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, h->st.contact_stats,
-                       cost_prev, order, h->N);
+                       cost_prev, order, h->N, snake);
     HIPCHK(hipGetLastError());
     return HA_OK;
 }

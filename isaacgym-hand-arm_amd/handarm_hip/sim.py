@@ -83,6 +83,7 @@ class HandArmSim:
         if rebalance_every is None:
             rebalance_every = int(os.environ.get("HA_REBALANCE", 1))
         self.rebalance_every = int(rebalance_every)
+        self._snake = int(os.environ.get("HA_ORDER_SNAKE", 0))     # A/B: alternate-block reversal of the order
         self._rb_count = 0
         if self.rebalance_every > 0:
             self._env_order = torch.arange(num_envs, dtype=torch.int32, device=self.device)
@@ -108,7 +109,7 @@ class HandArmSim:
         cheaper envs last, so the launch's tail shrinks (longest-processing-time order); a one-round launch spreads
         its heavy envs over the CUs. Results do not depend on the order (one workgroup per env)."""
         _lib.check(self.lib.ha_update_env_order(self.h, C.c_void_p(self._env_order.data_ptr()),
-                                                C.c_void_p(self._cost_prev.data_ptr()), self._stream()),
+                                                C.c_void_p(self._cost_prev.data_ptr()), self._snake, self._stream()),
                    "ha_update_env_order")
 
     def _init_kuka(self):
