@@ -421,6 +421,10 @@ struct StepIO {
     float* partials;        // 4 floats per group of 64 envs
     int32_t* counters;      // per group, then one for the groups; zero between launches
     float clip_act, clip_obs;
+    // ha_set_order_cost(h, 1): each env's workgroup start and end in this launch (100 MHz clock) for the
+    // dispatch-order refresh (null: off)
+    unsigned long long* tstart;
+    unsigned long long* tend;
 };
 
 // AllegroKuka extras: mean prev_episode_successes, mean / min / max true_objective over the shard, in the step launch.
@@ -648,7 +652,15 @@ __device__ unsigned int g_envhw[2 * 65536];
              int num_envs, int n_calls, uint32_t flags, int stat_slot, float* spill, const int32_t* env_ids,     \
              StepIO io) {                                                                                       \
         HA_ENV_T0();                                                                                            \
+        if (MODE == MODE_STEP && io.tend) {  /* by launch slot, like HA_ENV_T0 / T1 */                        \
+            unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                           \
+            if (threadIdx.x == 0) io.tstart[blockIdx.x] = t_;                                                   \
+        }                                                                                                       \
         env_body<FAM, MODE>(model, params, st, num_envs, n_calls, flags, stat_slot, spill, env_ids, io);       \
+        if (MODE == MODE_STEP && io.tend) {                                                                     \
+            __syncthreads();                                                                                    \
+            if (threadIdx.x == 0) io.tend[blockIdx.x] = __builtin_amdgcn_s_memrealtime();                      \
+        }                                                                                                       \
         HA_ENV_T1();                                                                                            \
     }
 HA_KERNEL(ha_step_kernel, HA_TASK_UR5SIH, MODE_STEP)
@@ -792,6 +804,8 @@ struct ha_handle_s {
     float* d_spill;       // split-row families: robot-block rows beyond the LDS slots, N x spill_floats
     const int32_t* order; // ha_set_env_order: env of workgroup i in full-shard launches (null: identity)
     StepIO io;            // ha_task_step_io: the step launch's folded head / tail (zero otherwise)
+    unsigned long long* d_tstart;   // ha_set_order_cost(1): workgroup start / end stamps per env
+    unsigned long long* d_tend;
     float* d_io_partials; // AllegroKuka extras: 4 floats per group of 64 envs
     int32_t* d_io_counters;   // and ceil(N / 64) + 1 counters, zero between launches
 };
@@ -997,6 +1011,8 @@ int ha_destroy(ha_handle h) {
     if (h->d_spill) (void)hipFree(h->d_spill);
     if (h->d_io_partials) (void)hipFree(h->d_io_partials);
     if (h->d_io_counters) (void)hipFree(h->d_io_counters);
+    if (h->d_tstart) (void)hipFree(h->d_tstart);
+    if (h->d_tend) (void)hipFree(h->d_tend);
     (void)hipEventDestroy(h->ev0);
     (void)hipEventDestroy(h->ev1);
     free(h);
@@ -1051,11 +1067,20 @@ int ha_simulate(ha_handle h, int32_t n_calls, uint32_t flags, void* stream) {
 extern "C" __global__ void __launch_bounds__(1024) ha_env_order_kernel(const int32_t* __restrict__ stats,
                                                                         int32_t* __restrict__ cost_prev,
                                                                         int32_t* __restrict__ order, int n,
-                                                                        int snake) {
+                                                                        int snake,
+                                                                        const unsigned long long* __restrict__ t0,
+                                                                        const unsigned long long* __restrict__ t1) {
     __shared__ int cnt[1024], pos[1024];
     int t = threadIdx.x;
+    if (t1) {
+        // the spans are per launch slot: slot s ran env order[s] (the order being replaced); cost_prev holds them per
+        // env for the passes below (5.12 us units: 100 MHz clock >> 9)
+        for (int q = t; q < n; q += 1024) cost_prev[order[q]] = (int)((t1[q] - t0[q]) >> 9);
+        __syncthreads();
+    }
     auto bucket = [&](int e) {
-        int cost = stats[4 * (size_t)e + 3] - cost_prev[e];
+        // the span, or the contacts offered since the last refresh
+        int cost = t1 ? cost_prev[e] : stats[4 * (size_t)e + 3] - cost_prev[e];
         return 1023 - (cost < 0 ? 0 : (cost > 1023 ? 1023 : cost));      // bucket 0: the most expensive envs
     };
     cnt[t] = 0;
@@ -1083,15 +1108,36 @@ extern "C" __global__ void __launch_bounds__(1024) ha_env_order_kernel(const int
             if (blk & 1) q = blk * snake + (last - 1 - j);
         }
         order[q] = e;
-        cost_prev[e] = stats[4 * (size_t)e + 3];
+        if (!t1) cost_prev[e] = stats[4 * (size_t)e + 3];
     }
 }
 
 int ha_update_env_order(ha_handle h, int32_t* order, int32_t* cost_prev, int32_t snake, void* stream) {
     if (!h || !h->bound || !order || !cost_prev || !h->st.contact_stats || snake < 0) return HA_E_ARG;
     hipLaunchKernelGGL(ha_env_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, h->st.contact_stats,
-                       cost_prev, order, h->N, snake);
+                       cost_prev, order, h->N, snake, (const unsigned long long*)h->d_tstart,
+                       (const unsigned long long*)h->d_tend);
     HIPCHK(hipGetLastError());
+    return HA_OK;
+}
+
+// the dispatch-order refresh's cost: 0 the contacts each env offered (default), 1 each env's workgroup span in the
+// last step launch (measured by the step kernels: two clock reads and two stores per env)
+int ha_set_order_cost(ha_handle h, int32_t mode) {
+    if (!h || mode < 0 || mode > 1) return HA_E_ARG;
+    if (mode == 1 && !h->d_tend) {
+        HIPCHK(hipMalloc(&h->d_tstart, sizeof(unsigned long long) * (size_t)h->N));
+        HIPCHK(hipMalloc(&h->d_tend, sizeof(unsigned long long) * (size_t)h->N));
+        HIPCHK(hipMemset(h->d_tstart, 0, sizeof(unsigned long long) * (size_t)h->N));
+        HIPCHK(hipMemset(h->d_tend, 0, sizeof(unsigned long long) * (size_t)h->N));
+    } else if (mode == 0 && h->d_tend) {
+        (void)hipFree(h->d_tstart);
+        (void)hipFree(h->d_tend);
+        h->d_tstart = nullptr;
+        h->d_tend = nullptr;
+    }
+    h->io.tstart = h->d_tstart;
+    h->io.tend = h->d_tend;
     return HA_OK;
 }
 
@@ -1220,9 +1266,12 @@ int ha_task_step_io(ha_handle h, uint32_t flags, const float* actions, float cli
     if (h->fam != HA_TASK_ALLEGRO_KUKA && h->fam != HA_TASK_ALLEGRO_HAND) return HA_E_ARG;
     if (scalars && (h->fam != HA_TASK_ALLEGRO_KUKA || !h->d_io_counters)) return HA_E_ARG;
     if ((actions && !(clip_actions >= 0.0f)) || (obs_out && !(clip_obs >= 0.0f))) return HA_E_ARG;
-    h->io = StepIO{actions, obs_out, scalars, h->d_io_partials, h->d_io_counters, clip_actions, clip_obs};
+    h->io = StepIO{actions, obs_out, scalars, h->d_io_partials, h->d_io_counters, clip_actions, clip_obs,
+                   h->d_tstart, h->d_tend};
     int rc = ha_task_step(h, flags, stream);
     h->io = StepIO{};
+    h->io.tstart = h->d_tstart;
+    h->io.tend = h->d_tend;
     return rc;
 }
 

@@ -42,6 +42,7 @@ SIGNATURES = {
     "ha_contact_capacity": ([H], C.c_int),
     "ha_set_env_order": ([H, C.c_void_p, C.c_int32], C.c_int),
     "ha_update_env_order": ([H, C.c_void_p, C.c_void_p, C.c_int32, S], C.c_int),
+    "ha_set_order_cost": ([H, C.c_int32], C.c_int),
     "ha_enable_kernel_timing": ([H, C.c_int32], C.c_int),
     "ha_kernel_times": ([H, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32)], C.c_int),
     "ha_pointclouds": ([H, C.POINTER(HM.HaPointcloud), S], C.c_int),

@@ -84,6 +84,10 @@ class HandArmSim:
             rebalance_every = int(os.environ.get("HA_REBALANCE", 1))
         self.rebalance_every = int(rebalance_every)
         self._snake = int(os.environ.get("HA_ORDER_SNAKE", 0))     # A/B: alternate-block reversal of the order
+        # the refresh sorts by each env's workgroup span in the last step launch (round 4: C4 +13% against the
+        # contacts offered, which stays available as HA_ORDER_COST=contacts for A/B runs)
+        if self.rebalance_every > 0 and os.environ.get("HA_ORDER_COST", "time") == "time":
+            _lib.check(self.lib.ha_set_order_cost(self.h, 1), "ha_set_order_cost")
         self._rb_count = 0
         if self.rebalance_every > 0:
             self._env_order = torch.arange(num_envs, dtype=torch.int32, device=self.device)

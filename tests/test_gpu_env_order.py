@@ -17,6 +17,7 @@ def test_env_order_is_a_longest_first_permutation(n):
     env.reset()
     sim = env.sim
     assert sim.rebalance_every > 0
+    assert sim.lib.ha_set_order_cost(sim.h, 0) == 0      # the contacts-offered cost (the default sorts by spans)
     g = torch.Generator(device="cuda:0").manual_seed(3)
     for _ in range(3):
         env.step(torch.rand((n, env.num_acts), device="cuda:0", generator=g) * 2 - 1)
@@ -31,3 +32,24 @@ def test_env_order_is_a_longest_first_permutation(n):
     assert (np.diff(cost) <= 0).all()
     assert np.array_equal(sim._cost_prev.cpu().numpy(), cs.astype(np.int32))
     assert cost[0] > cost[-1]           # the envs did differ in contacts
+
+
+@pytest.mark.gpu
+def test_env_order_by_workgroup_spans_is_a_permutation():
+    """The default cost: each env's workgroup span in the last step launch (stamped by the step kernel per launch
+    slot, mapped to envs through the order that launch used)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from handarm_hip.tasks import isaacgym_task_map
+    n = 1000
+    env = isaacgym_task_map["AllegroHand"]({"env": {"numEnvs": n}}, "cuda:0", "cuda:0")
+    env.reset()
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    orders = []
+    for _ in range(4):
+        env.step(torch.rand((n, env.num_acts), device="cuda:0", generator=g) * 2 - 1)
+        torch.cuda.synchronize()
+        orders.append(env.sim._env_order.cpu().numpy().copy())
+    for o in orders:
+        assert np.array_equal(np.sort(o), np.arange(n))
+    assert not all(np.array_equal(orders[0], o) for o in orders[1:])   # the spans differ, so does the order
