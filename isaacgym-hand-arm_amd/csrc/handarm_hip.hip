@@ -1071,16 +1071,31 @@ extern "C" __global__ void __launch_bounds__(1024) ha_env_order_kernel(const int
                                                                         const unsigned long long* __restrict__ t0,
                                                                         const unsigned long long* __restrict__ t1) {
     __shared__ int cnt[1024], pos[1024];
+    __shared__ int span_max;
     int t = threadIdx.x;
+    if (t == 0) span_max = 1;
+    __syncthreads();
     if (t1) {
         // the spans are per launch slot: slot s ran env order[s] (the order being replaced); cost_prev holds them per
-        // env for the passes below (5.12 us units: 100 MHz clock >> 9)
-        for (int q = t; q < n; q += 1024) cost_prev[order[q]] = (int)((t1[q] - t0[q]) >> 9);
+        // env for the passes below (100 MHz clock ticks)
+        int m = 1;
+        for (int q = t; q < n; q += 1024) {
+            unsigned long long d = t1[q] >= t0[q] ? t1[q] - t0[q] : 0ull;
+            int v = d > 0x7FFFFFFFull ? 0x7FFFFFFF : (int)d;
+            cost_prev[order[q]] = v;
+            m = v > m ? v : m;
+        }
+        atomicMax(&span_max, m);
         __syncthreads();
     }
+    const long long smax = span_max;
     auto bucket = [&](int e) {
-        // the span, or the contacts offered since the last refresh
-        int cost = t1 ? cost_prev[e] : stats[4 * (size_t)e + 3] - cost_prev[e];
+        // the span scaled so that the longest lands in bucket 0 (the spans of a long launch, C5's ~7 ms per env,
+        // would saturate a fixed unit), or the contacts offered since the last refresh
+        int cost = t1 ? (int)((long long)cost_prev[e] * 1023 / smax) : stats[4 * (size_t)e + 3] - cost_prev[e];
+#ifdef HA_X_ORDER_FIXED_UNIT    /* A/B: the fixed 5.12 us bucket of the first span-based order */
+        if (t1) cost = cost_prev[e] >> 9;
+#endif
         return 1023 - (cost < 0 ? 0 : (cost > 1023 ? 1023 : cost));      // bucket 0: the most expensive envs
     };
     cnt[t] = 0;
