@@ -1082,6 +1082,10 @@ extern "C" __global__ void __launch_bounds__(1024) ha_env_order_kernel(const int
         for (int q = t; q < n; q += 1024) {
             unsigned long long d = t1[q] >= t0[q] ? t1[q] - t0[q] : 0ull;
             int v = d > 0x7FFFFFFFull ? 0x7FFFFFFF : (int)d;
+#ifndef HA_X_ORDER_LAST_SPAN    /* A/B: the last span alone */
+            // half the last span plus half the previous estimate (C5 +1%, C4 +0.7% against the last span alone)
+            v = (int)(((long long)v + cost_prev[order[q]]) >> 1);
+#endif
             cost_prev[order[q]] = v;
             m = v > m ? v : m;
         }
