@@ -478,8 +478,9 @@ int ha_set_env_order(ha_handle h, const int32_t* order, int32_t n);
  * contacts since the last refresh (contact_stats column 3 minus cost_prev[N], which is then updated) first; order[N]
  * is typically the array handed to ha_set_env_order. snake > 0 reverses every other block of `snake` positions */
 int ha_update_env_order(ha_handle h, int32_t* order, int32_t* cost_prev, int32_t snake, void* stream);
-/* v12: the cost that refresh sorts by: 0 the contacts each env offered since the last refresh (default), 1 each
- * env's workgroup span in the last step launch (the step kernels then stamp their start and end) */
+/* v12: the cost that refresh sorts by: 0 the contacts each env offered since the last refresh (the handle's
+ * default), 1 a running estimate of each env's workgroup span in the step launches (half the last span plus half the
+ * previous estimate; the step kernels then stamp their start and end per launch slot). HandArmSim selects 1 */
 int ha_set_order_cost(ha_handle h, int32_t mode);
 /* time in ms of the most recent physics/step launch, from its HIP events; -1 when that launch was not timed (timing
  * off, or the ha_enable_kernel_timing record buffer full) or none ran */
