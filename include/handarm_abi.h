@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 12
+#define HA_ABI_VERSION 13
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -68,6 +68,12 @@ extern "C" {
 #define HA_MAX_MPAIRS 192
 #define HA_MAX_SELF_PAIRS 512  /* robot link-hull pairs tested for self-collision (v12) */
 #define HA_DRAW_STRIDE 80     /* floats of reset_draws per env (replayed host RNG draws) */
+/* v13: persistent contact manifolds (ha_state_t.contact_cache): one record of HA_PCM_REC floats per candidate pair
+ * slot of an env. Record: [0..2] the pair's relative position (side A's body origin in side B's body frame) when the
+ * manifold was built, [3] its point count k (0 = empty), [4..7] the relative rotation conj(q_B) q_A (xyzw), then per
+ * point t < k at 8 + 9 t: the point on A in A's frame (3), the point on B in B's frame (3), the normal in B's frame (3) */
+#define HA_PCM_REC 48
+#define HA_CSTAT 8             /* ha_state_t.contact_stats columns (v13: 8, was 4) */
 /* per-env domain-randomization samples (ha_state_t.dr_scale rows) */
 #define HA_DR_LINK_MASS 0      /* [HA_MAX_LINKS] robot link mass (and inertia) scale */
 #define HA_DR_OBJ_MASS 32      /* [HA_MAX_OBJ] object mass (and inertia) scale */
@@ -295,6 +301,14 @@ typedef struct ha_params_t {
     /* v10: narrow-phase switches (A/B timing, diagnostics; 0 = the full narrow phase): HA_NP_NO_EDGE_AXES skips
      * the edge-edge axes, HA_NP_NO_CLIP keeps a face manifold to its incident vertices (the v9 narrow phase) */
     int32_t narrow_phase_flags;
+    /* v13: persistent contact manifolds (PhysX's persistent contact manifold, PCM; inferred: its source is closed). A
+     * candidate pair whose relative pose moved less than pcm_lin_tol (m) and whose relative rotation stayed within
+     * pcm_cos_tol (|dot| of the relative quaternions, cos of half the angle) of the pose its record was built at
+     * reuses the record's points: each point's separation, position and normal are re-evaluated from the current
+     * body poses (points separated by more than contact_margin are dropped), and the narrow phase does not run.
+     * Otherwise the narrow phase runs and a pair that yields contacts rewrites its record. pcm_lin_tol <= 0 or a
+     * null contact_cache: every candidate pair runs the narrow phase (the round-4 behaviour). */
+    float pcm_lin_tol, pcm_cos_tol;
 } ha_params_t;
 
 /* Device buffers (caller-allocated). Layouts match the Isaac Gym tensors exactly. */
@@ -347,10 +361,19 @@ typedef struct ha_state_t {
     float* task_scalars;        /* [4] AllegroKuka host-curriculum scalars: success_tolerance,
                                  * tolerance objective, 1 if tolerance > target, keypoint success tolerance */
     /* v7 */
-    int32_t* contact_stats;     /* [N][4] contact-list diagnostics added up by every launch (null = off):
-                                 * substeps, substeps whose narrow phases offered more contacts than the list
-                                 * holds (the shallowest are dropped), max contacts offered in one substep,
-                                 * sum of contacts offered */
+    int32_t* contact_stats;     /* [N][HA_CSTAT] contact-list diagnostics added up by every launch (null = off):
+                                 * [0] substeps, [1] substeps whose pairs offered more contacts than the list holds
+                                 * (the shallowest are dropped), [2] max contacts offered in one substep, [3] sum of
+                                 * contacts offered, [4] sum of self-collision contacts offered (both bodies robot
+                                 * links), [5] pair manifolds refreshed from their persistent record (v13),
+                                 * [6] hull-pair narrow phases run (kernel diagnostics: exact culls such as the
+                                 * separating-face record are not counted), [7] 0 */
+    /* v13 */
+    float* contact_cache;       /* [N][ha_contact_cache_slots][HA_PCM_REC] persistent contact manifolds (null = off);
+                                 * zero-initialised by the caller; slot = the pair's index in the broad phase's
+                                 * enumeration (objects: ground, statics, later objects, link hulls; then link hulls x
+                                 * statics), then n_self_pairs self pairs. Keyed by relative pose: a caller that
+                                 * changes an env's object geometry (object_indices, object_scale) zeroes its rows */
 } ha_state_t;
 
 /* stats layout (int32): [0] num_resets, [1] num_successes, then per pool object
@@ -469,6 +492,8 @@ int ha_task_step_io(ha_handle h, uint32_t flags, const float* actions, float cli
                     float clip_obs, float* scalars, void* stream);
 /* v9: contacts per substep the handle's kernel family holds (over it, the shallowest give way) */
 int ha_contact_capacity(ha_handle h);
+/* v13: persistent-manifold record slots per env (ha_state_t.contact_cache rows of HA_PCM_REC floats) */
+int ha_contact_cache_slots(ha_handle h);
 /* v11: dispatch order of the full-shard launches (no gym counterpart: a scheduling hint; results do not depend on
  * it). order: device array of the N env indices, a permutation, that workgroup i of every later full-shard launch
  * simulates (kept by pointer: the caller keeps it alive), or NULL for the identity. Envs expected to take longest

@@ -116,7 +116,7 @@ struct EnvLDS {
     float v[MAXV];
     int nc, nr, noff, ng;                       // contacts kept / rows / contacts offered this substep /
                                                 // points gathered for a compound object pair
-    int cst[4];                                 // contact_stats of this launch (see ha_state_t)
+    int cst[HA_CSTAT];                          // contact_stats of this launch (see ha_state_t)
     union {
         PostScratch pd;                         // (the narrow-phase scratch, ColLayout, is sized per family)
         RowScratch rows;
@@ -337,6 +337,10 @@ struct SimCtx {
     const float* act_in;
     float* obs_out;
     float clip_act, clip_obs;
+    // persistent contact manifolds (ha_params_t v13): this env's records (ha_state_t.contact_cache; null: off), and
+    // the running pair's slot (-1: none) and description, whose narrow phase writes the record it emits
+    float* pcm;
+    int pslot, pkind, pA, pB;
 #ifdef HA_PROFILE
     int pk;                 // profiled build: kind of the running pair
     int pcls;               // profiled build: this substep is heavy (g_prof's second set)
@@ -772,13 +776,29 @@ HD f3 inv_scale(const SimCtx& c, int b) {
     return mk3(1.0f / sc[0], 1.0f / sc[1], 1.0f / sc[2]);
 }
 
-HD void store_chosen(SimCtx& c, int k, const f3* P, const f3* N, const float* S, int a, int b);
+HD void store_chosen(SimCtx& c, int k, const f3* P, const f3* N, const float* S, const int* CD, int a, int b);
+HD void pcm_store(SimCtx& c, int t, int k, f3 x, f3 n, float sep, int code);
+// A manifold point's anchor for its persistent record (v13; the oracle's PCM_*): the feature it came from - a vertex or
+// clipped edge point of side A, of side B, or neither (the midpoint of two edges' closest points) - plus PCM_NORMAL_A
+// when the normal is carried by side A (the reference face is A's; B for the ground and edge-edge contacts)
+#define PCM_FEAT_A 0
+#define PCM_FEAT_B 1
+#define PCM_FEAT_MID 2
+#define PCM_NORMAL_A 4
+// the contacts a pair offers to the list (lane 0; contact_stats columns 3 and 4 via EnvLDS noff / cst)
+HD void count_offered(SimCtx& c, int k, int a, int b) {
+    EnvLDS& s = *c.s;
+    if (c.lane == 0) {
+        s.noff += k;
+        if (a >= 100 && b >= 100) s.cst[4] += k;
+    }
+}
 
 // append up to 4 reduced contacts (lane 0 does the list bookkeeping, same policy as the oracle). n is the
 // lane's normal: one value over the wave for a convex pair; a compound object pair's gathered points keep
 // their piece pair's normal, and the area criterion then measures about the deepest point's normal. While
 // c.gather is set (a compound pair's piece pairs) the reduced points go to the gather buffer instead.
-HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int b) {
+HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int b, int code) {
     EnvLDS& s = *c.s;
     int lane = c.lane;
 #ifdef HA_AB_TIMING
@@ -818,13 +838,16 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
 #ifndef HA_EMIT_PARALLEL
 #define HA_EMIT_PARALLEL 1
 #endif
+    // the chosen lanes' ranks: point t of the manifold (the oracle's idx order)
+    int t = lane == i0 ? 0 : (k > 1 && lane == j1 ? 1 : (k > 2 && lane == j2 ? 2 : (k > 3 && lane == j3 ? 3 : -1)));
+    if (c.pslot >= 0 && !c.gather) pcm_store(c, t, k, pt, n, sep, code);    // the pair's record (ha_params_t v13)
     if (HA_EMIT_PARALLEL && !c.gather) {
         int nc0 = s.nc;
         if (nc0 + k <= c.maxc) {
             // room for all k points (the common case): each chosen lane writes its own point into slot nc + t,
             // the values lane 0 would write after broadcasting them (the chosen lanes are distinct)
-            if (lane == 0) { s.noff += k; s.nc = nc0 + k; }
-            int t = lane == i0 ? 0 : (k > 1 && lane == j1 ? 1 : (k > 2 && lane == j2 ? 2 : (k > 3 && lane == j3 ? 3 : -1)));
+            count_offered(c, k, a, b);
+            if (lane == 0) s.nc = nc0 + k;
             if (t >= 0) ct_put(c, nc0 + t, pt, n, sep, a, b);
             wsync();
             return;
@@ -833,19 +856,21 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
     // the chosen points to every lane
     f3 P[4], N[4];
     float S[4];
+    int CD[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         int src = t == 0 ? i0 : (t < k ? (t == 1 ? j1 : (t == 2 ? j2 : j3)) : 0);
         P[t] = mk3(bcast(pt.x, src), bcast(pt.y, src), bcast(pt.z, src));
         N[t] = mk3(bcast(n.x, src), bcast(n.y, src), bcast(n.z, src));
         S[t] = bcast(sep, src);
+        CD[t] = bcast_i(code, src);
     }
-    store_chosen(c, k, P, N, S, a, b);
+    store_chosen(c, k, P, N, S, CD, a, b);
 }
 
 // the k <= 4 chosen points of a manifold (wave-uniform P, N, S) into the gather buffer (a compound pair's piece
 // pairs) or the contact list: lane 0 appends, or (list full) replaces the shallowest contact if the new one is deeper
-HD void store_chosen(SimCtx& c, int k, const f3* P, const f3* N, const float* S, int a, int b) {
+HD void store_chosen(SimCtx& c, int k, const f3* P, const f3* N, const float* S, const int* CD, int a, int b) {
     EnvLDS& s = *c.s;
     int lane = c.lane;
     if (c.gather) {
@@ -859,6 +884,7 @@ HD void store_chosen(SimCtx& c, int k, const f3* P, const f3* N, const float* S,
                     st3(cs.gp[ng], P[t]);
                     cs.gp[ng][3] = S[t];
                     st3(cs.gn[ng], N[t]);
+                    cs.gn[ng][3] = __int_as_float(CD[t]);       // the point's persistent-record anchor
                     ng++;
                 }
             }
@@ -867,7 +893,7 @@ HD void store_chosen(SimCtx& c, int k, const f3* P, const f3* N, const float* S,
         wsync();
         return;
     }
-    if (lane == 0) s.noff += k;
+    count_offered(c, k, a, b);
     // lane 0 appends, or (list full) replaces the shallowest contact if this one is deeper: the shallowest is the first
     // maximum of sep over the list (the oracle's sequential strict-compare scan), found by a wave arg-max over
     // lanes = contacts instead of a scan on lane 0 (clutter scenes run with the list full)
@@ -914,7 +940,7 @@ HD void collide_ground(SimCtx& c, int hull, PoseF P, int a) {
             sep = v.z;
         }
     }
-    emit_contacts(c, valid, pt, sep, mk3(0, 0, 1), a, -1);
+    emit_contacts(c, valid, pt, sep, mk3(0, 0, 1), a, -1, PCM_FEAT_A);
 }
 
 // float <-> int mapping that preserves order (for LDS atomicMax over floats)
@@ -1286,7 +1312,7 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
             f3 n, pa, pb, e1, e2;
             edge_axis(cs, EA[la[bi]], EB[lb[bw - bi * nB]], cb, n, pa, e1, pb, e2);
             f3 x = edge_closest_mid(pa, e1, pb, e2);
-            emit_contacts(c, lane == 0, x, best, n, a, b);
+            emit_contacts(c, lane == 0, x, best, n, a, b, PCM_FEAT_MID);
             return;
         }
         wsync();                                            // the edge lists (cand / cmax) are reused below
@@ -1437,7 +1463,10 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         HPROF(31);
         if (__ballot(ok)) {
             f3 n = refB ? nref : nref * -1.0f;
-            emit_contacts(c, ok, x, sv, n, a, b);
+            // anchors: candidates (1) and (2) on the incident hull, (3) on the reference hull; the normal on the reference
+            int nA = refB ? 0 : PCM_NORMAL_A;
+            int code = (isref ? (refB ? PCM_FEAT_B : PCM_FEAT_A) : (refB ? PCM_FEAT_A : PCM_FEAT_B)) | nA;
+            emit_contacts(c, ok, x, sv, n, a, b, code);
             HPROF(29);
             return;
         }
@@ -1485,6 +1514,144 @@ HD void self_pair_hulls(const ha_model_t& m, int k, int& ha, int& hb) {
     hb = (int)(sp >> 8);
 }
 
+// ----------------------------------------------------------------------------- persistent contact manifolds (v13)
+// PhysX keeps a pair's contact manifold across substeps (persistent contact manifolds, PCM; inferred, its source is
+// closed) and refreshes its points from the bodies' current poses while their relative motion stays small. Here a
+// record per candidate pair (ha_state_t.contact_cache, slot = the pair's index in detect's enumeration, then the self
+// pairs) holds the manifold a narrow phase emitted: the relative pose it was built at, and per point the point on each
+// body in that body's frame and the normal in side B's frame. The oracle restates every expression (pcm_store,
+// pcm_refresh in physics_oracle.c), so results stay bit-identical.
+//
+// Side A / side B body poses and body codes of candidate pair (kind, A, B): the sides narrow_phase gives collide_hulls
+HD void pair_bodies(const SimCtx& c, int kind, int A, int B, PoseF& PA, PoseF& PB, int& a, int& b) {
+    const EnvLDS& s = *c.s;
+    const ha_model_t& m = *c.m;
+    if (kind <= 2) {
+        PA = object_pose_u(c, A);
+        a = A;
+        if (kind == 0) { PB = PoseF{mk3(0, 0, 0), qf{0, 0, 0, 1}}; b = -1; }    // the ground plane z = 0
+        else if (kind == 1) { PB = static_pose(m, B); b = -1; }
+        else { PB = object_pose_u(c, B); b = B; }
+    } else if (kind == 3) {
+        int Lk = m.hull_link[B];
+        PA = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])};
+        a = 100 + Lk;
+        PB = object_pose_u(c, A);
+        b = A;
+    } else if (kind == 4) {
+        int Lk = m.hull_link[A];
+        PA = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])};
+        a = 100 + Lk;
+        PB = static_pose(m, B);
+        b = -1;
+    } else {                                    // self pair A: hull b on side A, hull a on side B
+        int ha_, hb_;
+        self_pair_hulls(m, A, ha_, hb_);
+        int La = m.hull_link[ha_], Lb = m.hull_link[hb_];
+        PA = PoseF{ld3(s.lp[Lb]), ldq(s.lq[Lb])};
+        a = 100 + Lb;
+        PB = PoseF{ld3(s.lp[La]), ldq(s.lq[La])};
+        b = 100 + La;
+    }
+}
+HD qf qconj(qf q) { return qf{-q.x, -q.y, -q.z, q.w}; }
+
+// The record of the running pair's manifold (c.pslot), written by the chosen lanes of emit_contacts: lane of point
+// t < k its point on A (x + n sep / 2) in A's frame, its point on B (x - n sep / 2) in B's frame and its normal in B's
+// frame; lane 0 the relative pose and k. Vector stores: every record access of the kernel is a per-lane vector access
+HD void pcm_store(SimCtx& c, int t, int k, f3 x, f3 n, float sep, int code) {
+    PoseF PA, PB;
+    int a_, b_;
+    pair_bodies(c, c.pkind, c.pA, c.pB, PA, PB, a_, b_);
+    float* rec = c.pcm + (size_t)c.pslot * HA_PCM_REC;
+    qf qbc = qconj(PB.q);
+    if (t >= 0) {
+        float hs = 0.5f * sep;
+        qf qac = qconj(PA.q);
+        f3 la = qrot(qac, (x + n * hs) - PA.p);
+        f3 lb = qrot(qbc, (x - n * hs) - PB.p);
+        f3 ln = qrot((code & PCM_NORMAL_A) ? qac : qbc, n);
+        float* r = rec + 8 + 9 * t;
+        st3(r, la);
+        st3(r + 3, lb);
+        st3(r + 6, ln);
+        rec[44 + t] = (float)code;
+    }
+    if (c.lane == 0) {
+        st3(rec, qrot(qbc, PA.p - PB.p));
+        rec[3] = (float)k;
+        stq(rec + 4, qmul(qbc, PA.q));
+    }
+}
+
+// already-reduced points (lanes in order, valid ones only) into the contact list: the refreshed manifold of a record
+HD void emit_points(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int b) {
+    EnvLDS& s = *c.s;
+    int lane = c.lane;
+    uint64_t vm = __ballot(valid);
+    int k = __popcll(vm);
+    if (k == 0) return;
+    int nc0 = s.nc;
+    if (nc0 + k <= c.maxc) {
+        count_offered(c, k, a, b);
+        if (lane == 0) s.nc = nc0 + k;
+        if (valid) ct_put(c, nc0 + __popcll(vm & ((1ull << lane) - 1ull)), pt, n, sep, a, b);
+        wsync();
+        return;
+    }
+    f3 P[4], N[4];
+    float S[4];
+    int CD[4] = {0, 0, 0, 0};           // (the list path does not read the anchors)
+    uint64_t mk = vm;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        int src = mk ? __ffsll((unsigned long long)mk) - 1 : 0;
+        mk &= mk - 1;
+        P[t] = mk3(bcast(pt.x, src), bcast(pt.y, src), bcast(pt.z, src));
+        N[t] = mk3(bcast(n.x, src), bcast(n.y, src), bcast(n.z, src));
+        S[t] = bcast(sep, src);
+    }
+    store_chosen(c, k, P, N, S, CD, a, b);
+}
+
+// Pair slot `slot`'s record (oracle pcm_refresh): kh = its point count (read ahead by the caller). When it holds points
+// and the pair's relative pose (A's body in B's frame) is within pcm_lin_tol / pcm_cos_tol of the pose it was built at,
+// every point is re-evaluated from the current poses - the surface points carried by their bodies, the normal by B,
+// the separation along the normal, the point midway - those within the contact margin go to the list in record order,
+// and the pair needs no narrow phase (true)
+HD bool pcm_refresh(SimCtx& c, int slot, int kh, PoseF PA, PoseF PB, int a, int b) {
+    const ha_params_t& p = *c.p;
+    int lane = c.lane;
+    if (kh <= 0) return false;
+    const float* rec = c.pcm + (size_t)slot * HA_PCM_REC;
+    float hv = rec[lane & 7];               // the header, a word a lane (lane-indexed: never a scalar-cache load)
+    qf qbc = qconj(PB.q);
+    f3 d = qrot(qbc, PA.p - PB.p) - mk3(bcast(hv, 0), bcast(hv, 1), bcast(hv, 2));
+    float lt = p.pcm_lin_tol;
+    if (dot3(d, d) > lt * lt) return false;
+    qf qr = qmul(qbc, PA.q);
+    float cq = ((qr.x * bcast(hv, 4) + qr.y * bcast(hv, 5)) + qr.z * bcast(hv, 6)) + qr.w * bcast(hv, 7);
+    if (fabsf(cq) < p.pcm_cos_tol) return false;
+    bool valid = false;
+    f3 x = mk3(0, 0, 0), n = mk3(0, 0, 0);
+    float sp = 0.0f;
+    if (lane < kh && lane < 4) {
+        const float* r = rec + 8 + 9 * lane;
+        int code = (int)rec[44 + lane];
+        f3 wa = PA.p + qrot(PA.q, ld3(r));
+        f3 wb = PB.p + qrot(PB.q, ld3(r + 3));
+        n = qrot((code & PCM_NORMAL_A) ? PA.q : PB.q, ld3(r + 6));
+        sp = dot3(n, wa - wb);
+        valid = sp <= p.contact_margin;
+        // the point where the narrow phase puts it: half the separation off its feature along the normal
+        int f = code & 3;
+        x = f == PCM_FEAT_A ? wa - n * (0.5f * sp) : (f == PCM_FEAT_B ? wb + n * (0.5f * sp) : (wa + wb) * 0.5f);
+    }
+    emit_points(c, valid, x, sp, n, a, b);
+    if (lane == 0) c.s->cst[5] += 1;
+    return true;
+}
+
 // piece pairs of a candidate pair (1 unless an object is a compound of several convex pieces)
 HD int pair_pieces(const SimCtx& c, int kind, int A, int B) {
     const ha_model_t& m = *c.m;
@@ -1499,6 +1666,7 @@ HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
     const EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     if (kind == 0) {
+        if (c.lane == 0) c.s->cst[6] += 1;
         collide_ground(c, m.pool_hull[upool(c, A)] + j, object_pose_u(c, A), A);
         return;
     }
@@ -1540,6 +1708,7 @@ HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
         h1 = hb_; P1 = PoseF{ld3(s.lp[Lb]), ldq(s.lq[Lb])}; b1 = 100 + Lb;
         h2 = ha_; P2 = PoseF{ld3(s.lp[La]), ldq(s.lq[La])}; b2 = 100 + La; k2 = b2;
     }
+    if (c.lane == 0) c.s->cst[6] += 1;         // contact_stats: hull-pair narrow phases run (diagnostics)
     collide_hulls(c, h1, P1, h2, P2, b1, b2, b1, k2);
 }
 
@@ -1552,14 +1721,16 @@ HD void gather_emit(SimCtx& c, int kind, int A, int B) {
     bool valid = lane < s.ng;
     f3 pt = mk3(0, 0, 0), n = mk3(0, 0, 0);
     float sep = 0;
+    int code = 0;
     if (valid) {
         pt = ld3(cs.gp[lane]);
         sep = cs.gp[lane][3];
         n = ld3(cs.gn[lane]);
+        code = __float_as_int(cs.gn[lane][3]);
     }
     int a = kind == 3 ? 100 + c.m->hull_link[B] : A;
     int b = kind == 2 ? B : (kind == 3 ? A : -1);
-    emit_contacts(c, valid, pt, sep, n, a, b);
+    emit_contacts(c, valid, pt, sep, n, a, b, code);
 }
 
 // self-collision pass (ha_model_t v12; after every other pair, the oracle's order):
@@ -1575,7 +1746,7 @@ HD void gather_emit(SimCtx& c, int kind, int A, int B) {
 //     would stop on a face too (its SAT maximises over every face), so the pair is skipped with the same result.
 //     The record is a hint only: results never depend on it (the oracle has none);
 //  4. otherwise the hull narrow phase, which records the separating face for the next substep.
-HD void detect_self(SimCtx& c) {
+HD void detect_self(SimCtx& c, int npairs) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     int lane = c.lane, NLH = m.n_link_hulls, nsp = m.n_self_pairs;
@@ -1638,9 +1809,12 @@ HD void detect_self(SimCtx& c) {
         ncd += __popcll(mk);
     }
     wsync();
-    // the records of the first 64 candidates (in pair order, the order of the loop below), one load for all
+    // the records of the first 64 candidates (in pair order, the order of the loop below), one load for all; and the
+    // point counts of their persistent manifolds (slot npairs + pair)
     int crec = 0xFF;
     if (c.selfc && lane < ncd) crec = c.selfc[cdl[lane]];
+    float ckh = 0.0f;
+    if (c.pcm && lane < ncd) ckh = c.pcm[(size_t)(npairs + cdl[lane]) * HA_PCM_REC + 3];
 #ifdef HA_PROFILE
     PROF_COUNT(83, __builtin_amdgcn_s_memtime() - _s0);              // box table + box tests
 #endif
@@ -1661,9 +1835,24 @@ HD void detect_self(SimCtx& c) {
             PROF_COUNT(85, 1);                                              // candidates
 #endif
             int rec;
-            if (rank < 64) rec = __builtin_amdgcn_readlane(crec, rank);
-            else rec = __builtin_amdgcn_readfirstlane(c.selfc ? (int)c.selfc[k] : 0xFF);
+            float kh = 0.0f;
+            if (rank < 64) {
+                rec = __builtin_amdgcn_readlane(crec, rank);
+                kh = bcast(ckh, rank);
+            } else {
+                rec = __builtin_amdgcn_readfirstlane(c.selfc ? (int)c.selfc[k] : 0xFF);
+                if (c.pcm) kh = bcast(c.pcm[(size_t)(npairs + k) * HA_PCM_REC + (lane & 7)], 3);   // lane-indexed
+            }
             rank++;
+            c.pslot = -1;
+            if (c.pcm) {
+                // the pair's persistent manifold first (it decides the pair's contacts); then the separating-face record
+                PoseF PA, PB;
+                int a_, b_;
+                pair_bodies(c, 5, k, -1, PA, PB, a_, b_);
+                if (pcm_refresh(c, npairs + k, (int)kh, PA, PB, a_, b_)) continue;
+                c.pslot = npairs + k; c.pkind = 5; c.pA = k; c.pB = -1;
+            }
 #ifdef HA_PROFILE
             PROF_COUNT(86, rec != 0xFF);                                    // candidates with a record
 #endif
@@ -1703,6 +1892,7 @@ HD void detect_self(SimCtx& c) {
 #ifdef HA_X_SELF_DRY
             c.dry = false;
 #endif
+            c.pslot = -1;
             if (c.selfc && lane == 0 && c.sepf != rec) c.selfc[k] = (uint8_t)c.sepf;
 #ifdef HA_PROFILE
             wsync();
@@ -1786,6 +1976,8 @@ HD void detect(SimCtx& c) {
             }
         }
         uint64_t mask = __ballot(cand);
+        // the candidates' persistent-manifold point counts, one load for the batch (ha_params_t v13)
+        float ckh = (c.pcm && cand) ? c.pcm[(size_t)p * HA_PCM_REC + 3] : 0.0f;
         // one iteration per piece pair: a compound object (several convex pieces, ha_model_t v8) runs piece
         // pairs j = 0 .. np-1 of a candidate pair and then emits a single <= 4-point manifold for the object pair
         // (the oracle's gather_begin / gather_end). One loop and one call site per narrow phase (a single inlined
@@ -1804,6 +1996,18 @@ HD void detect(SimCtx& c) {
 #ifdef HA_PROFILE
             c.pk = kind;
 #endif
+            if (j == 0 && c.pcm) {
+                // the pair's persistent manifold: refreshed from its record, or the narrow phase writes the record
+                c.pslot = -1;
+                PoseF PA, PB;
+                int a_, b_;
+                pair_bodies(c, kind, A, B, PA, PB, a_, b_);
+                if (pcm_refresh(c, q, (int)bcast(ckh, bit), PA, PB, a_, b_)) {
+                    mask &= mask - 1;
+                    continue;
+                }
+                c.pslot = q; c.pkind = kind; c.pA = A; c.pB = B;
+            }
             int np = pair_pieces(c, kind, A, B);
 #ifdef HA_PROFILE
             unsigned long long _k0 = __builtin_amdgcn_s_memtime();
@@ -1830,6 +2034,7 @@ HD void detect(SimCtx& c) {
                 c.gather = false;
                 gather_emit(c, kind, A, B);
             }
+            c.pslot = -1;
 #ifdef HA_PROFILE
             wsync();
             PROF_COUNT(10 + kind, __builtin_amdgcn_s_memtime() - _k0);     // time / pairs / pairs with contacts
@@ -1839,7 +2044,7 @@ HD void detect(SimCtx& c) {
         }
     }
     wsync();
-    if constexpr (SELF) detect_self(c);
+    if constexpr (SELF) detect_self(c, npairs);
 }
 
 // ----------------------------------------------------------------------------- constraint rows

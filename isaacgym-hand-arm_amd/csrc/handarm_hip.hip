@@ -210,7 +210,7 @@ __device__ __forceinline__ void load_env(SimCtx& c, const ha_state_t& st, int en
         c.o[o].coll = st.collision_enabled ? st.collision_enabled[(size_t)env * NO + o] : 1;
     }
     for (int b = lane; b < MAXB; b += 64) s.u.pd.cforce[b][0] = s.u.pd.cforce[b][1] = s.u.pd.cforce[b][2] = 0.0f;
-    if (lane < 4) s.cst[lane] = 0;
+    if (lane < HA_CSTAT) s.cst[lane] = 0;
     wsync();
 }
 
@@ -291,8 +291,8 @@ __device__ __forceinline__ void store_env(SimCtx& c, const ha_state_t& st, int e
         bs[e] = v;
     }
     for (int e = lane; e < B * 3; e += 64) st.net_contact_force[(size_t)env * B * 3 + e] = s.u.pd.cforce[e / 3][e % 3];
-    if (st.contact_stats && lane < 4) {
-        int32_t* cs = st.contact_stats + (size_t)env * 4 + lane;
+    if (st.contact_stats && lane < HA_CSTAT) {
+        int32_t* cs = st.contact_stats + (size_t)env * HA_CSTAT + lane;
         *cs = lane == 2 ? (s.cst[2] > *cs ? s.cst[2] : *cs) : *cs + s.cst[lane];
     }
     wsync();
@@ -503,6 +503,17 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.selfc = PC::selfc ? reinterpret_cast<uint8_t*>(c.spill + PC::off_selfc) : nullptr;
     c.selfm = PC::selfc ? reinterpret_cast<uint32_t*>(smem + selfm_lds_offset<PC>()) : nullptr;
     c.sepf = 0xFF;
+    // persistent contact manifolds (ha_params_t v13): the env's records, when the caller bound the buffer and the
+    // tolerance is on; slots = detect's pairs (per object: ground, statics, later objects, link hulls; link hulls x
+    // statics) + the self pairs (ha_contact_cache_slots)
+    {
+        int NO = params->n_objects, NS = model->n_static, NLH = model->n_link_hulls;
+        size_t slots = (size_t)NO * (1 + NS + NLH) + (size_t)(NO * (NO - 1) / 2) + (size_t)NLH * NS + model->n_self_pairs;
+        c.pcm = (st.contact_cache && params->pcm_lin_tol > 0.0f) ? st.contact_cache + (size_t)env * slots * HA_PCM_REC
+                                                                   : nullptr;
+    }
+    c.pslot = -1;
+    c.pkind = c.pA = c.pB = 0;
 #ifdef HA_PROFILE
     c.pcls = 0;
 #endif
@@ -791,6 +802,7 @@ struct ha_handle_s {
     ha_params_t h_params;
     int N, NO, D, L, A, B, task, fam;
     int a0;               // actor_object0 (host copy)
+    int pcm_slots;        // persistent-manifold record slots per env (ha_contact_cache_slots)
     ha_state_t st;
     int bound;
     int stat_slots;
@@ -979,6 +991,9 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     h->fam = fam;
     h->h_params = *params;
     h->stat_slots = 1;
+    h->pcm_slots = params->n_objects * (1 + model->n_static + model->n_link_hulls) +
+                   params->n_objects * (params->n_objects - 1) / 2 + model->n_link_hulls * model->n_static +
+                   model->n_self_pairs;
     HIPCHK(hipMalloc(&h->d_model, sizeof(ha_model_t)));
     HIPCHK(hipMalloc(&h->d_params, sizeof(ha_params_t)));
     HIPCHK(hipMemcpy(h->d_model, model, sizeof(ha_model_t), hipMemcpyHostToDevice));
@@ -1096,7 +1111,7 @@ extern "C" __global__ void __launch_bounds__(1024) ha_env_order_kernel(const int
     auto bucket = [&](int e) {
         // the span scaled so that the longest lands in bucket 0 (the spans of a long launch, C5's ~7 ms per env,
         // would saturate a fixed unit), or the contacts offered since the last refresh
-        int cost = t1 ? (int)((long long)cost_prev[e] * 1023 / smax) : stats[4 * (size_t)e + 3] - cost_prev[e];
+        int cost = t1 ? (int)((long long)cost_prev[e] * 1023 / smax) : stats[HA_CSTAT * (size_t)e + 3] - cost_prev[e];
 #ifdef HA_X_ORDER_FIXED_UNIT    /* A/B: the fixed 5.12 us bucket of the first span-based order */
         if (t1) cost = cost_prev[e] >> 9;
 #endif
@@ -1127,12 +1142,14 @@ extern "C" __global__ void __launch_bounds__(1024) ha_env_order_kernel(const int
             if (blk & 1) q = blk * snake + (last - 1 - j);
         }
         order[q] = e;
-        if (!t1) cost_prev[e] = stats[4 * (size_t)e + 3];
+        if (!t1) cost_prev[e] = stats[HA_CSTAT * (size_t)e + 3];
     }
 }
 
 int ha_update_env_order(ha_handle h, int32_t* order, int32_t* cost_prev, int32_t snake, void* stream) {
     if (!h || !h->bound || !order || !cost_prev || !h->st.contact_stats || snake < 0) return HA_E_ARG;
+    // span mode maps launch slot q to env order[q]: only right for the order the step launches used
+    if (h->d_tend && order != h->order) return HA_E_ARG;
     hipLaunchKernelGGL(ha_env_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, h->st.contact_stats,
                        cost_prev, order, h->N, snake, (const unsigned long long*)h->d_tstart,
                        (const unsigned long long*)h->d_tend);
@@ -1158,6 +1175,11 @@ int ha_set_order_cost(ha_handle h, int32_t mode) {
     h->io.tstart = h->d_tstart;
     h->io.tend = h->d_tend;
     return HA_OK;
+}
+
+int ha_contact_cache_slots(ha_handle h) {
+    if (!h) return HA_E_ARG;
+    return h->pcm_slots;
 }
 
 int ha_set_env_order(ha_handle h, const int32_t* order, int32_t n) {

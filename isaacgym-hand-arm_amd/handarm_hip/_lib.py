@@ -40,6 +40,7 @@ SIGNATURES = {
     "ha_task_reset": ([H, C.c_uint32, S], C.c_int),
     "ha_last_kernel_ms": ([H], C.c_float),
     "ha_contact_capacity": ([H], C.c_int),
+    "ha_contact_cache_slots": ([H], C.c_int),
     "ha_set_env_order": ([H, C.c_void_p, C.c_int32], C.c_int),
     "ha_update_env_order": ([H, C.c_void_p, C.c_void_p, C.c_int32, S], C.c_int),
     "ha_set_order_cost": ([H, C.c_int32], C.c_int),

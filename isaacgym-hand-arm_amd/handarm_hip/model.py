@@ -132,6 +132,7 @@ class HaParams(C.Structure):
         ("contact_slop", f32), ("manifold_window", f32),                       # v9
         ("link_lin_damping", f32), ("link_ang_damping", f32), ("edge_rel_tol", f32), ("edge_abs_tol", f32),  # v10
         ("narrow_phase_flags", i32),
+        ("pcm_lin_tol", f32), ("pcm_cos_tol", f32),                           # v13
     ]
 
 
@@ -145,12 +146,34 @@ STATE_FIELDS = ["root_state", "rigid_body_state", "dof_state", "net_contact_forc
                 "ur5_target", "servo", "smoothed", "obs_cache", "reset_draws", "episode", "stats", "term_sums",
                 "flags", "collision_enabled", "dof_force", "reset_goal_buf", "successes", "goal_state",
                 "consecutive_successes", "dr_scale", "object_scale", "object_force", "task_state", "task_scalars",
-                "contact_stats"]
+                "contact_stats", "contact_cache"]
+PCM_REC = 48        # HA_PCM_REC: floats per persistent-manifold record (include/handarm_abi.h v13)
+CSTAT = 8           # HA_CSTAT: contact_stats columns
+
+
+def pcm_slots(model, n_obj):
+    """Persistent-manifold record slots per env (ha_contact_cache_slots): the broad phase's pair enumeration (per object
+    its ground, statics, later objects and link hulls; then link hulls x statics), then the self pairs."""
+    NS, NLH = model.n_static, model.n_link_hulls
+    return sum(1 + NS + (n_obj - 1 - o) + NLH for o in range(n_obj)) + NLH * NS + model.n_self_pairs
+
+
+_DEFAULT_SLOTS = {}
+
+
+def default_pcm_slots(n_obj=3):
+    """pcm_slots of the default Ur5Sih scene (state buffers sized without a model in hand)."""
+    if n_obj not in _DEFAULT_SLOTS:
+        _DEFAULT_SLOTS[n_obj] = pcm_slots(build_model(load_scene()), n_obj)
+    return _DEFAULT_SLOTS[n_obj]
 
 
 def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, num_actions=11, num_obs=147,
-               n_actors=None, n_bodies=None):
-    """name -> (shape, numpy dtype) of every ha_state_t buffer (Isaac Gym tensor layouts)."""
+               n_actors=None, n_bodies=None, n_pcm_slots=None):
+    """name -> (shape, numpy dtype) of every ha_state_t buffer (Isaac Gym tensor layouts). n_pcm_slots: persistent-
+    manifold slots per env (pcm_slots of the model; None: the default Ur5Sih scene's)."""
+    if n_pcm_slots is None:
+        n_pcm_slots = default_pcm_slots(n_obj)
     N, D, P = num_envs, n_dofs, num_initial_poses
     A = n_actors if n_actors is not None else 3 + n_obj
     B = n_bodies if n_bodies is not None else 1 + n_links + 1 + n_obj
@@ -169,7 +192,8 @@ def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, nu
         "dof_force": ((N, D), f), "reset_goal_buf": ((N,), i64), "successes": ((N,), f), "goal_state": ((N, 7), f),
         "consecutive_successes": ((1,), f), "dr_scale": ((N, DR_SIZE), f),
         "object_scale": ((N, n_obj, 3), f), "object_force": ((N, n_obj, 3), f), "task_state": ((N, AK_TS), f),
-        "task_scalars": ((4,), f), "contact_stats": ((N, 4), i32),
+        "task_scalars": ((4,), f), "contact_stats": ((N, CSTAT), i32),
+        "contact_cache": ((N, n_pcm_slots, PCM_REC), f),
     }
 
 
@@ -564,6 +588,9 @@ DEFAULT_TASK = dict(
     link_lin_damping=0.01, link_ang_damping=0.01,       # ur5sih.py:178-179
     edge_rel_tol=0.9, edge_abs_tol=0.0005,              # edge-edge vs face axis (handarm_abi.h v10)
     narrow_phase_flags=0,                               # HA_NP_* (A/B and diagnostics only)
+    # persistent contact manifolds (handarm_abi.h v13): a pair's record is reused while its relative pose stays within
+    # pcm_lin_tol (m) and pcm_cos_tol (cos of half the relative rotation angle) of the pose it was built at
+    pcm_lin_tol=0.0005, pcm_cos_tol=0.99999,
     joint_limit_margin=0.02, n_objects=3, num_initial_poses=1, max_episode_length=200,
     sih_alpha=0.8, reward_reaching=1.0, reward_lifting=5.0, reward_goal=50.0, reward_success=50.0,
     lifting_threshold=0.05, goal_threshold=0.05, goal_pos=(0.28, 0.58, 0.8), goal_noise=(0.15, 0.15, 0.1),
@@ -671,13 +698,16 @@ def build_params(cfg=None, task=None):
     p = HaParams()
     for k in ["dt", "substeps", "control_freq_inv", "solver_iters", "friction", "contact_margin", "baumgarte",
               "contact_slop", "manifold_window", "link_lin_damping", "link_ang_damping", "edge_rel_tol",
-              "edge_abs_tol", "narrow_phase_flags",
+              "edge_abs_tol", "narrow_phase_flags", "pcm_lin_tol", "pcm_cos_tol",
               "max_depen_vel", "object_ang_damping", "joint_limit_margin", "n_objects", "num_initial_poses",
               "max_episode_length", "sih_alpha", "reward_reaching", "reward_lifting", "reward_goal",
               "reward_success", "lifting_threshold", "goal_threshold", "seed"]:
         setattr(p, k, c[k])
     if os.environ.get("HA_NP_FLAGS"):          # A/B timing of the narrow-phase stages (HA_NP_*), diagnostics only
         p.narrow_phase_flags = int(os.environ["HA_NP_FLAGS"])
+    if os.environ.get("HA_PCM"):               # A/B of the persistent manifolds: "off" or "lin,cos" (diagnostics only)
+        v = os.environ["HA_PCM"]
+        p.pcm_lin_tol, p.pcm_cos_tol = (0.0, 1.0) if v == "off" else tuple(float(x) for x in v.split(","))
     p.gravity[:] = c["gravity"]
     p.action_dt = c["dt"]                      # VecTask.dt = sim_params.dt (vec_task.py:267)
     p.sih_beta = 1.0 - c["sih_alpha"]          # (1 - alpha) * s: python double, cast once (ur5sih.py:496)

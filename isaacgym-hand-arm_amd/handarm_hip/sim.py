@@ -48,7 +48,8 @@ class HandArmSim:
         self.stats_ring = stats_ring
         spec = HM.state_spec(num_envs, n_links=self.num_links, n_dofs=self.num_dofs, n_obj=self.n_obj,
                              num_initial_poses=self.params.num_initial_poses, num_actions=self.params.num_actions,
-                             num_obs=self.params.num_obs, n_actors=self.num_actors, n_bodies=self.num_bodies)
+                             num_obs=self.params.num_obs, n_actors=self.num_actors, n_bodies=self.num_bodies,
+                             n_pcm_slots=HM.pcm_slots(self.model, self.n_obj))
         spec["stats"] = ((stats_ring, HM.STAT_SIZE), spec["stats"][1])
         spec["term_sums"] = ((stats_ring, 4), spec["term_sums"][1])
         with torch.cuda.device(self.device):
@@ -71,6 +72,8 @@ class HandArmSim:
         self.h = h
         # contacts per substep the kernel family holds (clutter 84, Ur5Sih 21, AllegroKuka 21, AllegroHand 12)
         self.contact_capacity = int(self.lib.ha_contact_capacity(self.h))
+        # persistent-manifold records per env (the contact_cache rows; zero = empty)
+        assert int(self.lib.ha_contact_cache_slots(self.h)) == self.t["contact_cache"].shape[1]
         self.state = HM.HaState()
         null = HM.null_fields(task)
         for k in HM.STATE_FIELDS:
@@ -258,10 +261,14 @@ class HandArmSim:
             self.t["contact_stats"].zero_()
         sub = int(cs[:, 0].sum())
         import numpy as np
+        ref, nar = int(cs[:, 5].sum()), int(cs[:, 6].sum())
         return {"capacity": self.contact_capacity, "substeps": sub,
                 "at_capacity_frac": float(cs[:, 1].sum() / max(sub, 1)),
                 "offered_mean": float(cs[:, 3].sum() / max(sub, 1)), "offered_max": int(cs[:, 2].max()),
-                "env_max_p50": float(np.percentile(cs[:, 2], 50)), "env_max_p99": float(np.percentile(cs[:, 2], 99))}
+                "env_max_p50": float(np.percentile(cs[:, 2], 50)), "env_max_p99": float(np.percentile(cs[:, 2], 99)),
+                "self_offered_mean": float(cs[:, 4].sum() / max(sub, 1)),
+                "pcm_refreshed_per_substep": ref / max(sub, 1), "narrow_phases_per_substep": nar / max(sub, 1),
+                "pcm_refreshed_frac": ref / max(ref + nar, 1)}
 
     def last_kernel_ms(self):
         return float(self.lib.ha_last_kernel_ms(self.h))

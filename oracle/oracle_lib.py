@@ -30,6 +30,8 @@ def load():
     lib.hao_contacts.restype = C.c_int
     lib.hao_contacts.argtypes = [C.c_void_p, C.POINTER(HM.HaState), C.c_int, C.c_void_p, C.c_int]
     lib.hao_sincos.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    lib.hao_pcm_slots.restype = C.c_int
+    lib.hao_pcm_slots.argtypes = [C.POINTER(HM.HaModel), C.c_int]
     return lib
 
 
@@ -46,11 +48,12 @@ class HostState:
 
     def __init__(self, num_envs, n_obj=3, num_initial_poses=1, model=None, params=None):
         kw = {}
-        if model is not None:       # sizes/layout of the model's task (default: Ur5Sih)
-            kw = dict(n_links=model.n_links, n_dofs=model.n_dofs, n_actors=model.n_actors, n_bodies=model.n_bodies)
         if params is not None:
             kw.update(num_actions=params.num_actions, num_obs=params.num_obs)
             n_obj = params.n_objects
+        if model is not None:       # sizes/layout of the model's task (default: Ur5Sih)
+            kw.update(n_links=model.n_links, n_dofs=model.n_dofs, n_actors=model.n_actors, n_bodies=model.n_bodies,
+                      n_pcm_slots=HM.pcm_slots(model, n_obj))
         self.spec = HM.state_spec(num_envs, n_obj=n_obj, num_initial_poses=num_initial_poses, **kw)
         self.null = HM.null_fields(params.task if params is not None else HM.TASK_UR5SIH)
         self.arrays = {k: np.zeros(shape, dtype) for k, (shape, dtype) in self.spec.items()}

@@ -131,6 +131,7 @@ struct hao_s {
     ha_params_t p;
     int N, A, B, D, NO;
     int maxc;     /* contact capacity of the device kernel family (handarm_hip.hip family_of) */
+    int pcm_slots;/* persistent-manifold record slots per env (hao_pcm_slots) */
 };
 typedef struct hao_s* hao_handle;
 
@@ -152,6 +153,8 @@ typedef struct {
     float cforce[MAXB][3];
     float dforce[HA_MAX_DOFS];      /* joint force of the last substep: (drive + lower - upper impulse) / h */
     const float* dr;                /* this env's DR row (HA_DR_*) or NULL (ha_physics.h SimCtx::dr) */
+    float* pcm;                     /* this env's persistent-manifold records (ha_state_t.contact_cache) or NULL */
+    int cst[HA_CSTAT];              /* contact_stats of this call sequence (ha_physics.h EnvLDS::cst) */
 } env_t;
 
 static float body_friction(const hao_handle h, const env_t* e, int b);
@@ -398,9 +401,47 @@ static __thread float g_edge_rel, g_edge_abs;   /* ha_params_t.edge_rel_tol / ed
 static __thread int g_np_flags;                 /* ha_params_t.narrow_phase_flags */
 static __thread v3 g_pt[MAXGATHER], g_nrm[MAXGATHER];
 static __thread float g_sep[MAXGATHER];
+static __thread int g_code[MAXGATHER];
+/* contact_stats of the running detect(): contacts offered, self-collision contacts offered (both bodies links) */
+static __thread int g_noff, g_nself;
+/* A manifold point's anchor (ha_physics.h PCM_*): the feature the point came from - a vertex (or clipped edge point)
+ * of side A, of side B, or neither (the midpoint of two closest edge points) - and the body whose face carries the
+ * normal (the reference face; B for the ground and edge-edge contacts) */
+#define PCM_FEAT_A 0
+#define PCM_FEAT_B 1
+#define PCM_FEAT_MID 2
+#define PCM_NORMAL_A 4
+/* persistent manifold (ha_params_t v13) of the running pair: its record (NULL: none) and the two body poses */
+static __thread float* g_rec;
+static __thread pose_t g_PA, g_PB;
+
+static qt qconj(qt q) { return Q(-q.x, -q.y, -q.z, q.w); }
+/* the record of a pair's chosen points (ha_physics.h pcm_store): relative pose, then per point its point on A in A's
+ * frame, its point on B in B's frame and its normal in B's frame. x is midway between the two surface points, which
+ * sit half the separation along the normal on either side */
+static void pcm_store(float* rec, const v3* pts, const float* seps, const v3* nrm, v3 n, const int* codes,
+                      const int* idx, int k) {
+    qt qac = qconj(g_PA.q), qbc = qconj(g_PB.q);
+    for (int i = 0; i < k; i++) {
+        v3 x = pts[idx[i]], ni = nrm ? nrm[idx[i]] : n;
+        int code = codes[idx[i]];
+        float hs = 0.5f * seps[idx[i]];
+        v3 la = qrot(qac, sub(add(x, mul(ni, hs)), g_PA.p));
+        v3 lb = qrot(qbc, sub(sub(x, mul(ni, hs)), g_PB.p));
+        v3 ln = qrot((code & PCM_NORMAL_A) ? qac : qbc, ni);
+        float* r = rec + 8 + 9 * i;
+        st3(r, la); st3(r + 3, lb); st3(r + 6, ln);
+        rec[44 + i] = (float)code;
+    }
+    st3(rec, qrot(qbc, sub(g_PA.p, g_PB.p)));
+    rec[3] = (float)k;
+    stq(rec + 4, qmul(qbc, g_PA.q));
+}
 
 static void store_points(contact_t* out, int* nout, int maxout, const v3* pts, const float* seps, const v3* nrm,
                          v3 n, const int* idx, int k, int a, int b) {
+    g_noff += k;
+    if (a >= 100 && b >= 100) g_nself += k;
     for (int i = 0; i < k; i++) {
         v3 ni = nrm ? nrm[idx[i]] : n;
         if (*nout >= maxout) {
@@ -416,15 +457,17 @@ static void store_points(contact_t* out, int* nout, int maxout, const v3* pts, c
         c->x = pts[idx[i]]; c->n = ni; c->sep = seps[idx[i]]; c->a = a; c->b = b;
     }
 }
-static int emit(contact_t* out, int* nout, int maxout, v3* pts, float* seps, int nc, v3 n, int a, int b) {
+static int emit(contact_t* out, int* nout, int maxout, v3* pts, float* seps, const int* codes, int nc, v3 n, int a,
+                int b) {
     int idx[4];
     int k = reduce_manifold(pts, seps, nc, n, NULL, g_window, idx);
     if (g_on) {
         for (int i = 0; i < k && g_n < MAXGATHER; i++, g_n++) {
-            g_pt[g_n] = pts[idx[i]]; g_sep[g_n] = seps[idx[i]]; g_nrm[g_n] = n;
+            g_pt[g_n] = pts[idx[i]]; g_sep[g_n] = seps[idx[i]]; g_nrm[g_n] = n; g_code[g_n] = codes[idx[i]];
         }
         return k;
     }
+    if (g_rec && k > 0) pcm_store(g_rec, pts, seps, NULL, n, codes, idx, k);
     store_points(out, nout, maxout, pts, seps, NULL, n, idx, k, a, b);
     return k;
 }
@@ -433,7 +476,47 @@ static void gather_end(contact_t* out, int* nout, int maxout, int a, int b) {
     int idx[4];
     g_on = 0;
     int k = reduce_manifold(g_pt, g_sep, g_n, V(0, 0, 0), g_nrm, g_window, idx);
+    if (g_rec && k > 0) pcm_store(g_rec, g_pt, g_sep, g_nrm, V(0, 0, 0), g_code, idx, k);
     store_points(out, nout, maxout, g_pt, g_sep, g_nrm, V(0, 0, 0), idx, k, a, b);
+}
+/* A pair's persistent manifold (ha_physics.h pcm_refresh): when its record holds points and the pair's relative pose
+ * (side A's body in side B's frame) is within pcm_lin_tol / pcm_cos_tol of the pose the record was built at, each
+ * point is re-evaluated from the current poses (the two surface points and the normal carried by their bodies; the
+ * separation along the normal; the point midway), those within the contact margin are emitted in record order, and
+ * the pair's narrow phase is skipped (returns 1). Otherwise returns 0 and leaves the record to the narrow phase. */
+static int pcm_refresh(const ha_params_t* p, float* rec, pose_t PA, pose_t PB, int a, int b, contact_t* out, int* nout,
+                       int maxout) {
+    int k = (int)rec[3];
+    if (k <= 0) return 0;
+    qt qbc = qconj(PB.q);
+    v3 d = sub(qrot(qbc, sub(PA.p, PB.p)), ld3(rec));
+    float lt = p->pcm_lin_tol;
+    if (dot(d, d) > lt * lt) return 0;
+    qt qr = qmul(qbc, PA.q);
+    float cq = ((qr.x * rec[4] + qr.y * rec[5]) + qr.z * rec[6]) + qr.w * rec[7];
+    if (fabsf(cq) < p->pcm_cos_tol) return 0;
+    v3 pts[4], nrm[4];
+    float seps[4];
+    int idx[4], kv = 0;
+    for (int t = 0; t < k && t < 4; t++) {
+        const float* r = rec + 8 + 9 * t;
+        int code = (int)rec[44 + t];
+        v3 wa = add(PA.p, qrot(PA.q, ld3(r)));
+        v3 wb = add(PB.p, qrot(PB.q, ld3(r + 3)));
+        v3 n = qrot((code & PCM_NORMAL_A) ? PA.q : PB.q, ld3(r + 6));
+        float sp = dot(n, sub(wa, wb));
+        if (sp > p->contact_margin) continue;
+        int f = code & 3;
+        /* the point where the narrow phase puts it: half the separation off its feature along the normal */
+        pts[kv] = f == PCM_FEAT_A ? sub(wa, mul(n, 0.5f * sp)) : (f == PCM_FEAT_B ? add(wb, mul(n, 0.5f * sp))
+                                                                                   : mul(add(wa, wb), 0.5f));
+        nrm[kv] = n;
+        seps[kv] = sp;
+        idx[kv] = kv;
+        kv++;
+    }
+    store_points(out, nout, maxout, pts, seps, nrm, V(0, 0, 0), idx, kv, a, b);
+    return 1;
 }
 
 /* squared distance from point q to the segment p0 + t (p1 - p0), t in [0, 1] (ha_physics.h seg_point_d2) */
@@ -560,7 +643,8 @@ static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t
             v3 n, pa, pb, e1, e2;
             edge_axis(EA[la[bw / nB]], EB[lb[bw % nB]], wpa, wpb, va, vb, cb, &n, &pa, &e1, &pb, &e2);
             v3 x = edge_closest_mid(pa, e1, pb, e2);
-            emit(out, nout, maxout, &x, &best, 1, n, a, b);
+            int code = PCM_FEAT_MID;
+            emit(out, nout, maxout, &x, &best, &code, 1, n, a, b);
             return;
         }
     }
@@ -569,8 +653,12 @@ static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t
      * planes, (3) the reference face's loop vertices projected onto the incident face */
     v3 pts[MAXCAND];
     float seps[MAXCAND];
+    int codes[MAXCAND];
     for (int pass = 0; pass < 2; pass++) {
         int refB = (sepB >= sepA) ? (pass == 0) : (pass == 1);
+        /* anchors: candidates (1), (2) on the incident hull, (3) on the reference hull; the normal on the reference */
+        int nA = refB ? 0 : PCM_NORMAL_A;
+        int c_inc = (refB ? PCM_FEAT_A : PCM_FEAT_B) | nA, c_ref = (refB ? PCM_FEAT_B : PCM_FEAT_A) | nA;
         int hr = refB ? hb : ha, hi = refB ? ha : hb, kr = refB ? kB : kA;
         const wplane_t* wpr = refB ? wpb : wpa;
         const wplane_t* wpi = refB ? wpa : wpb;
@@ -592,6 +680,7 @@ static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t
             if (mx > margin) continue;
             pts[nc] = sub(vi[i], mul(nref, 0.5f * dist));
             seps[nc] = dist;
+            codes[nc] = c_inc;
             nc++;
         }
         int ki = -1;
@@ -623,10 +712,12 @@ static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t
             float de = dot(nref, xe) + dref, dx = dot(nref, xx) + dref;
             if (!outside && tin > 0.0f && tin <= tout && de <= margin && nv1 + 2 * j < 64) {
                 pts[nc] = sub(xe, mul(nref, 0.5f * de));
+                codes[nc] = c_inc;
                 seps[nc++] = de;
             }
             if (!outside && tout < 1.0f && tin < tout && dx <= margin && nv1 + 2 * j + 1 < 64) {
                 pts[nc] = sub(xx, mul(nref, 0.5f * dx));
+                codes[nc] = c_inc;
                 seps[nc++] = dx;
             }
         }
@@ -646,13 +737,14 @@ static void collide_hulls(const ha_model_t* m, int ha, pose_t PA, int hb, pose_t
                 }
                 if (sr <= margin && mx <= 0.0f && nv1 + 2 * lni + r < 64) {
                     pts[nc] = add(q, mul(nref, 0.5f * sr));
+                    codes[nc] = c_ref;
                     seps[nc++] = sr;
                 }
             }
         }
         if (nc > 0) {
             v3 n = refB ? nref : mul(nref, -1.0f);
-            emit(out, nout, maxout, pts, seps, nc, n, a, b);
+            emit(out, nout, maxout, pts, seps, codes, nc, n, a, b);
             return;
         }
     }
@@ -664,12 +756,13 @@ static void collide_ground(const ha_model_t* m, int ha, pose_t PA, float margin,
     if (c.z - scl_r(sca, m->hull_radius[ha]) > margin) return;
     v3 pts[64];
     float seps[64];
+    int codes[64];
     int nc = 0;
     for (int i = 0; i < m->hull_nverts[ha]; i++) {
         v3 v = hull_vert(m, ha, i, PA, sca);
-        if (v.z <= margin) { pts[nc] = sub(v, V(0, 0, 0.5f * v.z)); seps[nc] = v.z; nc++; }
+        if (v.z <= margin) { pts[nc] = sub(v, V(0, 0, 0.5f * v.z)); seps[nc] = v.z; codes[nc] = PCM_FEAT_A; nc++; }
     }
-    emit(out, nout, maxout, pts, seps, nc, V(0, 0, 1), a, -1);
+    emit(out, nout, maxout, pts, seps, codes, nc, V(0, 0, 1), a, -1);
 }
 
 /* sphere (center c, radius r) vs the table box: exact sphere-box overlap test (broad phase) */
@@ -684,7 +777,14 @@ static int near_box(const float* half, pose_t Pb, v3 c, float r) {
 }
 static pose_t static_pose(const ha_model_t* m, int k) { pose_t P = {ld3(m->static_pos[k]), ldq(m->static_quat[k])}; return P; }
 
-static int detect(const hao_handle h, const env_t* e, contact_t* out) {
+/* The pairs in the kernel's order (ha_physics.h pair_desc: per object its ground, statics, later objects and link hulls,
+ * then link hulls x statics, then the self pairs), each first through the kernel's broad phase (ha_physics.h detect:
+ * bounding spheres, the exact box for statics) - the persistent manifold (v13) is consulted for exactly the pairs that
+ * pass it - then its record or its narrow phase. pidx is the pair's record slot. */
+static const pose_t g_identity = {{0, 0, 0}, {0, 0, 0, 1}};
+static void pcm_begin(float* rec, pose_t PA, pose_t PB) { g_rec = rec; g_PA = PA; g_PB = PB; }
+
+static int detect(const hao_handle h, env_t* e, contact_t* out) {
     const ha_model_t* m = &h->m;
     const ha_params_t* p = &h->p;
     int nout = 0;
@@ -693,61 +793,103 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
     g_edge_rel = p->edge_rel_tol;
     g_edge_abs = p->edge_abs_tol;
     g_np_flags = p->narrow_phase_flags;
-    for (int o = 0; o < h->NO; o++) {
-        if (!e->coll[o]) continue;
+    g_noff = g_nself = 0;
+    g_rec = NULL;
+    int NO = h->NO, NS = m->n_static, NLH = m->n_link_hulls;
+    float* pcm = (e->pcm && p->pcm_lin_tol > 0.0f) ? e->pcm : NULL;
+    int pidx = 0, nref = 0, nnar = 0;
+#define PCM_REC(k) (pcm ? pcm + (size_t)(k) * HA_PCM_REC : NULL)
+#define PCM_TRY(k, PA, PB, a, b) (pcm && pcm_refresh(p, PCM_REC(k), PA, PB, a, b, out, &nout, h->maxc) ? (nref++, 1) : 0)
+    for (int o = 0; o < NO; o++) {
         int pa = e->pool[o];
         int ho = m->pool_hull[pa], no = m->pool_nhull[pa];     /* the object's convex pieces (ABI v8) */
         const float* so = env_scale(e, o);
         pose_t Po = {sub(e->oc[o], qrot(e->oq[o], scl(so, ld3(m->pool_com[pa])))), e->oq[o]};
+        /* the object's bounding sphere over all its pieces (the kernel's broad phase) */
+        v3 co = add(Po.p, qrot(Po.q, scl(so, ld3(m->pool_center[pa]))));
+        float ro = scl_r(so, m->pool_radius[pa]);
         /* a compound object (no > 1 pieces) emits one manifold per object pair (gather_begin / gather_end) */
-        if (no > 1) gather_begin();
-        for (int j = 0; j < no; j++) collide_ground(m, ho + j, Po, mg, o, so, out, &nout, h->maxc);
-        if (no > 1) gather_end(out, &nout, h->maxc, o, -1);
-        for (int st = 0; st < m->n_static; st++) {
-            pose_t Pst = static_pose(m, st);
-            if (near_box(m->static_half[st], Pst, add(Po.p, qrot(Po.q, scl(so, ld3(m->pool_center[pa])))),
-                         scl_r(so, m->pool_radius[pa]) + mg)) {
-                if (no > 1) gather_begin();
-                for (int j = 0; j < no; j++)     /* each piece's own sphere against the exact box too */
-                    if (near_box(m->static_half[st], Pst, add(Po.p, qrot(Po.q, scl(so, ld3(m->hull_center[ho + j])))),
-                                 scl_r(so, m->hull_radius[ho + j]) + mg))
-                        collide_hulls(m, ho + j, Po, m->static_hull[st], Pst, mg, o, -1, so, NULL, out, &nout, h->maxc);
-                if (no > 1) gather_end(out, &nout, h->maxc, o, -1);
-            }
+        if (e->coll[o] && co.z - ro <= mg && !PCM_TRY(pidx, Po, g_identity, o, -1)) {
+            pcm_begin(PCM_REC(pidx), Po, g_identity);
+            nnar += no;
+            if (no > 1) gather_begin();
+            for (int j = 0; j < no; j++) collide_ground(m, ho + j, Po, mg, o, so, out, &nout, h->maxc);
+            if (no > 1) gather_end(out, &nout, h->maxc, o, -1);
+            g_rec = NULL;
         }
-        for (int o2 = o + 1; o2 < h->NO; o2++) {
-            if (!e->coll[o2]) continue;
+        pidx++;
+        for (int st = 0; st < NS; st++, pidx++) {
+            pose_t Pst = static_pose(m, st);
+            int hs = m->static_hull[st];
+            v3 dc = sub(co, add(Pst.p, qrot(Pst.q, ld3(m->hull_center[hs]))));
+            float rr = ro + m->hull_radius[hs] + mg;
+            if (!e->coll[o] || !(dot(dc, dc) <= rr * rr) || !near_box(m->static_half[st], Pst, co, ro + mg)) continue;
+            if (PCM_TRY(pidx, Po, Pst, o, -1)) continue;
+            pcm_begin(PCM_REC(pidx), Po, Pst);
+            if (no > 1) gather_begin();
+            for (int j = 0; j < no; j++)     /* each piece's own sphere against the exact box too */
+                if (near_box(m->static_half[st], Pst, add(Po.p, qrot(Po.q, scl(so, ld3(m->hull_center[ho + j])))),
+                             scl_r(so, m->hull_radius[ho + j]) + mg)) {
+                    nnar++;
+                    collide_hulls(m, ho + j, Po, hs, Pst, mg, o, -1, so, NULL, out, &nout, h->maxc);
+                }
+            if (no > 1) gather_end(out, &nout, h->maxc, o, -1);
+            g_rec = NULL;
+        }
+        for (int o2 = o + 1; o2 < NO; o2++, pidx++) {
             int pb = e->pool[o2];
             int h2 = m->pool_hull[pb], n2 = m->pool_nhull[pb];
             const float* s2 = env_scale(e, o2);
             pose_t P2 = {sub(e->oc[o2], qrot(e->oq[o2], scl(s2, ld3(m->pool_com[pb])))), e->oq[o2]};
+            v3 dc = sub(co, add(P2.p, qrot(P2.q, scl(s2, ld3(m->pool_center[pb])))));
+            float rr = ro + scl_r(s2, m->pool_radius[pb]) + mg;
+            if (!e->coll[o] || !e->coll[o2] || !(dot(dc, dc) <= rr * rr)) continue;
+            if (PCM_TRY(pidx, Po, P2, o, o2)) continue;
+            pcm_begin(PCM_REC(pidx), Po, P2);
+            nnar += no * n2;
             if (no * n2 > 1) gather_begin();
             for (int j = 0; j < no; j++)
                 for (int j2 = 0; j2 < n2; j2++)
                     collide_hulls(m, ho + j, Po, h2 + j2, P2, mg, o, o2, so, s2, out, &nout, h->maxc);
             if (no * n2 > 1) gather_end(out, &nout, h->maxc, o, o2);
+            g_rec = NULL;
         }
-        for (int k = 0; k < m->n_link_hulls; k++) {
+        for (int k = 0; k < NLH; k++, pidx++) {
             int L = m->hull_link[k];
             pose_t PL = {e->lp[L], e->lq[L]};
+            v3 dc = sub(co, add(PL.p, qrot(PL.q, ld3(m->hull_center[k]))));
+            float rr = ro + m->hull_radius[k] + mg;
+            if (!e->coll[o] || !(dot(dc, dc) <= rr * rr)) continue;
+            if (PCM_TRY(pidx, PL, Po, 100 + L, o)) continue;
+            pcm_begin(PCM_REC(pidx), PL, Po);
+            nnar += no;
             if (no > 1) gather_begin();
             for (int j = 0; j < no; j++) collide_hulls(m, k, PL, ho + j, Po, mg, 100 + L, o, NULL, so, out, &nout, h->maxc);
             if (no > 1) gather_end(out, &nout, h->maxc, 100 + L, o);
+            g_rec = NULL;
         }
     }
-    for (int k = 0; k < m->n_link_hulls; k++) {
+    for (int k = 0; k < NLH; k++) {
         int L = m->hull_link[k];
-        if (!m->link_table_collide[L]) continue;
         pose_t PL = {e->lp[L], e->lq[L]};
-        for (int st = 0; st < m->n_static; st++) {
+        v3 ch = add(PL.p, qrot(PL.q, ld3(m->hull_center[k])));
+        for (int st = 0; st < NS; st++, pidx++) {
+            if (!m->link_table_collide[L]) continue;
             pose_t Pst = static_pose(m, st);
-            if (near_box(m->static_half[st], Pst, add(PL.p, qrot(PL.q, ld3(m->hull_center[k]))), m->hull_radius[k] + mg))
-                collide_hulls(m, k, PL, m->static_hull[st], Pst, mg, 100 + L, -1, NULL, NULL, out, &nout, h->maxc);
+            int hs = m->static_hull[st];
+            v3 dc = sub(ch, add(Pst.p, qrot(Pst.q, ld3(m->hull_center[hs]))));
+            float rr = m->hull_radius[k] + m->hull_radius[hs] + mg;
+            if (!(dot(dc, dc) <= rr * rr) || !near_box(m->static_half[st], Pst, ch, m->hull_radius[k] + mg)) continue;
+            if (PCM_TRY(pidx, PL, Pst, 100 + L, -1)) continue;
+            pcm_begin(PCM_REC(pidx), PL, Pst);
+            nnar++;
+            collide_hulls(m, k, PL, hs, Pst, mg, 100 + L, -1, NULL, NULL, out, &nout, h->maxc);
+            g_rec = NULL;
         }
     }
     /* self-collision (v12): link hull pairs of non-adjacent links whose oriented boxes come within the margin
        (include/ha_obb.h, the kernel's mid-phase) */
-    for (int k = 0; k < m->n_self_pairs; k++) {
+    for (int k = 0; k < m->n_self_pairs; k++, pidx++) {
         int ha = m->self_pair[k] & 255, hb = m->self_pair[k] >> 8;
         int la = m->hull_link[ha], lb = m->hull_link[hb];
         float pa[3] = {e->lp[la].x, e->lp[la].y, e->lp[la].z}, qa[4] = {e->lq[la].x, e->lq[la].y, e->lq[la].z, e->lq[la].w};
@@ -757,10 +899,31 @@ static int detect(const hao_handle h, const env_t* e, contact_t* out) {
         ha_obb_world(pb, qb, m->hull_obb[hb], cb, Rb);
         if (!ha_obb_near(ca, Ra, m->hull_obb[ha] + 3, cb, Rb, m->hull_obb[hb] + 3, mg)) continue;
         /* hull b on side A, hull a on side B (ha_physics.h narrow_phase kind 5): normal from a to b */
-        pose_t PA = {e->lp[la], e->lq[la]}, PB = {e->lp[lb], e->lq[lb]};
-        collide_hulls(m, hb, PB, ha, PA, mg, 100 + lb, 100 + la, NULL, NULL, out, &nout, h->maxc);
+        pose_t PA = {e->lp[lb], e->lq[lb]}, PB = {e->lp[la], e->lq[la]};
+        if (PCM_TRY(pidx, PA, PB, 100 + lb, 100 + la)) continue;
+        pcm_begin(PCM_REC(pidx), PA, PB);
+        nnar++;
+        collide_hulls(m, hb, PA, ha, PB, mg, 100 + lb, 100 + la, NULL, NULL, out, &nout, h->maxc);
+        g_rec = NULL;
     }
+#undef PCM_TRY
+#undef PCM_REC
+    /* contact_stats (ha_physics.h substep, EnvLDS::cst) */
+    e->cst[0] += 1;
+    e->cst[1] += g_noff > h->maxc ? 1 : 0;
+    e->cst[2] = g_noff > e->cst[2] ? g_noff : e->cst[2];
+    e->cst[3] += g_noff;
+    e->cst[4] += g_nself;
+    e->cst[5] += nref;
+    e->cst[6] += nnar;
     return nout;
+}
+
+/* record slots of an env (ha_contact_cache_slots): the kernel's pair enumeration, then the self pairs */
+int hao_pcm_slots(const ha_model_t* m, int n_objects) {
+    int NO = n_objects, NS = m->n_static, NLH = m->n_link_hulls, n = 0;
+    for (int o = 0; o < NO; o++) n += 1 + NS + (NO - 1 - o) + NLH;
+    return n + NLH * NS + m->n_self_pairs;
 }
 
 /* Jacobian row: relative velocity of body a minus body b at point x along dir, into J (len D+6*NO) */
@@ -1066,6 +1229,8 @@ static void load_env(const hao_handle h, const ha_state_t* S, int env, env_t* e,
     }
     memset(e->cforce, 0, sizeof(e->cforce));
     memset(e->dforce, 0, sizeof(e->dforce));
+    memset(e->cst, 0, sizeof(e->cst));
+    e->pcm = S->contact_cache ? S->contact_cache + (size_t)env * h->pcm_slots * HA_PCM_REC : NULL;
 }
 
 static void store_env(const hao_handle h, ha_state_t* S, int env, env_t* e) {
@@ -1110,9 +1275,14 @@ static void store_env(const hao_handle h, ha_state_t* S, int env, env_t* e) {
         memcpy(bs + (m->body_object0 + o) * 13, rs + (m->actor_object0 + o) * 13, 13 * sizeof(float));
     for (int b = 0; b < B; b++)
         for (int k = 0; k < 3; k++) S->net_contact_force[((size_t)env * B + b) * 3 + k] = e->cforce[b][k];
+    if (S->contact_stats) {     /* added up over launches like the kernel's (column 2: the maximum) */
+        int32_t* cs = S->contact_stats + (size_t)env * HA_CSTAT;
+        for (int k = 0; k < HA_CSTAT; k++) cs[k] = k == 2 ? (e->cst[2] > cs[2] ? e->cst[2] : cs[2]) : cs[k] + e->cst[k];
+    }
 }
 
 /* ------------------------------------------------------------------ public oracle API */
+int hao_pcm_slots(const ha_model_t* m, int n_objects);
 hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int num_envs) {
     hao_handle h = (hao_handle)calloc(1, sizeof(struct hao_s));
     h->m = *model;
@@ -1126,6 +1296,7 @@ hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int nu
        Ur5Sih 4 chunks of 21 (HA_CHUNKS), AllegroKuka 2 chunks of 21 (HA_AK_CONTACTS x HA_AK_CHUNKS), AllegroHand
        4 chunks of 12 (HA_AH_CONTACTS x HA_AH_CHUNKS); hao_set_capacity overrides it for A/B builds */
     h->maxc = params->task == HA_TASK_UR5SIH ? 4 * 21 : (params->task == HA_TASK_ALLEGRO_KUKA ? 2 * 21 : 4 * 12);
+    h->pcm_slots = hao_pcm_slots(model, params->n_objects);
     return h;
 }
 void hao_destroy(hao_handle h) { free(h); }
@@ -1157,6 +1328,7 @@ int hao_contacts(hao_handle h, ha_state_t* S, int env, float* out, int max_rows)
     env_t e;
     load_env(h, S, env, &e, 0);
     e.dr = (h->p.dr_enable && S->dr_scale) ? S->dr_scale + (size_t)env * HA_DR_SIZE : NULL;
+    e.pcm = NULL;                       /* the narrow phase's contacts, no persistent manifold */
     fk(h, &e);
     contact_t cs[MAXC];
     int nc = detect(h, &e, cs);

@@ -148,7 +148,8 @@ def fill_bin_scene(st, num_envs, scene, seed=0, n_obj=8, spread=1.0, pool=16):
     return st
 
 
-PHYSICS_OUTPUTS = ("dof_state", "root_state", "rigid_body_state", "net_contact_force", "dof_force")
+# the persistent contact manifolds (v13) are physics state too: the next call's contacts depend on them
+PHYSICS_OUTPUTS = ("dof_state", "root_state", "rigid_body_state", "net_contact_force", "dof_force", "contact_cache")
 
 
 def assert_physics_bit_identical(sim, st, n, fields=PHYSICS_OUTPUTS, tag=""):

@@ -57,6 +57,27 @@ def exact(sim, hs, names, tag):
         assert not bad.any(), f"{tag} {k}: {int(bad.sum())} elements differ (envs {np.unique(np.nonzero(bad)[0])[:10]})"
 
 
+def stats_match(sim, hs, tag, cap0=None, over_frac=0.25, self_frac=None, refreshed=False):
+    """The timed kernel's contact_stats equal the oracle chain's (substeps, substeps over capacity, max offered, sum
+    offered, self-collision contacts offered, manifolds refreshed from their persistent record); column 6 (narrow
+    phases run) is the kernel's own diagnostics. cap0: at least over_frac of the envs offered more contacts in a
+    substep than chunk 0 holds (the overflow chunks in the env's global area ran); self_frac: at least that fraction of
+    the envs offered self-collision contacts; refreshed: some persistent manifold was reused."""
+    g = get(sim, "contact_stats").reshape(hs["contact_stats"].shape)
+    o = hs["contact_stats"]
+    bad = g[:, :6] != o[:, :6]
+    assert not bad.any(), f"{tag} contact_stats: {int(bad.any(1).sum())} envs differ (columns {np.nonzero(bad.any(0))[0]})"
+    if cap0 is not None:
+        fr = float((g[:, 2] > cap0).mean())
+        assert fr >= over_frac, f"{tag}: only {fr:.2f} of the envs offered more than chunk 0's {cap0} contacts"
+    if self_frac is not None:
+        fs = float((g[:, 4] > 0).mean())
+        assert fs >= self_frac, f"{tag}: only {fs:.2f} of the envs offered self-collision contacts"
+    if refreshed:
+        assert g[:, 5].sum() > 0, f"{tag}: no persistent manifold was reused"
+    return g
+
+
 def near(a, b, atol, tag):
     d = np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64))
     assert np.isfinite(a).all(), f"{tag}: non-finite"
@@ -65,34 +86,32 @@ def near(a, b, atol, tag):
 
 
 # ----------------------------------------------------------------------------- AllegroKuka (C2)
-@pytest.mark.parametrize("sub", ["regrasping", "reorientation"])
-def test_kuka_fused_step_with_physics_matches_oracle_chain(sub):
-    """ak_step_kernel (the C2 headline kernel): goal and env resets in the first step, random forces firing in
-    every step, 3 fused steps against kuka_oracle.pre -> physics_oracle -> kuka_oracle.post."""
-    need_gpu()
+def _kuka_window(sub, n, scene_fn, act_fn, resets=True, force_prob=0.5, seed=11):
+    """K fused ak_step_kernel launches against kuka_oracle.pre -> physics_oracle -> kuka_oracle.post from the same
+    host state (scene_fn(sim, hs) fills it); returns the sim, the host state and the number of random forces fired."""
     from handarm_hip.sim import HandArmSim
     from oracle.oracle_lib import HostState, Oracle
-    n = 128
     sim = HandArmSim(n, "cuda:0", task_cfg={"task": HM.TASK_ALLEGRO_KUKA, "subtask": sub}, task=HM.TASK_ALLEGRO_KUKA)
     p, m = sim.params, sim.model
     lo = np.array(m.dof_lower[:23], np.float32)
     up = np.array(m.dof_upper[:23], np.float32)
     hs = HostState(n, model=m, params=p)
     pull_all(sim, hs)                                       # task_state keypoints, force probabilities, scalars
-    scenes.fill_kuka_scene(hs, n, lo, up, list(p.reset_pose), hs["object_scale"].copy(), list(m.table_pos), seed=4)
+    scene_fn(sim, hs, lo, up)
     hs["object_force"][:] = 0
-    rng = np.random.default_rng(11)
+    rng = np.random.default_rng(seed)
     hs["dof_position_targets"][:] = hs["sim_targets"]
-    hs["reset_buf"][:] = (np.arange(n) % 4 == 0)
-    hs["reset_goal_buf"][:] = (np.arange(n) % 4 == 1)
+    hs["reset_buf"][:] = (np.arange(n) % 4 == 0) if resets else 0
+    hs["reset_goal_buf"][:] = (np.arange(n) % 4 == 1) if resets else 0
     hs["progress_buf"][:] = rng.integers(1, 50, n)
-    hs["task_state"][:, HM.AK_FORCE_PROB] = 0.5
+    hs["task_state"][:, HM.AK_FORCE_PROB] = force_prob
+    hs["contact_stats"][:] = 0
     scalars = hs["task_scalars"].copy()
     push_all(sim, hs)
     orc = Oracle(m, p, n)
     fired = 0
     for t in range(K):
-        act = rng.uniform(-1, 1, (n, 23)).astype(np.float32)
+        act = act_fn(rng, n)
         draws = rng.uniform(0, 1, (n, HM.DRAW_STRIDE)).astype(np.float32)
         # the U[-1, 1) slots (ak_task.h AK_DRAW_*): regrasping's object position noise after each goal target, the
         # reset_idx object position noise and the DOF velocity draws (reorientation draws a goal quaternion there)
@@ -117,33 +136,89 @@ def test_kuka_fused_step_with_physics_matches_oracle_chain(sub):
         cols = [k for k in range(HM.AK_KP) if k != HM.AK_RNG]     # the RNG counter word is device-mode only
         near(get(sim, "task_state")[:, cols], hs["task_state"][:, cols], 1e-4, tag + " task_state")
         print(f"{tag}: obs max |d| {eo:.2e}, rew max |d| {er:.2e}, resets {int(hs['reset_buf'].sum())}")
-    assert fired > n // 4, "the random-force branch must fire"
+    return sim, hs, fired
+
+
+def _kuka_random_scene(sim, hs, lo, up):
+    scenes.fill_kuka_scene(hs, sim.num_envs, lo, up, list(sim.params.reset_pose), hs["object_scale"].copy(),
+                           list(sim.model.table_pos), seed=4)
+
+
+def _uniform_actions(rng, n):
+    return rng.uniform(-1, 1, (n, 23)).astype(np.float32)
+
+
+@pytest.mark.parametrize("sub", ["regrasping", "reorientation"])
+def test_kuka_fused_step_with_physics_matches_oracle_chain(sub):
+    """ak_step_kernel (the C2 headline kernel): goal and env resets in the first step, random forces firing in
+    every step, 3 fused steps against kuka_oracle.pre -> physics_oracle -> kuka_oracle.post."""
+    need_gpu()
+    sim, hs, fired = _kuka_window(sub, 128, _kuka_random_scene, _uniform_actions)
+    assert fired > 128 // 4, "the random-force branch must fire"
+    stats_match(sim, hs, f"kuka {sub}", self_frac=0.25)
+
+
+def kuka_closed_hand_scene(sim, hs, lo, up, seed=0):
+    """The fingers half closed (40-80% of their range) with their targets at the upper limits and the cuboid in the
+    palm (palm_offset from iiwa7_link_7, allegro_kuka_base.py:1430-1436), still: the grasp the C2 bench reaches late in
+    its episodes (offered up to 45 contacts per substep): cube-finger, cube-palm and finger-finger contacts at once"""
+    from oracle.oracle_lib import Oracle
+    from oracle import f32
+    n, p, m = sim.num_envs, sim.params, sim.model
+    _kuka_random_scene(sim, hs, lo, up)
+    rng = np.random.default_rng(seed)
+    ds = hs["dof_state"].reshape(n, 23, 2)
+    ds[:, 7:, 0] = lo[7:] + (up[7:] - lo[7:]) * rng.uniform(0.4, 0.8, (n, 16)).astype(np.float32)
+    ds[:, :, 1] = 0
+    hs["sim_targets"][:] = ds[..., 0]
+    hs["sim_targets"][:, 7:] = up[7:]
+    probe = hs.copy()
+    Oracle(m, p, n).simulate(probe, 1)
+    palm = probe["rigid_body_state"].reshape(n, m.n_bodies, 13)[:, m.body_robot0 + p.ak_palm_link]
+    off = np.broadcast_to(np.array(p.ak_palm_offset, np.float32), (n, 3))
+    rs = hs["root_state"].reshape(n, m.n_actors, 13)
+    rs[:, m.actor_object0, 0:3] = palm[:, 0:3] + f32.qrot(palm[:, 3:7], off) + rng.uniform(-0.01, 0.01, (n, 3))
+    rs[:, m.actor_object0, 7:13] = 0
+
+
+def test_kuka_fused_step_closed_hand_overflows_chunk0_and_matches_oracle_chain():
+    """ak_step_kernel with most envs over chunk 0's 21 contacts (the second chunk in the env's global area: rows,
+    row constants and contact entries; the robot blocks of link contacts past the 3 LDS slots in the spill rows) and
+    every env offering self-collision contacts: finger targets toward the upper limits (hand actions U[0.6, 1], arm
+    still), no resets, against the oracle chain."""
+    need_gpu()
+
+    def act(rng, n):
+        a = np.zeros((n, 23), np.float32)
+        a[:, 7:] = rng.uniform(0.6, 1.0, (n, 16))
+        return a
+    sim, hs, _ = _kuka_window("regrasping", 128, kuka_closed_hand_scene, act, resets=False, force_prob=0.0)
+    g = stats_match(sim, hs, "kuka closed hand", cap0=21, self_frac=0.9, refreshed=True)
+    print(f"kuka closed hand: envs over 21 contacts {(g[:, 2] > 21).mean():.2f}, max offered {g[:, 2].max()}, "
+          f"self contacts per substep {g[:, 4].sum() / g[:, 0].sum():.1f}, refreshed {g[:, 5].sum()}")
 
 
 # ----------------------------------------------------------------------------- AllegroHand (C3)
-def test_allegro_fused_step_with_physics_matches_oracle_chain():
-    """ah_step_kernel (C3): goal and env resets in the first step, 3 fused steps (2 gym.simulate each) against
-    the oracle chain, including the joint forces the full_state observation reads."""
-    need_gpu()
+def _allegro_window(n, seed, act_fn, resets=True):
     from handarm_hip.sim import HandArmSim
     from oracle.oracle_lib import HostState, Oracle
-    n = 128
     sim = HandArmSim(n, "cuda:0", task_cfg={"task": HM.TASK_ALLEGRO_HAND}, task=HM.TASK_ALLEGRO_HAND)
     p, m = sim.params, sim.model
     lo = np.array(m.dof_lower[:16], np.float32)
     up = np.array(m.dof_upper[:16], np.float32)
     hs = HostState(n, model=m, params=p)
     pull_all(sim, hs)
-    scenes.fill_allegro_scene(hs, n, lo, up, seed=6)
+    scenes.fill_allegro_scene(hs, n, lo, up, seed=seed)
     rng = np.random.default_rng(12)
     hs["dof_position_targets"][:] = hs["sim_targets"]
-    hs["reset_buf"][:] = (np.arange(n) % 4 == 0)
-    hs["reset_goal_buf"][:] = (np.arange(n) % 4 == 1)
+    hs["reset_buf"][:] = (np.arange(n) % 4 == 0) if resets else 0
+    hs["reset_goal_buf"][:] = (np.arange(n) % 4 == 1) if resets else 0
     hs["progress_buf"][:] = rng.integers(1, 50, n)
+    hs["contact_stats"][:] = 0
     push_all(sim, hs)
     orc = Oracle(m, p, n)
     for t in range(K):
-        act = rng.uniform(-1, 1, (n, 16)).astype(np.float32)
+        act = act_fn(rng, n)
         draws = rng.uniform(-1, 1, (n, HM.DRAW_STRIDE)).astype(np.float32)
         hs["actions"][:] = act
         put(sim, "actions", act)
@@ -159,6 +234,26 @@ def test_allegro_fused_step_with_physics_matches_oracle_chain():
         er = near(get(sim, "rew"), rew, 1e-4, tag + " rew")
         np.testing.assert_allclose(get(sim, "consecutive_successes")[0], cons, rtol=1e-5, atol=1e-6)
         print(f"{tag}: obs max |d| {eo:.2e}, rew max |d| {er:.2e}")
+    return sim, hs
+
+
+def test_allegro_fused_step_with_physics_matches_oracle_chain():
+    """ah_step_kernel (C3): goal and env resets in the first step, 3 fused steps (2 gym.simulate each) against
+    the oracle chain, including the joint forces the full_state observation reads."""
+    need_gpu()
+    sim, hs = _allegro_window(128, 6, lambda rng, n: rng.uniform(-1, 1, (n, 16)).astype(np.float32))
+    stats_match(sim, hs, "allegro", self_frac=0.25)
+
+
+def test_allegro_fused_step_closing_hand_overflows_chunk0_and_matches_oracle_chain():
+    """ah_step_kernel with the fingers closing on the cube (actions U[0.5, 1]: targets toward the upper limits, no
+    resets): envs over chunk 0's 12 contacts (chunks 1-3 in the env's global area) and self-collision contacts in
+    most envs, against the oracle chain."""
+    need_gpu()
+    sim, hs = _allegro_window(128, 0, lambda rng, n: rng.uniform(0.5, 1.0, (n, 16)).astype(np.float32), resets=False)
+    g = stats_match(sim, hs, "allegro closing hand", cap0=12, self_frac=0.5, refreshed=True)
+    print(f"allegro closing hand: envs over 12 contacts {(g[:, 2] > 12).mean():.2f}, max offered {g[:, 2].max()}, "
+          f"self contacts per substep {g[:, 4].sum() / g[:, 0].sum():.1f}, refreshed {g[:, 5].sum()}")
 
 
 # ----------------------------------------------------------------------------- Ur5Sih: C4 (DR) and C5 (clutter)
@@ -184,6 +279,7 @@ def _ur5sih_case(sim, n, seed, scene_fill):
     hs["reset_buf"][:] = (np.arange(n) % 4 == 0)
     hs["progress_buf"][:] = rng.integers(1, 150, n)
     hs["episode"][:] = rng.integers(0, 1000, n)
+    hs["contact_stats"][:] = 0
     return hs, rng
 
 
@@ -234,6 +330,38 @@ def test_ur5sih_dr_fused_step_with_physics_matches_oracle_chain():
         hs["dr_scale"][:] = _dr_rows(n, np.random.default_rng(2))
     hs, rng = _ur5sih_case(sim, n, 21, fill)
     _ur5sih_window(sim, hs, rng, n, "ur5sih DR")
+    stats_match(sim, hs, "ur5sih DR", refreshed=True)
+
+
+def test_ur5sih_pile_in_hand_fused_step_overflows_chunk0_and_matches_oracle_chain():
+    """ha_step_kernel (C4 kernel, DR on) with the three objects dropped together into the hand: more than chunk 0's 21
+    contacts in most envs (chunks 1-3 in the env's global area), resets in the window, against the oracle chain."""
+    need_gpu()
+    from handarm_hip.sim import HandArmSim
+    from oracle.oracle_lib import Oracle
+    from tests.test_gpu_dr import _dr_rows
+    n = 64
+    sim = HandArmSim(n, "cuda:0", task_cfg={"dr_enable": 1})
+    m = sim.model
+
+    def fill(hs):
+        scenes.fill_scene(hs, n, seed=13, near_hand=0.0)
+        hs["dr_scale"][:] = _dr_rows(n, np.random.default_rng(3))
+        probe = hs.copy()
+        Oracle(m, sim.params, n).simulate(probe, 1)
+        body = probe["rigid_body_state"].reshape(n, m.n_bodies, 13)
+        rng = np.random.default_rng(13)
+        hull_links = sorted({int(m.hull_link[k]) for k in range(m.n_link_hulls)})
+        rs = hs["root_state"].reshape(n, m.n_actors, 13)
+        for o in range(3):
+            lk = np.array(hull_links)[rng.integers(len(hull_links) // 2, len(hull_links), n)]
+            rs[:, m.actor_object0 + o, 0:3] = body[np.arange(n), m.body_robot0 + lk, 0:3] + rng.uniform(-0.015, 0.015, (n, 3))
+            rs[:, m.actor_object0 + o, 7:13] = 0.0
+    hs, rng = _ur5sih_case(sim, n, 23, fill)
+    _ur5sih_window(sim, hs, rng, n, "ur5sih pile")
+    g = stats_match(sim, hs, "ur5sih pile", cap0=21, refreshed=True)
+    print(f"ur5sih pile: envs over 21 contacts {(g[:, 2] > 21).mean():.2f}, max offered {g[:, 2].max()}, "
+          f"refreshed {g[:, 5].sum()}")
 
 
 def test_bin_fused_step_with_physics_matches_oracle_chain():
@@ -247,3 +375,5 @@ def test_bin_fused_step_with_physics_matches_oracle_chain():
         scenes.fill_bin_scene(hs, n, sim.scene, seed=8)
     hs, rng = _ur5sih_case(sim, n, 22, fill)
     _ur5sih_window(sim, hs, rng, n, "bin")
+    g = stats_match(sim, hs, "bin", cap0=21, refreshed=True)
+    print(f"bin: envs over 21 contacts {(g[:, 2] > 21).mean():.2f}, max offered {g[:, 2].max()}, refreshed {g[:, 5].sum()}")

@@ -96,3 +96,35 @@ def test_allegro_cube_in_the_closing_hand_overflows_chunk0_and_matches_oracle(se
           f"over capacity {cs[:, 1].sum()} of {cs[:, 0].sum()} substeps")
     assert over12 >= 0.1, "the scene must overflow chunk 0 (12 contacts) in some envs"
     scenes.assert_physics_bit_identical(sim, st, n, tag=f"allegro overflow seed {seed} calls {calls}")
+
+
+@pytest.mark.parametrize("calls", [1, 4])
+def test_kuka_closed_hand_overflows_chunk0_and_matches_oracle(calls):
+    """AllegroKuka (ak_simulate_kernel): chunk 0 holds 21 contacts in LDS, chunk 1 (21 more) sits in the env's global
+    area. The half-closed hand closing further on the cuboid in its palm offers more than 21 contacts per substep in
+    most envs (cube-finger, cube-palm and the hand's self-collision contacts); every physics output and the persistent
+    manifolds stay bit-identical to the oracle at the same capacity, and the contact statistics match."""
+    need_gpu()
+    from handarm_hip.sim import HandArmSim
+    from oracle.oracle_lib import HostState, Oracle
+    from tests.test_gpu_fused_steps import kuka_closed_hand_scene
+    n = 128
+    sim = HandArmSim(n, "cuda:0", task=HM.TASK_ALLEGRO_KUKA)
+    assert sim.contact_capacity == 42
+    lo = np.array(sim.model.dof_lower[:23], np.float32)
+    up = np.array(sim.model.dof_upper[:23], np.float32)
+    st = HostState(n, model=sim.model, params=sim.params)
+    st["object_scale"][:] = sim.t["object_scale"].cpu().numpy()
+    kuka_closed_hand_scene(sim, st, lo, up)
+    st["contact_stats"][:] = 0
+    push(sim, st)
+    sim.simulate(calls)
+    Oracle(sim.model, sim.params, n).simulate(st, calls)
+    cs = get(sim, "contact_stats")
+    over21 = (cs[:, 2] > 21).mean()
+    print(f"kuka closed hand: envs offering > 21 contacts {over21:.2f}, max offered {cs[:, 2].max()}, self contacts "
+          f"{cs[:, 4].sum()}, refreshed {cs[:, 5].sum()}, over capacity {cs[:, 1].sum()} of {cs[:, 0].sum()} substeps")
+    assert over21 >= 0.25, "the scene must overflow chunk 0 (21 contacts) in many envs"
+    assert (cs[:, 4] > 0).mean() >= 0.9, "self-collision contacts in (nearly) every env"
+    assert (cs[:, :6] == st["contact_stats"][:, :6]).all(), "contact statistics differ from the oracle's"
+    scenes.assert_physics_bit_identical(sim, st, n, tag=f"kuka overflow calls {calls}")
