@@ -216,7 +216,13 @@ struct PhysCfg {
     // OVF global area after those: dense rows of chunks 1.. (J then Y), the row constants of every chunk (6 x rpc x
     // NCH, the LDS RK layout), the contact entries of chunks 1.. (8 floats each)
     static constexpr int spill_dense = ovf && !split ? 2 * rpc * (NCH - 1) * row_stride<ND>() : 0;
-    static constexpr int spill_rk = ovf ? 6 * rpc * NCH : 0;
+    // PGS row constants (RK): 6 arrays of rk_stride floats (impulse, target velocity, 1/diagonal, friction, two Delassus
+    // entries), each indexed by the row over all chunks. The kernel's rk() indexes with rk_stride and both RK areas (LDS
+    // for the non-overflow multi-chunk family, the global area for OVF) are sized from it: one constant, so the index
+    // range and the allocation cannot disagree (the first overflow build indexed with the LDS layout's 63-row MAXR
+    // stride while AllegroHand's 12-contact chunks have 36 rows: DESIGN.md §3.12)
+    static constexpr int rk_stride = rpc * NCH;
+    static constexpr int spill_rk = ovf ? 6 * rk_stride : 0;
     static constexpr int spill_ct = ovf ? 8 * CAP * (NCH - 1) : 0;
     static constexpr int off_dense = spill_robot + spill_obj, off_rk = off_dense + spill_dense,
                          off_ct = off_rk + spill_rk;
@@ -245,7 +251,7 @@ __host__ __device__ constexpr size_t pc_rowdata_bytes() {
 }
 template <class PC>
 __host__ __device__ constexpr size_t pc_rows_bytes() {
-    return pc_rowdata_bytes<PC>() + (PC::nch > 1 && !PC::ovf ? 6 * sizeof(float) * (size_t)PC::rpc * PC::nch : 0);
+    return pc_rowdata_bytes<PC>() + (PC::nch > 1 && !PC::ovf ? 6 * sizeof(float) * (size_t)PC::rk_stride : 0);
 }
 // S ~ M^-1 (factor_inverse), D x D at stride D, sized for the family's DOF count: at the end of the union
 // (minv_in_union) or after it
@@ -341,6 +347,7 @@ struct SimCtx {
     // the running pair's slot (-1: none) and description, whose narrow phase writes the record it emits
     float* pcm;
     int pslot, pkind, pA, pB;
+    int pemit;              // points of the running pair's manifold staged for its record (pcm_commit), 0: none
 #ifdef HA_PROFILE
     int pk;                 // profiled build: kind of the running pair
     int pcls;               // profiled build: this substep is heavy (g_prof's second set)
@@ -777,7 +784,6 @@ HD f3 inv_scale(const SimCtx& c, int b) {
 }
 
 HD void store_chosen(SimCtx& c, int k, const f3* P, const f3* N, const float* S, const int* CD, int a, int b);
-HD void pcm_store(SimCtx& c, int t, int k, f3 x, f3 n, float sep, int code);
 // A manifold point's anchor for its persistent record (v13; the oracle's PCM_*): the feature it came from - a vertex or
 // clipped edge point of side A, of side B, or neither (the midpoint of two edges' closest points) - plus PCM_NORMAL_A
 // when the normal is carried by side A (the reference face is A's; B for the ground and edge-edge contacts)
@@ -840,7 +846,17 @@ HD void emit_contacts(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int 
 #endif
     // the chosen lanes' ranks: point t of the manifold (the oracle's idx order)
     int t = lane == i0 ? 0 : (k > 1 && lane == j1 ? 1 : (k > 2 && lane == j2 ? 2 : (k > 3 && lane == j3 ? 3 : -1)));
-    if (c.pslot >= 0 && !c.gather) pcm_store(c, t, k, pt, n, sep, code);    // the pair's record (ha_params_t v13)
+    if (c.pslot >= 0 && !c.gather) {
+        // the pair's manifold for its persistent record (ha_params_t v13), staged in the clipping candidates' scratch
+        // (free once the narrow phase has emitted; not part of the hull-side cache): point t = x, n, sep, anchor.
+        // pcm_commit writes the record after the pair, at one call site instead of one per emit site
+        float* q = reinterpret_cast<float*>(c.col.cand) + 8 * (t < 0 ? 0 : t);
+        if (t >= 0) {
+            q[0] = pt.x; q[1] = pt.y; q[2] = pt.z; q[3] = n.x; q[4] = n.y; q[5] = n.z; q[6] = sep;
+            q[7] = __int_as_float(code);
+        }
+        c.pemit = k;
+    }
     if (HA_EMIT_PARALLEL && !c.gather) {
         int nc0 = s.nc;
         if (nc0 + k <= c.maxc) {
@@ -1556,16 +1572,26 @@ HD void pair_bodies(const SimCtx& c, int kind, int A, int B, PoseF& PA, PoseF& P
 }
 HD qf qconj(qf q) { return qf{-q.x, -q.y, -q.z, q.w}; }
 
-// The record of the running pair's manifold (c.pslot), written by the chosen lanes of emit_contacts: lane of point
-// t < k its point on A (x + n sep / 2) in A's frame, its point on B (x - n sep / 2) in B's frame and its normal in B's
-// frame; lane 0 the relative pose and k. Vector stores: every record access of the kernel is a per-lane vector access
-HD void pcm_store(SimCtx& c, int t, int k, f3 x, f3 n, float sep, int code) {
+// The record of the running pair's manifold (c.pslot), from the points emit_contacts staged: lane t < k its point on
+// A (x + n sep / 2) in A's frame, its point on B (x - n sep / 2) in B's frame, its normal in the frame of the body that
+// carries it and its anchor; lane 0 the relative pose and k. Vector stores: every record access of the kernel is a
+// per-lane vector access
+HD void pcm_commit(SimCtx& c) {
+    int k = c.pemit;
+    c.pemit = 0;
+    if (c.pslot < 0 || k <= 0) return;
+    wsync();
     PoseF PA, PB;
     int a_, b_;
     pair_bodies(c, c.pkind, c.pA, c.pB, PA, PB, a_, b_);
     float* rec = c.pcm + (size_t)c.pslot * HA_PCM_REC;
     qf qbc = qconj(PB.q);
+    int t = c.lane < k ? c.lane : -1;
     if (t >= 0) {
+        const float* q = reinterpret_cast<const float*>(c.col.cand) + 8 * t;
+        f3 x = mk3(q[0], q[1], q[2]), n = mk3(q[3], q[4], q[5]);
+        float sep = q[6];
+        int code = __float_as_int(q[7]);
         float hs = 0.5f * sep;
         qf qac = qconj(PA.q);
         f3 la = qrot(qac, (x + n * hs) - PA.p);
@@ -1849,8 +1875,17 @@ HD void detect_self(SimCtx& c, int npairs) {
                 // the pair's persistent manifold first (it decides the pair's contacts); then the separating-face record
                 PoseF PA, PB;
                 int a_, b_;
+#ifdef HA_PROFILE
+                unsigned long long _q0 = __builtin_amdgcn_s_memtime();
+#endif
                 pair_bodies(c, 5, k, -1, PA, PB, a_, b_);
-                if (pcm_refresh(c, npairs + k, (int)kh, PA, PB, a_, b_)) continue;
+                bool refreshed = pcm_refresh(c, npairs + k, (int)kh, PA, PB, a_, b_);
+#ifdef HA_PROFILE
+                wsync();
+                PROF_COUNT(88, __builtin_amdgcn_s_memtime() - _q0);
+                PROF_COUNT(89, refreshed);
+#endif
+                if (refreshed) continue;
                 c.pslot = npairs + k; c.pkind = 5; c.pA = k; c.pB = -1;
             }
 #ifdef HA_PROFILE
@@ -1892,6 +1927,7 @@ HD void detect_self(SimCtx& c, int npairs) {
 #ifdef HA_X_SELF_DRY
             c.dry = false;
 #endif
+            pcm_commit(c);
             c.pslot = -1;
             if (c.selfc && lane == 0 && c.sepf != rec) c.selfc[k] = (uint8_t)c.sepf;
 #ifdef HA_PROFILE
@@ -2001,8 +2037,17 @@ HD void detect(SimCtx& c) {
                 c.pslot = -1;
                 PoseF PA, PB;
                 int a_, b_;
+#ifdef HA_PROFILE
+                unsigned long long _r0 = __builtin_amdgcn_s_memtime();
+#endif
                 pair_bodies(c, kind, A, B, PA, PB, a_, b_);
-                if (pcm_refresh(c, q, (int)bcast(ckh, bit), PA, PB, a_, b_)) {
+                bool refreshed = pcm_refresh(c, q, (int)bcast(ckh, bit), PA, PB, a_, b_);
+#ifdef HA_PROFILE
+                wsync();
+                PROF_COUNT(88, __builtin_amdgcn_s_memtime() - _r0);         // record checks + refreshes
+                PROF_COUNT(89, refreshed);
+#endif
+                if (refreshed) {
                     mask &= mask - 1;
                     continue;
                 }
@@ -2034,6 +2079,7 @@ HD void detect(SimCtx& c) {
                 c.gather = false;
                 gather_emit(c, kind, A, B);
             }
+            pcm_commit(c);
             c.pslot = -1;
 #ifdef HA_PROFILE
             wsync();
@@ -2267,7 +2313,8 @@ HD void substep(SimCtx& c, float hdt) {
     float* RK;
     if constexpr (PC::ovf) RK = c.spill + PC::off_rk;
     else RK = reinterpret_cast<float*>(reinterpret_cast<char*>(s.u.rows.J) + pc_rowdata_bytes<PC>());
-    auto rk = [&](int q, int row) -> float& { return RK[q * RPC * NCH + row]; };
+    static_assert(PC::rk_stride == RPC * NCH, "RK: one row-constant array per field, every chunk's rows");
+    auto rk = [&](int q, int row) -> float& { return RK[q * PC::rk_stride + row]; };   // q < 6, row < rk_stride
     const bool multi = NCH > 1 && (!PC::ovf || nc > CAP);       // wave-uniform
     // chunk ch's rows. LDS (true) / global (false) dense rows are separate instantiations, so that no pointer may
     // address both (a flat pointer would make chunk 0's LDS rows flat accesses too)

@@ -512,8 +512,12 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
         c.pcm = (st.contact_cache && params->pcm_lin_tol > 0.0f) ? st.contact_cache + (size_t)env * slots * HA_PCM_REC
                                                                    : nullptr;
     }
+#ifdef HA_X_NO_PCM     /* A/B builds only: the persistent-manifold code compiled out */
+    c.pcm = nullptr;
+#endif
     c.pslot = -1;
     c.pkind = c.pA = c.pB = 0;
+    c.pemit = 0;
 #ifdef HA_PROFILE
     c.pcls = 0;
 #endif

@@ -589,8 +589,9 @@ DEFAULT_TASK = dict(
     edge_rel_tol=0.9, edge_abs_tol=0.0005,              # edge-edge vs face axis (handarm_abi.h v10)
     narrow_phase_flags=0,                               # HA_NP_* (A/B and diagnostics only)
     # persistent contact manifolds (handarm_abi.h v13): a pair's record is reused while its relative pose stays within
-    # pcm_lin_tol (m) and pcm_cos_tol (cos of half the relative rotation angle) of the pose it was built at
-    pcm_lin_tol=0.0005, pcm_cos_tol=0.99999,
+    # pcm_lin_tol (m) and pcm_cos_tol (cos of half the relative rotation angle: 0.9998 = 2.3 degrees, PhysX's PCM
+    # rotation threshold) of the pose it was built at
+    pcm_lin_tol=0.001, pcm_cos_tol=0.9998,
     joint_limit_margin=0.02, n_objects=3, num_initial_poses=1, max_episode_length=200,
     sih_alpha=0.8, reward_reaching=1.0, reward_lifting=5.0, reward_goal=50.0, reward_success=50.0,
     lifting_threshold=0.05, goal_threshold=0.05, goal_pos=(0.28, 0.58, 0.8), goal_noise=(0.15, 0.15, 0.1),

@@ -89,12 +89,16 @@ class HandArmSim:
         self._snake = int(os.environ.get("HA_ORDER_SNAKE", 0))     # A/B: alternate-block reversal of the order
         # the refresh sorts by each env's workgroup span in the last step launch (round 4: C4 +13% against the
         # contacts offered, which stays available as HA_ORDER_COST=contacts for A/B runs)
-        if self.rebalance_every > 0 and os.environ.get("HA_ORDER_COST", "time") == "time":
-            _lib.check(self.lib.ha_set_order_cost(self.h, 1), "ha_set_order_cost")
+        order_cost = os.environ.get("HA_ORDER_COST", "time")
+        if order_cost not in ("time", "contacts"):
+            raise ValueError(f"HA_ORDER_COST must be 'time' or 'contacts', not {order_cost!r}")
         self._rb_count = 0
         if self.rebalance_every > 0:
             self._env_order = torch.arange(num_envs, dtype=torch.int32, device=self.device)
             self._cost_prev = torch.zeros(num_envs, dtype=torch.int32, device=self.device)
+            if order_cost == "time":
+                _lib.check(self.lib.ha_set_order_cost(self.h, 1), "ha_set_order_cost")
+                self._cost_prev.zero_()             # the estimates restart with the cost they measure
             _lib.check(self.lib.ha_set_env_order(self.h, C.c_void_p(self._env_order.data_ptr()), num_envs),
                        "ha_set_env_order")
 
@@ -243,7 +247,10 @@ class HandArmSim:
                                             C.c_void_p(obs_out.data_ptr()), float(clip_obs),
                                             C.c_void_p(scalars.data_ptr()) if scalars is not None else None,
                                             self._stream()), "ha_task_step_io")
-        return a            # keep the converted copy alive until the launch has read it (the caller holds it)
+        # the launch reads the converted copy asynchronously: hold it until the next step replaces it (a caller on
+        # another stream than the launch's would otherwise let the caching allocator reuse it too early)
+        self._act_hold = a
+        return a
 
     def task_observe(self, flags=0):
         _lib.check(self.lib.ha_task_observe(self.h, flags, self._stream()), "ha_task_observe")

@@ -128,7 +128,7 @@ def test_bin_link_contacts_spill_rows_match_oracle():
     rs[:, 4:7, 0:3] = body[:, sim.model.body_robot0 + np.array(links), 0:3]
     rs[:, 4:7, 7:13] = 0.0
     put(sim, "root_state", st["root_state"])
-    for k in ("dof_state", "sim_targets"):
+    for k in ("dof_state", "sim_targets", "contact_cache"):     # (the probe call above wrote manifold records)
         put(sim, k, st[k])
     sim.simulate(1)
     orc.simulate(st, 1)

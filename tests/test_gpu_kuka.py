@@ -144,7 +144,7 @@ def test_kuka_link_contacts_spill_rows_match_oracle():
     rs[:, m.actor_object0, 0:3] = body[:, m.body_robot0 + palm, 0:3]
     rs[:, m.actor_object0, 7:13] = 0.0
     put(sim, "root_state", st["root_state"])
-    for k in ("dof_state", "sim_targets"):
+    for k in ("dof_state", "sim_targets", "contact_cache"):     # (the probe call above wrote manifold records)
         put(sim, k, st[k])
     sim.simulate(1)
     orc.simulate(st, 1)

@@ -65,3 +65,28 @@ def test_fingers_and_thumb_stop_at_the_contact_slop(task):
     for e, k in enumerate(names):
         assert seps["on"][e] >= -(p.contact_slop + 5e-4), (k, seps["on"][e])
         assert seps["off"][e] < -0.01, (k, "the drive must push the links into each other", seps["off"][e])
+
+
+def test_no_self_contacts_at_the_reset_poses():
+    """the self pairs are every non-adjacent link pair (no exclude list). At each task's reset pose - AllegroHand
+    zero DOF positions clamped to the limits (allegro_hand.py:252-273), AllegroKuka the arm's desired pose with the
+    fingers at 0 (allegro_kuka_base.py:316-319) - at zero velocity, no pair of cooked hulls is within the contact offset,
+    so no standing self contact pushes against the PD drives at rest."""
+    for task in (HM.TASK_ALLEGRO_HAND, HM.TASK_ALLEGRO_KUKA):
+        scene, p, m, _, _ = _setup(task)
+        D = m.n_dofs
+        lo, up = np.array(m.dof_lower[:D], np.float32), np.array(m.dof_upper[:D], np.float32)
+        pose = np.array(list(p.reset_pose)[:D], np.float32) if task == HM.TASK_ALLEGRO_KUKA else np.zeros(D, np.float32)
+        st = HostState(1, model=m, params=p)
+        st["dof_state"].reshape(1, D, 2)[0, :, 0] = np.clip(pose, lo, up)
+        rs = st["root_state"].reshape(1, m.n_actors, 13)
+        rs[..., 6] = 1.0
+        rs[0, m.actor_object0, 0:3] = [5.0, 5.0, 5.0]         # the object out of reach
+        if task == HM.TASK_ALLEGRO_KUKA:
+            st["object_scale"][:] = 1.0
+        cs = Oracle(m, p, 1).contacts(st, 0)
+        assert not [r for r in cs if r[7] >= 100 and r[8] >= 100], (task, cs)
+        # and the oracle's simulate agrees: one call offers no self-collision contact
+        st["sim_targets"][0] = np.clip(pose, lo, up)
+        Oracle(m, p, 1).simulate(st, 1)
+        assert st["contact_stats"][0, 4] == 0

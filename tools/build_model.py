@@ -523,8 +523,10 @@ def build_cube(size=0.065, density=400.0):
             "inertia": [I, 0, 0, 0, I, 0, 0, 0, I], "hull": box_hull(half)}
 
 
-# self-collision of the Allegro actors (ha_model_t v12): every non-adjacent link pair, minus the link pairs whose
-# convex hulls already touch at the default pose (the cooked hulls are larger than the meshes near the joints)
+# self-collision of the Allegro actors (ha_model_t v12): every non-adjacent link pair ("exclude" can drop pairs). The
+# lists are empty: at each task's reset pose (AllegroHand: zero DOF positions clamped to the limits; AllegroKuka: the
+# arm's desired pose, fingers 0) no pair of cooked hulls is within the contact offset, so the hand starts without
+# standing self contacts (tests/test_self_collision.py::test_no_self_contacts_at_the_reset_poses)
 ALLEGRO_SELF_COLLISION = {"exclude": []}
 KUKA_SELF_COLLISION = {"exclude": []}
 

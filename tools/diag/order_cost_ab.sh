@@ -1,5 +1,6 @@
 #!/usr/bin/env bash
-# Dispatch-order cost: contacts offered (default) vs the last step's workgroup spans (HA_ORDER_COST=time), alternating
+# Dispatch-order cost: the workgroup-span estimate (HA_ORDER_COST=time, HandArmSim's default) vs the contacts offered
+# (HA_ORDER_COST=contacts; any other value is rejected by HandArmSim), alternating
 # runs: bash tools/diag/order_cost_ab.sh "TASK ..."   (GPU box; prints value and kernel ms)
 TASKS=${1:-"allegro_kuka allegro_hand ur5sih"}
 for t in $TASKS; do
