@@ -1539,20 +1539,23 @@ HD void self_pair_hulls(const ha_model_t& m, int k, int& ha, int& hb) {
 // pcm_refresh in physics_oracle.c), so results stay bit-identical.
 //
 // Side A / side B body poses and body codes of candidate pair (kind, A, B): the sides narrow_phase gives collide_hulls
+// (UNIFORM: the pair is wave-uniform and its object poses read the pool id through an SGPR; false: a per-lane pair)
+template <bool UNIFORM = true>
 HD void pair_bodies(const SimCtx& c, int kind, int A, int B, PoseF& PA, PoseF& PB, int& a, int& b) {
     const EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
+    auto opose = [&](int o) { return UNIFORM ? object_pose_u(c, o) : object_pose(c, o); };
     if (kind <= 2) {
-        PA = object_pose_u(c, A);
+        PA = opose(A);
         a = A;
         if (kind == 0) { PB = PoseF{mk3(0, 0, 0), qf{0, 0, 0, 1}}; b = -1; }    // the ground plane z = 0
         else if (kind == 1) { PB = static_pose(m, B); b = -1; }
-        else { PB = object_pose_u(c, B); b = B; }
+        else { PB = opose(B); b = B; }
     } else if (kind == 3) {
         int Lk = m.hull_link[B];
         PA = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])};
         a = 100 + Lk;
-        PB = object_pose_u(c, A);
+        PB = opose(A);
         b = A;
     } else if (kind == 4) {
         int Lk = m.hull_link[A];
@@ -1640,42 +1643,60 @@ HD void emit_points(SimCtx& c, bool valid, f3 pt, float sep, f3 n, int a, int b)
     store_chosen(c, k, P, N, S, CD, a, b);
 }
 
-// Pair slot `slot`'s record (oracle pcm_refresh): kh = its point count (read ahead by the caller). When it holds points
-// and the pair's relative pose (A's body in B's frame) is within pcm_lin_tol / pcm_cos_tol of the pose it was built at,
-// every point is re-evaluated from the current poses - the surface points carried by their bodies, the normal by B,
-// the separation along the normal, the point midway - those within the contact margin go to the list in record order,
-// and the pair needs no narrow phase (true)
-HD bool pcm_refresh(SimCtx& c, int slot, int kh, PoseF PA, PoseF PB, int a, int b) {
+// Pair slot `slot`'s record test (the oracle's pcm_refresh): it applies when it holds points and the pair's relative
+// pose (A's body in B's frame) is within pcm_lin_tol / pcm_cos_tol of the pose it was built at. Evaluated per lane for a
+// whole batch of candidate pairs at once (the broad phase's batch, or the first 64 self-pair candidates), so a pair whose
+// record does not apply costs no load latency of its own. The header comes in two 16-byte loads per lane
+HD bool pcm_valid_lane(const SimCtx& c, int slot, int kind, int A, int B) {
     const ha_params_t& p = *c.p;
-    int lane = c.lane;
-    if (kh <= 0) return false;
-    const float* rec = c.pcm + (size_t)slot * HA_PCM_REC;
-    float hv = rec[lane & 7];               // the header, a word a lane (lane-indexed: never a scalar-cache load)
+    const float4* h = reinterpret_cast<const float4*>(c.pcm + (size_t)slot * HA_PCM_REC);
+    float4 h0 = h[0], h1 = h[1];
+    if ((int)h0.w <= 0) return false;
+    PoseF PA, PB;
+    int a_, b_;
+    pair_bodies<false>(c, kind, A, B, PA, PB, a_, b_);
     qf qbc = qconj(PB.q);
-    f3 d = qrot(qbc, PA.p - PB.p) - mk3(bcast(hv, 0), bcast(hv, 1), bcast(hv, 2));
+    f3 d = qrot(qbc, PA.p - PB.p) - mk3(h0.x, h0.y, h0.z);
     float lt = p.pcm_lin_tol;
     if (dot3(d, d) > lt * lt) return false;
     qf qr = qmul(qbc, PA.q);
-    float cq = ((qr.x * bcast(hv, 4) + qr.y * bcast(hv, 5)) + qr.z * bcast(hv, 6)) + qr.w * bcast(hv, 7);
-    if (fabsf(cq) < p.pcm_cos_tol) return false;
+    float cq = ((qr.x * h1.x + qr.y * h1.y) + qr.z * h1.z) + qr.w * h1.w;
+    return !(fabsf(cq) < p.pcm_cos_tol);
+}
+// one record in one register: lane i < HA_PCM_REC holds word i (a 192-byte coalesced load, issued a pair ahead)
+HD float pcm_load(const SimCtx& c, int slot) {
+    return c.lane < HA_PCM_REC ? c.pcm[(size_t)slot * HA_PCM_REC + c.lane] : 0.0f;
+}
+// A pair whose record applies (pcm_valid_lane): every point is re-evaluated from the current poses - the surface points
+// carried by their bodies, the normal by the body that owns it, the separation along the normal, the point half the
+// separation off its feature - those within the contact margin go to the list in record order, and the pair needs no
+// narrow phase. rv = the record (pcm_load); lane t < k gathers its point's words by lane permutes
+HD void pcm_emit_record(SimCtx& c, float rv, int kind, int A, int B) {
+    const ha_params_t& p = *c.p;
+    int lane = c.lane;
+    int k = (int)bcast(rv, 3);
+    PoseF PA, PB;
+    int a, b;
+    pair_bodies(c, kind, A, B, PA, PB, a, b);
+    int t = lane < 4 ? lane : 0;
+    float r[9];
+#pragma unroll
+    for (int f = 0; f < 9; f++) r[f] = __shfl(rv, 8 + 9 * t + f);
+    int code = (int)__shfl(rv, 44 + t);
     bool valid = false;
     f3 x = mk3(0, 0, 0), n = mk3(0, 0, 0);
     float sp = 0.0f;
-    if (lane < kh && lane < 4) {
-        const float* r = rec + 8 + 9 * lane;
-        int code = (int)rec[44 + lane];
-        f3 wa = PA.p + qrot(PA.q, ld3(r));
-        f3 wb = PB.p + qrot(PB.q, ld3(r + 3));
-        n = qrot((code & PCM_NORMAL_A) ? PA.q : PB.q, ld3(r + 6));
+    if (lane < k && lane < 4) {
+        f3 wa = PA.p + qrot(PA.q, mk3(r[0], r[1], r[2]));
+        f3 wb = PB.p + qrot(PB.q, mk3(r[3], r[4], r[5]));
+        n = qrot((code & PCM_NORMAL_A) ? PA.q : PB.q, mk3(r[6], r[7], r[8]));
         sp = dot3(n, wa - wb);
         valid = sp <= p.contact_margin;
-        // the point where the narrow phase puts it: half the separation off its feature along the normal
         int f = code & 3;
         x = f == PCM_FEAT_A ? wa - n * (0.5f * sp) : (f == PCM_FEAT_B ? wb + n * (0.5f * sp) : (wa + wb) * 0.5f);
     }
     emit_points(c, valid, x, sp, n, a, b);
     if (lane == 0) c.s->cst[5] += 1;
-    return true;
 }
 
 // piece pairs of a candidate pair (1 unless an object is a compound of several convex pieces)
@@ -1839,8 +1860,13 @@ HD void detect_self(SimCtx& c, int npairs) {
     // point counts of their persistent manifolds (slot npairs + pair)
     int crec = 0xFF;
     if (c.selfc && lane < ncd) crec = c.selfc[cdl[lane]];
-    float ckh = 0.0f;
-    if (c.pcm && lane < ncd) ckh = c.pcm[(size_t)(npairs + cdl[lane]) * HA_PCM_REC + 3];
+    // the first 64 candidates whose persistent-manifold record applies (lane = candidate rank), tested at once; their
+    // records are loaded a candidate ahead
+    // (in a block of its own before the candidate loop, so that none of its values stay live into the narrow phases)
+    bool pv = false;
+    if (c.pcm && lane < ncd) pv = pcm_valid_lane(c, npairs + cdl[lane], 5, cdl[lane], -1);
+    uint64_t vmask = __ballot(pv);
+    asm volatile("" : "+s"(vmask));
 #ifdef HA_PROFILE
     PROF_COUNT(83, __builtin_amdgcn_s_memtime() - _s0);              // box table + box tests
 #endif
@@ -1861,32 +1887,32 @@ HD void detect_self(SimCtx& c, int npairs) {
             PROF_COUNT(85, 1);                                              // candidates
 #endif
             int rec;
-            float kh = 0.0f;
+            bool refresh = false;
             if (rank < 64) {
                 rec = __builtin_amdgcn_readlane(crec, rank);
-                kh = bcast(ckh, rank);
+                refresh = (vmask >> rank) & 1ull;
             } else {
                 rec = __builtin_amdgcn_readfirstlane(c.selfc ? (int)c.selfc[k] : 0xFF);
-                if (c.pcm) kh = bcast(c.pcm[(size_t)(npairs + k) * HA_PCM_REC + (lane & 7)], 3);   // lane-indexed
             }
-            rank++;
             c.pslot = -1;
             if (c.pcm) {
                 // the pair's persistent manifold first (it decides the pair's contacts); then the separating-face record
-                PoseF PA, PB;
-                int a_, b_;
 #ifdef HA_PROFILE
                 unsigned long long _q0 = __builtin_amdgcn_s_memtime();
 #endif
-                pair_bodies(c, 5, k, -1, PA, PB, a_, b_);
-                bool refreshed = pcm_refresh(c, npairs + k, (int)kh, PA, PB, a_, b_);
+                // (past the first 64 candidates: the same test in turn, on every lane)
+                if (rank >= 64) refresh = __ballot(pcm_valid_lane(c, npairs + k, 5, k, -1)) != 0ull;
+                if (refresh) pcm_emit_record(c, pcm_load(c, npairs + k), 5, k, -1);
 #ifdef HA_PROFILE
                 wsync();
                 PROF_COUNT(88, __builtin_amdgcn_s_memtime() - _q0);
-                PROF_COUNT(89, refreshed);
+                PROF_COUNT(89, refresh);
 #endif
-                if (refreshed) continue;
+                rank++;
+                if (refresh) continue;
                 c.pslot = npairs + k; c.pkind = 5; c.pA = k; c.pB = -1;
+            } else {
+                rank++;
             }
 #ifdef HA_PROFILE
             PROF_COUNT(86, rec != 0xFF);                                    // candidates with a record
@@ -2012,8 +2038,9 @@ HD void detect(SimCtx& c) {
             }
         }
         uint64_t mask = __ballot(cand);
-        // the candidates' persistent-manifold point counts, one load for the batch (ha_params_t v13)
-        float ckh = (c.pcm && cand) ? c.pcm[(size_t)p * HA_PCM_REC + 3] : 0.0f;
+        // the candidates whose persistent-manifold record applies (ha_params_t v13), tested for the whole batch at once;
+        // their records are then loaded a pair ahead of their turn (one register each)
+        uint64_t vmask = __ballot(c.pcm && cand && pcm_valid_lane(c, p, kind, A, B));
         // one iteration per piece pair: a compound object (several convex pieces, ha_model_t v8) runs piece
         // pairs j = 0 .. np-1 of a candidate pair and then emits a single <= 4-point manifold for the object pair
         // (the oracle's gather_begin / gather_end). One loop and one call site per narrow phase (a single inlined
@@ -2035,19 +2062,16 @@ HD void detect(SimCtx& c) {
             if (j == 0 && c.pcm) {
                 // the pair's persistent manifold: refreshed from its record, or the narrow phase writes the record
                 c.pslot = -1;
-                PoseF PA, PB;
-                int a_, b_;
+                if ((vmask >> bit) & 1ull) {
 #ifdef HA_PROFILE
-                unsigned long long _r0 = __builtin_amdgcn_s_memtime();
+                    unsigned long long _r0 = __builtin_amdgcn_s_memtime();
 #endif
-                pair_bodies(c, kind, A, B, PA, PB, a_, b_);
-                bool refreshed = pcm_refresh(c, q, (int)bcast(ckh, bit), PA, PB, a_, b_);
+                    pcm_emit_record(c, pcm_load(c, q), kind, A, B);
 #ifdef HA_PROFILE
-                wsync();
-                PROF_COUNT(88, __builtin_amdgcn_s_memtime() - _r0);         // record checks + refreshes
-                PROF_COUNT(89, refreshed);
+                    wsync();
+                    PROF_COUNT(88, __builtin_amdgcn_s_memtime() - _r0);     // refreshes
+                    PROF_COUNT(89, 1);
 #endif
-                if (refreshed) {
                     mask &= mask - 1;
                     continue;
                 }
