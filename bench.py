@@ -225,7 +225,7 @@ def cpu_baseline(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0, binpic
     from handarm_hip import model as HM
     from tests import scenes
     scene = HM.load_scene(HM.BIN_ASSET if binpick else HM.ASSET)
-    pool = [o["name"] for o in HM.load_scene()["objects"]] if pool16 else None
+    pool = (HM.POOL_WIDE if pool16 == "wide" else HM.POOL16) if pool16 else None
     model = HM.build_model(scene, pool)
     params, _ = HM.build_params({"n_objects": 8} if binpick else None)
     orc = Oracle(model, params, num_envs)
@@ -234,7 +234,7 @@ def cpu_baseline(num_envs=1024, min_seconds=12.0, max_steps=4000, seed=0, binpic
         scenes.fill_bin_scene(st, num_envs, scene, seed=seed)
     else:
         scenes.fill_scene(st, num_envs, seed=seed)
-        if pool16:      # C4: each env's 3 objects are a random.sample of the 16-object pool (multi_object.py:569)
+        if pool16:      # C4: each env's 3 objects are a random.sample of the pool (multi_object.py:569)
             st["object_indices"][:] = np.stack([np.random.default_rng(seed + e).choice(len(pool), 3, replace=False)
                                                 for e in range(num_envs)])
     A, B, no, a0 = model.n_actors, model.n_bodies, params.n_objects, model.actor_object0
@@ -276,21 +276,29 @@ CONFIGS = {
                            "8192 envs/GPU (65536 at 8 GPUs)"),
     "C5": ("binpick", 8192, "Multi-object bin-picking shard (hard_bin, 8 objects per env), 8192 envs/GPU "
                             "(32768 at 4 GPUs)"),
+    # C4 on the wide pool (round 5, f1): 3 objects per env from the 16-object pool plus the 8 concave objects of the
+    # reference's list as convex pieces (HM.POOL_WIDE)
+    "C4w": ("ur5sih_wide", 8192, "HandArmGrasp shard, DR on, 3 objects per env sampled from the 24-object YCB pool "
+                                 "(the 16-object pool + 8 concave objects decomposed into convex pieces), 8192 envs/GPU"),
 }
 STEP_KERNEL = {"allegro_kuka": "ak_step_kernel", "allegro_hand": "ah_step_kernel", "ur5sih": "ha_step_kernel",
-               "binpick": "hb_step_kernel"}
+               "binpick": "hb_step_kernel", "ur5sih_wide": "ha_step_kernel"}
 # VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md:54)
 VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
 NOMINAL_CLOCK_HZ = 2.4e9
 
 
-def pool16_names():
+def pool16_names(wide=False):
+    """C4 / C5 object pool: the 16-object YCB pool (HM.POOL16), or with wide the 24 objects incl. the 8 concave ones as
+    convex pieces (HM.POOL_WIDE, round 5)."""
     from handarm_hip import model as HM
-    return [o["name"] for o in HM.load_scene()["objects"]]
+    return list(HM.POOL_WIDE if wide else HM.POOL16)
 
 
 def make_env(task, envs, seed, device, args):
     from handarm_hip.tasks import AllegroHand, AllegroKuka, Ur5SihMultiObjectManipulation
+    wide = task == "ur5sih_wide" or args.wide_pool
+    task = "ur5sih" if task == "ur5sih_wide" else task
     if task == "allegro_kuka":
         return AllegroKuka({"env": {"numEnvs": envs, "subtask": args.subtask}, "seed": seed}, device, device)
     if task == "allegro_hand":
@@ -299,7 +307,7 @@ def make_env(task, envs, seed, device, args):
     if args.pointclouds:
         envcfg["observations"] = PC_STUDENT
     # C4 / C5 draw each env's objects by random.sample from the 16-object YCB pool (multi_object.py:569)
-    cfg = {"env": envcfg, "seed": seed, "objects": {"dataset": {"ycb": pool16_names()}}}
+    cfg = {"env": envcfg, "seed": seed, "objects": {"dataset": {"ycb": pool16_names(wide)}}}
     if task == "binpick":
         # config 5: Ur5SihMultiObject with bin.asset hard_bin and 8 objects
         cfg.update({"bin": {"asset": "hard_bin"}})
@@ -317,7 +325,7 @@ def bytes_per_env_step(task, env, args):
         return allegro_bytes_per_env_step()[0]
     if task == "binpick":
         return algorithmic_bytes_per_env_step(n_obj=8, num_obs=env.sim.params.num_obs, n_static_bodies=6)[0]
-    return algorithmic_bytes_per_env_step(dr=not args.no_dr)[0]
+    return algorithmic_bytes_per_env_step(dr=not args.no_dr)[0]          # ur5sih, ur5sih_wide
 
 
 def _profile_json(name, envs):
@@ -426,7 +434,7 @@ def run_config(task, envs, args, world, rank, device, log_interval_fn):
                                       "kernel_avg_ms": statistics.mean(pc_ms), "algorithmic_bytes_per_env": pb,
                                       "achieved": pach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": pach / HBM_PEAK_GBS}
-    if task in ("ur5sih", "binpick") and args.episode_steps > 0:
+    if task in ("ur5sih", "binpick", "ur5sih_wide") and args.episode_steps > 0:
         # the whole-episode window: the K-step window above starts right after the first reset, where
         # the arm has not reached the objects yet; the next episode_steps steps (one full 200-step episode, so one
         # synchronous reset step) give the steady-state rate and contact statistics north_star's figure is about
@@ -483,7 +491,7 @@ def run_cpu_baseline(task, args, seconds, threads=None):
             r = cpu_baseline_allegro(args.cpu_envs, seconds)
         else:
             r = cpu_baseline(args.cpu_envs // (4 if task == "binpick" else 1), seconds, binpick=task == "binpick",
-                             pool16=task == "ur5sih")
+                             pool16="wide" if task == "ur5sih_wide" else task == "ur5sih")
     finally:
         lib.hao_set_threads(prev)
     r["cores"] = threads or prev
@@ -498,9 +506,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--task", choices=["all", "allegro_kuka", "ur5sih", "allegro_hand", "binpick"], default="all",
+    ap.add_argument("--task", choices=["all", "allegro_kuka", "ur5sih", "allegro_hand", "binpick", "ur5sih_wide"],
+                    default="all",
                     help="all (default): the C2 headline (allegro_kuka) plus sub-records for C3 (allegro_hand), "
-                         "C4 (ur5sih shard) and C5 (binpick shard); or one of them alone")
+                         "C4 (ur5sih shard), C5 (binpick shard) and C4w (ur5sih shard on the 24-object pool); or one "
+                         "of them alone")
+    ap.add_argument("--wide-pool", action="store_true", help="ur5sih / binpick: draw the objects from the 24-object "
+                                                            "pool (the 8 concave objects as convex pieces)")
     ap.add_argument("--subtask", choices=["regrasping", "reorientation"], default="regrasping")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU of a single --task (default: its config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -527,7 +539,7 @@ def main():
         return parallel.reduce_episode_stats(env)            # RCCL all-reduce of the episode counters (N > 1)
 
     if args.task == "all":
-        head, subs = "C2", ["C3", "C4", "C5"]
+        head, subs = "C2", ["C3", "C4", "C5", "C4w"]
     else:
         head = next(k for k, v in CONFIGS.items() if v[0] == args.task)
         subs = []
@@ -553,7 +565,9 @@ def main():
             "allegro_hand": "synthetic (seeded U[-1,1] actions, AllegroHand.yaml cube scene)",
             "ur5sih": "synthetic (seeded U[-1,1] actions, YCB objects of the 16-object pool, dropped at init)",
             "binpick": "synthetic (seeded U[-1,1] actions, hard_bin tote + 8 YCB objects per env from the 16-object "
-                       "pool, dropped into the bin at init)"}
+                       "pool, dropped into the bin at init)",
+            "ur5sih_wide": "synthetic (seeded U[-1,1] actions, YCB objects of the 24-object pool incl. 8 concave ones as "
+                           "convex pieces, dropped at init)"}
     h = records[head]
     task, envs, label = CONFIGS[head]
     envs = h["envs_per_gpu"]

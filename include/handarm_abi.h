@@ -51,11 +51,11 @@ extern "C" {
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
 #define HA_MAX_DOFS 24
-#define HA_MAX_HULLS 64
-#define HA_MAX_VERTS 4096
-#define HA_MAX_PLANES 8192
-#define HA_MAX_EDGES 8192      /* hull edges, all hulls (v10) */
-#define HA_MAX_LOOP 16384      /* face-loop entries, all hulls (v10): 2 per edge */
+#define HA_MAX_HULLS 128    /* v13: 128 (the concave YCB objects' convex pieces) */
+#define HA_MAX_VERTS 8192
+#define HA_MAX_PLANES 16384
+#define HA_MAX_EDGES 16384     /* hull edges, all hulls (v10) */
+#define HA_MAX_LOOP 32768      /* face-loop entries, all hulls (v10): 2 per edge (16-bit loop starts) */
 #define HA_MAX_FACE_LOOP 21    /* vertices of one face loop (v10): a clipped manifold's 2 x 21 + 21 candidates fit a wave */
 #define HA_MAX_POOL 32
 #define HA_MAX_OBJ 8           /* objects per env: 3 in Ur5SihMultiObject.yaml:2, 8 for bin-picking (config 5) */

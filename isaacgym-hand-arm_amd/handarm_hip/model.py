@@ -21,8 +21,8 @@ ALLEGRO_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets
 KUKA_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "kuka_allegro_scene.json")
 BIN_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "ur5sih_bin_scene.json")
 
-MAX_LINKS, MAX_DOFS, MAX_HULLS, MAX_VERTS, MAX_PLANES = 32, 24, 64, 4096, 8192
-MAX_EDGES, MAX_LOOP, MAX_FACE_LOOP = 8192, 16384, 21
+MAX_LINKS, MAX_DOFS, MAX_HULLS, MAX_VERTS, MAX_PLANES = 32, 24, 128, 8192, 16384
+MAX_EDGES, MAX_LOOP, MAX_FACE_LOOP = 16384, 32768, 21
 MAX_POOL, MAX_OBJ, MAX_INIT_POSES, MAX_SPLINE_PIECES, N_SPLINES = 32, 8, 4, 8, 8
 MAX_STATIC = 10
 MAX_FIXED_BODIES = 8
@@ -149,6 +149,17 @@ STATE_FIELDS = ["root_state", "rigid_body_state", "dof_state", "net_contact_forc
                 "contact_stats", "contact_cache"]
 PCM_REC = 48        # HA_PCM_REC: floats per persistent-manifold record (include/handarm_abi.h v13)
 CSTAT = 8           # HA_CSTAT: contact_stats columns
+
+
+# The committed Ur5Sih scene's object pools (tools/build_model.py): the 16 objects of rounds 1-4 (the reference's default
+# set, Ur5SihMultiObject.yaml:11, plus 13 of its commented list, the mug decomposed), then the 8 clearly concave objects of
+# that list as convex pieces (round 5, f1). POOL16 is the bench's C4 / C5 pool; POOL_WIDE = all 24
+POOL16 = ["015_peach", "005_tomato_soup_can", "006_mustard_bottle", "004_sugar_box", "007_tuna_fish_can",
+          "008_pudding_box", "009_gelatin_box", "010_potted_meat_can", "013_apple", "014_lemon", "016_pear", "017_orange",
+          "018_plum", "025_mug", "061_foam_brick", "077_rubiks_cube"]
+CONCAVE_POOL = ["031_spoon", "033_spatula", "037_scissors", "042_adjustable_wrench", "050_medium_clamp", "065-a_cups",
+                "065-d_cups", "073-a_lego_duplo"]
+POOL_WIDE = POOL16 + CONCAVE_POOL
 
 
 def pcm_slots(model, n_obj):

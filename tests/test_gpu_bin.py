@@ -176,7 +176,7 @@ def test_bin_vectask_episode():
     from handarm_hip.tasks import Ur5SihMultiObjectManipulation
     n = 2048
     cfg = {"env": {"numEnvs": n}, "bin": {"asset": "hard_bin"},
-           "objects": {"num_objects": NO, "dataset": {"ycb": [o["name"] for o in HM.load_scene()["objects"]]}}}
+           "objects": {"num_objects": NO, "dataset": {"ycb": HM.POOL16}}}
     env = Ur5SihMultiObjectManipulation(cfg, "cuda:0", "cuda:0")
     obs = env.reset()["obs"]
     assert obs.shape == (n, 212) and env.num_actors == A and env.num_bodies == B

@@ -269,7 +269,7 @@ def test_vectask_episode_at_full_shard_size(dr):
     n = 8192
     cfg = {"env": {"numEnvs": n}}
     if dr:
-        cfg.update({"task": {"randomize": True}, "objects": {"dataset": {"ycb": [o["name"] for o in HM.load_scene()["objects"]]}}})
+        cfg.update({"task": {"randomize": True}, "objects": {"dataset": {"ycb": HM.POOL16}}})
     env = Ur5SihMultiObjectManipulation(cfg, "cuda:0", "cuda:0")
     obs = env.reset()["obs"]
     print("full-shard episode: constructed", flush=True)

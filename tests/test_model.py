@@ -48,8 +48,11 @@ def test_mug_is_a_compound_of_convex_pieces():
         names = [o["name"] for o in HM.load_scene(asset)["objects"]]
         mug = names.index("025_mug")
         assert m.pool_nhull[mug] >= 8
-        assert all(m.pool_nhull[i] == 1 for i in range(m.n_pool) if i != mug)
-        assert m.n_hulls <= 64 and m.pool_hull[mug] + m.pool_nhull[mug] <= m.n_hulls
+        # the other objects of the 16-object pool keep one hull; the concave ones of the wide pool are compounds
+        assert all(m.pool_nhull[i] == 1 for i in range(m.n_pool) if i != mug and names[i] in HM.POOL16)
+        assert all(m.pool_nhull[i] >= 4 for i in range(m.n_pool) if names[i] in HM.CONCAVE_POOL)
+        assert names[:16] == HM.POOL16 and names[16:] == HM.CONCAVE_POOL
+        assert m.n_hulls <= HM.MAX_HULLS and m.pool_hull[mug] + m.pool_nhull[mug] <= m.n_hulls
         pieces = range(m.pool_hull[mug], m.pool_hull[mug] + m.pool_nhull[mug])
         planes = np.ctypeslib.as_array(m.planes)
 

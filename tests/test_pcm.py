@@ -105,7 +105,10 @@ def test_resting_cuboids_reuse_their_records_and_rest_like_the_narrow_phase():
     assert (cs[:, 5] >= cs[:, 0] - 4).all(), cs[:, [0, 5, 6]]         # the table pair refreshed nearly every substep
     assert (off["contact_stats"][:, 5] == 0).all()
     ro, rf = on["root_state"].reshape(n, 4, 13)[:, 1], off["root_state"].reshape(n, 4, 13)[:, 1]
-    np.testing.assert_allclose(ro[:, 0:3], rf[:, 0:3], atol=5e-4)
+    # the records reuse points within 1 mm / 2.3 degrees of their build pose: 1 s of rest ends within 2 mm of the run
+    # without them (the long thin cuboids settle slowest), and every cuboid rests on its face at the table top
+    np.testing.assert_allclose(ro[:, 0:3], rf[:, 0:3], atol=2e-3)
+    np.testing.assert_allclose(ro[:, 2], 0.53 + 0.025 * scales[:, 0, 2], atol=1.5e-3)
     # the tall cuboids (scale 3) rock slowly either way (~0.1 rad/s): no faster with the records
     assert np.abs(ro[:, 7:13]).max(1).max() <= np.abs(rf[:, 7:13]).max(1).max() + 0.02
     fo = on["net_contact_force"].reshape(n, 27, 3)[:, 24, 2]
@@ -115,19 +118,19 @@ def test_resting_cuboids_reuse_their_records_and_rest_like_the_narrow_phase():
 
 def test_motion_past_the_tolerance_rebuilds_the_record():
     """A record is reused only while the relative pose stays within the tolerances: a cuboid pushed sideways at
-    20 cm/s moves 1.7 mm per substep (> pcm_lin_tol = 0.5 mm), so its table pair runs the narrow phase every
-    substep and its record is rebuilt at each new pose."""
+    40 cm/s moves 3.3 mm per substep (friction takes 8 cm/s per substep off; > pcm_lin_tol = 1 mm either way), so its
+    table pair runs the narrow phase every substep and its record is rebuilt at each new pose."""
     n = 4
     scene, model, params, st, scales, lo, up = setup(n)
     root = _resting_cuboids(n, model, st, scales)
-    root[:, 1, 7] = 0.2
+    root[:, 1, 7] = 0.4
     orc = Oracle(model, params, n)
     orc.simulate(st, 1)
     assert (st["contact_stats"][:, 6] >= 2).all()
     rec = st["contact_cache"][:, 1]
     assert (rec[:, 3] >= 1).all()
     # the record's relative position is the one of the last substep's pose (before its integration step), not the first
-    # substep's 1.7 mm behind it
+    # substep's 3 mm behind it
     tpos = np.array(model.static_pos[0], np.float32)
     x_last = root[:, 1, 0] - root[:, 1, 7] * (params.dt / params.substeps)
     np.testing.assert_allclose(rec[:, 0] + tpos[0], x_last, atol=2e-6)

@@ -338,6 +338,14 @@ def build_robot():
 # for its convex hull; every other pool object is within 20 %), so it alone is decomposed (tools/convex_decomp.py
 # decompose_vessel: base slab, 6 wall sectors, 2 handle pieces; the cavity and the handle gap stay open).
 DECOMPOSE = {"025_mug": "vessel"}
+# The wide pool (round 5, verdict f1): the clearly concave objects of the reference's commented dataset list
+# (Ur5SihMultiObject.yaml:8; mesh volume under half of the convex hull's), each decomposed like the mug -
+# (kind, voxel pitch): "acd" the general voxel ACD (tools/convex_decomp.py decompose, <= 8 pieces), "vessel" the
+# handle-less cups as a base slab and six wall sectors. Pieces are cooked to <= MAX_PIECE_VERTS vertices.
+CONCAVE_POOL = {"031_spoon": ("acd", 0.002), "033_spatula": ("acd", 0.0025), "037_scissors": ("acd", 0.002),
+                "042_adjustable_wrench": ("acd", 0.002), "050_medium_clamp": ("acd", 0.0015),
+                "065-a_cups": ("vessel", 0.001), "065-d_cups": ("vessel", 0.001), "073-a_lego_duplo": ("acd", 0.0015)}
+MAX_PIECE_VERTS = 32
 
 
 def build_object(name):
@@ -354,10 +362,16 @@ def build_object(name):
            "inertia": (I_unit * mass / vol).reshape(-1).tolist(), "hull": hull,
            "bbox_from_origin_pos": ctr.tolist(), "bbox_from_origin_quat": scipy_quat(R).tolist(),
            "bbox_extents": ext.tolist()}
-    if name in DECOMPOSE:
+    if name in DECOMPOSE or name in CONCAVE_POOL:
         import convex_decomp as CD
-        pieces, _ = CD.decompose_vessel(v, f)
-        rec["hulls"] = [hull_record(p, MAX_OBJ_VERTS) for p in pieces]
+        if name in DECOMPOSE:
+            pieces, _ = CD.decompose_vessel(v, f)
+            rec["hulls"] = [hull_record(p, MAX_OBJ_VERTS) for p in pieces]
+        else:
+            kind, h = CONCAVE_POOL[name]
+            pieces, _ = (CD.decompose_vessel(v, f, h=h, sectors=6, handle_pieces=0) if kind == "vessel"
+                         else CD.decompose(v, f, h=h, max_pieces=8, tol=0.1))
+            rec["hulls"] = [hull_record(p, MAX_PIECE_VERTS) for p in pieces]
         # mass properties of the actual (non-convex) shape: the closed mesh itself
         vol, com, I_unit = CD.mesh_volume_props(v, f)
         rec["com"] = com.tolist()
@@ -855,6 +869,41 @@ def main_pointclouds(seed=0):
           f"{list(zip(r_names, r_counts))} -> {PC_OUT}")
 
 
+def main_concave():
+    """Adds the CONCAVE_POOL objects to the committed Ur5Sih scene (after the 16-object pool, whose entries stay
+    untouched; the bin scene extends it) and their point-cloud samples to the committed npz (a generator seeded per
+    object name, so the existing samples - which the point-cloud goldens were made with - do not change)."""
+    import zlib
+    scene = json.load(open(OUT))
+    have = {o["name"] for o in scene["objects"]}
+    added = []
+    for name in CONCAVE_POOL:
+        if name in have:
+            continue
+        rec = build_object(name)
+        scene["objects"].append(rec)
+        added.append((name, len(rec["hulls"]), [len(h["verts"]) for h in rec["hulls"]]))
+    with open(OUT, "w") as f:
+        json.dump(scene, f, indent=None, separators=(",", ":"))
+    d = dict(np.load(PC_OUT))
+    names = [str(n) for n in d["object_names"]]
+    samples, areas = list(d["object_samples"]), list(d["object_areas"])
+    for rec in scene["objects"]:
+        if rec["name"] in names:
+            continue
+        urdf = os.path.join(ASSETS, "object_sets", "urdf", "ycb", rec["name"] + ".urdf")
+        link = ET.parse(urdf).getroot().find("link")
+        v, f = link_collision_mesh(link, os.path.dirname(urdf))
+        pts, area = sample_surface(v, f, PC_MAX_POINTS, np.random.default_rng(zlib.crc32(rec["name"].encode())))
+        names.append(rec["name"])
+        samples.append(pts.astype(np.float32))
+        areas.append(area)
+    d["object_names"], d["object_samples"], d["object_areas"] = np.array(names), np.array(samples, np.float32), \
+        np.array(areas, np.float64)
+    np.savez_compressed(PC_OUT, **d)
+    print(f"concave pool: added {added} -> {OUT}; point clouds for {len(names)} objects -> {PC_OUT}")
+
+
 def main_dof_friction():
     """Adds the DOF friction to the committed Allegro scenes without rebuilding their hulls: AllegroHand 0.01
     (allegro_hand.py:267), AllegroKuka the URDF's <dynamics friction> (AllegroKuka.yaml:58 dofFriction -1 keeps
@@ -876,6 +925,8 @@ if __name__ == "__main__":
         sys.exit(main_dof_friction())
     if "--pointclouds" in sys.argv:
         sys.exit(main_pointclouds())
+    if "--concave" in sys.argv:
+        sys.exit(main_concave())
     if "--bin" in sys.argv:
         sys.exit(main_bin())
     if "--allegro" in sys.argv:

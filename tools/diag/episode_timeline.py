@@ -17,7 +17,7 @@ from handarm_hip.tasks import Ur5SihMultiObjectManipulation  # noqa: E402
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 n = int(args[0]) if args else 8192
-pool = [o["name"] for o in HM.load_scene()["objects"]]
+pool = HM.POOL16
 env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}, "seed": 42, "task": {"randomize": "--nodr" not in sys.argv},
                                      "objects": {"dataset": {"ycb": pool}}}, "cuda:0", "cuda:0")
 env.reset()

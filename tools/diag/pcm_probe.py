@@ -69,7 +69,7 @@ def run_kuka(n, steps, seed=0):
 def run_ur5sih(n, steps, binpick=False, seed=0):
     from tests import scenes
     scene = HM.load_scene(HM.BIN_ASSET if binpick else HM.ASSET)
-    pool = [o["name"] for o in HM.load_scene()["objects"]]
+    pool = HM.POOL_WIDE if os.environ.get("HA_WIDE_POOL") else HM.POOL16
     model = HM.build_model(scene, None if binpick else pool)
     params, _ = HM.build_params({"n_objects": 8} if binpick else None)
     orc = Oracle(model, params, n)

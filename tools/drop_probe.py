@@ -16,7 +16,7 @@ n = int(args[0]) if args else 2048
 rounds = int(args[1]) if len(args) > 1 else 30
 nobin = "--nobin" in sys.argv          # the C4 scene: no bin, 3 objects of the 16-object pool on the table
 no = 3 if nobin else 8
-pool = [o["name"] for o in HM.load_scene()["objects"]]
+pool = HM.POOL16
 cfg = {"env": {"numEnvs": n}, "seed": 42, "objects": {"num_objects": no, "dataset": {"ycb": pool},
                                                         "drop": {"max_rounds": rounds, "place_remaining": False}}}
 if not nobin:

@@ -80,13 +80,13 @@ if __name__ == "__main__":
             env = AllegroKuka({"env": {"numEnvs": n}, "seed": 42}, "cuda:0", "cuda:0")
         elif "--bin" in sys.argv:       # bench --task binpick (config 5 shard)
             from handarm_hip import model as HM
-            pool = [o["name"] for o in HM.load_scene()["objects"]]
+            pool = HM.POOL_WIDE if "--wide" in sys.argv else HM.POOL16
             env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}, "seed": 42, "bin": {"asset": "hard_bin"},
                                                  "objects": {"num_objects": 8, "dataset": {"ycb": pool}}},
                                                 "cuda:0", "cuda:0")
         elif "--c4" in sys.argv:        # bench config 4: 16-object YCB pool, DR on (--nomug: the pool without the mug)
             from handarm_hip import model as HM
-            pool = [o["name"] for o in HM.load_scene()["objects"]]
+            pool = HM.POOL_WIDE if "--wide" in sys.argv else HM.POOL16
             if "--nomug" in sys.argv:
                 pool = [p for p in pool if "mug" not in p]
             env = Ur5SihMultiObjectManipulation({"env": {"numEnvs": n}, "seed": 42, "task": {"randomize": True},
