@@ -118,8 +118,8 @@ def cpu_baseline_kuka(num_envs=512, min_seconds=12.0, max_steps=4000, seed=0, su
     from oracle.oracle_lib import HostState, Oracle
     from handarm_hip import model as HM
     scene = HM.load_scene(HM.KUKA_ASSET)
-    model = HM.build_model(scene)
     params, cfg = HM.build_params({"subtask": subtask}, task=HM.TASK_ALLEGRO_KUKA)
+    model = HM.build_model(scene, posed=HM.posed_group(HM.TASK_ALLEGRO_KUKA, cfg))
     N = num_envs
     lo, up = np.array(model.dof_lower[:23], np.float32), np.array(model.dof_upper[:23], np.float32)
     scales, offs = HM.kuka_env_tables(N, scene, cfg)
@@ -142,9 +142,12 @@ def cpu_baseline_kuka(num_envs=512, min_seconds=12.0, max_steps=4000, seed=0, su
     while steps < max_steps and (steps < 2 or time.perf_counter() - t0 < min_seconds):
         steps += 1
         dr = rng.random((N, 80), dtype=np.float32)
-        for a_, b_ in ((3, 6), (12, 15), (18, 21), (48, 71)):
+        ds, G = KO.draw_slots(params), KO.goal_draws(params)     # the U[-1, 1) slots of ak_task.h AK_DRAW_*
+        u11 = {"regrasping": ((3, 6), (G + 3, G + 6)), "reorientation": (),
+               "throw": ((0, 1), (4, 7), (G, G + 1), (G + 4, G + 7))}[subtask]
+        for a_, b_ in u11 + ((ds["OBJ"], ds["OBJ"] + 3), (ds["VEL"], ds["VEL"] + 23)):
             dr[:, a_:b_] = dr[:, a_:b_] * 2 - 1
-        dr[:, 72:75] = rng.standard_normal((N, 3))
+        dr[:, ds["FORCE_N"]:ds["FORCE_N"] + 3] = rng.standard_normal((N, 3))
         a = rng.uniform(-1, 1, (N, 23)).astype(np.float32)
         KO.pre(params, st, a, dr, lo, up)
         hs["dof_state"][:] = st["dof"].reshape(-1, 2)
@@ -513,7 +516,7 @@ def main():
                          "of them alone")
     ap.add_argument("--wide-pool", action="store_true", help="ur5sih / binpick: draw the objects from the 24-object "
                                                             "pool (the 8 concave objects as convex pieces)")
-    ap.add_argument("--subtask", choices=["regrasping", "reorientation"], default="regrasping")
+    ap.add_argument("--subtask", choices=["regrasping", "reorientation", "throw"], default="regrasping")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU of a single --task (default: its config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dr", action="store_true", help="ur5sih: domain randomization off")

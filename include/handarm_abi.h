@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 13
+#define HA_ABI_VERSION 14
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -59,7 +59,7 @@ extern "C" {
 #define HA_MAX_FACE_LOOP 21    /* vertices of one face loop (v10): a clipped manifold's 2 x 21 + 21 candidates fit a wave */
 #define HA_MAX_POOL 32
 #define HA_MAX_OBJ 8           /* objects per env: 3 in Ur5SihMultiObject.yaml:2, 8 for bin-picking (config 5) */
-#define HA_MAX_STATIC 10       /* static boxes per env (table, or table-with-hole walls + bin pieces) */
+#define HA_MAX_STATIC 16       /* static hulls per env (table, table-with-hole walls + bin pieces, v14: the throw bucket) */
 #define HA_MAX_FIXED_BODIES 8  /* fixed rigid bodies with a model pose (table-with-hole links, bin) */
 #define HA_MAX_CONTACTS 84     /* contacts per env and substep: 21 (<= 3 objects), 84 (clutter, > 3 objects) */
 #define HA_MAX_INIT_POSES 4    /* objects.drop.num_initial_poses */
@@ -84,7 +84,7 @@ extern "C" {
 /* tasks (ha_params_t.task) */
 #define HA_TASK_UR5SIH 0        /* Ur5SihMultiObjectManipulation (tasks/hand_arm/task/multi_object_manipulation.py) */
 #define HA_TASK_ALLEGRO_HAND 1  /* AllegroHand in-hand reorientation (tasks/allegro_hand.py) */
-#define HA_TASK_ALLEGRO_KUKA 2  /* AllegroKuka regrasping / reorientation (tasks/allegro_kuka/) */
+#define HA_TASK_ALLEGRO_KUKA 2  /* AllegroKuka regrasping / reorientation / throw (tasks/allegro_kuka/) */
 
 /* AllegroKuka per-env task state (ha_state_t.task_state rows, floats; allegro_kuka_base.py:330-389) */
 #define HA_AK_LIFTED 0          /* lifted_object (0/1) */
@@ -202,6 +202,14 @@ typedef struct ha_model_t {
     int32_t n_self_pairs;
     uint16_t self_pair[HA_MAX_SELF_PAIRS];
     float hull_obb[HA_MAX_HULLS][12];
+    /* v14: statics carried by a per-env fixed-base actor (the AllegroKuka throw bucket, allegro_kuka_throw.py:51-82,
+     * moved by _reset_target :88-103). posed_actor = that actor's index in the env's root_state rows (-1: none); a
+     * static with static_posed[k] != 0 sits at static_pos / static_quat in that actor's frame, so its world pose is
+     * root_state[posed_actor] composed with it (p_actor + q_actor static_pos, q_actor static_quat), read at the
+     * start of each launch and after a reset moves the actor. Its rigid-body row is the actor's root state
+     * (body_goal / actor_goal name the actor's slot). */
+    int32_t posed_actor;
+    int32_t static_posed[HA_MAX_STATIC];
 } ha_model_t;
 
 /* Simulation + task parameters (Ur5SihBase.yaml, Ur5SihMultiObject*.yaml). */
@@ -259,7 +267,7 @@ typedef struct ha_params_t {
     float dr_obs_noise;                /* additive gaussian sigma on obs each step */
     float dr_act_noise;                /* additive gaussian sigma on actions (applied by the host wrapper) */
     /* v3: AllegroKuka (cfg/task/AllegroKuka.yaml:9-94, env/regrasping.yaml, allegro_kuka_base.py:53-400) */
-    int32_t ak_subtask;                /* 0 regrasping, 1 reorientation */
+    int32_t ak_subtask;                /* 0 regrasping, 1 reorientation, 2 throw (v14) */
     int32_t ak_num_keypoints;          /* 1 (regrasping) or 4 */
     float ak_keypoints[4][3];          /* unit keypoint offsets (_object_keypoint_offsets) */
     float ak_object_base_size, ak_keypoint_scale;

@@ -18,21 +18,25 @@
 #define AK_NUM_ACT 23
 #define AK_MAX_OBS 120
 
-// replayed draws (HA_FLAG_REPLAY_DRAWS) in reset_draws[env][...], in the reference's draw order:
-//   [0, 9)   reset_target_pose(goal_env_ids): target (3, U[0,1)); regrasping then reset_object_pose:
-//            position noise (3, U[-1,1)) + get_random_quat uvw (3, U[0,1)); reorientation: goal quat uvw (3)
-//   [9, 18)  reset_idx -> reset_target_pose(env_ids), same layout
-//   [18, 24) reset_idx -> reset_object_pose: position noise (3) + quat uvw (3)
-//   [24]     random_force_prob draw, [25, 48) dof draws U[0,1), [48, 71) dof velocity draws U[-1,1)
-//   [71]     per-step force selection torch.rand(N), [72, 75) torch.randn(3) of a selected env
+// replayed draws (HA_FLAG_REPLAY_DRAWS) in reset_draws[env][...], in the reference's draw order. G = the draws of one
+// reset_target_pose: 9 (regrasping: target (3, U[0,1)) + reset_object_pose's position noise (3, U[-1,1)) and
+// get_random_quat uvw (3, U[0,1)); reorientation: target (3) + goal quat uvw (3)), 10 for throw (bucket side
+// U[-1,1), side offset U[0,0.4), y U[-1,0.7), z U[0,1) + reset_object_pose (6); allegro_kuka_throw.py:85-101)
+//   [0, G)        reset_target_pose(goal_env_ids)
+//   [G, 2G)       reset_idx -> reset_target_pose(env_ids), same layout
+//   [2G, 2G+6)    reset_idx -> reset_object_pose: position noise (3) + quat uvw (3)
+//   [2G+6]        random_force_prob draw, [2G+7, 2G+30) dof draws U[0,1), [2G+30, 2G+53) dof velocity draws U[-1,1)
+//   [2G+53]       per-step force selection torch.rand(N), [2G+54, 2G+57) torch.randn(3) of a selected env
+// (G = 9: 0, 9, 18, 24, 25, 48, 71, 72 as before v14; G = 10 ends at 77 < HA_DRAW_STRIDE)
+HD int ak_goal_draws(const ha_params_t& p) { return p.ak_subtask == 2 ? 10 : 9; }
 #define AK_DRAW_GOAL 0
-#define AK_DRAW_RESET_GOAL 9
-#define AK_DRAW_OBJ 18
-#define AK_DRAW_FORCE_PROB 24
-#define AK_DRAW_DOF 25
-#define AK_DRAW_VEL 48
-#define AK_DRAW_FORCE_U 71
-#define AK_DRAW_FORCE_N 72
+#define AK_DRAW_RESET_GOAL(p) (ak_goal_draws(p))
+#define AK_DRAW_OBJ(p) (2 * ak_goal_draws(p))
+#define AK_DRAW_FORCE_PROB(p) (2 * ak_goal_draws(p) + 6)
+#define AK_DRAW_DOF(p) (2 * ak_goal_draws(p) + 7)
+#define AK_DRAW_VEL(p) (2 * ak_goal_draws(p) + 30)
+#define AK_DRAW_FORCE_U(p) (2 * ak_goal_draws(p) + 53)
+#define AK_DRAW_FORCE_N(p) (2 * ak_goal_draws(p) + 54)
 // per-env keypoint offsets (host-computed in python double, allegro_kuka_base.py:705-715) in task_state
 #define AK_TS_KP HA_AK_KP
 
@@ -57,6 +61,11 @@ HD float ak_draw01(const SimCtx& c, const ha_state_t& st, int env, uint32_t flag
 HD float ak_draw11(const SimCtx& c, const ha_state_t& st, int env, uint32_t flags, int k) {
     if (flags & HA_FLAG_REPLAY_DRAWS) return st.reset_draws[(size_t)env * HA_DRAW_STRIDE + k];
     return 2.0f * uniform01(c.p->seed, env, st.episode[env], 128 + k) - 1.0f;    // torch_rand_float(-1, 1)
+}
+
+HD float ak_draw_range(const SimCtx& c, const ha_state_t& st, int env, uint32_t flags, int k, float lo, float span) {
+    if (flags & HA_FLAG_REPLAY_DRAWS) return st.reset_draws[(size_t)env * HA_DRAW_STRIDE + k];
+    return span * uniform01(c.p->seed, env, st.episode[env], 128 + k) + lo;      // torch_rand_float(lo, lo + span)
 }
 
 // torch_jit_utils.py:81-90 quat_rotate (xyzw)
@@ -117,10 +126,31 @@ HD void ak_reset_target_pose(SimCtx& c, const ha_state_t& st, int env, uint32_t 
     const ha_model_t& m = *c.m;
     int lane = c.lane;
     float tgt[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) tgt[k] = p.ak_target_lo[k] + ak_draw01(c, st, env, flags, k0 + k) * p.ak_target_size[k];
     float* gs = st.goal_state + (size_t)env * 7;
     float* gr = st.root_state + ((size_t)env * m.n_actors + m.actor_goal) * 13;
+    if (p.ak_subtask == 2) {
+        // throw (allegro_kuka_throw.py:85-103): the bucket (the actor in the goal slot, carrying the posed statics)
+        // left or right of the table, the goal 5 cm above its origin, the object back on the table
+        float lr = ak_draw11(c, st, env, flags, k0);
+        float off = ak_draw_range(c, st, env, flags, k0 + 1, 0.0f, 0.4f);
+        float sg = lr > 0.0f ? 1.0f : (lr < 0.0f ? -1.0f : 0.0f);                // torch.sign
+        tgt[0] = (lr > 0.0f ? 0.5f : -0.5f) + sg * off;
+        tgt[1] = ak_draw_range(c, st, env, flags, k0 + 2, -1.0f, 1.7f);
+        tgt[2] = ak_draw01(c, st, env, flags, k0 + 3);
+        if (lane < 3) {
+            gr[lane] = tgt[lane];
+            gs[lane] = lane == 2 ? tgt[2] + 0.05f : tgt[lane];
+            c.s->sb[lane] = tgt[lane];                        // the posed statics follow the bucket this launch
+        }
+        ak_reset_object_pose(c, st, env, flags, k0 + 4, tsv);
+        if (lane == HA_AK_LIFTED) tsv = 0.0f;
+        if (lane == 0) st.reset_goal_buf[env] = 0;
+        if (lane == HA_AK_NEAR_GOAL) tsv = 0.0f;
+        if (lane == HA_AK_CLOSEST_KP) tsv = -1.0f;
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) tgt[k] = p.ak_target_lo[k] + ak_draw01(c, st, env, flags, k0 + k) * p.ak_target_size[k];
     if (lane < 3) {
         gs[lane] = tgt[lane];
         gr[lane] = tgt[lane];
@@ -152,20 +182,20 @@ HD void ak_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags, bool 
     int lane = c.lane, D = c.D;
     if (goal) ak_reset_target_pose(c, st, env, flags, AK_DRAW_GOAL, tsv);
     if (full) {
-        ak_reset_target_pose(c, st, env, flags, AK_DRAW_RESET_GOAL, tsv);
+        ak_reset_target_pose(c, st, env, flags, AK_DRAW_RESET_GOAL(p), tsv);
         if (lane >= HA_AK_RB_FORCE && lane < HA_AK_RB_FORCE + 3) tsv = 0.0f;
-        ak_reset_object_pose(c, st, env, flags, AK_DRAW_OBJ, tsv);
+        ak_reset_object_pose(c, st, env, flags, AK_DRAW_OBJ(p), tsv);
         if (lane == HA_AK_FORCE_PROB) {
             float llo = logf(p.ak_force_prob_lo), lhi = logf(p.ak_force_prob_hi);
-            tsv = expf((llo - lhi) * ak_draw01(c, st, env, flags, AK_DRAW_FORCE_PROB) + lhi);
+            tsv = expf((llo - lhi) * ak_draw01(c, st, env, flags, AK_DRAW_FORCE_PROB(p)) + lhi);
         }
         if (lane < D) {
             float lo = m.dof_lower[lane], up = m.dof_upper[lane], def = p.reset_pose[lane];
             float dmax = up - def, dmin = lo - def;
-            float rd = dmin + (dmax - dmin) * ak_draw01(c, st, env, flags, AK_DRAW_DOF + lane);
+            float rd = dmin + (dmax - dmin) * ak_draw01(c, st, env, flags, AK_DRAW_DOF(p) + lane);
             float coeff = lane < p.ak_num_arm_dofs ? p.ak_dof_noise_arm : p.ak_dof_noise_fingers;
             float pos = def + coeff * rd;
-            float vel = p.ak_dof_vel_noise * ak_draw11(c, st, env, flags, AK_DRAW_VEL + lane);
+            float vel = p.ak_dof_vel_noise * ak_draw11(c, st, env, flags, AK_DRAW_VEL(p) + lane);
             s.q[lane] = pos;
             s.qd[lane] = vel;
             s.tgt[lane] = pos;
@@ -224,13 +254,13 @@ HD void ak_forces(SimCtx& c, const ha_state_t& st, int env, uint32_t flags, floa
     if (p.ak_force_scale <= 0.0f) return;
     uint32_t ctr = __float_as_uint(bcast(tsv, HA_AK_RNG));
     float prob = bcast(tsv, HA_AK_FORCE_PROB);
-    float u = (flags & HA_FLAG_REPLAY_DRAWS) ? st.reset_draws[(size_t)env * HA_DRAW_STRIDE + AK_DRAW_FORCE_U]
+    float u = (flags & HA_FLAG_REPLAY_DRAWS) ? st.reset_draws[(size_t)env * HA_DRAW_STRIDE + AK_DRAW_FORCE_U(p)]
                                              : uniform01(p.seed ^ 0xA5A5A5A5ULL, env, ctr, 0);
     if (lane >= HA_AK_RB_FORCE && lane < HA_AK_RB_FORCE + 3) {
         int k = lane - HA_AK_RB_FORCE;
         tsv = tsv * p.ak_force_decay_step;
         if (u < prob) {
-            float g = (flags & HA_FLAG_REPLAY_DRAWS) ? st.reset_draws[(size_t)env * HA_DRAW_STRIDE + AK_DRAW_FORCE_N + k]
+            float g = (flags & HA_FLAG_REPLAY_DRAWS) ? st.reset_draws[(size_t)env * HA_DRAW_STRIDE + AK_DRAW_FORCE_N(p) + k]
                                                      : gauss01(p.seed, env, ctr, 1 + k);
             tsv = (g * p.ak_object_rb_mass) * p.ak_force_scale;
         }

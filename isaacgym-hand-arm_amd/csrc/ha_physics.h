@@ -117,6 +117,7 @@ struct EnvLDS {
     int nc, nr, noff, ng;                       // contacts kept / rows / contacts offered this substep /
                                                 // points gathered for a compound object pair
     int cst[HA_CSTAT];                          // contact_stats of this launch (see ha_state_t)
+    float sb[8];                                // pose of the actor carrying posed statics (v14): p[3], pad, q[4]
     union {
         PostScratch pd;                         // (the narrow-phase scratch, ColLayout, is sized per family)
         RowScratch rows;
@@ -1501,7 +1502,17 @@ HD bool sphere_near_box(const float* half, PoseF Pb, f3 c, float r) {
     float dz = fmaxf(fabsf(pl.z) - half[2], 0.0f);
     return dx * dx + dy * dy + dz * dz <= r * r;
 }
-HD PoseF static_pose(const ha_model_t& m, int k) { return PoseF{ld3(m.static_pos[k]), ldq(m.static_quat[k])}; }
+// static k's world pose: its model pose, composed with the env's posed actor (s.sb) when the actor carries it (v14)
+HD PoseF static_pose(const SimCtx& c, int k) {
+    const ha_model_t& m = *c.m;
+    PoseF P{ld3(m.static_pos[k]), ldq(m.static_quat[k])};
+    if (m.static_posed[k]) {
+        f3 bp = ld3(c.s->sb);
+        qf bq = ldq(c.s->sb + 4);
+        P = PoseF{bp + qrot(bq, P.p), qmul(bq, P.q)};
+    }
+    return P;
+}
 
 // pair enumeration in the oracle's order (see detect() in physics_oracle.c)
 // pair p -> (kind, A, B): kinds 0 object-ground, 1 object-static B, 2 object-object, 3 link hull B - object,
@@ -1549,7 +1560,7 @@ HD void pair_bodies(const SimCtx& c, int kind, int A, int B, PoseF& PA, PoseF& P
         PA = opose(A);
         a = A;
         if (kind == 0) { PB = PoseF{mk3(0, 0, 0), qf{0, 0, 0, 1}}; b = -1; }    // the ground plane z = 0
-        else if (kind == 1) { PB = static_pose(m, B); b = -1; }
+        else if (kind == 1) { PB = static_pose(c, B); b = -1; }
         else { PB = opose(B); b = B; }
     } else if (kind == 3) {
         int Lk = m.hull_link[B];
@@ -1561,7 +1572,7 @@ HD void pair_bodies(const SimCtx& c, int kind, int A, int B, PoseF& PA, PoseF& P
         int Lk = m.hull_link[A];
         PA = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])};
         a = 100 + Lk;
-        PB = static_pose(m, B);
+        PB = static_pose(c, B);
         b = -1;
     } else {                                    // self pair A: hull b on side A, hull a on side B
         int ha_, hb_;
@@ -1728,7 +1739,7 @@ HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
         PoseF Po = object_pose_u(c, A);
         PoseF Pb = object_pose_u(c, ob);
         if (kind == 1) {
-            h1 = ho + j; P1 = Po; b1 = A; h2 = m.static_hull[B]; P2 = static_pose(m, B); b2 = -1; k2 = -100 - B;
+            h1 = ho + j; P1 = Po; b1 = A; h2 = m.static_hull[B]; P2 = static_pose(c, B); b2 = -1; k2 = -100 - B;
             // the piece's own sphere against the exact box (the oracle's per-piece near_box; for a one-hull object
             // the broad phase's test again)
             f3 cp = Po.p + qrot(Po.q, scale3(c, A, ld3(m.hull_center[h1])));
@@ -1744,7 +1755,7 @@ HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
     } else if (kind == 4) {
         int Lk = m.hull_link[A];
         h1 = A; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = m.static_hull[B];
-        P2 = static_pose(m, B); b2 = -1; k2 = -100 - B;
+        P2 = static_pose(c, B); b2 = -1; k2 = -100 - B;
     } else {
         // self-collision pair (a, b), a < b: hull b on side A, hull a on side B (normal from a to b). Consecutive pairs
         // share hull a, so side B's world vertices / planes stay in the scratch and a pair whose side-A sphere clears one
@@ -2005,7 +2016,7 @@ HD void detect(SimCtx& c) {
                         float rb;
                         if (kind == 1) {
                             int hb = m.static_hull[B];
-                            Pb = static_pose(m, B); cl = ld3(m.hull_center[hb]); rb = m.hull_radius[hb];
+                            Pb = static_pose(c, B); cl = ld3(m.hull_center[hb]); rb = m.hull_radius[hb];
                         } else if (kind == 2) {
                             int pb = c.o[B].pool;
                             Pb = object_pose(c, B); cl = ld3(m.pool_center[pb]); rb = m.pool_radius[pb];
@@ -2025,7 +2036,7 @@ HD void detect(SimCtx& c) {
                 int Lk = m.hull_link[A];
                 cand = m.link_table_collide[Lk] != 0;
                 if (cand) {
-                    PoseF Pst = static_pose(m, B);
+                    PoseF Pst = static_pose(c, B);
                     int hs = m.static_hull[B];
                     f3 ch = ld3(s.lp[Lk]) + qrot(ldq(s.lq[Lk]), ld3(m.hull_center[A]));
                     f3 ct = Pst.p + qrot(Pst.q, ld3(m.hull_center[hs]));

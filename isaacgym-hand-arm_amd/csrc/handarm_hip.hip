@@ -211,6 +211,8 @@ __device__ __forceinline__ void load_env(SimCtx& c, const ha_state_t& st, int en
     }
     for (int b = lane; b < MAXB; b += 64) s.u.pd.cforce[b][0] = s.u.pd.cforce[b][1] = s.u.pd.cforce[b][2] = 0.0f;
     if (lane < HA_CSTAT) s.cst[lane] = 0;
+    if (m.posed_actor >= 0 && lane < 8)          // the actor carrying posed statics (v14): p[3], pad, q[4]
+        s.sb[lane] = lane == 3 ? 0.0f : st.root_state[((size_t)env * A + m.posed_actor) * 13 + (lane < 3 ? lane : lane - 1)];
     wsync();
 }
 
@@ -924,6 +926,12 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
         model->n_dofs + 6 * params->n_objects > MAXV || model->n_bodies > MAXB ||
         model->n_static < 0 || model->n_static > HA_MAX_STATIC || model->n_pool < 1 || model->n_pool > HA_MAX_POOL ||
         model->n_hulls > HA_MAX_HULLS)
+        return HA_E_MODEL;
+    // posed statics (v14): one carrying actor per env; the throw bucket is the actor in the goal slot
+    if (model->posed_actor < -1 || model->posed_actor >= model->n_actors) return HA_E_MODEL;
+    for (int k = 0; k < model->n_static; k++)
+        if (model->static_posed[k] && model->posed_actor < 0) return HA_E_MODEL;
+    if (params->task == HA_TASK_ALLEGRO_KUKA && params->ak_subtask == 2 && model->posed_actor != model->actor_goal)
         return HA_E_MODEL;
     // every hull must fit the family's narrow-phase scratch (ColLayout)
     int col_v = (fam == HA_TASK_ALLEGRO_KUKA || fam == HA_TASK_ALLEGRO_HAND) ? FamPhys<HA_TASK_ALLEGRO_HAND>::colv

@@ -24,7 +24,7 @@ BIN_ASSET = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "
 MAX_LINKS, MAX_DOFS, MAX_HULLS, MAX_VERTS, MAX_PLANES = 32, 24, 128, 8192, 16384
 MAX_EDGES, MAX_LOOP, MAX_FACE_LOOP = 16384, 32768, 21
 MAX_POOL, MAX_OBJ, MAX_INIT_POSES, MAX_SPLINE_PIECES, N_SPLINES = 32, 8, 4, 8, 8
-MAX_STATIC = 10
+MAX_STATIC = 16
 MAX_FIXED_BODIES = 8
 MAX_MPAIRS = 192
 MAX_SELF_PAIRS = 512
@@ -90,6 +90,7 @@ class HaModel(C.Structure):
         ("loop_v", arr(C.c_uint8, MAX_LOOP)),
         ("dof_friction", arr(f32, MAX_DOFS)),
         ("n_self_pairs", i32), ("self_pair", arr(C.c_uint16, MAX_SELF_PAIRS)), ("hull_obb", arr(f32, MAX_HULLS, 12)),  # v12
+        ("posed_actor", i32), ("static_posed", arr(i32, MAX_STATIC)),                                                 # v14
     ]
 
 
@@ -338,7 +339,9 @@ def _topology(h):
 NO_TABLE_CONTACT = {"shoulder_link", "upper_arm_link"}
 
 
-def build_model(scene, pool_names=None):
+def build_model(scene, pool_names=None, posed=None):
+    """posed: name of a group in scene["posed_statics"] (the AllegroKuka throw "bucket") whose convex pieces become
+    statics carried by a per-env actor (ha_model_t v14 posed_actor / static_posed)."""
     m = HaModel()
     rob = scene["robot"]
     links, dofs = rob["links"], rob["dofs"]
@@ -368,6 +371,10 @@ def build_model(scene, pool_names=None):
     table = scene.get("table")
     # static boxes: the table (static 0) and any extra pieces (table-with-hole walls, bin parts)
     statics = ([table] if table else []) + list(scene.get("statics", []))
+    n_world = len(statics)
+    group = scene["posed_statics"][posed] if posed else None
+    if group:
+        statics += group["pieces"]
     assert len(statics) <= MAX_STATIC
     # object pieces: the convex decomposition when the scene has one ("hulls", tools/convex_decomp.py), else the hull
     obj_hulls = [o.get("hulls") or [o["hull"]] for o in objects]
@@ -435,6 +442,8 @@ def build_model(scene, pool_names=None):
         m.static_pos[k][:] = st["pos"]
         m.static_quat[k][:] = st["quat"]
         m.static_half[k][:] = st["half_extents"]
+        m.static_posed[k] = int(k >= n_world)
+    m.posed_actor = scene["layout"][group["actor"]] if group else -1
     if table:
         m.table_hull = first_static
         m.table_pos[:] = table["pos"]
@@ -646,7 +655,8 @@ ALLEGRO_KUKA_TASK = dict(
     DEFAULT_TASK, task=TASK_ALLEGRO_KUKA, num_actions=23, n_objects=1, subtask="regrasping",
     dt=0.01667, substeps=2, control_freq_inv=1, solver_iters=8,          # AllegroKuka.yaml:27,210-223
     contact_margin=0.002, max_depen_vel=1000.0,                          # :226-229
-    episode_length={"regrasping": 300, "reorientation": 600}, success_steps={"regrasping": 30, "reorientation": 1},
+    episode_length={"regrasping": 300, "reorientation": 600, "throw": 300},
+    success_steps={"regrasping": 30, "reorientation": 1, "throw": 5},
     reset_position_noise=(0.1, 0.1, 0.02), reset_dof_pos_noise_fingers=0.1, reset_dof_pos_noise_arm=0.1,
     reset_dof_vel_noise=0.5, force_scale=2.0, force_prob_range=(0.001, 0.1), force_decay=0.99,
     force_decay_interval=0.08, lifting_rew_scale=20.0, lifting_bonus=300.0, lifting_bonus_threshold=0.15,
@@ -667,7 +677,27 @@ ALLEGRO_KUKA_TASK = dict(
     num_arm_dofs=7,
 )
 AK_KEYPOINTS = {"regrasping": [[0, 0, 0]],                                          # allegro_kuka_regrasping.py:46-48
-                "reorientation": [[1, 1, 1], [1, 1, -1], [-1, -1, 1], [-1, -1, -1]]}   # reorientation.py:48-54
+                "reorientation": [[1, 1, 1], [1, 1, -1], [-1, -1, 1], [-1, -1, -1]],   # reorientation.py:48-54
+                "throw": [[0, 0, 0]]}                                               # allegro_kuka_throw.py:47-49
+AK_SUBTASKS = {"regrasping": 0, "reorientation": 1, "throw": 2}                     # ha_params_t.ak_subtask
+# the throw bucket's creation pose: allegro_pose (0, 0.8, 0) + (-0.6, -1, 0.45) in gymapi.Vec3 float32 arithmetic
+# (allegro_kuka_base.py:606-607,632, allegro_kuka_throw.py:68-72)
+AK_BUCKET_POSE = (_f32(0.0 - 0.6), _f32(_f32(0.8) - 1.0), _f32(0.0 + 0.45))
+# env/<subtask>.yaml values beyond episodeLength / successSteps: throw has no random forces, a fixed 7.5 cm tolerance
+# and small cuboids only (env/throw.yaml:5-18; the object family is the scene's "object_dims_throw")
+AK_SUBTASK_CFG = {"throw": dict(force_scale=0.0, success_tolerance=0.075, target_success_tolerance=0.075)}
+
+
+def posed_group(task, cfg):
+    """The group of posed statics (ha_model_t v14) a task's model carries: the AllegroKuka throw bucket."""
+    if task == TASK_ALLEGRO_KUKA and (cfg or {}).get("subtask", ALLEGRO_KUKA_TASK["subtask"]) == "throw":
+        return "bucket"
+    return None
+
+
+def kuka_object_dims(scene, c):
+    """The subtask's cuboid family (allegro_kuka_base.py:485-512 with its with* flags)."""
+    return scene.get("object_dims_" + c["subtask"], scene["object_dims"])
 
 
 def kuka_tolerance_scalars(success_tolerance, c):
@@ -683,7 +713,7 @@ def kuka_tolerance_scalars(success_tolerance, c):
 def kuka_env_tables(num_envs, scene, c):
     """Per-env object scales (env i gets object_dims[i % len], allegro_kuka_base.py:687-707) and keypoint
     offsets (:708-715, python double, rounded once by to_torch)."""
-    dims = scene["object_dims"]
+    dims = kuka_object_dims(scene, c)
     kps = AK_KEYPOINTS[c["subtask"]]
     scales = np.zeros((num_envs, 1, 3), np.float32)
     offs = np.zeros((num_envs, 4, 3), np.float32)
@@ -705,6 +735,8 @@ def build_params(cfg=None, task=None):
     want = task if task is not None else (cfg or {}).get("task")
     c = dict(ALLEGRO_TASK if want == TASK_ALLEGRO_HAND else (ALLEGRO_KUKA_TASK if want == TASK_ALLEGRO_KUKA
                                                              else DEFAULT_TASK))
+    if want == TASK_ALLEGRO_KUKA:
+        c.update(AK_SUBTASK_CFG.get((cfg or {}).get("subtask", c["subtask"]), {}))
     if cfg:
         c.update(cfg)
     p = HaParams()
@@ -766,7 +798,7 @@ def _kuka_params(p, c):
     sub = c["subtask"]
     assert sub in AK_KEYPOINTS, sub
     kps = AK_KEYPOINTS[sub]
-    p.ak_subtask = 0 if sub == "regrasping" else 1
+    p.ak_subtask = AK_SUBTASKS[sub]
     p.ak_num_keypoints = len(kps)
     for j, kp in enumerate(kps):
         p.ak_keypoints[j][:] = kp
@@ -809,6 +841,6 @@ def _kuka_params(p, c):
     p.ak_palm_link = names.index(c["palm_link"])                    # find_asset_rigid_body_index (:642-644)
     p.ak_fingertip_links[:] = [names.index(n) for n in c["fingertip_links"]]
     # object_rb_masses: the object of env 0 (allegro_kuka_base.py:734-735), box of density 400
-    d0 = scene["object_dims"][0]
+    d0 = kuka_object_dims(scene, c)[0]
     p.ak_object_rb_mass = 400.0 * (c["object_base_size"] * d0[0]) * (c["object_base_size"] * d0[1]) * \
         (c["object_base_size"] * d0[2])

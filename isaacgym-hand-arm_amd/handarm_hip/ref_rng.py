@@ -77,18 +77,27 @@ class KukaDraws:
 
     The per-step force selection ``torch.rand(N) < random_force_prob`` is made here, with the reference's CPU
     arithmetic and the host copy of random_force_prob; the kernel gets the decision as draw 0 (selected) or 1
-    (not selected) in slot 71, which its ``u < prob`` test reproduces for every prob in (0, 1)."""
+    (not selected) in slot 71 (2 G + 53), which its ``u < prob`` test reproduces for every prob in (0, 1)."""
 
     def __init__(self, num_envs, subtask, prob_range, force_scale):
         self.n = num_envs
+        self.subtask = subtask
         self.regrasping = subtask == "regrasping"
+        self.G = 10 if subtask == "throw" else 9        # draws of one reset_target_pose (ak_task.h ak_goal_draws)
         self.prob_range = prob_range
         self.force_scale = force_scale
         _, self.prob = kuka_force_prob(num_envs, prob_range)          # __init__ draw (:323-327)
 
     def _target(self, D, ids, base):
-        """reset_target_pose -> _reset_target (regrasping.py:76-98 / reorientation.py:104-128)."""
+        """reset_target_pose -> _reset_target (regrasping.py:76-98 / reorientation.py:104-128 / throw.py:85-103)."""
         k = len(ids)
+        if self.subtask == "throw":
+            D[ids, base:base + 1] = torch_rand_float(-1.0, 1.0, (k, 1))     # left / right of the table
+            D[ids, base + 1:base + 2] = torch_rand_float(0, 0.4, (k, 1))
+            D[ids, base + 2:base + 3] = torch_rand_float(-1.0, 0.7, (k, 1))
+            D[ids, base + 3:base + 4] = torch_rand_float(0.0, 1.0, (k, 1))
+            self._object(D, ids, base + 4)
+            return
         D[ids, base:base + 3] = torch_rand_float(0.0, 1.0, (k, 3))
         if self.regrasping:
             self._object(D, ids, base + 3)                              # reset_object_pose (:1196-1220)
@@ -109,22 +118,23 @@ class KukaDraws:
         goal_ids = torch.as_tensor(reset_goal).nonzero(as_tuple=False).squeeze(-1)
         env_ids = torch.as_tensor(reset).nonzero(as_tuple=False).squeeze(-1)
         self._target(D, goal_ids, 0)                                    # reset_target_pose(reset_goal_env_ids)
+        G = self.G
         if len(env_ids) > 0:                                            # reset_idx(reset_env_ids), :1246-1353
-            self._target(D, env_ids, 9)
-            self._object(D, env_ids, 18)
+            self._target(D, env_ids, G)
+            self._object(D, env_ids, 2 * G)
             u, p = kuka_force_prob(len(env_ids), self.prob_range)
-            D[env_ids, 24] = u
+            D[env_ids, 2 * G + 6] = u
             self.prob[env_ids] = p
-            D[env_ids, 25:48] = torch_rand_float(0.0, 1.0, (len(env_ids), 23))
-            D[env_ids, 48:71] = torch_rand_float(-1.0, 1.0, (len(env_ids), 23))
+            D[env_ids, 2 * G + 7:2 * G + 30] = torch_rand_float(0.0, 1.0, (len(env_ids), 23))
+            D[env_ids, 2 * G + 30:2 * G + 53] = torch_rand_float(-1.0, 1.0, (len(env_ids), 23))
         raw = {"force_u": None}
         if forces and self.force_scale > 0.0:                           # :1399-1410
             u = torch.rand(N, device="cpu")
             sel = (u < self.prob).nonzero()
             g = torch.randn((len(sel), 1, 3), device="cpu")
-            D[:, 71] = 1.0
-            D[sel[:, 0], 71] = 0.0
-            D[sel[:, 0], 72:75] = g.reshape(len(sel), 3)
+            D[:, 2 * G + 53] = 1.0
+            D[sel[:, 0], 2 * G + 53] = 0.0
+            D[sel[:, 0], 2 * G + 54:2 * G + 57] = g.reshape(len(sel), 3)
             raw["force_u"] = u
         return D, raw
 

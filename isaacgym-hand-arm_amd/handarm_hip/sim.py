@@ -37,7 +37,7 @@ class HandArmSim:
         self.task = task
         default_scene = {HM.TASK_ALLEGRO_HAND: HM.ALLEGRO_ASSET, HM.TASK_ALLEGRO_KUKA: HM.KUKA_ASSET}.get(task, HM.ASSET)
         self.scene = scene if scene is not None else HM.load_scene(default_scene)
-        self.model = HM.build_model(self.scene, pool_names)
+        self.model = HM.build_model(self.scene, pool_names, posed=HM.posed_group(task, task_cfg))
         self.params, self.cfg = HM.build_params(task_cfg, task=task)
         self.num_envs = num_envs
         self.n_obj = self.params.n_objects
@@ -145,6 +145,10 @@ class HandArmSim:
         root = self.t["root_state"].view(N, self.num_actors, 13)
         root[:, self.model.actor_object0, 0:3] = init
         root[:, self.model.actor_goal, 0:3] = self.t["goal_state"][:, 0:3]
+        if p.ak_subtask == 2:
+            # throw: the bucket actor at bucket_pose = allegro_pose + (-0.6, -1, 0.45) in gymapi.Vec3 (float32) until
+            # the first reset places it (allegro_kuka_throw.py:68-72)
+            root[:, self.model.actor_goal, 0:3] = torch.tensor(HM.AK_BUCKET_POSE, device=self.device)
         root[:, self.model.actor_table, 0:3] = torch.tensor(list(self.model.table_pos), device=self.device)
         self.t["task_scalars"].copy_(torch.from_numpy(HM.kuka_tolerance_scalars(c["success_tolerance"], c)))
         self.t["reset_buf"].fill_(1)

@@ -1,11 +1,13 @@
 """AllegroKuka (KUKA iiwa7 + Allegro hand, 23 DOF) with the IsaacGymEnvs VecTask surface, backed by
 libhandarm_hip.
 
-Drop-in for tasks/allegro_kuka/allegro_kuka_regrasping.py:38 and allegro_kuka_reorientation.py:41
-(registered as "AllegroKukaRegrasping" / "AllegroKukaReorientation" in tasks/__init__.py, and as "AllegroKuka"
-with the subtask picked by cfg env.subtask like tasks/__init__.py's resolver). Config cfg/task/AllegroKuka.yaml +
+Drop-in for tasks/allegro_kuka/allegro_kuka_regrasping.py:38, allegro_kuka_reorientation.py:41 and
+allegro_kuka_throw.py:39 (registered as "AllegroKukaRegrasping" / "AllegroKukaReorientation" /
+"AllegroKukaThrow" in tasks/__init__.py, and as "AllegroKuka" with the subtask picked by cfg env.subtask like
+tasks/__init__.py's resolver). Config cfg/task/AllegroKuka.yaml +
 env/<subtask>.yaml: observationType "full_state" (93 + 6 x keypoints floats, clamped to +-10), procedurally
-generated cuboids (947 sizes, env i gets size i % 947), random object forces, tolerance curriculum.
+generated cuboids (947 sizes, env i gets size i % 947; throw: 654 small ones), random object forces, tolerance
+curriculum. Throw adds the bucket (a per-env fixed-base actor whose convex pieces the physics collides with).
 
 One fused kernel per step (ha_task_step -> ak_step_kernel): goal resets, reset_idx, hand/arm targets, random
 forces, 1 x 2 physics substeps, refresh, full_state observations, compute_kuka_reward and resets. The host only
@@ -69,6 +71,11 @@ class AllegroKuka:
                 env.get("randomizeObjectDimensions", True) is False:
             raise NotImplementedError("only the AllegroKuka.yaml defaults for relative control, privileged actions "
                                       "and object dimensions are implemented")
+        family = (True, False, False) if sub == "throw" else (True, True, True)      # env/throw.yaml:15-18
+        if tuple(bool(env.get(k, d)) for k, d in zip(("withSmallCuboids", "withBigCuboids", "withSticks"), family)) \
+                != family:
+            raise NotImplementedError(f"the {sub} subtask's cuboid family (withSmallCuboids / withBigCuboids / "
+                                      f"withSticks = {family}) is the one implemented")
         self.num_environments = int(env.get("numEnvs", 8192))
         self.num_agents = 1
         task_cfg = dict(task=HM.TASK_ALLEGRO_KUKA, subtask=sub, seed=int(cfg.get("seed", 42)))
@@ -88,6 +95,10 @@ class AllegroKuka:
         self.tcfg = self.sim.cfg
         p = self.sim.params
         self.subtask = sub
+        if sub == "throw":
+            # the bucket actors (allegro_kuka_throw.py:77-82): root_state rows n_actors e + actor 3, rigid body 26
+            self.bucket_object_indices = torch.arange(self.num_environments, device=sim_device) * \
+                self.sim.model.n_actors + self.sim.model.actor_goal
         self.clip_obs = float(env.get("clipObservations", np.inf))
         self.clip_actions = float(env.get("clipActions", np.inf))
         self.max_episode_length = p.max_episode_length
@@ -317,3 +328,11 @@ class AllegroKukaRegrasping(AllegroKuka):
 class AllegroKukaReorientation(AllegroKuka):
     def __init__(self, cfg, *args, **kwargs):
         super().__init__(cfg, *args, subtask="reorientation", **kwargs)
+
+
+class AllegroKukaThrow(AllegroKuka):
+    """allegro_kuka_throw.py:39-124: throw the cuboid into a bucket placed left or right of the table each goal.
+    The bucket is actor 3 (root_state rows 4 e + 3, rigid body 26) and its convex pieces collide as statics carried
+    by that actor (ha_model_t v14); bucket_object_indices names its actors like the reference's."""
+    def __init__(self, cfg, *args, **kwargs):
+        super().__init__(cfg, *args, subtask="throw", **kwargs)

@@ -13,8 +13,20 @@ from oracle import f32
 
 F = np.float32
 D, NARM = 23, 7
-DRAW_GOAL, DRAW_RESET_GOAL, DRAW_OBJ, DRAW_FORCE_PROB, DRAW_DOF, DRAW_VEL = 0, 9, 18, 24, 25, 48
-DRAW_FORCE_U, DRAW_FORCE_N = 71, 72
+DRAW_GOAL = 0
+
+
+def goal_draws(p):
+    """Draws of one reset_target_pose (ak_task.h ak_goal_draws): 9, throw 10 (bucket side, offset, y, z + the
+    object's 6)."""
+    return 10 if p.ak_subtask == 2 else 9
+
+
+def draw_slots(p):
+    """ak_task.h AK_DRAW_*: reset goal, object, force prob, dof, vel, force u, force n."""
+    G = goal_draws(p)
+    return dict(RESET_GOAL=G, OBJ=2 * G, FORCE_PROB=2 * G + 6, DOF=2 * G + 7, VEL=2 * G + 30, FORCE_U=2 * G + 53,
+                FORCE_N=2 * G + 54)
 
 
 def quat_rotate(q, v):
@@ -153,6 +165,23 @@ def _reset_object_pose(p, st, ids, dr, k0):
 
 
 def _reset_target_pose(p, st, ids, dr, k0):
+    if p.ak_subtask == 2:
+        # throw (allegro_kuka_throw.py:85-103): the bucket (actor 3) left / right of the table, goal 5 cm above it
+        lr = dr[ids, k0]
+        x = np.where(lr > 0, F(0.5), F(-0.5)).astype(F) + (np.sign(lr) * dr[ids, k0 + 1]).astype(F)
+        y, z = dr[ids, k0 + 2], dr[ids, k0 + 3]
+        st["root"][ids, 3, 0] = x
+        st["root"][ids, 3, 1] = y
+        st["root"][ids, 3, 2] = z
+        st["goal"][ids, 0] = x
+        st["goal"][ids, 1] = y
+        st["goal"][ids, 2] = z + F(0.05)
+        _reset_object_pose(p, st, ids, dr, k0 + 4)
+        st["ts"][ids, HM.AK_LIFTED] = 0
+        st["reset_goal"][ids] = 0
+        st["ts"][ids, HM.AK_NEAR_GOAL] = 0
+        st["ts"][ids, HM.AK_CLOSEST_KP] = -1
+        return
     lo, size = np.array(p.ak_target_lo, F), np.array(p.ak_target_size, F)
     tgt = lo + dr[ids, k0:k0 + 3] * size
     st["goal"][ids, 0:3] = tgt
@@ -174,22 +203,23 @@ def pre(p, st, actions, dr, lo, up):
     """pre_physics_step (allegro_kuka_base.py:1355-1414) on st (dict of numpy arrays, updated in place)."""
     goal_ids = np.nonzero(st["reset_goal"])[0]
     reset_ids = np.nonzero(st["reset"])[0]
+    ds = draw_slots(p)
     if len(goal_ids):
         _reset_target_pose(p, st, goal_ids, dr, DRAW_GOAL)
     if len(reset_ids):
         ids = reset_ids
-        _reset_target_pose(p, st, ids, dr, DRAW_RESET_GOAL)
+        _reset_target_pose(p, st, ids, dr, ds["RESET_GOAL"])
         st["ts"][ids, HM.AK_RB_FORCE:HM.AK_RB_FORCE + 3] = 0
-        _reset_object_pose(p, st, ids, dr, DRAW_OBJ)
+        _reset_object_pose(p, st, ids, dr, ds["OBJ"])
         llo, lhi = np.log(F(p.ak_force_prob_lo)), np.log(F(p.ak_force_prob_hi))
-        st["ts"][ids, HM.AK_FORCE_PROB] = np.exp((llo - lhi) * dr[ids, DRAW_FORCE_PROB] + lhi)
+        st["ts"][ids, HM.AK_FORCE_PROB] = np.exp((llo - lhi) * dr[ids, ds["FORCE_PROB"]] + lhi)
         default = np.array(list(p.reset_pose)[:D], F)
         dmax, dmin = up - default, lo - default
-        rd = dmin + (dmax - dmin) * dr[ids, DRAW_DOF:DRAW_DOF + D]
+        rd = dmin + (dmax - dmin) * dr[ids, ds["DOF"]:ds["DOF"] + D]
         coeff = np.array([p.ak_dof_noise_arm] * NARM + [p.ak_dof_noise_fingers] * (D - NARM), F)
         pos = default + coeff * rd
         st["dof"][ids, :, 0] = pos
-        st["dof"][ids, :, 1] = F(p.ak_dof_vel_noise) * dr[ids, DRAW_VEL:DRAW_VEL + D]
+        st["dof"][ids, :, 1] = F(p.ak_dof_vel_noise) * dr[ids, ds["VEL"]:ds["VEL"] + D]
         st["targets"][ids] = pos
         st["progress"][ids] = 0
         st["reset"][ids] = 0
@@ -215,10 +245,12 @@ def pre(p, st, actions, dr, lo, up):
     cur[:, :NARM] = np.maximum(np.minimum(t, up[:NARM]), lo[:NARM])
     st["targets"][:] = cur
     # random forces (:1399-1414)
+    if p.ak_force_scale <= 0:                 # forceScale 0 (throw): no decay, no draws (:1399)
+        return
     rf = st["ts"][:, HM.AK_RB_FORCE:HM.AK_RB_FORCE + 3]
     rf *= F(p.ak_force_decay_step)
-    sel = dr[:, DRAW_FORCE_U] < st["ts"][:, HM.AK_FORCE_PROB]
-    rf[sel] = (dr[sel, DRAW_FORCE_N:DRAW_FORCE_N + 3] * F(p.ak_object_rb_mass)) * F(p.ak_force_scale)
+    sel = dr[:, ds["FORCE_U"]] < st["ts"][:, HM.AK_FORCE_PROB]
+    rf[sel] = (dr[sel, ds["FORCE_N"]:ds["FORCE_N"] + 3] * F(p.ak_object_rb_mass)) * F(p.ak_force_scale)
 
 
 def timeout(p, progress, reset):

@@ -155,6 +155,7 @@ typedef struct {
     const float* dr;                /* this env's DR row (HA_DR_*) or NULL (ha_physics.h SimCtx::dr) */
     float* pcm;                     /* this env's persistent-manifold records (ha_state_t.contact_cache) or NULL */
     int cst[HA_CSTAT];              /* contact_stats of this call sequence (ha_physics.h EnvLDS::cst) */
+    float sb[8];                    /* the posed-static actor's pose (v14, ha_physics.h EnvLDS::sb): p, pad, q */
 } env_t;
 
 static float body_friction(const hao_handle h, const env_t* e, int b);
@@ -775,7 +776,18 @@ static int near_box(const float* half, pose_t Pb, v3 c, float r) {
     float dz = fmaxf(fabsf(pl.z) - half[2], 0.0f);
     return dx * dx + dy * dy + dz * dz <= r * r;
 }
-static pose_t static_pose(const ha_model_t* m, int k) { pose_t P = {ld3(m->static_pos[k]), ldq(m->static_quat[k])}; return P; }
+/* static k's world pose; a static carried by the env's posed actor composes that actor's pose with its own (v14,
+ * ha_physics.h static_pose) */
+static pose_t static_pose(const ha_model_t* m, const env_t* e, int k) {
+    pose_t P = {ld3(m->static_pos[k]), ldq(m->static_quat[k])};
+    if (m->static_posed[k]) {
+        v3 bp = ld3(e->sb);
+        qt bq = ldq(e->sb + 4);
+        pose_t R = {add(bp, qrot(bq, P.p)), qmul(bq, P.q)};
+        P = R;
+    }
+    return P;
+}
 
 /* The pairs in the kernel's order (ha_physics.h pair_desc: per object its ground, statics, later objects and link hulls,
  * then link hulls x statics, then the self pairs), each first through the kernel's broad phase (ha_physics.h detect:
@@ -819,7 +831,7 @@ static int detect(const hao_handle h, env_t* e, contact_t* out) {
         }
         pidx++;
         for (int st = 0; st < NS; st++, pidx++) {
-            pose_t Pst = static_pose(m, st);
+            pose_t Pst = static_pose(m, e, st);
             int hs = m->static_hull[st];
             v3 dc = sub(co, add(Pst.p, qrot(Pst.q, ld3(m->hull_center[hs]))));
             float rr = ro + m->hull_radius[hs] + mg;
@@ -875,7 +887,7 @@ static int detect(const hao_handle h, env_t* e, contact_t* out) {
         v3 ch = add(PL.p, qrot(PL.q, ld3(m->hull_center[k])));
         for (int st = 0; st < NS; st++, pidx++) {
             if (!m->link_table_collide[L]) continue;
-            pose_t Pst = static_pose(m, st);
+            pose_t Pst = static_pose(m, e, st);
             int hs = m->static_hull[st];
             v3 dc = sub(ch, add(Pst.p, qrot(Pst.q, ld3(m->hull_center[hs]))));
             float rr = m->hull_radius[k] + m->hull_radius[hs] + mg;
@@ -1231,6 +1243,12 @@ static void load_env(const hao_handle h, const ha_state_t* S, int env, env_t* e,
     memset(e->dforce, 0, sizeof(e->dforce));
     memset(e->cst, 0, sizeof(e->cst));
     e->pcm = S->contact_cache ? S->contact_cache + (size_t)env * h->pcm_slots * HA_PCM_REC : NULL;
+    memset(e->sb, 0, sizeof(e->sb));
+    if (m->posed_actor >= 0) {
+        const float* r = S->root_state + (env * A + m->posed_actor) * 13;
+        e->sb[0] = r[0]; e->sb[1] = r[1]; e->sb[2] = r[2];
+        e->sb[4] = r[3]; e->sb[5] = r[4]; e->sb[6] = r[5]; e->sb[7] = r[6];
+    }
 }
 
 static void store_env(const hao_handle h, ha_state_t* S, int env, env_t* e) {

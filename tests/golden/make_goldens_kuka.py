@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Golden vectors for the AllegroKuka tasks (config C2) by RUNNING THE REFERENCE
-(tasks/allegro_kuka/allegro_kuka_base.py + allegro_kuka_regrasping.py / allegro_kuka_reorientation.py).
+(tasks/allegro_kuka/allegro_kuka_base.py + allegro_kuka_regrasping.py / allegro_kuka_reorientation.py /
+allegro_kuka_throw.py).
 
 Run in the build container only (needs /root/reference):  python tests/golden/make_goldens_kuka.py
 Writes ``kuka_*.npz`` (data only) next to this file.
@@ -43,7 +44,7 @@ from handarm_hip import model as HM  # noqa: E402
 
 REF_CFG = "/root/reference/isaacgymenvs/cfg/task"
 SCENE = HM.KUKA_ASSET
-CLS = {"regrasping": "AllegroKukaRegrasping", "reorientation": "AllegroKukaReorientation"}
+CLS = {"regrasping": "AllegroKukaRegrasping", "reorientation": "AllegroKukaReorientation", "throw": "AllegroKukaThrow"}
 L, OBJ_BODY, TABLE_BODY, GOAL_BODY, NB = 24, 24, 25, 26, 27
 
 
@@ -150,6 +151,7 @@ def make_task(sub, N):
     t.allegro_hand_indices = torch.arange(N) * 4
     t.object_indices = torch.arange(N) * 4 + 1
     t.goal_object_indices = torch.arange(N) * 4 + 3
+    t.bucket_object_indices = torch.arange(N) * 4 + 3        # throw: the bucket is actor 3 (allegro_kuka_throw.py:77)
     t.set_actor_root_state_object_indices = []
     # __init__ tensors after VecTask.__init__ (:262-389)
     t.dof_state = torch.zeros(N * 23, 2)
@@ -304,8 +306,9 @@ def steps(sub, N=32, T=8, seed=2):
     torch.manual_seed(seed)          # seeded before the task is built: __init__'s random_force_prob draw is the
     mod, base, t, _, _ = make_task(sub, N)     # first draw of the stream (ref_rng.KukaDraws replays it)
     prob_init = t.random_force_prob.clone()
-    model = HM.build_model(HM.load_scene(SCENE))
     params, cfg = HM.build_params({"subtask": sub}, task=HM.TASK_ALLEGRO_KUKA)
+    model = HM.build_model(HM.load_scene(SCENE), posed=HM.posed_group(HM.TASK_ALLEGRO_KUKA, cfg))
+    G = 10 if sub == "throw" else 9                  # draws of one reset_target_pose (ak_task.h ak_goal_draws)
     st = HostState(N, model=model, params=params)
     st["object_scale"][:] = t.object_scales.numpy()[:, None, :]
     st["collision_enabled"][:] = 1
@@ -338,7 +341,7 @@ def steps(sub, N=32, T=8, seed=2):
     def rand(*a, **kw):
         v = real_rand(*a, **kw)
         if cur["phase"] == "force":
-            draws[cur["step"], :, 71] = v.numpy()
+            draws[cur["step"], :, 2 * G + 53] = v.numpy()
             cur["u"] = v
         elif cur["in_reset"]:
             put(cur["ids"], v)                       # random_force_prob draw of reset_idx
@@ -350,7 +353,7 @@ def steps(sub, N=32, T=8, seed=2):
             idx = (cur["u"] < t.random_force_prob).nonzero().reshape(-1).numpy()
             if len(idx) == 0:
                 return v
-            draws[cur["step"], idx, 72:75] = v.reshape(len(idx), 3).numpy()
+            draws[cur["step"], idx, 2 * G + 54:2 * G + 57] = v.reshape(len(idx), 3).numpy()
         return v
     o_rtp, o_rt, o_rop, o_ri, o_set = (t.reset_target_pose, t._reset_target, t.reset_object_pose, t.reset_idx,
                                        t.set_actor_root_state_tensor_indexed)
@@ -368,13 +371,13 @@ def steps(sub, N=32, T=8, seed=2):
 
     def rop(env_ids):
         if cur["in_reset"] and not cur["in_target"]:
-            cursor[env_ids.numpy()] = 18             # reset_idx's own reset_object_pose (AK_DRAW_OBJ)
+            cursor[env_ids.numpy()] = 2 * G          # reset_idx's own reset_object_pose (AK_DRAW_OBJ)
         cur["ids"] = env_ids
         return o_rop(env_ids)
 
     def ri(env_ids):
         cur["in_reset"], cur["ids"] = True, env_ids
-        cursor[env_ids.numpy()] = 9                  # AK_DRAW_RESET_GOAL
+        cursor[env_ids.numpy()] = G                  # AK_DRAW_RESET_GOAL
         try:
             return o_ri(env_ids)
         finally:
@@ -441,6 +444,7 @@ def steps(sub, N=32, T=8, seed=2):
 
 def object_dims_and_curriculum():
     mod, base, t, scales, names = make_task("regrasping", 4)
+    _, _, _, scales_throw, names_throw = make_task("throw", 4)     # env/throw.yaml: small cuboids only
     utils = refload.load("isaacgymenvs.tasks.allegro_kuka.allegro_kuka_utils")
     cases, results = [], []
     for last, frame, succ, tol in [(0, 2999, 5.0, 0.075), (0, 3000, 2.0, 0.075), (0, 3000, 3.5, 0.075),
@@ -451,14 +455,15 @@ def object_dims_and_curriculum():
         cases.append([last, frame, succ, tol])
         results.append([new_tol, new_last] + obj.tolist())
     np.savez_compressed(os.path.join(HERE, "kuka_object_dims.npz"), scales=scales,
-                        names=np.array(names), curriculum_in=np.array(cases, np.float64),
+                        names=np.array(names), scales_throw=scales_throw, names_throw=np.array(names_throw),
+                        curriculum_in=np.array(cases, np.float64),
                         curriculum_out=np.array(results, np.float64))
 
 
 if __name__ == "__main__":
     refload.install()
     object_dims_and_curriculum()
-    for sub in ("regrasping", "reorientation"):
+    for sub in sys.argv[1:] or ("regrasping", "reorientation", "throw"):
         obs_reward(sub)
         steps(sub)
     print("wrote kuka_object_dims.npz, kuka_obs_reward_*.npz, kuka_steps_*.npz")

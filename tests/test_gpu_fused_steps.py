@@ -14,6 +14,7 @@ import pytest
 import torch
 
 from handarm_hip import model as HM
+from oracle import kuka_oracle as KO
 from tests import scenes, step_chains
 
 pytestmark = pytest.mark.gpu
@@ -110,20 +111,30 @@ def _kuka_window(sub, n, scene_fn, act_fn, resets=True, force_prob=0.5, seed=11)
     push_all(sim, hs)
     orc = Oracle(m, p, n)
     fired = 0
+    ds, G = KO.draw_slots(p), KO.goal_draws(p)
     for t in range(K):
         act = act_fn(rng, n)
         draws = rng.uniform(0, 1, (n, HM.DRAW_STRIDE)).astype(np.float32)
         # the U[-1, 1) slots (ak_task.h AK_DRAW_*): regrasping's object position noise after each goal target, the
-        # reset_idx object position noise and the DOF velocity draws (reorientation draws a goal quaternion there)
-        slots = ((3, 6), (12, 15), (18, 21), (48, 71)) if sub == "regrasping" else ((18, 21), (48, 71))
+        # reset_idx object position noise and the DOF velocity draws (reorientation draws a goal quaternion there;
+        # throw the bucket side first and the object's position noise after the bucket's 4 draws)
+        slots = {"regrasping": ((3, 6), (G + 3, G + 6)), "reorientation": (),
+                 "throw": ((0, 1), (4, 7), (G, G + 1), (G + 4, G + 7))}[sub]
+        slots += ((ds["OBJ"], ds["OBJ"] + 3), (ds["VEL"], ds["VEL"] + 23))
         for k0, k1 in slots:
             draws[:, k0:k1] = rng.uniform(-1, 1, (n, k1 - k0))
-        draws[:, 72:75] = rng.standard_normal((n, 3))
+        if sub == "throw":                          # bucket offset U[0, 0.4), y U[-1, 0.7)
+            for k in (1, G + 1):
+                draws[:, k] *= 0.4
+            for k in (2, G + 2):
+                draws[:, k] = draws[:, k] * 1.7 - 1.0
+        draws[:, ds["FORCE_N"]:ds["FORCE_N"] + 3] = rng.standard_normal((n, 3))
         hs["actions"][:] = act
         hs["reset_draws"][:] = draws
         put(sim, "actions", act)
         put(sim, "reset_draws", draws)
-        fired += int((draws[:, 71] < hs["task_state"][:, HM.AK_FORCE_PROB]).sum())
+        if p.ak_force_scale > 0:
+            fired += int((draws[:, ds["FORCE_U"]] < hs["task_state"][:, HM.AK_FORCE_PROB]).sum())
         sim.task_step(HM.FLAG_REPLAY_DRAWS)
         obs, rew, timeout = step_chains.kuka_step(orc, hs, p, lo, up, scalars, draws)
         tag = f"kuka {sub} step {t}"
@@ -156,6 +167,40 @@ def test_kuka_fused_step_with_physics_matches_oracle_chain(sub):
     sim, hs, fired = _kuka_window(sub, 128, _kuka_random_scene, _uniform_actions)
     assert fired > 128 // 4, "the random-force branch must fire"
     stats_match(sim, hs, f"kuka {sub}", self_frac=0.25)
+
+
+def kuka_bucket_at_hand_scene(sim, hs, lo, up, seed=5):
+    """Throw: each env's bucket hangs where its hand is (the palm 8-18 cm above the bucket's floor, a few cm off its
+    axis), the cuboid inside the bucket: palm / finger hulls against the bucket's wall and floor pieces (link-static
+    pairs on the posed statics) and the cuboid against them, in every env at its own bucket pose."""
+    from oracle.oracle_lib import Oracle
+    n, p, m = sim.num_envs, sim.params, sim.model
+    _kuka_random_scene(sim, hs, lo, up)
+    rng = np.random.default_rng(seed)
+    probe = hs.copy()
+    Oracle(m, p, n).simulate(probe, 1)
+    palm = probe["rigid_body_state"].reshape(n, m.n_bodies, 13)[:, m.body_robot0 + p.ak_palm_link]
+    rs = hs["root_state"].reshape(n, m.n_actors, 13)
+    b = rs[:, m.actor_goal]
+    b[:] = 0
+    b[:, 0:3] = palm[:, 0:3] - np.array([0, 0, 1], np.float32) * rng.uniform(0.08, 0.18, (n, 1)) + \
+        np.concatenate([rng.uniform(-0.04, 0.04, (n, 2)), np.zeros((n, 1))], 1)
+    b[:, 6] = 1
+    rs[:, m.actor_object0, 0:3] = b[:, 0:3] + np.array([0.0, -0.002, 0.06], np.float32)
+    rs[:, m.actor_object0, 7:13] = 0
+    hs["goal_state"][:, 0:3] = b[:, 0:3] + np.array([0, 0, 0.05], np.float32)
+
+
+def test_kuka_throw_fused_step_with_physics_matches_oracle_chain():
+    """ak_step_kernel on the throw subtask: the bucket's 13 convex pieces as statics carried by actor 3 (ha_model_t
+    v14), hanging at each env's hand with the cuboid inside; goal and env resets in the first step move the buckets
+    of half the envs (allegro_kuka_throw.py:85-103), so the next steps collide with the new poses. 3 fused steps
+    against kuka_oracle.pre -> physics_oracle -> kuka_oracle.post, bit-identical physics."""
+    need_gpu()
+    sim, hs, fired = _kuka_window("throw", 128, kuka_bucket_at_hand_scene, _uniform_actions)
+    assert fired == 0 and sim.model.n_static == 14
+    g = stats_match(sim, hs, "kuka throw")
+    assert (g[:, 3] > 0).mean() > 0.9, "contacts with the bucket pieces in most envs"
 
 
 def kuka_closed_hand_scene(sim, hs, lo, up, seed=0):

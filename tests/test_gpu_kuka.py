@@ -1,6 +1,6 @@
 """GPU parity for the AllegroKuka tasks (config C2), through the C ABI:
 * task math (observe / reward / resets / targets / random forces / task state) against the reference-generated
-  goldens (bit-exact done masks and counters; float tolerances stated per check), both subtasks;
+  goldens (bit-exact done masks and counters; float tolerances stated per check), the three subtasks;
 * physics against the C oracle after one gym.simulate, with per-env cuboid dimensions and object forces
   (1-ulp-sensitivity-calibrated tolerance, as for Ur5Sih / AllegroHand);
 * the VecTask class over a full-size (4096-env) episode.
@@ -50,7 +50,7 @@ def get(sim, name):
     return sim.t[name].cpu().numpy()
 
 
-@pytest.mark.parametrize("sub", ["regrasping", "reorientation"])
+@pytest.mark.parametrize("sub", ["regrasping", "reorientation", "throw"])
 def test_kuka_observe_and_reward_against_reference_goldens(sub):
     d = np.load(os.path.join(G, f"kuka_obs_reward_{sub}.npz"))
     S, N = d["rew"].shape
@@ -71,7 +71,7 @@ def test_kuka_observe_and_reward_against_reference_goldens(sub):
         np.testing.assert_allclose(get(sim, "task_state")[:, :32], d["task_state"][s][:, :32], rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("sub", ["regrasping", "reorientation"])
+@pytest.mark.parametrize("sub", ["regrasping", "reorientation", "throw"])
 def test_kuka_step_with_resets_replayed_against_reference_goldens(sub):
     """The fused step kernel without physics: goal + env resets and random forces from the recorded reference
     draws, hand/arm targets, FK refresh, progress, full_state observations, reward, done, timeout."""
@@ -155,7 +155,7 @@ def test_kuka_link_contacts_spill_rows_match_oracle():
     scenes.assert_physics_bit_identical(sim, st, n, tag="kuka link contacts")
 
 
-@pytest.mark.parametrize("sub", ["regrasping", "reorientation"])
+@pytest.mark.parametrize("sub", ["regrasping", "reorientation", "throw"])
 def test_kuka_vectask_episode_at_full_size(sub):
     """C2 size (4096 envs): first step resets every env, then 150 random-action steps through the fused kernel;
     everything finite, observations within the +-10 clamp, cuboids stay in the scene, resets happen."""
@@ -164,7 +164,7 @@ def test_kuka_vectask_episode_at_full_size(sub):
     n = 4096
     env = isaacgym_task_map["AllegroKuka"]({"env": {"numEnvs": n, "subtask": sub}}, "cuda:0", "cuda:0")
     obs = env.reset()["obs"]
-    assert obs.shape == (n, 99 if sub == "regrasping" else 117)
+    assert obs.shape == (n, 117 if sub == "reorientation" else 99)
     g = torch.Generator(device="cuda:0").manual_seed(7)
     resets = 0
     for step in range(150):
@@ -306,3 +306,54 @@ def test_kuka_dropped_cuboids_on_the_gpu():
     drop_schedule(n, scales, lambda: orc.simulate(st, 1), lambda: st["root_state"].reshape(n, 4, 13),
                   lambda: st["dof_state"].reshape(n, 23, 2))
     scenes.assert_physics_bit_identical(sim, st, n, tag="kuka drop schedule")
+
+
+def test_throw_bucket_catches_cuboids_bit_identical_to_oracle():
+    """Throw physics on the kernel (ak_simulate_kernel): cuboids of the throw family dropped into buckets hanging at
+    per-env places of the arena (the posed statics read each env's actor-3 root state) come to rest on the bucket
+    floor, and after 60 calls every physics output is bit-identical to the C oracle; then half the buckets move
+    (as _reset_target does between calls) and the next 10 calls stay bit-identical."""
+    from oracle.oracle_lib import HostState, Oracle
+    n = 64
+    sim = make_sim(n, subtask="throw")
+    m = sim.model
+    assert m.n_static == 14 and m.posed_actor == m.actor_goal
+    lo = np.array(m.dof_lower[:23], np.float32)
+    up = np.array(m.dof_upper[:23], np.float32)
+    st = HostState(n, model=m, params=sim.params)
+    scales = get(sim, "object_scale")
+    scenes.fill_kuka_scene(st, n, lo, up, list(sim.params.reset_pose), scales, list(m.table_pos), seed=3)
+    rng = np.random.default_rng(3)
+    root = st["root_state"].reshape(n, 4, 13)
+    side = np.where(np.arange(n) % 2 == 0, 1.0, -1.0)
+    root[:, 3] = 0
+    root[:, 3, 0] = side * rng.uniform(0.55, 0.9, n)
+    root[:, 3, 1] = rng.uniform(-1.0, 0.7, n)
+    root[:, 3, 2] = rng.uniform(0.0, 1.0, n)
+    root[:, 3, 6] = 1
+    root[:, 1] = 0
+    root[:, 1, 0:3] = root[:, 3, 0:3] + np.c_[rng.uniform(-0.02, 0.02, (n, 2)), np.full(n, 0.15)]
+    q = rng.standard_normal((n, 4)).astype(np.float32) * [0.1, 0.1, 0.1, 1.0]
+    root[:, 1, 3:7] = q / np.linalg.norm(q, axis=1, keepdims=True)
+    for k in HM.STATE_FIELDS:
+        if k not in ("stats", "term_sums", "task_state", "task_scalars"):
+            put(sim, k, st[k])
+    orc = Oracle(m, sim.params, n)
+    sim.simulate(60)
+    orc.simulate(st, 60)
+    scenes.assert_physics_bit_identical(sim, st, n, tag="throw bucket drop")
+    obj = get(sim, "root_state").reshape(n, 4, 13)[:, 1]
+    b = root[:, 3, 0:3]
+    dz = obj[:, 2] - b[:, 2]
+    inside = np.hypot(obj[:, 0] - b[:, 0], obj[:, 1] - b[:, 1] + 0.002016) < 0.1
+    print(f"throw bucket drop: {inside.mean():.2f} inside, height above the bucket origin "
+          f"{np.quantile(dz, [0, 0.5, 1]).round(4).tolist()}")
+    assert inside.mean() > 0.9 and (dz[inside] > 0.009).all() and (dz[inside] < 0.2).all()
+    root[::2, 3, 0] += 0.4
+    put(sim, "root_state", st["root_state"])
+    sim.simulate(10)
+    orc.simulate(st, 10)
+    scenes.assert_physics_bit_identical(sim, st, n, tag="throw buckets moved")
+    obj2 = get(sim, "root_state").reshape(n, 4, 13)[:, 1]
+    high = root[::2, 3, 2] > 0.1                                # (a bucket on the ground has nothing to fall from)
+    assert high.sum() > 8 and (obj2[::2, 2][high] < obj[::2, 2][high] - 0.05).all()   # the moved buckets' cuboids fall

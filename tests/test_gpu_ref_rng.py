@@ -62,7 +62,7 @@ def test_ur5sih_reference_rng_episodes():
     assert e == E - 1
 
 
-@pytest.mark.parametrize("sub", ["regrasping", "reorientation"])
+@pytest.mark.parametrize("sub", ["regrasping", "reorientation", "throw"])
 def test_kuka_reference_rng_steps(sub):
     need_gpu()
     from handarm_hip.tasks import AllegroKuka

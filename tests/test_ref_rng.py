@@ -60,14 +60,18 @@ def _kuka(sub):
     kd = RR.KukaDraws(N, sub, tuple(c["force_prob_range"]), float(c["force_scale"]))
     np.testing.assert_array_equal(kd.prob.numpy(), d["random_force_prob_init"])
     fired = 0
+    fu = 2 * kd.G + 53                      # the force-selection slot (ak_task.h AK_DRAW_FORCE_U)
     for s in range(T):
         D, raw = kd.step(d["reset_in"][s], d["reset_goal_in"][s])
         D = D.numpy()
-        np.testing.assert_array_equal(D[:, :71], d["draws"][s][:, :71], err_msg=f"{sub} step {s} reset draws")
-        np.testing.assert_array_equal(raw["force_u"].numpy(), d["draws"][s][:, 71])
-        sel = D[:, 71] == 0.0
-        np.testing.assert_array_equal(sel, d["draws"][s][:, 71] < kd.prob.numpy())
-        np.testing.assert_array_equal(D[sel, 72:75], d["draws"][s][sel, 72:75])
+        np.testing.assert_array_equal(D[:, :fu], d["draws"][s][:, :fu], err_msg=f"{sub} step {s} reset draws")
+        if c["force_scale"] <= 0:           # throw: no force draws at all (allegro_kuka_base.py:1399)
+            assert raw["force_u"] is None and (d["draws"][s][:, fu:] == 0).all()
+            continue
+        np.testing.assert_array_equal(raw["force_u"].numpy(), d["draws"][s][:, fu])
+        sel = D[:, fu] == 0.0
+        np.testing.assert_array_equal(sel, d["draws"][s][:, fu] < kd.prob.numpy())
+        np.testing.assert_array_equal(D[sel, fu + 1:fu + 4], d["draws"][s][sel, fu + 1:fu + 4])
         fired += int(sel.sum())
         # the task_state row the reference left after this step holds its random_force_prob
         np.testing.assert_array_equal(kd.prob.numpy(), d["task_state"][s][:, HM.AK_FORCE_PROB])
@@ -80,6 +84,10 @@ def test_kuka_draws_reproduce_reference_regrasping():
 
 def test_kuka_draws_reproduce_reference_reorientation():
     assert _kuka("reorientation") > 0
+
+
+def test_kuka_draws_reproduce_reference_throw():
+    assert _kuka("throw") == 0              # forceScale 0 (env/throw.yaml)
 
 
 def test_allegro_draws_reproduce_reference():

@@ -29,12 +29,12 @@ def test_uniform01_hash_on_the_2_pow_minus_24_grid():
 
 def _kuka_setup(n, sub="regrasping"):
     scene = HM.load_scene(HM.KUKA_ASSET)
-    m = HM.build_model(scene)
     p, cfg = HM.build_params({"task": HM.TASK_ALLEGRO_KUKA, "subtask": sub}, task=HM.TASK_ALLEGRO_KUKA)
+    m = HM.build_model(scene, posed=HM.posed_group(HM.TASK_ALLEGRO_KUKA, cfg))
     return scene, m, p, cfg
 
 
-@pytest.mark.parametrize("sub", ["regrasping", "reorientation"])
+@pytest.mark.parametrize("sub", ["regrasping", "reorientation", "throw"])
 def test_kuka_chain_step_runs_with_resets_and_forces(sub):
     n = 16
     scene, m, p, cfg = _kuka_setup(n, sub)

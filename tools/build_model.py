@@ -569,11 +569,12 @@ KUKA_OUT = os.path.join(os.path.dirname(__file__), "..", "isaacgym-hand-arm_amd"
                         "assets", "kuka_allegro_scene.json")
 
 
-def kuka_object_dims():
+def kuka_object_dims(small=True, big=True, sticks=True):
     """The procedurally generated cuboid family (allegro_kuka/generate_cuboids.py:37-137) as per-axis
     scales of the 0.05 m base cube, in the order envs receive them: file names sorted, then shuffled
     with numpy default_rng(42) (allegro_kuka_base.py:411-428, 485-512). Files of the four generators
-    share one directory, so equal names overwrite each other exactly as on disk."""
+    share one directory, so equal names overwrite each other exactly as on disk. The flags are the config's
+    withSmallCuboids / withBigCuboids / withSticks (AllegroKuka.yaml:77-79; throw: small only, env/throw.yaml)."""
     files = set()
 
     def gen(scales, min_volume, max_volume, filters):
@@ -598,9 +599,12 @@ def kuka_object_dims():
         s = sorted(s)
         return s[2] <= s[0] * 3 or s[2] <= s[1] * 3
     gen([100], 1.0, 1.0, [])                                                          # default cube
-    gen([100, 50, 66, 75, 90, 110, 125, 150, 175, 200, 250, 300], 1.0, 2.5, [])       # withSmallCuboids
-    gen([100, 125, 150, 200, 250, 300, 350], 2.5, 15.0, [thin])                       # withBigCuboids
-    gen([100, 50, 75, 200, 300, 400, 500, 600], 2.5, 6.0, [thin, non_elongated])     # withSticks
+    if small:
+        gen([100, 50, 66, 75, 90, 110, 125, 150, 175, 200, 250, 300], 1.0, 2.5, [])   # withSmallCuboids
+    if big:
+        gen([100, 125, 150, 200, 250, 300, 350], 2.5, 15.0, [thin])                   # withBigCuboids
+    if sticks:
+        gen([100, 50, 75, 200, 300, 400, 500, 600], 2.5, 6.0, [thin, non_elongated])  # withSticks
     names = sorted(files)
     scales = [[float(t) / 100 for t in os.path.splitext(f)[0].split("_")[2:]] for f in names]
     pairs = list(zip(names, scales))
@@ -649,6 +653,75 @@ def main_kuka():
     print(f"kuka_allegro: links={L} dofs={len(robot['dofs'])} hulls={len(link_hulls)} "
           f"objects dims={len(scene['object_dims'])} bodies={[l['name'] for l in robot['links']]} "
           f"dof order={[d['name'] for d in robot['dofs']]} -> {KUKA_OUT} ({os.path.getsize(KUKA_OUT)} B)")
+
+
+BUCKET_OBJ = os.path.join(REF, "assets", "urdf", "objects", "meshes", "bucket.obj")
+
+
+def bucket_pieces():
+    """bucket.urdf (allegro_kuka_throw.py:51-66; the reference V-HACDs its mesh) as convex pieces in the bucket's
+    frame: meshes/bucket.obj is a 12-sided vessel (outer wall from the bottom ring r 0.082 at z 0 to the rim r 0.12
+    at z 0.198, inner wall from the floor ring r 0.0705 at z 0.0099 to r 0.1035 at the rim). Pieces: the 12 wall
+    sectors (the outer bottom, rim and inner rim vertices at two neighbouring angles, with the floor ring's vertices
+    brought down to the bottom plane z 0, so a sector's underside is the flat bottom and no sector face points down
+    into the bucket's inside: an object on the floor next to the wall is pushed up and inward, never down) and the
+    floor: the floor ring's 12-gon prism from the floor top (z 0.0099) down to 3 cm under the bottom, so that a
+    cuboid falling in at up to ~5 m/s cannot cross the slab's mid-plane within one substep (a 1 cm slab let the
+    fastest drops tunnel). Each piece's hull is stored about its box centre, with the box as the static's half
+    extents (the broad phase's sphere-near-box test needs the box to contain the hull)."""
+    v, _ = load_obj(BUCKET_OBJ)
+    ctr = np.array([0.0, v[:, 1].min() + 0.5 * (v[:, 1].max() - v[:, 1].min()), 0.0])
+    ctr[0] = 0.5 * (v[:, 0].min() + v[:, 0].max())
+    rel = v - ctr
+    r = np.hypot(rel[:, 0], rel[:, 1])
+    ang = np.round(np.degrees(np.arctan2(rel[:, 1], rel[:, 0])) / 30.0).astype(int) % 12
+    zlo, zhi = v[:, 2].min(), v[:, 2].max()
+    rings = {}
+    for name, sel in (("outer_bottom", np.isclose(v[:, 2], zlo, atol=1e-4)),
+                      ("floor", (v[:, 2] > zlo + 1e-3) & (v[:, 2] < zhi - 1e-3)),
+                      ("rim_outer", np.isclose(v[:, 2], zhi, atol=1e-4) & (r > 0.11)),
+                      ("rim_inner", np.isclose(v[:, 2], zhi, atol=1e-4) & (r < 0.11))):
+        idx = np.nonzero(sel)[0]
+        assert len(idx) == 12, (name, len(idx))
+        ring = np.zeros((12, 3))
+        ring[ang[idx]] = v[idx]
+        assert len(set(ang[idx])) == 12, name
+        rings[name] = ring
+    under = rings["floor"].copy()
+    under[:, 2] = zlo - 0.03
+    clouds = [np.concatenate([rings["floor"], under])]
+    base = rings["floor"].copy()
+    base[:, 2] = rings["outer_bottom"][:, 2]
+    wall = dict(rings, floor=base)
+    for i in range(12):
+        j = (i + 1) % 12
+        clouds.append(np.stack([wall[n][k] for n in wall for k in (i, j)]))
+    pieces = []
+    for pts in clouds:
+        lo, hi = pts.min(0), pts.max(0)
+        c = 0.5 * (lo + hi)
+        rec = hull_record(pts - c, MAX_PIECE_VERTS)
+        assert len(rec["verts"]) == len(pts), "every ring vertex is a hull vertex"
+        half = (0.5 * (hi - lo) * (1 + 1e-5) + 1e-6).tolist()
+        pieces.append({"pos": c.tolist(), "quat": [0.0, 0.0, 0.0, 1.0], "half_extents": half, "hull": rec})
+    return pieces
+
+
+def main_throw():
+    """Adds the AllegroKuka throw subtask's data to the committed Kuka scene without rebuilding it: the bucket's
+    convex pieces as statics carried by the actor in the goal slot (allegro_kuka_throw.py:68-82: the bucket is the
+    actor created after the table, actor 3 / body 26 like reorientation's goal), and the throw object family
+    (env/throw.yaml: withSmallCuboids only)."""
+    with open(KUKA_OUT) as f:
+        scene = json.load(f)
+    pieces = bucket_pieces()
+    scene["posed_statics"] = {"bucket": {"actor": "actor_goal", "pieces": pieces,
+                                         "source": "urdf/objects/bucket.urdf (meshes/bucket.obj), floor + 12 sectors"}}
+    scene["object_dims_throw"] = kuka_object_dims(small=True, big=False, sticks=False)
+    with open(KUKA_OUT, "w") as f:
+        json.dump(scene, f, indent=None, separators=(",", ":"))
+    print(f"throw: bucket {len(pieces)} pieces, verts {[len(p['hull']['verts']) for p in pieces]}, "
+          f"object dims {len(scene['object_dims_throw'])} -> {KUKA_OUT}")
 
 
 def main():
@@ -921,6 +994,8 @@ def main_dof_friction():
 
 
 if __name__ == "__main__":
+    if "--throw" in sys.argv:
+        sys.exit(main_throw())
     if "--dof-friction" in sys.argv:
         sys.exit(main_dof_friction())
     if "--pointclouds" in sys.argv:
