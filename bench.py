@@ -573,6 +573,10 @@ def main():
                            "convex pieces, dropped at init)"}
     h = records[head]
     task, envs, label = CONFIGS[head]
+    if task == "allegro_kuka" and args.subtask != "regrasping":
+        label = label.replace("AllegroKuka regrasping", f"AllegroKuka {args.subtask}")
+        data[task] = data[task].replace("random object forces on", "random object forces off" if args.subtask ==
+                                        "throw" else "random object forces on")
     envs = h["envs_per_gpu"]
     out = {
         "metric": METRIC, "value": h["value"], "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,

@@ -65,6 +65,12 @@ __host__ __device__ constexpr int task_contact_chunks() {
 }
 template <int FAM>
 __host__ __device__ constexpr bool task_overflow() { return FAM != FAM_UR5SIH_CLUTTER; }
+// persistent contact manifolds (v13) are compiled into every family but AllegroHand: with them its kernel needs 76 B/lane
+// of register spills (44 without) and measured 4.8 -> 5.0 ms per C3 step with twice the HBM traffic; its hand closes on
+// the cube and on itself every step, so few of its pairs keep a record long enough to pay back
+template <int FAM>
+__host__ __device__ constexpr bool task_pcm() { return FAM != HA_TASK_ALLEGRO_HAND; }
+static inline bool family_pcm(int fam) { return fam != HA_TASK_ALLEGRO_HAND; }
 // clutter family: 1 recomputes the object blocks of the contact rows in registers from the contact entries in the
 // rows phase and at every PGS fetch (PhysCfg RC) instead of storing them in the env's global row area. Measured on
 // C5 (round 3): 22.1 -> 30.8 ms per step, the ~140 VALU per fetch cost more than the stored rows' traffic, which the
@@ -96,6 +102,10 @@ __host__ __device__ constexpr bool task_overflow() { return FAM != FAM_UR5SIH_CL
 // AllegroKuka holds a full chunk (21) since round 3: with 2 LDS link slots its rows still fit in front of S in the
 // phase union (9.3 KB env block, 16 workgroups per CU); C2 over capacity 1.3% -> 0.09% of substeps for +2.7%
 // step time. AllegroHand stays at 12: 21 in the compact layout cost +9% (0.12%), the dense rows do not fit.
+// Waves per SIMD: AllegroKuka asks for 3 since round 5 (168 VGPRs, 8 B/lane scratch): with the self pass and the
+// persistent manifolds it needed 120 B/lane of spills at 4, whose scratch write-backs were 43% of its HBM traffic
+// (48.8 -> 27.8 KB per env) and cost more than the fourth wave won (C2 kernel 1.064 -> 1.043 ms,
+// tools/diag/ab_traffic.sh); AllegroHand stays at 4 (16384 envs: the fourth wave per SIMD is worth 10% there).
 #ifndef HA_AK_CONTACTS
 #define HA_AK_CONTACTS 21
 #endif
@@ -103,7 +113,7 @@ __host__ __device__ constexpr bool task_overflow() { return FAM != FAM_UR5SIH_CL
 #define HA_AH_CONTACTS 12
 #endif
 #ifndef HA_AK_WAVES_PER_EU
-#define HA_AK_WAVES_PER_EU 4
+#define HA_AK_WAVES_PER_EU 3
 #endif
 #ifndef HA_AH_WAVES_PER_EU
 #define HA_AH_WAVES_PER_EU 4
@@ -514,6 +524,7 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
         c.pcm = (st.contact_cache && params->pcm_lin_tol > 0.0f) ? st.contact_cache + (size_t)env * slots * HA_PCM_REC
                                                                    : nullptr;
     }
+    if constexpr (!task_pcm<FAM>()) c.pcm = nullptr;
 #ifdef HA_X_NO_PCM     /* A/B builds only: the persistent-manifold code compiled out */
     c.pcm = nullptr;
 #endif
@@ -1003,7 +1014,10 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     h->fam = fam;
     h->h_params = *params;
     h->stat_slots = 1;
-    h->pcm_slots = params->n_objects * (1 + model->n_static + model->n_link_hulls) +
+    // persistent-manifold records (v13): none when the tolerance is off, and none in a family built without them
+    if (params->pcm_lin_tol > 0.0f && !family_pcm(fam)) return HA_E_ARG;
+    h->pcm_slots = params->pcm_lin_tol <= 0.0f ? 0 :
+                   params->n_objects * (1 + model->n_static + model->n_link_hulls) +
                    params->n_objects * (params->n_objects - 1) / 2 + model->n_link_hulls * model->n_static +
                    model->n_self_pairs;
     HIPCHK(hipMalloc(&h->d_model, sizeof(ha_model_t)));

@@ -163,9 +163,12 @@ CONCAVE_POOL = ["031_spoon", "033_spatula", "037_scissors", "042_adjustable_wren
 POOL_WIDE = POOL16 + CONCAVE_POOL
 
 
-def pcm_slots(model, n_obj):
+def pcm_slots(model, n_obj, params=None):
     """Persistent-manifold record slots per env (ha_contact_cache_slots): the broad phase's pair enumeration (per object
-    its ground, statics, later objects and link hulls; then link hulls x statics), then the self pairs."""
+    its ground, statics, later objects and link hulls; then link hulls x statics), then the self pairs; none when the
+    params turn the records off (pcm_lin_tol 0: AllegroHand's default)."""
+    if params is not None and params.pcm_lin_tol <= 0:
+        return 0
     NS, NLH = model.n_static, model.n_link_hulls
     return sum(1 + NS + (n_obj - 1 - o) + NLH for o in range(n_obj)) + NLH * NS + model.n_self_pairs
 
@@ -629,6 +632,7 @@ DEFAULT_TASK = dict(
 ALLEGRO_TASK = dict(
     DEFAULT_TASK, task=TASK_ALLEGRO_HAND, num_actions=16, num_obs=88, n_objects=1,
     dt=0.01667, substeps=2, control_freq_inv=2, solver_iters=8,          # AllegroHand.yaml:23,160-173
+    pcm_lin_tol=0.0, pcm_cos_tol=1.0,        # no persistent manifolds in the AllegroHand family
     link_lin_damping=0.0, link_ang_damping=0.01,                         # allegro_hand.py:231 (linear: default 0)
     contact_margin=0.002, max_depen_vel=1000.0,                          # contact_offset, max_depenetration_velocity
     max_episode_length=600,                                              # episodeLength

@@ -53,7 +53,7 @@ class HostState:
             n_obj = params.n_objects
         if model is not None:       # sizes/layout of the model's task (default: Ur5Sih)
             kw.update(n_links=model.n_links, n_dofs=model.n_dofs, n_actors=model.n_actors, n_bodies=model.n_bodies,
-                      n_pcm_slots=HM.pcm_slots(model, n_obj))
+                      n_pcm_slots=HM.pcm_slots(model, n_obj, params))
         self.spec = HM.state_spec(num_envs, n_obj=n_obj, num_initial_poses=num_initial_poses, **kw)
         self.null = HM.null_fields(params.task if params is not None else HM.TASK_UR5SIH)
         self.arrays = {k: np.zeros(shape, dtype) for k, (shape, dtype) in self.spec.items()}
@@ -83,6 +83,12 @@ class Oracle:
         self.num_envs = num_envs
 
     def simulate(self, st, n_calls=1, begin=0, end=None):
+        # the records this oracle's params use (0 when they turn the persistent manifolds off) must fit the state's
+        # contact_cache rows: a HostState sized for params with the records off has none
+        need = HM.pcm_slots(self.model, self.params.n_objects, self.params)
+        have = st["contact_cache"].shape[1] if st["contact_cache"] is not None else 0
+        if need and have != need:
+            raise ValueError(f"contact_cache has {have} record slots per env, these params use {need}")
         s = st.ctypes()
         self.lib.hao_simulate(self.h, C.byref(s), n_calls, begin, self.num_envs if end is None else end)
 

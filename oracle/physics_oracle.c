@@ -1314,7 +1314,7 @@ hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int nu
        Ur5Sih 4 chunks of 21 (HA_CHUNKS), AllegroKuka 2 chunks of 21 (HA_AK_CONTACTS x HA_AK_CHUNKS), AllegroHand
        4 chunks of 12 (HA_AH_CONTACTS x HA_AH_CHUNKS); hao_set_capacity overrides it for A/B builds */
     h->maxc = params->task == HA_TASK_UR5SIH ? 4 * 21 : (params->task == HA_TASK_ALLEGRO_KUKA ? 2 * 21 : 4 * 12);
-    h->pcm_slots = hao_pcm_slots(model, params->n_objects);
+    h->pcm_slots = params->pcm_lin_tol > 0.0f ? hao_pcm_slots(model, params->n_objects) : 0;
     return h;
 }
 void hao_destroy(hao_handle h) { free(h); }
