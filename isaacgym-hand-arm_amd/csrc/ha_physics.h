@@ -184,9 +184,15 @@ __host__ __device__ inline size_t obj_lds_offset_rows(size_t rows) {
 // and row constants in the env's global area (L2-resident), so the contact capacity grows without LDS. A substep
 // with <= CAP contacts never touches that area; a substep over CAP swaps every chunk's row constants through it.
 template <int ND, int OCAP, int NCH, int KL = 8, int LCH = NCH, int CAP = MAXC, int CV = 64, int CP = 128,
-          int SPLIT = -1, int NG = HA_MAX_GATHER, bool MU = false, bool RC = false, bool OVF = false, bool SELF = false>
+          int SPLIT = -1, int NG = HA_MAX_GATHER, bool MU = false, bool RC = false, bool OVF = false, bool SELF = false,
+          bool PACK = false>
 struct PhysCfg {
     static constexpr int nd = ND, ocap = OCAP, nch = NCH;
+    // packed PGS passes (the clutter family): the contacts that touch no robot link are solved four at a time, one
+    // per 16-lane row, in passes of contacts on disjoint objects (ha_physics.h substep, "free passes"); their
+    // object-block rows must all be in the env's global row area
+    static constexpr bool pack = PACK;
+    static constexpr int max_passes = CAP * NCH;
     // the family's robot collides with itself (ha_model_t v12 self pairs; the Allegro families). Without it the
     // self-pair pass is not compiled (its registers would count against every family)
     static constexpr bool selfc = SELF;
@@ -241,6 +247,8 @@ struct PhysCfg {
     static_assert(!ovf || !rc, "overflow chunks with recomputed object blocks");
     static_assert(NG == 0 || NG == HA_MAX_GATHER, "gather buffer: HA_MAX_GATHER points or none");
     static_assert(CP >= 8, "sat_planes reads plane slots 0..7 of the narrow-phase scratch");
+    static_assert(!PACK || (SPLIT != 0 && OCAP > HA_SPLIT_ABOVE_OCAP && LCH == 0 && !RC && !OVF && NCH > 1),
+                  "packed passes: split rows, every object-block row in the global area, RK in LDS");
 };
 // bytes of the constraint rows proper, then (several contact chunks only) the per-row PGS constants of every
 // chunk (impulse, target velocity, 1/diag, friction, two Delassus entries: 6 floats x MAXR x chunks), which the
@@ -252,7 +260,8 @@ __host__ __device__ constexpr size_t pc_rowdata_bytes() {
 }
 template <class PC>
 __host__ __device__ constexpr size_t pc_rows_bytes() {
-    return pc_rowdata_bytes<PC>() + (PC::nch > 1 && !PC::ovf ? 6 * sizeof(float) * (size_t)PC::rk_stride : 0);
+    return pc_rowdata_bytes<PC>() + (PC::nch > 1 && !PC::ovf ? 6 * sizeof(float) * (size_t)PC::rk_stride : 0) +
+           (PC::pack ? sizeof(uint32_t) * (size_t)PC::max_passes : 0);      // the free passes (4 contact bytes each)
 }
 // S ~ M^-1 (factor_inverse), D x D at stride D, sized for the family's DOF count: at the end of the union
 // (minv_in_union) or after it
@@ -488,6 +497,14 @@ HD void wave_sum_rows3(float& a, float& b, float& c) {
     a = a + dpp_row_f<0x142, 0xA>(0.0f, a); b = b + dpp_row_f<0x142, 0xA>(0.0f, b); c = c + dpp_row_f<0x142, 0xA>(0.0f, c);
     a = a + dpp_row_f<0x143, 0xC>(0.0f, a); b = b + dpp_row_f<0x143, 0xC>(0.0f, b); c = c + dpp_row_f<0x143, 0xC>(0.0f, c);
     a = lane63(a); b = lane63(b); c = lane63(c);
+}
+// three 16-lane row sums (the first four steps of wave_sum_rows3): every lane of a row gets its row's
+// ((x0+x1)+(x2+x3)) + ((x4+x5)+(x6+x7)) ... = (Q0+Q1)+(Q2+Q3), the oracle's row_dot16
+HD void row_sum3(float& a, float& b, float& c) {
+    a += dpp_f<0xB1>(a); b += dpp_f<0xB1>(b); c += dpp_f<0xB1>(c);
+    a += dpp_f<0x4E>(a); b += dpp_f<0x4E>(b); c += dpp_f<0x4E>(c);
+    a += dpp_f<0x141>(a); b += dpp_f<0x141>(b); c += dpp_f<0x141>(c);
+    a += dpp_f<0x140>(a); b += dpp_f<0x140>(b); c += dpp_f<0x140>(c);
 }
 
 // ----------------------------------------------------------------------------- kinematics
@@ -2544,6 +2561,49 @@ HD void substep(SimCtx& c, float hdt) {
         if (ch < LCH) delassus_chunk(ch, std::true_type{});
         else delassus_chunk(ch, std::false_type{});
     }
+    // ---- free passes (PhysCfg PACK): the contacts that touch no robot link, packed four per pass on pairwise disjoint
+    //      objects by a greedy scan in contact order (each pass takes the lowest-index remaining contacts whose objects
+    //      the pass does not hold yet: physics_oracle.c packed_passes). A pass is four contact bytes (0xFF: none), in
+    //      the union after RK. Lane i holds contacts i and 64 + i; one ballot per pick
+    int npass = 0;
+    uint32_t* PASS = nullptr;
+    if constexpr (PC::pack) {
+        PASS = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(RK) + 6 * sizeof(float) * (size_t)PC::rk_stride);
+        int o00 = -1, o01 = -1, o10 = -1, o11 = -1;
+        if (lane < nc) {
+            int a_, b_;
+            ct_ab(c, lane, a_, b_);
+            o00 = (a_ >= 0 && a_ < 100) ? a_ : -1;
+            o01 = (b_ >= 0 && b_ < 100) ? b_ : -1;
+        }
+        if (CAP * NCH > 64 && lane + 64 < nc) {
+            int a_, b_;
+            ct_ab(c, lane + 64, a_, b_);
+            o10 = (a_ >= 0 && a_ < 100) ? a_ : -1;
+            o11 = (b_ >= 0 && b_ < 100) ? b_ : -1;
+        }
+        uint64_t rem0 = __ballot(lane < nc) & ~lmask0;
+        uint64_t rem1 = CAP * NCH > 64 ? __ballot(lane + 64 < nc) & ~lmask1 : 0ull;
+        while (rem0 | rem1) {
+            uint32_t objm = 0u, pk = 0xFFFFFFFFu;
+            uint64_t cand0 = rem0, cand1 = rem1;
+            for (int k = 0; k < 4 && (cand0 | cand1); k++) {
+                int ci = cand0 ? __ffsll((unsigned long long)cand0) - 1 : 64 + __ffsll((unsigned long long)cand1) - 1;
+                int oa = ci < 64 ? __builtin_amdgcn_readlane(o00, ci) : __builtin_amdgcn_readlane(o10, ci - 64);
+                int ob = ci < 64 ? __builtin_amdgcn_readlane(o01, ci) : __builtin_amdgcn_readlane(o11, ci - 64);
+                objm |= (oa >= 0 ? 1u << oa : 0u) | (ob >= 0 ? 1u << ob : 0u);
+                pk = (pk & ~(0xFFu << (8 * k))) | ((uint32_t)ci << (8 * k));
+                if (ci < 64) rem0 &= ~(1ull << ci);
+                else rem1 &= ~(1ull << (ci - 64));
+                bool t0 = (o00 >= 0 && ((objm >> o00) & 1u)) || (o01 >= 0 && ((objm >> o01) & 1u));
+                bool t1 = (o10 >= 0 && ((objm >> o10) & 1u)) || (o11 >= 0 && ((objm >> o11) & 1u));
+                cand0 = rem0 & ~__ballot(t0);
+                cand1 = rem1 & ~__ballot(t1);
+            }
+            if (lane == 0) PASS[npass] = pk;
+            npass++;
+        }
+    }
     PROF(4);
     // ---- joint rows, lane d: PD drive (soft implicit spring-damper, |impulse| <= effort h) and the
     //      lower/upper joint limits (hard, unilateral)
@@ -2769,6 +2829,95 @@ HD void substep(SimCtx& c, float hdt) {
             j0n = j0m; j1n = j1m; j2n = j2m; y0n = y0m; y1n = y1m; y2n = y2m;
             h0n = h0m; h1n = h1m; h2n = h2m; g0n = g0m; g1n = g1m; g2n = g2m;
         };
+        // one contact block from its three J.v sums, with the constants and impulses in RK (the packed family): the
+        // serial block's arithmetic (n0, d0, hi, n1 through the Delassus entries, n2), evaluated alike by every lane that
+        // calls it; `writer` stores the new impulses
+        auto solve_rk = [&](int ci, float jv0, float jv1, float jv2, bool writer, float& d0, float& d1, float& d2) {
+            int r0 = 3 * ci;
+            float l0 = rk(0, r0), l1 = rk(0, r0 + 1), l2 = rk(0, r0 + 2);
+            float n0 = l0 - (jv0 - rk(1, r0)) * rk(2, r0);
+            n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
+            d0 = n0 - l0;
+            float hi = rk(3, r0 + 1) * n0;
+            float n1 = l1 - (fmaf(rk(4, r0 + 1), d0, jv1) - rk(1, r0 + 1)) * rk(2, r0 + 1);
+            n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
+            d1 = n1 - l1;
+            float n2 = l2 - (fmaf(rk(5, r0 + 2), d1, fmaf(rk(4, r0 + 2), d0, jv2)) - rk(1, r0 + 2)) * rk(2, r0 + 2);
+            n2 = n2 < -hi ? -hi : (n2 > hi ? hi : n2);
+            d2 = n2 - l2;
+            if (writer) { rk(0, r0) = n0; rk(0, r0 + 1) = n1; rk(0, r0 + 2) = n2; }
+        };
+        if constexpr (PC::pack) {
+            // link contacts: whole-wave blocks in contact order, as the other families solve every contact
+            uint64_t lk0 = lmask0, lk1 = lmask1;
+            while (lk0 | lk1) {
+                int ci = lk0 ? __ffsll((unsigned long long)lk0) - 1 : 64 + __ffsll((unsigned long long)lk1) - 1;
+                if (ci < 64) lk0 &= lk0 - 1ull;
+                else lk1 &= lk1 - 1ull;
+                fetch(ci);
+                advance();
+                float jv0 = j0n * vreg, jv1 = j1n * vreg, jv2 = j2n * vreg;
+                if (VW == 2) {
+                    jv0 = jv0 + h0n * vregh;
+                    jv1 = jv1 + h1n * vregh;
+                    jv2 = jv2 + h2n * vregh;
+                }
+                wave_sum_rows3(jv0, jv1, jv2);
+                float d0, d1, d2;
+                solve_rk(ci, jv0, jv1, jv2, lane == 0, d0, d1, d2);
+                if (d0 != 0.0f) { vreg = fmaf(y0n, d0, vreg); if (VW == 2) vregh = fmaf(g0n, d0, vregh); }
+                if (d1 != 0.0f) { vreg = fmaf(y1n, d1, vreg); if (VW == 2) vregh = fmaf(g1n, d1, vregh); }
+                if (d2 != 0.0f) { vreg = fmaf(y2n, d2, vreg); if (VW == 2) vregh = fmaf(g2n, d2, vregh); }
+            }
+            // free passes: row rr = lane / 16 takes the pass's contact rr, its lane t < 12 the coordinate t of the
+            // contact's compact row (object slot t / 6, entry t % 6). The generalized velocity goes through LDS for the
+            // passes (contacts of one pass share no object, so their lanes read and write disjoint coordinates)
+            if (npass > 0) {
+                if (lane < NV) s.v[lane] = vreg;
+                if (VW == 2 && lane + 64 < NV) s.v[lane + 64] = vregh;
+                wsync();
+                const int rr = lane >> 4, t = lane & 15;
+#pragma unroll 1
+                for (int pp = 0; pp < npass; pp++) {
+                    int ci = (int)((PASS[pp] >> (8 * rr)) & 0xFFu);
+                    bool act = ci != 0xFF;
+                    int idx = -1;
+                    float x0 = 0.0f, x1 = 0.0f, x2 = 0.0f, y0 = 0.0f, y1 = 0.0f, y2 = 0.0f, vv = 0.0f;
+                    if (act && t < 12) {
+                        int a_, b_, so0, so1;
+                        ct_ab(c, ci, a_, b_);
+                        contact_slots(a_, b_, so0, so1);
+                        int o = t < 6 ? so0 : so1;
+                        if (o >= 0) {
+                            idx = D + 6 * o + (t < 6 ? t : t - 6);
+                            const float* Jo = orow_g(3 * ci, false);
+                            const float* Yo = orow_g(3 * ci, true);
+                            auto Jg = glb_f<true>(Jo);
+                            auto Yg = glb_f<true>(Yo);
+                            float j0 = Jg[t], j1 = Jg[OW + t], j2 = Jg[2 * OW + t];
+                            y0 = Yg[t]; y1 = Yg[OW + t]; y2 = Yg[2 * OW + t];
+                            vv = s.v[idx];
+                            x0 = j0 * vv; x1 = j1 * vv; x2 = j2 * vv;
+                        }
+                    }
+                    row_sum3(x0, x1, x2);
+                    if (act) {
+                        float d0, d1, d2;
+                        solve_rk(ci, x0, x1, x2, t == 0, d0, d1, d2);
+                        if (idx >= 0) {
+                            if (d0 != 0.0f) vv = fmaf(y0, d0, vv);
+                            if (d1 != 0.0f) vv = fmaf(y1, d1, vv);
+                            if (d2 != 0.0f) vv = fmaf(y2, d2, vv);
+                            s.v[idx] = vv;
+                        }
+                    }
+                    wsync();
+                }
+                vreg = lane < NV ? s.v[lane] : 0.0f;
+                vregh = (VW == 2 && lane + 64 < NV) ? s.v[lane + 64] : 0.0f;
+                wsync();
+            }
+        } else {
         if (nc > 0) { fetch(0); advance(); }
         if (nc > 1) fetch(1);
 #pragma unroll 1
@@ -2820,6 +2969,7 @@ HD void substep(SimCtx& c, float hdt) {
                 if (d2 != 0.0f) { vreg = fmaf(y2, d2, vreg); if (VW == 2) vregh = fmaf(g2, d2, vregh); }
             }
             if (multi && lane < RPC) rk(0, RPC * ch + lane) = klam;     // swap the impulses out
+        }
         }
     }
     // impulse of global row RPC ch + lane (xfer sits before RK in the union: no overlap)

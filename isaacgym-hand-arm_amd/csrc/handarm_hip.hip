@@ -78,6 +78,12 @@ static inline bool family_pcm(int fam) { return fam != HA_TASK_ALLEGRO_HAND; }
 #ifndef HB_RECOMPUTE
 #define HB_RECOMPUTE 0
 #endif
+// clutter family: the contacts that touch no robot link are solved in packed passes (four contacts on disjoint objects
+// per pass, one per 16-lane row) instead of one whole-wave contact block after another (PhysCfg PACK);
+// the oracle follows the same order for the configurations this family runs (physics_oracle.c packed_pgs)
+#ifndef HB_PACKED_PGS
+#define HB_PACKED_PGS 1
+#endif
 // clutter family: link contacts whose robot blocks stay in LDS (the rest use the global spill rows). 2 slots
 // keep the env block at <= 20 KB, i.e. 8 workgroups per CU (8 slots: 22.8 KB, 7 per CU)
 #ifndef HB_LINK_SLOTS
@@ -175,10 +181,11 @@ using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_c
                         task_compact<FAM>() ? 1 : -1, task_compact<FAM>() ? 0 : HA_MAX_GATHER, task_compact<FAM>(),
                         FAM == FAM_UR5SIH_CLUTTER && HB_RECOMPUTE, task_overflow<FAM>(),
 #ifdef HA_X_NO_SELF     /* A/B timing builds only: the Allegro families without their self-collision pass */
-                        false>;
+                        false,
 #else
-                        FAM == HA_TASK_ALLEGRO_HAND || FAM == HA_TASK_ALLEGRO_KUKA>;
+                        FAM == HA_TASK_ALLEGRO_HAND || FAM == HA_TASK_ALLEGRO_KUKA,
 #endif
+                        FAM == FAM_UR5SIH_CLUTTER && HB_PACKED_PGS>;
 
 
 // ----------------------------------------------------------------------------- state load/store

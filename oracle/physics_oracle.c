@@ -132,6 +132,7 @@ struct hao_s {
     int N, A, B, D, NO;
     int maxc;     /* contact capacity of the device kernel family (handarm_hip.hip family_of) */
     int pcm_slots;/* persistent-manifold record slots per env (hao_pcm_slots) */
+    int packed;   /* packed PGS passes: the clutter family's configurations (Ur5Sih with more than 3 objects) */
 };
 typedef struct hao_s* hao_handle;
 
@@ -992,6 +993,86 @@ static float body_friction(const hao_handle h, const env_t* e, int b) {
     return b >= 100 ? e->dr[HA_DR_LINK_FRIC + (b - 100)] : e->dr[HA_DR_OBJ_FRIC + b];
 }
 
+/* ---- packed PGS passes (ha_physics.h PhysCfg PACK: the clutter family) */
+static int is_link_contact(const contact_t* c) { return c->a >= 100 || c->b >= 100; }
+/* object slots of a contact's compact row (ha_physics.h contact_slots): so0 the lower object index */
+static void contact_slots(int a, int b, int* so0, int* so1) {
+    int oa = (a >= 0 && a < 100) ? a : -1, ob = (b >= 0 && b < 100) ? b : -1;
+    *so0 = oa < 0 ? ob : (ob < 0 ? oa : (oa < ob ? oa : ob));
+    *so1 = (oa >= 0 && ob >= 0) ? (oa < ob ? ob : oa) : -1;
+}
+/* The contacts that touch no link, four per pass on pairwise disjoint objects: each pass takes, in contact order, the
+ * remaining contacts whose objects it does not hold yet (static bodies never conflict). Returns the pass count. */
+static int packed_passes(const contact_t* cs, int nc, int passes[][4]) {
+    int done[MAXC] = {0}, np = 0, left = 0;
+    for (int c = 0; c < nc; c++) {
+        done[c] = is_link_contact(&cs[c]);
+        left += !done[c];
+    }
+    while (left > 0) {
+        unsigned objm = 0u;
+        int k = 0;
+        for (int q = 0; q < 4; q++) passes[np][q] = -1;
+        for (int c = 0; c < nc && k < 4; c++) {
+            if (done[c]) continue;
+            int so0, so1;
+            contact_slots(cs[c].a, cs[c].b, &so0, &so1);
+            if ((so0 >= 0 && ((objm >> so0) & 1u)) || (so1 >= 0 && ((objm >> so1) & 1u))) continue;
+            objm |= (so0 >= 0 ? 1u << so0 : 0u) | (so1 >= 0 ? 1u << so1 : 0u);
+            passes[np][k++] = c;
+            done[c] = 1;
+            left--;
+        }
+        np++;
+    }
+    return np;
+}
+/* One free contact of a pass (ha_physics.h free passes): the J.v sums over the 16-lane row that holds the contact's
+ * compact row (lanes 0-5 object slot 0, 6-11 slot 1, 12-15 empty; a missing slot adds zeros) by the row butterfly
+ * (Q0+Q1)+(Q2+Q3), the block arithmetic of the serial contact, and the updates of its objects' coordinates. */
+static float row_dot16(const float* x) {
+    float Q[4];
+    for (int q = 0; q < 4; q++) Q[q] = (x[4 * q] + x[4 * q + 1]) + (x[4 * q + 2] + x[4 * q + 3]);
+    return (Q[0] + Q[1]) + (Q[2] + Q[3]);
+}
+static void contact_block_packed(const contact_t* ct, int D, const float* J0, const float* J1, const float* J2,
+                                 const float* Y0, const float* Y1, const float* Y2, const float* vt, const float* winv,
+                                 float* lam, float mu, float a10, float a20, float a21, float* v) {
+    int so0, so1, idx[12];
+    contact_slots(ct->a, ct->b, &so0, &so1);
+    float x0[16] = {0}, x1[16] = {0}, x2[16] = {0};
+    for (int t = 0; t < 12; t++) {
+        int o = t < 6 ? so0 : so1;
+        idx[t] = o >= 0 ? D + 6 * o + (t < 6 ? t : t - 6) : -1;
+        if (idx[t] < 0) continue;
+        x0[t] = J0[idx[t]] * v[idx[t]];
+        x1[t] = J1[idx[t]] * v[idx[t]];
+        x2[t] = J2[idx[t]] * v[idx[t]];
+    }
+    float jv0 = row_dot16(x0), jv1 = row_dot16(x1), jv2 = row_dot16(x2);
+    float l0 = lam[0], l1 = lam[1], l2 = lam[2];
+    float n0 = l0 - (jv0 - vt[0]) * winv[0];
+    n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
+    float d0 = n0 - l0;
+    float hi = mu * n0;
+    float n1 = l1 - (fmaf(a10, d0, jv1) - vt[1]) * winv[1];
+    n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
+    float d1 = n1 - l1;
+    float n2 = l2 - (fmaf(a21, d1, fmaf(a20, d0, jv2)) - vt[2]) * winv[2];
+    n2 = n2 < -hi ? -hi : (n2 > hi ? hi : n2);
+    float d2 = n2 - l2;
+    lam[0] = n0; lam[1] = n1; lam[2] = n2;
+    for (int t = 0; t < 12; t++) {
+        int i = idx[t];
+        if (i < 0) continue;
+        float vv = v[i];
+        if (d0 != 0.0f) vv = fmaf(Y0[i], d0, vv);
+        if (d1 != 0.0f) vv = fmaf(Y1[i], d1, vv);
+        if (d2 != 0.0f) vv = fmaf(Y2[i], d2, vv);
+        v[i] = vv;
+    }
+}
+
 static void substep(const hao_handle h, env_t* e, float hdt) {
     const ha_model_t* m = &h->m;
     const ha_params_t* p = &h->p;
@@ -1110,6 +1191,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
         fcoef[d] = m->dof_friction[d];
         lam_fr[d] = 0.0f;
     }
+    int passes[MAXC][4], npass = h->packed ? packed_passes(cs, nc, passes) : 0;
     /* projected Gauss-Seidel, velocity form: joint rows d = 0..D-1 (drive, lower, upper), then the
      * contact rows; v is updated after every row */
     for (int it = 0; it < p->solver_iters; it++) {
@@ -1152,8 +1234,11 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
             }
         }
         /* contact blocks (ha_physics.h): the three J.v reductions of a contact from the same v; the
-         * friction rows see the normal / first-friction update through the block's Delassus entries */
+         * friction rows see the normal / first-friction update through the block's Delassus entries. The packed
+         * configuration (the clutter family) solves the link contacts this way in contact order and then the free
+         * passes (contact_block_packed) */
         for (int c = 0; c < nc; c++) {
+            if (h->packed && !is_link_contact(&cs[c])) continue;
             int r0 = 3 * c;
             float jv0 = wave_dot(R.J[r0], v, NV), jv1 = wave_dot(R.J[r0 + 1], v, NV), jv2 = wave_dot(R.J[r0 + 2], v, NV);
             float l0 = lam[r0], l1 = lam[r0 + 1], l2 = lam[r0 + 2];
@@ -1174,6 +1259,15 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
             if (d1 != 0.0f) for (int k = 0; k < NV; k++) v[k] = fmaf(R.Y[r0 + 1][k], d1, v[k]);
             if (d2 != 0.0f) for (int k = 0; k < NV; k++) v[k] = fmaf(R.Y[r0 + 2][k], d2, v[k]);
         }
+        if (h->packed)
+            for (int q = 0; q < npass; q++)
+                for (int k = 0; k < 4; k++)
+                    if (passes[q][k] >= 0) {
+                        int c = passes[q][k], r0 = 3 * c;
+                        float mu = 0.5f * (body_friction(h, e, cs[c].a) + body_friction(h, e, cs[c].b));
+                        contact_block_packed(&cs[c], D, R.J[r0], R.J[r0 + 1], R.J[r0 + 2], R.Y[r0], R.Y[r0 + 1],
+                                             R.Y[r0 + 2], R.vt + r0, winv + r0, lam + r0, mu, a10[c], a20[c], a21[c], v);
+                    }
     }
     for (int d = 0; d < D; d++) e->dforce[d] = (((dlam[d] + lam_lo[d]) - lam_up[d]) + lam_fr[d]) / hdt;
     /* contact forces per body (net_contact_force): the last substep's forces */
@@ -1315,6 +1409,7 @@ hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int nu
        4 chunks of 12 (HA_AH_CONTACTS x HA_AH_CHUNKS); hao_set_capacity overrides it for A/B builds */
     h->maxc = params->task == HA_TASK_UR5SIH ? 4 * 21 : (params->task == HA_TASK_ALLEGRO_KUKA ? 2 * 21 : 4 * 12);
     h->pcm_slots = params->pcm_lin_tol > 0.0f ? hao_pcm_slots(model, params->n_objects) : 0;
+    h->packed = params->task == HA_TASK_UR5SIH && params->n_objects > 3;      /* handarm_hip.hip family_of */
     return h;
 }
 void hao_destroy(hao_handle h) { free(h); }
