@@ -183,6 +183,7 @@ __host__ __device__ inline size_t obj_lds_offset_rows(size_t rows) {
 // entries, rows, the PGS row constants in registers), and chunks 1..NCH-1 keep their contact entries, constraint rows
 // and row constants in the env's global area (L2-resident), so the contact capacity grows without LDS. A substep
 // with <= CAP contacts never touches that area; a substep over CAP swaps every chunk's row constants through it.
+#define HA_PAIRF_LINK_HULLS 64     /* link hulls the pair face records are sized for */
 template <int ND, int OCAP, int NCH, int KL = 8, int LCH = NCH, int CAP = MAXC, int CV = 64, int CP = 128,
           int SPLIT = -1, int NG = HA_MAX_GATHER, bool MU = false, bool RC = false, bool OVF = false, bool SELF = false,
           bool PACK = false>
@@ -192,7 +193,8 @@ struct PhysCfg {
     // per 16-lane row, in passes of contacts on disjoint objects (ha_physics.h substep, "free passes"); their
     // object-block rows must all be in the env's global row area
     static constexpr bool pack = PACK;
-    static constexpr int max_passes = CAP * NCH;
+    // overflow families pack only the substeps whose contacts fit chunk 0 (rows and row constants lane-resident)
+    static constexpr int max_passes = OVF ? CAP : CAP * NCH;
     // the family's robot collides with itself (ha_model_t v12 self pairs; the Allegro families). Without it the
     // self-pair pass is not compiled (its registers would count against every family)
     static constexpr bool selfc = SELF;
@@ -236,7 +238,13 @@ struct PhysCfg {
     // self-collision families: one byte per self pair, the separating face of the pair's last narrow phase
     static constexpr int spill_selfc = SELF ? HA_MAX_SELF_PAIRS / 4 : 0;
     static constexpr int off_selfc = off_ct + spill_ct;
-    static constexpr int spill_floats = off_selfc + spill_selfc;
+    // every family: one byte per candidate pair of detect's enumeration, the separating face of the pair's last narrow
+    // phase (the self pairs' record, for the other pairs); bounded for up to HA_PAIRF_LINK_HULLS link hulls and
+    // HA_MAX_STATIC statics (ha_create checks the model against it)
+    static constexpr int pairf_bytes = OCAP * (1 + HA_MAX_STATIC + OCAP + HA_PAIRF_LINK_HULLS) + HA_PAIRF_LINK_HULLS * HA_MAX_STATIC;
+    static constexpr int spill_pairf = (pairf_bytes + 3) / 4;
+    static constexpr int off_pairf = off_selfc + spill_selfc;
+    static constexpr int spill_floats = off_pairf + spill_pairf;
     static_assert(ND + 6 * OCAP <= MAXV, "generalized velocity exceeds MAXV");
     static_assert(!split || (KL >= 0 && KL <= CAP * NCH), "LDS link slots must not exceed the contact capacity");
     static_assert(!split || CAP * NCH <= 128, "split rows: <= 128 contacts");
@@ -247,8 +255,9 @@ struct PhysCfg {
     static_assert(!ovf || !rc, "overflow chunks with recomputed object blocks");
     static_assert(NG == 0 || NG == HA_MAX_GATHER, "gather buffer: HA_MAX_GATHER points or none");
     static_assert(CP >= 8, "sat_planes reads plane slots 0..7 of the narrow-phase scratch");
-    static_assert(!PACK || (SPLIT != 0 && OCAP > HA_SPLIT_ABOVE_OCAP && LCH == 0 && !RC && !OVF && NCH > 1),
-                  "packed passes: split rows, every object-block row in the global area, RK in LDS");
+    static_assert(!PACK || (SPLIT != 0 && OCAP > HA_SPLIT_ABOVE_OCAP && !RC && NCH > 1 && (OVF ? CAP <= 21 : LCH == 0)),
+                  "packed passes: split rows; either every object-block row in the global area with RK in LDS, or "
+                  "(overflow chunks) chunk 0's rows in LDS with their constants in registers");
 };
 // bytes of the constraint rows proper, then (several contact chunks only) the per-row PGS constants of every
 // chunk (impulse, target velocity, 1/diag, friction, two Delassus entries: 6 floats x MAXR x chunks), which the
@@ -262,6 +271,11 @@ template <class PC>
 __host__ __device__ constexpr size_t pc_rows_bytes() {
     return pc_rowdata_bytes<PC>() + (PC::nch > 1 && !PC::ovf ? 6 * sizeof(float) * (size_t)PC::rk_stride : 0) +
            (PC::pack ? sizeof(uint32_t) * (size_t)PC::max_passes : 0);      // the free passes (4 contact bytes each)
+}
+// the free passes' list in the phase union: after the row data and (several LDS chunks) RK
+template <class PC>
+__host__ __device__ constexpr size_t pc_pass_offset() {
+    return pc_rowdata_bytes<PC>() + (PC::nch > 1 && !PC::ovf ? 6 * sizeof(float) * (size_t)PC::rk_stride : 0);
 }
 // S ~ M^-1 (factor_inverse), D x D at stride D, sized for the family's DOF count: at the end of the union
 // (minv_in_union) or after it
@@ -347,6 +361,7 @@ struct SimCtx {
     // k: face k of side A, 0xFF: none), and the env's per-pair record of it in its global area (null otherwise)
     int sepf;
     uint8_t* selfc;
+    uint8_t* pairf;         // the candidate pairs' separating-face records (PhysCfg off_pairf; null: off)
     uint32_t* selfm;        // LDS: this substep's self-pair candidates, a bit a pair (selfm_lds_offset; null otherwise)
     // VecTask.step's head and tail folded into the step launch (ha_task_step_io; null / unused otherwise): the caller's
     // raw actions, clamped to +-clip_act where the task reads them (act_at), and a second, clamped copy of obs
@@ -1190,7 +1205,7 @@ HD void collide_hulls(SimCtx& c, int ha, PoseF PA, int hb, PoseF PB, int a, int 
         }
         float scm = wave_max(sc);
         if (scm - scale_radius(c, a, m.hull_radius[ha]) > mg + 1e-3f) {
-            if (c.selfc) {                  // self pair: B's face k separates A, the hint detect_self checks next time
+            if (c.selfc || c.pairf) {       // B's face k separates A: the hint the pair's next detection checks first
                 wave_argmax(sc, kc);
                 c.sepf = 0x80 | kc;
             }
@@ -1995,6 +2010,45 @@ HD void detect_self(SimCtx& c, int npairs) {
     wsync();
 }
 
+// The separating-face record of a one-piece candidate pair (PhysCfg off_pairf): the face its last narrow phase ended on
+// (bit 7 set: a face of side B's hull, else of side A's; the low 7 bits its plane) against the other side's world
+// vertices at the current poses, with the narrow phase's own expressions (world_plane, the posed vertices, dot + d).
+// Separated by more than the margin, the hull SAT would end on a face as well and the pair has no contacts: skipping it
+// changes no result (the oracle has no record and runs the narrow phase). Sides as narrow_phase gives them
+HD bool sep_face_skip(const SimCtx& c, int kind, int A, int B, int rec) {
+    const EnvLDS& s = *c.s;
+    const ha_model_t& m = *c.m;
+    int h1, h2, b1, b2;
+    PoseF P1, P2;
+    if (kind == 1) {
+        h1 = m.pool_hull[upool(c, A)]; P1 = object_pose_u(c, A); b1 = A;
+        h2 = m.static_hull[B]; P2 = static_pose(c, B); b2 = -1;
+    } else if (kind == 2) {
+        h1 = m.pool_hull[upool(c, A)]; P1 = object_pose_u(c, A); b1 = A;
+        h2 = m.pool_hull[upool(c, B)]; P2 = object_pose_u(c, B); b2 = B;
+    } else if (kind == 3) {
+        int Lk = m.hull_link[B];
+        h1 = B; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk;
+        h2 = m.pool_hull[upool(c, A)]; P2 = object_pose_u(c, A); b2 = A;
+    } else {
+        int Lk = m.hull_link[A];
+        h1 = A; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk;
+        h2 = m.static_hull[B]; P2 = static_pose(c, B); b2 = -1;
+    }
+    bool fb = (rec & 0x80) != 0;
+    int kf = rec & 0x7F;
+    int hf = fb ? h2 : h1, hv = fb ? h1 : h2, bf = fb ? b2 : b1, bv = fb ? b1 : b2;
+    PoseF PF = fb ? P2 : P1, PV = fb ? P1 : P2;
+    if (kf >= m.hull_nplanes[hf]) return false;
+    f3 n;
+    float d;
+    world_plane(m, hf, kf, PF, body_scaled(c, bf), inv_scale(c, bf), n, d);
+    float v = 3.0e38f;
+    if (c.lane < m.hull_nverts[hv])
+        v = dot3(n, PV.p + qrot(PV.q, scale3(c, bv, ld3(m.verts[m.hull_vert_start[hv] + c.lane])))) + d;
+    return wave_min(v) > c.p->contact_margin;
+}
+
 template <bool SELF>
 HD void detect(SimCtx& c) {
     EnvLDS& s = *c.s;
@@ -2069,6 +2123,8 @@ HD void detect(SimCtx& c) {
         // the candidates whose persistent-manifold record applies (ha_params_t v13), tested for the whole batch at once;
         // their records are then loaded a pair ahead of their turn (one register each)
         uint64_t vmask = __ballot(c.pcm && cand && pcm_valid_lane(c, p, kind, A, B));
+        // and the candidates' separating-face records, one byte load each
+        int frec = (cand && c.pairf) ? (int)c.pairf[p] : 0xFF;
         // one iteration per piece pair: a compound object (several convex pieces, ha_model_t v8) runs piece
         // pairs j = 0 .. np-1 of a candidate pair and then emits a single <= 4-point manifold for the object pair
         // (the oracle's gather_begin / gather_end). One loop and one call site per narrow phase (a single inlined
@@ -2106,6 +2162,27 @@ HD void detect(SimCtx& c) {
                 c.pslot = q; c.pkind = kind; c.pA = A; c.pB = B;
             }
             int np = pair_pieces(c, kind, A, B);
+            int rec = 0xFF;
+            if (c.pairf && kind != 0 && np == 1) {
+                rec = __builtin_amdgcn_readlane(frec, bit);
+#ifdef HA_PROFILE
+                unsigned long long _f0 = __builtin_amdgcn_s_memtime();
+#endif
+                bool fskip = rec != 0xFF && sep_face_skip(c, kind, A, B, rec);
+#ifdef HA_PROFILE
+                if (rec != 0xFF) {
+                    wsync();
+                    PROF_COUNT(90, __builtin_amdgcn_s_memtime() - _f0);     // face-record checks: time / checks / skips
+                    PROF_COUNT(91, 1);
+                    PROF_COUNT(92, fskip);
+                }
+#endif
+                if (fskip) {
+                    c.pslot = -1;
+                    mask &= mask - 1;
+                    continue;                    // separated on that face, as the narrow phase would find
+                }
+            }
 #ifdef HA_PROFILE
             unsigned long long _k0 = __builtin_amdgcn_s_memtime();
             int _nc0 = s.nc;
@@ -2133,6 +2210,7 @@ HD void detect(SimCtx& c) {
             }
             pcm_commit(c);
             c.pslot = -1;
+            if (c.pairf && kind != 0 && np == 1 && lane == 0 && c.sepf != rec) c.pairf[q] = (uint8_t)c.sepf;
 #ifdef HA_PROFILE
             wsync();
             PROF_COUNT(10 + kind, __builtin_amdgcn_s_memtime() - _k0);     // time / pairs / pairs with contacts
@@ -2567,8 +2645,10 @@ HD void substep(SimCtx& c, float hdt) {
     //      the union after RK. Lane i holds contacts i and 64 + i; one ballot per pick
     int npass = 0;
     uint32_t* PASS = nullptr;
-    if constexpr (PC::pack) {
-        PASS = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(RK) + 6 * sizeof(float) * (size_t)PC::rk_stride);
+    // overflow families: only a substep whose contacts fit chunk 0 (its rows in LDS, constants in registers) is packed
+    const bool packed = PC::pack && (!PC::ovf || nc <= CAP);           // wave-uniform
+    if (packed) {
+        PASS = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s.u.rows.J) + pc_pass_offset<PC>());
         int o00 = -1, o01 = -1, o10 = -1, o11 = -1;
         if (lane < nc) {
             int a_, b_;
@@ -2829,25 +2909,39 @@ HD void substep(SimCtx& c, float hdt) {
             j0n = j0m; j1n = j1m; j2n = j2m; y0n = y0m; y1n = y1m; y2n = y2m;
             h0n = h0m; h1n = h1m; h2n = h2m; g0n = g0m; g1n = g1m; g2n = g2m;
         };
-        // one contact block from its three J.v sums, with the constants and impulses in RK (the packed family): the
-        // serial block's arithmetic (n0, d0, hi, n1 through the Delassus entries, n2), evaluated alike by every lane that
-        // calls it; `writer` stores the new impulses
-        auto solve_rk = [&](int ci, float jv0, float jv1, float jv2, bool writer, float& d0, float& d1, float& d2) {
+        // packed families: a contact block's constants (impulses, target velocities, 1/diagonals of its three rows, the
+        // friction coefficient, the Delassus entries a10 a20 a21) - from RK (LDS), or with overflow chunks from the
+        // registers of the lanes that own its rows in chunk 0 - and the serial block's arithmetic on them (n0, d0,
+        // hi, n1 through the Delassus entries, n2), evaluated alike by every lane that calls it
+        auto consts = [&](int ci, float* K) {
             int r0 = 3 * ci;
-            float l0 = rk(0, r0), l1 = rk(0, r0 + 1), l2 = rk(0, r0 + 2);
-            float n0 = l0 - (jv0 - rk(1, r0)) * rk(2, r0);
-            n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
-            d0 = n0 - l0;
-            float hi = rk(3, r0 + 1) * n0;
-            float n1 = l1 - (fmaf(rk(4, r0 + 1), d0, jv1) - rk(1, r0 + 1)) * rk(2, r0 + 1);
-            n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
-            d1 = n1 - l1;
-            float n2 = l2 - (fmaf(rk(5, r0 + 2), d1, fmaf(rk(4, r0 + 2), d0, jv2)) - rk(1, r0 + 2)) * rk(2, r0 + 2);
-            n2 = n2 < -hi ? -hi : (n2 > hi ? hi : n2);
-            d2 = n2 - l2;
-            if (writer) { rk(0, r0) = n0; rk(0, r0 + 1) = n1; rk(0, r0 + 2) = n2; }
+            if constexpr (!PC::ovf) {
+                K[0] = rk(0, r0); K[1] = rk(0, r0 + 1); K[2] = rk(0, r0 + 2);
+                K[3] = rk(1, r0); K[4] = rk(1, r0 + 1); K[5] = rk(1, r0 + 2);
+                K[6] = rk(2, r0); K[7] = rk(2, r0 + 1); K[8] = rk(2, r0 + 2);
+                K[9] = rk(3, r0 + 1); K[10] = rk(4, r0 + 1); K[11] = rk(4, r0 + 2); K[12] = rk(5, r0 + 2);
+            } else {
+                K[0] = __shfl(klam, r0); K[1] = __shfl(klam, r0 + 1); K[2] = __shfl(klam, r0 + 2);
+                K[3] = __shfl(kvt, r0); K[4] = __shfl(kvt, r0 + 1); K[5] = __shfl(kvt, r0 + 2);
+                K[6] = __shfl(kwinv, r0); K[7] = __shfl(kwinv, r0 + 1); K[8] = __shfl(kwinv, r0 + 2);
+                K[9] = __shfl(kcmu, r0 + 1); K[10] = __shfl(kca0, r0 + 1); K[11] = __shfl(kca0, r0 + 2);
+                K[12] = __shfl(kca1, r0 + 2);
+            }
         };
-        if constexpr (PC::pack) {
+        auto block = [&](const float* K, float jv0, float jv1, float jv2, float& n0, float& n1, float& n2, float& d0,
+                         float& d1, float& d2) {
+            n0 = K[0] - (jv0 - K[3]) * K[6];
+            n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
+            d0 = n0 - K[0];
+            float hi = K[9] * n0;
+            n1 = K[1] - (fmaf(K[10], d0, jv1) - K[4]) * K[7];
+            n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
+            d1 = n1 - K[1];
+            n2 = K[2] - (fmaf(K[12], d1, fmaf(K[11], d0, jv2)) - K[5]) * K[8];
+            n2 = n2 < -hi ? -hi : (n2 > hi ? hi : n2);
+            d2 = n2 - K[2];
+        };
+        if (packed) {
             // link contacts: whole-wave blocks in contact order, as the other families solve every contact
             uint64_t lk0 = lmask0, lk1 = lmask1;
             while (lk0 | lk1) {
@@ -2863,8 +2957,17 @@ HD void substep(SimCtx& c, float hdt) {
                     jv2 = jv2 + h2n * vregh;
                 }
                 wave_sum_rows3(jv0, jv1, jv2);
-                float d0, d1, d2;
-                solve_rk(ci, jv0, jv1, jv2, lane == 0, d0, d1, d2);
+                float K[13], n0, n1, n2, d0, d1, d2;
+                consts(ci, K);
+                block(K, jv0, jv1, jv2, n0, n1, n2, d0, d1, d2);
+                int r0 = 3 * ci;
+                if constexpr (!PC::ovf) {
+                    if (lane == 0) { rk(0, r0) = n0; rk(0, r0 + 1) = n1; rk(0, r0 + 2) = n2; }
+                } else {
+                    if (lane == r0) klam = n0;
+                    if (lane == r0 + 1) klam = n1;
+                    if (lane == r0 + 2) klam = n2;
+                }
                 if (d0 != 0.0f) { vreg = fmaf(y0n, d0, vreg); if (VW == 2) vregh = fmaf(g0n, d0, vregh); }
                 if (d1 != 0.0f) { vreg = fmaf(y1n, d1, vreg); if (VW == 2) vregh = fmaf(g1n, d1, vregh); }
                 if (d2 != 0.0f) { vreg = fmaf(y2n, d2, vreg); if (VW == 2) vregh = fmaf(g2n, d2, vregh); }
@@ -2879,7 +2982,8 @@ HD void substep(SimCtx& c, float hdt) {
                 const int rr = lane >> 4, t = lane & 15;
 #pragma unroll 1
                 for (int pp = 0; pp < npass; pp++) {
-                    int ci = (int)((PASS[pp] >> (8 * rr)) & 0xFFu);
+                    uint32_t pk = PASS[pp];
+                    int ci = (int)((pk >> (8 * rr)) & 0xFFu);
                     bool act = ci != 0xFF;
                     int idx = -1;
                     float x0 = 0.0f, x1 = 0.0f, x2 = 0.0f, y0 = 0.0f, y1 = 0.0f, y2 = 0.0f, vv = 0.0f;
@@ -2890,26 +2994,44 @@ HD void substep(SimCtx& c, float hdt) {
                         int o = t < 6 ? so0 : so1;
                         if (o >= 0) {
                             idx = D + 6 * o + (t < 6 ? t : t - 6);
-                            const float* Jo = orow_g(3 * ci, false);
-                            const float* Yo = orow_g(3 * ci, true);
-                            auto Jg = glb_f<true>(Jo);
-                            auto Yg = glb_f<true>(Yo);
-                            float j0 = Jg[t], j1 = Jg[OW + t], j2 = Jg[2 * OW + t];
-                            y0 = Yg[t]; y1 = Yg[OW + t]; y2 = Yg[2 * OW + t];
+                            float j0, j1, j2;
+                            if constexpr (PC::ovf) {            // chunk 0's object rows, in LDS
+                                auto Jl = lds_f<true>(Ob + 3 * ci * OW);
+                                auto Yl = lds_f<true>(ObY + 3 * ci * OW);
+                                j0 = Jl[t]; j1 = Jl[OW + t]; j2 = Jl[2 * OW + t];
+                                y0 = Yl[t]; y1 = Yl[OW + t]; y2 = Yl[2 * OW + t];
+                            } else {                            // the env's global row area
+                                auto Jg = glb_f<true>(orow_g(3 * ci, false));
+                                auto Yg = glb_f<true>(orow_g(3 * ci, true));
+                                j0 = Jg[t]; j1 = Jg[OW + t]; j2 = Jg[2 * OW + t];
+                                y0 = Yg[t]; y1 = Yg[OW + t]; y2 = Yg[2 * OW + t];
+                            }
                             vv = s.v[idx];
                             x0 = j0 * vv; x1 = j1 * vv; x2 = j2 * vv;
                         }
                     }
                     row_sum3(x0, x1, x2);
-                    if (act) {
-                        float d0, d1, d2;
-                        solve_rk(ci, x0, x1, x2, t == 0, d0, d1, d2);
-                        if (idx >= 0) {
-                            if (d0 != 0.0f) vv = fmaf(y0, d0, vv);
-                            if (d1 != 0.0f) vv = fmaf(y1, d1, vv);
-                            if (d2 != 0.0f) vv = fmaf(y2, d2, vv);
-                            s.v[idx] = vv;
-                        }
+                    float K[13], n0, n1, n2, d0, d1, d2;
+                    consts(act ? ci : 0, K);
+                    block(K, x0, x1, x2, n0, n1, n2, d0, d1, d2);
+                    if (act && idx >= 0) {
+                        if (d0 != 0.0f) vv = fmaf(y0, d0, vv);
+                        if (d1 != 0.0f) vv = fmaf(y1, d1, vv);
+                        if (d2 != 0.0f) vv = fmaf(y2, d2, vv);
+                        s.v[idx] = vv;
+                    }
+                    if constexpr (!PC::ovf) {
+                        if (act && t == 0) { rk(0, 3 * ci) = n0; rk(0, 3 * ci + 1) = n1; rk(0, 3 * ci + 2) = n2; }
+                    } else {
+                        // the impulses back to the lanes that own the rows: lane 3 c + k takes n_k of the pass row
+                        // holding contact c
+                        int myc = lane / 3, mk = lane - 3 * myc, pos = -1;
+#pragma unroll
+                        for (int q = 0; q < 4; q++)
+                            if ((int)((pk >> (8 * q)) & 0xFFu) == myc) pos = q;
+                        int srcl = 16 * (pos < 0 ? 0 : pos);
+                        float m0 = __shfl(n0, srcl), m1 = __shfl(n1, srcl), m2 = __shfl(n2, srcl);
+                        if (pos >= 0 && lane < RPC) klam = mk == 0 ? m0 : (mk == 1 ? m1 : m2);
                     }
                     wsync();
                 }

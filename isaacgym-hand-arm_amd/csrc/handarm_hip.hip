@@ -84,6 +84,14 @@ static inline bool family_pcm(int fam) { return fam != HA_TASK_ALLEGRO_HAND; }
 #ifndef HB_PACKED_PGS
 #define HB_PACKED_PGS 1
 #endif
+// the Ur5Sih 3-object family can pack the substeps whose contacts fit chunk 0 (<= 21: rows in LDS, row constants in
+// the registers of the lanes owning the rows, gathered by lane permutes): measured off. Three objects give passes of
+// at most three contacts (~4 passes for 12 contacts), and the 16 permutes per pass cost more than the blocks saved:
+// C4 shard 3.14 -> 3.69 ms per step (r5j, bit-identical). A build with -DHA_PACKED_PGS=1 needs the oracle's
+// h->packed = 1 for these configurations (physics_oracle.c)
+#ifndef HA_PACKED_PGS
+#define HA_PACKED_PGS 0
+#endif
 // clutter family: link contacts whose robot blocks stay in LDS (the rest use the global spill rows). 2 slots
 // keep the env block at <= 20 KB, i.e. 8 workgroups per CU (8 slots: 22.8 KB, 7 per CU)
 #ifndef HB_LINK_SLOTS
@@ -185,7 +193,7 @@ using FamPhys = PhysCfg<task_nd<FAM>(), task_obj_capacity<FAM>(), task_contact_c
 #else
                         FAM == HA_TASK_ALLEGRO_HAND || FAM == HA_TASK_ALLEGRO_KUKA,
 #endif
-                        FAM == FAM_UR5SIH_CLUTTER && HB_PACKED_PGS>;
+                        (FAM == FAM_UR5SIH_CLUTTER && HB_PACKED_PGS) || (FAM == HA_TASK_UR5SIH && HA_PACKED_PGS)>;
 
 
 // ----------------------------------------------------------------------------- state load/store
@@ -520,6 +528,16 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.k = reinterpret_cast<ContactLDS*>(smem + contact_lds_offset<PC>());
     c.spill = (PC::split || PC::ovf || PC::selfc) ? spill + (size_t)env * PC::spill_floats : nullptr;
     c.selfc = PC::selfc ? reinterpret_cast<uint8_t*>(c.spill + PC::off_selfc) : nullptr;
+    // separating-face records of the broad phase's pairs: the clutter family only. There most candidate object pairs in
+    // the bin are apart (5.8 narrow phases a substep, 0.2 with contacts) and each needs a fresh hull setup; with the
+    // records 4.8 of them are skipped (narrow phases 13.8% -> 2.2% of the substep, checks 5.9%). In the Allegro
+    // families the separated pairs are link hulls against the cube, whose side is cached across consecutive pairs so
+    // the narrow phase's sphere cull is cheaper than a record check (C3: checks 6.8% for 3.5% saved), and the record
+    // register cost spills (tools/phase_profile.py, r5l)
+    c.pairf = (c.spill && FAM == FAM_UR5SIH_CLUTTER) ? reinterpret_cast<uint8_t*>(c.spill + PC::off_pairf) : nullptr;
+#ifdef HA_X_NO_PAIRF    /* A/B builds only: no separating-face records for the broad phase's pairs */
+    c.pairf = nullptr;
+#endif
     c.selfm = PC::selfc ? reinterpret_cast<uint32_t*>(smem + selfm_lds_offset<PC>()) : nullptr;
     c.sepf = 0xFF;
     // persistent contact manifolds (ha_params_t v13): the env's records, when the caller bound the buffer and the
@@ -866,6 +884,14 @@ static size_t spill_floats(int fam) {
         default: return FamPhys<HA_TASK_UR5SIH>::spill_floats;
     }
 }
+static int pairf_bytes(int fam) {
+    switch (fam) {
+        case FAM_UR5SIH_CLUTTER: return FamPhys<FAM_UR5SIH_CLUTTER>::pairf_bytes;
+        case HA_TASK_ALLEGRO_HAND: return FamPhys<HA_TASK_ALLEGRO_HAND>::pairf_bytes;
+        case HA_TASK_ALLEGRO_KUKA: return FamPhys<HA_TASK_ALLEGRO_KUKA>::pairf_bytes;
+        default: return FamPhys<HA_TASK_UR5SIH>::pairf_bytes;
+    }
+}
 static int obj_capacity(int fam) {
     switch (fam) {
         case FAM_UR5SIH_CLUTTER: return task_obj_capacity<FAM_UR5SIH_CLUTTER>();
@@ -1021,6 +1047,11 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     h->fam = fam;
     h->h_params = *params;
     h->stat_slots = 1;
+    // the broad phase's pairs must fit the family's separating-face records (one byte each in the env's global area)
+    {
+        int NO = params->n_objects, NS = model->n_static, NLH = model->n_link_hulls;
+        if (NO * (1 + NS + NLH) + NO * (NO - 1) / 2 + NLH * NS > pairf_bytes(fam)) return HA_E_MODEL;
+    }
     // persistent-manifold records (v13): none when the tolerance is off, and none in a family built without them
     if (params->pcm_lin_tol > 0.0f && !family_pcm(fam)) return HA_E_ARG;
     h->pcm_slots = params->pcm_lin_tol <= 0.0f ? 0 :

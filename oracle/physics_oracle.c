@@ -132,7 +132,7 @@ struct hao_s {
     int N, A, B, D, NO;
     int maxc;     /* contact capacity of the device kernel family (handarm_hip.hip family_of) */
     int pcm_slots;/* persistent-manifold record slots per env (hao_pcm_slots) */
-    int packed;   /* packed PGS passes: the clutter family's configurations (Ur5Sih with more than 3 objects) */
+    int packed;   /* packed PGS passes: 2 the clutter family (Ur5Sih, > 3 objects), 1 Ur5Sih <= 3 objects (nc <= 21) */
 };
 typedef struct hao_s* hao_handle;
 
@@ -1191,7 +1191,8 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
         fcoef[d] = m->dof_friction[d];
         lam_fr[d] = 0.0f;
     }
-    int passes[MAXC][4], npass = h->packed ? packed_passes(cs, nc, passes) : 0;
+    int packed = h->packed == 2 || (h->packed == 1 && nc <= 21);
+    int passes[MAXC][4], npass = packed ? packed_passes(cs, nc, passes) : 0;
     /* projected Gauss-Seidel, velocity form: joint rows d = 0..D-1 (drive, lower, upper), then the
      * contact rows; v is updated after every row */
     for (int it = 0; it < p->solver_iters; it++) {
@@ -1238,7 +1239,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
          * configuration (the clutter family) solves the link contacts this way in contact order and then the free
          * passes (contact_block_packed) */
         for (int c = 0; c < nc; c++) {
-            if (h->packed && !is_link_contact(&cs[c])) continue;
+            if (packed && !is_link_contact(&cs[c])) continue;
             int r0 = 3 * c;
             float jv0 = wave_dot(R.J[r0], v, NV), jv1 = wave_dot(R.J[r0 + 1], v, NV), jv2 = wave_dot(R.J[r0 + 2], v, NV);
             float l0 = lam[r0], l1 = lam[r0 + 1], l2 = lam[r0 + 2];
@@ -1259,7 +1260,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
             if (d1 != 0.0f) for (int k = 0; k < NV; k++) v[k] = fmaf(R.Y[r0 + 1][k], d1, v[k]);
             if (d2 != 0.0f) for (int k = 0; k < NV; k++) v[k] = fmaf(R.Y[r0 + 2][k], d2, v[k]);
         }
-        if (h->packed)
+        if (packed)
             for (int q = 0; q < npass; q++)
                 for (int k = 0; k < 4; k++)
                     if (passes[q][k] >= 0) {
@@ -1409,7 +1410,9 @@ hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int nu
        4 chunks of 12 (HA_AH_CONTACTS x HA_AH_CHUNKS); hao_set_capacity overrides it for A/B builds */
     h->maxc = params->task == HA_TASK_UR5SIH ? 4 * 21 : (params->task == HA_TASK_ALLEGRO_KUKA ? 2 * 21 : 4 * 12);
     h->pcm_slots = params->pcm_lin_tol > 0.0f ? hao_pcm_slots(model, params->n_objects) : 0;
-    h->packed = params->task == HA_TASK_UR5SIH && params->n_objects > 3;      /* handarm_hip.hip family_of */
+    /* packed PGS passes: the clutter family (handarm_hip.hip HB_PACKED_PGS). 1 would pack the 3-object family's substeps
+     * whose contacts fit its chunk 0 (21), as a -DHA_PACKED_PGS=1 kernel build does (measured slower, off) */
+    h->packed = params->task == HA_TASK_UR5SIH && params->n_objects > 3 ? 2 : 0;
     return h;
 }
 void hao_destroy(hao_handle h) { free(h); }
