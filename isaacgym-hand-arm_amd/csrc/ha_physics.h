@@ -193,7 +193,8 @@ struct PhysCfg {
     // per 16-lane row, in passes of contacts on disjoint objects (ha_physics.h substep, "free passes"); their
     // object-block rows must all be in the env's global row area
     static constexpr bool pack = PACK;
-    // overflow families pack only the substeps whose contacts fit chunk 0 (rows and row constants lane-resident)
+    // overflow families pack only the substeps whose contacts fit chunk 0 (their rows in LDS); max_passes also counts
+    // the contacts whose constants PK holds
     static constexpr int max_passes = OVF ? CAP : CAP * NCH;
     // the family's robot collides with itself (ha_model_t v12 self pairs; the Allegro families). Without it the
     // self-pair pass is not compiled (its registers would count against every family)
@@ -267,16 +268,18 @@ __host__ __device__ constexpr size_t pc_rowdata_bytes() {
     return PC::split ? 2 * sizeof(float) * ((size_t)PC::rpc * PC::lch * PC::ow + 3 * (size_t)PC::kl * PC::nd)
                      : 2 * sizeof(float) * (size_t)PC::rpc * PC::lch * row_stride<PC::nd>();
 }
+// packed families (PhysCfg PACK) keep a packed substep's PGS constants per contact instead (PK, 12 floats: impulses
+// l0 l1 l2, the normal row's target velocity, the three 1/diagonals, the friction coefficient, the Delassus entries
+// a10 a20 a21, 0; the friction rows' target velocities are 0)
+#define HA_PK 12
 template <class PC>
 __host__ __device__ constexpr size_t pc_rows_bytes() {
-    return pc_rowdata_bytes<PC>() + (PC::nch > 1 && !PC::ovf ? 6 * sizeof(float) * (size_t)PC::rk_stride : 0) +
-           (PC::pack ? sizeof(uint32_t) * (size_t)PC::max_passes : 0);      // the free passes (4 contact bytes each)
+    return PC::pack ? pc_rowdata_bytes<PC>() + sizeof(float) * HA_PK * (size_t)PC::max_passes
+                    : pc_rowdata_bytes<PC>() + (PC::nch > 1 && !PC::ovf ? 6 * sizeof(float) * (size_t)PC::rk_stride : 0);
 }
-// the free passes' list in the phase union: after the row data and (several LDS chunks) RK
 template <class PC>
-__host__ __device__ constexpr size_t pc_pass_offset() {
-    return pc_rowdata_bytes<PC>() + (PC::nch > 1 && !PC::ovf ? 6 * sizeof(float) * (size_t)PC::rk_stride : 0);
-}
+__host__ __device__ constexpr size_t pc_pk_offset() { return pc_rowdata_bytes<PC>(); }
+
 // S ~ M^-1 (factor_inverse), D x D at stride D, sized for the family's DOF count: at the end of the union
 // (minv_in_union) or after it
 // (after the constraint rows when those reach past it: the union then grows by the difference, which the
@@ -2446,6 +2449,10 @@ HD void substep(SimCtx& c, float hdt) {
     static_assert(PC::rk_stride == RPC * NCH, "RK: one row-constant array per field, every chunk's rows");
     auto rk = [&](int q, int row) -> float& { return RK[q * PC::rk_stride + row]; };   // q < 6, row < rk_stride
     const bool multi = NCH > 1 && (!PC::ovf || nc > CAP);       // wave-uniform
+    // packed sweeps (PhysCfg PACK): every substep of the clutter family, the overflow families' substeps whose contacts
+    // fit chunk 0. Their row constants go to PK (per contact) instead of registers / RK
+    const bool packed = PC::pack && (!PC::ovf || nc <= CAP);           // wave-uniform
+    float* PK = PC::pack ? reinterpret_cast<float*>(reinterpret_cast<char*>(s.u.rows.J) + pc_pk_offset<PC>()) : nullptr;
     // chunk ch's rows. LDS (true) / global (false) dense rows are separate instantiations, so that no pointer may
     // address both (a flat pointer would make chunk 0's LDS rows flat accesses too)
     auto rows_chunk = [&](int ch, auto lds_tag) {
@@ -2550,7 +2557,17 @@ HD void substep(SimCtx& c, float hdt) {
         if (NCH == 1 || (PC::ovf && ch == 0)) {
             kvt = vt_; kwinv = winv_; kcmu = cmu_;
         }
-        if (multi && lane < RPC) {
+        if (packed) {
+            if (lane < RPC && r < nr) {
+                int ck = r / 3, k = r - 3 * ck;
+                HA_AS_LDS float* q = (HA_AS_LDS float*)(PK + HA_PK * ck);
+                q[k] = 0.0f;                                // the impulse
+                q[4 + k] = winv_;
+                if (k == 0) q[3] = vt_;
+                if (k == 1) q[7] = cmu_;
+                if (k == 2) q[11] = 0.0f;
+            }
+        } else if (multi && lane < RPC) {
             rk(0, r) = 0.0f; rk(1, r) = vt_; rk(2, r) = winv_; rk(3, r) = cmu_;
         }
     };
@@ -2629,7 +2646,14 @@ HD void substep(SimCtx& c, float hdt) {
         if (NCH == 1 || (PC::ovf && ch == 0)) {
             kca0 = ca0_; kca1 = ca1_;
         }
-        if (multi && lane < RPC) {
+        if (packed) {
+            if (lane < RPC && r < nr && r % 3 != 0) {
+                int ck = r / 3, k = r - 3 * ck;
+                HA_AS_LDS float* q = (HA_AS_LDS float*)(PK + HA_PK * ck);
+                if (k == 1) q[8] = ca0_;
+                else { q[9] = ca0_; q[10] = ca1_; }
+            }
+        } else if (multi && lane < RPC) {
             rk(4, r) = ca0_; rk(5, r) = ca1_;
         }
     };
@@ -2644,11 +2668,11 @@ HD void substep(SimCtx& c, float hdt) {
     //      the pass does not hold yet: physics_oracle.c packed_passes). A pass is four contact bytes (0xFF: none), in
     //      the union after RK. Lane i holds contacts i and 64 + i; one ballot per pick
     int npass = 0;
-    uint32_t* PASS = nullptr;
-    // overflow families: only a substep whose contacts fit chunk 0 (its rows in LDS, constants in registers) is packed
-    const bool packed = PC::pack && (!PC::ovf || nc <= CAP);           // wave-uniform
+    // the pass list stays in registers: pass p is lane p's pair (plo, phi) (p >= 64: plo2, phi2), four 16-bit fields,
+    // one per contact: its index (0xFF: none), object slot 0 + 1 and object slot 1 + 1 (contact_slots), so that a
+    // sweep decodes a pass from two scalars without an LDS round trip
+    uint32_t plo = 0xFFFFFFFFu, phi = 0xFFFFFFFFu, plo2 = 0xFFFFFFFFu, phi2 = 0xFFFFFFFFu;
     if (packed) {
-        PASS = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s.u.rows.J) + pc_pass_offset<PC>());
         int o00 = -1, o01 = -1, o10 = -1, o11 = -1;
         if (lane < nc) {
             int a_, b_;
@@ -2665,14 +2689,18 @@ HD void substep(SimCtx& c, float hdt) {
         uint64_t rem0 = __ballot(lane < nc) & ~lmask0;
         uint64_t rem1 = CAP * NCH > 64 ? __ballot(lane + 64 < nc) & ~lmask1 : 0ull;
         while (rem0 | rem1) {
-            uint32_t objm = 0u, pk = 0xFFFFFFFFu;
+            uint32_t objm = 0u;
+            uint64_t pk = ~0ull;
             uint64_t cand0 = rem0, cand1 = rem1;
             for (int k = 0; k < 4 && (cand0 | cand1); k++) {
                 int ci = cand0 ? __ffsll((unsigned long long)cand0) - 1 : 64 + __ffsll((unsigned long long)cand1) - 1;
                 int oa = ci < 64 ? __builtin_amdgcn_readlane(o00, ci) : __builtin_amdgcn_readlane(o10, ci - 64);
                 int ob = ci < 64 ? __builtin_amdgcn_readlane(o01, ci) : __builtin_amdgcn_readlane(o11, ci - 64);
                 objm |= (oa >= 0 ? 1u << oa : 0u) | (ob >= 0 ? 1u << ob : 0u);
-                pk = (pk & ~(0xFFu << (8 * k))) | ((uint32_t)ci << (8 * k));
+                int so0 = oa < 0 ? ob : (ob < 0 ? oa : (oa < ob ? oa : ob));
+                int so1 = (oa >= 0 && ob >= 0) ? (oa < ob ? ob : oa) : -1;
+                uint64_t fld = (uint64_t)ci | ((uint64_t)(so0 + 1) << 8) | ((uint64_t)(so1 + 1) << 12);
+                pk = (pk & ~(0xFFFFull << (16 * k))) | (fld << (16 * k));
                 if (ci < 64) rem0 &= ~(1ull << ci);
                 else rem1 &= ~(1ull << (ci - 64));
                 bool t0 = (o00 >= 0 && ((objm >> o00) & 1u)) || (o01 >= 0 && ((objm >> o01) & 1u));
@@ -2680,7 +2708,11 @@ HD void substep(SimCtx& c, float hdt) {
                 cand0 = rem0 & ~__ballot(t0);
                 cand1 = rem1 & ~__ballot(t1);
             }
-            if (lane == 0) PASS[npass] = pk;
+            if (npass < 64) {
+                if (lane == npass) { plo = (uint32_t)pk; phi = (uint32_t)(pk >> 32); }
+            } else if (lane == npass - 64) {
+                plo2 = (uint32_t)pk; phi2 = (uint32_t)(pk >> 32);
+            }
             npass++;
         }
     }
@@ -2728,7 +2760,7 @@ HD void substep(SimCtx& c, float hdt) {
         sl = rk(0, row); svt = rk(1, row); swinv = rk(2, row);
         scmu = rk(3, row); sca0 = rk(4, row); sca1 = rk(5, row);
     };
-    if (multi && lane < RPC) stage(0);
+    if (!packed && multi && lane < RPC) stage(0);
     const int nca = (nc + CAP - 1) / CAP;                   // chunks in use (wave-uniform)
 #ifdef HA_AB_PGS_TWICE
     for (int it = 0; it < 2 * p.solver_iters; it++) {
@@ -2913,34 +2945,33 @@ HD void substep(SimCtx& c, float hdt) {
         // friction coefficient, the Delassus entries a10 a20 a21) - from RK (LDS), or with overflow chunks from the
         // registers of the lanes that own its rows in chunk 0 - and the serial block's arithmetic on them (n0, d0,
         // hi, n1 through the Delassus entries, n2), evaluated alike by every lane that calls it
-        auto consts = [&](int ci, float* K) {
-            int r0 = 3 * ci;
-            if constexpr (!PC::ovf) {
-                K[0] = rk(0, r0); K[1] = rk(0, r0 + 1); K[2] = rk(0, r0 + 2);
-                K[3] = rk(1, r0); K[4] = rk(1, r0 + 1); K[5] = rk(1, r0 + 2);
-                K[6] = rk(2, r0); K[7] = rk(2, r0 + 1); K[8] = rk(2, r0 + 2);
-                K[9] = rk(3, r0 + 1); K[10] = rk(4, r0 + 1); K[11] = rk(4, r0 + 2); K[12] = rk(5, r0 + 2);
-            } else {
-                K[0] = __shfl(klam, r0); K[1] = __shfl(klam, r0 + 1); K[2] = __shfl(klam, r0 + 2);
-                K[3] = __shfl(kvt, r0); K[4] = __shfl(kvt, r0 + 1); K[5] = __shfl(kvt, r0 + 2);
-                K[6] = __shfl(kwinv, r0); K[7] = __shfl(kwinv, r0 + 1); K[8] = __shfl(kwinv, r0 + 2);
-                K[9] = __shfl(kcmu, r0 + 1); K[10] = __shfl(kca0, r0 + 1); K[11] = __shfl(kca0, r0 + 2);
-                K[12] = __shfl(kca1, r0 + 2);
-            }
+        auto consts = [&](int ci, float* K) {                // three 16-byte LDS loads (a broadcast per row)
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const HA_AS_LDS f4v* q = (const HA_AS_LDS f4v*)(PK + HA_PK * ci);
+            f4v a = q[0], b = q[1], e = q[2];
+            K[0] = a.x; K[1] = a.y; K[2] = a.z; K[3] = a.w;
+            K[4] = b.x; K[5] = b.y; K[6] = b.z; K[7] = b.w;
+            K[8] = e.x; K[9] = e.y; K[10] = e.z;
         };
+        // the friction rows' target velocity is 0: x - 0 is x, so the oracle's (jv1 - vt1) is jv1 here
         auto block = [&](const float* K, float jv0, float jv1, float jv2, float& n0, float& n1, float& n2, float& d0,
                          float& d1, float& d2) {
-            n0 = K[0] - (jv0 - K[3]) * K[6];
+            n0 = K[0] - (jv0 - K[3]) * K[4];
             n0 = n0 < 0.0f ? 0.0f : (n0 > 3.0e38f ? 3.0e38f : n0);
             d0 = n0 - K[0];
-            float hi = K[9] * n0;
-            n1 = K[1] - (fmaf(K[10], d0, jv1) - K[4]) * K[7];
+            float hi = K[7] * n0;
+            n1 = K[1] - fmaf(K[8], d0, jv1) * K[5];
             n1 = n1 < -hi ? -hi : (n1 > hi ? hi : n1);
             d1 = n1 - K[1];
-            n2 = K[2] - (fmaf(K[12], d1, fmaf(K[11], d0, jv2)) - K[5]) * K[8];
+            n2 = K[2] - fmaf(K[10], d1, fmaf(K[9], d0, jv2)) * K[6];
             n2 = n2 < -hi ? -hi : (n2 > hi ? hi : n2);
             d2 = n2 - K[2];
         };
+        auto put_lams = [&](int ci, float n0, float n1, float n2) {
+            HA_AS_LDS float* q = (HA_AS_LDS float*)(PK + HA_PK * ci);
+            q[0] = n0; q[1] = n1; q[2] = n2;
+        };
+        HA_AS_LDS float* sv = (HA_AS_LDS float*)s.v;      // the generalized velocity of the passes (LDS accesses)
         if (packed) {
             // link contacts: whole-wave blocks in contact order, as the other families solve every contact
             uint64_t lk0 = lmask0, lk1 = lmask1;
@@ -2957,17 +2988,10 @@ HD void substep(SimCtx& c, float hdt) {
                     jv2 = jv2 + h2n * vregh;
                 }
                 wave_sum_rows3(jv0, jv1, jv2);
-                float K[13], n0, n1, n2, d0, d1, d2;
+                float K[11], n0, n1, n2, d0, d1, d2;
                 consts(ci, K);
                 block(K, jv0, jv1, jv2, n0, n1, n2, d0, d1, d2);
-                int r0 = 3 * ci;
-                if constexpr (!PC::ovf) {
-                    if (lane == 0) { rk(0, r0) = n0; rk(0, r0 + 1) = n1; rk(0, r0 + 2) = n2; }
-                } else {
-                    if (lane == r0) klam = n0;
-                    if (lane == r0 + 1) klam = n1;
-                    if (lane == r0 + 2) klam = n2;
-                }
+                if (lane == 0) put_lams(ci, n0, n1, n2);
                 if (d0 != 0.0f) { vreg = fmaf(y0n, d0, vreg); if (VW == 2) vregh = fmaf(g0n, d0, vregh); }
                 if (d1 != 0.0f) { vreg = fmaf(y1n, d1, vreg); if (VW == 2) vregh = fmaf(g1n, d1, vregh); }
                 if (d2 != 0.0f) { vreg = fmaf(y2n, d2, vreg); if (VW == 2) vregh = fmaf(g2n, d2, vregh); }
@@ -2976,22 +3000,27 @@ HD void substep(SimCtx& c, float hdt) {
             // contact's compact row (object slot t / 6, entry t % 6). The generalized velocity goes through LDS for the
             // passes (contacts of one pass share no object, so their lanes read and write disjoint coordinates)
             if (npass > 0) {
-                if (lane < NV) s.v[lane] = vreg;
-                if (VW == 2 && lane + 64 < NV) s.v[lane + 64] = vregh;
+                if (lane < NV) sv[lane] = vreg;
+                if (VW == 2 && lane + 64 < NV) sv[lane + 64] = vregh;
                 wsync();
                 const int rr = lane >> 4, t = lane & 15;
 #pragma unroll 1
                 for (int pp = 0; pp < npass; pp++) {
-                    uint32_t pk = PASS[pp];
-                    int ci = (int)((pk >> (8 * rr)) & 0xFFu);
+                    uint32_t lo, hi;
+                    if (CAP * NCH <= 64 || pp < 64) {
+                        lo = __builtin_amdgcn_readlane(plo, pp);
+                        hi = __builtin_amdgcn_readlane(phi, pp);
+                    } else {
+                        lo = __builtin_amdgcn_readlane(plo2, pp - 64);
+                        hi = __builtin_amdgcn_readlane(phi2, pp - 64);
+                    }
+                    uint32_t fld = ((rr < 2 ? lo : hi) >> (16 * (rr & 1))) & 0xFFFFu;
+                    int ci = (int)(fld & 0xFFu);
                     bool act = ci != 0xFF;
                     int idx = -1;
                     float x0 = 0.0f, x1 = 0.0f, x2 = 0.0f, y0 = 0.0f, y1 = 0.0f, y2 = 0.0f, vv = 0.0f;
                     if (act && t < 12) {
-                        int a_, b_, so0, so1;
-                        ct_ab(c, ci, a_, b_);
-                        contact_slots(a_, b_, so0, so1);
-                        int o = t < 6 ? so0 : so1;
+                        int o = (int)(t < 6 ? (fld >> 8) & 0xFu : fld >> 12) - 1;
                         if (o >= 0) {
                             idx = D + 6 * o + (t < 6 ? t : t - 6);
                             float j0, j1, j2;
@@ -3006,37 +3035,27 @@ HD void substep(SimCtx& c, float hdt) {
                                 j0 = Jg[t]; j1 = Jg[OW + t]; j2 = Jg[2 * OW + t];
                                 y0 = Yg[t]; y1 = Yg[OW + t]; y2 = Yg[2 * OW + t];
                             }
-                            vv = s.v[idx];
+                            vv = sv[idx];
                             x0 = j0 * vv; x1 = j1 * vv; x2 = j2 * vv;
                         }
                     }
                     row_sum3(x0, x1, x2);
-                    float K[13], n0, n1, n2, d0, d1, d2;
-                    consts(act ? ci : 0, K);
-                    block(K, x0, x1, x2, n0, n1, n2, d0, d1, d2);
-                    if (act && idx >= 0) {
-                        if (d0 != 0.0f) vv = fmaf(y0, d0, vv);
-                        if (d1 != 0.0f) vv = fmaf(y1, d1, vv);
-                        if (d2 != 0.0f) vv = fmaf(y2, d2, vv);
-                        s.v[idx] = vv;
-                    }
-                    if constexpr (!PC::ovf) {
-                        if (act && t == 0) { rk(0, 3 * ci) = n0; rk(0, 3 * ci + 1) = n1; rk(0, 3 * ci + 2) = n2; }
-                    } else {
-                        // the impulses back to the lanes that own the rows: lane 3 c + k takes n_k of the pass row
-                        // holding contact c
-                        int myc = lane / 3, mk = lane - 3 * myc, pos = -1;
-#pragma unroll
-                        for (int q = 0; q < 4; q++)
-                            if ((int)((pk >> (8 * q)) & 0xFFu) == myc) pos = q;
-                        int srcl = 16 * (pos < 0 ? 0 : pos);
-                        float m0 = __shfl(n0, srcl), m1 = __shfl(n1, srcl), m2 = __shfl(n2, srcl);
-                        if (pos >= 0 && lane < RPC) klam = mk == 0 ? m0 : (mk == 1 ? m1 : m2);
+                    if (act) {
+                        float K[11], n0, n1, n2, d0, d1, d2;
+                        consts(ci, K);
+                        block(K, x0, x1, x2, n0, n1, n2, d0, d1, d2);
+                        if (idx >= 0) {
+                            if (d0 != 0.0f) vv = fmaf(y0, d0, vv);
+                            if (d1 != 0.0f) vv = fmaf(y1, d1, vv);
+                            if (d2 != 0.0f) vv = fmaf(y2, d2, vv);
+                            sv[idx] = vv;
+                        }
+                        if (t == 0) put_lams(ci, n0, n1, n2);
                     }
                     wsync();
                 }
-                vreg = lane < NV ? s.v[lane] : 0.0f;
-                vregh = (VW == 2 && lane + 64 < NV) ? s.v[lane + 64] : 0.0f;
+                vreg = lane < NV ? sv[lane] : 0.0f;
+                vregh = (VW == 2 && lane + 64 < NV) ? sv[lane + 64] : 0.0f;
                 wsync();
             }
         } else {
@@ -3094,8 +3113,10 @@ HD void substep(SimCtx& c, float hdt) {
         }
         }
     }
-    // impulse of global row RPC ch + lane (xfer sits before RK in the union: no overlap)
-    if (!multi) {
+    // impulse of global row RPC ch + lane (xfer sits before RK / PK in the union: no overlap)
+    if (packed) {
+        for (int r = lane; r < nr; r += 64) s.u.xfer[r] = ((HA_AS_LDS float*)PK)[HA_PK * (r / 3) + r % 3];
+    } else if (!multi) {
         if (lane < RPC) s.u.xfer[lane] = klam;
     } else {
 #pragma unroll 1

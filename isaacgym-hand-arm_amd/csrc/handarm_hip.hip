@@ -84,11 +84,11 @@ static inline bool family_pcm(int fam) { return fam != HA_TASK_ALLEGRO_HAND; }
 #ifndef HB_PACKED_PGS
 #define HB_PACKED_PGS 1
 #endif
-// the Ur5Sih 3-object family can pack the substeps whose contacts fit chunk 0 (<= 21: rows in LDS, row constants in
-// the registers of the lanes owning the rows, gathered by lane permutes): measured off. Three objects give passes of
-// at most three contacts (~4 passes for 12 contacts), and the 16 permutes per pass cost more than the blocks saved:
-// C4 shard 3.14 -> 3.69 ms per step (r5j, bit-identical). A build with -DHA_PACKED_PGS=1 needs the oracle's
-// h->packed = 1 for these configurations (physics_oracle.c)
+// the Ur5Sih 3-object family can pack the substeps whose contacts fit chunk 0 (<= 21: rows in LDS, the constants per
+// contact in PK, the rest serial over the overflow chunks): measured off. Three objects give passes of at most three
+// contacts, a bench env offers ~12 of which ~4 objects' worth share an object, so a sweep still runs ~4-5 passes of
+// ~2-3 contacts, each slower than the serial block it replaces: C4 shard 3.14 -> 3.60 ms per step (r5j-r5p,
+// bit-identical; with lane-permuted constants 3.69 ms). A -DHA_PACKED_PGS=1 build needs the oracle's h->packed = 1
 #ifndef HA_PACKED_PGS
 #define HA_PACKED_PGS 0
 #endif

@@ -1410,8 +1410,8 @@ hao_handle hao_create(const ha_model_t* model, const ha_params_t* params, int nu
        4 chunks of 12 (HA_AH_CONTACTS x HA_AH_CHUNKS); hao_set_capacity overrides it for A/B builds */
     h->maxc = params->task == HA_TASK_UR5SIH ? 4 * 21 : (params->task == HA_TASK_ALLEGRO_KUKA ? 2 * 21 : 4 * 12);
     h->pcm_slots = params->pcm_lin_tol > 0.0f ? hao_pcm_slots(model, params->n_objects) : 0;
-    /* packed PGS passes: the clutter family (handarm_hip.hip HB_PACKED_PGS). 1 would pack the 3-object family's substeps
-     * whose contacts fit its chunk 0 (21), as a -DHA_PACKED_PGS=1 kernel build does (measured slower, off) */
+    /* packed PGS passes (handarm_hip.hip HB_PACKED_PGS): 2 every substep of the clutter family; 1 would pack the 3-object
+     * family's substeps whose contacts fit its chunk 0 (21), as a -DHA_PACKED_PGS=1 kernel build does (off: slower) */
     h->packed = params->task == HA_TASK_UR5SIH && params->n_objects > 3 ? 2 : 0;
     return h;
 }
