@@ -159,10 +159,12 @@ __host__ __device__ constexpr int task_col_planes() { return (FAM == HA_TASK_ALL
 #ifndef HA_AK_COMPACT
 #define HA_AK_COMPACT 1
 #endif
-// (3 since round 4: with the hand's self contacts most contacts touch links; the third slot fits in front of S,
-// 9.9 KB per env, still 16 workgroups per CU: C2 -0.4% and fewer spill-row writes)
+// (3 in round 4: with the hand's self contacts most contacts touch links. 9 since round 5: at 3 waves per SIMD the
+// CU holds 12 workgroups, so the LDS may grow to 13.3 KB per env (552 B per slot; 9 is the most that keeps 12 per CU).
+// A/B on C2 (profiles/README.md): 3 slots 1.037 ms / 27.8 KB HBM per env, 6 slots 1.018 ms / 20.5 KB, 9 slots
+// 1.015 ms / 14.5 KB)
 #ifndef HA_AK_LINK_SLOTS
-#define HA_AK_LINK_SLOTS 3
+#define HA_AK_LINK_SLOTS 9
 #endif
 // AllegroHand in the same compact layout (split rows, no gather buffer, S in the union): every AllegroHand contact
 // touches a finger link, so its rows are robot blocks in HA_AH_LINK_SLOTS LDS slots and the global spill rows

@@ -146,12 +146,16 @@ def test_kuka_link_contacts_spill_rows_match_oracle():
     put(sim, "root_state", st["root_state"])
     for k in ("dof_state", "sim_targets", "contact_cache"):     # (the probe call above wrote manifold records)
         put(sim, k, st[k])
+    st0 = st.copy()
     sim.simulate(1)
     orc.simulate(st, 1)
     f = get(sim, "net_contact_force").reshape(n, B, 3)[:, m.body_robot0:m.body_robot0 + m.n_links]
     touched = (np.abs(f).sum(-1) > 0).sum(1)
     print("kuka link-contact scene: robot links in contact per env: median %d, max %d" % (np.median(touched), touched.max()))
-    assert touched.max() > 3, "no env has more link contacts than the LDS link slots (HA_AK_LINK_SLOTS = 3)"
+    assert touched.max() > 3, "no env has the cuboid on several links"
+    # link contacts past the LDS slots (HA_AK_LINK_SLOTS = 9) go to the spill rows: most envs of this scene have more
+    link = [int(((c[:, 7] >= 100) | (c[:, 8] >= 100)).sum()) for c in (orc.contacts(st0, e) for e in range(n))]
+    assert sum(k > 9 for k in link) > n // 4, link
     scenes.assert_physics_bit_identical(sim, st, n, tag="kuka link contacts")
 
 
