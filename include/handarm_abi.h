@@ -198,7 +198,10 @@ typedef struct ha_model_t {
      * collides every link pair of the articulation except parent and child. self_pair[k] = hull a | hull b << 8
      * (link hulls of two such links, a < b), tested after the link-static pairs; hull_obb[h] = the link hull's
      * oriented box in the link frame (centre[3], half extents[3], quat[4] xyzw, pad[2]) for the mid-phase cull
-     * (include/ha_obb.h). n_self_pairs = 0: no self-collision (Ur5Sih: filter 0b1, ur5sih.py:123-125). */
+     * (include/ha_obb.h). n_self_pairs = 0: no self-collision (Ur5Sih: filter 0b1, ur5sih.py:123-125).
+     * A one-piece pool object's hull carries a box too: its bounding box in the body frame with the identity
+     * orientation (scaled with the env's object_scale), for the broad phase's box cull of the Allegro families.
+     * ha_create refuses a model whose link hulls or one-piece object hulls do not lie inside their boxes. */
     int32_t n_self_pairs;
     uint16_t self_pair[HA_MAX_SELF_PAIRS];
     float hull_obb[HA_MAX_HULLS][12];

@@ -943,6 +943,24 @@ int ha_struct_sizes(int32_t* model_size, int32_t* params_size, int32_t* state_si
     return HA_OK;
 }
 
+// hull k's vertices inside its hull_obb box (centre, half extents, orientation in the body frame), within 1e-5 m
+static bool hull_in_box(const ha_model_t* m, int k) {
+    const float* ob = m->hull_obb[k];
+    if (!(ob[3] >= 0.0f && ob[4] >= 0.0f && ob[5] >= 0.0f)) return false;
+    const float zero[3] = {0.0f, 0.0f, 0.0f}, id[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+    float c[3], R[9];
+    ha_obb_world(zero, id, ob, c, R);
+    for (int v = 0; v < m->hull_nverts[k]; v++) {
+        const float* x = m->verts[m->hull_vert_start[k] + v];
+        float d[3] = {x[0] - c[0], x[1] - c[1], x[2] - c[2]};
+        for (int i = 0; i < 3; i++) {
+            float l = R[i] * d[0] + R[3 + i] * d[1] + R[6 + i] * d[2];
+            if (fabsf(l) > ob[3 + i] + 1e-5f) return false;
+        }
+    }
+    return true;
+}
+
 int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_envs, ha_handle* out) {
     if (!model || !params || !out || num_envs <= 0) return HA_E_ARG;
     if (params->task != HA_TASK_UR5SIH && params->task != HA_TASK_ALLEGRO_HAND && params->task != HA_TASK_ALLEGRO_KUKA)
@@ -1015,6 +1033,14 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
                 (int)(e >> 24) >= np_)
                 return HA_E_MODEL;
         }
+    }
+    // the broad phase's box cull (ha_physics.h pair_boxes_near): every link hull and every one-piece pool object's hull
+    // inside its hull_obb box
+    if (model->n_link_hulls < 0 || model->n_link_hulls > model->n_hulls) return HA_E_MODEL;
+    for (int k = 0; k < model->n_hulls; k++) {
+        bool boxed = k < model->n_link_hulls;
+        for (int p = 0; p < model->n_pool; p++) boxed = boxed || (model->pool_nhull[p] == 1 && model->pool_hull[p] == k);
+        if (boxed && !hull_in_box(model, k)) return HA_E_MODEL;
     }
     // self-collision pairs (v12): two link hulls of the model each; only the Allegro families' kernels run them
     if (model->n_self_pairs < 0 || model->n_self_pairs > HA_MAX_SELF_PAIRS) return HA_E_MODEL;

@@ -427,6 +427,7 @@ def build_model(scene, pool_names=None, posed=None):
         if len(obj_hulls[i]) == 1:          # the hull's own sphere (bit-identical broad phase for one-hull objects)
             m.pool_center[i][:] = obj_hulls[i][0]["center"]
             m.pool_radius[i] = obj_hulls[i][0]["radius"]
+            m.hull_obb[m.pool_hull[i]][:] = object_box(obj_hulls[i][0]["verts"])
         else:
             pts = np.concatenate([np.asarray(h["verts"], np.float64) for h in obj_hulls[i]])
             ctr = 0.5 * (pts.min(0) + pts.max(0))
@@ -524,6 +525,16 @@ def hull_obb(verts):
         q[3] = (R[k, j] - R[j, k]) / S
     q = np.asarray(q) / np.linalg.norm(q)
     return list(c) + list(half) + list(q) + [0.0, 0.0]
+
+
+def object_box(verts):
+    """A one-piece pool object's box for the broad phase's box cull (ha_physics.h pair_boxes_near): the hull's bounding
+    box in the body frame (identity orientation, so a per-env object scale scales its centre and half extents), padded
+    like hull_obb; the same 12-float record."""
+    v = np.asarray(verts, np.float64)
+    lo, hi = v.min(0), v.max(0)
+    half = (hi - lo) / 2 * (1 + 1e-5) + 1e-6
+    return list((lo + hi) / 2) + list(half) + [0.0, 0.0, 0.0, 1.0, 0.0, 0.0]
 
 
 def _self_collision(m, scene, links):
