@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 14
+#define HA_ABI_VERSION 15
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -320,6 +320,13 @@ typedef struct ha_params_t {
      * Otherwise the narrow phase runs and a pair that yields contacts rewrites its record. pcm_lin_tol <= 0 or a
      * null contact_cache: every candidate pair runs the narrow phase (the round-4 behaviour). */
     float pcm_lin_tol, pcm_cos_tol;
+    /* v15: AllegroHand options (allegro_hand.py:66-121,406-504,602-616; cfg/task/AllegroHand.yaml observationType,
+     * asymmetric_observations, useRelativeControl, dofSpeedScale) */
+    int32_t ah_obs_type;               /* 0 "full_state" (88 floats), 1 "full" (72), 2 "full_no_vel" (50); = num_obs */
+    int32_t ah_asymmetric;             /* compute_full_state(True): the 88-float state vector (dof forces included) goes
+                                        * to teacher_obs ([N][88], VecTask's states_buf) as well */
+    int32_t ah_relative_control;       /* targets = prev_targets + dofSpeedScale * dt * actions, clamped (no average) */
+    float ah_speed_dt;                 /* shadow_hand_dof_speed_scale * dt: python double, rounded once */
 } ha_params_t;
 
 /* Device buffers (caller-allocated). Layouts match the Isaac Gym tensors exactly. */
@@ -333,7 +340,7 @@ typedef struct ha_state_t {
     /* task */
     const float* actions;       /* [N][11] (ha_task_step_io stores the clamped caller actions here) */
     float* obs;                 /* [N][147] */
-    float* teacher_obs;         /* [N][147] */
+    float* teacher_obs;         /* [N][147] (AllegroHand with ah_asymmetric: [N][88], the states buffer) */
     float* rew;                 /* [N] */
     int64_t* reset_buf;         /* [N] */
     int64_t* progress_buf;      /* [N] */

@@ -3,13 +3,15 @@
 //   pre_physics_step  allegro_hand.py:586-625  (goal resets, reset_idx, absolute targets + moving average)
 //   reset_target_pose allegro_hand.py:506-522
 //   reset_idx         allegro_hand.py:524-584
-//   compute_full_state allegro_hand.py:462-504 (observationType "full_state", 88 floats)
+//   compute_observations allegro_hand.py:406-504 (observationType "full_state" 88 floats, "full" 72, "full_no_vel" 50;
+//                        asymmetric_observations: the full_state vector to the states buffer too)
 //   compute_hand_reward allegro_hand.py:663-719
 #pragma once
 #include "ha_task.h"
 
 #define AH_ND 16
-#define AH_NUM_OBS 88
+#define AH_NUM_OBS 88           /* full_state; ha_params_t.num_obs is the observation type's size */
+#define AH_NUM_STATES 88
 #define AH_NUM_ACT 16
 
 // replayed draws (HA_FLAG_REPLAY_DRAWS) in reset_draws[env][...], in the reference's draw order:
@@ -121,7 +123,8 @@ HD void ah_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags, bool 
     wsync();
 }
 
-// absolute targets with moving average and clamp (allegro_hand.py:607-616; useRelativeControl False)
+// targets (allegro_hand.py:602-616): useRelativeControl prev + dofSpeedScale * dt * action, else absolute targets with
+// the moving average; clamped either way
 HD void ah_controller(SimCtx& c, const ha_state_t& st, int env) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
@@ -132,8 +135,13 @@ HD void ah_controller(SimCtx& c, const ha_state_t& st, int env) {
         float a = act_at(c, st, (size_t)env * AH_NUM_ACT + lane);
         if (c.act_in) const_cast<float*>(st.actions)[(size_t)env * AH_NUM_ACT + lane] = a;          // the task's stored actions
         float* prev = st.dof_position_targets + (size_t)env * D;
-        float cur = 0.5f * (a + 1.0f) * (up - lo) + lo;                           // scale()
-        cur = p.ah_act_moving_average * cur + p.sih_beta * prev[lane];           // sih_beta := 1 - ama (python double)
+        float cur;
+        if (p.ah_relative_control) {
+            cur = prev[lane] + p.ah_speed_dt * a;
+        } else {
+            cur = 0.5f * (a + 1.0f) * (up - lo) + lo;                            // scale()
+            cur = p.ah_act_moving_average * cur + p.sih_beta * prev[lane];       // sih_beta := 1 - ama (python double)
+        }
         cur = fmaxf(fminf(cur, up), lo);                                         // tensor_clamp
         prev[lane] = cur;
         s.tgt[lane] = cur;
@@ -152,21 +160,39 @@ HD void ah_post(SimCtx& c, const ha_state_t& st, int env, const AhIn& in, bool o
         float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
         ref_quat_mul(&in.obj[3], gc, qdiff);
     }
-    float* ob = st.obs + (size_t)env * AH_NUM_OBS;
-    for (int k = lane; k < AH_NUM_OBS; k += 64) {
-        float v;
+    // compute_full_state (:484-504): 88 floats; element k of it
+    auto full_state = [&](int k) -> float {
         if (k < 16) {
             float lo = m.dof_lower[k], up = m.dof_upper[k];
-            v = (2.0f * in.q[k] - up - lo) / (up - lo);                          // unscale()
-        } else if (k < 32) v = p.ah_vel_obs_scale * in.qd[k - 16];
-        else if (k < 48) v = p.ah_force_torque_obs_scale * in.f[k - 32];
-        else if (k < 58) v = in.obj[k - 48];                                     // pose + linvel
-        else if (k < 61) v = p.ah_vel_obs_scale * in.obj[k - 48];                // angvel
-        else if (k < 68) v = gs[k - 61];
-        else if (k < 72) v = qdiff[k - 68];
-        else v = act_at(c, st, (size_t)env * AH_NUM_ACT + (k - 72));
+            return (2.0f * in.q[k] - up - lo) / (up - lo);                       // unscale()
+        }
+        if (k < 32) return p.ah_vel_obs_scale * in.qd[k - 16];
+        if (k < 48) return p.ah_force_torque_obs_scale * in.f[k - 32];
+        if (k < 58) return in.obj[k - 48];                                       // pose + linvel
+        if (k < 61) return p.ah_vel_obs_scale * in.obj[k - 48];                  // angvel
+        if (k < 68) return gs[k - 61];
+        if (k < 72) return qdiff[k - 68];
+        return act_at(c, st, (size_t)env * AH_NUM_ACT + (k - 72));
+    };
+    const int nobs = p.num_obs;
+    float* ob = st.obs + (size_t)env * nobs;
+    for (int k = lane; k < nobs; k += 64) {
+        float v;
+        if (p.ah_obs_type == 0) {
+            v = full_state(k);
+        } else if (p.ah_obs_type == 1) {
+            // compute_full_observations (:448-460): dof pos, vel, object pose / linvel / angvel, goal, qdiff, actions
+            v = full_state(k < 32 ? k : k + 16);
+        } else {
+            // compute_full_observations(no_vel=True) (:439-446): dof pos, object pose, goal pose, qdiff, actions
+            v = full_state(k < 16 ? k : (k < 23 ? k + 32 : k + 38));
+        }
         ob[k] = v;
-        obs_out_put(c, (size_t)env * AH_NUM_OBS + k, v);
+        obs_out_put(c, (size_t)env * nobs + k, v);
+    }
+    if (p.ah_asymmetric && st.teacher_obs) {
+        float* sb = st.teacher_obs + (size_t)env * AH_NUM_STATES;
+        for (int k = lane; k < AH_NUM_STATES; k += 64) sb[k] = full_state(k);
     }
     if (obs_only) return;
     if (lane == 0) {

@@ -979,6 +979,11 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     if (model->n_actors < 1 || model->n_bodies < model->n_links + params->n_objects) return HA_E_MODEL;
     int fam = family_of(params);
     if (params->task == HA_TASK_UR5SIH && params->num_obs != 108 + 13 * params->n_objects) return HA_E_ARG;
+    // AllegroHand observation types (v15): num_obs is the type's size (allegro_hand.py:106-112)
+    if (params->task == HA_TASK_ALLEGRO_HAND &&
+        (params->ah_obs_type < 0 || params->ah_obs_type > 2 ||
+         params->num_obs != (params->ah_obs_type == 0 ? 88 : (params->ah_obs_type == 1 ? 72 : 50))))
+        return HA_E_ARG;
     if (model->actor_object0 < 0 || model->actor_object0 + params->n_objects > model->n_actors ||
         model->body_object0 < 0 || model->body_object0 + params->n_objects > model->n_bodies)
         return HA_E_MODEL;

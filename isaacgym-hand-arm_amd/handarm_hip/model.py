@@ -134,6 +134,7 @@ class HaParams(C.Structure):
         ("link_lin_damping", f32), ("link_ang_damping", f32), ("edge_rel_tol", f32), ("edge_abs_tol", f32),  # v10
         ("narrow_phase_flags", i32),
         ("pcm_lin_tol", f32), ("pcm_cos_tol", f32),                           # v13
+        ("ah_obs_type", i32), ("ah_asymmetric", i32), ("ah_relative_control", i32), ("ah_speed_dt", f32),   # v15
     ]
 
 
@@ -184,7 +185,7 @@ def default_pcm_slots(n_obj=3):
 
 
 def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, num_actions=11, num_obs=147,
-               n_actors=None, n_bodies=None, n_pcm_slots=None):
+               n_actors=None, n_bodies=None, n_pcm_slots=None, num_states=None):
     """name -> (shape, numpy dtype) of every ha_state_t buffer (Isaac Gym tensor layouts). n_pcm_slots: persistent-
     manifold slots per env (pcm_slots of the model; None: the default Ur5Sih scene's)."""
     if n_pcm_slots is None:
@@ -196,7 +197,8 @@ def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, nu
     return {
         "root_state": ((N * A, 13), f), "rigid_body_state": ((N * B, 13), f), "dof_state": ((N * D, 2), f),
         "net_contact_force": ((N * B, 3), f), "sim_targets": ((N, D), f), "dof_position_targets": ((N, D), f),
-        "actions": ((N, num_actions), f), "obs": ((N, num_obs), f), "teacher_obs": ((N, num_obs), f),
+        "actions": ((N, num_actions), f), "obs": ((N, num_obs), f),
+        "teacher_obs": ((N, num_states if num_states is not None else num_obs), f),
         "rew": ((N,), f), "reset_buf": ((N,), i64), "progress_buf": ((N,), i64), "timeout_buf": ((N,), u8),
         "goal_reached_before": ((N,), u8), "goal_pos": ((N, 3), f), "target_object_index": ((N,), i64),
         "object_configuration_indices": ((N,), i64), "object_indices": ((N, n_obj), i64),
@@ -653,11 +655,25 @@ ALLEGRO_TASK = dict(
     reset_position_noise=0.01, reset_dof_pos_noise=0.2, reset_dof_vel_noise=0.0, act_moving_average=1.0,
     vel_obs_scale=0.2, force_torque_obs_scale=10.0,                      # allegro_hand.py:57-58
     clip_observations=5.0, clip_actions=1.0,
+    # observationType, asymmetric_observations, useRelativeControl, dofSpeedScale (AllegroHand.yaml:14-19,42-43)
+    obs_type="full_state", asymmetric=False, relative_control=False, dof_speed_scale=20.0,
     # hand at (0, 0, 0.5); object at hand + (0, -0.2, 0.06); goal_states = object - 0.04 z; goal actor at
     # goal_states + displacement (allegro_hand.py:284-300,363-365)
     object_init=(0.0, -0.2, 0.56, 0.0, 0.0, 0.0, 1.0), goal_init=(0.0, -0.2, 0.52),
     goal_displacement=(-0.2, -0.06, 0.12),
 )
+
+
+# AllegroHand observation types (allegro_hand.py:99-112): ha_params_t.ah_obs_type and num_obs; the states buffer of
+# asymmetric observations is the 88-float full_state vector (num_states, allegro_hand.py:121-124)
+AH_OBS_TYPES = {"full_state": 0, "full": 1, "full_no_vel": 2}
+AH_NUM_OBS = {"full_state": 88, "full": 72, "full_no_vel": 50}
+AH_NUM_STATES = 88
+
+
+def num_states(params):
+    """teacher_obs width: AllegroHand's states buffer (asymmetric observations) or the task's observation size."""
+    return AH_NUM_STATES if params.task == TASK_ALLEGRO_HAND and params.ah_asymmetric else params.num_obs
 
 
 # AllegroKuka (config C2): cfg/task/AllegroKuka.yaml:9-94,210-231 + env/regrasping.yaml (default subtask here:
@@ -797,6 +813,11 @@ def build_params(cfg=None, task=None):
                   "reset_position_noise", "reset_dof_pos_noise", "reset_dof_vel_noise", "act_moving_average",
                   "vel_obs_scale", "force_torque_obs_scale"]:
             setattr(p, "ah_" + k, c[k])
+        p.ah_obs_type = AH_OBS_TYPES[c["obs_type"]]
+        p.num_obs = AH_NUM_OBS[c["obs_type"]]                 # allegro_hand.py:106-112
+        p.ah_asymmetric = int(bool(c["asymmetric"]))
+        p.ah_relative_control = int(bool(c["relative_control"]))
+        p.ah_speed_dt = c["dof_speed_scale"] * c["dt"]       # shadow_hand_dof_speed_scale * self.dt (python double)
         p.ah_object_init[:] = c["object_init"]
         p.ah_goal_init[:] = c["goal_init"]
         p.ah_goal_displacement[:] = c["goal_displacement"]

@@ -49,7 +49,8 @@ class HandArmSim:
         spec = HM.state_spec(num_envs, n_links=self.num_links, n_dofs=self.num_dofs, n_obj=self.n_obj,
                              num_initial_poses=self.params.num_initial_poses, num_actions=self.params.num_actions,
                              num_obs=self.params.num_obs, n_actors=self.num_actors, n_bodies=self.num_bodies,
-                             n_pcm_slots=HM.pcm_slots(self.model, self.n_obj, self.params))
+                             n_pcm_slots=HM.pcm_slots(self.model, self.n_obj, self.params),
+                             num_states=HM.num_states(self.params))
         spec["stats"] = ((stats_ring, HM.STAT_SIZE), spec["stats"][1])
         spec["term_sums"] = ((stats_ring, 4), spec["term_sums"][1])
         with torch.cuda.device(self.device):

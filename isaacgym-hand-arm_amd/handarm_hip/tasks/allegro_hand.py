@@ -2,11 +2,12 @@
 
 Drop-in for tasks/allegro_hand.py:40 (registered as "AllegroHand" in tasks/__init__.py). Config
 cfg/task/AllegroHand.yaml: 16 DOF Allegro hand (allegro_touch_sensor.urdf, fixed base, gravity off),
-one 0.065 m cube, a goal cube that only carries a pose, observationType "full_state" (88 floats),
-controlFrequencyInv 2, episodeLength 600.
+one 0.065 m cube, a goal cube that only carries a pose, observationType "full_state" (88 floats; "full" 72 and
+"full_no_vel" 50 too, and asymmetric_observations' 88-float states buffer), absolute or relative control
+(useRelativeControl, dofSpeedScale), controlFrequencyInv 2, episodeLength 600.
 
-One fused kernel per step (ha_task_step -> ah_step_kernel): goal resets, reset_idx, absolute targets
-with moving average, 2 x 2 physics substeps, refresh, full_state observations, compute_hand_reward; then a
+One fused kernel per step (ha_task_step -> ah_step_kernel): goal resets, reset_idx, targets (absolute with moving
+average, or relative), 2 x 2 physics substeps, refresh, observations, compute_hand_reward; then a
 one-thread kernel updates the global consecutive_successes average (allegro_hand.py:714-717). No host
 syncs on the step path.
 """
@@ -30,18 +31,21 @@ class AllegroHand:
         self.num_environments = int(env.get("numEnvs", 16384))
         self.num_agents = 1
         self.obs_type = env.get("observationType", "full_state")
-        if self.obs_type != "full_state":
-            raise NotImplementedError("observationType must be 'full_state' (the AllegroHand.yaml default)")
-        if env.get("objectType", "block") != "block" or env.get("useRelativeControl", False) \
-                or float(env.get("forceScale", 0.0)) != 0.0 or env.get("asymmetric_observations", False):
-            raise NotImplementedError("only the AllegroHand.yaml defaults (block, absolute control, no random "
-                                      "forces, symmetric observations) are implemented")
+        if self.obs_type not in HM.AH_OBS_TYPES:                      # allegro_hand.py:102-104
+            raise Exception("Unknown type of observations!\nobservationType should be one of: [openai, full_no_vel, "
+                            "full, full_state]")
+        if env.get("objectType", "block") != "block" or float(env.get("forceScale", 0.0)) != 0.0:
+            raise NotImplementedError("objectType 'block' and forceScale 0 (the AllegroHand.yaml values) are implemented")
+        self.asymmetric_obs = bool(env.get("asymmetric_observations", False))
+        self.use_relative_control = bool(env.get("useRelativeControl", False))
         self.control_freq_inv = int(env.get("controlFrequencyInv", c["control_freq_inv"]))
         self.clip_obs = float(env.get("clipObservations", c["clip_observations"]))
         self.clip_actions = float(env.get("clipActions", c["clip_actions"]))
         self.max_episode_length = int(env.get("episodeLength", c["max_episode_length"]))
         task_cfg = dict(task=HM.TASK_ALLEGRO_HAND, control_freq_inv=self.control_freq_inv,
-                        max_episode_length=self.max_episode_length, seed=int(cfg.get("seed", 42)))
+                        max_episode_length=self.max_episode_length, seed=int(cfg.get("seed", 42)),
+                        obs_type=self.obs_type, asymmetric=self.asymmetric_obs,
+                        relative_control=self.use_relative_control)
         for key, name in [("distRewardScale", "dist_reward_scale"), ("rotRewardScale", "rot_reward_scale"),
                           ("rotEps", "rot_eps"), ("actionPenaltyScale", "action_penalty_scale"),
                           ("successTolerance", "success_tolerance"), ("reachGoalBonus", "reach_goal_bonus"),
@@ -50,14 +54,17 @@ class AllegroHand:
                           ("resetPositionNoise", "reset_position_noise"),
                           ("resetDofPosRandomInterval", "reset_dof_pos_noise"),
                           ("resetDofVelRandomInterval", "reset_dof_vel_noise"),
-                          ("actionsMovingAverage", "act_moving_average")]:
+                          ("actionsMovingAverage", "act_moving_average"), ("dofSpeedScale", "dof_speed_scale")]:
             if key in env:
                 task_cfg[name] = type(c[name])(env[key])
         self.sim = HandArmSim(self.num_environments, sim_device, task_cfg=task_cfg, task=HM.TASK_ALLEGRO_HAND)
         self.sim_flags = 0
         N, t = self.num_environments, self.sim.t
-        self.num_observations, self.num_actions, self.num_states = 88, 16, 0
+        # numObservations by observationType, numStates 88 with asymmetric observations (allegro_hand.py:106-124)
+        self.num_observations, self.num_actions = HM.AH_NUM_OBS[self.obs_type], 16
+        self.num_states = HM.AH_NUM_STATES if self.asymmetric_obs else 0
         self.obs_buf = t["obs"]
+        self.states_buf = t["teacher_obs"] if self.asymmetric_obs else None
         self.rew_buf = t["rew"]
         self.reset_buf = t["reset_buf"]
         self.reset_goal_buf = t["reset_goal_buf"]
@@ -157,12 +164,22 @@ class AllegroHand:
         cs = self.consecutive_successes.view(())                                     # allegro_hand.py:393 (1 value)
         self.extras["consecutive_successes"] = cs.clone() if self.fresh_outputs else cs
         self.obs_dict["obs"] = out.to(self.rl_device)
+        self._put_states()
         return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras
+
+    def get_state(self):
+        """VecTask.get_state (vec_task.py:375-376): the clamped states buffer."""
+        return torch.clamp(self.states_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+
+    def _put_states(self):
+        if self.num_states > 0:                                        # vec_task.py:438-439,471-472,488-489
+            self.obs_dict["states"] = self.get_state()
 
     def reset(self):
         """VecTask.reset (vec_task.py:459-474): compute_observations only."""
         self.sim.task_observe(HM.FLAG_OBS_ONLY)
         self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        self._put_states()
         return self.obs_dict
 
     def reset_idx(self, env_ids, goal_env_ids=None):
@@ -186,5 +203,6 @@ class AllegroHand:
         if len(done_env_ids) > 0:
             self.reset_idx(done_env_ids)
         self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        self._put_states()
         return self.obs_dict, done_env_ids
 

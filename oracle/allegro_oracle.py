@@ -19,7 +19,8 @@ CFG = dict(dist_reward_scale=-10.0, rot_reward_scale=1.0, rot_eps=0.1, action_pe
            force_torque_obs_scale=10.0, reset_position_noise=0.01, reset_dof_pos_noise=0.2,
            reset_dof_vel_noise=0.0, act_moving_average=1.0,
            object_init=(0.0, -0.2, 0.56, 0.0, 0.0, 0.0, 1.0), goal_init=(0.0, -0.2, 0.52),
-           goal_displacement=(-0.2, -0.06, 0.12))
+           goal_displacement=(-0.2, -0.06, 0.12), obs_type="full_state", asymmetric=False, relative_control=False,
+           dof_speed_scale=20.0, dt=0.01667)
 
 
 def _quat_from_angle_axis(angle, axis):
@@ -54,6 +55,33 @@ def observations(dof_pos, dof_vel, dof_force, obj, goal_state, actions, lo, up, 
     o[:, 61:68] = goal_state[:, 0:7]
     o[:, 68:72] = quat_mul(obj[:, 3:7], quat_conjugate(goal_state[:, 3:7]))
     o[:, 72:88] = actions
+    return o
+
+
+def observations_typed(obs_type, dof_pos, dof_vel, dof_force, obj, goal_state, actions, lo, up, c=CFG):
+    """compute_observations (allegro_hand.py:425-432): compute_full_observations(no_vel) (:437-460) for "full_no_vel"
+    (50 floats) and "full" (72), compute_full_state (:484-504) for "full_state" (88)."""
+    if obs_type == "full_state":
+        return observations(dof_pos, dof_vel, dof_force, obj, goal_state, actions, lo, up, c)
+    N = dof_pos.shape[0]
+    qd = quat_mul(obj[:, 3:7], quat_conjugate(goal_state[:, 3:7]))
+    if obs_type == "full_no_vel":
+        o = np.zeros((N, 50), F)
+        o[:, 0:16] = unscale(dof_pos, lo, up)
+        o[:, 16:23] = obj[:, 0:7]
+        o[:, 23:30] = goal_state[:, 0:7]
+        o[:, 30:34] = qd
+        o[:, 34:50] = actions
+        return o
+    o = np.zeros((N, 72), F)
+    o[:, 0:16] = unscale(dof_pos, lo, up)
+    o[:, 16:32] = F(c["vel_obs_scale"]) * dof_vel
+    o[:, 32:39] = obj[:, 0:7]
+    o[:, 39:42] = obj[:, 7:10]
+    o[:, 42:45] = F(c["vel_obs_scale"]) * obj[:, 10:13]
+    o[:, 45:52] = goal_state[:, 0:7]
+    o[:, 52:56] = qd
+    o[:, 56:72] = actions
     return o
 
 
@@ -123,6 +151,13 @@ def targets_from_actions(actions, prev, lo, up, c=CFG):
     return np.maximum(np.minimum(cur, up), lo).astype(F)
 
 
+def targets_relative(actions, prev, lo, up, c=CFG):
+    """allegro_hand.py:602-605 (useRelativeControl): prev_targets + dofSpeedScale * dt * actions, clamped; the scalar
+    product is a python double, rounded once where it meets the float32 tensor."""
+    cur = prev + F(c["dof_speed_scale"] * c["dt"]) * actions
+    return np.maximum(np.minimum(cur, up), lo).astype(F)
+
+
 def step_no_physics(st, actions, draws, lo, up, c=CFG):
     """pre_physics_step -> (no simulate) -> post_physics_step on dict st (mutated):
     dof (N,16,2), root (N,3,13), goal_state (N,7), targets (N,16), reset, reset_goal, progress, successes, cons."""
@@ -137,10 +172,16 @@ def step_no_physics(st, actions, draws, lo, up, c=CFG):
             env_reset(st["root"], st["dof"][..., 0], st["dof"][..., 1], st["targets"], e,
                       draws[e, DRAW_RESET:DRAW_RESET + 37], lo, up, c)
             st["progress"][e], st["reset"][e], st["successes"][e] = 0, 0, 0
-    st["targets"] = targets_from_actions(actions, st["targets"], lo, up, c)
+    if c.get("relative_control", False):
+        st["targets"] = targets_relative(actions, st["targets"], lo, up, c)
+    else:
+        st["targets"] = targets_from_actions(actions, st["targets"], lo, up, c)
     st["progress"] = st["progress"] + 1
-    obs = observations(st["dof"][..., 0], st["dof"][..., 1], np.zeros((N, D), F), st["root"][:, 1],
-                       st["goal_state"], actions, lo, up, c)
+    args = (st["dof"][..., 0], st["dof"][..., 1], np.zeros((N, D), F), st["root"][:, 1], st["goal_state"], actions,
+            lo, up, c)
+    obs = observations_typed(c.get("obs_type", "full_state"), *args)
+    if c.get("asymmetric", False):
+        st["states"] = observations(*args)
     rew, st["reset"], st["reset_goal"], st["progress"], st["successes"], st["cons"] = reward(
         st["root"][:, 1], st["goal_state"], actions, st["reset"], st["reset_goal"], st["progress"], st["successes"],
         st["cons"], c)

@@ -49,7 +49,7 @@ class HostState:
     def __init__(self, num_envs, n_obj=3, num_initial_poses=1, model=None, params=None):
         kw = {}
         if params is not None:
-            kw.update(num_actions=params.num_actions, num_obs=params.num_obs)
+            kw.update(num_actions=params.num_actions, num_obs=params.num_obs, num_states=HM.num_states(params))
             n_obj = params.n_objects
         if model is not None:       # sizes/layout of the model's task (default: Ur5Sih)
             kw.update(n_links=model.n_links, n_dofs=model.n_dofs, n_actors=model.n_actors, n_bodies=model.n_bodies,

@@ -12,6 +12,8 @@ Reference code exercised, unmodified, through a fake ``self`` carrying what ``_c
     then ``post_physics_step`` (:627-633) and VecTask.step's timeout rule (vec_task.py:424), over several
     steps with goal and env resets: ``allegro_steps.npz``. ``torch_rand_float`` is wrapped to record its
     draws per env in the order the device replays them (ah_task.h AH_DRAW_*).
+  * the same steps run with observationType "full" + useRelativeControl and "full_no_vel" +
+    asymmetric_observations (:99-124, 425-504, 602-605): ``allegro_variants.npz`` (``--variants`` writes only it).
 ``gym.simulate`` is a no-op in the fake gym: these goldens pin the task math only.
 """
 import json
@@ -147,14 +149,28 @@ def obs_reward(N=32, steps=5, seed=1):
     np.savez_compressed(os.path.join(HERE, "allegro_obs_reward.npz"), **{k: np.stack(v) for k, v in out.items()})
 
 
-def steps(N=24, T=8, seed=2):
-    """pre_physics_step -> (no physics) -> post_physics_step, with replayable draws."""
+VARIANTS = {  # the allegro_variants.npz runs: (observationType, asymmetric_observations, useRelativeControl)
+    "full_rel": ("full", False, True),
+    "novel_asym": ("full_no_vel", True, False),
+}
+
+
+def steps(N=24, T=8, seed=2, variant=None):
+    """pre_physics_step -> (no physics) -> post_physics_step, with replayable draws. variant: a VARIANTS key (the
+    task's obs_type / asymmetric_obs / use_relative_control set as allegro_hand.py:99-124 would; returns the arrays)."""
     torch.manual_seed(seed)          # seeded before the task is built: __init__'s draw is part of the stream
     mod, t = make_task(N)
+    if variant is not None:
+        t.obs_type, t.asymmetric_obs, t.use_relative_control = VARIANTS[variant]
+        t.num_observations = {"full_no_vel": 50, "full": 72, "full_state": 88}[t.obs_type]
+        t.obs_buf = torch.zeros(N, t.num_observations)
+        t.num_states = 88 if t.asymmetric_obs else 0
+        t.states_buf = torch.zeros(N, 88)
     g = torch.Generator().manual_seed(seed)
     draws = np.zeros((T, N, DRAW_STRIDE), np.float32)
     cur = {"step": 0, "phase": None, "ids": None}
-    real = mod.torch_rand_float
+    real = getattr(mod, "_real_torch_rand_float", mod.torch_rand_float)     # (a previous run left its wrapper)
+    mod._real_torch_rand_float = real
 
     def rec(lower, upper, shape, device):
         v = real(lower, upper, shape, device)
@@ -205,14 +221,30 @@ def steps(N=24, T=8, seed=2):
                      ("cons", t.consecutive_successes), ("targets_after", t.prev_targets), ("dof_after", t.dof_state),
                      ("root_after", t.root_state_tensor)]:
             out[k].append(v.clone().numpy())
+        if variant is not None:
+            out.setdefault("states", []).append(t.states_buf.clone().numpy())
     res = {k: np.stack(v) for k, v in out.items()}
     res["draws"] = draws
     res["seed"] = np.array(seed)
+    if variant is not None:
+        return res
     np.savez_compressed(os.path.join(HERE, "allegro_steps.npz"), **res)
+
+
+def variants():
+    """allegro_variants.npz: the steps run per VARIANTS entry, keys '<variant>/<array>'."""
+    out = {}
+    for v in VARIANTS:
+        for k, a in steps(variant=v, seed=5).items():
+            out[v + "/" + k] = a
+    np.savez_compressed(os.path.join(HERE, "allegro_variants.npz"), **out)
 
 
 if __name__ == "__main__":
     refload.install()
-    obs_reward()
-    steps()
-    print("wrote allegro_obs_reward.npz, allegro_steps.npz")
+    if "--variants" not in sys.argv:
+        obs_reward()
+        steps()
+        print("wrote allegro_obs_reward.npz, allegro_steps.npz")
+    variants()
+    print("wrote allegro_variants.npz")

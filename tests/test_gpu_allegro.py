@@ -94,6 +94,62 @@ def test_allegro_step_with_resets_replayed_against_reference_goldens():
         np.testing.assert_allclose(get(sim, "consecutive_successes")[0], d["cons"][t][0], rtol=1e-6)
 
 
+@pytest.mark.parametrize("variant,cfg", [("full_rel", dict(obs_type="full", relative_control=True)),
+                                         ("novel_asym", dict(obs_type="full_no_vel", asymmetric=True))])
+def test_allegro_observation_types_and_relative_control_against_reference_goldens(variant, cfg):
+    """The same fused step without physics for observationType "full" (72) + useRelativeControl and "full_no_vel"
+    (50) + asymmetric_observations (the states buffer: teacher_obs, 88 floats) (allegro_variants.npz)."""
+    g = np.load(os.path.join(G, "allegro_variants.npz"))
+    d = {k.split("/", 1)[1]: g[k] for k in g.files if k.startswith(variant + "/")}
+    T, N = d["rew"].shape
+    sim = make_sim(N, **cfg)
+    assert sim.t["obs"].shape[1] == d["obs"].shape[-1]
+    for k, gk in [("dof_state", "dof_state"), ("goal_state", "goal_state"), ("dof_position_targets", "targets"),
+                  ("reset_buf", "reset_in"), ("reset_goal_buf", "reset_goal_in"), ("successes", "successes_in")]:
+        put(sim, k, d[gk][0])
+    flags = HM.FLAG_NO_PHYSICS | HM.FLAG_REPLAY_DRAWS
+    for t in range(T):
+        put(sim, "root_state", d["root_state"][t])
+        put(sim, "progress_buf", d["progress_in"][t])
+        put(sim, "actions", d["actions"][t])
+        dr = np.zeros((N, HM.DRAW_STRIDE), np.float32)
+        dr[:, :d["draws"].shape[-1]] = d["draws"][t]
+        put(sim, "reset_draws", dr)
+        sim.task_step(flags)
+        np.testing.assert_array_equal(get(sim, "reset_buf"), d["reset"][t])
+        np.testing.assert_array_equal(get(sim, "timeout_buf").astype(bool), d["timeout"][t])
+        np.testing.assert_allclose(get(sim, "dof_position_targets"), d["targets_after"][t], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(get(sim, "obs"), d["obs"][t], rtol=1e-5, atol=2e-6)
+        np.testing.assert_allclose(get(sim, "rew"), d["rew"][t], rtol=1e-5, atol=1e-4)
+        if cfg.get("asymmetric"):
+            np.testing.assert_allclose(get(sim, "teacher_obs"), d["states"][t], rtol=1e-5, atol=2e-6)
+
+
+def test_allegro_vectask_asymmetric_relative_episode():
+    """VecTask surface with the options: obs_dict["obs"] 50 wide, obs_dict["states"] the clamped 88-float states,
+    num_states 88; relative control moves the targets by at most dofSpeedScale * dt per step."""
+    need_gpu()
+    from handarm_hip.tasks import isaacgym_task_map
+    n = 256
+    env = isaacgym_task_map["AllegroHand"]({"env": {"numEnvs": n, "observationType": "full_no_vel",
+                                                    "asymmetric_observations": True, "useRelativeControl": True}},
+                                           "cuda:0", "cuda:0")
+    assert (env.num_obs, env.num_states) == (50, 88)
+    o = env.reset()
+    assert o["obs"].shape == (n, 50) and o["states"].shape == (n, 88)
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    _, _, d, _ = env.step(torch.zeros((n, 16), device="cuda:0"))
+    for _ in range(20):
+        prev, was_reset = env.prev_targets.clone(), d.bool().clone()      # envs flagged now reset in the next step
+        o, r, d, e = env.step(torch.rand((n, 16), device="cuda:0", generator=g) * 2 - 1)
+        moved = (env.prev_targets - prev).abs()[~was_reset]
+        assert moved.max().item() <= 20.0 * 0.01667 + 1e-5
+        assert o["states"].shape == (n, 88) and torch.isfinite(o["states"]).all()
+        assert o["states"].abs().max().item() <= 5.0 and torch.isfinite(o["obs"]).all()
+        # the states' object pose columns are the observation's (full_state 48:55 vs full_no_vel 16:23)
+        torch.testing.assert_close(o["states"][:, 48:55], o["obs"][:, 16:23])
+
+
 def _oracle_and_sim(n, seed):
     from oracle.oracle_lib import HostState, Oracle
     sim = make_sim(n)
