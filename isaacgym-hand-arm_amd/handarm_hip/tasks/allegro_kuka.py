@@ -67,9 +67,10 @@ class AllegroKuka:
         if env.get("observationType", "full_state") != "full_state" or env.get("objectType", "block") != "block":
             raise NotImplementedError("observationType 'full_state' and objectType 'block' (the AllegroKuka.yaml "
                                       "values) are implemented")
-        if env.get("useRelativeControl", False) or env.get("privilegedActions", False) or \
-                env.get("randomizeObjectDimensions", True) is False:
-            raise NotImplementedError("only the AllegroKuka.yaml defaults for relative control, privileged actions "
+        if env.get("useRelativeControl", False):       # the reference's own answer (allegro_kuka_base.py:1373-1374)
+            raise NotImplementedError("Use relative control False for now")
+        if env.get("privilegedActions", False) or env.get("randomizeObjectDimensions", True) is False:
+            raise NotImplementedError("only the AllegroKuka.yaml defaults for privileged actions (object torques) "
                                       "and object dimensions are implemented")
         family = (True, False, False) if sub == "throw" else (True, True, True)      # env/throw.yaml:15-18
         if tuple(bool(env.get(k, d)) for k, d in zip(("withSmallCuboids", "withBigCuboids", "withSticks"), family)) \
