@@ -2118,6 +2118,9 @@ HD void detect(SimCtx& c) {
     npairs += NLH * NS;
     wsync();
     for (int base = 0; base < npairs; base += 64) {
+#ifdef HA_PROFILE
+        unsigned long long _b0 = __builtin_amdgcn_s_memtime();
+#endif
         // parallel broad phase: one pair per lane
         bool cand = false;
         int p = base + lane;
@@ -2196,6 +2199,14 @@ HD void detect(SimCtx& c) {
         uint64_t vmask = __ballot(c.pcm && cand && pcm_valid_lane(c, p, kind, A, B));
         // and the candidates' separating-face records, one byte load each
         int frec = (cand && c.pairf) ? (int)c.pairf[p] : 0xFF;
+#ifdef HA_PROFILE
+        {   // the batch's broad phase: sphere / box tests, record validity, face-record loads (waited for here)
+            int fw = wave_min_i(frec);
+            wsync();
+            PROF_COUNT(93, __builtin_amdgcn_s_memtime() - _b0 + (fw < -1 ? 1 : 0));
+            PROF_COUNT(94, 1);
+        }
+#endif
         // one iteration per piece pair: a compound object (several convex pieces, ha_model_t v8) runs piece
         // pairs j = 0 .. np-1 of a candidate pair and then emits a single <= 4-point manifold for the object pair
         // (the oracle's gather_begin / gather_end). One loop and one call site per narrow phase (a single inlined

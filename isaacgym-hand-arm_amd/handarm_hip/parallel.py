@@ -54,10 +54,10 @@ def init_distributed(backend=None):
 
 def describe():
     """The process group as bench.py reports it: backend and the world size an all-reduce of ones over it counts
-    (so a scaling record shows that RCCL saw every rank)."""
-    if world() == 1:
-        return {"backend": None, "world_size": 1}
+    (so a scaling record shows that RCCL saw every rank). No process group: backend None."""
     import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return {"backend": None, "world_size": 1}
     dev = f"cuda:{torch.cuda.current_device()}" if dist.get_backend() == "nccl" else "cpu"
     t = torch.ones(1, device=dev)
     dist.all_reduce(t)

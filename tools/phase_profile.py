@@ -54,6 +54,9 @@ if __name__ == "__main__":
             t_, n_, h_ = (10 + k, 15 + k, 20 + k) if k < 5 else (80, 81, 82)       # self pairs (kind 5) at 80..82
             print(f"    narrow {name:10s}: {buf[n_] / sub:6.2f} pairs/substep, {buf[h_] / sub:6.2f} with contacts, "
                   f"{100.0 * buf[t_] / tot:5.1f}% of substep cycles", flush=True)
+        if buf[94]:
+            print(f"    broad phase: {buf[94] / sub:6.2f} batches of 64 pairs/substep (tests, record validity, face-record "
+                  f"loads) {100.0 * buf[93] / tot:5.1f}% of substep cycles", flush=True)
         if buf[90]:
             print(f"    pair face records: {buf[91] / sub:6.2f} checks/substep, {buf[92] / sub:6.2f} pairs skipped; checks "
                   f"{100.0 * buf[90] / tot:5.1f}% of substep cycles", flush=True)
