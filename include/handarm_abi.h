@@ -327,6 +327,13 @@ typedef struct ha_params_t {
                                         * to teacher_obs ([N][88], VecTask's states_buf) as well */
     int32_t ah_relative_control;       /* targets = prev_targets + dofSpeedScale * dt * actions, clamped (no average) */
     float ah_speed_dt;                 /* shadow_hand_dof_speed_scale * dt: python double, rounded once */
+    /* random object forces (forceScale > 0; allegro_hand.py:66-70,557-560,617-625): decay by ah_force_decay_step
+     * (torch.pow(forceDecay, dt / forceDecayInterval) in fp32) each step, then with probability random_force_prob
+     * (drawn log-uniformly in [lo, hi] at reset) a new force N(0, 1)^3 * mass * forceScale in the object frame, applied
+     * to the first physics call of the step (an applied force lasts one gym.simulate). Per-env state in task_state
+     * (AH_TS_* of ah_task.h) */
+    float ah_force_scale, ah_force_prob_lo, ah_force_prob_hi, ah_force_decay_step;
+    float ah_object_rb_mass;           /* object_rb_masses: the cube's mass */
 } ha_params_t;
 
 /* Device buffers (caller-allocated). Layouts match the Isaac Gym tensors exactly. */

@@ -18,9 +18,23 @@
 //   [0, 4)   reset_target_pose(goal_env_ids): torch_rand_float(-1, 1, (n, 4))
 //   [4, 41)  reset_idx rand_floats: torch_rand_float(-1, 1, (n, 2 * 16 + 5))
 //   [41, 45) reset_idx -> reset_target_pose(env_ids): torch_rand_float(-1, 1, (n, 4))
+//   [45]     reset_idx: random_force_prob's torch.rand (:559-560)
+//   [46]     pre_physics_step: torch.rand(num_envs) against random_force_prob (:621)
+//   [47, 50) torch.randn(3) of a selected env (:622-623); [50] 1 when the reference selected the env (the host's
+//            comparison, so a replayed run cannot differ from it by a last-bit difference of exp / log)
 #define AH_DRAW_GOAL 0
 #define AH_DRAW_RESET 4
 #define AH_DRAW_RESET_GOAL 41
+#define AH_DRAW_FORCE_PROB 45
+#define AH_DRAW_FORCE_U 46
+#define AH_DRAW_FORCE_N 47
+#define AH_DRAW_FORCE_SEL 50
+// an AllegroHand env's task_state row (random object forces, forceScale > 0): the force in the object frame, its
+// random_force_prob and the counter of its device-mode force draws
+#define AH_TS_FORCE 0
+#define AH_TS_PROB 3
+#define AH_TS_RNG 4
+#define AH_TS_N 8
 
 // What the observation reads after the refresh: dof pos / vel / force, object root state.
 struct AhIn {
@@ -60,7 +74,7 @@ HD void ah_randomize_rotation(float r0, float r1, float* q) {
 // uses draw [0, 4); a full reset re-draws the goal at [41, 45) after the object/hand draw [4, 41), so
 // the later draw wins exactly as in the reference. The hand/object state is reset in LDS (load_env ran
 // first) and in the root/dof tensors.
-HD void ah_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags, bool goal, bool full) {
+HD void ah_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags, bool goal, bool full, float& tsv) {
     EnvLDS& s = *c.s;
     const ha_params_t& p = *c.p;
     const ha_model_t& m = *c.m;
@@ -118,6 +132,14 @@ HD void ah_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags, bool 
             st.reset_buf[env] = 0;
             st.successes[env] = 0.0f;
         }
+        // rb_forces[env_ids] = 0; random_force_prob = exp((log lo - log hi) * U[0, 1) + log hi) (:532,557-560)
+        if (lane >= AH_TS_FORCE && lane < AH_TS_FORCE + 3) tsv = 0.0f;
+        if (lane == AH_TS_PROB) {
+            float u = (flags & HA_FLAG_REPLAY_DRAWS) ? st.reset_draws[(size_t)env * HA_DRAW_STRIDE + AH_DRAW_FORCE_PROB]
+                                                     : uniform01(p.seed, env, st.episode[env], 64 + AH_DRAW_FORCE_PROB);
+            float llo = logf(p.ah_force_prob_lo), lhi = logf(p.ah_force_prob_hi);
+            tsv = expf((llo - lhi) * u + lhi);
+        }
     }
     if (lane == 0 && (goal || full)) st.episode[env] = st.episode[env] + 1;
     wsync();
@@ -146,6 +168,32 @@ HD void ah_controller(SimCtx& c, const ha_state_t& st, int env) {
         prev[lane] = cur;
         s.tgt[lane] = cur;
     }
+    wsync();
+}
+
+// random object forces (allegro_hand.py:617-625): decay, a new N(0, 1)^3 * mass * forceScale force with probability
+// random_force_prob, applied in LOCAL_SPACE at the object COM -> the world force of the step's first physics call
+HD void ah_forces(SimCtx& c, const ha_state_t& st, int env, uint32_t flags, float& tsv) {
+    const ha_params_t& p = *c.p;
+    int lane = c.lane;
+    if (p.ah_force_scale <= 0.0f) return;
+    bool replay = (flags & HA_FLAG_REPLAY_DRAWS) != 0;
+    const float* dr = st.reset_draws + (size_t)env * HA_DRAW_STRIDE;
+    uint32_t ctr = __float_as_uint(bcast(tsv, AH_TS_RNG));
+    float prob = bcast(tsv, AH_TS_PROB);
+    float u = replay ? dr[AH_DRAW_FORCE_U] : uniform01(p.seed ^ 0x5EED5EEDULL, env, ctr, 0);
+    bool sel = replay ? dr[AH_DRAW_FORCE_SEL] != 0.0f : u < prob;
+    if (lane >= AH_TS_FORCE && lane < AH_TS_FORCE + 3) {
+        int k = lane - AH_TS_FORCE;
+        tsv = tsv * p.ah_force_decay_step;
+        if (sel) {
+            float g = replay ? dr[AH_DRAW_FORCE_N + k] : gauss01(p.seed ^ 0x5EED5EEDULL, env, ctr, 1 + k);
+            tsv = (g * p.ah_object_rb_mass) * p.ah_force_scale;
+        }
+    }
+    if (lane == AH_TS_RNG) tsv = __uint_as_float(ctr + 1u);
+    f3 fl = mk3(bcast(tsv, AH_TS_FORCE), bcast(tsv, AH_TS_FORCE + 1), bcast(tsv, AH_TS_FORCE + 2));
+    if (lane == 0) st3(c.o[0].ofx, qrot(ldq(c.o[0].oq), fl));
     wsync();
 }
 

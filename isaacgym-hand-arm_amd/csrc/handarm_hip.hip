@@ -362,10 +362,15 @@ __device__ void snapshot_from_tensors(SimCtx& c, const ha_state_t& st, int env, 
 // always inlined: as an outlined call (the inliner's choice once it grows past its threshold) the step runs
 // ~40% slower (call ABI: stack spills, no cross-phase register allocation)
 template <class PC>
+// n_calls gym.simulate calls. An applied object force (ha_state_t.object_force for ha_simulate, the tasks' random
+// forces) lasts one call: apply_rigid_body_force_tensors acts on the next simulate (the oracle's simulate_env alike)
 __device__ __forceinline__ void run_physics(SimCtx& c, int n_calls) {
     float hdt = c.p->dt / (float)c.p->substeps;
-    for (int k = 0; k < n_calls; k++)
+    for (int k = 0; k < n_calls; k++) {
         for (int sub = 0; sub < c.p->substeps; sub++) substep<PC>(c, hdt);
+        if (c.lane < c.NO) c.o[c.lane].ofx[0] = c.o[c.lane].ofx[1] = c.o[c.lane].ofx[2] = 0.0f;
+        wsync();
+    }
 }
 
 // AllegroHand observation staging
@@ -633,14 +638,20 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
         return;
     }
     if (TASK == HA_TASK_ALLEGRO_HAND) {
-        // pre_physics_step (allegro_hand.py:586-625): goal / env resets, then targets from the actions
+        // pre_physics_step (allegro_hand.py:586-625): goal / env resets, targets from the actions, random forces.
+        // Lane k holds task_state field k (AH_TS_*) in tsv
+        float* tsg = S.task_state ? S.task_state + (size_t)env * HA_AK_TS : nullptr;
+        float tsv = (tsg && c.lane < AH_TS_N) ? tsg[c.lane] : 0.0f;
         bool goal = S.reset_goal_buf[env] != 0, full = S.reset_buf[env] != 0;
-        if (goal || full) ah_reset(c, S, env, flags, goal, full);
+        if (goal || full) ah_reset(c, S, env, flags, goal, full, tsv);
         if (MODE == MODE_RESET) {
+            if (tsg && c.lane < AH_TS_N) tsg[c.lane] = tsv;
             store_env(c, S, env);
             return;
         }
         ah_controller(c, S, env);
+        ah_forces(c, S, env, flags, tsv);
+        if (tsg && c.lane < AH_TS_N) tsg[c.lane] = tsv;
         if (!(flags & HA_FLAG_NO_PHYSICS)) run_physics<PC>(c, c.p->control_freq_inv);   // vec_task.py:409-412
         after_physics(c, env);
         store_env(c, S, env);

@@ -135,6 +135,8 @@ class HaParams(C.Structure):
         ("narrow_phase_flags", i32),
         ("pcm_lin_tol", f32), ("pcm_cos_tol", f32),                           # v13
         ("ah_obs_type", i32), ("ah_asymmetric", i32), ("ah_relative_control", i32), ("ah_speed_dt", f32),   # v15
+        ("ah_force_scale", f32), ("ah_force_prob_lo", f32), ("ah_force_prob_hi", f32), ("ah_force_decay_step", f32),
+        ("ah_object_rb_mass", f32),
     ]
 
 
@@ -657,6 +659,8 @@ ALLEGRO_TASK = dict(
     clip_observations=5.0, clip_actions=1.0,
     # observationType, asymmetric_observations, useRelativeControl, dofSpeedScale (AllegroHand.yaml:14-19,42-43)
     obs_type="full_state", asymmetric=False, relative_control=False, dof_speed_scale=20.0,
+    # forceScale, forceProbRange, forceDecay, forceDecayInterval (AllegroHand.yaml:26-29; allegro_hand.py:66-70)
+    force_scale=0.0, force_prob_range=(0.001, 0.1), force_decay=0.99, force_decay_interval=0.08,
     # hand at (0, 0, 0.5); object at hand + (0, -0.2, 0.06); goal_states = object - 0.04 z; goal actor at
     # goal_states + displacement (allegro_hand.py:284-300,363-365)
     object_init=(0.0, -0.2, 0.56, 0.0, 0.0, 0.0, 1.0), goal_init=(0.0, -0.2, 0.52),
@@ -818,6 +822,12 @@ def build_params(cfg=None, task=None):
         p.ah_asymmetric = int(bool(c["asymmetric"]))
         p.ah_relative_control = int(bool(c["relative_control"]))
         p.ah_speed_dt = c["dof_speed_scale"] * c["dt"]       # shadow_hand_dof_speed_scale * self.dt (python double)
+        import torch
+        p.ah_force_scale = c["force_scale"]
+        p.ah_force_prob_lo, p.ah_force_prob_hi = c["force_prob_range"]
+        # torch.pow(to_torch(forceDecay), dt / forceDecayInterval): a float32 tensor to a python-double power
+        p.ah_force_decay_step = float(torch.pow(torch.tensor(c["force_decay"], dtype=torch.float32),
+                                                c["dt"] / c["force_decay_interval"]))
         p.ah_object_init[:] = c["object_init"]
         p.ah_goal_init[:] = c["goal_init"]
         p.ah_goal_displacement[:] = c["goal_displacement"]

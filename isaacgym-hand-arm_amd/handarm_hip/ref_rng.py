@@ -143,10 +143,15 @@ class KukaDraws:
 class AllegroDraws:
     """The draws of one AllegroHand pre_physics_step (allegro_hand.py:586-599), slot layout of ah_task.h."""
 
-    def __init__(self, num_envs, num_dofs=16):
+    def __init__(self, num_envs, num_dofs=16, force_scale=0.0, force_prob_range=(0.001, 0.1)):
         self.n = num_envs
         self.nd = num_dofs
-        torch.rand(num_envs, device="cpu")                             # random_force_prob at __init__ (:193-194)
+        self.force_scale = float(force_scale)
+        self.lo, self.hi = torch.tensor(force_prob_range, dtype=torch.float32)
+        self.prob = self._prob(torch.rand(num_envs, device="cpu"))     # random_force_prob at __init__ (:191-194)
+
+    def _prob(self, u):
+        return torch.exp((torch.log(self.lo) - torch.log(self.hi)) * u + torch.log(self.hi))
 
     def step(self, reset, reset_goal):
         N = self.n
@@ -159,7 +164,16 @@ class AllegroDraws:
             R = len(env_ids)
             D[env_ids, 4:4 + 2 * self.nd + 5] = torch_rand_float(-1.0, 1.0, (R, 2 * self.nd + 5))
             D[env_ids, 41:45] = torch_rand_float(-1.0, 1.0, (R, 4))   # reset_target_pose(env_ids)
-            torch.rand(R, device="cpu")                                 # random_force_prob (:559-560)
+            u = torch.rand(R, device="cpu")                             # random_force_prob (:557-560)
+            D[env_ids, 45] = u
+            self.prob[env_ids] = self._prob(u)
+        if self.force_scale > 0.0:                                      # random forces (:617-623)
+            u = torch.rand(N, device="cpu")
+            D[:, 46] = u
+            idx = (u < self.prob).nonzero(as_tuple=False)              # force_indices, (k, 1)
+            g = torch.randn((len(idx), 1, 3), device="cpu")
+            D[idx[:, 0], 47:50] = g[:, 0, :]
+            D[idx[:, 0], 50] = 1.0                                      # the selection (ah_task.h AH_DRAW_FORCE_SEL)
         return D
 
 

@@ -69,6 +69,8 @@ class HandArmSim:
         if task == HM.TASK_ALLEGRO_KUKA:
             self._init_kuka()
         h = C.c_void_p()
+        if task == HM.TASK_ALLEGRO_HAND:            # object_rb_masses (allegro_hand.py:355-357): the cube's mass
+            self.params.ah_object_rb_mass = self.model.pool_mass[0]
         _lib.check(self.lib.ha_create(C.byref(self.model), C.byref(self.params), num_envs, C.byref(h)), "ha_create")
         self.h = h
         # contacts per substep the kernel family holds (clutter 84, Ur5Sih 21, AllegroKuka 21, AllegroHand 12)

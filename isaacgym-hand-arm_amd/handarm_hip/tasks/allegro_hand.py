@@ -4,7 +4,7 @@ Drop-in for tasks/allegro_hand.py:40 (registered as "AllegroHand" in tasks/__ini
 cfg/task/AllegroHand.yaml: 16 DOF Allegro hand (allegro_touch_sensor.urdf, fixed base, gravity off),
 one 0.065 m cube, a goal cube that only carries a pose, observationType "full_state" (88 floats; "full" 72 and
 "full_no_vel" 50 too, and asymmetric_observations' 88-float states buffer), absolute or relative control
-(useRelativeControl, dofSpeedScale), controlFrequencyInv 2, episodeLength 600.
+(useRelativeControl, dofSpeedScale), random object forces (forceScale), controlFrequencyInv 2, episodeLength 600.
 
 One fused kernel per step (ha_task_step -> ah_step_kernel): goal resets, reset_idx, targets (absolute with moving
 average, or relative), 2 x 2 physics substeps, refresh, observations, compute_hand_reward; then a
@@ -34,8 +34,8 @@ class AllegroHand:
         if self.obs_type not in HM.AH_OBS_TYPES:                      # allegro_hand.py:102-104
             raise Exception("Unknown type of observations!\nobservationType should be one of: [openai, full_no_vel, "
                             "full, full_state]")
-        if env.get("objectType", "block") != "block" or float(env.get("forceScale", 0.0)) != 0.0:
-            raise NotImplementedError("objectType 'block' and forceScale 0 (the AllegroHand.yaml values) are implemented")
+        if env.get("objectType", "block") != "block":
+            raise NotImplementedError("objectType 'block' (the AllegroHand.yaml value) is implemented")
         self.asymmetric_obs = bool(env.get("asymmetric_observations", False))
         self.use_relative_control = bool(env.get("useRelativeControl", False))
         self.control_freq_inv = int(env.get("controlFrequencyInv", c["control_freq_inv"]))
@@ -54,9 +54,13 @@ class AllegroHand:
                           ("resetPositionNoise", "reset_position_noise"),
                           ("resetDofPosRandomInterval", "reset_dof_pos_noise"),
                           ("resetDofVelRandomInterval", "reset_dof_vel_noise"),
-                          ("actionsMovingAverage", "act_moving_average"), ("dofSpeedScale", "dof_speed_scale")]:
+                          ("actionsMovingAverage", "act_moving_average"), ("dofSpeedScale", "dof_speed_scale"),
+                          ("forceScale", "force_scale"), ("forceDecay", "force_decay"),
+                          ("forceDecayInterval", "force_decay_interval")]:
             if key in env:
                 task_cfg[name] = type(c[name])(env[key])
+        if "forceProbRange" in env:
+            task_cfg["force_prob_range"] = tuple(float(x) for x in env["forceProbRange"])
         self.sim = HandArmSim(self.num_environments, sim_device, task_cfg=task_cfg, task=HM.TASK_ALLEGRO_HAND)
         self.sim_flags = 0
         N, t = self.num_environments, self.sim.t
@@ -95,7 +99,8 @@ class AllegroHand:
         # seed-faithful draws (handarm_hip/ref_rng.py): every reset value from torch's global CPU generator in
         # the reference's order (the __init__ random_force_prob draw happens here, as at allegro_hand.py:193)
         self.reference_rng = bool(cfg.get("sim", {}).get("reference_rng", False))
-        self._rr = RR.AllegroDraws(N) if self.reference_rng else None
+        self._rr = RR.AllegroDraws(N, force_scale=self.sim.cfg["force_scale"],
+                                   force_prob_range=self.sim.cfg["force_prob_range"]) if self.reference_rng else None
         self.extras = {}
         self.obs_dict = {}
         # obs_dict["obs"] = clamp(obs_buf) by the step launch (ha_task_step_io) into one of two alternating buffers: step t's obs

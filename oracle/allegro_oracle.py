@@ -20,7 +20,27 @@ CFG = dict(dist_reward_scale=-10.0, rot_reward_scale=1.0, rot_eps=0.1, action_pe
            reset_dof_vel_noise=0.0, act_moving_average=1.0,
            object_init=(0.0, -0.2, 0.56, 0.0, 0.0, 0.0, 1.0), goal_init=(0.0, -0.2, 0.52),
            goal_displacement=(-0.2, -0.06, 0.12), obs_type="full_state", asymmetric=False, relative_control=False,
-           dof_speed_scale=20.0, dt=0.01667)
+           dof_speed_scale=20.0, dt=0.01667, force_scale=0.0, force_prob_range=(0.001, 0.1), force_decay=0.99,
+           force_decay_interval=0.08, object_rb_mass=0.10985)
+DRAW_FORCE_PROB, DRAW_FORCE_U, DRAW_FORCE_N, DRAW_FORCE_SEL = 45, 46, 47, 50   # ah_task.h AH_DRAW_FORCE_*
+
+
+def force_prob(u, c=CFG):
+    """random_force_prob (allegro_hand.py:557-560): exp((log lo - log hi) u + log hi) in float32."""
+    lo, hi = np.log(np.asarray(c["force_prob_range"], F)).astype(F)
+    return np.exp((lo - hi) * np.asarray(u, F) + hi).astype(F)
+
+
+def forces_step(force, draws, c=CFG):
+    """pre_physics_step's random forces (:617-623) on force (N, 3), object frame: decay by
+    torch.pow(forceDecay, dt / forceDecayInterval) (fp32), then N(0, 1)^3 * mass * forceScale for the envs the
+    draws select (slot 50: the reference's torch.rand(N) < random_force_prob)."""
+    import torch
+    decay = F(torch.pow(torch.tensor(c["force_decay"], dtype=torch.float32), c["dt"] / c["force_decay_interval"]))
+    force = (force * decay).astype(F)
+    sel = draws[:, DRAW_FORCE_SEL] != 0
+    force[sel] = (draws[sel, DRAW_FORCE_N:DRAW_FORCE_N + 3] * F(c["object_rb_mass"])) * F(c["force_scale"])
+    return force
 
 
 def _quat_from_angle_axis(angle, axis):
@@ -172,10 +192,15 @@ def step_no_physics(st, actions, draws, lo, up, c=CFG):
             env_reset(st["root"], st["dof"][..., 0], st["dof"][..., 1], st["targets"], e,
                       draws[e, DRAW_RESET:DRAW_RESET + 37], lo, up, c)
             st["progress"][e], st["reset"][e], st["successes"][e] = 0, 0, 0
+            if "force" in st:                                    # rb_forces = 0, random_force_prob (:532,557-560)
+                st["force"][e] = 0
+                st["prob"][e] = force_prob(draws[e, DRAW_FORCE_PROB], c)
     if c.get("relative_control", False):
         st["targets"] = targets_relative(actions, st["targets"], lo, up, c)
     else:
         st["targets"] = targets_from_actions(actions, st["targets"], lo, up, c)
+    if c.get("force_scale", 0.0) > 0.0:
+        st["force"] = forces_step(st["force"], draws, c)
     st["progress"] = st["progress"] + 1
     args = (st["dof"][..., 0], st["dof"][..., 1], np.zeros((N, D), F), st["root"][:, 1], st["goal_state"], actions,
             lo, up, c)

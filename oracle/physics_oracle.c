@@ -1433,8 +1433,12 @@ static void simulate_env(const hao_handle h, ha_state_t* S, int env, int n_calls
     load_env(h, S, env, &e, 1);
     e.dr = (h->p.dr_enable && S->dr_scale) ? S->dr_scale + (size_t)env * HA_DR_SIZE : NULL;
     float hdt = h->p.dt / (float)h->p.substeps;
-    for (int c = 0; c < n_calls; c++)
+    for (int c = 0; c < n_calls; c++) {
         for (int s = 0; s < h->p.substeps; s++) substep(h, &e, hdt);
+        /* an applied force lasts one gym.simulate (apply_rigid_body_force_tensors, then the next simulate call):
+         * the later calls of a multi-call launch run without it (handarm_hip.hip run_physics force_once) */
+        for (int o = 0; o < NOBJ; o++) e.ofx[o] = (v3){0.0f, 0.0f, 0.0f};
+    }
     /* net contact force of the last substep (PhysX reports the last substep's forces) */
     store_env(h, S, env, &e);
 }

@@ -12,8 +12,9 @@ Reference code exercised, unmodified, through a fake ``self`` carrying what ``_c
     then ``post_physics_step`` (:627-633) and VecTask.step's timeout rule (vec_task.py:424), over several
     steps with goal and env resets: ``allegro_steps.npz``. ``torch_rand_float`` is wrapped to record its
     draws per env in the order the device replays them (ah_task.h AH_DRAW_*).
-  * the same steps run with observationType "full" + useRelativeControl and "full_no_vel" +
-    asymmetric_observations (:99-124, 425-504, 602-605): ``allegro_variants.npz`` (``--variants`` writes only it).
+  * the same steps run with observationType "full" + useRelativeControl, "full_no_vel" + asymmetric_observations
+    and forceScale 1 (:99-124, 425-504, 557-560, 602-605, 617-623; torch.rand / torch.randn recorded too):
+    ``allegro_variants.npz`` (``--variants`` writes only it).
 ``gym.simulate`` is a no-op in the fake gym: these goldens pin the task math only.
 """
 import json
@@ -149,10 +150,12 @@ def obs_reward(N=32, steps=5, seed=1):
     np.savez_compressed(os.path.join(HERE, "allegro_obs_reward.npz"), **{k: np.stack(v) for k, v in out.items()})
 
 
-VARIANTS = {  # the allegro_variants.npz runs: (observationType, asymmetric_observations, useRelativeControl)
-    "full_rel": ("full", False, True),
-    "novel_asym": ("full_no_vel", True, False),
+VARIANTS = {  # the allegro_variants.npz runs: (observationType, asymmetric_observations, useRelativeControl, forceScale)
+    "full_rel": ("full", False, True, 0.0),
+    "novel_asym": ("full_no_vel", True, False, 0.0),
+    "force": ("full_state", False, False, 1.0),
 }
+FORCE_STRIDE = 51            # draw slots with the random-force draws (ah_task.h AH_DRAW_FORCE_*)
 
 
 def steps(N=24, T=8, seed=2, variant=None):
@@ -161,13 +164,13 @@ def steps(N=24, T=8, seed=2, variant=None):
     torch.manual_seed(seed)          # seeded before the task is built: __init__'s draw is part of the stream
     mod, t = make_task(N)
     if variant is not None:
-        t.obs_type, t.asymmetric_obs, t.use_relative_control = VARIANTS[variant]
+        t.obs_type, t.asymmetric_obs, t.use_relative_control, t.force_scale = VARIANTS[variant]
         t.num_observations = {"full_no_vel": 50, "full": 72, "full_state": 88}[t.obs_type]
         t.obs_buf = torch.zeros(N, t.num_observations)
         t.num_states = 88 if t.asymmetric_obs else 0
         t.states_buf = torch.zeros(N, 88)
     g = torch.Generator().manual_seed(seed)
-    draws = np.zeros((T, N, DRAW_STRIDE), np.float32)
+    draws = np.zeros((T, N, DRAW_STRIDE if variant is None else FORCE_STRIDE), np.float32)
     cur = {"step": 0, "phase": None, "ids": None}
     real = getattr(mod, "_real_torch_rand_float", mod.torch_rand_float)     # (a previous run left its wrapper)
     mod._real_torch_rand_float = real
@@ -192,7 +195,9 @@ def steps(N=24, T=8, seed=2, variant=None):
 
     def ri(env_ids, goal_env_ids):
         cur["phase"], cur["ids"] = "reset", env_ids
-        return orig_ri(env_ids, goal_env_ids)
+        r = orig_ri(env_ids, goal_env_ids)
+        cur["phase"] = "after_reset"             # (the force block's torch.rand follows)
+        return r
     t.reset_target_pose, t.reset_idx = rtp, ri
     keys = ["dof_state", "root_state", "goal_state", "targets", "actions", "reset_in", "reset_goal_in",
             "progress_in", "successes_in", "obs", "rew", "reset", "reset_goal", "progress", "successes", "timeout",
@@ -212,7 +217,33 @@ def steps(N=24, T=8, seed=2, variant=None):
                      ("progress_in", t.progress_buf), ("successes_in", t.successes)]:
             out[k].append(v.clone().numpy())
         out["actions"].append(actions.clone().numpy())
-        t.pre_physics_step(actions)
+        if variant is None:
+            t.pre_physics_step(actions)
+        else:
+            # torch.rand / torch.randn of pre_physics_step: random_force_prob inside reset_idx (:559-560, after its
+            # reset_target_pose), the force selection torch.rand(num_envs) and the selected envs' torch.randn (:621-623)
+            real_rand, real_randn = torch.rand, torch.randn
+            sel = {}
+
+            def rand_rec(*a, **kw):
+                v = real_rand(*a, **kw)
+                if cur["phase"] == "reset_goal":
+                    draws[cur["step"], cur["ids"].numpy(), 45] = v.numpy()
+                else:
+                    draws[cur["step"], :, 46] = v.numpy()
+                    sel["ids"] = (v < t.random_force_prob).nonzero(as_tuple=False)[:, 0].numpy()
+                return v
+
+            def randn_rec(*a, **kw):
+                v = real_randn(*a, **kw)
+                ids = sel["ids"]
+                draws[cur["step"], ids, 47:50] = v.reshape(len(ids), 3).numpy()
+                draws[cur["step"], ids, 50] = 1.0
+                return v
+            with mock.patch.object(torch, "rand", rand_rec), mock.patch.object(torch, "randn", randn_rec):
+                t.pre_physics_step(actions)
+            out.setdefault("force_after", []).append(t.rb_forces[:, 17, :].clone().numpy())
+            out.setdefault("prob_after", []).append(t.random_force_prob.clone().numpy())
         cur["phase"] = None
         t.post_physics_step()
         t.timeout_buf = (t.progress_buf >= t.max_episode_length - 1) & (t.reset_buf != 0)   # vec_task.py:424

@@ -72,8 +72,17 @@ def allegro_step(orc, hs, p, lo, up, draws):
             AO.env_reset(root, dof[..., 0], dof[..., 1], hs["dof_position_targets"], e,
                          draws[e, AO.DRAW_RESET:AO.DRAW_RESET + 37], lo, up, c)
             hs["progress_buf"][e], hs["reset_buf"][e], hs["successes"][e] = 0, 0, 0
+            hs["task_state"][e, 0:3] = 0                              # rb_forces[env_ids] = 0 (ah_task.h AH_TS_*)
     hs["dof_position_targets"][:] = AO.targets_from_actions(hs["actions"], hs["dof_position_targets"], lo, up, c)
     hs["sim_targets"][:] = hs["dof_position_targets"]
+    if p.ah_force_scale > 0:
+        # random forces (ah_forces, replayed selection): decay, new N(0,1)^3 * mass * scale, LOCAL_SPACE -> world force
+        # of the step's first physics call (the oracle's simulate applies object_force to its first call only)
+        f = hs["task_state"][:, 0:3] * F(p.ah_force_decay_step)
+        sel = draws[:, AO.DRAW_FORCE_SEL] != 0
+        f[sel] = (draws[sel, AO.DRAW_FORCE_N:AO.DRAW_FORCE_N + 3] * F(p.ah_object_rb_mass)) * F(p.ah_force_scale)
+        hs["task_state"][:, 0:3] = f
+        hs["object_force"].reshape(N, 3)[:] = f32.qrot(root[:, 1, 3:7], f)
     orc.simulate(hs, p.control_freq_inv)
     hs["progress_buf"][:] = hs["progress_buf"] + 1
     obs = AO.observations(dof[..., 0], dof[..., 1], hs["dof_force"], root[:, 1], hs["goal_state"], hs["actions"], lo, up, c)

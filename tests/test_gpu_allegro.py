@@ -95,10 +95,12 @@ def test_allegro_step_with_resets_replayed_against_reference_goldens():
 
 
 @pytest.mark.parametrize("variant,cfg", [("full_rel", dict(obs_type="full", relative_control=True)),
-                                         ("novel_asym", dict(obs_type="full_no_vel", asymmetric=True))])
+                                         ("novel_asym", dict(obs_type="full_no_vel", asymmetric=True)),
+                                         ("force", dict(force_scale=1.0))])
 def test_allegro_observation_types_and_relative_control_against_reference_goldens(variant, cfg):
-    """The same fused step without physics for observationType "full" (72) + useRelativeControl and "full_no_vel"
-    (50) + asymmetric_observations (the states buffer: teacher_obs, 88 floats) (allegro_variants.npz)."""
+    """The same fused step without physics for observationType "full" (72) + useRelativeControl, "full_no_vel"
+    (50) + asymmetric_observations (the states buffer: teacher_obs, 88 floats) and forceScale 1 (the object force and
+    random_force_prob in task_state) (allegro_variants.npz)."""
     g = np.load(os.path.join(G, "allegro_variants.npz"))
     d = {k.split("/", 1)[1]: g[k] for k in g.files if k.startswith(variant + "/")}
     T, N = d["rew"].shape
@@ -123,6 +125,10 @@ def test_allegro_observation_types_and_relative_control_against_reference_golden
         np.testing.assert_allclose(get(sim, "rew"), d["rew"][t], rtol=1e-5, atol=1e-4)
         if cfg.get("asymmetric"):
             np.testing.assert_allclose(get(sim, "teacher_obs"), d["states"][t], rtol=1e-5, atol=2e-6)
+        ts = get(sim, "task_state")
+        np.testing.assert_allclose(ts[:, 3], d["prob_after"][t], rtol=1e-6)          # random_force_prob
+        if cfg.get("force_scale", 0) > 0:                                           # rb_forces of the object body
+            np.testing.assert_allclose(ts[:, 0:3], d["force_after"][t], rtol=1e-6, atol=1e-9)
 
 
 def test_allegro_vectask_asymmetric_relative_episode():

@@ -244,10 +244,11 @@ def test_kuka_fused_step_closed_hand_overflows_chunk0_and_matches_oracle_chain()
 
 
 # ----------------------------------------------------------------------------- AllegroHand (C3)
-def _allegro_window(n, seed, act_fn, resets=True):
+def _allegro_window(n, seed, act_fn, resets=True, force_scale=0.0):
     from handarm_hip.sim import HandArmSim
     from oracle.oracle_lib import HostState, Oracle
-    sim = HandArmSim(n, "cuda:0", task_cfg={"task": HM.TASK_ALLEGRO_HAND}, task=HM.TASK_ALLEGRO_HAND)
+    sim = HandArmSim(n, "cuda:0", task_cfg={"task": HM.TASK_ALLEGRO_HAND, "force_scale": force_scale},
+                     task=HM.TASK_ALLEGRO_HAND)
     p, m = sim.params, sim.model
     lo = np.array(m.dof_lower[:16], np.float32)
     up = np.array(m.dof_upper[:16], np.float32)
@@ -274,6 +275,8 @@ def _allegro_window(n, seed, act_fn, resets=True):
         scenes.assert_physics_bit_identical(sim, hs, n, tag=tag)
         exact(sim, hs, ["dof_position_targets", "sim_targets", "goal_state", "reset_buf", "reset_goal_buf",
                         "progress_buf", "successes"], tag)
+        if force_scale > 0:          # the object force state (task_state AH_TS_FORCE) bit for bit
+            np.testing.assert_array_equal(get(sim, "task_state")[:, 0:3], hs["task_state"][:, 0:3], err_msg=tag)
         assert (get(sim, "timeout_buf").astype(bool) == timeout).all(), tag
         eo = near(get(sim, "obs"), obs, 1e-4, tag + " obs")
         er = near(get(sim, "rew"), rew, 1e-4, tag + " rew")
@@ -288,6 +291,14 @@ def test_allegro_fused_step_with_physics_matches_oracle_chain():
     need_gpu()
     sim, hs = _allegro_window(128, 6, lambda rng, n: rng.uniform(-1, 1, (n, 16)).astype(np.float32))
     stats_match(sim, hs, "allegro", self_frac=0.25)
+
+
+def test_allegro_fused_step_with_random_forces_matches_oracle_chain():
+    """ah_step_kernel with forceScale 1 (allegro_hand.py:617-625): every env draws a new force each step (replayed
+    selection), applied to the first of the step's two physics calls, against the oracle chain."""
+    need_gpu()
+    sim, hs = _allegro_window(128, 6, lambda rng, n: rng.uniform(-1, 1, (n, 16)).astype(np.float32), force_scale=1.0)
+    assert np.abs(hs["task_state"][:, 0:3]).max() > 0.01
 
 
 def test_allegro_fused_step_closing_hand_overflows_chunk0_and_matches_oracle_chain():

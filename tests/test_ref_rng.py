@@ -97,5 +97,20 @@ def test_allegro_draws_reproduce_reference():
     ad = RR.AllegroDraws(N)
     for s in range(T):
         D = ad.step(d["reset_in"][s], d["reset_goal_in"][s]).numpy()
+        w = 45                      # allegro_steps.npz records the torch_rand_float draws (slots 0-44)
+        np.testing.assert_array_equal(D[:, :w], d["draws"][s][:, :w], err_msg=f"step {s}")
+
+
+def test_allegro_force_draws_reproduce_reference():
+    """forceScale 1 (allegro_variants.npz "force"): random_force_prob's torch.rand at reset, the force selection
+    torch.rand(N) and the selected envs' torch.randn in the reference's order, and the host's selection (slot 50)."""
+    g = np.load(os.path.join(G, "allegro_variants.npz"))
+    d = {k.split("/", 1)[1]: g[k] for k in g.files if k.startswith("force/")}
+    T, N = d["rew"].shape
+    torch.manual_seed(int(d["seed"]))
+    ad = RR.AllegroDraws(N, force_scale=1.0)
+    for s in range(T):
+        D = ad.step(d["reset_in"][s], d["reset_goal_in"][s]).numpy()
         w = d["draws"].shape[-1]
         np.testing.assert_array_equal(D[:, :w], d["draws"][s], err_msg=f"step {s}")
+        np.testing.assert_array_equal(ad.prob.numpy(), d["prob_after"][s])
