@@ -333,7 +333,9 @@ typedef struct ha_params_t {
      * to the first physics call of the step (an applied force lasts one gym.simulate). Per-env state in task_state
      * (AH_TS_* of ah_task.h) */
     float ah_force_scale, ah_force_prob_lo, ah_force_prob_hi, ah_force_decay_step;
-    float ah_object_rb_mass;           /* object_rb_masses: the cube's mass */
+    float ah_object_rb_mass;           /* object_rb_masses: the object's mass */
+    int32_t ah_object_type;            /* objectType 0 block, 1 egg, 2 pen (allegro_hand.py:82-97; the pool entry of
+                                        * the scene; pen: randomize_rotation_pen at reset, :542-546) */
 } ha_params_t;
 
 /* Device buffers (caller-allocated). Layouts match the Isaac Gym tensors exactly. */

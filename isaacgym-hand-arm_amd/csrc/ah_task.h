@@ -105,8 +105,19 @@ HD void ah_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags, bool 
 #pragma unroll
         for (int k = 0; k < 3; k++) pos[k] = ini[k] + noise * ah_draw(c, st, env, flags, AH_DRAW_RESET + k);
         float rot[4];
-        ah_randomize_rotation(ah_draw(c, st, env, flags, AH_DRAW_RESET + 3), ah_draw(c, st, env, flags, AH_DRAW_RESET + 4),
-                              rot);
+        if (p.ah_object_type == 2) {
+            // randomize_rotation_pen(rand0, rand1, 0.3) (:542-546, 729-732): about x by 0.5 pi + rand0 max_angle, then
+            // about z by rand0 pi (rand1 unused)
+            const float PI_F = 3.14159265358979323846f;
+            float r0 = ah_draw(c, st, env, flags, AH_DRAW_RESET + 3);
+            float qa[4], qb[4];
+            ah_quat_from_angle_axis(1.57079632679489661923f + r0 * 0.3f, 0, qa);
+            ah_quat_from_angle_axis(r0 * PI_F, 2, qb);
+            ref_quat_mul(qa, qb, rot);
+        } else {
+            ah_randomize_rotation(ah_draw(c, st, env, flags, AH_DRAW_RESET + 3),
+                                  ah_draw(c, st, env, flags, AH_DRAW_RESET + 4), rot);
+        }
         float* r = st.root_state + ((size_t)env * A + m.actor_object0) * 13;
         if (lane < 13) r[lane] = lane < 3 ? pos[lane] : (lane < 7 ? rot[lane - 3] : 0.0f);
         if (lane == 0) {

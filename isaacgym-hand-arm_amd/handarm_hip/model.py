@@ -136,7 +136,7 @@ class HaParams(C.Structure):
         ("pcm_lin_tol", f32), ("pcm_cos_tol", f32),                           # v13
         ("ah_obs_type", i32), ("ah_asymmetric", i32), ("ah_relative_control", i32), ("ah_speed_dt", f32),   # v15
         ("ah_force_scale", f32), ("ah_force_prob_lo", f32), ("ah_force_prob_hi", f32), ("ah_force_decay_step", f32),
-        ("ah_object_rb_mass", f32),
+        ("ah_object_rb_mass", f32), ("ah_object_type", i32),
     ]
 
 
@@ -673,6 +673,8 @@ ALLEGRO_TASK = dict(
 AH_OBS_TYPES = {"full_state": 0, "full": 1, "full_no_vel": 2}
 AH_NUM_OBS = {"full_state": 88, "full": 72, "full_no_vel": 50}
 AH_NUM_STATES = 88
+# objectType (allegro_hand.py:82-97): the AllegroHand scene's pool entries (tools/build_model.py main_allegro)
+AH_OBJECT_TYPES = {"block": 0, "egg": 1, "pen": 2}
 
 
 def num_states(params):
@@ -828,8 +830,16 @@ def build_params(cfg=None, task=None):
         # torch.pow(to_torch(forceDecay), dt / forceDecayInterval): a float32 tensor to a python-double power
         p.ah_force_decay_step = float(torch.pow(torch.tensor(c["force_decay"], dtype=torch.float32),
                                                 c["dt"] / c["force_decay_interval"]))
-        p.ah_object_init[:] = c["object_init"]
-        p.ah_goal_init[:] = c["goal_init"]
+        p.ah_object_type = AH_OBJECT_TYPES[c.get("object_type", "block")]
+        obj_init, goal_init = list(c["object_init"]), list(c["goal_init"])
+        if c.get("object_type") == "pen":
+            # object_start_pose.p.z = hand z + 0.02 (a gymapi.Vec3 float), goal_states z - 0.04 in fp32 (:295-296,
+            # 363-365); compute_hand_reward doubles the success tolerance (ignore_z_rot, :675-676)
+            obj_init[2] = float(np.float32(0.5 + 0.02))
+            goal_init[2] = float(np.float32(np.float32(obj_init[2]) - np.float32(0.04)))
+            p.ah_success_tolerance = 2.0 * c["success_tolerance"]
+        p.ah_object_init[:] = obj_init
+        p.ah_goal_init[:] = goal_init
         p.ah_goal_displacement[:] = c["goal_displacement"]
         # (1.0 - act_moving_average) * prev_targets: python double, cast once (allegro_hand.py:612-613)
         p.sih_beta = 1.0 - c["act_moving_average"]

@@ -59,6 +59,8 @@ class HandArmSim:
         self.t["root_state"].view(num_envs, self.num_actors, 13)[..., 6] = 1.0
         self.t["goal_state"][:, 6] = 1.0
         self.t["collision_enabled"].fill_(1)
+        if task == HM.TASK_ALLEGRO_HAND:          # objectType: the scene's pool entry in every env
+            self.t["object_indices"].fill_(int(self.params.ah_object_type))
         # domain-randomization rows start at the nominal values (mass scale 1, friction) until the first
         # reset samples them (ha_task.h dr_sample)
         dr = self.t["dr_scale"]
@@ -69,8 +71,8 @@ class HandArmSim:
         if task == HM.TASK_ALLEGRO_KUKA:
             self._init_kuka()
         h = C.c_void_p()
-        if task == HM.TASK_ALLEGRO_HAND:            # object_rb_masses (allegro_hand.py:355-357): the cube's mass
-            self.params.ah_object_rb_mass = self.model.pool_mass[0]
+        if task == HM.TASK_ALLEGRO_HAND:            # object_rb_masses (allegro_hand.py:355-357): the object's mass
+            self.params.ah_object_rb_mass = self.model.pool_mass[self.params.ah_object_type]
         _lib.check(self.lib.ha_create(C.byref(self.model), C.byref(self.params), num_envs, C.byref(h)), "ha_create")
         self.h = h
         # contacts per substep the kernel family holds (clutter 84, Ur5Sih 21, AllegroKuka 21, AllegroHand 12)

@@ -2,7 +2,7 @@
 
 Drop-in for tasks/allegro_hand.py:40 (registered as "AllegroHand" in tasks/__init__.py). Config
 cfg/task/AllegroHand.yaml: 16 DOF Allegro hand (allegro_touch_sensor.urdf, fixed base, gravity off),
-one 0.065 m cube, a goal cube that only carries a pose, observationType "full_state" (88 floats; "full" 72 and
+one 0.065 m cube (objectType block; egg and pen too), a goal object that only carries a pose, observationType "full_state" (88 floats; "full" 72 and
 "full_no_vel" 50 too, and asymmetric_observations' 88-float states buffer), absolute or relative control
 (useRelativeControl, dofSpeedScale), random object forces (forceScale), controlFrequencyInv 2, episodeLength 600.
 
@@ -34,8 +34,9 @@ class AllegroHand:
         if self.obs_type not in HM.AH_OBS_TYPES:                      # allegro_hand.py:102-104
             raise Exception("Unknown type of observations!\nobservationType should be one of: [openai, full_no_vel, "
                             "full, full_state]")
-        if env.get("objectType", "block") != "block":
-            raise NotImplementedError("objectType 'block' (the AllegroHand.yaml value) is implemented")
+        self.object_type = env.get("objectType", "block")
+        assert self.object_type in HM.AH_OBJECT_TYPES                  # allegro_hand.py:82-83
+        self.ignore_z = self.object_type == "pen"
         self.asymmetric_obs = bool(env.get("asymmetric_observations", False))
         self.use_relative_control = bool(env.get("useRelativeControl", False))
         self.control_freq_inv = int(env.get("controlFrequencyInv", c["control_freq_inv"]))
@@ -45,7 +46,7 @@ class AllegroHand:
         task_cfg = dict(task=HM.TASK_ALLEGRO_HAND, control_freq_inv=self.control_freq_inv,
                         max_episode_length=self.max_episode_length, seed=int(cfg.get("seed", 42)),
                         obs_type=self.obs_type, asymmetric=self.asymmetric_obs,
-                        relative_control=self.use_relative_control)
+                        relative_control=self.use_relative_control, object_type=self.object_type)
         for key, name in [("distRewardScale", "dist_reward_scale"), ("rotRewardScale", "rot_reward_scale"),
                           ("rotEps", "rot_eps"), ("actionPenaltyScale", "action_penalty_scale"),
                           ("successTolerance", "success_tolerance"), ("reachGoalBonus", "reach_goal_bonus"),
@@ -89,8 +90,8 @@ class AllegroHand:
         r = self.root_state_tensor.view(N, 3, 13)
         r[:, 0, 0:3] = torch.tensor(list(self.sim.model.base_pos), device=sim_device)
         r[:, 0, 3:7] = torch.tensor(list(self.sim.model.base_quat), device=sim_device)
-        r[:, 1, 0:7] = torch.tensor(c["object_init"], device=sim_device)
-        self.goal_states[:, 0:3] = torch.tensor(c["goal_init"], device=sim_device)
+        r[:, 1, 0:7] = torch.tensor(list(self.sim.params.ah_object_init), device=sim_device)
+        self.goal_states[:, 0:3] = torch.tensor(list(self.sim.params.ah_goal_init), device=sim_device)
         self.goal_states[:, 3:7] = torch.tensor([0.0, 0.0, 0.0, 1.0], device=sim_device)
         r[:, 2, 0:3] = self.goal_states[:, 0:3] + torch.tensor(c["goal_displacement"], device=sim_device)
         r[:, 2, 6] = 1.0

@@ -49,7 +49,7 @@ def _quat_from_angle_axis(angle, axis):
     th = np.asarray(angle, F) / F(2.0)
     sn, cs = f32.sincos(th)
     z = F(0.0) * sn
-    q = [sn if axis == 0 else z, sn if axis == 1 else z, z, cs]
+    q = [sn if axis == 0 else z, sn if axis == 1 else z, sn if axis == 2 else z, cs]
     n = np.sqrt(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]).astype(F)
     n = np.maximum(n, F(1e-9))
     return np.stack([c / n for c in q], -1).astype(F)
@@ -147,12 +147,21 @@ def goal_reset(goal_state, root, env, g0, g1, c=CFG):
     root[env, 2, 7:13] = 0
 
 
+def randomize_rotation_pen(rand0):
+    """allegro_hand.py:729-732 with max_angle torch.tensor(0.3): x by 0.5 pi + rand0 0.3, then z by rand0 pi."""
+    r0 = np.asarray(rand0, F)
+    return quat_mul(_quat_from_angle_axis(F(0.5 * np.pi) + r0 * F(0.3), 0), _quat_from_angle_axis(r0 * F(np.pi), 2))
+
+
 def env_reset(root, dof_pos, dof_vel, targets, env, r, lo, up, c=CFG):
     """reset_idx body for one env (allegro_hand.py:533-579) from its 37 draws r."""
     init = np.asarray(c["object_init"], F)
     noise = F(c["reset_position_noise"])
     root[env, 1, 0:3] = init[0:3] + noise * r[0:3]
-    root[env, 1, 3:7] = randomize_rotation(np.array([r[3]], F), np.array([r[4]], F))[0]
+    if c.get("object_type") == "pen":
+        root[env, 1, 3:7] = randomize_rotation_pen(np.array([r[3]], F))[0]
+    else:
+        root[env, 1, 3:7] = randomize_rotation(np.array([r[3]], F), np.array([r[4]], F))[0]
     root[env, 1, 7:13] = 0
     dmax, dmin = up - F(0), lo - F(0)
     rd = dmin + ((dmax - dmin) * F(0.5)) * (r[5:5 + D] + F(1))

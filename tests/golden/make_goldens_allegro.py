@@ -12,8 +12,8 @@ Reference code exercised, unmodified, through a fake ``self`` carrying what ``_c
     then ``post_physics_step`` (:627-633) and VecTask.step's timeout rule (vec_task.py:424), over several
     steps with goal and env resets: ``allegro_steps.npz``. ``torch_rand_float`` is wrapped to record its
     draws per env in the order the device replays them (ah_task.h AH_DRAW_*).
-  * the same steps run with observationType "full" + useRelativeControl, "full_no_vel" + asymmetric_observations
-    and forceScale 1 (:99-124, 425-504, 557-560, 602-605, 617-623; torch.rand / torch.randn recorded too):
+  * the same steps run with observationType "full" + useRelativeControl, "full_no_vel" + asymmetric_observations,
+    objectType egg and pen (:82-97, 295-296, 542-546, 675-676) and forceScale 1 (:99-124, 425-504, 557-560, 602-605, 617-623; torch.rand / torch.randn recorded too):
     ``allegro_variants.npz`` (``--variants`` writes only it).
 ``gym.simulate`` is a no-op in the fake gym: these goldens pin the task math only.
 """
@@ -150,10 +150,13 @@ def obs_reward(N=32, steps=5, seed=1):
     np.savez_compressed(os.path.join(HERE, "allegro_obs_reward.npz"), **{k: np.stack(v) for k, v in out.items()})
 
 
-VARIANTS = {  # the allegro_variants.npz runs: (observationType, asymmetric_observations, useRelativeControl, forceScale)
-    "full_rel": ("full", False, True, 0.0),
-    "novel_asym": ("full_no_vel", True, False, 0.0),
-    "force": ("full_state", False, False, 1.0),
+VARIANTS = {  # the allegro_variants.npz runs: (observationType, asymmetric_observations, useRelativeControl, forceScale,
+    #            objectType)
+    "full_rel": ("full", False, True, 0.0, "block"),
+    "novel_asym": ("full_no_vel", True, False, 0.0, "block"),
+    "force": ("full_state", False, False, 1.0, "block"),
+    "egg": ("full_state", False, False, 0.0, "egg"),
+    "pen": ("full_state", False, False, 0.0, "pen"),
 }
 FORCE_STRIDE = 51            # draw slots with the random-force draws (ah_task.h AH_DRAW_FORCE_*)
 
@@ -164,7 +167,13 @@ def steps(N=24, T=8, seed=2, variant=None):
     torch.manual_seed(seed)          # seeded before the task is built: __init__'s draw is part of the stream
     mod, t = make_task(N)
     if variant is not None:
-        t.obs_type, t.asymmetric_obs, t.use_relative_control, t.force_scale = VARIANTS[variant]
+        t.obs_type, t.asymmetric_obs, t.use_relative_control, t.force_scale, t.object_type = VARIANTS[variant]
+        if t.object_type == "pen":
+            # object_start_pose.p.z = hand z + 0.02 (:295-296), goal_states = object - 0.04 z (:363-365)
+            t.object_init_state[:, 2] = float(np.float32(0.5 + 0.02))
+            t.goal_states = t.object_init_state.clone()
+            t.goal_states[:, 2] -= 0.04
+            t.goal_init_state = t.goal_states.clone()
         t.num_observations = {"full_no_vel": 50, "full": 72, "full_state": 88}[t.obs_type]
         t.obs_buf = torch.zeros(N, t.num_observations)
         t.num_states = 88 if t.asymmetric_obs else 0

@@ -96,11 +96,12 @@ def test_allegro_step_with_resets_replayed_against_reference_goldens():
 
 @pytest.mark.parametrize("variant,cfg", [("full_rel", dict(obs_type="full", relative_control=True)),
                                          ("novel_asym", dict(obs_type="full_no_vel", asymmetric=True)),
-                                         ("force", dict(force_scale=1.0))])
+                                         ("force", dict(force_scale=1.0)),
+                                         ("egg", dict(object_type="egg")), ("pen", dict(object_type="pen"))])
 def test_allegro_observation_types_and_relative_control_against_reference_goldens(variant, cfg):
     """The same fused step without physics for observationType "full" (72) + useRelativeControl, "full_no_vel"
-    (50) + asymmetric_observations (the states buffer: teacher_obs, 88 floats) and forceScale 1 (the object force and
-    random_force_prob in task_state) (allegro_variants.npz)."""
+    (50) + asymmetric_observations (the states buffer: teacher_obs, 88 floats), forceScale 1 (the object force and
+    random_force_prob in task_state) and objectType egg / pen (allegro_variants.npz)."""
     g = np.load(os.path.join(G, "allegro_variants.npz"))
     d = {k.split("/", 1)[1]: g[k] for k in g.files if k.startswith(variant + "/")}
     T, N = d["rew"].shape
@@ -154,6 +155,37 @@ def test_allegro_vectask_asymmetric_relative_episode():
         assert o["states"].abs().max().item() <= 5.0 and torch.isfinite(o["obs"]).all()
         # the states' object pose columns are the observation's (full_state 48:55 vs full_no_vel 16:23)
         torch.testing.assert_close(o["states"][:, 48:55], o["obs"][:, 16:23])
+
+
+@pytest.mark.parametrize("obj", ["egg", "pen"])
+def test_allegro_egg_and_pen_episode(obj):
+    """objectType egg / pen through the VecTask surface: the pool entry in every env, its hull and mass in the physics
+    (tools/build_model.py build_egg / build_pen), 60 random-action steps stay finite with the object held or dropped
+    onto nothing (no table: a dropped object falls and the env resets), and the physics matches the C oracle bit for
+    bit for one gym.simulate of the reset scene."""
+    need_gpu()
+    from handarm_hip.tasks import isaacgym_task_map
+    from oracle.oracle_lib import HostState, Oracle
+    n = 256
+    env = isaacgym_task_map["AllegroHand"]({"env": {"numEnvs": n, "objectType": obj}}, "cuda:0", "cuda:0")
+    assert (env.sim.t["object_indices"] == HM.AH_OBJECT_TYPES[obj]).all()
+    env.reset()
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    resets = 0
+    for _ in range(60):
+        o, r, d, e = env.step(torch.rand((n, 16), device="cuda:0", generator=g) * 2 - 1)
+        assert torch.isfinite(o["obs"]).all() and torch.isfinite(r).all()
+        resets += int(d.sum())
+    assert resets > 0
+    sim = env.sim
+    hs = HostState(n, model=sim.model, params=sim.params)
+    torch.cuda.synchronize()
+    for k in HM.STATE_FIELDS:
+        if k in hs.arrays and k in sim.t and sim.t[k].numel() == hs[k].size:
+            hs[k][...] = sim.t[k].cpu().numpy().reshape(hs[k].shape)
+    sim.simulate(1)
+    Oracle(sim.model, sim.params, n).simulate(hs, 1)
+    scenes.assert_physics_bit_identical(sim, hs, n, tag=obj)
 
 
 def _oracle_and_sim(n, seed):

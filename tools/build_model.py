@@ -537,6 +537,43 @@ def build_cube(size=0.065, density=400.0):
             "inertia": [I, 0, 0, 0, I, 0, 0, 0, I], "hull": box_hull(half)}
 
 
+def build_egg(density=1000.0):
+    """mjcf/open_ai_assets/hand/egg.xml: ellipsoid, semi-axes 0.03 x 0.03 x 0.04 (the object geom; MJCF default density
+    1000) as a 32-vertex hull of points on its surface; mass and inertia of the ellipsoid."""
+    a, b, c = 0.03, 0.03, 0.04
+    pts = [[0.0, 0.0, c], [0.0, 0.0, -c]]
+    for k, zf in enumerate((-0.75, -0.3, 0.3, 0.75)):
+        n = 6 if abs(zf) > 0.5 else 9
+        for j in range(n):
+            t = 2 * math.pi * (j + 0.5 * k) / n
+            r = math.sqrt(1 - zf * zf)
+            pts.append([a * r * math.cos(t), b * r * math.sin(t), c * zf])
+    mass = density * 4.0 / 3.0 * math.pi * a * b * c
+    I = [mass / 5 * (b * b + c * c), mass / 5 * (a * a + c * c), mass / 5 * (a * a + b * b)]
+    return {"name": "egg", "mass": mass, "com": [0, 0, 0], "inertia": [I[0], 0, 0, 0, I[1], 0, 0, 0, I[2]],
+            "hull": hull_record(np.array(pts), 32)}
+
+
+def build_pen(density=1000.0):
+    """mjcf/open_ai_assets/hand/pen.xml: capsule, radius 0.008, half-length 0.1 along z (MJCF default density 1000) as
+    a 32-vertex hull (two 8-point rings at the ends of the cylinder, two 7-point rings on the caps, the tips); mass and
+    inertia of the capsule."""
+    r, hl = 0.008, 0.1
+    pts = [[0.0, 0.0, hl + r], [0.0, 0.0, -hl - r]]
+    for z, rr, n, off in ((hl, r, 8, 0.0), (-hl, r, 8, 0.0), (hl + 0.7 * r, r * math.sqrt(1 - 0.49), 7, 0.5),
+                          (-hl - 0.7 * r, r * math.sqrt(1 - 0.49), 7, 0.5)):
+        for j in range(n):
+            t = 2 * math.pi * (j + off) / n
+            pts.append([rr * math.cos(t), rr * math.sin(t), z])
+    h = 2 * hl
+    m_cyl = density * math.pi * r * r * h
+    m_sph = density * 4.0 / 3.0 * math.pi * r ** 3
+    Ixx = m_cyl * (h * h / 12 + r * r / 4) + m_sph * (2 * r * r / 5 + h * h / 4 + 3 * h * r / 8)
+    Izz = m_cyl * r * r / 2 + m_sph * 2 * r * r / 5
+    return {"name": "pen", "mass": m_cyl + m_sph, "com": [0, 0, 0], "inertia": [Ixx, 0, 0, 0, Ixx, 0, 0, 0, Izz],
+            "hull": hull_record(np.array(pts), 32)}
+
+
 # self-collision of the Allegro actors (ha_model_t v12): every non-adjacent link pair ("exclude" can drop pairs). The
 # lists are empty: at each task's reset pose (AllegroHand: zero DOF positions clamped to the limits; AllegroKuka: the
 # arm's desired pose, fingers 0) no pair of cooked hulls is within the contact offset, so the hand starts without
@@ -548,7 +585,8 @@ KUKA_SELF_COLLISION = {"exclude": []}
 def main_allegro():
     robot, link_hulls = build_allegro()
     L = len(robot["links"])
-    scene = {"robot": robot, "link_hulls": link_hulls, "objects": [build_cube()], "table": None,
+    # objectType block / egg / pen (allegro_hand.py:82-97): pool entries 0 / 1 / 2
+    scene = {"robot": robot, "link_hulls": link_hulls, "objects": [build_cube(), build_egg(), build_pen()], "table": None,
              "objects_per_env": 1,
              # actors hand 0, object 1, goal 2; bodies hand links, object, goal (allegro_hand.py:330-357)
              "layout": {"n_actors": 3, "actor_robot": 0, "actor_object0": 1, "actor_goal": 2, "actor_table": -1,
