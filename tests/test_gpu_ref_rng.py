@@ -158,3 +158,30 @@ def test_ur5sih_reference_rng_draw_order_with_point_clouds(monkeypatch):
     # each pose's drop draws form one run between two randperms
     runs = "".join("p" if x == "perm" else "d" for x in head).split("p")[1:-1]
     assert len(runs) == P and all(len(r) >= env.num_objects for r in runs), head
+
+
+@pytest.mark.parametrize("variant,env_cfg", [("force", {"forceScale": 1.0}), ("pen", {"objectType": "pen"})])
+def test_allegro_reference_rng_variants(variant, env_cfg):
+    """reference_rng through env.step() for forceScale 1 (the force selection and normals drawn on the host in the
+    reference's order) and objectType pen (randomize_rotation_pen): allegro_variants.npz, physics off."""
+    need_gpu()
+    from handarm_hip.tasks import AllegroHand
+    g = np.load(os.path.join(G, "allegro_variants.npz"))
+    d = {k.split("/", 1)[1]: g[k] for k in g.files if k.startswith(variant + "/")}
+    T, N = d["rew"].shape
+    torch.manual_seed(int(d["seed"]))
+    env = AllegroHand({"env": dict({"numEnvs": N}, **env_cfg), "sim": {"reference_rng": True}}, "cuda:0", "cuda:0")
+    env.sim_flags = HM.FLAG_NO_PHYSICS
+    sim = env.sim
+    for k, gk in [("dof_state", "dof_state"), ("goal_state", "goal_state"), ("dof_position_targets", "targets"),
+                  ("reset_buf", "reset_in"), ("reset_goal_buf", "reset_goal_in"), ("successes", "successes_in")]:
+        put(sim, k, d[gk][0])
+    for t in range(T):
+        put(sim, "root_state", d["root_state"][t])
+        put(sim, "progress_buf", d["progress_in"][t])
+        env.step(torch.as_tensor(d["actions"][t], device="cuda:0"))
+        np.testing.assert_array_equal(get(sim, "reset_buf"), d["reset"][t])
+        np.testing.assert_allclose(get(sim, "root_state"), d["root_after"][t], rtol=1e-5, atol=2e-6)
+        np.testing.assert_allclose(get(sim, "obs"), d["obs"][t], rtol=1e-5, atol=2e-6)
+        if variant == "force":
+            np.testing.assert_allclose(get(sim, "task_state")[:, 0:3], d["force_after"][t], rtol=1e-6, atol=1e-9)
