@@ -504,6 +504,40 @@ def run_cpu_baseline(task, args, seconds, threads=None):
     return r
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def check_gpu_count(n):
+    """One rank per GPU: refuse N > torch.cuda.device_count() (which does not initialise the GPU) with exit code 2,
+    unless the gloo share-GPU rehearsal is asked for (HA_DIST_BACKEND=gloo HA_DIST_SHARE_GPU=1)."""
+    share = os.environ.get("HA_DIST_SHARE_GPU") == "1" and os.environ.get("HA_DIST_BACKEND") == "gloo"
+    ndev = torch.cuda.device_count()
+    if n > ndev and not (share and ndev > 0):
+        print(f"bench.py: --gpus {n} asks for {n} ranks but this node has {ndev} GPU(s); one rank per GPU is the "
+              f"process model (set HA_DIST_BACKEND=gloo HA_DIST_SHARE_GPU=1 to rehearse more ranks on fewer GPUs)",
+              file=sys.stderr)
+        return False
+    return True
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` started without torchrun: start N ranks (one process per GPU) under
+    torch.distributed.run as a CHILD process and return its exit code (the reference scales the same way:
+    `torchrun --nproc_per_node=N`, README.md:165-172; one sim per cuda:LOCAL_RANK, rlgames_utils.py:89-107).
+    Runs before this process makes any GPU call: torch.cuda.device_count() does not initialise the GPU.
+    The children inherit stdout, so rank 0's JSON line is this process's output."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # RCCL over dmabuf IPC on this host driver
+    import subprocess
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -529,6 +563,15 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU sample of the headline config")
     ap.add_argument("--cpu-seconds-sub", type=float, default=4.0, help="CPU sample of each sub-record")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ:
+        if not check_gpu_count(args.gpus):
+            sys.exit(2)
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        ap.error(f"--gpus {args.gpus} but torchrun started WORLD_SIZE={os.environ['WORLD_SIZE']} ranks")
 
     from handarm_hip import parallel
     rank, local_rank, world, device = parallel.init_distributed("nccl")
