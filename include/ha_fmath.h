@@ -53,5 +53,52 @@ HA_FM_FN void ha_sincosf(float x, float* s_out, float* c_out) {
     *c_out = c;
 }
 
+/* Natural logarithm and exponential for the domain-randomization samplers (loguniform, Box-Muller gaussian), shared
+ * for the same reason: the C oracle and numpy (oracle/f32.py) restate the samples bit for bit. Cephes logf / expf:
+ * the argument split by its exponent bits (log) or by round(x / ln 2) with a two-part ln 2 (exp), then a minimax
+ * polynomial; about 1 ulp. ha_logf takes positive normal arguments (the samplers' u >= 2^-24 and positive ranges);
+ * ha_expf clamps its result exponent to the normal range. */
+HA_FM_FN float ha_bits_float_(int i) {
+    union { int i; float f; } u;
+    u.i = i;
+    return u.f;
+}
+HA_FM_FN int ha_float_bits_(float f) {
+    union { int i; float f; } u;
+    u.f = f;
+    return u.i;
+}
+HA_FM_FN float ha_logf(float x) {
+    int ix = ha_float_bits_(x);
+    int e = ((ix >> 23) & 0xff) - 126;                        /* x = m 2^e, m in [0.5, 1) */
+    float m = ha_bits_float_((ix & 0x007fffff) | 0x3f000000);
+    if (m < 0.707106781186547524f) {
+        e -= 1;
+        m = (m + m) - 1.0f;
+    } else {
+        m = m - 1.0f;
+    }
+    float z = m * m;
+    float y = ((((((((7.0376836292e-2f * m - 1.1514610310e-1f) * m + 1.1676998740e-1f) * m - 1.2420140846e-1f) * m
+                   + 1.4249322787e-1f) * m - 1.6668057665e-1f) * m + 2.0000714765e-1f) * m - 2.4999993993e-1f) * m
+               + 3.3333331174e-1f) * m * z;
+    float fe = (float)e;
+    y = y + -2.12194440e-4f * fe;
+    y = y + -0.5f * z;
+    float r = m + y;
+    return r + 0.693359375f * fe;
+}
+HA_FM_FN float ha_expf(float x) {
+    x = x > 88.0f ? 88.0f : (x < -87.0f ? -87.0f : x);
+    float z = ha_floorf_(1.44269504088896341f * x + 0.5f);
+    x = x - z * 0.693359375f;
+    x = x - z * -2.12194440e-4f;
+    int n = (int)z;
+    float xx = x * x;
+    float y = (((((1.9875691500e-4f * x + 1.3981999507e-3f) * x + 8.3334519073e-3f) * x + 4.1665795894e-2f) * x
+                + 1.6666665459e-1f) * x + 5.0000001201e-1f) * xx + x + 1.0f;
+    return y * ha_bits_float_((n + 127) << 23);
+}
+
 #undef HA_FM_FN
 #endif

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define HA_ABI_VERSION 15
+#define HA_ABI_VERSION 16
 
 /* capacities of the static model */
 #define HA_MAX_LINKS 32
@@ -74,12 +74,71 @@ extern "C" {
  * point t < k at 8 + 9 t: the point on A in A's frame (3), the point on B in B's frame (3), the normal in B's frame (3) */
 #define HA_PCM_REC 48
 #define HA_CSTAT 8             /* ha_state_t.contact_stats columns (v13: 8, was 4) */
-/* per-env domain-randomization samples (ha_state_t.dr_scale rows) */
-#define HA_DR_LINK_MASS 0      /* [HA_MAX_LINKS] robot link mass (and inertia) scale */
+/* per-env domain-randomization samples (ha_state_t.dr_scale rows): the actor properties of the env as
+ * apply_randomizations last set them (tasks/base/vec_task.py:788-864). Rows hold the nominal values until an env's
+ * first sample (handarm_hip/dr.py default_rows). */
+#define HA_DR_LINK_MASS 0      /* [HA_MAX_LINKS] robot link mass (and inertia) scale: new mass / nominal mass */
 #define HA_DR_OBJ_MASS 32      /* [HA_MAX_OBJ] object mass (and inertia) scale */
 #define HA_DR_LINK_FRIC 40     /* [HA_MAX_LINKS] robot link friction */
 #define HA_DR_OBJ_FRIC 72      /* [HA_MAX_OBJ] object friction */
-#define HA_DR_SIZE 80
+#define HA_DR_DOF_KP 80        /* [HA_MAX_DOFS] v16: drive stiffness (dof_properties stiffness) */
+#define HA_DR_DOF_KD 104       /* [HA_MAX_DOFS] v16: drive damping (dof_properties damping) */
+#define HA_DR_DOF_LOWER 128    /* [HA_MAX_DOFS] v16: joint lower limit the physics enforces (dof_properties lower) */
+#define HA_DR_DOF_UPPER 152    /* [HA_MAX_DOFS] v16: joint upper limit (dof_properties upper) */
+#define HA_DR_OBJ_SCALE 176    /* [HA_MAX_OBJ] v16: object actor scale (set_actor_scale; geometry x s, mass x s^3) */
+#define HA_DR_SIZE 184
+
+/* v16: schema-driven domain randomization (task.randomization_params, vec_task.py:646-876, dr_utils.py:71-238).
+ * One ha_dr_attr_t per randomized quantity, ha_params_t.dr_attr[HA_DRA_*]; dist 0 = not randomized. */
+#define HA_DRA_OBS 0           /* observations: noise on obs_buf after post_physics_step (vec_task.py:426-428) */
+#define HA_DRA_ACT 1           /* actions: noise before the action clamp (vec_task.py:400-402) */
+#define HA_DRA_GRAVITY 2       /* sim_params gravity (dr_utils.py:163-173), one value for the shard */
+#define HA_DRA_LINK_MASS 3     /* robot actor rigid_body_properties mass (per link) */
+#define HA_DRA_LINK_FRIC 4     /* robot actor rigid_shape_properties friction (per link: its shapes share one draw) */
+#define HA_DRA_DOF_KD 5        /* robot actor dof_properties damping (per DOF) */
+#define HA_DRA_DOF_KP 6        /* robot actor dof_properties stiffness (per DOF) */
+#define HA_DRA_DOF_LOWER 7     /* robot actor dof_properties lower (per DOF) */
+#define HA_DRA_DOF_UPPER 8     /* robot actor dof_properties upper (per DOF) */
+#define HA_DRA_OBJ_MASS 9      /* object actor rigid_body_properties mass */
+#define HA_DRA_OBJ_FRIC 10     /* object actor rigid_shape_properties friction */
+#define HA_DRA_OBJ_SCALE 11    /* object actor scale */
+#define HA_DRA_N 12
+#define HA_DR_DIST_OFF 0
+#define HA_DR_DIST_UNIFORM 1
+#define HA_DR_DIST_LOGUNIFORM 2
+#define HA_DR_DIST_GAUSSIAN 3
+#define HA_DR_OP_ADDITIVE 0
+#define HA_DR_OP_SCALING 1
+#define HA_DR_SCHED_NONE 0
+#define HA_DR_SCHED_LINEAR 1   /* min(frame, schedule_steps) / schedule_steps */
+#define HA_DR_SCHED_CONSTANT 2 /* 0 before schedule_steps frames, 1 after */
+typedef struct ha_dr_attr_t {
+    int32_t dist, op, sched, sched_steps;
+    float range[2];            /* uniform / loguniform: lo, hi; gaussian: mu, sigma (np.random.normal(mu, var)) */
+    float range_corr[2];       /* observations / actions: range_correlated (default 0, 0) */
+    int32_t num_buckets;       /* > 0: the value snaps to the bucket grid over `range` (get_bucketed_val) */
+    int32_t setup_only;        /* sampled at the first randomization only */
+} ha_dr_attr_t;
+
+/* v16: the shard-wide randomization state (ha_state_t.dr_global, HA_DRG_SIZE floats; int fields as int32 bits), kept
+ * by the launch that precedes every step (and reset) launch while dr_enable is on: gym.get_frame_count, last_rand_step,
+ * first_randomization, and the non-env randomizations (noise parameters, gravity) of apply_randomizations. The host
+ * writes it once (handarm_hip/dr.py init_global). */
+#define HA_DRG_FRAME 0         /* int: gym frame count when this step's pre_physics_step runs (the schedules' clock) */
+#define HA_DRG_FRAME_NEXT 1    /* int: frame count after this step's gym.simulate calls */
+#define HA_DRG_LAST_RAND 2     /* int: last_rand_step (frame of the last non-env randomization; -1 none) */
+#define HA_DRG_FIRST 3         /* int: 1 until the first apply_randomizations ran */
+#define HA_DRG_ALL 4           /* int: this step's randomization is the first one: every env samples */
+#define HA_DRG_STEP 5          /* int: step counter of the white noise */
+#define HA_DRG_EPOCH 6         /* int: non-env randomizations so far (the correlated noise is redrawn at each) */
+#define HA_DRG_VALID 7         /* int: dr_randomizations holds observations / actions (after the first one) */
+#define HA_DRG_OBS 8           /* [4] observation noise: corr scale, corr offset, white scale, white offset */
+#define HA_DRG_ACT 12          /* [4] action noise (current) */
+#define HA_DRG_ACT_USE 16      /* [4] action noise this step's VecTask.step applies (before its apply_randomizations) */
+#define HA_DRG_ACT_EPOCH 20    /* int: epoch of that action noise's correlated term */
+#define HA_DRG_ACT_ON 21       /* int: this step's actions get noise */
+#define HA_DRG_GRAVITY 24      /* [3] sim_params gravity (current) */
+#define HA_DRG_SIZE 32
 
 /* tasks (ha_params_t.task) */
 #define HA_TASK_UR5SIH 0        /* Ur5SihMultiObjectManipulation (tasks/hand_arm/task/multi_object_manipulation.py) */
@@ -260,15 +319,9 @@ typedef struct ha_params_t {
     float ah_object_init[7];   /* object start pose (pos, quat xyzw) */
     float ah_goal_init[3];     /* goal_init_state position (object start - 0.04 z) */
     float ah_goal_displacement[3];
-    /* v2: domain randomization (BASELINE config 4 "DR on"; ranges of cfg/task/AllegroKuka.yaml:121-207,
-     * sampled per env at reset on the device). Contact friction = mean of the two bodies' frictions
-     * (PhysX average combine); static geometry keeps `friction`. */
-    int32_t dr_enable;
-    float dr_mass_lo, dr_mass_hi;      /* uniform scaling of link / object mass and inertia */
-    float dr_fric_lo, dr_fric_hi;      /* uniform scaling of friction, then bucketed */
-    int32_t dr_fric_buckets;           /* 250 */
-    float dr_obs_noise;                /* additive gaussian sigma on obs each step */
-    float dr_act_noise;                /* additive gaussian sigma on actions (applied by the host wrapper) */
+    /* v2: domain randomization on (v16: schema-driven, dr_attr below). Contact friction = mean of the two bodies'
+     * frictions (PhysX average combine); static geometry keeps `friction`. */
+    int32_t dr_enable;                 /* v16: the schema of dr_attr / dr_frequency below */
     /* v3: AllegroKuka (cfg/task/AllegroKuka.yaml:9-94, env/regrasping.yaml, allegro_kuka_base.py:53-400) */
     int32_t ak_subtask;                /* 0 regrasping, 1 reorientation, 2 throw (v14) */
     int32_t ak_num_keypoints;          /* 1 (regrasping) or 4 */
@@ -336,6 +389,14 @@ typedef struct ha_params_t {
     float ah_object_rb_mass;           /* object_rb_masses: the object's mass */
     int32_t ah_object_type;            /* objectType 0 block, 1 egg, 2 pen (allegro_hand.py:82-97; the pool entry of
                                         * the scene; pen: randomize_rotation_pen at reset, :542-546) */
+    /* v16: task.randomization_params (vec_task.py:646-876): `frequency` (env steps between re-randomizations of an
+     * env, and frames between non-env randomizations) and one spec per randomized quantity (HA_DRA_*) */
+    int32_t dr_frequency;
+    ha_dr_attr_t dr_attr[HA_DRA_N];
+    /* v16: AllegroKuka privilegedActions (allegro_kuka_base.py:62-74,1359-1361,1417-1424): 3 leading actions are an
+     * object torque x privilegedActionsTorque (ENV_SPACE, the step's physics call); num_actions = 26 */
+    int32_t ak_privileged_actions;
+    float ak_privileged_torque;
 } ha_params_t;
 
 /* Device buffers (caller-allocated). Layouts match the Isaac Gym tensors exactly. */
@@ -383,7 +444,9 @@ typedef struct ha_state_t {
     float* object_scale;        /* [N][n_obj][3] per-env object dimension scale of the pool hull (null = 1);
                                  * mass scales with the volume, inertia with the scaled second moments */
     float* object_force;        /* [N][n_obj][3] world force at the object COM for the next ha_simulate
-                                 * (gym.apply_rigid_body_force_tensors; consumed, i.e. zeroed, by it) */
+                                 * (gym.apply_rigid_body_force_tensors; consumed, i.e. zeroed, by it). Since v15 it
+                                 * acts on the FIRST of the n_calls gym.simulate calls of that ha_simulate only (an
+                                 * applied force lasts one simulate; before v15 it acted on all n) */
     float* task_state;          /* [N][HA_AK_TS] AllegroKuka per-env task state */
     float* task_scalars;        /* [4] AllegroKuka host-curriculum scalars: success_tolerance,
                                  * tolerance objective, 1 if tolerance > target, keypoint success tolerance */
@@ -401,6 +464,12 @@ typedef struct ha_state_t {
                                  * enumeration (objects: ground, statics, later objects, link hulls; then link hulls x
                                  * statics), then n_self_pairs self pairs. Keyed by relative pose: a caller that
                                  * changes an env's object geometry (object_indices, object_scale) zeroes its rows */
+    /* v16 */
+    float* dr_global;           /* [HA_DRG_SIZE] shard-wide randomization state (dr_enable; see HA_DRG_*) */
+    int32_t* randomize_buf;     /* [N] steps since the env's actor properties were last randomized (vec_task.py:352) */
+    float* object_torque;       /* [N][n_obj][3] world torque on the object for the next ha_simulate
+                                 * (apply_rigid_body_force_tensors' torque tensor; consumed like object_force, on
+                                 * the first of its n_calls calls; null = none) */
 } ha_state_t;
 
 /* stats layout (int32): [0] num_resets, [1] num_successes, then per pool object

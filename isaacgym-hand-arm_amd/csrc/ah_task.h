@@ -165,7 +165,7 @@ HD void ah_controller(SimCtx& c, const ha_state_t& st, int env) {
     int lane = c.lane, D = c.D;
     if (lane < D) {
         float lo = m.dof_lower[lane], up = m.dof_upper[lane];
-        float a = act_at(c, st, (size_t)env * AH_NUM_ACT + lane);
+        float a = act_at(c, st, env, lane, AH_NUM_ACT);
         if (c.act_in) const_cast<float*>(st.actions)[(size_t)env * AH_NUM_ACT + lane] = a;          // the task's stored actions
         float* prev = st.dof_position_targets + (size_t)env * D;
         float cur;
@@ -231,7 +231,7 @@ HD void ah_post(SimCtx& c, const ha_state_t& st, int env, const AhIn& in, bool o
         if (k < 61) return p.ah_vel_obs_scale * in.obj[k - 48];                  // angvel
         if (k < 68) return gs[k - 61];
         if (k < 72) return qdiff[k - 68];
-        return act_at(c, st, (size_t)env * AH_NUM_ACT + (k - 72));
+        return act_at(c, st, env, k - 72, AH_NUM_ACT);
     };
     const int nobs = p.num_obs;
     float* ob = st.obs + (size_t)env * nobs;
@@ -246,6 +246,7 @@ HD void ah_post(SimCtx& c, const ha_state_t& st, int env, const AhIn& in, bool o
             // compute_full_observations(no_vel=True) (:439-446): dof pos, object pose, goal pose, qdiff, actions
             v = full_state(k < 16 ? k : (k < 23 ? k + 32 : k + 38));
         }
+        if (!obs_only) v = dr_obs(c, env, k, v);        // DR observation noise on obs_buf (vec_task.py:426-428)
         ob[k] = v;
         obs_out_put(c, (size_t)env * nobs + k, v);
     }
@@ -263,7 +264,7 @@ HD void ah_post(SimCtx& c, const ha_state_t& st, int env, const AhIn& in, bool o
         float rot_rew = 1.0f / (fabsf(rot_dist) + p.ah_rot_eps) * p.ah_rot_reward_scale;
         float ap = 0.0f;
         for (int k = 0; k < AH_NUM_ACT; k++) {
-            float ak = act_at(c, st, (size_t)env * AH_NUM_ACT + k);
+            float ak = act_at(c, st, env, k, AH_NUM_ACT);
             ap += ak * ak;
         }
         float reward = dist_rew + rot_rew + ap * p.ah_action_penalty_scale;

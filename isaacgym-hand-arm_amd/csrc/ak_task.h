@@ -225,11 +225,16 @@ HD void ak_controller(SimCtx& c, const ha_state_t& st, int env) {
     EnvLDS& s = *c.s;
     const ha_model_t& m = *c.m;
     const ha_params_t& p = *c.p;
-    int lane = c.lane, D = c.D;
+    int lane = c.lane, D = c.D, na = p.num_actions;
+    // privilegedActions (v16): actions[:, :3] are the object torque and the hand reads actions[:, 3:][:, 7:23], while
+    // the arm reads self.actions[:, :7] - the unstripped actions, torque columns included (allegro_kuka_base.py:1357-
+    // 1397, as written)
+    int pv = p.ak_privileged_actions ? 3 : 0;
+    if (c.act_in && lane < na)
+        const_cast<float*>(st.actions)[(size_t)env * na + lane] = act_at(c, st, env, lane, na);    // self.actions
     if (lane < D) {
         float lo = m.dof_lower[lane], up = m.dof_upper[lane];
-        float a = act_at(c, st, (size_t)env * AK_NUM_ACT + lane);
-        if (c.act_in) const_cast<float*>(st.actions)[(size_t)env * AK_NUM_ACT + lane] = a;          // the task's stored actions
+        float a = act_at(c, st, env, lane >= p.ak_num_arm_dofs ? lane + pv : lane, na);
         float* prev = st.dof_position_targets + (size_t)env * D;
         float cur;
         if (lane >= p.ak_num_arm_dofs) {
@@ -246,12 +251,17 @@ HD void ak_controller(SimCtx& c, const ha_state_t& st, int env) {
 }
 
 // random object forces (allegro_kuka_base.py:1399-1414): decay, re-draw with probability random_force_prob,
-// applied in LOCAL_SPACE at the object COM -> world force for this physics call
+// applied in LOCAL_SPACE at the object COM -> world force for this physics call; then the privileged actions' object
+// torque (:1417-1424): actions[:, :3] x privilegedActionsTorque in ENV_SPACE
 HD void ak_forces(SimCtx& c, const ha_state_t& st, int env, uint32_t flags, float& tsv) {
     EnvLDS& s = *c.s;
     const ha_params_t& p = *c.p;
     int lane = c.lane;
-    if (p.ak_force_scale <= 0.0f) return;
+    if (p.ak_privileged_actions && lane < 3) c.o[0].otq[lane] = act_at(c, st, env, lane, p.num_actions) * p.ak_privileged_torque;
+    if (p.ak_force_scale <= 0.0f) {
+        wsync();
+        return;
+    }
     uint32_t ctr = __float_as_uint(bcast(tsv, HA_AK_RNG));
     float prob = bcast(tsv, HA_AK_FORCE_PROB);
     float u = (flags & HA_FLAG_REPLAY_DRAWS) ? st.reset_draws[(size_t)env * HA_DRAW_STRIDE + AK_DRAW_FORCE_U(p)]
@@ -428,6 +438,7 @@ HD void ak_post(SimCtx& c, const ha_state_t& st, int env, AkPost& ak, bool obs_o
     for (int k = lane; k < nobs; k += 64) {
         float v = ak.obs[k];
         if (clampv > 0.0f && !obs_only) v = fminf(fmaxf(v, -clampv), clampv);   // clamp_obs (post_physics_step)
+        if (!obs_only) v = dr_obs(c, env, k, v);        // DR observation noise on obs_buf (vec_task.py:426-428)
         og[k] = v;
         obs_out_put(c, (size_t)env * nobs + k, v);
     }

@@ -91,7 +91,8 @@ struct PostScratch {
 // that use it.
 struct ObjLDS {
     float oc[4], oq[4], ov[4], ow[4];   // COM position, orientation, linear / angular velocity
-    float oIinv[12];                    // world inverse inertia (3x3, padded)
+    float oIinv[9];                     // world inverse inertia (3x3)
+    float otq[3];                       // v16: world torque for this physics call (apply_rigid_body_force_tensors)
     float osc[4];                       // per-env dimension scale of the pool hull; [3] = 1 when scaled
     float ofx[4];                       // world force on the COM for this physics call (apply_rigid_body_force)
     float om;                           // mass
@@ -354,6 +355,7 @@ struct SimCtx {
     int lane, D, NO, L;
     int maxc;               // contact capacity (MAXC x chunks of the kernel family)
     const float* dr;        // this env's domain-randomization row (HA_DR_*), or null when DR is off
+    const float* drg;       // v16: the shard-wide randomization state (ha_state_t.dr_global, HA_DRG_*), null: DR off
     float* spill;           // split rows: this env's global robot-block rows beyond the LDS slots (J, then Y)
     // narrow-phase cache: (hull, body) whose world vertices / planes are in ColScratch side A / side B. Within one
     // detect() the poses do not change, so consecutive pairs that share a side skip its setup (same values).
@@ -385,12 +387,6 @@ struct SimCtx {
 #endif
 };
 
-// action i of the step (env-major index): the caller's raw action clamped (vec_task.py:400-404, torch.clamp) when the
-// launch got them (ha_task_step_io), else the bound actions tensor
-HD float act_at(const SimCtx& c, const ha_state_t& st, size_t i) {
-    if (c.act_in) return fminf(fmaxf(c.act_in[i], -c.clip_act), c.clip_act);
-    return st.actions[i];
-}
 // obs_dict["obs"] = clamp(obs_buf, -clip, clip) (vec_task.py:437) next to obs_buf, when the launch asks for it
 HD void obs_out_put(const SimCtx& c, size_t i, float v) {
     if (c.obs_out) c.obs_out[i] = fminf(fmaxf(v, -c.clip_obs), c.clip_obs);
@@ -2438,9 +2434,11 @@ HD void substep(SimCtx& c, float hdt) {
         mass = mass * sc;
         c.o[o].om = mass;
         c.o[o].oc[3] = 1.0f / mass;     // the rows' 1 / m (obj_blocks reads it instead of dividing per PGS fetch)
-        // external force (zero unless a task applied one): constant over the call's substeps
-        f3 lv = (ld3(c.o[o].ov) + ld3(p.gravity) * hdt) + ld3(c.o[o].ofx) * (hdt / mass);
-        f3 av = ld3(c.o[o].ow) * damp;
+        // external force and torque (zero unless a task applied them): constant over the call's substeps. Gravity: the
+        // shard's randomized sim_params gravity when DR is on (v16)
+        const float* grav = c.drg ? c.drg + HA_DRG_GRAVITY : p.gravity;
+        f3 lv = (ld3(c.o[o].ov) + ld3(grav) * hdt) + ld3(c.o[o].ofx) * (hdt / mass);
+        f3 av = ld3(c.o[o].ow) * damp + mv3(Ii, ld3(c.o[o].otq)) * hdt;
         float* vo = s.v + D + 6 * o;
         vo[0] = lv.x; vo[1] = lv.y; vo[2] = lv.z; vo[3] = av.x; vo[4] = av.y; vo[5] = av.z;
     }
@@ -2808,7 +2806,11 @@ HD void substep(SimCtx& c, float hdt) {
     int act_lo = 0, act_up = 0;
     if (lane < D) {
         fcoef = m.dof_friction[lane];
-        float kp = m.dof_kp[lane], kd = m.dof_kd[lane];
+        // DR (v16): the env's dof_properties stiffness / damping / lower / upper (dr_scale row: nominal until sampled)
+        float kp = c.dr ? c.dr[HA_DR_DOF_KP + lane] : m.dof_kp[lane];
+        float kd = c.dr ? c.dr[HA_DR_DOF_KD + lane] : m.dof_kd[lane];
+        float jlo = c.dr ? c.dr[HA_DR_DOF_LOWER + lane] : m.dof_lower[lane];
+        float jup = c.dr ? c.dr[HA_DR_DOF_UPPER + lane] : m.dof_upper[lane];
         float den = kd + hdt * kp;
         float mii = c.Minv[lane * D + lane];
         dgam = 1.0f / (hdt * den);
@@ -2816,7 +2818,7 @@ HD void substep(SimCtx& c, float hdt) {
         dwinv = 1.0f / (mii + dgam);
         dlim = m.dof_effort[lane] * hdt;
         lwinv = 1.0f / (mii + 1e-9f);
-        float s_lo = s.q[lane] - m.dof_lower[lane], s_up = m.dof_upper[lane] - s.q[lane];
+        float s_lo = s.q[lane] - jlo, s_up = jup - s.q[lane];
         act_lo = s_lo <= p.joint_limit_margin;
         act_up = s_up <= p.joint_limit_margin;
         vt_lo = s_lo > 0 ? -s_lo / hdt : -p.baumgarte * s_lo / hdt;

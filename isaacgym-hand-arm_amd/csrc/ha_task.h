@@ -3,7 +3,7 @@
 // task/multi_object_manipulation.py (reset, reward, done). Compiled with -ffp-contract=off and the
 // reference's own quaternion formulas so observations are bit-exact against the oracle.
 #pragma once
-#include "ha_physics.h"
+#include "ha_dr.h"
 
 #define NUM_ACT 11
 // observation size for n objects: 80 + 3 n (object_pos) + 10 n (object_bounding_box) + 10 + 15 + 3
@@ -72,13 +72,13 @@ HD void controller_step(SimCtx& c, const ha_state_t& st, int env) {
     float* tgt = st.dof_position_targets + (size_t)env * D;
     float* servo_sh = s.u.xfer + 8;
     if (lane < 6) {
-        float u = st.ur5_target[env * 6 + lane] + p.action_dt * st.actions[env * NUM_ACT + lane];
+        float u = st.ur5_target[env * 6 + lane] + p.action_dt * act_at(c, st, env, lane, NUM_ACT);
         st.ur5_target[env * 6 + lane] = u;
         s.u.xfer[lane] = u;
     } else if (lane < 11) {
         int i = lane - 6;
         float beta = p.sih_beta;
-        float sm = p.sih_alpha * st.actions[env * NUM_ACT + lane] + beta * st.smoothed[env * 5 + i];
+        float sm = p.sih_alpha * act_at(c, st, env, lane, NUM_ACT) + beta * st.smoothed[env * 5 + i];
         st.smoothed[env * 5 + i] = sm;
         float sv = st.servo[env * 5 + i] + 100.0f * sm;
         sv = sv < p.servo_lower[i] ? p.servo_lower[i] : sv;
@@ -106,50 +106,7 @@ HD void controller_step(SimCtx& c, const ha_state_t& st, int env) {
     wsync();
 }
 
-// ----------------------------------------------------------------------------- RNG (device mode)
-HD uint32_t mix32(uint32_t x) {
-    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
-    return x;
-}
-HD float uniform01(uint64_t seed, uint32_t env, uint32_t episode, uint32_t k) {
-    uint32_t h = mix32((uint32_t)seed ^ mix32(env * 0x9E3779B9U ^ mix32(episode * 0x85EBCA6BU + k + (uint32_t)(seed >> 32))));
-    return (h >> 8) * (1.0f / 16777216.0f);
-}
-
-// standard normal by Box-Muller from two counter-based uniforms
-HD float gauss01(uint64_t seed, uint32_t env, uint32_t ctr, uint32_t k) {
-    float u1 = uniform01(seed ^ 0x9E3779B97F4A7C15ULL, env, ctr, 2 * k);
-    float u2 = uniform01(seed ^ 0x9E3779B97F4A7C15ULL, env, ctr, 2 * k + 1);
-    u1 = fmaxf(u1, 1.0f / 16777216.0f);
-    return sqrtf(-2.0f * logf(u1)) * cosf(6.28318530717958647692f * u2);
-}
-
-// Domain randomization samples of one env at reset (BASELINE config 4 "DR on"; dr_utils.py:71-147 semantics:
-// uniform scaling per rigid body, friction scaling then bucketing into num_buckets values over the range)
-HD float dr_bucket(float v, float lo, float hi, int nb) {
-    float w = hi - lo;
-    int i = (int)floorf((v - lo) / w * (float)nb);
-    i = i < 0 ? 0 : (i >= nb ? nb - 1 : i);
-    return w * (float)i / (float)nb + lo;
-}
-HD void dr_sample(const SimCtx& c, const ha_state_t& st, int env) {
-    const ha_params_t& p = *c.p;
-    if (!p.dr_enable || !st.dr_scale) return;
-    int lane = c.lane;
-    float* row = st.dr_scale + (size_t)env * HA_DR_SIZE;
-    uint32_t ep = st.episode[env];
-    auto u = [&](int k, float lo, float hi) { return lo + (hi - lo) * uniform01(p.seed, env, ep, 1000 + k); };
-    if (lane < HA_MAX_LINKS) {
-        row[HA_DR_LINK_MASS + lane] = u(lane, p.dr_mass_lo, p.dr_mass_hi);
-        row[HA_DR_LINK_FRIC + lane] = dr_bucket(p.friction * u(100 + lane, p.dr_fric_lo, p.dr_fric_hi), p.dr_fric_lo,
-                                                p.dr_fric_hi, p.dr_fric_buckets);
-    }
-    if (lane < NOBJ) {
-        row[HA_DR_OBJ_MASS + lane] = u(50 + lane, p.dr_mass_lo, p.dr_mass_hi);
-        row[HA_DR_OBJ_FRIC + lane] = dr_bucket(p.friction * u(150 + lane, p.dr_fric_lo, p.dr_fric_hi), p.dr_fric_lo,
-                                               p.dr_fric_hi, p.dr_fric_buckets);
-    }
-}
+// (the device RNG, mix32 / uniform01 / gauss01, lives in ha_dr.h)
 
 // ----------------------------------------------------------------------------- reset_idx (steady state)
 // multi_object_manipulation.py:62-71 + _reset_objects :73-91, _reset_target_object :193-209,
@@ -172,7 +129,6 @@ HD void task_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags) {
 #pragma unroll
         for (int k = 0; k < 3; k++) dr[2 + k] = uniform01(p.seed, env, ep, 2 + k);
     }
-    dr_sample(c, st, env);
     int cfg = (int)dr[0], tgt_obj = (int)dr[1];
     cfg = cfg < 0 ? 0 : (cfg >= P ? P - 1 : cfg);
     tgt_obj = tgt_obj < 0 ? 0 : (tgt_obj >= NO ? NO - 1 : tgt_obj);
@@ -186,7 +142,7 @@ HD void task_reset(SimCtx& c, const ha_state_t& st, int env, uint32_t flags) {
         for (int k = 7; k < 13; k++) r[k] = 0.0f;
         qf q = ldq(quat0);
         stq(c.o[o].oq, q);
-        st3(c.o[o].oc, ld3(pos0) + qrot(q, ld3(c.m->pool_com[c.o[o].pool])));
+        st3(c.o[o].oc, ld3(pos0) + qrot(q, scale3(c, o, ld3(c.m->pool_com[c.o[o].pool]))));
         st3(c.o[o].ov, mk3(0, 0, 0));
         st3(c.o[o].ow, mk3(0, 0, 0));
     } else if (lane >= 8 && lane < 11) {
@@ -282,12 +238,10 @@ HD void post_step(SimCtx& c, const ha_state_t& st, int env, const ObsIn& in, boo
     wsync();
     // DR observation noise (vec_task.py:427-428: applied to obs_buf after post_physics_step, not to the
     // teacher observations and not in VecTask.reset)
-    bool noise = !obs_only && p.dr_enable;
-    uint32_t nctr = (st.episode[env] << 12) ^ (uint32_t)st.progress_buf[env];
     for (int e = lane; e < NOBS; e += 64) {
         float v = ob[e];
         st.teacher_obs[(size_t)env * NOBS + e] = v;
-        if (noise) v = v + p.dr_obs_noise * gauss01(p.seed, env, nctr, e);
+        if (!obs_only) v = dr_obs(c, env, e, v);
         st.obs[(size_t)env * NOBS + e] = v;
     }
     if (obs_only) return;     // VecTask.reset(): compute_observations without a refresh

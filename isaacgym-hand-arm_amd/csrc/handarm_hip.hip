@@ -216,18 +216,18 @@ __device__ __forceinline__ void load_env(SimCtx& c, const ha_state_t& st, int en
         const float* r = st.root_state + ((size_t)env * A + m.actor_object0 + o) * 13;
         int pid = (int)st.object_indices[(size_t)env * NO + o];
         c.o[o].pool = pid;
-        if (st.object_scale) {
-            const float* sc = st.object_scale + ((size_t)env * NO + o) * 3;
-            c.o[o].osc[0] = sc[0]; c.o[o].osc[1] = sc[1]; c.o[o].osc[2] = sc[2]; c.o[o].osc[3] = 1.0f;
-        } else {
-            c.o[o].osc[0] = c.o[o].osc[1] = c.o[o].osc[2] = 1.0f;
-            c.o[o].osc[3] = 0.0f;
-        }
+        dr_object_scale(c, st, env, o);         // object_scale row x the DR actor scale (ha_dr.h)
         c.o[o].ofx[0] = c.o[o].ofx[1] = c.o[o].ofx[2] = c.o[o].ofx[3] = 0.0f;
+        c.o[o].otq[0] = c.o[o].otq[1] = c.o[o].otq[2] = 0.0f;
         if (take_force && st.object_force) {
             float* fo = st.object_force + ((size_t)env * NO + o) * 3;
             c.o[o].ofx[0] = fo[0]; c.o[o].ofx[1] = fo[1]; c.o[o].ofx[2] = fo[2];
             fo[0] = fo[1] = fo[2] = 0.0f;
+        }
+        if (take_force && st.object_torque) {
+            float* tq = st.object_torque + ((size_t)env * NO + o) * 3;
+            c.o[o].otq[0] = tq[0]; c.o[o].otq[1] = tq[1]; c.o[o].otq[2] = tq[2];
+            tq[0] = tq[1] = tq[2] = 0.0f;
         }
         qf q = ldq(r + 3);
         stq(c.o[o].oq, q);
@@ -368,7 +368,10 @@ __device__ __forceinline__ void run_physics(SimCtx& c, int n_calls) {
     float hdt = c.p->dt / (float)c.p->substeps;
     for (int k = 0; k < n_calls; k++) {
         for (int sub = 0; sub < c.p->substeps; sub++) substep<PC>(c, hdt);
-        if (c.lane < c.NO) c.o[c.lane].ofx[0] = c.o[c.lane].ofx[1] = c.o[c.lane].ofx[2] = 0.0f;
+        if (c.lane < c.NO) {
+            c.o[c.lane].ofx[0] = c.o[c.lane].ofx[1] = c.o[c.lane].ofx[2] = 0.0f;
+            c.o[c.lane].otq[0] = c.o[c.lane].otq[1] = c.o[c.lane].otq[2] = 0.0f;
+        }
         wsync();
     }
 }
@@ -579,6 +582,9 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
     c.NO = params->n_objects;
     c.L = model->n_links;
     c.dr = (params->dr_enable && st.dr_scale) ? st.dr_scale + (size_t)env * HA_DR_SIZE : nullptr;
+    // v16: the shard-wide DR state (ha_dr_global_kernel ran before this launch); with it the per-env sampling, the
+    // noise and the randomized gravity are on
+    c.drg = (c.dr && st.dr_global) ? st.dr_global : nullptr;
     ObsIn& in = c.s->u.pd.in;
     AhIn& ain = *reinterpret_cast<AhIn*>(&c.s->u.pd.in);
     AkPost& akp = *reinterpret_cast<AkPost*>(&c.s->u.pd.in);
@@ -613,6 +619,9 @@ __device__ __forceinline__ void env_body(const ha_model_t* __restrict__ model, c
         store_env(c, S, env);
         return;
     }
+    // apply_randomizations' per-env part (ha_dr.h) before the task's resets; the Ur5Sih reset launch resets every env
+    if (c.drg) dr_env_pre(c, S, env, (MODE == MODE_RESET && TASK == HA_TASK_UR5SIH) || S.reset_buf[env] != 0,
+                          MODE == MODE_STEP);
     if (TASK == HA_TASK_ALLEGRO_KUKA) {
         // pre_physics_step (allegro_kuka_base.py:1355-1424). Lane k holds task_state field k in tsv; it goes
         // back to HBM before the physics (whose LDS union overwrites everything) and ak_post reloads it.
@@ -790,6 +799,23 @@ extern "C" __global__ void ha_copy_indexed_kernel(float* dst, const float* src, 
     int i = t / per, k = t % per;
     size_t base = (size_t)idx[i] * per;
     dst[base + k] = src[base + k];
+}
+
+// ----------------------------------------------------------------------------- domain randomization, shard-wide
+// apply_randomizations' non-env part before a step (mode 0) or reset (mode 1) launch (ha_dr.h dr_global_update): one
+// workgroup ORs the reset flags (reset_idx runs, and with it apply_randomizations, when any env resets), then one
+// lane updates dr_global. force_any: the launch resets every env regardless of the flags (the Ur5Sih reset launch).
+extern "C" __global__ void __launch_bounds__(256) ha_dr_global_kernel(const ha_params_t* __restrict__ params,
+                                                                       const int64_t* __restrict__ reset_buf, int n,
+                                                                       float* __restrict__ g, int mode, int force_any) {
+    __shared__ int any;
+    if (threadIdx.x == 0) any = force_any;
+    __syncthreads();
+    int a = 0;
+    for (int i = threadIdx.x; i < n; i += 256) a |= reset_buf[i] != 0 ? 1 : 0;
+    if (a) any = 1;                     // every writer stores 1
+    __syncthreads();
+    if (threadIdx.x == 0) dr_global_update(*params, g, any, mode);
 }
 
 // ----------------------------------------------------------------------------- step epilogue
@@ -986,6 +1012,21 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
         if (params->ak_palm_link < 0 || params->ak_palm_link >= model->n_links) return HA_E_MODEL;
         for (int i = 0; i < 4; i++)
             if (params->ak_fingertip_links[i] < 0 || params->ak_fingertip_links[i] >= model->n_links) return HA_E_MODEL;
+        // privilegedActions (v16): 3 torque actions ahead of the 23
+        if (params->num_actions != AK_NUM_ACT + (params->ak_privileged_actions ? 3 : 0)) return HA_E_ARG;
+    }
+    // the DR schema (v16): known distributions / operations / schedules, positive loguniform ranges, a frequency
+    if (params->dr_enable) {
+        if (params->dr_frequency < 1) return HA_E_ARG;
+        for (int k = 0; k < HA_DRA_N; k++) {
+            const ha_dr_attr_t& a = params->dr_attr[k];
+            if (a.dist < HA_DR_DIST_OFF || a.dist > HA_DR_DIST_GAUSSIAN || a.op < HA_DR_OP_ADDITIVE ||
+                a.op > HA_DR_OP_SCALING || a.sched < HA_DR_SCHED_NONE || a.sched > HA_DR_SCHED_CONSTANT ||
+                (a.sched == HA_DR_SCHED_LINEAR && a.sched_steps < 1) || a.num_buckets < 0)
+                return HA_E_ARG;
+            if (a.dist == HA_DR_DIST_LOGUNIFORM && !(a.range[0] > 0.0f && a.range[1] > 0.0f)) return HA_E_ARG;
+            if ((k == HA_DRA_OBS || k == HA_DRA_ACT) && a.dist == HA_DR_DIST_LOGUNIFORM) return HA_E_ARG;
+        }
     }
     if (model->n_actors < 1 || model->n_bodies < model->n_links + params->n_objects) return HA_E_MODEL;
     int fam = family_of(params);
@@ -1054,9 +1095,12 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     // inside its hull_obb box
     if (model->n_link_hulls < 0 || model->n_link_hulls > model->n_hulls) return HA_E_MODEL;
     for (int k = 0; k < model->n_hulls; k++) {
-        bool boxed = k < model->n_link_hulls;
-        for (int p = 0; p < model->n_pool; p++) boxed = boxed || (model->pool_nhull[p] == 1 && model->pool_hull[p] == k);
-        if (boxed && !hull_in_box(model, k)) return HA_E_MODEL;
+        bool boxed = k < model->n_link_hulls, obj = false;
+        for (int p = 0; p < model->n_pool; p++) obj = obj || (model->pool_nhull[p] == 1 && model->pool_hull[p] == k);
+        if ((boxed || obj) && !hull_in_box(model, k)) return HA_E_MODEL;
+        // a one-piece object's box is read with the identity orientation (ha_physics.h object_box): refuse any other
+        const float* oq = model->hull_obb[k] + 6;
+        if (obj && !(oq[0] == 0.0f && oq[1] == 0.0f && oq[2] == 0.0f && oq[3] == 1.0f)) return HA_E_MODEL;
     }
     // self-collision pairs (v12): two link hulls of the model each; only the Allegro families' kernels run them
     if (model->n_self_pairs < 0 || model->n_self_pairs > HA_MAX_SELF_PAIRS) return HA_E_MODEL;
@@ -1385,10 +1429,24 @@ int ha_set_stats_ring(ha_handle h, int32_t n_slots) {
 // the task buffers a fused entry point needs besides the physics tensors
 static bool task_bound(ha_handle h) {
     const ha_state_t& s = h->st;
+    // DR on (v16): the rows, the shard-wide state and the per-env counters the sampling keys on
+    if (h->h_params.dr_enable && !(s.dr_scale && s.dr_global && s.randomize_buf && s.episode && s.reset_buf))
+        return false;
     if (h->task == HA_TASK_ALLEGRO_KUKA)
         return s.task_state && s.task_scalars && s.object_scale && s.goal_state && s.successes && s.reset_goal_buf &&
                s.dof_position_targets && s.reset_buf && s.progress_buf && s.rew && s.timeout_buf && s.episode;
+    // AllegroHand random forces keep their decayed force, probability and RNG counter in task_state (AH_TS_*)
+    if (h->task == HA_TASK_ALLEGRO_HAND && h->h_params.ah_force_scale > 0.0f && !s.task_state) return false;
     return true;
+}
+
+// the shard-wide DR update before a step / reset launch (dr_enable only)
+static int dr_global(ha_handle h, int mode, void* stream) {
+    if (!h->h_params.dr_enable) return HA_OK;
+    hipLaunchKernelGGL(ha_dr_global_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, h->d_params, h->st.reset_buf,
+                       h->N, h->st.dr_global, mode, mode == 1 && h->task == HA_TASK_UR5SIH ? 1 : 0);
+    HIPCHK(hipGetLastError());
+    return HA_OK;
 }
 
 int ha_task_step(ha_handle h, uint32_t flags, void* stream) {
@@ -1398,7 +1456,9 @@ int ha_task_step(ha_handle h, uint32_t flags, void* stream) {
     int slot = (int)(h->step_counter % h->stat_slots);
     int next = (int)((h->step_counter + 1) % h->stat_slots);
     h->step_counter++;
-    int rc = launch(h, MODE_STEP, next, flags, slot, stream);     // clears `next` for the following step
+    int rc = dr_global(h, 0, stream);
+    if (rc != HA_OK) return rc;
+    rc = launch(h, MODE_STEP, next, flags, slot, stream);         // clears `next` for the following step
     if (rc == HA_OK && h->task == HA_TASK_ALLEGRO_HAND && h->st.consecutive_successes) {
         // consecutive_successes EWMA over the shard's resets of this step (allegro_hand.py:714-717)
         hipLaunchKernelGGL(ah_consecutive_successes_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
@@ -1445,6 +1505,8 @@ int ha_task_observe(ha_handle h, uint32_t flags, void* stream) {
 
 int ha_task_reset(ha_handle h, uint32_t flags, void* stream) {
     if (!h || !h->bound || !task_bound(h)) return HA_E_STATE;
+    int rc = dr_global(h, 1, stream);
+    if (rc != HA_OK) return rc;
     return launch(h, MODE_RESET, 0, flags, 0, stream);
 }
 

@@ -8,7 +8,7 @@ CSRC = os.path.join(os.path.dirname(PKG), "csrc")
 INCLUDE = os.path.join(os.path.dirname(os.path.dirname(PKG)), "include")
 LIB = os.path.join(PKG, "libhandarm_hip.so")
 SOURCES = ["handarm_hip.hip"]
-HEADERS = ["ha_device.h", "ha_physics.h", "ha_task.h", "ah_task.h", "ak_task.h", "ha_pointcloud.h", "ha_camera.h"]
+HEADERS = ["ha_device.h", "ha_physics.h", "ha_dr.h", "ha_task.h", "ah_task.h", "ak_task.h", "ha_pointcloud.h", "ha_camera.h"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wno-unused-result"]
 

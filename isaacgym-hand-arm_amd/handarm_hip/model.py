@@ -30,8 +30,19 @@ MAX_MPAIRS = 192
 MAX_SELF_PAIRS = 512
 STAT_SIZE = 2 + 2 * MAX_POOL
 DRAW_STRIDE = 80
-DR_SIZE = 80
+DR_SIZE = 184
 DR_LINK_MASS, DR_OBJ_MASS, DR_LINK_FRIC, DR_OBJ_FRIC = 0, 32, 40, 72
+DR_DOF_KP, DR_DOF_KD, DR_DOF_LOWER, DR_DOF_UPPER, DR_OBJ_SCALE = 80, 104, 128, 152, 176      # v16
+# v16: randomized quantities (ha_params_t.dr_attr[HA_DRA_*]) and the shard-wide DR state (ha_state_t.dr_global)
+DRA_OBS, DRA_ACT, DRA_GRAVITY, DRA_LINK_MASS, DRA_LINK_FRIC, DRA_DOF_KD, DRA_DOF_KP, DRA_DOF_LOWER, DRA_DOF_UPPER, \
+    DRA_OBJ_MASS, DRA_OBJ_FRIC, DRA_OBJ_SCALE = range(12)
+DRA_N = 12
+DR_DIST = {"off": 0, "uniform": 1, "loguniform": 2, "gaussian": 3}
+DR_OP = {"additive": 0, "scaling": 1}
+DR_SCHED = {None: 0, "linear": 1, "constant": 2}
+DRG_FRAME, DRG_FRAME_NEXT, DRG_LAST_RAND, DRG_FIRST, DRG_ALL, DRG_STEP, DRG_EPOCH, DRG_VALID = range(8)
+DRG_OBS, DRG_ACT, DRG_ACT_USE, DRG_ACT_EPOCH, DRG_ACT_ON, DRG_GRAVITY = 8, 12, 16, 20, 21, 24
+DRG_SIZE = 32
 TASK_UR5SIH, TASK_ALLEGRO_HAND, TASK_ALLEGRO_KUKA = 0, 1, 2
 # AllegroKuka task_state row (HA_AK_* in handarm_abi.h)
 AK_TS = 48
@@ -48,6 +59,12 @@ FLAG_OBS_ONLY = 4
 NP_NO_EDGE_AXES, NP_NO_CLIP = 1, 2      # ha_params_t.narrow_phase_flags
 
 f32, i32 = C.c_float, C.c_int32
+
+
+class HaDrAttr(C.Structure):
+    """ha_dr_attr_t (include/handarm_abi.h v16): one randomized quantity of task.randomization_params."""
+    _fields_ = [("dist", i32), ("op", i32), ("sched", i32), ("sched_steps", i32), ("range", f32 * 2),
+                ("range_corr", f32 * 2), ("num_buckets", i32), ("setup_only", i32)]
 
 
 def arr(t, *dims):
@@ -114,8 +131,7 @@ class HaParams(C.Structure):
         ("ah_reset_position_noise", f32), ("ah_reset_dof_pos_noise", f32), ("ah_reset_dof_vel_noise", f32),
         ("ah_act_moving_average", f32), ("ah_vel_obs_scale", f32), ("ah_force_torque_obs_scale", f32),
         ("ah_object_init", arr(f32, 7)), ("ah_goal_init", arr(f32, 3)), ("ah_goal_displacement", arr(f32, 3)),
-        ("dr_enable", i32), ("dr_mass_lo", f32), ("dr_mass_hi", f32), ("dr_fric_lo", f32), ("dr_fric_hi", f32),
-        ("dr_fric_buckets", i32), ("dr_obs_noise", f32), ("dr_act_noise", f32),
+        ("dr_enable", i32),
         ("ak_subtask", i32), ("ak_num_keypoints", i32), ("ak_keypoints", arr(f32, 4, 3)),
         ("ak_object_base_size", f32), ("ak_keypoint_scale", f32), ("ak_initial_tolerance", f32),
         ("ak_target_tolerance", f32), ("ak_lifting_rew_scale", f32), ("ak_lifting_bonus", f32),
@@ -137,6 +153,8 @@ class HaParams(C.Structure):
         ("ah_obs_type", i32), ("ah_asymmetric", i32), ("ah_relative_control", i32), ("ah_speed_dt", f32),   # v15
         ("ah_force_scale", f32), ("ah_force_prob_lo", f32), ("ah_force_prob_hi", f32), ("ah_force_decay_step", f32),
         ("ah_object_rb_mass", f32), ("ah_object_type", i32),
+        ("dr_frequency", i32), ("dr_attr", HaDrAttr * 12),                   # v16
+        ("ak_privileged_actions", i32), ("ak_privileged_torque", f32),
     ]
 
 
@@ -150,7 +168,7 @@ STATE_FIELDS = ["root_state", "rigid_body_state", "dof_state", "net_contact_forc
                 "ur5_target", "servo", "smoothed", "obs_cache", "reset_draws", "episode", "stats", "term_sums",
                 "flags", "collision_enabled", "dof_force", "reset_goal_buf", "successes", "goal_state",
                 "consecutive_successes", "dr_scale", "object_scale", "object_force", "task_state", "task_scalars",
-                "contact_stats", "contact_cache"]
+                "contact_stats", "contact_cache", "dr_global", "randomize_buf", "object_torque"]
 PCM_REC = 48        # HA_PCM_REC: floats per persistent-manifold record (include/handarm_abi.h v13)
 CSTAT = 8           # HA_CSTAT: contact_stats columns
 
@@ -213,6 +231,7 @@ def state_spec(num_envs, n_links=29, n_dofs=17, n_obj=3, num_initial_poses=1, nu
         "object_scale": ((N, n_obj, 3), f), "object_force": ((N, n_obj, 3), f), "task_state": ((N, AK_TS), f),
         "task_scalars": ((4,), f), "contact_stats": ((N, CSTAT), i32),
         "contact_cache": ((N, n_pcm_slots, PCM_REC), f),
+        "dr_global": ((DRG_SIZE,), f), "randomize_buf": ((N,), i32), "object_torque": ((N, n_obj, 3), f),
     }
 
 
@@ -633,8 +652,7 @@ DEFAULT_TASK = dict(
     joint_limit_margin=0.02, n_objects=3, num_initial_poses=1, max_episode_length=200,
     sih_alpha=0.8, reward_reaching=1.0, reward_lifting=5.0, reward_goal=50.0, reward_success=50.0,
     lifting_threshold=0.05, goal_threshold=0.05, goal_pos=(0.28, 0.58, 0.8), goal_noise=(0.15, 0.15, 0.1),
-    dr_enable=0, dr_mass=(0.5, 1.5), dr_friction=(0.7, 1.3), dr_friction_buckets=250, dr_obs_noise=0.002,
-    dr_act_noise=0.05,     # BASELINE config 4 "DR on" (ranges of AllegroKuka.yaml:121-207)
+    dr_enable=0,           # task.randomize; the schema: handarm_hip/dr.py (apply_schema)
     drop_pos=(0.28, 0.58, 1.5), drop_noise=(0.1, 0.1, 0.0), drop_num_steps=100,
     reset_pose=(0.6985, -1.4106, 1.2932, 0.1174, 0.6983, 1.5708, 0., 0., 0., 0., 0., 0., 0., 0., -1.571, 0., 0.),
     bringup_pose=(0., -1.571, 0., 0., 0., 0., 0., 0., 0., 0., 0., 0., 0., 0., -1.571, 0., 0.),
@@ -804,13 +822,13 @@ def build_params(cfg=None, task=None):
         p.spline_pieces[i] = tab.shape[1]
         sp[i, :, :tab.shape[1]] = tab
     p.thumb_opposition_gain = np.float32(-1.571 / 2675)
-    p.dr_enable = int(c.get("dr_enable", 0))
-    p.dr_mass_lo, p.dr_mass_hi = c.get("dr_mass", (0.5, 1.5))
-    p.dr_fric_lo, p.dr_fric_hi = c.get("dr_friction", (0.7, 1.3))
-    p.dr_fric_buckets = int(c.get("dr_friction_buckets", 250))
-    p.dr_obs_noise = c.get("dr_obs_noise", 0.002)
-    p.dr_act_noise = c.get("dr_act_noise", 0.05)
     p.task = c.get("task", TASK_UR5SIH)
+    # domain randomization (v16): task.randomize + task.randomization_params (handarm_hip/dr.py); dr_enable without a
+    # schema takes the task family's default (Ur5Sih: the build's config-4 definition)
+    p.dr_enable = int(c.get("dr_enable", 0))
+    if p.dr_enable:
+        from . import dr as DR
+        DR.apply_schema(p, c.get("randomization_params"), p.task)
     p.num_actions = c.get("num_actions", 11)
     p.num_obs = c.get("num_obs", ur5sih_num_obs(int(c["n_objects"])))
     if p.task == TASK_ALLEGRO_HAND:
@@ -859,7 +877,10 @@ def _kuka_params(p, c):
     for j, kp in enumerate(kps):
         p.ak_keypoints[j][:] = kp
     p.num_obs = 93 + 6 * len(kps)                      # full_state_size (allegro_kuka_base.py:185-220)
-    p.num_actions = 23
+    # privilegedActions: 3 object-torque actions ahead of the 23 (allegro_kuka_base.py:62-74), privilegedActionsTorque
+    p.ak_privileged_actions = int(bool(c.get("privileged_actions", False)))
+    p.ak_privileged_torque = c.get("privileged_actions_torque", 0.02)
+    p.num_actions = 23 + 3 * p.ak_privileged_actions
     p.max_episode_length = c.get("max_episode_length_override") or c["episode_length"][sub]
     p.ak_success_steps = c["success_steps"][sub] if isinstance(c["success_steps"], dict) else c["success_steps"]
     for k in ["object_base_size", "keypoint_scale", "lifting_rew_scale", "lifting_bonus", "lifting_bonus_threshold",

@@ -61,13 +61,11 @@ class HandArmSim:
         self.t["collision_enabled"].fill_(1)
         if task == HM.TASK_ALLEGRO_HAND:          # objectType: the scene's pool entry in every env
             self.t["object_indices"].fill_(int(self.params.ah_object_type))
-        # domain-randomization rows start at the nominal values (mass scale 1, friction) until the first
-        # reset samples them (ha_task.h dr_sample)
-        dr = self.t["dr_scale"]
-        dr[:, HM.DR_LINK_MASS:HM.DR_LINK_MASS + HM.MAX_LINKS] = 1.0
-        dr[:, HM.DR_OBJ_MASS:HM.DR_OBJ_MASS + HM.MAX_OBJ] = 1.0
-        dr[:, HM.DR_LINK_FRIC:HM.DR_LINK_FRIC + HM.MAX_LINKS] = self.params.friction
-        dr[:, HM.DR_OBJ_FRIC:HM.DR_OBJ_FRIC + HM.MAX_OBJ] = self.params.friction
+        # domain-randomization rows start at the nominal values (mass ratio 1, friction, the model's DOF gains and
+        # limits, scale 1) until an env's first sample, and the shard-wide state at frame 0 (handarm_hip/dr.py)
+        from . import dr as DR
+        self.t["dr_scale"].copy_(torch.from_numpy(DR.default_rows(self.model, self.params, num_envs)))
+        self.t["dr_global"].copy_(torch.from_numpy(DR.init_global(self.params)))
         if task == HM.TASK_ALLEGRO_KUKA:
             self._init_kuka()
         h = C.c_void_p()

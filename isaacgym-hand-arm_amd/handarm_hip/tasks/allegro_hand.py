@@ -62,6 +62,13 @@ class AllegroHand:
                 task_cfg[name] = type(c[name])(env[key])
         if "forceProbRange" in env:
             task_cfg["force_prob_range"] = tuple(float(x) for x in env["forceProbRange"])
+        # task.randomize (AllegroHand.yaml:67-150): the reference's AllegroHand counts randomize_buf but never calls
+        # apply_randomizations; here the same device engine as AllegroKuka's runs the schema (handarm_hip/dr.py)
+        task = cfg.get("task", {}) or {}
+        self.randomize = bool(task.get("randomize", False))
+        if self.randomize:
+            task_cfg["dr_enable"] = 1
+            task_cfg["randomization_params"] = task.get("randomization_params")
         self.sim = HandArmSim(self.num_environments, sim_device, task_cfg=task_cfg, task=HM.TASK_ALLEGRO_HAND)
         self.sim_flags = 0
         N, t = self.num_environments, self.sim.t
@@ -73,6 +80,7 @@ class AllegroHand:
         self.rew_buf = t["rew"]
         self.reset_buf = t["reset_buf"]
         self.reset_goal_buf = t["reset_goal_buf"]
+        self.randomize_buf = t["randomize_buf"]           # vec_task.py:352 (counted on the device)
         self.progress_buf = t["progress_buf"]
         self.timeout_buf = t["timeout_buf"]
         self.successes = t["successes"]

@@ -69,9 +69,8 @@ class AllegroKuka:
                                       "values) are implemented")
         if env.get("useRelativeControl", False):       # the reference's own answer (allegro_kuka_base.py:1373-1374)
             raise NotImplementedError("Use relative control False for now")
-        if env.get("privilegedActions", False) or env.get("randomizeObjectDimensions", True) is False:
-            raise NotImplementedError("only the AllegroKuka.yaml defaults for privileged actions (object torques) "
-                                      "and object dimensions are implemented")
+        if env.get("randomizeObjectDimensions", True) is False:
+            raise NotImplementedError("only the AllegroKuka.yaml default for object dimensions is implemented")
         family = (True, False, False) if sub == "throw" else (True, True, True)      # env/throw.yaml:15-18
         if tuple(bool(env.get(k, d)) for k, d in zip(("withSmallCuboids", "withBigCuboids", "withSticks"), family)) \
                 != family:
@@ -92,6 +91,18 @@ class AllegroKuka:
                                                 float(env["resetPositionNoiseZ"]))
         if "forceProbRange" in env:
             task_cfg["force_prob_range"] = tuple(float(x) for x in env["forceProbRange"])
+        # privilegedActions / privilegedActionsTorque (AllegroKuka.yaml:54-55, allegro_kuka_base.py:62-74): 3 object
+        # torque actions ahead of the 23
+        self.privileged_actions = bool(env.get("privilegedActions", False))
+        task_cfg["privileged_actions"] = self.privileged_actions
+        task_cfg["privileged_actions_torque"] = float(env.get("privilegedActionsTorque", 0.02))
+        # task.randomize / task.randomization_params (AllegroKuka.yaml:115-207): apply_randomizations from reset_idx
+        # (allegro_kuka_base.py:1248-1249), on the device (handarm_hip/dr.py, csrc/ha_dr.h)
+        task = cfg.get("task", {}) or {}
+        self.randomize = bool(task.get("randomize", False))
+        if self.randomize:
+            task_cfg["dr_enable"] = 1
+            task_cfg["randomization_params"] = task.get("randomization_params")
         self.sim = HandArmSim(self.num_environments, sim_device, task_cfg=task_cfg, task=HM.TASK_ALLEGRO_KUKA)
         self.tcfg = self.sim.cfg
         p = self.sim.params
@@ -106,12 +117,13 @@ class AllegroKuka:
         self.sim_flags = 0
         N, t = self.num_environments, self.sim.t
         self.num_observations = self.num_states = p.num_obs
-        self.num_actions = 23
+        self.num_actions = p.num_actions                # 23, or 26 with privilegedActions
         self.obs_buf = t["obs"]
         self.states_buf = torch.zeros((N, self.num_states), device=sim_device)    # allocated, never written
         self.rew_buf = t["rew"]
         self.reset_buf = t["reset_buf"]
         self.reset_goal_buf = t["reset_goal_buf"]
+        self.randomize_buf = t["randomize_buf"]           # vec_task.py:352 (counted on the device)
         self.progress_buf = t["progress_buf"]
         self.timeout_buf = t["timeout_buf"]
         self.successes = t["successes"]

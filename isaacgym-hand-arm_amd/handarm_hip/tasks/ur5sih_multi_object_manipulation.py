@@ -95,14 +95,18 @@ class Ur5SihMultiObjectManipulation:
         task_cfg = dict(control_freq_inv=self.control_freq_inv, max_episode_length=self.max_episode_length,
                         n_objects=self.num_objects, num_initial_poses=self.num_initial_poses,
                         seed=int(cfg.get("seed", 42)))
-        # BASELINE config 4 "DR on": device-side domain randomization (mass / friction resampled at reset,
-        # observation noise in the step kernel, action noise below). The reference's Ur5Sih `randomize`
-        # flag has no consumer, so this is the build's own switch: cfg["task"]["randomize"].
+        # BASELINE config 4 "DR on": device-side domain randomization (handarm_hip/dr.py, csrc/ha_dr.h: actor
+        # properties resampled at reset, action and observation noise in the step kernel). The reference's Ur5Sih
+        # `randomize` flag has no consumer, so this is the build's own switch: cfg["task"]["randomize"],
+        # with cfg["task"]["randomization_params"] in the reference's schema, or the build's config-4 schema
+        # (dr.UR5SIH_SCHEMA) when it has none
         self.randomize = bool(_get(cfg, "task.randomize", False))
         # seed-faithful draws (handarm_hip/ref_rng.py): resets, drops and cloud permutations from torch's global
         # CPU generator in the reference's order, instead of the device counter hash
         self.reference_rng = bool(_get(cfg, "sim.reference_rng", False))
         task_cfg["dr_enable"] = int(self.randomize)
+        if self.randomize:
+            task_cfg["randomization_params"] = _get(cfg, "task.randomization_params", None)
         rew = _get(cfg, "rl.reward", None)
         if rew:
             for k in REWARD_TERMS:
@@ -142,6 +146,7 @@ class Ur5SihMultiObjectManipulation:
         self.teacher_obs_buf = t["teacher_obs"]
         self.rew_buf = t["rew"]
         self.reset_buf = t["reset_buf"]
+        self.randomize_buf = t["randomize_buf"]           # vec_task.py:352 (counted on the device)
         self.progress_buf = t["progress_buf"]
         self.timeout_buf = t["timeout_buf"]
         self.goal_pos = t["goal_pos"]
@@ -556,8 +561,8 @@ class Ur5SihMultiObjectManipulation:
     def step(self, actions):
         if not self.objects_dropped and bool(self.reset_buf.any()):
             self._drop_initialisation()
-        if self.randomize:      # action noise before the clamp (vec_task.py:400-404)
-            actions = actions + self.sim.params.dr_act_noise * torch.randn_like(actions)
+        # (DR action noise: added by the step kernel where it reads the actions, ha_dr.h act_at; with the HandArm
+        # configs' clipActions unset the clamp below is the identity, so noise-then-clamp (vec_task.py:400-404) is kept)
         torch.clamp(actions, -self.clip_actions, self.clip_actions, out=self.actions_buf)
         if self._stat_pending >= self.sim.stats_ring - 1:
             # ring full (this step's launch clears the slot after its own, the oldest pending one): reduce

@@ -32,6 +32,43 @@ def sincos(x):
     return s, c
 
 
+def logf(x):
+    """include/ha_fmath.h ha_logf (Cephes logf, exponent split by bits) for positive normal float32 arrays."""
+    x = np.asarray(x, F)
+    ix = x.view(np.int32)
+    e = ((ix >> 23) & 0xFF) - 126
+    m = ((ix & 0x007FFFFF) | 0x3F000000).astype(np.int32).view(F)
+    low = m < F(0.707106781186547524)
+    e = np.where(low, e - 1, e)
+    m = np.where(low, (m + m) - F(1.0), m - F(1.0)).astype(F)
+    z = m * m
+    y = F(7.0376836292e-2) * m - F(1.1514610310e-1)
+    for c in (1.1676998740e-1, -1.2420140846e-1, 1.4249322787e-1, -1.6668057665e-1, 2.0000714765e-1,
+              -2.4999993993e-1, 3.3333331174e-1):
+        y = y * m + F(c)
+    y = (y * m) * z
+    fe = e.astype(F)
+    y = y + F(-2.12194440e-4) * fe
+    y = y + F(-0.5) * z
+    r = m + y
+    return (r + F(0.693359375) * fe).astype(F)
+
+
+def expf(x):
+    """include/ha_fmath.h ha_expf (Cephes expf, two-part ln 2, result exponent by bits)."""
+    x = np.clip(np.asarray(x, F), F(-87.0), F(88.0)).astype(F)
+    z = np.floor(F(1.44269504088896341) * x + F(0.5)).astype(F)
+    x = x - z * F(0.693359375)
+    x = x - z * F(-2.12194440e-4)
+    n = z.astype(np.int32)
+    xx = x * x
+    y = F(1.9875691500e-4) * x + F(1.3981999507e-3)
+    for c in (8.3334519073e-3, 4.1665795894e-2, 1.6666665459e-1, 5.0000001201e-1):
+        y = y * x + F(c)
+    y = (y * xx + x) + F(1.0)
+    return (y * ((n + 127) << 23).astype(np.int32).view(F)).astype(F)
+
+
 def cross(a, b):
     """ha_device.h cross3 (per component a.y b.z - a.z b.y ...)."""
     return np.stack([a[..., 1] * b[..., 2] - a[..., 2] * b[..., 1],

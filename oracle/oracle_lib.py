@@ -58,6 +58,12 @@ class HostState:
         self.null = HM.null_fields(params.task if params is not None else HM.TASK_UR5SIH)
         self.arrays = {k: np.zeros(shape, dtype) for k, (shape, dtype) in self.spec.items()}
         self.num_envs = num_envs
+        if params is not None and params.dr_enable:
+            # DR on: nominal rows and the frame-0 shard state, as HandArmSim starts them (handarm_hip/dr.py)
+            from handarm_hip import dr as DR
+            m = model if model is not None else HM.build_model(HM.load_scene())
+            self.arrays["dr_scale"][:] = DR.default_rows(m, params, num_envs)
+            self.arrays["dr_global"][:] = DR.init_global(params)
 
     def __getitem__(self, k):
         return self.arrays[k]

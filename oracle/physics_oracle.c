@@ -151,9 +151,11 @@ typedef struct {
     float osc[NOBJ][3];             /* per-env object dimension scale (ha_state_t.object_scale) */
     int oscaled[NOBJ];
     v3 ofx[NOBJ];                   /* world force on the object COM for this call (object_force) */
+    v3 otq[NOBJ];                   /* world torque on the object for this call (object_torque, v16) */
     float cforce[MAXB][3];
     float dforce[HA_MAX_DOFS];      /* joint force of the last substep: (drive + lower - upper impulse) / h */
     const float* dr;                /* this env's DR row (HA_DR_*) or NULL (ha_physics.h SimCtx::dr) */
+    const float* drg;               /* the shard-wide DR state (HA_DRG_*) or NULL (ha_physics.h SimCtx::drg, v16) */
     float* pcm;                     /* this env's persistent-manifold records (ha_state_t.contact_cache) or NULL */
     int cst[HA_CSTAT];              /* contact_stats of this call sequence (ha_physics.h EnvLDS::cst) */
     float sb[8];                    /* the posed-static actor's pose (v14, ha_physics.h EnvLDS::sb): p, pad, q */
@@ -1117,8 +1119,9 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
         inv3(Iw, e->oIinv[o]);
         mass = mass * sc;
         e->om[o] = mass;
-        v3 lv = add(add(e->ov[o], mul(ld3(p->gravity), hdt)), mul(e->ofx[o], hdt / mass));
-        v3 av = mul(e->ow[o], damp);
+        const float* grav = e->drg ? e->drg + HA_DRG_GRAVITY : p->gravity;
+        v3 lv = add(add(e->ov[o], mul(ld3(grav), hdt)), mul(e->ofx[o], hdt / mass));
+        v3 av = add(mul(e->ow[o], damp), mul(mv(e->oIinv[o], e->otq[o]), hdt));
         float* vo = v + D + 6 * o;
         vo[0] = lv.x; vo[1] = lv.y; vo[2] = lv.z; vo[3] = av.x; vo[4] = av.y; vo[5] = av.z;
     }
@@ -1173,7 +1176,11 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
     float fcoef[HA_MAX_DOFS], lam_fr[HA_MAX_DOFS];
     int act_lo[HA_MAX_DOFS], act_up[HA_MAX_DOFS];
     for (int d = 0; d < D; d++) {
-        float kp = m->dof_kp[d], kd = m->dof_kd[d];
+        /* DR (v16): the env's dof_properties stiffness / damping / lower / upper (ha_physics.h joint rows) */
+        float kp = e->dr ? e->dr[HA_DR_DOF_KP + d] : m->dof_kp[d];
+        float kd = e->dr ? e->dr[HA_DR_DOF_KD + d] : m->dof_kd[d];
+        float jlo = e->dr ? e->dr[HA_DR_DOF_LOWER + d] : m->dof_lower[d];
+        float jup = e->dr ? e->dr[HA_DR_DOF_UPPER + d] : m->dof_upper[d];
         float den = kd + hdt * kp;
         float mii = Minv[d * D + d];
         dgam[d] = 1.0f / (hdt * den);
@@ -1182,7 +1189,7 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
         dlim[d] = m->dof_effort[d] * hdt;
         dlam[d] = 0.0f;
         lwinv[d] = 1.0f / (mii + 1e-9f);
-        float s_lo = e->q[d] - m->dof_lower[d], s_up = m->dof_upper[d] - e->q[d];
+        float s_lo = e->q[d] - jlo, s_up = jup - e->q[d];
         act_lo[d] = s_lo <= p->joint_limit_margin;
         act_up[d] = s_up <= p->joint_limit_margin;
         vt_lo[d] = s_lo > 0 ? -s_lo / hdt : -p->baumgarte * s_lo / hdt;
@@ -1311,6 +1318,8 @@ static void substep(const hao_handle h, env_t* e, float hdt) {
 static void load_env(const hao_handle h, const ha_state_t* S, int env, env_t* e, int take_force) {
     const ha_model_t* m = &h->m;
     int D = h->D, A = h->A;
+    e->dr = (h->p.dr_enable && S->dr_scale) ? S->dr_scale + (size_t)env * HA_DR_SIZE : NULL;
+    e->drg = (e->dr && S->dr_global) ? S->dr_global : NULL;
     for (int d = 0; d < D; d++) {
         e->q[d] = S->dof_state[(env * D + d) * 2];
         e->qd[d] = S->dof_state[(env * D + d) * 2 + 1];
@@ -1320,13 +1329,22 @@ static void load_env(const hao_handle h, const ha_state_t* S, int env, env_t* e,
         const float* r = S->root_state + (env * A + m->actor_object0 + o) * 13;
         int pid = (int)S->object_indices[env * h->NO + o];
         e->pool[o] = pid;
-        e->oscaled[o] = S->object_scale != NULL;
-        for (int k = 0; k < 3; k++) e->osc[o][k] = S->object_scale ? S->object_scale[(env * h->NO + o) * 3 + k] : 1.0f;
+        /* object_scale row x the DR actor scale (ha_dr.h dr_object_scale); unscaled when neither applies */
+        float ds = e->dr ? e->dr[HA_DR_OBJ_SCALE + o] : 1.0f;
+        e->oscaled[o] = S->object_scale != NULL || ds != 1.0f;
+        for (int k = 0; k < 3; k++) e->osc[o][k] = (S->object_scale ? S->object_scale[(env * h->NO + o) * 3 + k] : 1.0f) * ds;
+        if (!e->oscaled[o]) e->osc[o][0] = e->osc[o][1] = e->osc[o][2] = 1.0f;
         e->ofx[o] = V(0, 0, 0);
+        e->otq[o] = V(0, 0, 0);
         if (take_force && S->object_force) {
             float* fo = S->object_force + (env * h->NO + o) * 3;
             e->ofx[o] = ld3(fo);
             fo[0] = fo[1] = fo[2] = 0.0f;
+        }
+        if (take_force && S->object_torque) {
+            float* tq = S->object_torque + (env * h->NO + o) * 3;
+            e->otq[o] = ld3(tq);
+            tq[0] = tq[1] = tq[2] = 0.0f;
         }
         e->oq[o] = ldq(r + 3);
         e->oc[o] = add(ld3(r), qrot(e->oq[o], scl(env_scale(e, o), ld3(m->pool_com[pid]))));
@@ -1431,13 +1449,12 @@ int hao_struct_sizes(int32_t* model_size, int32_t* params_size, int32_t* state_s
 static void simulate_env(const hao_handle h, ha_state_t* S, int env, int n_calls) {
     env_t e;
     load_env(h, S, env, &e, 1);
-    e.dr = (h->p.dr_enable && S->dr_scale) ? S->dr_scale + (size_t)env * HA_DR_SIZE : NULL;
     float hdt = h->p.dt / (float)h->p.substeps;
     for (int c = 0; c < n_calls; c++) {
         for (int s = 0; s < h->p.substeps; s++) substep(h, &e, hdt);
         /* an applied force lasts one gym.simulate (apply_rigid_body_force_tensors, then the next simulate call):
          * the later calls of a multi-call launch run without it (handarm_hip.hip run_physics force_once) */
-        for (int o = 0; o < NOBJ; o++) e.ofx[o] = (v3){0.0f, 0.0f, 0.0f};
+        for (int o = 0; o < NOBJ; o++) e.ofx[o] = e.otq[o] = (v3){0.0f, 0.0f, 0.0f};
     }
     /* net contact force of the last substep (PhysX reports the last substep's forces) */
     store_env(h, S, env, &e);
@@ -1447,7 +1464,6 @@ static void simulate_env(const hao_handle h, ha_state_t* S, int env, int n_calls
 int hao_contacts(hao_handle h, ha_state_t* S, int env, float* out, int max_rows) {
     env_t e;
     load_env(h, S, env, &e, 0);
-    e.dr = (h->p.dr_enable && S->dr_scale) ? S->dr_scale + (size_t)env * HA_DR_SIZE : NULL;
     e.pcm = NULL;                       /* the narrow phase's contacts, no persistent manifold */
     fk(h, &e);
     contact_t cs[MAXC];

@@ -21,6 +21,7 @@ import numpy as np
 from handarm_hip import model as HM
 from oracle import f32
 from oracle import allegro_oracle as AO
+from oracle import dr_oracle as DO
 from oracle import kuka_oracle as KO
 from oracle import task_oracle as TO
 
@@ -35,8 +36,15 @@ def kuka_step(orc, hs, p, lo, up, scalars, draws):
     st = dict(dof=hs["dof_state"].reshape(N, D, 2), root=hs["root_state"].reshape(N, A, 13), goal=hs["goal_state"],
               targets=hs["dof_position_targets"], reset=hs["reset_buf"], reset_goal=hs["reset_goal_buf"],
               progress=hs["progress_buf"], successes=hs["successes"], ts=hs["task_state"])
-    KO.pre(p, st, hs["actions"], draws, lo, up)
+    dr_pre(p, orc.model, hs)
+    act = noisy_actions(p, hs, hs["actions"])
+    # privilegedActions: torque actions 0..2; the hand reads actions[:, 3:][:, 7:23], the arm self.actions[:, :7]
+    pv = 3 if p.ak_privileged_actions else 0
+    eff = np.concatenate([act[:, :7], act[:, 7 + pv:23 + pv]], 1) if pv else act
+    KO.pre(p, st, eff, draws, lo, up)
     hs["sim_targets"][:] = hs["dof_position_targets"]
+    if pv:
+        hs["object_torque"].reshape(N, 3)[:] = act[:, 0:3] * F(p.ak_privileged_torque)
     # apply_rigid_body_force_tensors(LOCAL_SPACE) at the object COM: world force = R(q_object) F_local (ak_forces)
     a0 = orc.model.actor_object0
     fl = hs["task_state"][:, HM.AK_RB_FORCE:HM.AK_RB_FORCE + 3]
@@ -49,6 +57,8 @@ def kuka_step(orc, hs, p, lo, up, scalars, draws):
                                        hs["goal_state"], hs["progress_buf"], hs["successes"], hs["reset_buf"],
                                        hs["object_scale"].reshape(N, 3), scalars, lo, up)
     hs["reset_buf"][:], hs["reset_goal_buf"][:], hs["progress_buf"][:], hs["successes"][:] = rs, rg, pr, sc
+    if p.dr_enable:
+        obs = DO.obs_noise(p, hs["dr_global"], obs)
     hs["rew"][:] = rew
     hs["obs"][:] = obs
     return obs, rew, KO.timeout(p, pr, rs)
@@ -62,6 +72,8 @@ def allegro_step(orc, hs, p, lo, up, draws):
     c["act_moving_average"] = float(p.ah_act_moving_average)
     root = hs["root_state"].reshape(N, 3, 13)
     dof = hs["dof_state"].reshape(N, D, 2)
+    dr_pre(p, orc.model, hs)
+    act = noisy_actions(p, hs, hs["actions"])               # self.actions: targets, obs and the action penalty
     for e in range(N):
         goal, full = hs["reset_goal_buf"][e] != 0, hs["reset_buf"][e] != 0
         if goal or full:
@@ -73,7 +85,7 @@ def allegro_step(orc, hs, p, lo, up, draws):
                          draws[e, AO.DRAW_RESET:AO.DRAW_RESET + 37], lo, up, c)
             hs["progress_buf"][e], hs["reset_buf"][e], hs["successes"][e] = 0, 0, 0
             hs["task_state"][e, 0:3] = 0                              # rb_forces[env_ids] = 0 (ah_task.h AH_TS_*)
-    hs["dof_position_targets"][:] = AO.targets_from_actions(hs["actions"], hs["dof_position_targets"], lo, up, c)
+    hs["dof_position_targets"][:] = AO.targets_from_actions(act, hs["dof_position_targets"], lo, up, c)
     hs["sim_targets"][:] = hs["dof_position_targets"]
     if p.ah_force_scale > 0:
         # random forces (ah_forces, replayed selection): decay, new N(0,1)^3 * mass * scale, LOCAL_SPACE -> world force
@@ -85,12 +97,14 @@ def allegro_step(orc, hs, p, lo, up, draws):
         hs["object_force"].reshape(N, 3)[:] = f32.qrot(root[:, 1, 3:7], f)
     orc.simulate(hs, p.control_freq_inv)
     hs["progress_buf"][:] = hs["progress_buf"] + 1
-    obs = AO.observations(dof[..., 0], dof[..., 1], hs["dof_force"], root[:, 1], hs["goal_state"], hs["actions"], lo, up, c)
-    rew, rs, rg, pr, sc, cons = AO.reward(root[:, 1], hs["goal_state"], hs["actions"], hs["reset_buf"],
+    obs = AO.observations(dof[..., 0], dof[..., 1], hs["dof_force"], root[:, 1], hs["goal_state"], act, lo, up, c)
+    rew, rs, rg, pr, sc, cons = AO.reward(root[:, 1], hs["goal_state"], act, hs["reset_buf"],
                                           hs["reset_goal_buf"], hs["progress_buf"], hs["successes"],
                                           hs["consecutive_successes"][0], c)
     hs["reset_buf"][:], hs["reset_goal_buf"][:], hs["progress_buf"][:], hs["successes"][:] = rs, rg, pr, sc
     hs["consecutive_successes"][0] = cons
+    if p.dr_enable:
+        obs = DO.obs_noise(p, hs["dr_global"], obs)
     hs["rew"][:] = rew
     hs["obs"][:] = obs
     timeout = (pr >= c["max_episode_length"] - 1) & (rs != 0)
@@ -98,34 +112,26 @@ def allegro_step(orc, hs, p, lo, up, draws):
 
 
 # ----------------------------------------------------------------------------- Ur5Sih (3 objects / clutter)
-def dr_sample_rows(p, env, episode):
-    """ha_task.h dr_sample for the listed envs: per-link / per-object mass scale U[lo, hi] and friction
-    friction x U[lo, hi] bucketed into dr_fric_buckets values (dr_utils.py:71-147 semantics), from the device-mode
-    counter hash (uniform01(seed, env, episode, 1000 + k)). float32, operation for operation."""
-    env = np.asarray(env, np.uint32)
-    episode = np.asarray(episode, np.uint32)
-    n = len(env)
-    rows = np.zeros((n, HM.DR_SIZE), F)
-    mlo, mhi, flo, fhi = F(p.dr_mass_lo), F(p.dr_mass_hi), F(p.dr_fric_lo), F(p.dr_fric_hi)
-    nb = int(p.dr_fric_buckets)
+def dr_pre(p, model, hs, mode=0, full=None):
+    """The DR launch that precedes a step / reset launch (ha_dr_global_kernel) and each env's dr_env_pre, on hs
+    (oracle/dr_oracle.py). full: the envs being reset (default: reset_buf). Returns the envs that sampled."""
+    if not p.dr_enable:
+        return None
+    N = hs.num_envs
+    full = (hs["reset_buf"] != 0) if full is None else np.asarray(full, bool)
+    DO.global_update(p, hs["dr_global"], bool(full.any()), mode)
+    pools = hs["object_indices"].reshape(N, -1)
+    all_ = hs["dr_global"].view(np.int32)[HM.DRG_ALL] != 0
+    smp = DO.env_pre(p, model, hs["dr_scale"], hs["randomize_buf"], hs["episode"], pools, full, hs["dr_global"],
+                     mode == 0)
+    if DO.active(p, HM.DRA_OBJ_SCALE, all_) and hs["contact_cache"] is not None and hs["contact_cache"].size:
+        hs["contact_cache"][smp, :, 3] = 0            # a rescaled object's persistent manifolds are void
+    return smp
 
-    def u(k, lo, hi):
-        return (lo + (hi - lo) * f32.uniform01(p.seed, env, episode, 1000 + k)).astype(F)
 
-    def bucket(v):
-        w = fhi - flo
-        i = np.floor((v - flo) / w * F(nb)).astype(np.int64)
-        i = np.clip(i, 0, nb - 1)
-        return (w * i.astype(F) / F(nb) + flo).astype(F)
-
-    fr = F(p.friction)
-    for L in range(HM.MAX_LINKS):
-        rows[:, HM.DR_LINK_MASS + L] = u(L, mlo, mhi)
-        rows[:, HM.DR_LINK_FRIC + L] = bucket(fr * u(100 + L, flo, fhi))
-    for o in range(HM.MAX_OBJ):
-        rows[:, HM.DR_OBJ_MASS + o] = u(50 + o, mlo, mhi)
-        rows[:, HM.DR_OBJ_FRIC + o] = bucket(fr * u(150 + o, flo, fhi))
-    return rows
+def noisy_actions(p, hs, raw):
+    """act_at's action noise (oracle/dr_oracle.py act_noise) on the raw actions of this step."""
+    return DO.act_noise(p, hs["dr_global"], raw) if p.dr_enable else np.asarray(raw, F)
 
 
 def ur5sih_step(orc, hs, p, model, draws):
@@ -135,15 +141,17 @@ def ur5sih_step(orc, hs, p, model, draws):
     A, B = model.n_actors, model.n_bodies
     a0 = model.actor_object0
     actors = np.arange(a0, a0 + NO)
+    dr_pre(p, model, hs)
+    raw = hs["actions"].copy()
+    hs["actions"][:] = noisy_actions(p, hs, raw)          # the controller reads them through act_at
     orc.controller(hs)
+    hs["actions"][:] = raw
     root = hs["root_state"].reshape(N, A, 13)
     dof = hs["dof_state"].reshape(N, D, 2)
     resets = np.nonzero(hs["reset_buf"])[0]
     if len(resets):
         cfgs = np.clip(draws[resets, 0].astype(np.int64), 0, int(p.num_initial_poses) - 1)
         tgts = np.clip(draws[resets, 1].astype(np.int64), 0, NO - 1)
-        if p.dr_enable:
-            hs["dr_scale"][resets] = dr_sample_rows(p, resets, hs["episode"][resets])
         for i, e in enumerate(resets):
             cfg = cfgs[i]
             pos0 = hs["object_pos_initial"][e, cfg]
@@ -185,12 +193,7 @@ def ur5sih_step(orc, hs, p, model, draws):
     teacher, _ = TO.observations(root, body, dof, hs["dof_position_targets"], hs["goal_pos"], hs["target_object_index"],
                                  bb(model.pool_bbox_pos), bb(model.pool_bbox_quat), bb(model.pool_bbox_ext),
                                  hs["obs_cache"], object_actors=actors)
-    obs = teacher.copy()
-    if p.dr_enable:
-        nctr = (hs["episode"].astype(np.uint32) << np.uint32(12)) ^ hs["progress_buf"].astype(np.uint32)
-        cols = np.arange(teacher.shape[1])
-        noise = f32.gauss01(p.seed, np.arange(N, dtype=np.uint32)[:, None], nctr[:, None], cols[None, :])
-        obs = (teacher + F(p.dr_obs_noise) * noise).astype(F)
+    obs = DO.obs_noise(p, hs["dr_global"], teacher) if p.dr_enable else teacher.copy()
     hs["obs_cache"][:] = root[:, actors, 0:7]
     prog = hs["progress_buf"] + 1
     hs["progress_buf"][:] = prog

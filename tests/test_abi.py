@@ -27,7 +27,7 @@ def test_struct_layouts_match(lib):
     a, b, c = C.c_int32(), C.c_int32(), C.c_int32()
     assert lib.ha_struct_sizes(C.byref(a), C.byref(b), C.byref(c)) == 0
     assert (a.value, b.value, c.value) == (C.sizeof(HM.HaModel), C.sizeof(HM.HaParams), C.sizeof(HM.HaState))
-    assert lib.ha_abi_version() == 15
+    assert lib.ha_abi_version() == 16
 
 
 def test_oracle_struct_layouts_match():

@@ -87,12 +87,31 @@ def near(a, b, atol, tag):
 
 
 # ----------------------------------------------------------------------------- AllegroKuka (C2)
-def _kuka_window(sub, n, scene_fn, act_fn, resets=True, force_prob=0.5, seed=11):
+def inject_resets(sim, hs, t, n):
+    """Env resets every step of a DR window (a quarter of the envs, rotating), on both sides: the re-randomization
+    gate (randomize_buf >= frequency at a reset) then fires inside the window."""
+    if t == 0:
+        return
+    r = np.where((np.arange(n) + t) % 4 == 0, 1, hs["reset_buf"]).astype(np.int64)
+    hs["reset_buf"][:] = r
+    put(sim, "reset_buf", r)
+
+
+def dr_exact(sim, hs, tag):
+    """The DR state bit for bit: the env rows, the per-env counters, the shard-wide state (ha_dr.h vs dr_oracle)."""
+    exact(sim, hs, ["dr_scale", "randomize_buf"], tag)
+    g, o = get(sim, "dr_global").view(np.int32), hs["dr_global"].view(np.int32)
+    assert (g == o).all(), f"{tag} dr_global differs at {np.nonzero(g != o)[0]}: {g[g != o]} vs {o[g != o]}"
+
+
+def _kuka_window(sub, n, scene_fn, act_fn, resets=True, force_prob=0.5, seed=11, cfg=None, dr_frame=None):
     """K fused ak_step_kernel launches against kuka_oracle.pre -> physics_oracle -> kuka_oracle.post from the same
-    host state (scene_fn(sim, hs) fills it); returns the sim, the host state and the number of random forces fired."""
+    host state (scene_fn(sim, hs) fills it); returns the sim, the host state and the number of random forces fired.
+    cfg: extra task config (DR schema, privileged actions); dr_frame: the gym frame count the DR window starts at."""
     from handarm_hip.sim import HandArmSim
     from oracle.oracle_lib import HostState, Oracle
-    sim = HandArmSim(n, "cuda:0", task_cfg={"task": HM.TASK_ALLEGRO_KUKA, "subtask": sub}, task=HM.TASK_ALLEGRO_KUKA)
+    sim = HandArmSim(n, "cuda:0", task_cfg={"task": HM.TASK_ALLEGRO_KUKA, "subtask": sub, **(cfg or {})},
+                     task=HM.TASK_ALLEGRO_KUKA)
     p, m = sim.params, sim.model
     lo = np.array(m.dof_lower[:23], np.float32)
     up = np.array(m.dof_upper[:23], np.float32)
@@ -107,6 +126,8 @@ def _kuka_window(sub, n, scene_fn, act_fn, resets=True, force_prob=0.5, seed=11)
     hs["progress_buf"][:] = rng.integers(1, 50, n)
     hs["task_state"][:, HM.AK_FORCE_PROB] = force_prob
     hs["contact_stats"][:] = 0
+    if dr_frame is not None:
+        hs["dr_global"].view(np.int32)[HM.DRG_FRAME_NEXT] = dr_frame
     scalars = hs["task_scalars"].copy()
     push_all(sim, hs)
     orc = Oracle(m, p, n)
@@ -133,11 +154,15 @@ def _kuka_window(sub, n, scene_fn, act_fn, resets=True, force_prob=0.5, seed=11)
         hs["reset_draws"][:] = draws
         put(sim, "actions", act)
         put(sim, "reset_draws", draws)
+        if p.dr_enable:
+            inject_resets(sim, hs, t, n)
         if p.ak_force_scale > 0:
             fired += int((draws[:, ds["FORCE_U"]] < hs["task_state"][:, HM.AK_FORCE_PROB]).sum())
         sim.task_step(HM.FLAG_REPLAY_DRAWS)
         obs, rew, timeout = step_chains.kuka_step(orc, hs, p, lo, up, scalars, draws)
         tag = f"kuka {sub} step {t}"
+        if p.dr_enable:
+            dr_exact(sim, hs, tag)
         scenes.assert_physics_bit_identical(sim, hs, n, tag=tag)
         exact(sim, hs, ["dof_position_targets", "sim_targets", "goal_state", "reset_buf", "reset_goal_buf",
                         "progress_buf", "successes"], tag)
@@ -244,10 +269,10 @@ def test_kuka_fused_step_closed_hand_overflows_chunk0_and_matches_oracle_chain()
 
 
 # ----------------------------------------------------------------------------- AllegroHand (C3)
-def _allegro_window(n, seed, act_fn, resets=True, force_scale=0.0):
+def _allegro_window(n, seed, act_fn, resets=True, force_scale=0.0, cfg=None):
     from handarm_hip.sim import HandArmSim
     from oracle.oracle_lib import HostState, Oracle
-    sim = HandArmSim(n, "cuda:0", task_cfg={"task": HM.TASK_ALLEGRO_HAND, "force_scale": force_scale},
+    sim = HandArmSim(n, "cuda:0", task_cfg={"task": HM.TASK_ALLEGRO_HAND, "force_scale": force_scale, **(cfg or {})},
                      task=HM.TASK_ALLEGRO_HAND)
     p, m = sim.params, sim.model
     lo = np.array(m.dof_lower[:16], np.float32)
@@ -269,9 +294,13 @@ def _allegro_window(n, seed, act_fn, resets=True, force_scale=0.0):
         hs["actions"][:] = act
         put(sim, "actions", act)
         put(sim, "reset_draws", draws)
+        if p.dr_enable:
+            inject_resets(sim, hs, t, n)
         sim.task_step(HM.FLAG_REPLAY_DRAWS)
         obs, rew, timeout, cons = step_chains.allegro_step(orc, hs, p, lo, up, draws)
         tag = f"allegro step {t}"
+        if p.dr_enable:
+            dr_exact(sim, hs, tag)
         scenes.assert_physics_bit_identical(sim, hs, n, tag=tag)
         exact(sim, hs, ["dof_position_targets", "sim_targets", "goal_state", "reset_buf", "reset_goal_buf",
                         "progress_buf", "successes"], tag)

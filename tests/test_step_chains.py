@@ -90,7 +90,6 @@ def test_ur5sih_chain_step_runs_with_resets(bin_scene):
         scenes.fill_bin_scene(hs, n, scene, seed=3)
     else:
         scenes.fill_scene(hs, n, seed=3, near_hand=0.0)
-        hs["dr_scale"][:] = step_chains.dr_sample_rows(p, np.arange(n), np.zeros(n))
     NO, a0 = int(p.n_objects), m.actor_object0
     root = hs["root_state"].reshape(n, m.n_actors, 13)
     hs["object_pos_initial"][:, 0] = root[:, a0:a0 + NO, 0:3]
