@@ -114,10 +114,18 @@ extern "C" {
 #define HA_DR_SCHED_CONSTANT 2 /* 0 before schedule_steps frames, 1 after */
 typedef struct ha_dr_attr_t {
     int32_t dist, op, sched, sched_steps;
-    float range[2];            /* uniform / loguniform: lo, hi; gaussian: mu, sigma (np.random.normal(mu, var)) */
-    float range_corr[2];       /* observations / actions: range_correlated (default 0, 0) */
+    double range[2];           /* uniform / loguniform: lo, hi; gaussian: mu, sigma (np.random.normal(mu, var));
+                                * python doubles, as the reference computes the schedules and samples in double */
+    double range_corr[2];      /* observations / actions: range_correlated (default 0, 0) */
     int32_t num_buckets;       /* > 0: the value snaps to the bucket grid over `range` (get_bucketed_val) */
     int32_t setup_only;        /* sampled at the first randomization only */
+    /* robot list properties (link mass / friction) when the object actor randomizes the same property after the robot:
+     * apply_randomizations keeps ONE original_props entry per property name, written by every actor at the first
+     * randomization (the object, processed last, wins; vec_task.py:828-832), so later randomizations zip the robot's
+     * bodies with the object's one: only the first later_elems elements are re-sampled, from the object's nominal
+     * value (later_og_object). later_elems -1: every element, from its own nominal value */
+    int32_t later_elems;
+    int32_t later_og_object;
 } ha_dr_attr_t;
 
 /* v16: the shard-wide randomization state (ha_state_t.dr_global, HA_DRG_SIZE floats; int fields as int32 bits), kept
@@ -138,6 +146,9 @@ typedef struct ha_dr_attr_t {
 #define HA_DRG_ACT_EPOCH 20    /* int: epoch of that action noise's correlated term */
 #define HA_DRG_ACT_ON 21       /* int: this step's actions get noise */
 #define HA_DRG_GRAVITY 24      /* [3] sim_params gravity (current) */
+#define HA_DRG_GRAVITY_OG 27   /* [3] the gravity the samples apply to: the first randomization's result after it (the
+                                * reference's original_props["sim_params"] holds the prop whose gravity that call
+                                * rewrote in place, vec_task.py:760-766, dr_utils.py:163-173) */
 #define HA_DRG_SIZE 32
 
 /* tasks (ha_params_t.task) */

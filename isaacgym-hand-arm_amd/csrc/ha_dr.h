@@ -61,8 +61,8 @@ HD double dr_sched(const ha_dr_attr_t& a, int frame) {
     return 1.0;
 }
 
-// the scheduled range (dr_utils.py:98-130): gaussian (mu, var), else (lo, hi); python double, rounded once
-HD void dr_range(const ha_dr_attr_t& a, int frame, float& r0, float& r1) {
+// the scheduled range (dr_utils.py:98-130): gaussian (mu, var), else (lo, hi), in python double
+HD void dr_range(const ha_dr_attr_t& a, int frame, double& r0, double& r1) {
     double s = dr_sched(a, frame), lo = a.range[0], hi = a.range[1];
     if (a.dist == HA_DR_DIST_GAUSSIAN) {
         if (a.op == HA_DR_OP_ADDITIVE) { lo *= s; hi *= s; }
@@ -71,49 +71,51 @@ HD void dr_range(const ha_dr_attr_t& a, int frame, float& r0, float& r1) {
         if (a.op == HA_DR_OP_ADDITIVE) { lo *= s; hi *= s; }
         else { lo = lo * s + 1.0 * (1.0 - s); hi = hi * s + 1.0 * (1.0 - s); }
     }
-    r0 = (float)lo;
-    r1 = (float)hi;
+    r0 = lo;
+    r1 = hi;
 }
 
 // get_bucketed_val (dr_utils.py:135-145): the bucket grid over the unscheduled range (2 sqrt(var) around mu for a
-// non-uniform distribution); bisect(buckets, v) - 1, so a value below the grid takes the LAST bucket (index -1)
-HD float dr_bucket(float v, const ha_dr_attr_t& a) {
-    float lo, hi;
+// non-uniform distribution), in python double; bisect(buckets, v) - 1, so a value below the grid takes the LAST
+// bucket (index -1)
+HD double dr_bucket(double v, const ha_dr_attr_t& a) {
+    double lo, hi;
     if (a.dist == HA_DR_DIST_UNIFORM) {
         lo = a.range[0];
         hi = a.range[1];
     } else {
-        float sd = sqrtf(a.range[1]);
-        lo = a.range[0] - 2.0f * sd;
-        hi = a.range[0] + 2.0f * sd;
+        double sd = sqrt(a.range[1]);
+        lo = a.range[0] - 2.0 * sd;
+        hi = a.range[0] + 2.0 * sd;
     }
     int nb = a.num_buckets;
-    float w = hi - lo;
-    float t = floorf((v - lo) / w * (float)nb);
-    int i = !(t >= 0.0f) ? nb - 1 : (t > (float)(nb - 1) ? nb - 1 : (int)t);
-    return w * (float)i / (float)nb + lo;
+    double w = hi - lo;
+    double t = floor((v - lo) / w * (double)nb);
+    int i = !(t >= 0.0) ? nb - 1 : (t > (double)(nb - 1) ? nb - 1 : (int)t);
+    return w * (double)i / (double)nb + lo;
 }
 
-// one sample (generate_random_samples) applied to the nominal value og (apply_random_samples, dr_utils.py:186-208)
-HD float dr_value(const ha_dr_attr_t& a, float r0, float r1, float og, float u, float g) {
-    float smp;
+// one sample (generate_random_samples) applied to the nominal value og (apply_random_samples, dr_utils.py:186-208),
+// in python double like the reference (the draw u / g is a float32 value), rounded once to the float32 property
+HD float dr_value(const ha_dr_attr_t& a, double r0, double r1, float og, float u, float g) {
+    double smp;
     if (a.dist == HA_DR_DIST_GAUSSIAN) {
-        smp = r0 + r1 * g;                                      // np.random.normal(mu, var): var is the std
+        smp = r0 + r1 * (double)g;                              // np.random.normal(mu, var): var is the std
     } else if (a.dist == HA_DR_DIST_LOGUNIFORM) {
-        float l0 = ha_logf(r0), l1 = ha_logf(r1);
-        smp = ha_expf(l0 + (l1 - l0) * u);
+        float l0 = ha_logf((float)r0), l1 = ha_logf((float)r1);     // the shared float32 log / exp (oracle: f32.py)
+        smp = (double)ha_expf(l0 + (l1 - l0) * u);
     } else {
-        smp = r0 + (r1 - r0) * u;
+        smp = r0 + (r1 - r0) * (double)u;
     }
-    float v = a.op == HA_DR_OP_SCALING ? og * smp : og + smp;
+    double v = a.op == HA_DR_OP_SCALING ? (double)og * smp : (double)og + smp;
     if (a.num_buckets > 0) v = dr_bucket(v, a);
-    return v;
+    return (float)v;
 }
 
 // one randomized quantity of this env, element k (lane-parallel callers): the dr_scale entry it leaves
 HD float dr_attr_sample(const ha_params_t& p, int attr, int env, uint32_t ep, int k, int frame, float og) {
     const ha_dr_attr_t& a = p.dr_attr[attr];
-    float r0, r1;
+    double r0, r1;
     dr_range(a, frame, r0, r1);
     uint32_t key = 64u * (uint32_t)attr + (uint32_t)k;
     float u = 0.0f, g = 0.0f;
@@ -121,15 +123,22 @@ HD float dr_attr_sample(const ha_params_t& p, int attr, int env, uint32_t ep, in
     else u = uniform01(p.seed ^ DR_SALT_ENV, env, ep, key);
     return dr_value(a, r0, r1, og, u, g);
 }
-// mass attributes keep the ratio new / nominal mass (inertia scales with it: recomputeInertia, dr_utils.py:63-64)
-HD float dr_mass_ratio(const ha_params_t& p, int attr, int env, uint32_t ep, int k, int frame, float og) {
+// mass attributes keep the ratio new / nominal mass (inertia scales with it: recomputeInertia, dr_utils.py:63-64);
+// og: the value the reference's sample multiplies (its original_props entry), own: the body's nominal mass
+HD float dr_mass_ratio(const ha_params_t& p, int attr, int env, uint32_t ep, int k, int frame, float og, float own) {
     const ha_dr_attr_t& a = p.dr_attr[attr];
-    if (a.op == HA_DR_OP_SCALING && a.num_buckets == 0) return dr_attr_sample(p, attr, env, ep, k, frame, 1.0f);
-    return dr_attr_sample(p, attr, env, ep, k, frame, og) / og;
+    if (a.op == HA_DR_OP_SCALING && a.num_buckets == 0 && og == own)
+        return dr_attr_sample(p, attr, env, ep, k, frame, 1.0f);
+    return dr_attr_sample(p, attr, env, ep, k, frame, og) / own;
 }
 HD bool dr_active(const ha_params_t& p, int attr, bool all) {
     const ha_dr_attr_t& a = p.dr_attr[attr];
     return a.dist != HA_DR_DIST_OFF && (all || !a.setup_only);
+}
+// element k of a robot list property is re-sampled in this randomization (ha_dr_attr_t.later_elems)
+HD bool dr_elem(const ha_params_t& p, int attr, bool all, int k) {
+    const ha_dr_attr_t& a = p.dr_attr[attr];
+    return dr_active(p, attr, all) && (all || a.later_elems < 0 || k < a.later_elems);
 }
 
 // object o's dimension scale in LDS: the env's object_scale row (AllegroKuka's cuboid dims) times the DR actor scale;
@@ -167,9 +176,13 @@ HD void dr_env_pre(SimCtx& c, const ha_state_t& st, int env, bool full, bool ste
     float* row = st.dr_scale + (size_t)env * HA_DR_SIZE;
     uint32_t ep = st.episode[env];
     if (lane < c.L) {
-        if (dr_active(p, HA_DRA_LINK_MASS, all))
-            row[HA_DR_LINK_MASS + lane] = dr_mass_ratio(p, HA_DRA_LINK_MASS, env, ep, lane, frame, m.link_mass[lane]);
-        if (dr_active(p, HA_DRA_LINK_FRIC, all))
+        // after the first randomization the robot's list properties may take the object's original value (later_og)
+        if (dr_elem(p, HA_DRA_LINK_MASS, all, lane)) {
+            float own = m.link_mass[lane];
+            float og = (!all && p.dr_attr[HA_DRA_LINK_MASS].later_og_object) ? m.pool_mass[c.o[0].pool] : own;
+            row[HA_DR_LINK_MASS + lane] = dr_mass_ratio(p, HA_DRA_LINK_MASS, env, ep, lane, frame, og, own);
+        }
+        if (dr_elem(p, HA_DRA_LINK_FRIC, all, lane))
             row[HA_DR_LINK_FRIC + lane] = dr_attr_sample(p, HA_DRA_LINK_FRIC, env, ep, lane, frame, p.friction);
     }
     if (lane < c.D) {
@@ -186,7 +199,8 @@ HD void dr_env_pre(SimCtx& c, const ha_state_t& st, int env, bool full, bool ste
     if (lane < c.NO) {
         int o = lane;
         if (dr_active(p, HA_DRA_OBJ_MASS, all))
-            row[HA_DR_OBJ_MASS + o] = dr_mass_ratio(p, HA_DRA_OBJ_MASS, env, ep, o, frame, m.pool_mass[c.o[o].pool]);
+            row[HA_DR_OBJ_MASS + o] = dr_mass_ratio(p, HA_DRA_OBJ_MASS, env, ep, o, frame, m.pool_mass[c.o[o].pool],
+                                                    m.pool_mass[c.o[o].pool]);
         if (dr_active(p, HA_DRA_OBJ_FRIC, all))
             row[HA_DR_OBJ_FRIC + o] = dr_attr_sample(p, HA_DRA_OBJ_FRIC, env, ep, o, frame, p.friction);
         if (rescale) {
@@ -293,14 +307,18 @@ HD void dr_global_update(const ha_params_t& p, float* g, int any, int mode) {
         dr_noise_params(p.dr_attr[HA_DRA_ACT], frame, g + HA_DRG_ACT);
         const ha_dr_attr_t& a = p.dr_attr[HA_DRA_GRAVITY];
         if (a.dist != HA_DR_DIST_OFF) {
-            // gravity = original + sample per axis (dr_utils.py:163-173), from the original sim params
-            float r0, r1;
+            // gravity = original op sample per axis (dr_utils.py:163-173). The reference's original gravity is the
+            // first randomization's prop, rewritten in place by that call: later samples apply to its result
+            double r0, r1;
             dr_range(a, frame, r0, r1);
             for (int k = 0; k < 3; k++) {
                 float u = 0.0f, gg = 0.0f;
                 if (a.dist == HA_DR_DIST_GAUSSIAN) gg = dr_gauss(p.seed ^ DR_SALT_GRAV, 0, (uint32_t)epoch, k);
                 else u = uniform01(p.seed ^ DR_SALT_GRAV, 0, (uint32_t)epoch, k);
-                g[HA_DRG_GRAVITY + k] = dr_value(a, r0, r1, p.gravity[k], u, gg);
+                float og = all ? p.gravity[k] : g[HA_DRG_GRAVITY_OG + k];
+                float v = dr_value(a, r0, r1, og, u, gg);
+                g[HA_DRG_GRAVITY + k] = v;
+                if (all) g[HA_DRG_GRAVITY_OG + k] = v;
             }
         }
     }

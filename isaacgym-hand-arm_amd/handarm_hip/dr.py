@@ -18,7 +18,9 @@ What is built, per key of the schema (anything else raises NotImplementedError):
   ``dof_properties`` damping / stiffness / lower / upper (per DOF), ``rigid_body_properties`` mass (per link; inertia
   scales with it) and ``rigid_shape_properties`` friction (per link: a link's shapes share one draw, PhysX's average
   combine with the other body); the ``object`` actor with ``scale``, mass and friction; ``color`` is accepted and
-  ignored (no renderer). ``num_buckets`` snaps a value to get_bucketed_val's grid. ``setup_only``: sampled at the
+  ignored (no renderer). ``num_buckets`` snaps a value to get_bucketed_val's grid. One original value per property
+  name (vec_task.py:828-832): with the object after the robot, later randomizations re-sample only the robot's first
+  link, from the object's value (ha_dr_attr_t.later_elems / later_og_object). ``setup_only``: sampled at the
   first randomization only; a property group with one setup_only attribute is not re-applied after it
   (``set_random_properties = False``, vec_task.py:843-864). AllegroKuka runs its first apply_randomizations from
   reset_idx after the sim is initialised (vec_task.py:286-289, allegro_kuka_base.py:1248), so its setup_only
@@ -165,6 +167,7 @@ def _attr(spec, where, noise=False, setup_only=False):
         a.range_corr[0], a.range_corr[1] = float(c0), float(c1)
     a.num_buckets = int(spec.get("num_buckets", 0) or 0)
     a.setup_only = int(bool(spec.get("setup_only", False)) or setup_only)
+    a.later_elems = -1
     return a
 
 
@@ -188,6 +191,7 @@ def parse(rp, task):
             raise NotImplementedError(f"randomization_params sim_params.{attr} is not implemented (gravity is)")
         attrs[HM.DRA_GRAVITY] = _attr(spec, "sim_params.gravity")
     actors = ACTORS[task]
+    order = []                                   # (actor kind, property) in the schema's order
     for actor, props in (rp.pop("actor_params", None) or {}).items():
         if actor not in actors:
             raise NotImplementedError(f"randomization_params actor_params.{actor}: the {sorted(actors)} actors are "
@@ -203,8 +207,9 @@ def parse(rp, task):
                                               f"implemented")
                 attrs[HM.DRA_OBJ_SCALE] = _attr(pattrs, where)
                 continue
-            if not isinstance(pattrs, dict):
-                raise NotImplementedError(f"randomization_params {where}: expected a mapping")
+            if not isinstance(pattrs, dict) or not any(k[:2] == (kind, prop) for k in PROPS):
+                raise NotImplementedError(f"randomization_params {where} is not implemented")
+            order.append((kind, prop))
             # one setup_only attribute keeps the whole property from being set again (vec_task.py:843-864)
             group_setup = any(isinstance(v, dict) and v.get("setup_only", False) for v in pattrs.values())
             for attr, spec in pattrs.items():
@@ -214,6 +219,21 @@ def parse(rp, task):
                 attrs[idx] = _attr(spec, f"{where}.{attr}", setup_only=group_setup)
     if rp:
         raise NotImplementedError(f"randomization_params keys {sorted(rp)} are not implemented")
+    # apply_randomizations keeps one original_props entry per property NAME, written by every actor at the first
+    # randomization (vec_task.py:828-832): the actor processed last wins, and later randomizations zip the other
+    # actor's bodies / shapes with that one entry. With the robot first and the object (one body, one shape in the
+    # Allegro scenes) last, later randomizations re-sample only the robot's first link, from the object's nominal value
+    for prop, idx in (("rigid_body_properties", HM.DRA_LINK_MASS), ("rigid_shape_properties", HM.DRA_LINK_FRIC)):
+        kinds = [k for k, pr in order if pr == prop]
+        if idx in attrs:
+            attrs[idx].later_elems = -1
+        if "robot" in kinds and "object" in kinds:
+            if kinds.index("object") < kinds.index("robot"):
+                raise NotImplementedError(f"randomization_params: the object's {prop} before the robot's (its shared "
+                                          f"original_props entry would be the robot's) is not implemented")
+            if idx in attrs:
+                attrs[idx].later_elems = 1
+                attrs[idx].later_og_object = 1
     if task == HM.TASK_ALLEGRO_KUKA:
         # the first apply_randomizations runs from reset_idx, after sim_initialized: setup_only never applies
         attrs = {k: a for k, a in attrs.items() if not a.setup_only}
@@ -225,7 +245,9 @@ def apply_schema(p, rp, task):
     frequency, attrs = parse(rp, task)
     p.dr_frequency = frequency
     for k in range(HM.DRA_N):
-        p.dr_attr[k] = attrs.get(k, HM.HaDrAttr())
+        off = HM.HaDrAttr()
+        off.later_elems = -1
+        p.dr_attr[k] = attrs.get(k, off)
 
 
 def default_rows(model, params, num_envs, object_mass=None):
@@ -251,6 +273,7 @@ def init_global(params):
     gi[HM.DRG_LAST_RAND] = -1
     gi[HM.DRG_FIRST] = 1
     g[HM.DRG_GRAVITY:HM.DRG_GRAVITY + 3] = list(params.gravity)
+    g[HM.DRG_GRAVITY_OG:HM.DRG_GRAVITY_OG + 3] = list(params.gravity)
     return g
 
 

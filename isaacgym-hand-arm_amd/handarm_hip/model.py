@@ -41,7 +41,7 @@ DR_DIST = {"off": 0, "uniform": 1, "loguniform": 2, "gaussian": 3}
 DR_OP = {"additive": 0, "scaling": 1}
 DR_SCHED = {None: 0, "linear": 1, "constant": 2}
 DRG_FRAME, DRG_FRAME_NEXT, DRG_LAST_RAND, DRG_FIRST, DRG_ALL, DRG_STEP, DRG_EPOCH, DRG_VALID = range(8)
-DRG_OBS, DRG_ACT, DRG_ACT_USE, DRG_ACT_EPOCH, DRG_ACT_ON, DRG_GRAVITY = 8, 12, 16, 20, 21, 24
+DRG_OBS, DRG_ACT, DRG_ACT_USE, DRG_ACT_EPOCH, DRG_ACT_ON, DRG_GRAVITY, DRG_GRAVITY_OG = 8, 12, 16, 20, 21, 24, 27
 DRG_SIZE = 32
 TASK_UR5SIH, TASK_ALLEGRO_HAND, TASK_ALLEGRO_KUKA = 0, 1, 2
 # AllegroKuka task_state row (HA_AK_* in handarm_abi.h)
@@ -63,8 +63,9 @@ f32, i32 = C.c_float, C.c_int32
 
 class HaDrAttr(C.Structure):
     """ha_dr_attr_t (include/handarm_abi.h v16): one randomized quantity of task.randomization_params."""
-    _fields_ = [("dist", i32), ("op", i32), ("sched", i32), ("sched_steps", i32), ("range", f32 * 2),
-                ("range_corr", f32 * 2), ("num_buckets", i32), ("setup_only", i32)]
+    _fields_ = [("dist", i32), ("op", i32), ("sched", i32), ("sched_steps", i32), ("range", C.c_double * 2),
+                ("range_corr", C.c_double * 2), ("num_buckets", i32), ("setup_only", i32), ("later_elems", i32),
+                ("later_og_object", i32)]
 
 
 def arr(t, *dims):

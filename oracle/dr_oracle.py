@@ -51,7 +51,7 @@ def sched(a, frame):
 
 
 def scheduled_range(a, frame):
-    """dr_range (dr_utils.py:98-130): (mu, var) for gaussian, else (lo, hi), python double, rounded once."""
+    """dr_range (dr_utils.py:98-130): (mu, var) for gaussian, else (lo, hi), in python double."""
     s = sched(a, frame)
     lo, hi = float(a.range[0]), float(a.range[1])
     if a.dist == DIST_GAUSSIAN:
@@ -68,40 +68,41 @@ def scheduled_range(a, frame):
         else:
             lo = lo * s + 1.0 * (1.0 - s)
             hi = hi * s + 1.0 * (1.0 - s)
-    return F(lo), F(hi)
+    return lo, hi
 
 
 def bucket(v, a):
-    """dr_bucket (get_bucketed_val, dr_utils.py:135-145): below the grid takes the last bucket (bisect - 1 = -1)."""
-    v = np.asarray(v, F)
+    """dr_bucket (get_bucketed_val, dr_utils.py:135-145), in double: below the grid takes the last bucket
+    (bisect - 1 = -1)."""
+    v = np.asarray(v, np.float64)
     if a.dist == DIST_UNIFORM:
-        lo, hi = F(a.range[0]), F(a.range[1])
+        lo, hi = float(a.range[0]), float(a.range[1])
     else:
-        sd = np.sqrt(F(a.range[1]))
-        lo, hi = F(a.range[0]) - F(2.0) * sd, F(a.range[0]) + F(2.0) * sd
+        sd = np.sqrt(float(a.range[1]))
+        lo, hi = float(a.range[0]) - 2.0 * sd, float(a.range[0]) + 2.0 * sd
     nb = int(a.num_buckets)
-    w = F(hi - lo)
+    w = hi - lo
     with np.errstate(invalid="ignore"):
-        t = np.floor(((v - lo) / w) * F(nb)).astype(F)
-    i = np.where(~(t >= 0), nb - 1, np.where(t > F(nb - 1), nb - 1, np.nan_to_num(t, nan=0).astype(np.int64)))
-    return (((w * i.astype(F)) / F(nb)) + lo).astype(F)
+        t = np.floor((v - lo) / w * float(nb))
+    i = np.where(~(t >= 0), nb - 1, np.where(t > nb - 1, nb - 1, np.nan_to_num(t, nan=0).astype(np.int64)))
+    return w * i.astype(np.float64) / float(nb) + lo
 
 
 def value(a, r0, r1, og, u, g):
-    """dr_value: one sample applied to the nominal value og (float32)."""
-    og = np.asarray(og, F)
+    """dr_value: one sample applied to the nominal value og, in double (the draw u / g float32), rounded to float32;
+    loguniform through the shared float32 log / exp."""
+    og = np.asarray(og, F).astype(np.float64)
     if a.dist == DIST_GAUSSIAN:
-        smp = r0 + r1 * np.asarray(g, F)
+        smp = r0 + r1 * np.asarray(g, F).astype(np.float64)
     elif a.dist == DIST_LOGUNIFORM:
         l0, l1 = f32.logf(np.array([r0], F))[0], f32.logf(np.array([r1], F))[0]
-        smp = f32.expf(l0 + (l1 - l0) * np.asarray(u, F))
+        smp = f32.expf(l0 + (l1 - l0) * np.asarray(u, F)).astype(np.float64)
     else:
-        smp = r0 + (r1 - r0) * np.asarray(u, F)
-    smp = np.asarray(smp, F)
-    v = (og * smp if a.op == OP_SCALING else og + smp).astype(F)
+        smp = r0 + (r1 - r0) * np.asarray(u, F).astype(np.float64)
+    v = og * smp if a.op == OP_SCALING else og + smp
     if a.num_buckets > 0:
         v = bucket(v, a)
-    return v
+    return np.asarray(v).astype(F)
 
 
 def attr_sample(p, attr, env, ep, k, frame, og):
@@ -115,17 +116,30 @@ def attr_sample(p, attr, env, ep, k, frame, og):
     return value(a, r0, r1, og, f32.uniform01(seed, env, ep, key), 0)
 
 
-def mass_ratio(p, attr, env, ep, k, frame, og):
+def mass_ratio(p, attr, env, ep, k, frame, og, own=None):
+    """dr_mass_ratio: og the value the sample multiplies, own the body's nominal mass (default og)."""
     a = p.dr_attr[attr]
-    if a.op == OP_SCALING and a.num_buckets == 0:
-        return attr_sample(p, attr, env, ep, k, frame, F(1.0))
     og = np.asarray(og, F)
-    return (attr_sample(p, attr, env, ep, k, frame, og) / og).astype(F)
+    own = og if own is None else np.asarray(own, F)
+    general = (attr_sample(p, attr, env, ep, k, frame, og) / own).astype(F)
+    if not (a.op == OP_SCALING and a.num_buckets == 0):
+        return general
+    simple = attr_sample(p, attr, env, ep, k, frame, F(1.0))        # elementwise where og == own (the device's test)
+    same = np.broadcast_to(og == own, general.shape)
+    return np.where(same, np.broadcast_to(simple, general.shape), general).astype(F)
 
 
 def active(p, attr, all_):
     a = p.dr_attr[attr]
     return a.dist != DIST_OFF and (all_ or not a.setup_only)
+
+
+def elems(p, attr, all_, n):
+    """dr_elem: the elements of a robot list property re-sampled in this randomization."""
+    a = p.dr_attr[attr]
+    if not active(p, attr, all_):
+        return 0
+    return n if (all_ or a.later_elems < 0) else min(n, a.later_elems)
 
 
 def env_pre(p, model, rows, rb, episode, pools, reset, g, step):
@@ -148,11 +162,17 @@ def env_pre(p, model, rows, rb, episode, pools, reset, g, step):
     E, EP = envs[:, None], ep[:, None]
     L, D, NO = model.n_links, model.n_dofs, pools.shape[1]
     li, di, oi = np.arange(L, dtype=np.uint32)[None], np.arange(D, dtype=np.uint32)[None], np.arange(NO, dtype=np.uint32)[None]
-    if active(p, HM.DRA_LINK_MASS, all_):
-        rows[envs, HM.DR_LINK_MASS:HM.DR_LINK_MASS + L] = mass_ratio(p, HM.DRA_LINK_MASS, E, EP, li, frame,
-                                                                      np.array(list(model.link_mass)[:L], F)[None])
-    if active(p, HM.DRA_LINK_FRIC, all_):
-        rows[envs, HM.DR_LINK_FRIC:HM.DR_LINK_FRIC + L] = attr_sample(p, HM.DRA_LINK_FRIC, E, EP, li, frame, F(p.friction))
+    n = elems(p, HM.DRA_LINK_MASS, all_, L)
+    if n:
+        own = np.array(list(model.link_mass)[:n], F)[None]
+        og = own
+        if not all_ and p.dr_attr[HM.DRA_LINK_MASS].later_og_object:
+            og = np.array(list(model.pool_mass), F)[pools[envs, 0]][:, None]
+        rows[envs, HM.DR_LINK_MASS:HM.DR_LINK_MASS + n] = mass_ratio(p, HM.DRA_LINK_MASS, E, EP, li[:, :n], frame, og, own)
+    n = elems(p, HM.DRA_LINK_FRIC, all_, L)
+    if n:
+        rows[envs, HM.DR_LINK_FRIC:HM.DR_LINK_FRIC + n] = attr_sample(p, HM.DRA_LINK_FRIC, E, EP, li[:, :n], frame,
+                                                                       F(p.friction))
     for attr, slot, name in ((HM.DRA_DOF_KD, HM.DR_DOF_KD, "dof_kd"), (HM.DRA_DOF_KP, HM.DR_DOF_KP, "dof_kp"),
                              (HM.DRA_DOF_LOWER, HM.DR_DOF_LOWER, "dof_lower"),
                              (HM.DRA_DOF_UPPER, HM.DR_DOF_UPPER, "dof_upper")):
@@ -220,7 +240,10 @@ def global_update(p, g, any_reset, mode):
             k = np.arange(3, dtype=np.uint32)
             gg = gauss(seed, np.uint32(0), np.uint32(epoch), k) if a.dist == DIST_GAUSSIAN else np.zeros(3, F)
             u = f32.uniform01(seed, np.uint32(0), np.uint32(epoch), k) if a.dist != DIST_GAUSSIAN else np.zeros(3, F)
-            g[HM.DRG_GRAVITY:HM.DRG_GRAVITY + 3] = value(a, r0, r1, np.array(list(p.gravity), F), u, gg)
+            og = np.array(list(p.gravity), F) if all_ else g[HM.DRG_GRAVITY_OG:HM.DRG_GRAVITY_OG + 3].copy()
+            g[HM.DRG_GRAVITY:HM.DRG_GRAVITY + 3] = value(a, r0, r1, og, u, gg)
+            if all_:
+                g[HM.DRG_GRAVITY_OG:HM.DRG_GRAVITY_OG + 3] = g[HM.DRG_GRAVITY:HM.DRG_GRAVITY + 3]
     frames = p.control_freq_inv if mode == 0 else 0
     if p.task == HM.TASK_UR5SIH and any_reset:
         frames += 1

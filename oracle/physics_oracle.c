@@ -1535,3 +1535,10 @@ void hao_controller(hao_handle h, ha_state_t* S, int env) {
 void hao_sincos(const float* x, int n, float* s, float* c) {
     for (int i = 0; i < n; i++) ha_sincosf(x[i], &s[i], &c[i]);
 }
+/* test helper: ha_logf(x) and ha_expf(1e-3 x - 3) (the DR samplers' shared log / exp, include/ha_fmath.h) */
+void hao_logexp(const float* x, int n, float* lo, float* ex) {
+    for (int i = 0; i < n; i++) {
+        lo[i] = ha_logf(x[i]);
+        ex[i] = ha_expf(x[i] * 1e-3f - 3.0f);
+    }
+}
