@@ -20,8 +20,8 @@ cfg/task/env/<subtask>.yaml, read here with yaml.safe_load):
     (torch_rand_float, torch.rand, torch.randn) is recorded per env in the slot the device replays
     (ak_task.h AK_DRAW_*).
 ``gym.simulate`` is not run: between pre- and post-physics the rigid-body tensor is refreshed from the dof
-state by the build's own forward kinematics (the C oracle with zero substeps), which is what the device's
-no-physics step does too; these goldens pin the task math, not the physics.
+state by an independent float64 forward kinematics (tests/kinematics.py, not the FK the kernel and the C oracle
+share), which is what the device's no-physics step computes too; these goldens pin the task math and the FK.
 """
 import json
 import os
@@ -41,6 +41,7 @@ sys.path.insert(0, os.path.join(ROOT, "isaacgym-hand-arm_amd"))
 import refload  # noqa: E402
 
 from handarm_hip import model as HM  # noqa: E402
+from tests.kinematics import Chain  # noqa: E402
 
 REF_CFG = "/root/reference/isaacgymenvs/cfg/task"
 SCENE = HM.KUKA_ASSET
@@ -292,13 +293,21 @@ def obs_reward(sub, N=48, steps=4, seed=1):
     np.savez_compressed(os.path.join(HERE, f"kuka_obs_reward_{sub}.npz"), **res)
 
 
-def refresh_bodies(t, orc, st):
-    """Rigid-body tensor from the dof / root state by the build's FK (oracle simulate with 0 calls)."""
+def refresh_bodies(t, chain, model):
+    """Rigid-body tensor from the dof / root state: the robot's rows by the INDEPENDENT float64 forward kinematics of
+    tests/kinematics.py (not the C oracle's FK, which the kernel shares), rounded to float32; the object, table and
+    goal rows are their actors' root states, as refresh_rigid_body_state_tensor gives them."""
     N = t.num_environments
-    st["dof_state"][:] = t.dof_state.numpy()
-    st["root_state"][:] = t.root_state_tensor.numpy()
-    orc.simulate(st, 0)
-    t.rigid_body_states[:] = torch.from_numpy(st["rigid_body_state"].reshape(N, NB, 13))
+    D, A, L = model.n_dofs, model.n_actors, model.n_links
+    dof = t.dof_state.numpy().reshape(N, D, 2)
+    root = t.root_state_tensor.numpy().reshape(N, A, 13)
+    rb = np.zeros((N, NB, 13), np.float32)
+    for e in range(N):
+        rb[e, model.body_robot0:model.body_robot0 + L] = chain.body_states(dof[e, :, 0], dof[e, :, 1])
+    rb[:, model.body_object0] = root[:, model.actor_object0]
+    rb[:, model.body_table] = root[:, model.actor_table]
+    rb[:, model.body_goal] = root[:, model.actor_goal]
+    t.rigid_body_states[:] = torch.from_numpy(rb)
 
 
 def steps(sub, N=32, T=8, seed=2):
@@ -313,6 +322,7 @@ def steps(sub, N=32, T=8, seed=2):
     st["object_scale"][:] = t.object_scales.numpy()[:, None, :]
     st["collision_enabled"][:] = 1
     orc = Oracle(model, params, N)
+    chain = Chain(HM.load_scene(SCENE))
     g = torch.Generator().manual_seed(seed)
     draws = np.zeros((T, N, HM.DRAW_STRIDE), np.float32)
     cur = {"step": 0, "ids": None, "phase": "pre", "in_target": False, "in_reset": False, "u": None}
@@ -423,7 +433,7 @@ def steps(sub, N=32, T=8, seed=2):
             rec("task_state_in", pack_task_state(t))
             t.pre_physics_step(actions)
             cur["phase"] = "post"
-            refresh_bodies(t, orc, st)
+            refresh_bodies(t, chain, model)
             t.post_physics_step()
             t.timeout_buf = (t.progress_buf >= t.max_episode_length - 1) & (t.reset_buf != 0)   # vec_task.py:424
             for k, v in [("obs", t.obs_buf), ("rew", t.rew_buf), ("reset", t.reset_buf),
