@@ -331,21 +331,30 @@ def bytes_per_env_step(task, env, args):
     return algorithmic_bytes_per_env_step(dr=not args.no_dr)[0]          # ur5sih, ur5sih_wide
 
 
-def _profile_json(name, envs):
-    fn = os.path.join(ROOT, "profiles", name)
+# configs whose step kernel another config shares: their committed SQ / PMC summaries carry the config in the name
+# (profiles/sq_<kernel>_<key>.json), so C4w never borrows C4's (verdict r05 Weak #7)
+PROFILE_TAG = {"C4w": "C4w"}
+
+
+def _profile_json(name, envs, key=None):
+    """profiles/<name>[_<tag>].json of this config's workload (None when that workload has no committed summary)."""
+    tag = PROFILE_TAG.get(key)
+    fn = os.path.join(ROOT, "profiles", f"{name}_{tag}.json" if tag else f"{name}.json")
     if not os.path.exists(fn):
         return None
     with open(fn) as f:
         d = json.load(f)
-    return d if d.get("envs") == envs else None
+    if d.get("envs") != envs or (d.get("workload") not in (None, key)):
+        return None
+    return d
 
 
-def compute_roofline(kernel, envs, kavg_ms):
+def compute_roofline(kernel, envs, kavg_ms, key=None):
     """Second roofline: VALU issue. Wave-instructions per launch come from the committed
     rocprofv3 SQ pass of the same workload (profiles/sq_<kernel>.json, tools/sq_summary.py); the kernel time is
     this run's. Mean resident waves per SIMD = 4 x SQ_WAVE_CYCLES (quad-cycles) / (kernel cycles at the nominal
     2.4 GHz) / 1024 SIMDs."""
-    sq = _profile_json(f"sq_{kernel}.json", envs)
+    sq = _profile_json(f"sq_{kernel}", envs, key)
     if sq is None or not kavg_ms == kavg_ms:
         return None
     t = kavg_ms * 1e-3
@@ -354,10 +363,11 @@ def compute_roofline(kernel, envs, kavg_ms):
             "frac": rate / VALU_PEAK_WAVE_INSTS, "valu_insts_per_launch": sq["valu_insts_per_launch"],
             "waves_per_simd": 4 * sq["wave_cycles_per_launch"] / (t * NOMINAL_CLOCK_HZ) / 1024,
             "valu_active_frac": sq.get("valu_active_frac"),
-            "valu_lane_utilization": sq.get("valu_lane_utilization"), "source": f"profiles/sq_{kernel}.json"}
+            "valu_lane_utilization": sq.get("valu_lane_utilization"),
+            "source": "profiles/sq_{}{}.json".format(kernel, "_" + PROFILE_TAG[key] if key in PROFILE_TAG else "")}
 
 
-def run_config(task, envs, args, world, rank, device, log_interval_fn):
+def run_config(task, envs, args, world, rank, device, log_interval_fn, key=None):
     """Build the env, W warmup steps (the first includes the all-env reset and, for the HandArm tasks, drop
     init), then exactly K timed steps between barrier + synchronize pairs; returns the record (rank 0 gets the
     max over ranks)."""
@@ -419,7 +429,7 @@ def run_config(task, envs, args, world, rank, device, log_interval_fn):
     kavg = statistics.mean(kern_ms) if kern_ms else float("nan")
     bytes_env = bytes_per_env_step(task, env, args)
     achieved = bytes_env * envs / (kavg * 1e-3) / 1e9
-    tj = _profile_json(f"traffic_{kernel}.json", envs)
+    tj = _profile_json(f"traffic_{kernel}", envs, key)
     rec = {
         "value": world * envs * args.steps / elapsed, "unit": "env-steps/s",
         "ms_per_step": elapsed / args.steps * 1e3, "p50_ms_per_step": statistics.median(step_ms),
@@ -427,7 +437,7 @@ def run_config(task, envs, args, world, rank, device, log_interval_fn):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": tj.get("hbm_bytes_per_launch") if tj else None,
                      "kernel": kernel, "kernel_avg_ms": kavg, "algorithmic_bytes_per_env_step": bytes_env},
-        "compute_roofline": compute_roofline(kernel, envs, kavg),
+        "compute_roofline": compute_roofline(kernel, envs, kavg, key),
         **extra,
     }
     if pcs is not None:
@@ -594,7 +604,7 @@ def main():
         task, envs, _ = CONFIGS[key]
         if key == head and args.envs:
             envs = args.envs
-        records[key] = run_config(task, envs, args, world, rank, device, log_interval)
+        records[key] = run_config(task, envs, args, world, rank, device, log_interval, key)
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         for key in [head] + subs:
             task = CONFIGS[key][0]

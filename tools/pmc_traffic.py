@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--kernel", default="ha_step_kernel")
     ap.add_argument("--last", type=int, default=8)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--workload", default=None, help="bench config key when configs share the kernel (C4w)")
     a = ap.parse_args()
     fk = counter_values(a.fetch, "FETCH_SIZE", a.kernel)[-a.last:]
     wk = counter_values(a.write, "WRITE_SIZE", a.kernel)[-a.last:]
@@ -46,7 +47,7 @@ def main():
         raise SystemExit("no dispatches of the kernel found")
     fetch_kib, write_kib = statistics.mean(fk), statistics.mean(wk)
     hbm = (2.0 * fetch_kib + write_kib) * 1024.0
-    out = {"kernel": a.kernel, "envs": a.envs, "dispatches": [len(fk), len(wk)],
+    out = {"kernel": a.kernel, "envs": a.envs, "workload": a.workload, "dispatches": [len(fk), len(wk)],
            "fetch_size_kib_raw": fetch_kib, "write_size_kib_raw": write_kib,
            "hbm_bytes_per_launch": hbm, "hbm_bytes_per_env": hbm / a.envs,
            "correction": "read side x2 (gfx950 FETCH_SIZE half-count); width-uncalibrated estimate"}

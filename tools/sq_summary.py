@@ -29,9 +29,10 @@ def main():
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--envs", type=int, required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--workload", default=None, help="bench config key when configs share the kernel (C4w)")
     a = ap.parse_args()
     m = per_dispatch(a.csv, a.kernel)
-    out = {"kernel": a.kernel, "envs": a.envs, "counters_mean_per_launch": m,
+    out = {"kernel": a.kernel, "envs": a.envs, "workload": a.workload, "counters_mean_per_launch": m,
            "valu_insts_per_launch": m.get("SQ_INSTS_VALU"),
            "wave_cycles_per_launch": m.get("SQ_WAVE_CYCLES"),
            "valu_active_frac": (m["SQ_ACTIVE_INST_VALU"] / m["SQ_WAVE_CYCLES"])
