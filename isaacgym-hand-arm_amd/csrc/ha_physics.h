@@ -1616,6 +1616,122 @@ HD bool pair_desc(const SimCtx& c, int p, int& kind, int& A, int& B) {
     if (p < NLH * NS) { kind = 4; A = p / NS; B = p - A * NS; return true; }
     return false;
 }
+
+// ----------------------------------------------------------------------------- hierarchical broad phase (round 6)
+// Most of the enumeration above is link-hull pairs (C5: 176 object-link and 132 link-static of 392), and in a bin
+// scene nearly all of them fail the sphere / box tests. Before the 64-pair batches, detect() bounds the link hulls
+// in quads (hulls 4g .. 4g+3, one DPP quad of lanes): centre C_g = the mean of the quad's hull centres, radius R_g =
+// max_k (|c_k - C_g| + r_k). A pair (object o, hull k) passes the sphere test only if |c_o - c_k| <= r_o + r_k + mg,
+// and then |c_o - C_g| <= r_o + R_g + mg (triangle inequality); a link-static pair passes the box test only if the
+// box distance of c_k is <= r_k + mg, and the box distance is 1-Lipschitz, so that of C_g is <= R_g + mg. The quad
+// tests (with 0.1% + 1 mm of slack over float rounding) therefore reject only pairs the per-pair tests reject, and
+// the batches run over the pairs of the quads that pass, in the enumeration's order with their enumeration index
+// (record slots, face records): the contacts, their order and every record are those of the flat enumeration,
+// which the oracle keeps. om: bit o*G + g = object o near quad g; sm: bit g*NS + b = static b near quad g.
+HD int quad_hulls(uint32_t g, int G, int NLH) {
+    return 4 * __builtin_popcount(g) - (int)((g >> (G - 1)) & 1u) * (4 * G - NLH);
+}
+// the t-th hull of the quads set in g
+HD int quad_hull(uint32_t g, int t, int NLH) {
+    for (int q = 0; g; q++, g >>= 1) {
+        if (!(g & 1u)) continue;
+        int nh = min(4, NLH - 4 * q);
+        if (t < nh) return 4 * q + t;
+        t -= nh;
+    }
+    return -1;
+}
+// pair r of the culled enumeration: its kind / sides, and p = its index in the flat one (pair_desc)
+HD bool pair_compact(const SimCtx& c, int G, uint64_t om, uint64_t sm, int& p, int& kind, int& A, int& B) {
+    int NO = c.NO, NLH = c.m->n_link_hulls, NS = c.m->n_static;
+    int r = p, orig = 0;
+    uint32_t gm = (1u << G) - 1u;
+    for (int o = 0; o < NO; o++) {
+        int head = 1 + NS + (NO - 1 - o);
+        uint32_t g = (uint32_t)(om >> (o * G)) & gm;
+        int nl = quad_hulls(g, G, NLH);
+        if (r < head + nl) {
+            A = o;
+            if (r == 0) { kind = 0; B = -1; }
+            else if (r < 1 + NS) { kind = 1; B = r - 1; }
+            else if (r < head) { kind = 2; B = o + 1 + (r - 1 - NS); }
+            else { kind = 3; B = quad_hull(g, r - head, NLH); }
+            p = orig + (kind == 3 ? head + B : r);
+            return true;
+        }
+        r -= head + nl;
+        orig += head + NLH;
+    }
+    uint32_t bm = (1u << NS) - 1u;
+    for (int q = 0; q < G; q++) {
+        uint32_t s = (uint32_t)(sm >> (q * NS)) & bm;
+        int pc = __builtin_popcount(s), cnt = min(4, NLH - 4 * q) * pc;
+        if (r < cnt) {
+            int h = r / pc, k = r - h * pc;
+            for (; k > 0; k--) s &= s - 1u;
+            kind = 4; A = 4 * q + h; B = __builtin_ctz(s);
+            p = orig + A * NS + B;
+            return true;
+        }
+        r -= cnt;
+    }
+    return false;
+}
+// the quads' object / static masks and the culled pair count (G quads; G * NO <= 64, G * NS <= 64)
+HD void broad_quads(const SimCtx& c, int G, uint64_t& om, uint64_t& sm, int& neff) {
+    const EnvLDS& s = *c.s;
+    const ha_model_t& m = *c.m;
+    int lane = c.lane, NO = c.NO, NLH = m.n_link_hulls, NS = m.n_static;
+    float mg = c.p->contact_margin;
+    bool hv = lane < NLH;
+    f3 ch = mk3(0.0f, 0.0f, 0.0f);
+    float rk = 0.0f;
+    if (hv) {
+        int Lk = m.hull_link[lane];
+        ch = ld3(s.lp[Lk]) + qrot(ldq(s.lq[Lk]), ld3(m.hull_center[lane]));
+        rk = m.hull_radius[lane];
+    }
+    f3 C = ch;
+    C.x += dpp_f<0xB1>(C.x); C.y += dpp_f<0xB1>(C.y); C.z += dpp_f<0xB1>(C.z);
+    C.x += dpp_f<0x4E>(C.x); C.y += dpp_f<0x4E>(C.y); C.z += dpp_f<0x4E>(C.z);
+    C = C * (1.0f / (float)max(1, min(4, NLH - (lane & ~3))));
+    f3 dc = ch - C;
+    float d = hv ? sqrtf(dot3(dc, dc)) + rk : 0.0f;
+    d = fmaxf(d, dpp_f<0xB1>(d));
+    d = fmaxf(d, dpp_f<0x4E>(d));
+    float R = d * 1.001f + mg + 1.0e-3f;
+    // statics near each quad (every lane of a quad holds its sphere; lane 4g's bits are read)
+    uint32_t sb = 0;
+    for (int b = 0; b < NS; b++)
+        if (sphere_near_box(m.static_half[b], static_pose(c, b), C, R)) sb |= 1u << b;
+    // quads near each object (lane o; an object with collisions off has no candidate pairs)
+    f3 co = mk3(0.0f, 0.0f, 0.0f);
+    float ro = -1.0e30f;
+    if (lane < NO && c.o[lane].coll != 0) {
+        int pa = c.o[lane].pool;
+        PoseF Po = object_pose(c, lane);
+        co = Po.p + qrot(Po.q, scale3(c, lane, ld3(m.pool_center[pa])));
+        ro = scale_radius(c, lane, m.pool_radius[pa]);
+    }
+    uint32_t ob = 0;
+    sm = 0;
+    neff = 0;
+    for (int q = 0; q < G; q++) {
+        f3 Cq = mk3(bcast(C.x, 4 * q), bcast(C.y, 4 * q), bcast(C.z, 4 * q));
+        float rr = (ro + bcast(R, 4 * q)) * 1.0001f;
+        f3 dq = co - Cq;
+        if (ro > -1.0e29f && dot3(dq, dq) <= rr * rr) ob |= 1u << q;
+        uint32_t sq = (uint32_t)bcast_i((int)sb, 4 * q);
+        sm |= (uint64_t)sq << (q * NS);
+        neff += min(4, NLH - 4 * q) * __builtin_popcount(sq);
+    }
+    om = 0;
+    for (int o = 0; o < NO; o++) {
+        uint32_t g = (uint32_t)bcast_i((int)ob, o);
+        om |= (uint64_t)g << (o * G);
+        neff += 1 + NS + (NO - 1 - o) + quad_hulls(g, G, NLH);
+    }
+}
 // the two link hulls of self-collision pair k
 HD void self_pair_hulls(const ha_model_t& m, int k, int& ha, int& hb) {
     uint32_t sp = m.self_pair[k];
@@ -1830,9 +1946,25 @@ HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
         } else if (kind == 2) {
             int j1 = j / n2;
             h1 = ho + j1; P1 = Po; b1 = A; h2 = m.pool_hull[pb] + (j - j1 * n2); P2 = Pb; b2 = B; k2 = B;
+            // a compound pair's piece pair: the two pieces' own spheres first (round 6; PhysX's broad phase sees each
+            // convex shape of an actor on its own). One-hull objects: their piece sphere is the broad phase's sphere
+            if (m.pool_nhull[pa] * n2 > 1) {
+                f3 c1 = Po.p + qrot(Po.q, scale3(c, A, ld3(m.hull_center[h1])));
+                f3 c2 = Pb.p + qrot(Pb.q, scale3(c, B, ld3(m.hull_center[h2])));
+                float rr = scale_radius(c, A, m.hull_radius[h1]) + scale_radius(c, B, m.hull_radius[h2]) + c.p->contact_margin;
+                f3 dc = c1 - c2;
+                if (!(dot3(dc, dc) <= rr * rr)) return;
+            }
         } else {
             int Lk = m.hull_link[B];
             h1 = B; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = ho + j; P2 = Pb; b2 = A; k2 = A;
+            if (n2 > 1) {           // the link hull's sphere against the piece's (as kind 2)
+                f3 c1 = P1.p + qrot(P1.q, ld3(m.hull_center[B]));
+                f3 c2 = Pb.p + qrot(Pb.q, scale3(c, A, ld3(m.hull_center[h2])));
+                float rr = m.hull_radius[B] + scale_radius(c, A, m.hull_radius[h2]) + c.p->contact_margin;
+                f3 dc = c1 - c2;
+                if (!(dot3(dc, dc) <= rr * rr)) return;
+            }
         }
     } else if (kind == 4) {
         int Lk = m.hull_link[A];
@@ -2113,15 +2245,25 @@ HD void detect(SimCtx& c) {
     for (int o = 0; o < NO; o++) npairs += 1 + NS + (NO - 1 - o) + NLH;
     npairs += NLH * NS;
     wsync();
-    for (int base = 0; base < npairs; base += 64) {
+    // the quad cull (above pair_compact) where the flat enumeration takes more than one batch
+    int G = (NLH + 3) >> 2, neff = npairs;
+    uint64_t om = 0, sm = 0;
+#ifdef HA_X_FLAT_BROAD      /* A/B timing builds only: the flat enumeration */
+    bool hier = false;
+#else
+    // (the Allegro scenes' enumerations fit one batch: compiled out of their kernels)
+    bool hier = !SELF && npairs > 64 && G >= 1 && G * NO <= 64 && G * NS <= 64;
+#endif
+    if (hier) broad_quads(c, G, om, sm, neff);
+    for (int base = 0; base < neff; base += 64) {
 #ifdef HA_PROFILE
         unsigned long long _b0 = __builtin_amdgcn_s_memtime();
 #endif
-        // parallel broad phase: one pair per lane
+        // parallel broad phase: one pair per lane (p: its index in the flat enumeration)
         bool cand = false;
         int p = base + lane;
         int kind = -1, A = -1, B = -1;
-        if (p < npairs && pair_desc(c, p, kind, A, B)) {
+        if (p < neff && (hier ? pair_compact(c, G, om, sm, p, kind, A, B) : pair_desc(c, p, kind, A, B))) {
             float mg = c.p->contact_margin;
             if (kind <= 3) {
                 cand = c.o[A].coll != 0;
@@ -2211,7 +2353,8 @@ HD void detect(SimCtx& c) {
         while (mask) {
             int bit = __ffsll((unsigned long long)mask) - 1;
             int q = base + bit;
-            pair_desc(c, q, kind, A, B);
+            if (hier) pair_compact(c, G, om, sm, q, kind, A, B);
+            else pair_desc(c, q, kind, A, B);
             // the pair is wave-uniform: say so, so that the narrow phase branches on scalars (no exec-masked regions)
 #ifndef HA_X_DIVERGENT_PAIR   /* diagnostic: the pair indices left as the compiler sees them */
             kind = __builtin_amdgcn_readfirstlane(kind);

@@ -861,11 +861,20 @@ static int detect(const hao_handle h, env_t* e, contact_t* out) {
             if (!e->coll[o] || !e->coll[o2] || !(dot(dc, dc) <= rr * rr)) continue;
             if (PCM_TRY(pidx, Po, P2, o, o2)) continue;
             pcm_begin(PCM_REC(pidx), Po, P2);
-            nnar += no * n2;
             if (no * n2 > 1) gather_begin();
             for (int j = 0; j < no; j++)
-                for (int j2 = 0; j2 < n2; j2++)
+                for (int j2 = 0; j2 < n2; j2++) {
+                    /* a compound pair's piece pair: the pieces' own spheres first (ha_physics.h narrow_phase, round 6) */
+                    if (no * n2 > 1) {
+                        v3 c1 = add(Po.p, qrot(Po.q, scl(so, ld3(m->hull_center[ho + j]))));
+                        v3 c2 = add(P2.p, qrot(P2.q, scl(s2, ld3(m->hull_center[h2 + j2]))));
+                        float rp = scl_r(so, m->hull_radius[ho + j]) + scl_r(s2, m->hull_radius[h2 + j2]) + mg;
+                        v3 dp = sub(c1, c2);
+                        if (!(dot(dp, dp) <= rp * rp)) continue;
+                    }
+                    nnar++;
                     collide_hulls(m, ho + j, Po, h2 + j2, P2, mg, o, o2, so, s2, out, &nout, h->maxc);
+                }
             if (no * n2 > 1) gather_end(out, &nout, h->maxc, o, o2);
             g_rec = NULL;
         }
@@ -877,9 +886,18 @@ static int detect(const hao_handle h, env_t* e, contact_t* out) {
             if (!e->coll[o] || !(dot(dc, dc) <= rr * rr)) continue;
             if (PCM_TRY(pidx, PL, Po, 100 + L, o)) continue;
             pcm_begin(PCM_REC(pidx), PL, Po);
-            nnar += no;
             if (no > 1) gather_begin();
-            for (int j = 0; j < no; j++) collide_hulls(m, k, PL, ho + j, Po, mg, 100 + L, o, NULL, so, out, &nout, h->maxc);
+            for (int j = 0; j < no; j++) {
+                if (no > 1) {       /* the link hull's sphere against the piece's */
+                    v3 c1 = add(PL.p, qrot(PL.q, ld3(m->hull_center[k])));
+                    v3 c2 = add(Po.p, qrot(Po.q, scl(so, ld3(m->hull_center[ho + j]))));
+                    float rp = m->hull_radius[k] + scl_r(so, m->hull_radius[ho + j]) + mg;
+                    v3 dp = sub(c1, c2);
+                    if (!(dot(dp, dp) <= rp * rp)) continue;
+                }
+                nnar++;
+                collide_hulls(m, k, PL, ho + j, Po, mg, 100 + L, o, NULL, so, out, &nout, h->maxc);
+            }
             if (no > 1) gather_end(out, &nout, h->maxc, 100 + L, o);
             g_rec = NULL;
         }
