@@ -1533,6 +1533,23 @@ HD bool sphere_near_box(const float* half, PoseF Pb, f3 c, float r) {
     float dz = fmaxf(fabsf(pl.z) - half[2], 0.0f);
     return dx * dx + dy * dy + dz * dz <= r * r;
 }
+// Two unscaled hulls' oriented boxes (hull_obb: link hulls and, since round 6, every piece of a compound object),
+// posed by their bodies, within the margin on all 15 axes (include/ha_obb.h, the oracle's text too): a compound pair's
+// piece pair that fails it cannot touch, so its narrow phase is skipped in both. Elongated pieces (spoon, wrench,
+// scissors) have loose spheres: in the C4w tail envs the boxes reject two thirds of the piece pairs the spheres keep
+#ifdef HA_PIECE_BOX_CALL      /* A/B: the box test as a real call (its temporaries off the caller's registers) */
+__device__ __attribute__((noinline))
+#else
+HD
+#endif
+bool piece_boxes_near(const ha_model_t& m, int h1, PoseF P1, int h2, PoseF P2, float mg) {
+    float p1[3] = {P1.p.x, P1.p.y, P1.p.z}, q1[4] = {P1.q.x, P1.q.y, P1.q.z, P1.q.w};
+    float p2[3] = {P2.p.x, P2.p.y, P2.p.z}, q2[4] = {P2.q.x, P2.q.y, P2.q.z, P2.q.w};
+    float c1[3], R1[9], c2[3], R2[9];
+    ha_obb_world(p1, q1, m.hull_obb[h1], c1, R1);
+    ha_obb_world(p2, q2, m.hull_obb[h2], c2, R2);
+    return ha_obb_sat(c1, R1, m.hull_obb[h1] + 3, c2, R2, m.hull_obb[h2] + 3, mg) != 0;
+}
 // static k's world pose: its model pose, composed with the env's posed actor (s.sb) when the actor carries it (v14)
 HD PoseF static_pose(const SimCtx& c, int k) {
     const ha_model_t& m = *c.m;
@@ -1917,6 +1934,48 @@ HD int pair_pieces(const SimCtx& c, int kind, int A, int B) {
     return n;
 }
 
+// Compound pairs (kinds 2, 3; round 6): which of piece pairs j0 .. j0 + 63 can touch. Lane t tests piece pair j0 + t:
+// the two pieces' own spheres, then (unscaled bodies) their oriented boxes (piece_boxes_near); PhysX's broad phase
+// sees each convex shape of an actor on its own. The oracle tests each piece pair the same way before its narrow phase
+// (physics_oracle.c detect). A block of its own that derives everything from the pair's indices again, so that none of
+// its values stay live into the narrow phases (VGPRs); the result is one 64-bit mask (SGPRs)
+HD uint64_t piece_mask(const SimCtx& c, int kind, int A, int B, int j0, int np) {
+    const EnvLDS& s = *c.s;
+    const ha_model_t& m = *c.m;
+    int jj = j0 + c.lane;
+    bool near = false;
+    if (jj < np) {
+        int ho = m.pool_hull[upool(c, A)];
+        float mg = c.p->contact_margin;
+        int h1, h2, b1, b2;
+        PoseF P1, P2;
+        f3 c1;
+        float r1;
+        if (kind == 2) {
+            int pb = upool(c, B), n2 = m.pool_nhull[pb];
+            int j1 = jj / n2;
+            h1 = ho + j1; h2 = m.pool_hull[pb] + (jj - j1 * n2);
+            P1 = object_pose_u(c, A); P2 = object_pose_u(c, B); b1 = A; b2 = B;
+            c1 = P1.p + qrot(P1.q, scale3(c, A, ld3(m.hull_center[h1])));
+            r1 = scale_radius(c, A, m.hull_radius[h1]);
+        } else {
+            int Lk = m.hull_link[B];
+            h1 = B; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = -1;
+            h2 = ho + jj; P2 = object_pose_u(c, A); b2 = A;
+            c1 = P1.p + qrot(P1.q, ld3(m.hull_center[B]));
+            r1 = m.hull_radius[B];
+        }
+        f3 c2 = P2.p + qrot(P2.q, scale3(c, b2, ld3(m.hull_center[h2])));
+        float rr = r1 + scale_radius(c, b2, m.hull_radius[h2]) + mg;
+        f3 dc = c1 - c2;
+        near = dot3(dc, dc) <= rr * rr;
+#ifndef HA_X_NO_PIECE_BOX
+        if (near && !body_scaled(c, b1) && !body_scaled(c, b2)) near = piece_boxes_near(m, h1, P1, h2, P2, mg);
+#endif
+    }
+    return __ballot(near);
+}
+
 // narrow phase of piece pair j of candidate pair (kind, A, B): the two sides' hulls, poses and body codes
 HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
     const EnvLDS& s = *c.s;
@@ -1946,25 +2005,9 @@ HD void narrow_phase(SimCtx& c, int kind, int A, int B, int j) {
         } else if (kind == 2) {
             int j1 = j / n2;
             h1 = ho + j1; P1 = Po; b1 = A; h2 = m.pool_hull[pb] + (j - j1 * n2); P2 = Pb; b2 = B; k2 = B;
-            // a compound pair's piece pair: the two pieces' own spheres first (round 6; PhysX's broad phase sees each
-            // convex shape of an actor on its own). One-hull objects: their piece sphere is the broad phase's sphere
-            if (m.pool_nhull[pa] * n2 > 1) {
-                f3 c1 = Po.p + qrot(Po.q, scale3(c, A, ld3(m.hull_center[h1])));
-                f3 c2 = Pb.p + qrot(Pb.q, scale3(c, B, ld3(m.hull_center[h2])));
-                float rr = scale_radius(c, A, m.hull_radius[h1]) + scale_radius(c, B, m.hull_radius[h2]) + c.p->contact_margin;
-                f3 dc = c1 - c2;
-                if (!(dot3(dc, dc) <= rr * rr)) return;
-            }
         } else {
             int Lk = m.hull_link[B];
             h1 = B; P1 = PoseF{ld3(s.lp[Lk]), ldq(s.lq[Lk])}; b1 = 100 + Lk; h2 = ho + j; P2 = Pb; b2 = A; k2 = A;
-            if (n2 > 1) {           // the link hull's sphere against the piece's (as kind 2)
-                f3 c1 = P1.p + qrot(P1.q, ld3(m.hull_center[B]));
-                f3 c2 = Pb.p + qrot(Pb.q, scale3(c, A, ld3(m.hull_center[h2])));
-                float rr = m.hull_radius[B] + scale_radius(c, A, m.hull_radius[h2]) + c.p->contact_margin;
-                f3 dc = c1 - c2;
-                if (!(dot3(dc, dc) <= rr * rr)) return;
-            }
         }
     } else if (kind == 4) {
         int Lk = m.hull_link[A];
@@ -2350,6 +2393,7 @@ HD void detect(SimCtx& c) {
         // (the oracle's gather_begin / gather_end). One loop and one call site per narrow phase (a single inlined
         // copy; a nested piece loop would keep its hoisted invariants live over the narrow phase: VGPRs)
         int j = 0;
+        uint64_t pmask = 0;
         while (mask) {
             int bit = __ffsll((unsigned long long)mask) - 1;
             int q = base + bit;
@@ -2413,14 +2457,22 @@ HD void detect(SimCtx& c) {
                 c.gather = true;
                 wsync();
             }
+            // a compound pair's piece pairs that can touch (piece_mask, 64 at a time); the others run no narrow phase
+            bool run = true;
+            if constexpr (!SELF) {
+                if (np > 1 && (kind == 2 || kind == 3)) {
+                    if ((j & 63) == 0) pmask = piece_mask(c, kind, A, B, j, np);
+                    run = ((pmask >> (j & 63)) & 1ull) != 0;
+                }
+            }
 #ifdef HA_AB_NARROW_TWICE
-            for (int rep = 0; rep < 2; rep++) {     // one call site: the same code size as the product
+            for (int rep = 0; rep < 2 && run; rep++) {     // one call site: the same code size as the product
                 if (rep == 1) { c.dry = true; c.colA_h = c.colB_h = -1; }
                 narrow_phase(c, kind, A, B, j);
             }
             c.dry = false;
 #else
-            narrow_phase(c, kind, A, B, j);
+            if (run) narrow_phase(c, kind, A, B, j);
 #endif
             if (++j < np) continue;
             j = 0;

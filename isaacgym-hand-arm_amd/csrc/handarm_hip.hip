@@ -1096,7 +1096,12 @@ int ha_create(const ha_model_t* model, const ha_params_t* params, int32_t num_en
     if (model->n_link_hulls < 0 || model->n_link_hulls > model->n_hulls) return HA_E_MODEL;
     for (int k = 0; k < model->n_hulls; k++) {
         bool boxed = k < model->n_link_hulls, obj = false;
-        for (int p = 0; p < model->n_pool; p++) obj = obj || (model->pool_nhull[p] == 1 && model->pool_hull[p] == k);
+        for (int p = 0; p < model->n_pool; p++) {
+            obj = obj || (model->pool_nhull[p] == 1 && model->pool_hull[p] == k);
+            // a compound object's pieces: the piece-pair box cull (ha_physics.h piece_boxes_near, round 6)
+            boxed = boxed || (model->pool_nhull[p] > 1 && k >= model->pool_hull[p] &&
+                              k < model->pool_hull[p] + model->pool_nhull[p]);
+        }
         if ((boxed || obj) && !hull_in_box(model, k)) return HA_E_MODEL;
         // a one-piece object's box is read with the identity orientation (ha_physics.h object_box): refuse any other
         const float* oq = model->hull_obb[k] + 6;

@@ -457,6 +457,8 @@ def build_model(scene, pool_names=None, posed=None):
             ctr = 0.5 * (pts.min(0) + pts.max(0))
             m.pool_center[i][:] = ctr
             m.pool_radius[i] = float(np.linalg.norm(pts - ctr, axis=1).max()) * (1 + 1e-6)
+            for j, h in enumerate(obj_hulls[i]):      # each piece's oriented box (the piece-pair box cull, round 6)
+                m.hull_obb[m.pool_hull[i] + j][:] = hull_obb(h["verts"])
         m.pool_mass[i] = o["mass"]
         m.pool_com[i][:] = o["com"]
         m.pool_inertia[i][:] = o["inertia"]

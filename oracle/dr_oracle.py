@@ -121,7 +121,8 @@ def mass_ratio(p, attr, env, ep, k, frame, og, own=None):
     a = p.dr_attr[attr]
     og = np.asarray(og, F)
     own = og if own is None else np.asarray(own, F)
-    general = (attr_sample(p, attr, env, ep, k, frame, og) / own).astype(F)
+    with np.errstate(invalid="ignore", divide="ignore"):     # massless bodies (own 0): og == own, `simple` is taken
+        general = (attr_sample(p, attr, env, ep, k, frame, og) / own).astype(F)
     if not (a.op == OP_SCALING and a.num_buckets == 0):
         return general
     simple = attr_sample(p, attr, env, ep, k, frame, F(1.0))        # elementwise where og == own (the device's test)

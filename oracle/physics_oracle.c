@@ -779,6 +779,16 @@ static int near_box(const float* half, pose_t Pb, v3 c, float r) {
     float dz = fmaxf(fabsf(pl.z) - half[2], 0.0f);
     return dx * dx + dy * dy + dz * dz <= r * r;
 }
+/* two unscaled hulls' oriented boxes posed by their bodies within the margin on all 15 axes (include/ha_obb.h;
+ * ha_physics.h piece_boxes_near): a compound pair's piece pair that fails it is skipped (round 6) */
+static int piece_boxes_near(const ha_model_t* m, int h1, pose_t P1, int h2, pose_t P2, float mg) {
+    float p1[3] = {P1.p.x, P1.p.y, P1.p.z}, q1[4] = {P1.q.x, P1.q.y, P1.q.z, P1.q.w};
+    float p2[3] = {P2.p.x, P2.p.y, P2.p.z}, q2[4] = {P2.q.x, P2.q.y, P2.q.z, P2.q.w};
+    float c1[3], R1[9], c2[3], R2[9];
+    ha_obb_world(p1, q1, m->hull_obb[h1], c1, R1);
+    ha_obb_world(p2, q2, m->hull_obb[h2], c2, R2);
+    return ha_obb_sat(c1, R1, m->hull_obb[h1] + 3, c2, R2, m->hull_obb[h2] + 3, mg);
+}
 /* static k's world pose; a static carried by the env's posed actor composes that actor's pose with its own (v14,
  * ha_physics.h static_pose) */
 static pose_t static_pose(const ha_model_t* m, const env_t* e, int k) {
@@ -871,6 +881,7 @@ static int detect(const hao_handle h, env_t* e, contact_t* out) {
                         float rp = scl_r(so, m->hull_radius[ho + j]) + scl_r(s2, m->hull_radius[h2 + j2]) + mg;
                         v3 dp = sub(c1, c2);
                         if (!(dot(dp, dp) <= rp * rp)) continue;
+                        if (!so && !s2 && !piece_boxes_near(m, ho + j, Po, h2 + j2, P2, mg)) continue;
                     }
                     nnar++;
                     collide_hulls(m, ho + j, Po, h2 + j2, P2, mg, o, o2, so, s2, out, &nout, h->maxc);
@@ -894,6 +905,7 @@ static int detect(const hao_handle h, env_t* e, contact_t* out) {
                     float rp = m->hull_radius[k] + scl_r(so, m->hull_radius[ho + j]) + mg;
                     v3 dp = sub(c1, c2);
                     if (!(dot(dp, dp) <= rp * rp)) continue;
+                    if (!so && !piece_boxes_near(m, k, PL, ho + j, Po, mg)) continue;
                 }
                 nnar++;
                 collide_hulls(m, k, PL, ho + j, Po, mg, 100 + L, o, NULL, so, out, &nout, h->maxc);

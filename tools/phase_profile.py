@@ -194,6 +194,25 @@ if __name__ == "__main__":
                                                 for x in xs), flush=True)
             hist, edges = np.histogram(dur, bins=12)
             print("  histogram: " + "  ".join(f"{edges[i]:.0f}:{hist[i]}" for i in range(12)), flush=True)
+            # the slowest envs: contact_stats of the step (substeps, over capacity, max offered, offered, self,
+            # refreshed records, narrow phases) and their objects (pool ids, positions)
+            oid = sim.t["object_indices"].cpu().numpy() if "object_indices" in sim.t else None
+            rs = sim.t["root_state"].cpu().numpy().reshape(n, -1, 13)
+            for e in np.argsort(dur)[::-1][:6]:
+                print(f"  slow env {e}: {dur[e]:.0f} us, start {st[e]:.0f}, stats {cs[e].tolist()}", flush=True)
+                if oid is not None:
+                    names = globals().get("pool")
+                    ids = [names[i] if names else i for i in oid[e].tolist()]
+                    print(f"    objects {ids}; actor root z {np.round(rs[e, :, 2], 3).tolist()}", flush=True)
+            if os.environ.get("HA_DUMP_SLOW"):
+                # the slowest envs' state after the step (every per-env tensor), for an oracle replay on the CPU
+                top = np.argsort(dur)[::-1][:4]
+                dump = {"envs": top, "dur": dur[top], "stats": cs[top]}
+                for k, v in sim.t.items():
+                    if hasattr(v, "dim") and v.dim() >= 1 and v.shape[0] >= n and v.shape[0] % n == 0:
+                        vv = v.reshape(n, v.shape[0] // n, *v.shape[1:])      # (N * A, 13) rows: per env
+                        dump[k] = vv[torch.as_tensor(top.copy(), device=v.device)].cpu().numpy()
+                np.savez(os.environ["HA_DUMP_SLOW"], **dump)
         sys.exit(0)
     for objects in (False, True):
         lib.ha_profile_read(raw, 1)
