@@ -75,6 +75,21 @@ def test_every_culled_hull_lies_inside_its_box(asset):
             assert list(ob[6:10]) == [0, 0, 0, 1]        # identity: a per-env object scale scales the box
 
 
+@pytest.mark.parametrize("asset,pool", [(HM.ASSET, HM.POOL_WIDE), (HM.BIN_ASSET, None)])
+def test_compound_pieces_lie_inside_their_boxes(asset, pool):
+    """Round 6: every piece of a compound object (the mug; the wide pool's concave objects) carries a fitted box
+    (model.py hull_obb) that holds its vertices: the piece-pair cull (ha_physics.h piece_mask / piece_boxes_near, the
+    oracle's piece_boxes_near) tests those boxes, and ha_create refuses a model whose pieces leave them."""
+    m = HM.build_model(HM.load_scene(asset), pool)
+    pieces = [m.pool_hull[p] + j for p in range(m.n_pool) if m.pool_nhull[p] > 1 for j in range(m.pool_nhull[p])]
+    assert len(pieces) >= (40 if pool else 2)
+    for h in pieces:
+        ob = np.array(m.hull_obb[h], np.float64)
+        assert abs(np.linalg.norm(ob[6:10]) - 1.0) < 1e-6
+        loc = (_hull_verts(m, h) - ob[0:3]) @ _qmat(ob[6:10])
+        assert (np.abs(loc) <= ob[3:6] + 1e-7).all(), h
+
+
 def _object_box(m, st, e, o, n_obj):
     A = m.n_actors
     root = st["root_state"].reshape(-1, A, 13)[e, m.actor_object0 + o]
