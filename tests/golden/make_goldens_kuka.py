@@ -310,11 +310,16 @@ def refresh_bodies(t, chain, model):
     t.rigid_body_states[:] = torch.from_numpy(rb)
 
 
-def steps(sub, N=32, T=8, seed=2):
+def steps(sub, N=32, T=8, seed=2, privileged=False):
+    """privileged: privilegedActions True (allegro_kuka_base.py:62-74, 1359-1361, 1417-1424): 26 actions, the first
+    three scaled by privilegedActionsTorque into action_torques on the object (recorded as "torques")."""
     from oracle.oracle_lib import HostState, Oracle
     torch.manual_seed(seed)          # seeded before the task is built: __init__'s random_force_prob draw is the
     mod, base, t, _, _ = make_task(sub, N)     # first draw of the stream (ref_rng.KukaDraws replays it)
     prob_init = t.random_force_prob.clone()
+    if privileged:
+        t.privileged_actions = True
+        t.privileged_actions_torque = env_cfg(sub)["privilegedActionsTorque"]
     params, cfg = HM.build_params({"subtask": sub}, task=HM.TASK_ALLEGRO_KUKA)
     model = HM.build_model(HM.load_scene(SCENE), posed=HM.posed_group(HM.TASK_ALLEGRO_KUKA, cfg))
     G = 10 if sub == "throw" else 9                  # draws of one reset_target_pose (ak_task.h ak_goal_draws)
@@ -420,7 +425,7 @@ def steps(sub, N=32, T=8, seed=2):
                 r[fall, 1, 2] = 0.05
                 t.arm_hand_dof_vel[:] = 0.3 * real_randn(N, 23, generator=g)
                 t.progress_buf[real_rand(N, generator=g) < 0.1] = t.max_episode_length - 2
-            actions = 2 * real_rand(N, 23, generator=g) - 1
+            actions = 2 * real_rand(N, 26 if privileged else 23, generator=g) - 1
             rec("dof_state", t.dof_state.numpy())
             rec("root_state", t.root_state_tensor.numpy())
             rec("goal_state", t.goal_states[:, 0:7].numpy())
@@ -442,6 +447,8 @@ def steps(sub, N=32, T=8, seed=2):
                          ("root_after", t.root_state_tensor), ("goal_after", t.goal_states[:, 0:7])]:
                 rec(k, v.numpy())
             rec("task_state", pack_task_state(t))
+            if privileged:
+                rec("torques", t.action_torques[:, OBJ_BODY].numpy())
     base.torch_rand_float, mod.torch_rand_float = real_trf, orig_mod_trf
     res = {k: np.stack(v) for k, v in out.items()}
     res["draws"] = draws
@@ -449,7 +456,7 @@ def steps(sub, N=32, T=8, seed=2):
     res["random_force_prob_init"] = prob_init.numpy()
     res["seed"] = np.array(seed)
     assert set(keys_in) <= set(res)
-    np.savez_compressed(os.path.join(HERE, f"kuka_steps_{sub}.npz"), **res)
+    np.savez_compressed(os.path.join(HERE, f"kuka_steps_{sub}{'_privileged' if privileged else ''}.npz"), **res)
 
 
 def object_dims_and_curriculum():
@@ -476,4 +483,5 @@ if __name__ == "__main__":
     for sub in sys.argv[1:] or ("regrasping", "reorientation", "throw"):
         obs_reward(sub)
         steps(sub)
+    steps("regrasping", privileged=True)
     print("wrote kuka_object_dims.npz, kuka_obs_reward_*.npz, kuka_steps_*.npz")

@@ -71,13 +71,17 @@ def test_kuka_observe_and_reward_against_reference_goldens(sub):
         np.testing.assert_allclose(get(sim, "task_state")[:, :32], d["task_state"][s][:, :32], rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("sub", ["regrasping", "reorientation", "throw"])
-def test_kuka_step_with_resets_replayed_against_reference_goldens(sub):
+@pytest.mark.parametrize("sub,privileged", [("regrasping", False), ("reorientation", False), ("throw", False),
+                                            ("regrasping", True)])
+def test_kuka_step_with_resets_replayed_against_reference_goldens(sub, privileged):
     """The fused step kernel without physics: goal + env resets and random forces from the recorded reference
-    draws, hand/arm targets, FK refresh, progress, full_state observations, reward, done, timeout."""
-    d = np.load(os.path.join(G, f"kuka_steps_{sub}.npz"))
+    draws, hand/arm targets, FK refresh, progress, full_state observations, reward, done, timeout. privileged: the
+    26-action variant (its targets read the reference's action slices; the object torque it applies is not a state
+    output of a physics-free step: tests/test_kuka_golden.py pins its value against the same golden and
+    tests/test_gpu_dr_schema.py its effect on the physics against the oracle chain)."""
+    d = np.load(os.path.join(G, f"kuka_steps_{sub}{'_privileged' if privileged else ''}.npz"))
     T, N = d["rew"].shape
-    sim = make_sim(N, subtask=sub)
+    sim = make_sim(N, subtask=sub, privileged_actions=privileged)
     flags = HM.FLAG_NO_PHYSICS | HM.FLAG_REPLAY_DRAWS
     for t in range(T):
         for k, g in [("dof_state", "dof_state"), ("root_state", "root_state"), ("goal_state", "goal_state"),
