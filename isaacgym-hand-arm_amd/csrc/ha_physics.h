@@ -2462,7 +2462,14 @@ HD void detect(SimCtx& c) {
             if constexpr (!SELF) {
                 if (np > 1 && (kind == 2 || kind == 3)) {
                     if ((j & 63) == 0) pmask = piece_mask(c, kind, A, B, j, np);
-                    run = ((pmask >> (j & 63)) & 1ull) != 0;
+                    uint64_t rest = pmask >> (j & 63);
+                    run = (rest & 1ull) != 0;
+                    if (!run) {
+                        // straight to the next piece pair that can touch (or the chunk's end): the loop's ++j lands there
+                        rest >>= 1;
+                        int nxt = rest ? j + __ffsll((unsigned long long)rest) : (j | 63) + 1;
+                        j = (nxt < np ? nxt : np) - 1;
+                    }
                 }
             }
 #ifdef HA_AB_NARROW_TWICE
