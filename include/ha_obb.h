@@ -96,5 +96,17 @@ HA_OB_FN int ha_obb_near(const float* ca, const float* Ra, const float* ha, cons
     return ha_obb_sat(ca, Ra, ha, cb, Rb, hb, mg);
 }
 
+/* Two posed boxes within the margin on all 15 axes, from the bodies' poses (p, q xyzw) and the boxes' records ob
+ * (centre, half extents, quat in the body frame): ha_obb_world of each, then ha_obb_sat - the compound piece-pair cull
+ * of the step kernels and the oracle (round 6). (A form in box A's frame from the relative quaternion held half the
+ * live values and removed the kernels' spills, but measured 2% slower on C4 / C4w / C5: profiles/r06_ab_*) */
+HA_OB_FN int ha_obb_pair_near(const float* p1, const float* q1, const float* ob1, const float* p2, const float* q2,
+                              const float* ob2, float mg) {
+    float c1[3], R1[9], c2[3], R2[9];
+    ha_obb_world(p1, q1, ob1, c1, R1);
+    ha_obb_world(p2, q2, ob2, c2, R2);
+    return ha_obb_sat(c1, R1, ob1 + 3, c2, R2, ob2 + 3, mg);
+}
+
 #undef HA_OB_FN
 #endif

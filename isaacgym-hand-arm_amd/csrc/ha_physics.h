@@ -1545,10 +1545,7 @@ HD
 bool piece_boxes_near(const ha_model_t& m, int h1, PoseF P1, int h2, PoseF P2, float mg) {
     float p1[3] = {P1.p.x, P1.p.y, P1.p.z}, q1[4] = {P1.q.x, P1.q.y, P1.q.z, P1.q.w};
     float p2[3] = {P2.p.x, P2.p.y, P2.p.z}, q2[4] = {P2.q.x, P2.q.y, P2.q.z, P2.q.w};
-    float c1[3], R1[9], c2[3], R2[9];
-    ha_obb_world(p1, q1, m.hull_obb[h1], c1, R1);
-    ha_obb_world(p2, q2, m.hull_obb[h2], c2, R2);
-    return ha_obb_sat(c1, R1, m.hull_obb[h1] + 3, c2, R2, m.hull_obb[h2] + 3, mg) != 0;
+    return ha_obb_pair_near(p1, q1, m.hull_obb[h1], p2, q2, m.hull_obb[h2], mg) != 0;
 }
 // static k's world pose: its model pose, composed with the env's posed actor (s.sb) when the actor carries it (v14)
 HD PoseF static_pose(const SimCtx& c, int k) {

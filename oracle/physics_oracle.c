@@ -784,10 +784,7 @@ static int near_box(const float* half, pose_t Pb, v3 c, float r) {
 static int piece_boxes_near(const ha_model_t* m, int h1, pose_t P1, int h2, pose_t P2, float mg) {
     float p1[3] = {P1.p.x, P1.p.y, P1.p.z}, q1[4] = {P1.q.x, P1.q.y, P1.q.z, P1.q.w};
     float p2[3] = {P2.p.x, P2.p.y, P2.p.z}, q2[4] = {P2.q.x, P2.q.y, P2.q.z, P2.q.w};
-    float c1[3], R1[9], c2[3], R2[9];
-    ha_obb_world(p1, q1, m->hull_obb[h1], c1, R1);
-    ha_obb_world(p2, q2, m->hull_obb[h2], c2, R2);
-    return ha_obb_sat(c1, R1, m->hull_obb[h1] + 3, c2, R2, m->hull_obb[h2] + 3, mg);
+    return ha_obb_pair_near(p1, q1, m->hull_obb[h1], p2, q2, m->hull_obb[h2], mg);
 }
 /* static k's world pose; a static carried by the env's posed actor composes that actor's pose with its own (v14,
  * ha_physics.h static_pose) */
@@ -1469,6 +1466,11 @@ void hao_set_capacity(hao_handle h, int maxc) { if (maxc > 0 && maxc <= MAXC) h-
 /* OpenMP threads of hao_simulate (bench.py's cpu_baseline reports an all-cores and a 1-thread sample) */
 void hao_set_threads(int n) { if (n > 0) omp_set_num_threads(n); }
 int hao_get_threads(void) { return omp_get_max_threads(); }
+/* test hook: the compound piece-pair box test (include/ha_obb.h ha_obb_pair_near), for tests/test_box_cull.py */
+int hao_obb_pair_near(const float* p1, const float* q1, const float* ob1, const float* p2, const float* q2,
+                      const float* ob2, float mg) {
+    return ha_obb_pair_near(p1, q1, ob1, p2, q2, ob2, mg);
+}
 int hao_struct_sizes(int32_t* model_size, int32_t* params_size, int32_t* state_size) {
     *model_size = (int32_t)sizeof(ha_model_t);
     *params_size = (int32_t)sizeof(ha_params_t);

@@ -90,6 +90,46 @@ def test_compound_pieces_lie_inside_their_boxes(asset, pool):
         assert (np.abs(loc) <= ob[3:6] + 1e-7).all(), h
 
 
+def test_piece_pair_box_test_is_the_double_precision_sat():
+    """include/ha_obb.h ha_obb_pair_near (the compound piece-pair cull of kernel and oracle, built in box A's frame from
+    the relative quaternion) against boxes_near in float64 on posed pieces of the wide pool: every pair it declares
+    apart is apart in float64 by more than the margin less 1e-5 m, and every pair it keeps is within the margin plus
+    1e-5 m, so it decides as the exact test does up to float32 rounding."""
+    import ctypes as C
+    from oracle.oracle_lib import load
+    lib = load()
+    f3 = C.POINTER(C.c_float)
+    lib.hao_obb_pair_near.argtypes = [f3] * 6 + [C.c_float]
+    m = HM.build_model(HM.load_scene(HM.ASSET), HM.POOL_WIDE)
+    pieces = [m.pool_hull[p] + j for p in range(m.n_pool) if m.pool_nhull[p] > 1 for j in range(m.pool_nhull[p])]
+    rng = np.random.default_rng(7)
+    mg = 0.01
+    kept = apart = 0
+
+    def ptr(a):
+        return np.ascontiguousarray(a, np.float32).ctypes.data_as(f3)
+
+    def posed(p, q, ob):
+        return p + _qrot(q, ob[0:3]), _qmul(q, ob[6:10]), ob[3:6]
+    for _ in range(3000):
+        h1, h2 = rng.choice(pieces, 2)
+        p1 = rng.normal(0, 0.02, 3).astype(np.float32)
+        p2 = (p1 + rng.normal(0, 0.05, 3)).astype(np.float32)
+        q1, q2 = (q / np.linalg.norm(q) for q in rng.normal(size=(2, 4)))
+        q1, q2 = q1.astype(np.float32), q2.astype(np.float32)
+        ob1, ob2 = np.array(m.hull_obb[h1], np.float32), np.array(m.hull_obb[h2], np.float32)
+        got = lib.hao_obb_pair_near(ptr(p1), ptr(q1), ptr(ob1), ptr(p2), ptr(q2), ptr(ob2), mg)
+        a = posed(p1.astype(np.float64), q1.astype(np.float64), ob1.astype(np.float64))
+        b = posed(p2.astype(np.float64), q2.astype(np.float64), ob2.astype(np.float64))
+        if got:
+            kept += 1
+            assert boxes_near(*a, *b, mg + 1e-5)
+        else:
+            apart += 1
+            assert not boxes_near(*a, *b, mg - 1e-5)
+    assert kept > 300 and apart > 300
+
+
 def _object_box(m, st, e, o, n_obj):
     A = m.n_actors
     root = st["root_state"].reshape(-1, A, 13)[e, m.actor_object0 + o]
