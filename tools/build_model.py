@@ -539,16 +539,19 @@ def build_cube(size=0.065, density=400.0):
 
 def build_egg(density=1000.0):
     """mjcf/open_ai_assets/hand/egg.xml: ellipsoid, semi-axes 0.03 x 0.03 x 0.04 (the object geom; MJCF default density
-    1000) as a 32-vertex hull of points on its surface; mass and inertia of the ellipsoid."""
+    1000) as a 32-vertex hull: the two tips and five rings (5, 6, 8, 6, 5 points, one on the equator), scaled about
+    the centre so that the hull's volume is the ellipsoid's (the mass and inertia are the ellipsoid's; round 6: the
+    inscribed hull without an equator ring was about 10% narrower than the ellipsoid at the equator)."""
+    from scipy.spatial import ConvexHull
     a, b, c = 0.03, 0.03, 0.04
     pts = [[0.0, 0.0, c], [0.0, 0.0, -c]]
-    for k, zf in enumerate((-0.75, -0.3, 0.3, 0.75)):
-        n = 6 if abs(zf) > 0.5 else 9
+    for k, (zf, n) in enumerate(((-0.8, 5), (-0.45, 6), (0.0, 8), (0.45, 6), (0.8, 5))):
         for j in range(n):
             t = 2 * math.pi * (j + 0.5 * k) / n
             r = math.sqrt(1 - zf * zf)
             pts.append([a * r * math.cos(t), b * r * math.sin(t), c * zf])
     mass = density * 4.0 / 3.0 * math.pi * a * b * c
+    pts = np.array(pts) * (4.0 / 3.0 * math.pi * a * b * c / ConvexHull(np.array(pts)).volume) ** (1.0 / 3.0)
     I = [mass / 5 * (b * b + c * c), mass / 5 * (a * a + c * c), mass / 5 * (a * a + b * b)]
     return {"name": "egg", "mass": mass, "com": [0, 0, 0], "inertia": [I[0], 0, 0, 0, I[1], 0, 0, 0, I[2]],
             "hull": hull_record(np.array(pts), 32)}
