@@ -271,7 +271,10 @@ typedef struct ha_model_t {
      * (include/ha_obb.h). n_self_pairs = 0: no self-collision (Ur5Sih: filter 0b1, ur5sih.py:123-125).
      * A one-piece pool object's hull carries a box too: its bounding box in the body frame with the identity
      * orientation (scaled with the env's object_scale), for the broad phase's box cull of the Allegro families.
-     * ha_create refuses a model whose link hulls or one-piece object hulls do not lie inside their boxes. */
+     * Each piece of a compound pool object (pool_nhull > 1) carries its fitted box (any orientation), for the
+     * piece-pair cull of compound pairs (round 6, include/ha_obb.h ha_obb_pair_near; unscaled bodies only).
+     * ha_create refuses a model whose link hulls, one-piece object hulls or compound pieces do not lie inside their
+     * boxes. */
     int32_t n_self_pairs;
     uint16_t self_pair[HA_MAX_SELF_PAIRS];
     float hull_obb[HA_MAX_HULLS][12];
