@@ -1537,7 +1537,7 @@ HD bool sphere_near_box(const float* half, PoseF Pb, f3 c, float r) {
 // posed by their bodies, within the margin on all 15 axes (include/ha_obb.h, the oracle's text too): a compound pair's
 // piece pair that fails it cannot touch, so its narrow phase is skipped in both. Elongated pieces (spoon, wrench,
 // scissors) have loose spheres: in the C4w tail envs the boxes reject two thirds of the piece pairs the spheres keep
-#ifdef HA_PIECE_BOX_CALL      /* A/B: the box test as a real call (its temporaries off the caller's registers) */
+#ifdef HA_PIECE_BOX_CALL      /* A/B: the box test as a real call (C4w 6.27 vs 6.17 ms inline, profiles/r06_ab_*) */
 __device__ __attribute__((noinline))
 #else
 HD
@@ -1966,7 +1966,7 @@ HD uint64_t piece_mask(const SimCtx& c, int kind, int A, int B, int j0, int np) 
         float rr = r1 + scale_radius(c, b2, m.hull_radius[h2]) + mg;
         f3 dc = c1 - c2;
         near = dot3(dc, dc) <= rr * rr;
-#ifndef HA_X_NO_PIECE_BOX
+#ifndef HA_X_NO_PIECE_BOX      /* A/B timing builds only (the oracle keeps the box test): the piece spheres alone */
         if (near && !body_scaled(c, b1) && !body_scaled(c, b2)) near = piece_boxes_near(m, h1, P1, h2, P2, mg);
 #endif
     }
