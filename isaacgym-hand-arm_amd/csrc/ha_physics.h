@@ -2373,7 +2373,8 @@ HD void detect(SimCtx& c) {
         }
 #endif
         // the candidates whose persistent-manifold record applies (ha_params_t v13), tested for the whole batch at once;
-        // their records are then loaded a pair ahead of their turn (one register each)
+        // each record is loaded at its turn (loading it one refresh ahead measured C4 +1.5%, C5 -0.7%, C2 / C4w +-0:
+        // profiles/r06_ab_record_prefetch.txt)
         uint64_t vmask = __ballot(c.pcm && cand && pcm_valid_lane(c, p, kind, A, B));
         // and the candidates' separating-face records, one byte load each
         int frec = (cand && c.pairf) ? (int)c.pairf[p] : 0xFF;
