@@ -10,7 +10,8 @@ differences, link damping from the COM Jacobians, the converged implicit PD driv
   limits, joint friction 0) equals the closed-form implicit PD step, with random joint velocities (Coriolis and link
   damping in play): this pins CRBA / the mass matrix with armature, RNEA's velocity-product forces, the drive rows'
   gamma / bias and the symplectic integration;
-* the GPU kernel does the same on the device (``-m gpu``).
+* the GPU kernel does the same on the device (``-m gpu``);
+* the shared float32 math (include/ha_fmath.h: sincos, log, exp) is held against float64 numpy.
 The AllegroKuka golden vectors' fingertip / palm rows come from this FK too (tests/golden/make_goldens_kuka.py)."""
 import copy
 
@@ -129,3 +130,40 @@ def test_kernel_drive_step_matches_closed_form(task, asset):
     torch.cuda.synchronize()
     out = sim.t["dof_state"].cpu().numpy().reshape(n, m.n_dofs, 2)
     _check_step(Chain(scene), p, q, qd, tgt, out, f"kernel task {task}")
+
+
+def _ulp_err(got, ref):
+    return np.abs(got.astype(np.float64) - ref) / np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64)
+
+
+def test_shared_float32_math_against_float64():
+    """include/ha_fmath.h is one text compiled into the kernels and the C oracle, so a bit-identity test cannot see a
+    defect in it. Here its sine / cosine, log and exp (as compiled into the oracle; the kernels are bit-identical to
+    the oracle in every fused-step test) are held against float64 numpy: within 1.5 ulp of the float32-rounded exact
+    value (sincos where |f| > 1e-3, absolute 8e-8 below that), log and exp within 1 ulp."""
+    import ctypes as C
+    from oracle import oracle_lib
+    lib = oracle_lib.load()
+    lib.hao_sincos.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    lib.hao_logexp.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    F = np.float32
+    rng = np.random.default_rng(1)
+    x = np.concatenate([rng.uniform(-3.2, 3.2, 100000), rng.uniform(-2000, 2000, 100000)]).astype(F)
+    s, c = np.empty_like(x), np.empty_like(x)
+    lib.hao_sincos(x.ctypes.data, x.size, s.ctypes.data, c.ctypes.data)
+    for got, ref in ((s, np.sin(x.astype(np.float64))), (c, np.cos(x.astype(np.float64)))):
+        big = np.abs(ref) > 1e-3
+        assert _ulp_err(got[big], ref[big]).max() < 1.5
+        assert np.abs(got[~big] - ref[~big]).max() < 8e-8
+    xl = np.concatenate([rng.uniform(2 ** -24, 1, 100000), np.exp(rng.uniform(-80, 80, 100000))]).astype(F)
+    y = rng.uniform(-80, 80, xl.size)
+    xe = ((y + 3.0) / 1e-3).astype(F)                 # hao_logexp's exp argument is 1e-3 x - 3 (float32)
+    lo, _ = np.empty_like(xl), np.empty_like(xl)
+    lib.hao_logexp(xl.ctypes.data, xl.size, lo.ctypes.data, _.ctypes.data)
+    ref = np.log(xl.astype(np.float64))
+    big = np.abs(ref) > 1e-3
+    assert _ulp_err(lo[big], ref[big]).max() < 1.0
+    _, ex = np.empty_like(xe), np.empty_like(xe)
+    lib.hao_logexp(xe.ctypes.data, xe.size, _.ctypes.data, ex.ctypes.data)
+    arg = (xe * F(1e-3)).astype(F) - F(3.0)
+    assert _ulp_err(ex, np.exp(arg.astype(np.float64))).max() < 1.0
