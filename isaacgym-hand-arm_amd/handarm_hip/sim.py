@@ -91,10 +91,13 @@ class HandArmSim:
         self.rebalance_every = int(rebalance_every)
         self._snake = int(os.environ.get("HA_ORDER_SNAKE", 0))     # A/B: alternate-block reversal of the order
         # the refresh sorts by each env's workgroup span in the last step launch (round 4: C4 +13% against the
-        # contacts offered, which stays available as HA_ORDER_COST=contacts for A/B runs)
-        order_cost = os.environ.get("HA_ORDER_COST", "time")
+        # contacts offered). AllegroHand sorts by the contacts offered instead: its spans repeat poorly from step to
+        # step (correlation 0.38 against C5's 0.60, profiles/r06_order_quality.txt) and the contact count, which
+        # tracks an env's span at 0.8, measured its kernel 0.5-0.7% faster. HA_ORDER_COST overrides (A/B runs)
+        order_cost = os.environ.get("HA_ORDER_COST", "contacts" if task == HM.TASK_ALLEGRO_HAND else "time")
         if order_cost not in ("time", "contacts"):
             raise ValueError(f"HA_ORDER_COST must be 'time' or 'contacts', not {order_cost!r}")
+        self.order_cost = order_cost
         self._rb_count = 0
         if self.rebalance_every > 0:
             self._env_order = torch.arange(num_envs, dtype=torch.int32, device=self.device)

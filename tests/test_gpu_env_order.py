@@ -36,13 +36,18 @@ def test_env_order_is_a_longest_first_permutation(n):
 
 @pytest.mark.gpu
 def test_env_order_by_workgroup_spans_is_a_permutation():
-    """The default cost: each env's workgroup span in the last step launch (stamped by the step kernel per launch
-    slot, mapped to envs through the order that launch used)."""
+    """The default cost (AllegroKuka, Ur5Sih): each env's workgroup span in the last step launch (stamped by the step
+    kernel per launch slot, mapped to envs through the order that launch used). AllegroHand sorts by the contacts
+    offered by default (round 6)."""
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     from handarm_hip.tasks import isaacgym_task_map
     n = 1000
-    env = isaacgym_task_map["AllegroHand"]({"env": {"numEnvs": n}}, "cuda:0", "cuda:0")
+    ah = isaacgym_task_map["AllegroHand"]({"env": {"numEnvs": 64}}, "cuda:0", "cuda:0")
+    assert ah.sim.order_cost == "contacts"
+    del ah
+    env = isaacgym_task_map["AllegroKuka"]({"env": {"numEnvs": n}}, "cuda:0", "cuda:0")
+    assert env.sim.order_cost == "time"
     env.reset()
     g = torch.Generator(device="cuda:0").manual_seed(4)
     orders = []
